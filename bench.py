@@ -1,0 +1,200 @@
+#!/usr/bin/env python3
+"""Tracker FPS benchmark of the MI355X MixFormer RGB-T forward path (BASELINE.json `metric`).
+
+A step = one template+search forward (both modalities, boxes out) of B frames per GPU on
+synthetic inputs resident in HBM (fresh frames rotated from a pool each step, copied into the
+static input buffers), replayed as one hipGraph.  N>1: one process per GPU (torchrun), each an
+independent replica tracking its own sequences ("replicas only": the path has no exchange step),
+so scaling is weak and value = frames of all ranks / max-over-ranks time.
+
+Extra fields: `roofline` for the kernel with the largest share of device time and `roofline_mam`
+for the MAM attention kernel (algorithmic FLOPs per launch / average launch time measured with HIP
+events in an eager pass over the same plan), and `cpu_baseline` = the oracle's fp32 CPU forward
+(oracle/forward.py, a restatement of the reference) on a bounded sample, rank 0 at N=1 only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "multi-modal-tracking_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "tracker FPS (template+search fwd) MixViT-B RGB-T @320px, 1/2/4/8 MI355X"
+PEAK = {"bf16": 2500.0, "f32": 157.3}  # dense MFMA TFLOP/s, MI355X_MICROARCH.md
+VARIANT_NAMES = {"rgbt": "mixformer_vit_rgbt (two-stream)", "shared": "mixformer_vit_rgbt_shared",
+                 "asym": "asymmetric_shared", "asym_online": "asymmetric_shared_online_score"}
+
+
+def state_dict_keys(variant, hidden=768, depth=12, search=320, template=128, fusion_layers=2):
+    """(name, shape) list of the reference model's state_dict (drop-in key names)."""
+    from mmt_amd.model import reference_state_dict_shapes
+    return reference_state_dict_shapes(variant, hidden=hidden, depth=depth, search=search, template=template,
+                                       fusion_layers=fusion_layers)
+
+
+def plan_flops(rt, entry):
+    """Algorithmic FLOPs of one plan entry (GEMM: 2MNK per group; MAM: 4*d*H*sum(Lq*Lk))."""
+    fn, args, name, keep = entry
+    if keep is None:
+        return 0.0
+    if hasattr(keep, "K"):
+        return 2.0 * keep.M * keep.N * keep.K * keep.groups
+    d = rt.d
+    lk_s = d.ntok + (d.n_t if keep.asym else 0)
+    return 4.0 * 64 * keep.H * keep.S * (d.n_t * d.n_t + d.ns * lk_s)
+
+
+def kernel_profile(rt, plan, reps=20):
+    """Average device time per plan entry, HIP events around each launch on the launch stream."""
+    s = torch.cuda.current_stream()
+    n = len(plan)
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(n + 1)] for _ in range(reps)]
+    for r in range(reps):
+        for i, (fn, args, name, _) in enumerate(plan):
+            ev[r][i].record(s)
+            fn(*args, s.cuda_stream)
+        ev[r][n].record(s)
+    torch.cuda.synchronize()
+    tot = [0.0] * n
+    for r in range(reps):
+        for i in range(n):
+            tot[i] += ev[r][i].elapsed_time(ev[r][i + 1])
+    return [t / reps for t in tot]  # ms per launch
+
+
+def roofline(rt, plan, times, dtype):
+    by = {}
+    for e, t in zip(plan, times):
+        nm = e[2]
+        a = by.setdefault(nm, {"t": 0.0, "n": 0, "flops": 0.0})
+        a["t"] += t
+        a["n"] += 1
+        a["flops"] += plan_flops(rt, e)
+    total = sum(a["t"] for a in by.values())
+    dom = max(by, key=lambda k: by[k]["t"])
+
+    def obj(nm):
+        a = by[nm]
+        avg_ms = a["t"] / a["n"]
+        ach = (a["flops"] / a["n"]) / (avg_ms * 1e-3) / 1e12
+        return {"kernel": nm, "bound": "mfma", "achieved": round(ach, 2), "peak": PEAK[dtype], "unit": "TFLOP/s",
+                "frac": round(ach / PEAK[dtype], 4), "traffic": None, "avg_launch_us": round(avg_ms * 1e3, 2),
+                "launches_per_step": a["n"], "share_of_device_time": round(a["t"] / total, 4)}
+
+    return obj(dom), obj("mam_attention"), total, by
+
+
+def cpu_baseline(variant, B, budget_s=12.0):
+    """Oracle (fp32 CPU restatement of the reference forward), bounded sample."""
+    from mmt_amd import synthetic
+    from oracle.forward import forward as oracle_forward, state_dict_to_torch
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
+    torch.set_num_threads(threads)
+    sd = state_dict_to_torch(synthetic.synth_state_dict(state_dict_keys(variant)))
+    t, o, s = synthetic.synth_inputs(B)
+    oracle_forward(sd, variant, t, o, s)
+    n, t0 = 0, time.perf_counter()
+    while n < 3 or time.perf_counter() - t0 < budget_s:
+        oracle_forward(sd, variant, t, o, s)
+        n += 1
+        if n >= 200:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(n * B / dt, 3), "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": "%d fp32 CPU forwards of B=%d (%s, 128/320), %.1f s, oracle/forward.py" % (n, B, variant, dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=1, help="frames (sequences) per GPU per step")
+    ap.add_argument("--variant", default="rgbt", choices=list(VARIANT_NAMES))
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-graph", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from mmt_amd import synthetic
+    from mmt_amd.runtime import MixFormerRGBTRuntime
+
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    keys = state_dict_keys(args.variant)
+    sd = {k: torch.from_numpy(v) for k, v in synthetic.synth_state_dict(keys).items()}
+    rt = MixFormerRGBTRuntime(sd, args.variant, dtype=dtype)
+    B = args.batch
+    score = args.variant == "asym_online"
+    pool = []
+    for i in range(4):  # distinct frames per rank, resident in HBM before timing
+        t, o, s = synthetic.synth_inputs(B, seed=1 + 4 * rank + i)
+        pool.append(([x.cuda() for x in t], [x.cuda() for x in o], [x.cuda() for x in s]))
+    use_graph = not args.no_graph
+
+    def step(i):
+        t, o, s = pool[i % len(pool)]
+        return rt.forward(t, o, s, run_score_head=score, use_graph=use_graph)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = tt.item()
+
+    ws = rt.workspace(B)
+    plan = ws["plan_score"] if score else ws["plan"]
+    times = kernel_profile(rt, plan)
+    dom, mam, dev_ms, by = roofline(rt, plan, times, args.dtype)
+
+    if rank == 0:
+        frames = world * B * args.steps
+        out = {
+            "metric": METRIC, "value": round(frames / elapsed, 2), "unit": "frames/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+            "data": "synthetic N(0,1) frames (seeded), seed-hash random-init weights (mmt-synth-v1)",
+            "config": {"workload": "%s ViT-B 128px template x2 + 320px search, RGB+TIR, %d frame(s)/GPU/step%s"
+                                   % (VARIANT_NAMES[args.variant], B, ", score head on" if score else ""),
+                       "variant": args.variant, "batch_per_gpu": B, "template": 128, "search": 320,
+                       "parallelism": "replicas" if world > 1 else "single", "hip_graph": use_graph},
+            "roofline": dom, "roofline_mam": mam,
+            "device_ms_per_step_eager": round(dev_ms, 4), "launches_per_step": len(plan),
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.variant, B)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,173 @@
+/*
+ * mmt_hip.h — C ABI of libmmt_hip.so, the MI355X (gfx950) kernels behind the MixFormer RGB-T
+ * tracking forward path.
+ *
+ * Conventions
+ *   - every entry point is `extern "C"`, takes plain device pointers, sizes and a hipStream_t
+ *     (passed as void*), allocates nothing, keeps no global state, and returns 0 on success or
+ *     a negative status (-hipError_t, or MMT_EBADARG for a rejected shape);
+ *   - `dtype` selects the compute/storage type of the matmul operands: MMT_F32 or MMT_BF16
+ *     (bf16 operands, fp32 accumulation, fp32 softmax / norm statistics);
+ *   - tensors are row-major and contiguous unless a stride argument says otherwise.
+ *
+ * What each entry replaces in the reference (LZ-QWQ/Multi-modal-Tracking):
+ *   mmt_ms_deform_attn_forward  pybind `MultiScaleDeformableAttention.ms_deform_attn_forward`
+ *       lib/models/mixformer_vit_rgbt/deformable_attention/ops/src/vision.cpp:13-16,
+ *       ms_deform_attn_cuda.cu:20-80 (same tensor meaning; fp64/fp32/bf16)
+ *   mmt_prroi_pool_forward      `_prroi_pooling.prroi_pooling_forward_cuda`
+ *       external/PreciseRoIPooling/pytorch/prroi_pool/src/prroi_pooling_gpu.c:22-50,
+ *       prroi_pooling_gpu_impl.cu:149-212, 388-400 (plus explicit feature strides)
+ *   mmt_gemm                    the eager nn.Linear / 1x1-conv / 3x3-conv (+BN+ReLU) / patch-embed
+ *       calls of mixformer.py:26-76, :137-138, fusion_utils.py:252-278, deformable_encoder*.py,
+ *       head.py:7-20,159-198, score_decoder.py (implicit GEMM, fused epilogues)
+ *   mmt_mam_attention           Attention.forward MAM softmax(QK^T)V, mixformer.py:52-78 /
+ *       asymmetric_shared.py:55-104
+ *   mmt_layernorm / mmt_groupnorm  nn.LayerNorm / nn.GroupNorm on the hot path
+ *   mmt_patch_im2col            PatchEmbed conv input staging, mixformer.py:29-34
+ *   mmt_msda_bimodal            MSDeformAttn_Bimodal.forward middle part (offset/weight softmax,
+ *       sampling locations, MSDA gather), ms_deform_attn_bimodal.py:97-128
+ *   mmt_corner_softargmax       conv5 + pyramid adds + soft_argmax + box_xyxy_to_cxcywh,
+ *       head.py:191-212, mixformer.py:419-432
+ *   mmt_conv3x3_c1              the 1-channel conv-BN-ReLU of adjust3/adjust4, head.py:115-120
+ *   mmt_spm_attention           ScoreDecoder single-query attention, score_decoder.py:55-61
+ */
+#ifndef MMT_HIP_H_
+#define MMT_HIP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MMT_F32 0
+#define MMT_BF16 1
+#define MMT_F64 2
+#define MMT_EBADARG (-10000)
+#define MMT_MAX_GROUPS 2
+
+/* ---------------------------------------------------------------- GEMM / implicit-GEMM conv
+ * C[g][m][n] = epi( sum_k A[g](m,k) * W[g][n][k] + bias[g][n] )
+ * A addressing (GEMM mode, conv_h == 0):
+ *   seg = m / a_seg_rows, A(m,k) = a[g] + (seg % a_segs_a)*a_stride_a + (seg / a_segs_a)*a_stride_b
+ *                                  + (m % a_seg_rows)*lda + k        (k <  k_split, or k_split == 0)
+ *                                  same with a1[g] and k - k_split       (k >= k_split)
+ * A addressing (conv mode, conv_h > 0): NHWC implicit im2col of a 3x3/pad-1 (conv_k3=1) or 1x1
+ *   conv producing a conv_h x conv_h map; the input map is conv_h/conv_up square, pixel stride
+ *   lda (channels are contiguous, conv_cin of them), k = (ky*3+kx)*conv_cin + ci.
+ * Epilogue: v = act(acc + bias) with act 0 none / 1 GELU(erf) / 2 ReLU;
+ *   c2 == NULL: C = v (+ R if r != NULL);  c2 != NULL: C = v, C2 = v + R.
+ *   R row index: r_mode 0 -> m, 1 -> m % r_p0, 2 -> conv map m=(b,y,x) of an r_p0 x r_p0 map read
+ *   at (y / r_p1, x / r_p1) of an (r_p0/r_p1)^2 map.  R is fp32 (or dtype if r_t); C/C2 are fp32
+ *   if c_f32 else dtype.
+ */
+typedef struct {
+    const void* a[MMT_MAX_GROUPS];
+    const void* a1[MMT_MAX_GROUPS];
+    const void* w[MMT_MAX_GROUPS];
+    const float* bias[MMT_MAX_GROUPS];
+    const float* r[MMT_MAX_GROUPS];
+    void* c[MMT_MAX_GROUPS];
+    void* c2[MMT_MAX_GROUPS];
+    int64_t lda, ldr, ldc;
+    int64_t a_seg_rows, a_segs_a, a_stride_a, a_stride_b;
+    int32_t M, N, K, k_split;
+    int32_t act, c_f32;
+    int32_t r_mode, r_p0, r_p1;
+    int32_t conv_h, conv_up, conv_cin, conv_k3;
+    int32_t groups;
+    int32_t r_t; /* 1: R is stored in `dtype` instead of fp32 */
+} mmt_gemm_params;
+
+int mmt_gemm(const mmt_gemm_params* p, int dtype, void* stream);
+
+/* ---------------------------------------------------------------- MAM attention
+ * qkv: [S][ntok][3*C] (dtype) as produced by the fused qkv Linear (reshape(B,N,3,H,d) order);
+ * out: [S][ntok][C].  Queries [0,n_t) attend keys [0,n_t) of their own sequence; queries
+ * [n_t,ntok) attend all ntok keys (asym == 0) or [tmpl(V) | tmpl(I) | own search] (asym == 1;
+ * sequence s of modality m = s / Bm, batch b = s % Bm).  Head dim C/H must be 64.
+ */
+typedef struct {
+    const void* qkv;
+    void* out;
+    int32_t S, Bm, ntok, n_t, C, H, asym;
+    float scale;
+} mmt_attn_params;
+
+int mmt_mam_attention(const mmt_attn_params* p, int dtype, void* stream);
+
+/* ---------------------------------------------------------------- norms / elementwise
+ * LayerNorm over the last dim C (C % 256 == 0) of fp32 rows; x = in[row] (+ add[row % add_rows]);
+ * gamma/beta chosen per group = row / rows_per_group (up to 2 groups).  Writes out_f32 and/or
+ * out_t (dtype) when non-NULL.
+ */
+int mmt_layernorm(const float* in, const float* add, int64_t add_rows, float* out_f32, void* out_t,
+                  const float* gamma0, const float* beta0, const float* gamma1, const float* beta1,
+                  int64_t rows, int64_t rows_per_group, int C, float eps, int dtype, void* stream);
+
+/* GroupNorm over [n_inst][P][Ctot] fp32 (channels-last, P positions, Ctot channels in `groups`
+ * equal groups), per-instance affine set chosen by inst / inst_per_set (2 sets max).  Outputs
+ * fp32 and/or dtype copies with the same layout. */
+int mmt_groupnorm(const float* in, float* out_f32, void* out_t, const float* gamma0, const float* beta0,
+                  const float* gamma1, const float* beta1, int n_inst, int inst_per_set, int P, int Ctot,
+                  int groups, float eps, int dtype, void* stream);
+
+/* out_t[i] = (dtype) in[i] (+ add[i % add_n] if add) for n elements; also writes out_f32 = in+add
+ * when out_f32 != NULL. */
+int mmt_add_cast(const float* in, const float* add, int64_t add_n, float* out_f32, void* out_t, int64_t n,
+                 int dtype, void* stream);
+
+/* Patch staging for the 16x16/s16 patch-embed conv: for each of S = 2*Bm sequences
+ * (modality m = s / Bm, batch b = s % Bm) the row block [tmpl | online | search] of tokens, each row
+ * = (c, ky, kx) flattened (3*P*P), from fp32 NCHW images img_t[m], img_o[m], img_s[m]. */
+int mmt_patch_im2col(const float* img_t0, const float* img_t1, const float* img_o0, const float* img_o1,
+                     const float* img_s0, const float* img_s1, void* out, int Bm, int ht, int hs, int patch,
+                     int dtype, void* stream);
+
+/* ---------------------------------------------------------------- deformable attention
+ * Reference-op replacement: value (N,S,M,D), spatial_shapes (L,2) int64, level_start (L) int64,
+ * loc (N,Lq,M,L,P,2), attn (N,Lq,M,L,P) -> out (N,Lq,M*D); dtype MMT_F64 / MMT_F32 / MMT_BF16. */
+int mmt_ms_deform_attn_forward(const void* value, const int64_t* spatial_shapes, const int64_t* level_start,
+                               const void* sampling_loc, const void* attn_weight, void* out, int N, int S,
+                               int M, int D, int Lq, int L, int P, int dtype, void* stream);
+
+/* Bimodal encoder layer core (ms_deform_attn_bimodal.py:97-128) for nq queries per modality on an
+ * hw x hw map, 8 heads x 64 ch, 2 levels x 4 points: offw[b*nq+q][192] fp32 = [sampling_offsets
+ * (128) | attention logits (64)] from the [q_v | q_i] Linear; value [2][B][nq][512] (dtype);
+ * out[b*nq+q][512] (dtype) -- identical for both modalities, as in the reference. */
+int mmt_msda_bimodal(const float* offw, const void* value, void* out, int B, int hw, int dtype, void* stream);
+
+/* ---------------------------------------------------------------- corner head / SPM
+ * Cout=1 3x3/pad-1 conv (+bias, BN folded) + ReLU on NHWC input [G][B][h*h][cin] (pixel stride
+ * in_stride) -> out fp32 [G][B][h*h]. */
+int mmt_conv3x3_c1(const void* in, const void* w, const float* bias, float* out, int G, int B, int h,
+                   int cin, int64_t in_stride, int dtype, void* stream);
+
+/* score(p) = x4[g][b][p] . w5[g] + b5[g] + a3[g][b][up4(p)] + a4[g][b][up2(p)] on an fh x fh map
+ * (g = 0 top-left, 1 bottom-right), softmax over the map, expectation of stride*col / stride*row,
+ * / (fh*stride).  boxes_cxcywh / boxes_xyxy: [B][4] fp32.  If rois != NULL also writes the
+ * score-head RoIs [B][5] = (b, box_cxcywh_to_xyxy(cxcywh) * roi_scale) (asymmetric_shared_online.py:409,
+ * score_decoder.py:38-44). */
+int mmt_corner_softargmax(const void* x4, const float* w5, const float* b5, const float* a3, const float* a4,
+                          float* boxes_cxcywh, float* boxes_xyxy, float* rois, float roi_scale, int B, int fh, int c4,
+                          int stride, int dtype, void* stream);
+
+/* PrRoIPool2D forward.  features fp32 with strides (batch, channel, y, x) in elements, rois
+ * [R][5] = (batch, x0, y0, x1, y1); out element (r, c, ph, pw) at r*o_r + c*o_c + (ph*pw_+pw)*o_p
+ * (the reference's [R][C][ph][pw] is o_r = C*ph*pw, o_c = ph*pw, o_p = 1). */
+int mmt_prroi_pool_forward(const float* features, const float* rois, float* out, int R, int C, int H, int W,
+                           int64_t s_b, int64_t s_c, int64_t s_h, int64_t s_w, int ph, int pw,
+                           float spatial_scale, int64_t o_r, int64_t o_c, int64_t o_p, void* stream);
+
+/* ScoreDecoder attention: q [B][C] fp32 (one query per batch), kv [B][Lk][2C] fp32 (k | v),
+ * H heads of C/H (= 64), scale; out [B][C] fp32 (dtype copy optional via out_t). */
+int mmt_spm_attention(const float* q, int64_t q_stride, const float* kv, float* out, int B, int Lk, int C, int H,
+                      float scale, void* stream);
+
+/* Library version string (for diagnostics). */
+const char* mmt_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MMT_HIP_H_ */

@@ -1,0 +1,65 @@
+// Shared device helpers for the gfx950 (CDNA4) kernels of libmmt_hip.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mmt_hip.h"
+
+typedef uint16_t bf16_t;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define MMT_DEV __device__ __forceinline__
+
+MMT_DEV float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+MMT_DEV bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
+
+template <typename T> MMT_DEV float to_f(T v);
+template <> MMT_DEV float to_f<float>(float v) { return v; }
+template <> MMT_DEV float to_f<bf16_t>(bf16_t v) { return bf2f(v); }
+template <typename T> MMT_DEV T from_f(float v);
+template <> MMT_DEV float from_f<float>(float v) { return v; }
+template <> MMT_DEV bf16_t from_f<bf16_t>(float v) { return f2bf(v); }
+
+MMT_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f)); }
+
+MMT_DEV float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+MMT_DEV float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// Block-wide sum for blockDim.x == NT (multiple of 64); `red` needs NT/64 floats of LDS.
+template <int NT>
+MMT_DEV float block_sum(float v, float* red) {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) t += red[i];
+    return t;
+}
+template <int NT>
+MMT_DEV float block_max(float v, float* red) {
+    v = wave_max(v);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    float t = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) t = fmaxf(t, red[i]);
+    return t;
+}
+
+static inline int hip_status(hipError_t e) { return e == hipSuccess ? 0 : -(int)e; }
+static inline int launch_status() { return hip_status(hipGetLastError()); }

@@ -1,0 +1,241 @@
+// Corner-head tail, PrRoIPool and score-decoder attention for gfx950.
+//   mmt_conv3x3_c1         the Cout=1 conv-BN-ReLU closing adjust3_* / adjust4_* (head.py:115-120),
+//                          BN folded into (w, bias) on the host
+//   mmt_corner_softargmax  conv5_* (1x1, 48->1) + F.interpolate(adjust3, x4) + F.interpolate(adjust4,
+//                          x2) (head.py:191-192), softmax over the 80x80 map and the expectation of the
+//                          coordinate grids (head.py:138-145, 200-212), /img_sz, box_xyxy_to_cxcywh
+//                          (lib/utils/box_ops.py:27-32); one workgroup per frame, both corners
+//   mmt_prroi_pool_forward PrRoIPoolingForward (prroi_pooling_gpu_impl.cu:149-212) with explicit
+//                          feature strides so the channels-last fusion output is pooled in place
+//   mmt_spm_attention      ScoreDecoder single-query multi-head attention (score_decoder.py:55-61)
+#include "common.hpp"
+
+namespace {
+
+template <typename T>
+__global__ __launch_bounds__(256) void conv3x3_c1_kernel(const T* __restrict__ in, const T* __restrict__ w,
+                                                         const float* __restrict__ bias, float* __restrict__ out, int B,
+                                                         int h, int cin, int64_t in_stride) {
+    const int g = blockIdx.y;
+    const int64_t npx = (int64_t)B * h * h;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= npx) return;
+    const int b = idx / (h * h), rem = idx % (h * h), y = rem / h, x = rem % h;
+    const T* ib = in + (int64_t)g * npx * in_stride + (int64_t)b * h * h * in_stride;
+    const T* wg = w + (int64_t)g * 9 * cin;
+    float acc = bias[g];
+    for (int ky = 0; ky < 3; ++ky) {
+        const int iy = y + ky - 1;
+        if (iy < 0 || iy >= h) continue;
+        for (int kx = 0; kx < 3; ++kx) {
+            const int ix = x + kx - 1;
+            if (ix < 0 || ix >= h) continue;
+            const T* px = ib + ((int64_t)iy * h + ix) * in_stride;
+            const T* wt = wg + (ky * 3 + kx) * cin;
+            for (int ci = 0; ci < cin; ++ci) acc += to_f<T>(px[ci]) * to_f<T>(wt[ci]);
+        }
+    }
+    out[(int64_t)g * npx + idx] = fmaxf(acc, 0.f);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void corner_softargmax_kernel(const T* __restrict__ x4, const float* __restrict__ w5,
+                                                                const float* __restrict__ b5, const float* __restrict__ a3,
+                                                                const float* __restrict__ a4, float* __restrict__ cxcywh,
+                                                                float* __restrict__ xyxy, float* __restrict__ rois,
+                                                                float roi_scale, int B, int fh, int c4, int stride) {
+    extern __shared__ float sc[];  // fh*fh scores
+    __shared__ float red[4];
+    const int b = blockIdx.x;
+    const int np = fh * fh, f4 = fh / 4, f2 = fh / 2;
+    float res[4];
+    for (int g = 0; g < 2; ++g) {
+        const T* xb = x4 + ((int64_t)g * B + b) * np * c4;
+        const float* wg = w5 + g * c4;
+        const float* a3b = a3 + ((int64_t)g * B + b) * f4 * f4;
+        const float* a4b = a4 + ((int64_t)g * B + b) * f2 * f2;
+        float mx = -INFINITY;
+        for (int p = threadIdx.x; p < np; p += 256) {
+            const int y = p / fh, x = p % fh;
+            const T* px = xb + (int64_t)p * c4;
+            float s = 0.f;
+            for (int ci = 0; ci < c4; ++ci) s += to_f<T>(px[ci]) * wg[ci];
+            s = (s + b5[g]) + a3b[(y / 4) * f4 + x / 4] + a4b[(y / 2) * f2 + x / 2];
+            sc[p] = s;
+            mx = fmaxf(mx, s);
+        }
+        mx = block_max<256>(mx, red);
+        float se = 0.f, sx = 0.f, sy = 0.f;
+        for (int p = threadIdx.x; p < np; p += 256) {
+            const float e = expf(sc[p] - mx);
+            se += e;
+            sx += e * (float)(stride * (p % fh));
+            sy += e * (float)(stride * (p / fh));
+        }
+        se = block_sum<256>(se, red);
+        sx = block_sum<256>(sx, red);
+        sy = block_sum<256>(sy, red);
+        const float img = (float)(fh * stride);
+        res[2 * g] = (sx / se) / img;
+        res[2 * g + 1] = (sy / se) / img;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        if (xyxy) {
+            xyxy[b * 4 + 0] = res[0]; xyxy[b * 4 + 1] = res[1];
+            xyxy[b * 4 + 2] = res[2]; xyxy[b * 4 + 3] = res[3];
+        }
+        const float cx = (res[0] + res[2]) / 2, cy = (res[1] + res[3]) / 2;
+        const float w = res[2] - res[0], h = res[3] - res[1];
+        cxcywh[b * 4 + 0] = cx;
+        cxcywh[b * 4 + 1] = cy;
+        cxcywh[b * 4 + 2] = w;
+        cxcywh[b * 4 + 3] = h;
+        if (rois) {  // box_cxcywh_to_xyxy(coord) * feature size, with the batch index
+            rois[b * 5 + 0] = (float)b;
+            rois[b * 5 + 1] = (cx - 0.5f * w) * roi_scale;
+            rois[b * 5 + 2] = (cy - 0.5f * h) * roi_scale;
+            rois[b * 5 + 3] = (cx + 0.5f * w) * roi_scale;
+            rois[b * 5 + 4] = (cy + 0.5f * h) * roi_scale;
+        }
+    }
+}
+
+MMT_DEV float prroi_get(const float* d, int h, int w, int H, int W, int64_t sh, int64_t sw) {
+    return (h < 0 || w < 0 || h >= H || w >= W) ? 0.f : d[h * sh + w * sw];
+}
+MMT_DEV float prroi_term(float a, float b, float la, float lb) {
+    return (la - 0.5f * la * la - a + 0.5f * a * a) * (lb - 0.5f * lb * lb - b + 0.5f * b * b);
+}
+// PrRoIPoolingMatCalculation, prroi_pooling_gpu_impl.cu:71-106
+MMT_DEV float prroi_mat(const float* d, int s_h, int s_w, int e_h, int e_w, float y0, float x0, float y1, float x1,
+                        int H, int W, int64_t sh, int64_t sw) {
+    float sum = 0.f;
+    float alpha = x0 - (float)s_w, beta = y0 - (float)s_h, la = x1 - (float)s_w, lb = y1 - (float)s_h;
+    sum += prroi_get(d, s_h, s_w, H, W, sh, sw) * prroi_term(alpha, beta, la, lb);
+    alpha = (float)e_w - x1;
+    la = (float)e_w - x0;
+    sum += prroi_get(d, s_h, e_w, H, W, sh, sw) * prroi_term(alpha, beta, la, lb);
+    alpha = x0 - (float)s_w;
+    beta = (float)e_h - y1;
+    la = x1 - (float)s_w;
+    lb = (float)e_h - y0;
+    sum += prroi_get(d, e_h, s_w, H, W, sh, sw) * prroi_term(alpha, beta, la, lb);
+    alpha = (float)e_w - x1;
+    la = (float)e_w - x0;
+    sum += prroi_get(d, e_h, e_w, H, W, sh, sw) * prroi_term(alpha, beta, la, lb);
+    return sum;
+}
+
+__global__ __launch_bounds__(256) void prroi_kernel(const float* __restrict__ feat, const float* __restrict__ rois,
+                                                    float* __restrict__ out, int R, int C, int H, int W, int64_t s_b,
+                                                    int64_t s_c, int64_t s_h, int64_t s_w, int PH, int PW, float scale,
+                                                    int64_t o_r, int64_t o_c, int64_t o_p) {
+    const int64_t total = (int64_t)R * C * PH * PW;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const int pw = idx % PW, ph = (idx / PW) % PH;
+    const int c = (idx / PW / PH) % C;
+    const int n = idx / PW / PH / C;
+    const float* roi = rois + n * 5;
+    const int bi = (int)roi[0];
+    const float x0 = roi[1] * scale, y0 = roi[2] * scale, x1 = roi[3] * scale, y1 = roi[4] * scale;
+    const float rw = fmaxf(x1 - x0, 0.f), rh = fmaxf(y1 - y0, 0.f);
+    const float bh = rh / (float)PH, bw = rw / (float)PW;
+    const float* d = feat + bi * s_b + c * s_c;
+    const float ws = x0 + bw * pw, hs = y0 + bh * ph;
+    const float we = ws + bw, he = hs + bh;
+    const float win = fmaxf(0.f, bw * bh);
+    float* dst = out + (int64_t)n * o_r + (int64_t)c * o_c + (int64_t)(ph * PW + pw) * o_p;
+    if (win == 0.f) {
+        *dst = 0.f;
+        return;
+    }
+    const int sw_ = (int)floorf(ws), ew = (int)ceilf(we), sh_ = (int)floorf(hs), eh = (int)ceilf(he);
+    float sum = 0.f;
+    for (int wi = sw_; wi < ew; ++wi)
+        for (int hi = sh_; hi < eh; ++hi)
+            sum += prroi_mat(d, hi, wi, hi + 1, wi + 1, fmaxf(hs, (float)hi), fmaxf(ws, (float)wi),
+                             fminf(he, (float)hi + 1.f), fminf(we, (float)(wi + 1)), H, W, s_h, s_w);
+    *dst = sum / win;
+}
+
+// one wave per (batch, head); lane = channel within the head (64)
+__global__ __launch_bounds__(64) void spm_attention_kernel(const float* __restrict__ q, int64_t q_stride,
+                                                           const float* __restrict__ kv, float* __restrict__ out, int Lk,
+                                                           int C, float scale) {
+    extern __shared__ float sc[];  // Lk
+    const int h = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
+    const float qd = q[b * q_stride + h * 64 + d];
+    const float* kb = kv + (int64_t)b * Lk * 2 * C + h * 64 + d;
+    float mx = -INFINITY;
+    for (int t = 0; t < Lk; ++t) {
+        const float s = wave_sum(qd * kb[(int64_t)t * 2 * C]) * scale;
+        if (d == 0) sc[t] = s;
+        mx = fmaxf(mx, s);
+    }
+    __syncthreads();
+    float se = 0.f, acc = 0.f;
+    for (int t = 0; t < Lk; ++t) {
+        const float e = expf(sc[t] - mx);
+        se += e;
+        acc += e * kb[(int64_t)t * 2 * C + C];
+    }
+    out[(int64_t)b * C + h * 64 + d] = acc / se;
+}
+
+}  // namespace
+
+extern "C" int mmt_conv3x3_c1(const void* in, const void* w, const float* bias, float* out, int G, int B, int h, int cin,
+                              int64_t in_stride, int dtype, void* stream) {
+    if (!in || !w || !bias || !out || G <= 0 || B <= 0 || h <= 0 || cin <= 0) return MMT_EBADARG;
+    const int64_t npx = (int64_t)B * h * h;
+    dim3 grid((unsigned)((npx + 255) / 256), G);
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == MMT_BF16)
+        hipLaunchKernelGGL(conv3x3_c1_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)in, (const bf16_t*)w, bias,
+                           out, B, h, cin, in_stride);
+    else if (dtype == MMT_F32)
+        hipLaunchKernelGGL(conv3x3_c1_kernel<float>, grid, dim3(256), 0, st, (const float*)in, (const float*)w, bias,
+                           out, B, h, cin, in_stride);
+    else return MMT_EBADARG;
+    return launch_status();
+}
+
+extern "C" int mmt_corner_softargmax(const void* x4, const float* w5, const float* b5, const float* a3, const float* a4,
+                                     float* boxes_cxcywh, float* boxes_xyxy, float* rois, float roi_scale, int B, int fh,
+                                     int c4, int stride, int dtype, void* stream) {
+    if (!x4 || !w5 || !b5 || !a3 || !a4 || !boxes_cxcywh || B <= 0 || fh <= 0 || fh % 4 || c4 <= 0) return MMT_EBADARG;
+    const size_t lds = (size_t)fh * fh * sizeof(float);
+    if (lds > 60000) return MMT_EBADARG;
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == MMT_BF16)
+        hipLaunchKernelGGL(corner_softargmax_kernel<bf16_t>, dim3(B), dim3(256), lds, st, (const bf16_t*)x4, w5, b5, a3,
+                           a4, boxes_cxcywh, boxes_xyxy, rois, roi_scale, B, fh, c4, stride);
+    else if (dtype == MMT_F32)
+        hipLaunchKernelGGL(corner_softargmax_kernel<float>, dim3(B), dim3(256), lds, st, (const float*)x4, w5, b5, a3,
+                           a4, boxes_cxcywh, boxes_xyxy, rois, roi_scale, B, fh, c4, stride);
+    else return MMT_EBADARG;
+    return launch_status();
+}
+
+extern "C" int mmt_prroi_pool_forward(const float* features, const float* rois, float* out, int R, int C, int H, int W,
+                                      int64_t s_b, int64_t s_c, int64_t s_h, int64_t s_w, int ph, int pw,
+                                      float spatial_scale, int64_t o_r, int64_t o_c, int64_t o_p, void* stream) {
+    if (!features || !rois || !out || R < 0 || C <= 0 || H <= 0 || W <= 0 || ph <= 0 || pw <= 0) return MMT_EBADARG;
+    if (R == 0) return 0;
+    const int64_t total = (int64_t)R * C * ph * pw;
+    hipLaunchKernelGGL(prroi_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, features,
+                       rois, out, R, C, H, W, s_b, s_c, s_h, s_w, ph, pw, spatial_scale, o_r, o_c, o_p);
+    return launch_status();
+}
+
+extern "C" int mmt_spm_attention(const float* q, int64_t q_stride, const float* kv, float* out, int B, int Lk, int C,
+                                 int H, float scale, void* stream) {
+    if (!q || !kv || !out || B <= 0 || Lk <= 0 || Lk > 8192 || C != H * 64) return MMT_EBADARG;
+    hipLaunchKernelGGL(spm_attention_kernel, dim3(H, B), dim3(64), Lk * sizeof(float), (hipStream_t)stream, q, q_stride,
+                       kv, out, Lk, C, scale);
+    return launch_status();
+}
+
+extern "C" const char* mmt_version(void) { return "libmmt_hip 0.1 gfx950"; }

@@ -1,0 +1,153 @@
+// Multi-scale deformable attention (MSDA) for gfx950.
+//
+// mmt_ms_deform_attn_forward — drop-in for the reference op `ms_deform_attn_forward`
+//   (ops/src/vision.cpp:13-16 -> ms_deform_attn_cuda.cu:20-80 -> ms_deform_im2col_cuda.cuh:237-299):
+//   out[n,q,m*D+c] = sum_l sum_p w[n,q,m,l,p] * bilinear(V_l[n,:,:,m,c], loc*(W_l,H_l) - 0.5),
+//   taps outside the map read 0 and a sample is skipped unless -1 < h < H and -1 < w < W
+//   (cuh:55-78, :285-291).  fp64 / fp32 / bf16 (the reference dispatches fp32/fp64 only).
+//   One thread per output channel with the channel index fastest: a wave reads whole value rows.
+//
+// mmt_msda_bimodal — the fused middle of MSDeformAttn_Bimodal.forward
+//   (ms_deform_attn_bimodal.py:97-128): softmax of the 8 (level, point) logits per head, sampling
+//   location = reference point of the query's own cell + offset / (W, H), and the bimodal gather
+//   (level 0 = RGB map, level 1 = TIR map).  The reference duplicates the offsets/weights of its
+//   400 bimodal queries onto both 400-query halves and its reference points are per cell, so both
+//   halves produce identical rows; this kernel computes them once (B*nq rows, not 2*B*nq).
+//   Layout: one 512-thread workgroup per (batch, query) = 8 waves = 8 heads, lane = channel.
+#include "common.hpp"
+
+namespace {
+
+template <typename T> struct Acc { using type = float; };
+template <> struct Acc<double> { using type = double; };
+
+template <typename T> MMT_DEV typename Acc<T>::type ld(const T* p) { return to_f<T>(*p); }
+template <> MMT_DEV double ld<double>(const double* p) { return *p; }
+template <typename T> MMT_DEV void st(T* p, typename Acc<T>::type v) { *p = from_f<T>(v); }
+template <> MMT_DEV void st<double>(double* p, double v) { *p = v; }
+
+// ms_deform_attn_im2col_bilinear (cuh:33-84): v points at (0,0) of this (head, channel) plane,
+// `stride` elements between consecutive pixels.
+template <typename T, typename A>
+MMT_DEV A bilinear(const T* v, int H, int W, int64_t stride, A h, A w) {
+    const int hl = (int)floor(h), wl = (int)floor(w);
+    const int hh_ = hl + 1, wh_ = wl + 1;
+    const A lh = h - (A)hl, lw = w - (A)wl;
+    const A hh = (A)1 - lh, hw = (A)1 - lw;
+    A v1 = 0, v2 = 0, v3 = 0, v4 = 0;
+    if (hl >= 0 && wl >= 0) v1 = ld<T>(v + ((int64_t)hl * W + wl) * stride);
+    if (hl >= 0 && wh_ <= W - 1) v2 = ld<T>(v + ((int64_t)hl * W + wh_) * stride);
+    if (hh_ <= H - 1 && wl >= 0) v3 = ld<T>(v + ((int64_t)hh_ * W + wl) * stride);
+    if (hh_ <= H - 1 && wh_ <= W - 1) v4 = ld<T>(v + ((int64_t)hh_ * W + wh_) * stride);
+    const A w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
+    return w1 * v1 + w2 * v2 + w3 * v3 + w4 * v4;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void msda_generic_kernel(const T* __restrict__ value, const int64_t* __restrict__ shapes,
+                                                           const int64_t* __restrict__ lstart, const T* __restrict__ loc,
+                                                           const T* __restrict__ aw, T* __restrict__ out, int N, int S,
+                                                           int M, int D, int Lq, int L, int P, int64_t total) {
+    using A = typename Acc<T>::type;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * blockDim.x) {
+        const int c = idx % D;
+        const int64_t samp = idx / D;  // (n, q, m)
+        const int m = samp % M;
+        const int n = (int)(samp / ((int64_t)M * Lq));
+        int64_t wi = samp * L * P;
+        A col = 0;
+        for (int l = 0; l < L; ++l) {
+            const int H = (int)shapes[2 * l], W = (int)shapes[2 * l + 1];
+            const T* vbase = value + (((int64_t)n * S + lstart[l]) * M + m) * D + c;
+            for (int p = 0; p < P; ++p, ++wi) {
+                const A lx = ld<T>(loc + 2 * wi), ly = ld<T>(loc + 2 * wi + 1), w = ld<T>(aw + wi);
+                const A h_im = ly * (A)H - (A)0.5, w_im = lx * (A)W - (A)0.5;
+                if (h_im > (A)-1 && w_im > (A)-1 && h_im < (A)H && w_im < (A)W)
+                    col += bilinear<T, A>(vbase, H, W, (int64_t)M * D, h_im, w_im) * w;
+            }
+        }
+        st<T>(out + idx, col);
+    }
+}
+
+// 8 heads x 2 levels x 4 points, 64 channels per head.
+template <typename T>
+__global__ __launch_bounds__(512) void msda_bimodal_kernel(const float* __restrict__ offw, const T* __restrict__ value,
+                                                           T* __restrict__ out, int B, int hw) {
+    constexpr int NH = 8, NL = 2, NP = 4, DH = 64, CM = NH * DH;
+    const int row = blockIdx.x;  // b * nq + q
+    const int nq = hw * hw;
+    const int b = row / nq, q = row % nq;
+    const int m = threadIdx.x >> 6, c = threadIdx.x & 63;
+    const float* ow = offw + (int64_t)row * (NH * NL * NP * 3);
+    // softmax over the 8 logits of this head (fp32, max-subtracted)
+    float lg[NL * NP];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < NL * NP; ++i) {
+        lg[i] = ow[NH * NL * NP * 2 + m * NL * NP + i];
+        mx = fmaxf(mx, lg[i]);
+    }
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < NL * NP; ++i) {
+        lg[i] = expf(lg[i] - mx);
+        sum += lg[i];
+    }
+    const float inv = 1.f / sum;
+    const float rx = ((float)(q % hw) + 0.5f) / (float)hw;
+    const float ry = ((float)(q / hw) + 0.5f) / (float)hw;
+    float col = 0.f;
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+        const T* vb = value + ((int64_t)(l * B + b) * nq) * CM + m * DH + c;
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+            const int oi = ((m * NL + l) * NP + p) * 2;
+            const float lx = rx + ow[oi] / (float)hw;
+            const float ly = ry + ow[oi + 1] / (float)hw;
+            const float h_im = ly * (float)hw - 0.5f, w_im = lx * (float)hw - 0.5f;
+            if (h_im > -1.f && w_im > -1.f && h_im < (float)hw && w_im < (float)hw)
+                col += bilinear<T, float>(vb, hw, hw, CM, h_im, w_im) * (lg[l * NP + p] * inv);
+        }
+    }
+    out[(int64_t)row * CM + m * DH + c] = from_f<T>(col);
+}
+
+}  // namespace
+
+extern "C" int mmt_ms_deform_attn_forward(const void* value, const int64_t* spatial_shapes, const int64_t* level_start,
+                                          const void* sampling_loc, const void* attn_weight, void* out, int N, int S,
+                                          int M, int D, int Lq, int L, int P, int dtype, void* stream) {
+    if (!value || !spatial_shapes || !level_start || !sampling_loc || !attn_weight || !out) return MMT_EBADARG;
+    if (N <= 0 || S <= 0 || M <= 0 || D <= 0 || Lq <= 0 || L <= 0 || P <= 0) return MMT_EBADARG;
+    const int64_t total = (int64_t)N * Lq * M * D;
+    const int64_t want = (total + 255) / 256;
+    dim3 grid((unsigned)(want < 65536 ? want : 65536));
+    hipStream_t st = (hipStream_t)stream;
+#define MSDA_CASE(T)                                                                                            \
+    hipLaunchKernelGGL((msda_generic_kernel<T>), grid, dim3(256), 0, st, (const T*)value, spatial_shapes,     \
+                       level_start, (const T*)sampling_loc, (const T*)attn_weight, (T*)out, N, S, M, D, Lq, L, P, \
+                       total)
+    if (dtype == MMT_F32) MSDA_CASE(float);
+    else if (dtype == MMT_F64) MSDA_CASE(double);
+    else if (dtype == MMT_BF16) MSDA_CASE(bf16_t);
+    else return MMT_EBADARG;
+#undef MSDA_CASE
+    return launch_status();
+}
+
+extern "C" int mmt_msda_bimodal(const float* offw, const void* value, void* out, int B, int hw, int dtype,
+                                void* stream) {
+    if (!offw || !value || !out || B <= 0 || hw <= 0) return MMT_EBADARG;
+    dim3 grid((unsigned)(B * hw * hw));
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == MMT_BF16)
+        hipLaunchKernelGGL((msda_bimodal_kernel<bf16_t>), grid, dim3(512), 0, st, offw, (const bf16_t*)value,
+                           (bf16_t*)out, B, hw);
+    else if (dtype == MMT_F32)
+        hipLaunchKernelGGL((msda_bimodal_kernel<float>), grid, dim3(512), 0, st, offw, (const float*)value,
+                           (float*)out, B, hw);
+    else return MMT_EBADARG;
+    return launch_status();
+}

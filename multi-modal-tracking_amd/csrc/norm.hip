@@ -1,0 +1,229 @@
+// Normalisation / staging kernels (HBM-bound, one pass, vectorised 16-B accesses).
+//   mmt_layernorm    nn.LayerNorm of the ViT blocks (eps 1e-6, mixformer.py:137-138; shared/asym
+//                    per-modality norm1_v/_i, norm2_v/_i, mixformer_shared.py:149-157) and of the
+//                    fusion encoder (eps 1e-5, deformable_encoder_lnspecific.py:153-155 with the
+//                    src + output_proj residual fused in via a broadcast row map)
+//   mmt_groupnorm    nn.GroupNorm(32) after the fusion 1x1 convs (fusion_utils.py:252-268)
+//   mmt_add_cast     src + pos -> bf16 query staging (ms_deform_attn_bimodal.py:93-95)
+//   mmt_patch_im2col PatchEmbed input staging for the patch GEMM (mixformer.py:29-34, :237-247)
+#include "common.hpp"
+
+namespace {
+
+// One wave per row; C = 64 * 4 * V floats (V float4 per lane).
+template <typename T, int V>
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ in, const float* __restrict__ add,
+                                                        int64_t add_rows, float* out_f32, T* out_t, const float* g0,
+                                                        const float* b0, const float* g1, const float* b1,
+                                                        int64_t rows, int64_t rpg, float eps) {
+    constexpr int C = 256 * V;
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const float4* x4 = (const float4*)(in + row * C);
+    const float4* a4 = add ? (const float4*)(add + (row % add_rows) * C) : nullptr;
+    float4 v[V];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        v[i] = x4[lane + 64 * i];
+        if (a4) {
+            const float4 a = a4[lane + 64 * i];
+            v[i].x += a.x; v[i].y += a.y; v[i].z += a.z; v[i].w += a.w;
+        }
+        s += v[i].x + v[i].y + v[i].z + v[i].w;
+    }
+    const float mean = wave_sum(s) * (1.f / C);
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        const float dx = v[i].x - mean, dy = v[i].y - mean, dz = v[i].z - mean, dw = v[i].w - mean;
+        q += dx * dx + dy * dy + dz * dz + dw * dw;
+    }
+    const float rstd = rsqrtf(wave_sum(q) * (1.f / C) + eps);
+    const bool second = g1 && (row / rpg) >= 1;
+    const float4* gg = (const float4*)(second ? g1 : g0);
+    const float4* bb = (const float4*)(second ? b1 : b0);
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        const int idx = lane + 64 * i;
+        const float4 ga = gg[idx], be = bb[idx];
+        float4 y;
+        y.x = (v[i].x - mean) * rstd * ga.x + be.x;
+        y.y = (v[i].y - mean) * rstd * ga.y + be.y;
+        y.z = (v[i].z - mean) * rstd * ga.z + be.z;
+        y.w = (v[i].w - mean) * rstd * ga.w + be.w;
+        if (out_f32) ((float4*)(out_f32 + row * C))[idx] = y;
+        if (out_t) {
+            if constexpr (sizeof(T) == 2) {
+                uint2 pk;
+                pk.x = (uint32_t)f2bf(y.x) | ((uint32_t)f2bf(y.y) << 16);
+                pk.y = (uint32_t)f2bf(y.z) | ((uint32_t)f2bf(y.w) << 16);
+                ((uint2*)(out_t + row * C))[idx] = pk;
+            } else {
+                ((float4*)(out_t + row * C))[idx] = y;
+            }
+        }
+    }
+}
+
+// GroupNorm: one block per (instance, group); two passes for the statistics (torch's numerics:
+// mean first, then mean of squared deviations), one pass to write.
+template <typename T>
+__global__ __launch_bounds__(256) void groupnorm_kernel(const float* __restrict__ in, float* out_f32, T* out_t,
+                                                        const float* g0, const float* b0, const float* g1,
+                                                        const float* b1, int inst_per_set, int P, int Ctot, int groups,
+                                                        float eps) {
+    __shared__ float red[4];
+    const int inst = blockIdx.y, grp = blockIdx.x;
+    const int cg = Ctot / groups;
+    const int n = P * cg;
+    const float* x = in + (int64_t)inst * P * Ctot + grp * cg;
+    float s = 0.f;
+    for (int i = threadIdx.x; i < n; i += 256) s += x[(int64_t)(i / cg) * Ctot + (i % cg)];
+    const float mean = block_sum<256>(s, red) / n;
+    float q = 0.f;
+    for (int i = threadIdx.x; i < n; i += 256) {
+        const float d = x[(int64_t)(i / cg) * Ctot + (i % cg)] - mean;
+        q += d * d;
+    }
+    const float rstd = rsqrtf(block_sum<256>(q, red) / n + eps);
+    const bool second = g1 && inst >= inst_per_set;
+    const float* gg = (second ? g1 : g0) + grp * cg;
+    const float* bb = (second ? b1 : b0) + grp * cg;
+    for (int i = threadIdx.x; i < n; i += 256) {
+        const int64_t off = (int64_t)inst * P * Ctot + (int64_t)(i / cg) * Ctot + grp * cg + (i % cg);
+        const float y = (in[off] - mean) * rstd * gg[i % cg] + bb[i % cg];
+        if (out_f32) out_f32[off] = y;
+        if (out_t) out_t[off] = from_f<T>(y);
+    }
+}
+
+template <typename T>
+__global__ void add_cast_kernel(const float* __restrict__ in, const float* __restrict__ add, int64_t add_n,
+                                float* out_f32, T* out_t, int64_t n4) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n4) return;
+    float4 v = ((const float4*)in)[i];
+    if (add) {
+        const float4 a = ((const float4*)add)[i % (add_n / 4)];
+        v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+    }
+    if (out_f32) ((float4*)out_f32)[i] = v;
+    if (out_t) {
+        if constexpr (sizeof(T) == 2) {
+            uint2 pk;
+            pk.x = (uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16);
+            pk.y = (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16);
+            ((uint2*)out_t)[i] = pk;
+        } else {
+            ((float4*)out_t)[i] = v;
+        }
+    }
+}
+
+// One thread per (sequence-row token, channel, ky): 16 contiguous kx pixels -> 16 outputs.
+template <typename T>
+__global__ void patch_im2col_kernel(const float* t0, const float* t1, const float* o0, const float* o1, const float* s0,
+                                    const float* s1, T* out, int Bm, int ht, int hs, int P, int64_t total) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const int gt = ht / P, gs = hs / P;
+    const int nt = gt * gt, ntok = 2 * nt + gs * gs;
+    const int ky = idx % P;
+    const int c = (idx / P) % 3;
+    const int64_t row = idx / (3 * P);
+    const int tok = row % ntok;
+    const int64_t seq = row / ntok;
+    const int m = (int)(seq / Bm), b = (int)(seq % Bm);
+    const float* img;
+    int hw, g, t;
+    if (tok < nt) { img = m ? t1 : t0; hw = ht; g = gt; t = tok; }
+    else if (tok < 2 * nt) { img = m ? o1 : o0; hw = ht; g = gt; t = tok - nt; }
+    else { img = m ? s1 : s0; hw = hs; g = gs; t = tok - 2 * nt; }
+    const int py = t / g, px = t % g;
+    const float* src = img + (((int64_t)b * 3 + c) * hw + (py * P + ky)) * hw + px * P;
+    T* dst = out + row * (3 * P * P) + (c * P + ky) * P;
+    for (int kx = 0; kx < P; kx += 4) {
+        const float4 v = *(const float4*)(src + kx);
+        dst[kx + 0] = from_f<T>(v.x);
+        dst[kx + 1] = from_f<T>(v.y);
+        dst[kx + 2] = from_f<T>(v.z);
+        dst[kx + 3] = from_f<T>(v.w);
+    }
+}
+
+}  // namespace
+
+extern "C" int mmt_layernorm(const float* in, const float* add, int64_t add_rows, float* out_f32, void* out_t,
+                             const float* gamma0, const float* beta0, const float* gamma1, const float* beta1,
+                             int64_t rows, int64_t rows_per_group, int C, float eps, int dtype, void* stream) {
+    if (!in || !gamma0 || !beta0 || rows <= 0 || (C % 256) || C < 256 || C > 1024) return MMT_EBADARG;
+    if (add && add_rows <= 0) return MMT_EBADARG;
+    if (gamma1 && (rows_per_group <= 0 || !beta1)) return MMT_EBADARG;
+    if (rows_per_group <= 0) rows_per_group = rows;
+    hipStream_t st = (hipStream_t)stream;
+    dim3 grid((unsigned)((rows + 3) / 4));
+#define LN_CASE(T, V)                                                                                              \
+    hipLaunchKernelGGL((layernorm_kernel<T, V>), grid, dim3(256), 0, st, in, add, add_rows, out_f32, (T*)out_t,  \
+                       gamma0, beta0, gamma1, beta1, rows, rows_per_group, eps)
+    const int V = C / 256;
+    if (dtype == MMT_BF16) {
+        if (V == 2) LN_CASE(bf16_t, 2); else if (V == 3) LN_CASE(bf16_t, 3); else LN_CASE(bf16_t, 4);
+    } else if (dtype == MMT_F32) {
+        if (V == 2) LN_CASE(float, 2); else if (V == 3) LN_CASE(float, 3); else LN_CASE(float, 4);
+    } else return MMT_EBADARG;
+#undef LN_CASE
+    return launch_status();
+}
+
+extern "C" int mmt_groupnorm(const float* in, float* out_f32, void* out_t, const float* gamma0, const float* beta0,
+                             const float* gamma1, const float* beta1, int n_inst, int inst_per_set, int P, int Ctot,
+                             int groups, float eps, int dtype, void* stream) {
+    if (!in || !gamma0 || !beta0 || n_inst <= 0 || P <= 0 || groups <= 0 || Ctot % groups) return MMT_EBADARG;
+    if (inst_per_set <= 0) inst_per_set = n_inst;
+    dim3 grid(groups, n_inst);
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == MMT_BF16)
+        hipLaunchKernelGGL((groupnorm_kernel<bf16_t>), grid, dim3(256), 0, st, in, out_f32, (bf16_t*)out_t, gamma0,
+                           beta0, gamma1, beta1, inst_per_set, P, Ctot, groups, eps);
+    else if (dtype == MMT_F32)
+        hipLaunchKernelGGL((groupnorm_kernel<float>), grid, dim3(256), 0, st, in, out_f32, (float*)out_t, gamma0,
+                           beta0, gamma1, beta1, inst_per_set, P, Ctot, groups, eps);
+    else return MMT_EBADARG;
+    return launch_status();
+}
+
+extern "C" int mmt_add_cast(const float* in, const float* add, int64_t add_n, float* out_f32, void* out_t, int64_t n,
+                            int dtype, void* stream) {
+    if (!in || n <= 0 || (n % 4) || (add && (add_n <= 0 || add_n % 4))) return MMT_EBADARG;
+    const int64_t n4 = n / 4;
+    dim3 grid((unsigned)((n4 + 255) / 256));
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == MMT_BF16)
+        hipLaunchKernelGGL((add_cast_kernel<bf16_t>), grid, dim3(256), 0, st, in, add, add_n, out_f32, (bf16_t*)out_t, n4);
+    else if (dtype == MMT_F32)
+        hipLaunchKernelGGL((add_cast_kernel<float>), grid, dim3(256), 0, st, in, add, add_n, out_f32, (float*)out_t, n4);
+    else return MMT_EBADARG;
+    return launch_status();
+}
+
+extern "C" int mmt_patch_im2col(const float* img_t0, const float* img_t1, const float* img_o0, const float* img_o1,
+                                const float* img_s0, const float* img_s1, void* out, int Bm, int ht, int hs, int patch,
+                                int dtype, void* stream) {
+    if (!img_t0 || !img_t1 || !img_o0 || !img_o1 || !img_s0 || !img_s1 || !out || Bm <= 0) return MMT_EBADARG;
+    if (patch % 4 || ht % patch || hs % patch) return MMT_EBADARG;
+    const int gt = ht / patch, gs = hs / patch;
+    const int64_t rows = (int64_t)2 * Bm * (2 * gt * gt + gs * gs);
+    const int64_t total = rows * 3 * patch;
+    dim3 grid((unsigned)((total + 255) / 256));
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == MMT_BF16)
+        hipLaunchKernelGGL((patch_im2col_kernel<bf16_t>), grid, dim3(256), 0, st, img_t0, img_t1, img_o0, img_o1,
+                           img_s0, img_s1, (bf16_t*)out, Bm, ht, hs, patch, total);
+    else if (dtype == MMT_F32)
+        hipLaunchKernelGGL((patch_im2col_kernel<float>), grid, dim3(256), 0, st, img_t0, img_t1, img_o0, img_o1,
+                           img_s0, img_s1, (float*)out, Bm, ht, hs, patch, total);
+    else return MMT_EBADARG;
+    return launch_status();
+}

@@ -1,0 +1,85 @@
+"""ctypes binding of libmmt_hip.so (include/mmt_hip.h).
+
+The library is the product: there is no CPU or PyTorch fallback.  If it is missing or fails to
+load, importing this module raises.  torch is imported first so that the library binds to the
+HIP runtime torch already loaded (same SONAME), i.e. streams and device pointers are shared.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (loads the HIP runtime the kernels must share)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmmt_hip.so")
+
+MMT_F32, MMT_BF16, MMT_F64 = 0, 1, 2
+MAX_GROUPS = 2
+
+vp = ctypes.c_void_p
+i32 = ctypes.c_int32
+i64 = ctypes.c_int64
+f32 = ctypes.c_float
+
+
+class GemmParams(ctypes.Structure):
+    _fields_ = [
+        ("a", vp * MAX_GROUPS), ("a1", vp * MAX_GROUPS), ("w", vp * MAX_GROUPS), ("bias", vp * MAX_GROUPS),
+        ("r", vp * MAX_GROUPS), ("c", vp * MAX_GROUPS), ("c2", vp * MAX_GROUPS),
+        ("lda", i64), ("ldr", i64), ("ldc", i64),
+        ("a_seg_rows", i64), ("a_segs_a", i64), ("a_stride_a", i64), ("a_stride_b", i64),
+        ("M", i32), ("N", i32), ("K", i32), ("k_split", i32),
+        ("act", i32), ("c_f32", i32),
+        ("r_mode", i32), ("r_p0", i32), ("r_p1", i32),
+        ("conv_h", i32), ("conv_up", i32), ("conv_cin", i32), ("conv_k3", i32),
+        ("groups", i32), ("r_t", i32),
+    ]
+
+
+class AttnParams(ctypes.Structure):
+    _fields_ = [("qkv", vp), ("out", vp), ("S", i32), ("Bm", i32), ("ntok", i32), ("n_t", i32), ("C", i32),
+                ("H", i32), ("asym", i32), ("scale", f32)]
+
+
+_PROTOS = {
+    "mmt_gemm": [ctypes.POINTER(GemmParams), i32, vp],
+    "mmt_mam_attention": [ctypes.POINTER(AttnParams), i32, vp],
+    "mmt_layernorm": [vp, vp, i64, vp, vp, vp, vp, vp, vp, i64, i64, i32, f32, i32, vp],
+    "mmt_groupnorm": [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, f32, i32, vp],
+    "mmt_add_cast": [vp, vp, i64, vp, vp, i64, i32, vp],
+    "mmt_patch_im2col": [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp],
+    "mmt_ms_deform_attn_forward": [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp],
+    "mmt_msda_bimodal": [vp, vp, vp, i32, i32, i32, vp],
+    "mmt_conv3x3_c1": [vp, vp, vp, vp, i32, i32, i32, i32, i64, i32, vp],
+    "mmt_corner_softargmax": [vp, vp, vp, vp, vp, vp, vp, vp, f32, i32, i32, i32, i32, i32, vp],
+    "mmt_prroi_pool_forward": [vp, vp, vp, i32, i32, i32, i32, i64, i64, i64, i64, i32, i32, f32, i64, i64, i64, vp],
+    "mmt_spm_attention": [vp, i64, vp, vp, i32, i32, i32, i32, f32, vp],
+}
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            "libmmt_hip.so not found at %s: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(or `make -C multi-modal-tracking_amd/csrc`). There is no CPU fallback." % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, args in _PROTOS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = ctypes.c_int
+    lib.mmt_version.argtypes = []
+    lib.mmt_version.restype = ctypes.c_char_p
+    return lib
+
+
+LIB = _load()
+EXPORTED = tuple(_PROTOS) + ("mmt_version",)
+
+
+class MMTError(RuntimeError):
+    pass
+
+
+def check(status, name):
+    if status != 0:
+        if status == -10000:
+            raise MMTError("%s: rejected arguments (MMT_EBADARG)" % name)
+        raise MMTError("%s: HIP error %d" % (name, -status))

@@ -1,0 +1,513 @@
+"""MI355X runtime for one MixFormer RGB-T forward: weights, workspace and launch plan.
+
+The per-frame work is a fixed list of libmmt_hip.so launches (the "plan", ~110-130 calls) over
+a workspace allocated once per batch size; every call's pointers and shapes are resolved when
+the plan is built, so a frame is `for fn, args in plan: fn(*args, stream)` — or one hipGraph
+replay (`capture()`), which removes the host launch cost altogether.
+
+HBM layout (B = frames, S = 2B sequences stored modality-major: s = m*B + b, m = 0 RGB / 1 TIR,
+ntok = 2*n_t + n_s tokens per sequence, C = 768 for ViT-B):
+  X    fp32 [S*ntok][C]      residual stream (patch-embed + pos written straight into it)
+  XN   dt   [S*ntok][C]      LayerNorm output = GEMM A operand
+  QKV  dt   [S*ntok][3C]     fused qkv Linear output, read in place by the MAM kernel
+  AO   dt   [S*ntok][C]      attention output = proj A operand
+  HID  dt   [S*ntok][4C]     GELU(fc1) output
+  fusion encoder: SRC fp32 / SRCT dt [2][B*n_s][512] (modality-major, i.e. the reference's
+  (B, 2*n_s, 512) with the halves as the outer index), head: NHWC maps.
+`dt` is the compute dtype (bf16 or fp32).  Accumulation, softmax and norm statistics are fp32.
+
+Weight preparation (load time, torch on device): casts, Linear/conv weights to [N][K] with
+K = (ky, kx, cin) for convs, eval-mode BatchNorm folded into the conv, the six first-level head
+convs that read the fused map merged into one GEMM (N = 1344), the MSDA offset and weight
+Linears merged (N = 192), fixed position tables and the score-token query constant.
+"""
+import math
+
+import torch
+
+from . import _lib
+from ._lib import LIB, GemmParams, AttnParams, check, MMT_F32, MMT_BF16
+
+VARIANTS = ("rgbt", "shared", "asym", "asym_online")
+
+
+def _ptr(t, off=0):
+    return t.data_ptr() + off * t.element_size()
+
+
+class Dims:
+    def __init__(self, sd, variant):
+        pre = "backbone_v." if variant == "rgbt" else "backbone."
+        self.C = sd[pre + "pos_embed_s"].shape[-1]
+        self.H = self.C // 64
+        self.depth = 0
+        while (pre + "blocks.%d.mlp.fc1.weight" % self.depth) in sd:
+            self.depth += 1
+        self.nt1 = sd[pre + "pos_embed_t"].shape[1]
+        self.ns = sd[pre + "pos_embed_s"].shape[1]
+        self.gt = int(round(self.nt1 ** 0.5))
+        self.gs = int(round(self.ns ** 0.5))
+        self.patch = 16
+        self.ht, self.hs = self.gt * self.patch, self.gs * self.patch
+        self.n_t = 2 * self.nt1
+        self.ntok = self.n_t + self.ns
+        self.hidden = sd[pre + "blocks.0.mlp.fc1.weight"].shape[0]
+        self.d_model = sd["fusion_vi.adjust_v.0.weight"].shape[0]
+        self.fusion_layers = 0
+        while ("fusion_vi.fusion_attention.encoder.layers.%d.linear1.weight" % self.fusion_layers) in sd:
+            self.fusion_layers += 1
+        self.ffn = sd["fusion_vi.fusion_attention.encoder.layers.0.linear1.weight"].shape[0]
+        self.hc = sd["box_head.conv1_tl.0.weight"].shape[0]
+        self.fh = 4 * self.gs
+
+
+class MixFormerRGBTRuntime:
+    """Compiled forward of one of the four hot-path variants on the current CUDA (HIP) device."""
+
+    def __init__(self, state_dict, variant, dtype=torch.bfloat16, device="cuda"):
+        if variant not in VARIANTS:
+            raise ValueError("unknown variant %r" % (variant,))
+        if dtype not in (torch.bfloat16, torch.float32):
+            raise ValueError("dtype must be torch.bfloat16 or torch.float32")
+        self.variant = variant
+        self.dtype = dtype
+        self.cdt = MMT_BF16 if dtype == torch.bfloat16 else MMT_F32
+        self.device = torch.device(device)
+        sd = {k: v.detach() for k, v in state_dict.items()}
+        self.d = Dims(sd, variant)
+        if self.d.C % 256 or self.d.d_model != 512 or self.d.C // 64 * 64 != self.d.C:
+            raise ValueError("unsupported dims C=%d d_model=%d" % (self.d.C, self.d.d_model))
+        self.w = {}
+        self._prepare(sd)
+        self._ws = {}
+        self._graphs = {}
+
+    # ------------------------------------------------------------------ weights
+    def _T(self, x):
+        return x.detach().to(self.device, self.dtype).contiguous()
+
+    def _F(self, x):
+        return x.detach().to(self.device, torch.float32).contiguous()
+
+    def _fold(self, sd, name):
+        """conv() block (head.py:7-20): Conv3x3 -> BatchNorm2d(eval) -> ReLU, BN folded."""
+        w = sd[name + ".0.weight"].double()
+        b = sd[name + ".0.bias"].double()
+        g, beta = sd[name + ".1.weight"].double(), sd[name + ".1.bias"].double()
+        mean, var = sd[name + ".1.running_mean"].double(), sd[name + ".1.running_var"].double()
+        s = g / torch.sqrt(var + 1e-5)
+        w = w * s.view(-1, 1, 1, 1)
+        b = (b - mean) * s + beta
+        return w.permute(0, 2, 3, 1).reshape(w.shape[0], -1), b
+
+    def _prepare(self, sd):
+        d, W = self.d, self.w
+        C = d.C
+        pres = ["backbone_v.", "backbone_i."] if self.variant == "rgbt" else ["backbone."]
+        W["bb"] = []
+        for pre in pres:
+            bb = {"patch_w": self._T(sd[pre + "patch_embed.proj.weight"].reshape(C, -1)),
+                  "patch_b": self._F(sd[pre + "patch_embed.proj.bias"]),
+                  "pos": self._F(torch.cat([sd[pre + "pos_embed_t"][0], sd[pre + "pos_embed_t"][0],
+                                            sd[pre + "pos_embed_s"][0]], 0)),
+                  "blocks": []}
+            for i in range(d.depth):
+                b = pre + "blocks.%d." % i
+                blk = {}
+                for nm in ("attn.qkv", "attn.proj", "mlp.fc1", "mlp.fc2"):
+                    blk[nm + ".w"] = self._T(sd[b + nm + ".weight"])
+                    blk[nm + ".b"] = self._F(sd[b + nm + ".bias"])
+                if self.variant == "rgbt":
+                    for nm in ("norm1", "norm2"):
+                        blk[nm] = (self._F(sd[b + nm + ".weight"]), self._F(sd[b + nm + ".bias"]))
+                else:
+                    for nm in ("norm1", "norm2"):
+                        blk[nm + "_v"] = (self._F(sd[b + nm + "_v.weight"]), self._F(sd[b + nm + "_v.bias"]))
+                        blk[nm + "_i"] = (self._F(sd[b + nm + "_i.weight"]), self._F(sd[b + nm + "_i.bias"]))
+                bb["blocks"].append(blk)
+            W["bb"].append(bb)
+        # fusion
+        f = "fusion_vi."
+        for m in ("v", "i"):
+            W["adj_" + m + ".w"] = self._T(sd[f + "adjust_%s.0.weight" % m].reshape(d.d_model, C))
+            W["adj_" + m + ".b"] = self._F(sd[f + "adjust_%s.0.bias" % m])
+            W["adj_" + m + ".gn"] = (self._F(sd[f + "adjust_%s.1.weight" % m]), self._F(sd[f + "adjust_%s.1.bias" % m]))
+        W["adj_cat.w"] = self._T(sd[f + "adjust_cat.0.weight"].reshape(C, 2 * d.d_model))
+        W["adj_cat.b"] = self._F(sd[f + "adjust_cat.0.bias"])
+        W["adj_cat.gn"] = (self._F(sd[f + "adjust_cat.1.weight"]), self._F(sd[f + "adjust_cat.1.bias"]))
+        fa = f + "fusion_attention."
+        W["level_embed"] = self._F(sd[fa + "level_embed"])
+        W["enc"] = []
+        for li in range(d.fusion_layers):
+            lp = fa + "encoder.layers.%d." % li
+            sa = lp + "self_attn."
+            e = {"value.w": self._T(sd[sa + "value_proj.weight"]), "value.b": self._F(sd[sa + "value_proj.bias"]),
+                 "offw.w": self._T(torch.cat([sd[sa + "sampling_offsets.weight"], sd[sa + "attention_weights.weight"]], 0)),
+                 "offw.b": self._F(torch.cat([sd[sa + "sampling_offsets.bias"], sd[sa + "attention_weights.bias"]], 0)),
+                 "out.w": self._T(sd[sa + "output_proj.weight"]), "out.b": self._F(sd[sa + "output_proj.bias"]),
+                 "l1.w": self._T(sd[lp + "linear1.weight"]), "l1.b": self._F(sd[lp + "linear1.bias"]),
+                 "l2.w": self._T(sd[lp + "linear2.weight"]), "l2.b": self._F(sd[lp + "linear2.bias"])}
+            for nm in ("norm1_v", "norm1_i", "norm2_v", "norm2_i"):
+                e[nm] = (self._F(sd[lp + nm + ".weight"]), self._F(sd[lp + nm + ".bias"]))
+            W["enc"].append(e)
+        W["pos_sine"] = self._F(_sine_pos(d.gs, d.d_model))  # [ns][512]
+        # corner head
+        h = "box_head."
+        ws, bs = [], []
+        for nm in ("conv1_tl", "conv1_br", "adjust1_tl", "adjust1_br", "adjust2_tl", "adjust2_br"):
+            w_, b_ = self._fold(sd, h + nm)
+            ws.append(w_)
+            bs.append(b_)
+        W["h0.w"], W["h0.b"] = self._T(torch.cat(ws, 0)), self._F(torch.cat(bs, 0))
+        for nm in ("conv2", "conv3", "conv4"):
+            for br in ("tl", "br"):
+                w_, b_ = self._fold(sd, h + nm + "_" + br)
+                W[nm + "_" + br + ".w"], W[nm + "_" + br + ".b"] = self._T(w_), self._F(b_)
+        for br in ("tl", "br"):
+            for nm, idx in (("adjust3", 0), ("adjust3", 1), ("adjust4", 0)):
+                w_, b_ = self._fold(sd, h + "%s_%s.%d" % (nm, br, idx))
+                W["%s.%d_%s.w" % (nm, idx, br)], W["%s.%d_%s.b" % (nm, idx, br)] = self._T(w_), self._F(b_)
+        c1 = []
+        for nm in ("adjust3_tl.2", "adjust3_br.2", "adjust4_tl.1", "adjust4_br.1"):
+            c1.append(self._fold(sd, h + nm))
+        W["a3c1.w"] = self._T(torch.stack([c1[0][0][0], c1[1][0][0]]))
+        W["a3c1.b"] = self._F(torch.stack([c1[0][1][0], c1[1][1][0]]))
+        W["a4c1.w"] = self._T(torch.stack([c1[2][0][0], c1[3][0][0]]))
+        W["a4c1.b"] = self._F(torch.stack([c1[2][1][0], c1[3][1][0]]))
+        W["c5.w"] = self._F(torch.stack([sd[h + "conv5_tl.weight"].reshape(-1), sd[h + "conv5_br.weight"].reshape(-1)]))
+        W["c5.b"] = self._F(torch.cat([sd[h + "conv5_tl.bias"], sd[h + "conv5_br.bias"]]))
+        # score decoder (fp32 throughout: its work is negligible)
+        if self.variant == "asym_online":
+            s = "score_branch."
+            F = self._F
+            x0 = torch.nn.functional.layer_norm(sd[s + "score_token"].double().reshape(1, C), (C,),
+                                                sd[s + "norm1.weight"].double(), sd[s + "norm1.bias"].double(), 1e-5)
+            W["spm.q0"] = F(torch.nn.functional.linear(x0, sd[s + "proj_q.0.weight"].double(),
+                                                       sd[s + "proj_q.0.bias"].double()).reshape(C))
+            for i in range(2):
+                W["spm.kv%d.w" % i] = F(torch.cat([sd[s + "proj_k.%d.weight" % i], sd[s + "proj_v.%d.weight" % i]], 0))
+                W["spm.kv%d.b" % i] = F(torch.cat([sd[s + "proj_k.%d.bias" % i], sd[s + "proj_v.%d.bias" % i]], 0))
+                W["spm.proj%d.w" % i], W["spm.proj%d.b" % i] = F(sd[s + "proj.%d.weight" % i]), F(sd[s + "proj.%d.bias" % i])
+                W["spm.norm2.%d" % i] = (F(sd[s + "norm2.%d.weight" % i]), F(sd[s + "norm2.%d.bias" % i]))
+            W["spm.q1.w"], W["spm.q1.b"] = F(sd[s + "proj_q.1.weight"]), F(sd[s + "proj_q.1.bias"])
+            n = 0
+            while (s + "score_head.layers.%d.weight" % n) in sd:
+                W["spm.mlp%d.w" % n] = F(sd[s + "score_head.layers.%d.weight" % n])
+                W["spm.mlp%d.b" % n] = F(sd[s + "score_head.layers.%d.bias" % n])
+                n += 1
+            W["spm.mlp_n"] = n
+
+    # ------------------------------------------------------------------ workspace
+    def workspace(self, B):
+        if B in self._ws:
+            return self._ws[B]
+        d = self.d
+        dev, dt, f32 = self.device, self.dtype, torch.float32
+        S, R, C = 2 * B, 2 * B * d.ntok, d.C
+        ns, dm, hc = d.ns, d.d_model, d.hc
+        e = lambda *shape, t=dt: torch.empty(*shape, device=dev, dtype=t)  # noqa: E731
+        ws = {
+            "B": B,
+            "in_t": [e(B, 3, d.ht, d.ht, t=f32) for _ in range(2)],
+            "in_o": [e(B, 3, d.ht, d.ht, t=f32) for _ in range(2)],
+            "in_s": [e(B, 3, d.hs, d.hs, t=f32) for _ in range(2)],
+            "PATCH": e(R, 3 * d.patch * d.patch), "X": e(R, C, t=f32), "XN": e(R, C), "QKV": e(R, 3 * C),
+            "AO": e(R, C), "HID": e(R, d.hidden), "XT": e(R, C),
+            "Y1": e(2, B * ns, dm, t=f32), "SRC": e(2, B * ns, dm, t=f32), "SRCT": e(2, B * ns, dm),
+            "QS": e(2, B * ns, dm), "VAL": e(2, B * ns, dm), "OFFW": e(B * ns, 192, t=f32), "MS": e(B * ns, dm),
+            "SRC2": e(B * ns, dm, t=f32), "H2": e(2 * B * ns, d.ffn), "Y2": e(B * ns, C, t=f32),
+            "FUS": e(B * ns, C, t=f32), "FUST": e(B * ns, C),
+            "H0": e(B * ns, 2 * hc + hc + hc // 2), "X2": e(2, B * ns, hc // 2), "S1": e(2, B * ns, hc // 2),
+            "X3": e(2, B * 4 * ns, hc // 4), "S2": e(2, B * 4 * ns, hc // 4), "X4": e(2, B * 16 * ns, hc // 8),
+            "A3a": e(2, B * ns, hc // 4), "A3b": e(2, B * ns, hc // 8), "A3": e(2, B, ns, t=f32),
+            "A4a": e(2, B * 4 * ns, hc // 8), "A4": e(2, B, 4 * ns, t=f32),
+            "BOX": e(B, 4, t=f32), "XYXY": e(B, 4, t=f32), "ROIS": e(B, 5, t=f32),
+        }
+        pos = self.w["pos_sine"]  # [ns][512]
+        le = self.w["level_embed"]
+        ws["POSE"] = torch.stack([(pos + le[l]).unsqueeze(0).expand(B, ns, dm).reshape(B * ns, dm)
+                                  for l in range(2)]).contiguous()
+        if self.variant == "asym_online":
+            ws.update({"ROIT": e(B * 16, C, t=f32), "KV0": e(B * 16, 2 * C, t=f32), "AT": e(B, C, t=f32),
+                       "XS": e(B, C, t=f32), "Q1": e(B, C, t=f32), "KV1": e(B * d.n_t, 2 * C, t=f32),
+                       "M1": e(B, C, t=f32), "M2": e(B, C, t=f32), "SC": e(B, 1, t=f32)})
+        ws["plan"] = self._build_plan(ws, False)
+        if self.variant == "asym_online":
+            ws["plan_score"] = self._build_plan(ws, True)
+        self._ws[B] = ws
+        return ws
+
+    # ------------------------------------------------------------------ plan construction
+    def _gemm(self, plan, name, *, a, w, c, M, N, K, lda, ldc, bias=None, r=None, ldr=0, c2=None, a1=None,
+              k_split=0, act=0, c_f32=0, seg=None, r_mode=0, r_p0=0, r_p1=1, conv=None, r_t=0, dtype=None):
+        p = GemmParams()
+        G = len(a)
+        for g in range(G):
+            p.a[g] = a[g]
+            p.w[g] = w[g]
+            p.c[g] = c[g]
+            p.bias[g] = bias[g] if bias else None
+            p.r[g] = r[g] if r else None
+            p.c2[g] = c2[g] if c2 else None
+            p.a1[g] = a1[g] if a1 else None
+        p.lda, p.ldc, p.ldr = lda, ldc, ldr
+        if seg is None:
+            p.a_seg_rows, p.a_segs_a, p.a_stride_a, p.a_stride_b = max(M, 1), 1, 0, 0
+        else:
+            p.a_seg_rows, p.a_segs_a, p.a_stride_a, p.a_stride_b = seg
+        p.M, p.N, p.K, p.k_split = M, N, K, k_split
+        p.act, p.c_f32 = act, c_f32
+        p.r_mode, p.r_p0, p.r_p1 = r_mode, r_p0, r_p1
+        if conv:
+            p.conv_h, p.conv_up, p.conv_cin, p.conv_k3 = conv
+        p.groups = G
+        p.r_t = r_t
+        plan.append((LIB.mmt_gemm, (ctypes_byref(p), self.cdt if dtype is None else dtype), name, p))
+
+    def _build_plan(self, ws, score):
+        d, W, B = self.d, self.w, ws["B"]
+        plan = []
+        C, ntok, ns, nt1, dm = d.C, d.ntok, d.ns, d.nt1, d.d_model
+        S = 2 * B
+        R = S * ntok
+        two = self.variant == "rgbt"
+        P = _ptr
+        X, XN, QKV, AO, HID = ws["X"], ws["XN"], ws["QKV"], ws["AO"], ws["HID"]
+        cdt = self.cdt
+        # --- patch embed (im2col + GEMM, + bias + pos-embed) -> X
+        plan.append((LIB.mmt_patch_im2col, tuple(P(t) for t in ws["in_t"]) + tuple(P(t) for t in ws["in_o"])
+                     + tuple(P(t) for t in ws["in_s"]) + (P(ws["PATCH"]), B, d.ht, d.hs, d.patch, cdt), "patch_im2col", None))
+        KP = 3 * d.patch * d.patch
+        if two:
+            gm = B * ntok
+            self._gemm(plan, "patch_gemm", a=[P(ws["PATCH"]), P(ws["PATCH"], gm * KP)],
+                       w=[P(W["bb"][g]["patch_w"]) for g in range(2)], c=[P(X), P(X, gm * C)], M=gm, N=C, K=KP,
+                       lda=KP, ldc=C, bias=[P(W["bb"][g]["patch_b"]) for g in range(2)],
+                       r=[P(W["bb"][g]["pos"]) for g in range(2)], ldr=C, r_mode=1, r_p0=ntok, c_f32=1)
+        else:
+            self._gemm(plan, "patch_gemm", a=[P(ws["PATCH"])], w=[P(W["bb"][0]["patch_w"])], c=[P(X)], M=R, N=C, K=KP,
+                       lda=KP, ldc=C, bias=[P(W["bb"][0]["patch_b"])], r=[P(W["bb"][0]["pos"])], ldr=C, r_mode=1,
+                       r_p0=ntok, c_f32=1)
+        # --- transformer blocks
+        gm = B * ntok
+        for i in range(d.depth):
+            if two:
+                blks = [W["bb"][g]["blocks"][i] for g in range(2)]
+                n1 = [blks[0]["norm1"], blks[1]["norm1"]]
+                n2 = [blks[0]["norm2"], blks[1]["norm2"]]
+                wl = lambda nm: [P(blks[g][nm]) for g in range(2)]  # noqa: E731
+                rows = lambda t, k: [P(t), P(t, gm * k)]  # noqa: E731
+                Mg = gm
+            else:
+                blk = W["bb"][0]["blocks"][i]
+                n1 = [blk["norm1_v"], blk["norm1_i"]]
+                n2 = [blk["norm2_v"], blk["norm2_i"]]
+                wl = lambda nm: [P(blk[nm])]  # noqa: E731
+                rows = lambda t, k: [P(t)]  # noqa: E731
+                Mg = R
+            plan.append((LIB.mmt_layernorm, (P(X), None, 0, None, P(XN), P(n1[0][0]), P(n1[0][1]), P(n1[1][0]),
+                                             P(n1[1][1]), R, gm, C, 1e-6, cdt), "ln1", None))
+            self._gemm(plan, "qkv", a=rows(XN, C), w=wl("attn.qkv.w"), c=rows(QKV, 3 * C), M=Mg, N=3 * C, K=C,
+                       lda=C, ldc=3 * C, bias=wl("attn.qkv.b"))
+            ap = AttnParams()
+            ap.qkv, ap.out, ap.S, ap.Bm, ap.ntok, ap.n_t, ap.C, ap.H = P(QKV), P(AO), S, B, ntok, d.n_t, C, d.H
+            ap.asym = 1 if self.variant in ("asym", "asym_online") else 0
+            ap.scale = (C // d.H) ** -0.5
+            plan.append((LIB.mmt_mam_attention, (ctypes_byref(ap), cdt), "mam_attention", ap))
+            self._gemm(plan, "proj", a=rows(AO, C), w=wl("attn.proj.w"), c=rows(X, C), M=Mg, N=C, K=C, lda=C,
+                       ldc=C, bias=wl("attn.proj.b"), r=rows(X, C), ldr=C, c_f32=1)
+            plan.append((LIB.mmt_layernorm, (P(X), None, 0, None, P(XN), P(n2[0][0]), P(n2[0][1]), P(n2[1][0]),
+                                             P(n2[1][1]), R, gm, C, 1e-6, cdt), "ln2", None))
+            self._gemm(plan, "fc1", a=rows(XN, C), w=wl("mlp.fc1.w"), c=rows(HID, d.hidden), M=Mg, N=d.hidden, K=C,
+                       lda=C, ldc=d.hidden, bias=wl("mlp.fc1.b"), act=1)
+            self._gemm(plan, "fc2", a=rows(HID, d.hidden), w=wl("mlp.fc2.w"), c=rows(X, C), M=Mg, N=C, K=d.hidden,
+                       lda=d.hidden, ldc=C, bias=wl("mlp.fc2.b"), r=rows(X, C), ldr=C, c_f32=1)
+        XT = ws["XT"]
+        plan.append((LIB.mmt_add_cast, (P(X), None, 0, None, P(XT), R * C, cdt), "cast_x", None))
+        # --- fusion: adjust_v / adjust_i (1x1 conv on the search tokens) + GroupNorm
+        Y1, SRC, SRCT, QS, VAL = ws["Y1"], ws["SRC"], ws["SRCT"], ws["QS"], ws["VAL"]
+        Mf = B * ns
+        self._gemm(plan, "fusion_adjust", a=[P(XT, d.n_t * C), P(XT, B * ntok * C + d.n_t * C)],
+                   w=[P(W["adj_v.w"]), P(W["adj_i.w"])], c=[P(Y1), P(Y1, Mf * dm)], M=Mf, N=dm, K=C, lda=C, ldc=dm,
+                   bias=[P(W["adj_v.b"]), P(W["adj_i.b"])], seg=(ns, 1 << 40, ntok * C, 0), c_f32=1)
+        plan.append((LIB.mmt_groupnorm, (P(Y1), P(SRC), P(SRCT), P(W["adj_v.gn"][0]), P(W["adj_v.gn"][1]),
+                                         P(W["adj_i.gn"][0]), P(W["adj_i.gn"][1]), 2 * B, B, ns, dm, 32, 1e-5, cdt),
+                     "fusion_gn", None))
+        for e in W["enc"]:
+            plan.append((LIB.mmt_add_cast, (P(SRC), P(ws["POSE"]), 2 * Mf * dm, None, P(QS), 2 * Mf * dm, cdt),
+                         "enc_query", None))
+            self._gemm(plan, "enc_value", a=[P(SRCT)], w=[P(e["value.w"])], c=[P(VAL)], M=2 * Mf, N=dm, K=dm, lda=dm,
+                       ldc=dm, bias=[P(e["value.b"])])
+            self._gemm(plan, "enc_offw", a=[P(QS)], a1=[P(QS, Mf * dm)], k_split=dm, w=[P(e["offw.w"])],
+                       c=[P(ws["OFFW"])], M=Mf, N=192, K=2 * dm, lda=dm, ldc=192, bias=[P(e["offw.b"])], c_f32=1)
+            plan.append((LIB.mmt_msda_bimodal, (P(ws["OFFW"]), P(VAL), P(ws["MS"]), B, d.gs, cdt), "msda_bimodal", None))
+            self._gemm(plan, "enc_outproj", a=[P(ws["MS"])], w=[P(e["out.w"])], c=[P(ws["SRC2"])], M=Mf, N=dm, K=dm,
+                       lda=dm, ldc=dm, bias=[P(e["out.b"])], c_f32=1)
+            plan.append((LIB.mmt_layernorm, (P(SRC), P(ws["SRC2"]), Mf, P(SRC), P(SRCT), P(e["norm1_v"][0]),
+                                             P(e["norm1_v"][1]), P(e["norm1_i"][0]), P(e["norm1_i"][1]), 2 * Mf, Mf,
+                                             dm, 1e-5, cdt), "enc_ln1", None))
+            self._gemm(plan, "enc_linear1", a=[P(SRCT)], w=[P(e["l1.w"])], c=[P(ws["H2"])], M=2 * Mf, N=d.ffn, K=dm,
+                       lda=dm, ldc=d.ffn, bias=[P(e["l1.b"])], act=2)
+            self._gemm(plan, "enc_linear2", a=[P(ws["H2"])], w=[P(e["l2.w"])], c=[P(SRC)], M=2 * Mf, N=dm, K=d.ffn,
+                       lda=d.ffn, ldc=dm, bias=[P(e["l2.b"])], r=[P(SRC)], ldr=dm, c_f32=1)
+            plan.append((LIB.mmt_layernorm, (P(SRC), None, 0, P(SRC), P(SRCT), P(e["norm2_v"][0]), P(e["norm2_v"][1]),
+                                             P(e["norm2_i"][0]), P(e["norm2_i"][1]), 2 * Mf, Mf, dm, 1e-5, cdt),
+                         "enc_ln2", None))
+        self._gemm(plan, "fusion_adjust_cat", a=[P(SRCT)], a1=[P(SRCT, Mf * dm)], k_split=dm, w=[P(W["adj_cat.w"])],
+                   c=[P(ws["Y2"])], M=Mf, N=C, K=2 * dm, lda=dm, ldc=C, bias=[P(W["adj_cat.b"])], c_f32=1)
+        plan.append((LIB.mmt_groupnorm, (P(ws["Y2"]), P(ws["FUS"]), P(ws["FUST"]), P(W["adj_cat.gn"][0]),
+                                         P(W["adj_cat.gn"][1]), None, None, B, B, ns, C, 32, 1e-5, cdt),
+                     "fusion_gn_cat", None))
+        # --- corner head (NHWC implicit-GEMM convs, BN folded, upsampling folded into addressing)
+        hc, gs = d.hc, d.gs
+        H0 = ws["H0"]
+        n0 = 2 * hc + hc + hc // 2
+        self._gemm(plan, "head_conv1_adj12", a=[P(ws["FUST"])], w=[P(W["h0.w"])], c=[P(H0)], M=B * ns, N=n0, K=9 * C,
+                   lda=C, ldc=n0, bias=[P(W["h0.b"])], act=2, conv=(gs, 1, C, 1))
+        h2, h4, h8 = hc // 2, hc // 4, hc // 8
+        X2, S1, X3, S2, X4 = ws["X2"], ws["S1"], ws["X3"], ws["S2"], ws["X4"]
+        br = ("tl", "br")
+        self._gemm(plan, "head_conv2", a=[P(H0, g * hc) for g in range(2)], w=[P(W["conv2_%s.w" % b]) for b in br],
+                   c=[P(X2, g * B * ns * h2) for g in range(2)], c2=[P(S1, g * B * ns * h2) for g in range(2)],
+                   r=[P(H0, 2 * hc + g * h2) for g in range(2)], ldr=n0, r_t=1, M=B * ns, N=h2, K=9 * hc, lda=n0,
+                   ldc=h2, bias=[P(W["conv2_%s.b" % b]) for b in br], act=2, conv=(gs, 1, hc, 1))
+        self._gemm(plan, "head_conv3", a=[P(S1, g * B * ns * h2) for g in range(2)], w=[P(W["conv3_%s.w" % b]) for b in br],
+                   c=[P(X3, g * B * 4 * ns * h4) for g in range(2)], c2=[P(S2, g * B * 4 * ns * h4) for g in range(2)],
+                   r=[P(H0, 2 * hc + hc + g * h4) for g in range(2)], ldr=n0, r_t=1, r_mode=2, r_p0=2 * gs, r_p1=2,
+                   M=B * 4 * ns, N=h4, K=9 * h2, lda=h2, ldc=h4, bias=[P(W["conv3_%s.b" % b]) for b in br], act=2,
+                   conv=(2 * gs, 2, h2, 1))
+        self._gemm(plan, "head_conv4", a=[P(S2, g * B * 4 * ns * h4) for g in range(2)], w=[P(W["conv4_%s.w" % b]) for b in br],
+                   c=[P(X4, g * B * 16 * ns * h8) for g in range(2)], M=B * 16 * ns, N=h8, K=9 * h4, lda=h4, ldc=h8,
+                   bias=[P(W["conv4_%s.b" % b]) for b in br], act=2, conv=(4 * gs, 2, h4, 1))
+        self._gemm(plan, "head_adjust3_0", a=[P(X2, g * B * ns * h2) for g in range(2)],
+                   w=[P(W["adjust3.0_%s.w" % b]) for b in br], c=[P(ws["A3a"], g * B * ns * h4) for g in range(2)],
+                   M=B * ns, N=h4, K=9 * h2, lda=h2, ldc=h4, bias=[P(W["adjust3.0_%s.b" % b]) for b in br], act=2,
+                   conv=(gs, 1, h2, 1))
+        self._gemm(plan, "head_adjust3_1", a=[P(ws["A3a"], g * B * ns * h4) for g in range(2)],
+                   w=[P(W["adjust3.1_%s.w" % b]) for b in br], c=[P(ws["A3b"], g * B * ns * h8) for g in range(2)],
+                   M=B * ns, N=h8, K=9 * h4, lda=h4, ldc=h8, bias=[P(W["adjust3.1_%s.b" % b]) for b in br], act=2,
+                   conv=(gs, 1, h4, 1))
+        plan.append((LIB.mmt_conv3x3_c1, (P(ws["A3b"]), P(W["a3c1.w"]), P(W["a3c1.b"]), P(ws["A3"]), 2, B, gs, h8, h8,
+                                          cdt), "head_adjust3_2", None))
+        self._gemm(plan, "head_adjust4_0", a=[P(X3, g * B * 4 * ns * h4) for g in range(2)],
+                   w=[P(W["adjust4.0_%s.w" % b]) for b in br], c=[P(ws["A4a"], g * B * 4 * ns * h8) for g in range(2)],
+                   M=B * 4 * ns, N=h8, K=9 * h4, lda=h4, ldc=h8, bias=[P(W["adjust4.0_%s.b" % b]) for b in br], act=2,
+                   conv=(2 * gs, 1, h4, 1))
+        plan.append((LIB.mmt_conv3x3_c1, (P(ws["A4a"]), P(W["a4c1.w"]), P(W["a4c1.b"]), P(ws["A4"]), 2, B, 2 * gs, h8,
+                                          h8, cdt), "head_adjust4_1", None))
+        plan.append((LIB.mmt_corner_softargmax, (P(X4), P(W["c5.w"]), P(W["c5.b"]), P(ws["A3"]), P(ws["A4"]),
+                                                 P(ws["BOX"]), P(ws["XYXY"]), P(ws["ROIS"]) if score else None,
+                                                 float(gs), B, d.fh, h8, 4, cdt), "corner_softargmax", None))
+        if score:
+            self._plan_spm(plan, ws)
+        return plan
+
+    def _plan_spm(self, plan, ws):
+        """ScoreDecoder (score_decoder.py:32-66), fp32."""
+        d, W, B = self.d, self.w, ws["B"]
+        P, C, ns, gs = _ptr, d.C, d.ns, d.gs
+        F32 = MMT_F32
+        # PrRoIPool(4,4,1.0) on the channels-last fused map -> tokens [B][16][C]
+        plan.append((LIB.mmt_prroi_pool_forward, (P(ws["FUS"]), P(ws["ROIS"]), P(ws["ROIT"]), B, C, gs, gs, ns * C, 1,
+                                                  gs * C, C, 4, 4, 1.0, 16 * C, 1, C), "spm_prroi", None))
+        self._gemm(plan, "spm_kv0", a=[P(ws["ROIT"])], w=[P(W["spm.kv0.w"])], c=[P(ws["KV0"])], M=B * 16, N=2 * C, K=C,
+                   lda=C, ldc=2 * C, bias=[P(W["spm.kv0.b"])], c_f32=1, dtype=F32)
+        scale = C ** -0.5
+        plan.append((LIB.mmt_spm_attention, (P(W["spm.q0"]), 0, P(ws["KV0"]), P(ws["AT"]), B, 16, C, d.H, scale),
+                     "spm_attn0", None))
+        self._gemm(plan, "spm_proj0", a=[P(ws["AT"])], w=[P(W["spm.proj0.w"])], c=[P(ws["XS"])], M=B, N=C, K=C, lda=C,
+                   ldc=C, bias=[P(W["spm.proj0.b"])], c_f32=1, dtype=F32)
+        n = W["spm.norm2.0"]
+        plan.append((LIB.mmt_layernorm, (P(ws["XS"]), None, 0, P(ws["XS"]), None, P(n[0]), P(n[1]), None, None, B, B, C,
+                                         1e-5, F32), "spm_ln0", None))
+        self._gemm(plan, "spm_q1", a=[P(ws["XS"])], w=[P(W["spm.q1.w"])], c=[P(ws["Q1"])], M=B, N=C, K=C, lda=C, ldc=C,
+                   bias=[P(W["spm.q1.b"])], c_f32=1, dtype=F32)
+        # template tokens of both modalities from the fp32 residual stream: [b][m][t]
+        self._gemm(plan, "spm_kv1", a=[P(ws["X"])], w=[P(W["spm.kv1.w"])], c=[P(ws["KV1"])], M=B * 2 * d.nt1, N=2 * C,
+                   K=C, lda=C, ldc=2 * C, bias=[P(W["spm.kv1.b"])], seg=(d.nt1, 2, B * d.ntok * C, d.ntok * C),
+                   c_f32=1, dtype=F32)
+        plan.append((LIB.mmt_spm_attention, (P(ws["Q1"]), C, P(ws["KV1"]), P(ws["AT"]), B, 2 * d.nt1, C, d.H, scale),
+                     "spm_attn1", None))
+        self._gemm(plan, "spm_proj1", a=[P(ws["AT"])], w=[P(W["spm.proj1.w"])], c=[P(ws["XS"])], M=B, N=C, K=C, lda=C,
+                   ldc=C, bias=[P(W["spm.proj1.b"])], c_f32=1, dtype=F32)
+        n = W["spm.norm2.1"]
+        plan.append((LIB.mmt_layernorm, (P(ws["XS"]), None, 0, P(ws["XS"]), None, P(n[0]), P(n[1]), None, None, B, B, C,
+                                         1e-5, F32), "spm_ln1", None))
+        src = ws["XS"]
+        nl = W["spm.mlp_n"]
+        for i in range(nl):
+            last = i == nl - 1
+            dst = ws["SC"] if last else (ws["M1"] if i % 2 == 0 else ws["M2"])
+            N = W["spm.mlp%d.w" % i].shape[0]
+            self._gemm(plan, "spm_mlp%d" % i, a=[P(src)], w=[P(W["spm.mlp%d.w" % i])], c=[P(dst)], M=B, N=N, K=C,
+                       lda=C, ldc=N, bias=[P(W["spm.mlp%d.b" % i])], act=0 if last else 2, c_f32=1, dtype=F32)
+            src = dst
+
+    # ------------------------------------------------------------------ execution
+    def run_plan(self, plan, stream=None):
+        s = torch.cuda.current_stream().cuda_stream if stream is None else stream
+        for fn, args, name, _keep in plan:
+            st = fn(*args, s)
+            if st != 0:
+                check(st, name)
+
+    def load_inputs(self, ws, template, online_template, search):
+        for dst, src in zip(ws["in_t"] + ws["in_o"] + ws["in_s"], list(template) + list(online_template) + list(search)):
+            if src.shape != dst.shape:
+                raise ValueError("input shape %s, expected %s" % (tuple(src.shape), tuple(dst.shape)))
+            dst.copy_(src, non_blocking=True)
+
+    def forward(self, template, online_template, search, run_score_head=False, use_graph=False):
+        """template / online_template / search: [rgb, tir] lists of (B,3,H,W) fp32 device tensors.
+        Returns (boxes_cxcywh (B,4) fp32, scores (B,) fp32 or None) — views of the workspace."""
+        B = template[0].shape[0]
+        ws = self.workspace(B)
+        score = bool(run_score_head) and self.variant == "asym_online"
+        self.load_inputs(ws, template, online_template, search)
+        if use_graph:
+            g = self._graphs.get((B, score))
+            if g is None:
+                g = self.capture(B, score)
+            g.replay()
+        else:
+            self.run_plan(ws["plan_score"] if score else ws["plan"])
+        return ws["BOX"], (ws["SC"].view(-1) if score else None)
+
+    def capture(self, B, score=False):
+        """Record the plan of batch B as one hipGraph (inputs are the workspace's static buffers)."""
+        ws = self.workspace(B)
+        plan = ws["plan_score"] if score else ws["plan"]
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self.run_plan(plan)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.run_plan(plan)
+        self._graphs[(B, score)] = g
+        return g
+
+
+def ctypes_byref(p):
+    import ctypes
+    return ctypes.byref(p)
+
+
+def _sine_pos(g, c):
+    """PositionEmbeddingSine(c/2, normalize=True) on a g x g all-valid map, flattened to
+    [g*g][c] (position_encoding.py:34-54)."""
+    npf = c // 2
+    ones = torch.ones(1, g, g)
+    y = ones.cumsum(1, dtype=torch.float32)
+    x = ones.cumsum(2, dtype=torch.float32)
+    eps, scale = 1e-6, 2 * math.pi
+    y = (y - 0.5) / (y[:, -1:, :] + eps) * scale
+    x = (x - 0.5) / (x[:, :, -1:] + eps) * scale
+    dim_t = torch.arange(npf, dtype=torch.float32)
+    dim_t = 10000 ** (2 * (dim_t // 2) / npf)
+    px = x[:, :, :, None] / dim_t
+    py = y[:, :, :, None] / dim_t
+    px = torch.stack((px[:, :, :, 0::2].sin(), px[:, :, :, 1::2].cos()), dim=4).flatten(3)
+    py = torch.stack((py[:, :, :, 0::2].sin(), py[:, :, :, 1::2].cos()), dim=4).flatten(3)
+    return torch.cat((py, px), dim=3).reshape(g * g, c)

@@ -1,0 +1,64 @@
+"""The C-ABI library loads (without a GPU) and exports every entry point include/mmt_hip.h declares."""
+import ctypes
+import os
+import re
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "mmt_hip.h")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(mmt_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_header_declares_expected_entry_points():
+    syms = declared_symbols()
+    for s in ("mmt_gemm", "mmt_mam_attention", "mmt_ms_deform_attn_forward", "mmt_prroi_pool_forward",
+              "mmt_layernorm", "mmt_groupnorm", "mmt_msda_bimodal", "mmt_corner_softargmax"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol():
+    from mmt_amd import _lib
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [s for s in declared_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+    assert set(declared_symbols()) == set(_lib.EXPORTED)
+    assert _lib.LIB.mmt_version().startswith(b"libmmt_hip")
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """ctypes mirrors of the param structs have the C sizes and field offsets (checked by gcc)."""
+    import subprocess
+    from mmt_amd import _lib
+    fields = [f for f, _ in _lib.GemmParams._fields_]
+    afields = [f for f, _ in _lib.AttnParams._fields_]
+    src = ['#include <stdio.h>', '#include <stddef.h>', '#include "%s"' % HEADER, "int main(void){",
+           'printf("%zu %zu\\n", sizeof(mmt_gemm_params), sizeof(mmt_attn_params));']
+    src += ['printf("%%zu\\n", offsetof(mmt_gemm_params, %s));' % f for f in fields]
+    src += ['printf("%%zu\\n", offsetof(mmt_attn_params, %s));' % f for f in afields]
+    src += ["return 0;}"]
+    c = tmp_path / "abi.c"
+    c.write_text("\n".join(src))
+    exe = tmp_path / "abi"
+    subprocess.check_call(["gcc", str(c), "-o", str(exe)])
+    out = subprocess.check_output([str(exe)]).decode().split()
+    assert int(out[0]) == ctypes.sizeof(_lib.GemmParams)
+    assert int(out[1]) == ctypes.sizeof(_lib.AttnParams)
+    offs = [int(x) for x in out[2:]]
+    assert offs[:len(fields)] == [getattr(_lib.GemmParams, f).offset for f in fields]
+    assert offs[len(fields):] == [getattr(_lib.AttnParams, f).offset for f in afields]
+
+
+def test_bad_arguments_rejected_without_gpu_work():
+    """Shape validation happens on the host before any launch (MMT_EBADARG)."""
+    from mmt_amd import _lib
+    p = _lib.GemmParams()
+    p.M, p.N, p.K, p.groups = 0, 16, 16, 1
+    assert _lib.LIB.mmt_gemm(ctypes.byref(p), _lib.MMT_BF16, None) == -10000
+    a = _lib.AttnParams()
+    a.C, a.H = 100, 2
+    assert _lib.LIB.mmt_mam_attention(ctypes.byref(a), _lib.MMT_BF16, None) == -10000

@@ -1,0 +1,77 @@
+"""End-to-end parity of the HIP forward (mmt_amd.runtime) with the reference golden vectors.
+
+Boxes (cxcywh in [0,1] of the search crop) must match within 1e-3 (fp32 path) / 1e-2 (bf16 path),
+the tolerances BASELINE.json's north_star states; the score logit within the same bounds."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+CASES = [("rgbt", 1), ("shared", 1), ("asym", 1), ("asym_online", 1), ("shared", 2)]
+_RT = {}
+
+
+def _runtime(variant, dtype):
+    key = (variant, dtype)
+    if key not in _RT:
+        from mmt_amd import synthetic
+        from mmt_amd.runtime import MixFormerRGBTRuntime
+        keys = json.load(open(GOLDEN + "/state_dict_%s.json" % variant))
+        sd = {k: torch.from_numpy(v) for k, v in synthetic.synth_state_dict(keys).items()}
+        _RT[key] = MixFormerRGBTRuntime(sd, variant, dtype=dtype)
+    return _RT[key]
+
+
+def _inputs(B):
+    from mmt_amd import synthetic
+    t, o, s = synthetic.synth_inputs(B)
+    return [x.cuda() for x in t], [x.cuda() for x in o], [x.cuda() for x in s]
+
+
+@pytest.mark.parametrize("dname,tol", [("f32", 1e-3), ("bf16", 1e-2)])
+@pytest.mark.parametrize("variant,B", CASES)
+def test_model_matches_reference(variant, B, dname, tol):
+    dtype = torch.float32 if dname == "f32" else torch.bfloat16
+    rt = _runtime(variant, dtype)
+    t, o, s = _inputs(B)
+    score = variant == "asym_online"
+    box, sc = rt.forward(t, o, s, run_score_head=score)
+    torch.cuda.synchronize()
+    gold = np.load(GOLDEN + "/model_%s_b%d.npz" % (variant, B))
+    err = np.abs(box.cpu().numpy() - gold["pred_boxes"].reshape(B, 4)).max()
+    print("%s B=%d %s box err %.3g" % (variant, B, dname, err))
+    assert err <= tol, err
+    if score:
+        serr = np.abs(sc.cpu().numpy() - gold["pred_scores"].reshape(-1)).max()
+        print("score err %.3g" % serr)
+        assert serr <= tol * max(1.0, float(np.abs(gold["pred_scores"]).max())), serr
+
+
+@pytest.mark.parametrize("variant", ["rgbt", "asym_online"])
+def test_graph_replay_is_bitwise_eager(variant):
+    rt = _runtime(variant, torch.bfloat16)
+    t, o, s = _inputs(1)
+    score = variant == "asym_online"
+    b0, s0 = rt.forward(t, o, s, run_score_head=score)
+    b0, s0 = b0.clone(), (s0.clone() if s0 is not None else None)
+    b1, s1 = rt.forward(t, o, s, run_score_head=score, use_graph=True)
+    torch.cuda.synchronize()
+    assert torch.equal(b0, b1)
+    if score:
+        assert torch.equal(s0, s1)
+
+
+def test_batch_rows_independent():
+    """Frame b of a batch equals the same frame run alone (no cross-batch leakage)."""
+    rt = _runtime("asym", torch.bfloat16)
+    t, o, s = _inputs(2)
+    b2, _ = rt.forward(t, o, s)
+    b2 = b2.clone()
+    b1, _ = rt.forward([x[1:2] for x in t], [x[1:2] for x in o], [x[1:2] for x in s])
+    torch.cuda.synchronize()
+    assert (b2[1] - b1[0]).abs().max().item() < 1e-5

@@ -1,0 +1,333 @@
+"""Per-kernel parity of libmmt_hip.so on the GPU against fp32/fp64 references (oracle or torch CPU).
+
+Tolerances: fp32 kernels 1e-4..1e-5 relative to the reference magnitude; bf16 kernels ~1e-2
+(operands rounded to bf16, fp32 accumulation)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+DT = {"f32": torch.float32, "bf16": torch.bfloat16}
+
+
+def _lib():
+    from mmt_amd import _lib
+    return _lib
+
+
+def _gemm(a, w, c, M, N, K, lda, ldc, dtype, **kw):
+    L = _lib()
+    p = L.GemmParams()
+    G = len(a)
+    for g in range(G):
+        p.a[g] = a[g]
+        p.w[g] = w[g]
+        p.c[g] = c[g]
+        p.bias[g] = kw["bias"][g] if kw.get("bias") else None
+        p.r[g] = kw["r"][g] if kw.get("r") else None
+        p.c2[g] = kw["c2"][g] if kw.get("c2") else None
+        p.a1[g] = kw["a1"][g] if kw.get("a1") else None
+    p.lda, p.ldc, p.ldr = lda, ldc, kw.get("ldr", 0)
+    seg = kw.get("seg")
+    p.a_seg_rows, p.a_segs_a, p.a_stride_a, p.a_stride_b = seg if seg else (M, 1, 0, 0)
+    p.M, p.N, p.K, p.k_split = M, N, K, kw.get("k_split", 0)
+    p.act, p.c_f32 = kw.get("act", 0), kw.get("c_f32", 0)
+    p.r_mode, p.r_p0, p.r_p1 = kw.get("r_mode", 0), kw.get("r_p0", 0), kw.get("r_p1", 1)
+    if kw.get("conv"):
+        p.conv_h, p.conv_up, p.conv_cin, p.conv_k3 = kw["conv"]
+    p.groups = G
+    p.r_t = kw.get("r_t", 0)
+    L.check(L.LIB.mmt_gemm(p, L.MMT_BF16 if dtype == torch.bfloat16 else L.MMT_F32,
+                           torch.cuda.current_stream().cuda_stream), "mmt_gemm")
+
+
+def _tol(dt):
+    return 2e-2 if dt == torch.bfloat16 else 2e-5
+
+
+@pytest.mark.parametrize("dname", ["f32", "bf16"])
+@pytest.mark.parametrize("M,N,K,act", [(300, 200, 192, 0), (1056, 2304, 768, 0), (128, 128, 64, 1), (77, 192, 1024, 2)])
+def test_gemm_plain(dname, M, N, K, act):
+    dt = DT[dname]
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g)
+    W = torch.randn(N, K, generator=g) / math.sqrt(K)
+    b = torch.randn(N, generator=g)
+    R = torch.randn(M, N, generator=g)
+    Ad, Wd = A.to(dt).cuda(), W.to(dt).cuda()
+    out = torch.empty(M, N, device="cuda")
+    _gemm([Ad.data_ptr()], [Wd.data_ptr()], [out.data_ptr()], M, N, K, K, N, dt, bias=[b.cuda().data_ptr()],
+          r=[R.cuda().data_ptr()], ldr=N, act=act, c_f32=1)
+    torch.cuda.synchronize()
+    ref = A.to(dt).float() @ W.to(dt).float().t() + b
+    ref = {0: ref, 1: F.gelu(ref), 2: F.relu(ref)}[act] + R
+    err = (out.cpu() - ref).abs().max().item()
+    assert err <= 1e-3 * ref.abs().max().item() + 1e-4, err
+
+
+@pytest.mark.parametrize("dname", ["f32", "bf16"])
+def test_gemm_groups_segments_ksplit(dname):
+    dt = DT[dname]
+    g = torch.Generator().manual_seed(1)
+    # A rows come from segments of 5 rows spaced 9 rows apart (like search tokens after templates),
+    # K split over two sources; two groups with their own weights / outputs.
+    M, N, K, ks = 20, 96, 64, 32
+    src0 = torch.randn(2, 40, ks, generator=g)
+    src1 = torch.randn(2, 40, ks, generator=g)
+    W = torch.randn(2, N, K, generator=g) / 8
+    outs = torch.zeros(2, M, N, device="cuda", dtype=dt)
+    s0, s1, Wd = src0.to(dt).cuda(), src1.to(dt).cuda(), W.to(dt).cuda()
+    _gemm([s0[0].data_ptr() + 4 * ks * s0.element_size(), s0[1].data_ptr() + 4 * ks * s0.element_size()],
+          [Wd[0].data_ptr(), Wd[1].data_ptr()], [outs[0].data_ptr(), outs[1].data_ptr()], M, N, K, ks, N, dt,
+          a1=[s1[0].data_ptr() + 4 * ks * s1.element_size(), s1[1].data_ptr() + 4 * ks * s1.element_size()],
+          k_split=ks, seg=(5, 1 << 40, 9 * ks, 0))
+    torch.cuda.synchronize()
+    for grp in range(2):
+        rows = [4 + 9 * (r // 5) + r % 5 for r in range(M)]
+        A = torch.cat([src0[grp, rows], src1[grp, rows]], 1).to(dt).float()
+        ref = A @ W[grp].to(dt).float().t()
+        err = (outs[grp].float().cpu() - ref).abs().max().item()
+        assert err <= _tol(dt) * ref.abs().max().item(), (grp, err)
+
+
+@pytest.mark.parametrize("dname", ["f32", "bf16"])
+@pytest.mark.parametrize("h,up,cin,cout", [(20, 1, 64, 96), (40, 2, 32, 48), (10, 1, 16, 200)])
+def test_conv3x3_implicit_gemm(dname, h, up, cin, cout):
+    dt = DT[dname]
+    B = 2
+    g = torch.Generator().manual_seed(h + cin)
+    hi = h // up
+    x = torch.randn(B, cin, hi, hi, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) / math.sqrt(9 * cin)
+    b = torch.randn(cout, generator=g)
+    res = torch.randn(B, cout, hi, hi, generator=g)  # residual at the input resolution, read upsampled
+    xin = x.permute(0, 2, 3, 1).contiguous().to(dt).cuda()
+    wk = w.permute(0, 2, 3, 1).reshape(cout, -1).contiguous().to(dt).cuda()
+    rr = res.permute(0, 2, 3, 1).contiguous().cuda()
+    out = torch.empty(B * h * h, cout, device="cuda", dtype=dt)
+    out2 = torch.empty_like(out)
+    _gemm([xin.data_ptr()], [wk.data_ptr()], [out.data_ptr()], B * h * h, cout, 9 * cin, cin, cout, dt,
+          bias=[b.cuda().data_ptr()], act=2, conv=(h, up, cin, 1), c2=[out2.data_ptr()], r=[rr.data_ptr()], ldr=cout,
+          r_mode=2, r_p0=h, r_p1=up)
+    torch.cuda.synchronize()
+    xu = F.interpolate(x.to(dt).float(), scale_factor=up) if up > 1 else x.to(dt).float()
+    ref = F.relu(F.conv2d(xu, w.to(dt).float(), b, padding=1))
+    ref2 = ref + (F.interpolate(res, scale_factor=up) if up > 1 else res)
+    o = out.float().cpu().reshape(B, h, h, cout).permute(0, 3, 1, 2)
+    o2 = out2.float().cpu().reshape(B, h, h, cout).permute(0, 3, 1, 2)
+    tol = _tol(dt) * ref2.abs().max().item() + 1e-5
+    assert (o - ref).abs().max().item() <= tol
+    assert (o2 - ref2).abs().max().item() <= tol
+
+
+def _attn_ref(qkv, S, Bm, ntok, n_t, C, H, asym):
+    d = C // H
+    q, k, v = qkv.view(S, ntok, 3, H, d).permute(2, 0, 3, 1, 4).unbind(0)
+    out = torch.empty(S, H, ntok, d)
+    sc = d ** -0.5
+    for s in range(S):
+        out[s, :, :n_t] = torch.softmax(q[s, :, :n_t] @ k[s, :, :n_t].transpose(-1, -2) * sc, -1) @ v[s, :, :n_t]
+        if asym:
+            b = s % Bm
+            kk = torch.cat([k[b, :, :n_t], k[b + Bm, :, :n_t], k[s, :, n_t:]], 1)
+            vv = torch.cat([v[b, :, :n_t], v[b + Bm, :, :n_t], v[s, :, n_t:]], 1)
+        else:
+            kk, vv = k[s], v[s]
+        out[s, :, n_t:] = torch.softmax(q[s, :, n_t:] @ kk.transpose(-1, -2) * sc, -1) @ vv
+    return out.permute(0, 2, 1, 3).reshape(S, ntok, C)
+
+
+@pytest.mark.parametrize("dname", ["f32", "bf16"])
+@pytest.mark.parametrize("asym", [0, 1])
+@pytest.mark.parametrize("Bm,ntok,n_t,H", [(1, 528, 128, 12), (2, 100, 36, 2), (1, 70, 8, 1)])
+def test_mam_attention(dname, asym, Bm, ntok, n_t, H):
+    dt = DT[dname]
+    L = _lib()
+    S, C = 2 * Bm, 64 * H
+    g = torch.Generator().manual_seed(ntok + asym)
+    qkv = torch.randn(S, ntok, 3 * C, generator=g)
+    qd = qkv.to(dt).cuda()
+    out = torch.empty(S, ntok, C, device="cuda", dtype=dt)
+    p = L.AttnParams()
+    p.qkv, p.out, p.S, p.Bm, p.ntok, p.n_t, p.C, p.H, p.asym, p.scale = qd.data_ptr(), out.data_ptr(), S, Bm, ntok, n_t, C, H, asym, 0.125
+    L.check(L.LIB.mmt_mam_attention(p, L.MMT_BF16 if dt == torch.bfloat16 else L.MMT_F32,
+                                    torch.cuda.current_stream().cuda_stream), "attn")
+    torch.cuda.synchronize()
+    ref = _attn_ref(qkv.to(dt).float(), S, Bm, ntok, n_t, C, H, asym)
+    err = (out.float().cpu() - ref).abs().max().item()
+    assert err <= (1.5e-2 if dt == torch.bfloat16 else 2e-5), err
+
+
+def test_mam_attention_rescale_branch():
+    """Online-softmax rescale forced: one key per query block carries a huge score in a late tile."""
+    L = _lib()
+    S, Bm, ntok, n_t, H, C = 2, 1, 528, 128, 1, 64
+    g = torch.Generator().manual_seed(9)
+    qkv = torch.randn(S, ntok, 3 * C, generator=g) * 0.5
+    qkv[:, 500, C:2 * C] = qkv[:, 300, :C] * 6  # key 500 aligned with query 300
+    qd = qkv.cuda()
+    out = torch.empty(S, ntok, C, device="cuda")
+    p = L.AttnParams()
+    p.qkv, p.out, p.S, p.Bm, p.ntok, p.n_t, p.C, p.H, p.asym, p.scale = qd.data_ptr(), out.data_ptr(), S, Bm, ntok, n_t, C, H, 0, 0.125
+    L.check(L.LIB.mmt_mam_attention(p, L.MMT_F32, torch.cuda.current_stream().cuda_stream), "attn")
+    torch.cuda.synchronize()
+    ref = _attn_ref(qkv.double(), S, Bm, ntok, n_t, C, H, 0).float()
+    assert (out.cpu() - ref).abs().max().item() < 5e-5
+
+
+@pytest.mark.parametrize("dname", ["f32", "bf16"])
+@pytest.mark.parametrize("C", [512, 768, 1024])
+def test_layernorm_groups_and_add(dname, C):
+    dt = DT[dname]
+    L = _lib()
+    rows, rpg = 50, 25
+    g = torch.Generator().manual_seed(C)
+    x = torch.randn(rows, C, generator=g) * 3 + 1
+    add = torch.randn(rpg, C, generator=g)
+    ga, ba, gb, bb = (torch.randn(C, generator=g) for _ in range(4))
+    xd = x.cuda()
+    of = torch.empty(rows, C, device="cuda")
+    ot = torch.empty(rows, C, device="cuda", dtype=dt)
+    gs = [t.cuda() for t in (ga, ba, gb, bb)]
+    L.check(L.LIB.mmt_layernorm(xd.data_ptr(), add.cuda().data_ptr(), rpg, of.data_ptr(), ot.data_ptr(),
+                                *[t.data_ptr() for t in gs], rows, rpg, C, 1e-5,
+                                L.MMT_BF16 if dt == torch.bfloat16 else L.MMT_F32,
+                                torch.cuda.current_stream().cuda_stream), "ln")
+    torch.cuda.synchronize()
+    xa = x + torch.cat([add, add])
+    ref = torch.cat([F.layer_norm(xa[:rpg], (C,), ga, ba, 1e-5), F.layer_norm(xa[rpg:], (C,), gb, bb, 1e-5)])
+    assert (of.cpu() - ref).abs().max().item() < 2e-5
+    assert (ot.float().cpu() - ref).abs().max().item() < (3e-2 if dt == torch.bfloat16 else 2e-5)
+
+
+def test_groupnorm():
+    L = _lib()
+    n, P, Ct, G = 4, 400, 768, 32
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(n, P, Ct, generator=g) * 2 + 0.5
+    ga, ba, gb, bb = (torch.randn(Ct, generator=g) for _ in range(4))
+    out = torch.empty(n, P, Ct, device="cuda")
+    gs = [t.cuda() for t in (ga, ba, gb, bb)]
+    L.check(L.LIB.mmt_groupnorm(x.cuda().data_ptr(), out.data_ptr(), None, *[t.data_ptr() for t in gs], n, 2, P, Ct, G,
+                                1e-5, L.MMT_F32, torch.cuda.current_stream().cuda_stream), "gn")
+    torch.cuda.synchronize()
+    xin = x.permute(0, 2, 1)
+    ref = torch.cat([F.group_norm(xin[:2], G, ga, ba, 1e-5), F.group_norm(xin[2:], G, gb, bb, 1e-5)]).permute(0, 2, 1)
+    assert (out.cpu() - ref).abs().max().item() < 3e-5
+
+
+def _msda_call(value, shapes, starts, loc, w, dtcode):
+    L = _lib()
+    N, S, M, D = value.shape
+    _, Lq, _, Lv, Pn, _ = loc.shape
+    out = torch.empty(N, Lq, M * D, device="cuda", dtype=value.dtype)
+    sh = torch.as_tensor(shapes, dtype=torch.long).cuda()
+    st = torch.as_tensor(starts, dtype=torch.long).cuda()
+    L.check(L.LIB.mmt_ms_deform_attn_forward(value.data_ptr(), sh.data_ptr(), st.data_ptr(), loc.data_ptr(), w.data_ptr(),
+                                             out.data_ptr(), N, S, M, D, Lq, Lv, Pn, dtcode,
+                                             torch.cuda.current_stream().cuda_stream), "msda")
+    torch.cuda.synchronize()
+    return out.cpu()
+
+
+@pytest.mark.parametrize("tag", ["double", "float"])
+def test_msda_reference_op_test_vectors(tag):
+    """ops/test.py:28-59 cases (golden vectors from the reference's own pytorch core)."""
+    L = _lib()
+    z = np.load(GOLDEN + "/op_msda.npz")
+    dt = torch.float64 if tag == "double" else torch.float32
+    v = torch.from_numpy(z["test_%s_value" % tag]).to(dt).cuda()
+    loc = torch.from_numpy(z["test_%s_loc" % tag]).to(dt).cuda()
+    w = torch.from_numpy(z["test_%s_w" % tag]).to(dt).cuda()
+    out = _msda_call(v, [(6, 4), (3, 2)], [0, 24], loc, w, L.MMT_F64 if tag == "double" else L.MMT_F32)
+    ref = torch.from_numpy(z["test_%s_out" % tag])
+    if tag == "double":
+        assert torch.allclose(out, ref.double())
+    else:
+        assert torch.allclose(out, ref, rtol=1e-2, atol=1e-3)
+        assert (out - ref).abs().max().item() < 1e-7
+
+
+@pytest.mark.parametrize("channels", [30, 32, 64, 71, 1025, 2048, 3096])
+def test_msda_channels_sweep(channels):
+    """Channel counts of ops/test.py:62-89 (forward parity vs the oracle restatement, fp64)."""
+    from oracle.msda import ms_deform_attn
+    L = _lib()
+    torch.manual_seed(3)
+    shapes = [(6, 4), (3, 2)]
+    v = torch.rand(1, 30, 2, channels, dtype=torch.float64) * 0.01
+    loc = torch.rand(1, 2, 2, 2, 2, 2, dtype=torch.float64)
+    w = torch.rand(1, 2, 2, 2, 2, dtype=torch.float64) + 1e-5
+    w /= w.sum(-1, keepdim=True).sum(-2, keepdim=True)
+    out = _msda_call(v.cuda(), shapes, [0, 24], loc.cuda(), w.cuda(), L.MMT_F64)
+    ref = ms_deform_attn(v, shapes, [0, 24], loc, w)
+    assert torch.allclose(out, ref, rtol=1e-12, atol=1e-15)
+
+
+@pytest.mark.parametrize("dname", ["f32", "bf16"])
+def test_msda_bimodal_vs_oracle(dname):
+    from oracle.msda import ms_deform_attn
+    dt = DT[dname]
+    L = _lib()
+    B, hw = 2, 20
+    nq = hw * hw
+    g = torch.Generator().manual_seed(11)
+    value = torch.randn(2, B, nq, 512, generator=g)
+    offw = torch.randn(B * nq, 192, generator=g)
+    offw[:, :128] *= 3.0
+    out = torch.empty(B * nq, 512, device="cuda", dtype=dt)
+    L.check(L.LIB.mmt_msda_bimodal(offw.cuda().data_ptr(), value.to(dt).cuda().data_ptr(), out.data_ptr(), B, hw,
+                                   L.MMT_BF16 if dt == torch.bfloat16 else L.MMT_F32,
+                                   torch.cuda.current_stream().cuda_stream), "msda_bimodal")
+    torch.cuda.synchronize()
+    # reference formulation (ms_deform_attn_bimodal.py:97-128) on the v-half queries
+    off = offw[:, :128].view(B, nq, 8, 2, 4, 2)
+    aw = torch.softmax(offw[:, 128:].view(B, nq, 8, 8), -1).view(B, nq, 8, 2, 4)
+    ry, rx = torch.meshgrid(torch.linspace(0.5, hw - 0.5, hw), torch.linspace(0.5, hw - 0.5, hw), indexing="ij")
+    ref_pts = torch.stack([rx.reshape(-1) / hw, ry.reshape(-1) / hw], -1)
+    loc = ref_pts[None, :, None, None, None, :] + off / torch.tensor([hw, hw])
+    val = torch.cat([value[0], value[1]], 1).to(dt).float().view(B, 2 * nq, 8, 64)
+    ref = ms_deform_attn(val, [(hw, hw), (hw, hw)], [0, nq], loc, aw).reshape(B * nq, 512)
+    err = (out.float().cpu() - ref).abs().max().item()
+    assert err <= (2e-2 if dt == torch.bfloat16 else 2e-5) * max(1.0, ref.abs().max().item()), err
+
+
+def test_prroi_known_answer():
+    """test_prroi_pooling2d.py:21-35: integer RoIs at scale 0.5 equal avg_pool2d(k=2, s=1) slices."""
+    from oracle.prroi import prroi_pool2d
+    L = _lib()
+    g = torch.Generator().manual_seed(4)
+    feat = torch.rand(4, 16, 24, 32, generator=g)
+    rois = torch.tensor([[0, 0, 0, 14, 14], [1, 14, 14, 28, 28]], dtype=torch.float32)
+    out = torch.empty(2, 16, 7, 7, device="cuda")
+    fd = feat.cuda()
+    L.check(L.LIB.mmt_prroi_pool_forward(fd.data_ptr(), rois.cuda().data_ptr(), out.data_ptr(), 2, 16, 24, 32,
+                                         16 * 24 * 32, 24 * 32, 32, 1, 7, 7, 0.5, 16 * 49, 49, 1,
+                                         torch.cuda.current_stream().cuda_stream), "prroi")
+    torch.cuda.synchronize()
+    gold = F.avg_pool2d(feat, kernel_size=2, stride=1)
+    ref = torch.stack((gold[0, :, :7, :7], gold[1, :, 7:14, 7:14]), 0)
+    assert torch.allclose(out.cpu(), ref, atol=1e-5)
+    o2 = torch.from_numpy(prroi_pool2d(feat.numpy(), rois.numpy(), 7, 7, 0.5))
+    assert torch.allclose(out.cpu(), o2, atol=1e-6)
+
+
+def test_prroi_fractional_vs_oracle():
+    from oracle.prroi import prroi_pool2d
+    L = _lib()
+    g = torch.Generator().manual_seed(5)
+    feat = torch.randn(2, 8, 20, 20, generator=g)
+    rois = torch.tensor([[0, 1.3, 2.7, 15.2, 9.9], [1, -2.0, 3.5, 7.25, 21.0], [0, 5.0, 5.0, 5.0, 9.0]])
+    out = torch.empty(3, 8, 4, 4, device="cuda")
+    L.check(L.LIB.mmt_prroi_pool_forward(feat.cuda().data_ptr(), rois.cuda().data_ptr(), out.data_ptr(), 3, 8, 20, 20,
+                                         8 * 400, 400, 20, 1, 4, 4, 1.0, 8 * 16, 16, 1,
+                                         torch.cuda.current_stream().cuda_stream), "prroi")
+    torch.cuda.synchronize()
+    ref = torch.from_numpy(prroi_pool2d(feat.numpy(), rois.numpy(), 4, 4, 1.0))
+    assert (out.cpu() - ref).abs().max().item() < 1e-5
