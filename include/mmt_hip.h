@@ -145,12 +145,13 @@ int mmt_conv3x3_c1(const void* in, const void* w, const float* bias, float* out,
 
 /* score(p) = x4[g][b][p] . w5[g] + b5[g] + a3[g][b][up4(p)] + a4[g][b][up2(p)] on an fh x fh map
  * (g = 0 top-left, 1 bottom-right), softmax over the map, expectation of stride*col / stride*row,
- * / (fh*stride).  boxes_cxcywh / boxes_xyxy: [B][4] fp32.  If rois != NULL also writes the
- * score-head RoIs [B][5] = (b, box_cxcywh_to_xyxy(cxcywh) * roi_scale) (asymmetric_shared_online.py:409,
- * score_decoder.py:38-44). */
+ * / (fh*stride).  score_maps: [2][B][fh*fh] fp32 workspace, left holding the two score maps.
+ * boxes_cxcywh / boxes_xyxy: [B][4] fp32.  If rois != NULL also writes the score-head RoIs
+ * [B][5] = (b, box_cxcywh_to_xyxy(cxcywh) * roi_scale) (asymmetric_shared_online.py:409,
+ * score_decoder.py:38-44).  x4 channels c4 must be a multiple of 8 (bf16) / 4 (fp32). */
 int mmt_corner_softargmax(const void* x4, const float* w5, const float* b5, const float* a3, const float* a4,
-                          float* boxes_cxcywh, float* boxes_xyxy, float* rois, float roi_scale, int B, int fh, int c4,
-                          int stride, int dtype, void* stream);
+                          float* score_maps, float* boxes_cxcywh, float* boxes_xyxy, float* rois, float roi_scale,
+                          int B, int fh, int c4, int stride, int dtype, void* stream);
 
 /* PrRoIPool2D forward.  features fp32 with strides (batch, channel, y, x) in elements, rois
  * [R][5] = (batch, x0, y0, x1, y1); out element (r, c, ph, pw) at r*o_r + c*o_c + (ph*pw_+pw)*o_p

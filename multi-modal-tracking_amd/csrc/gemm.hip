@@ -7,26 +7,26 @@
 //   - NHWC implicit-GEMM 3x3 and 1x1 convolutions whose input is read through a nearest-upsample
 //     index map (the pyramid head's F.interpolate + conv, never materialised),
 //   - up to two independent "groups" (modalities / corner branches) per launch (blockIdx.z).
-// Tiling: 128x128 output tile per 256-thread workgroup (4 waves, 2x2, 64x64 per wave as 4x4
-// 16x16 MFMA tiles), K staged 128 bytes per row per step (64 bf16 / 32 fp32) through a
-// double-buffered, XOR-swizzled LDS image (register staging: global loads for step k+1 are in
-// flight while step k runs on the matrix cores).  bf16 uses v_mfma_f32_16x16x32_bf16, fp32 uses
-// the exact-f32 v_mfma_f32_16x16x4_f32.  Epilogue: bias, GELU(erf)/ReLU, fp32 residual with a
-// row map (identity, modulo, or down-sampled conv map), optional second output.
+// Tiling: BMxBN output tile per 256-thread workgroup (4 waves, 2x2; 128x128 for large M, 64x64
+// when the grid would not fill the 256 CUs, which is the batch-1 tracking case), K staged 128
+// bytes per row per step (64 bf16 / 32 fp32) through a double-buffered XOR-swizzled LDS image.
+// Global->LDS staging goes through a ring of DEPTH register sets: DEPTH K-steps of loads are in
+// flight while the matrix cores work on the current one (the batch-1 GEMMs are latency-bound, not
+// bandwidth-bound).  bf16 uses v_mfma_f32_16x16x32_bf16, fp32 the exact-f32 v_mfma_f32_16x16x4_f32.
+// Epilogue: bias, GELU(erf)/ReLU, residual with a row map (identity, modulo, or down-sampled conv
+// map; fp32 or compute dtype), optional second output (C2 = C + R).
 #include "common.hpp"
 
 namespace {
 
-constexpr int BM = 128, BN = 128, NCH = 8, NT = 256;
+constexpr int NCH = 8, NT = 256, DEPTH = 3;
 
-struct ConvGeom {
-    int h, up, cin, k3;
-};
-
-template <typename T, bool CONV>
-__global__ __launch_bounds__(NT, 2) void gemm_kernel(const mmt_gemm_params p) {
+template <typename T, bool CONV, int BM, int BN>
+__global__ __launch_bounds__(NT) void gemm_kernel(const mmt_gemm_params p) {
     constexpr int EPC = 16 / (int)sizeof(T);
     constexpr int KT = NCH * EPC;
+    constexpr int AR = BM / 32, BR = BN / 32;  // staged 16-B chunks per thread per K-step
+    constexpr int WM = BM / 2, WN = BN / 2, MT = WM / 16, NTL = WN / 16;
     __shared__ uint4 lds[2][(BM + BN) * NCH];
 
     const int g = blockIdx.z;
@@ -43,14 +43,13 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const mmt_gemm_params p) {
     const T* W = (const T*)p.w[g];
     const int M = p.M, N = p.N, K = p.K;
 
-    int64_t aoff[4], boff[4];
-    bool aval[4], bval[4];
-    int ay[4], ax[4];
+    int64_t aoff[AR], boff[BR];
+    bool aval[AR], bval[BR];
+    int ay[AR], ax[AR];
     const int ch = p.conv_h, cup = p.conv_up > 0 ? p.conv_up : 1, hi = CONV ? p.conv_h / cup : 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int row = (tid >> 3) + 32 * i;
-        const int m = m0 + row;
+    for (int i = 0; i < AR; ++i) {
+        const int m = m0 + (tid >> 3) + 32 * i;
         aval[i] = m < M;
         if (!CONV) {
             const int64_t seg = m / p.a_seg_rows;
@@ -63,76 +62,84 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const mmt_gemm_params p) {
             ax[i] = rem - ay[i] * ch;
             aoff[i] = (int64_t)b * hi * hi;
         }
-        const int n = n0 + row;
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+        const int n = n0 + (tid >> 3) + 32 * i;
         bval[i] = n < N;
         boff[i] = (int64_t)n * K;
     }
 
-    uint4 ra[4], rb[4];
-    auto load_tile = [&](int kt) {
+    struct Stage {
+        uint4 a[AR], b[BR];
+    };
+    auto load_tile = [&](int kt, Stage& s) {
         const int k = kt * KT + c * EPC;
+        const bool kin = k < K;
+        int iy_d = 0, ix_d = 0, ci = k;
+        if (CONV && p.conv_k3) {
+            const int tap = k / p.conv_cin;
+            ci = k - tap * p.conv_cin;
+            iy_d = tap / 3 - 1;
+            ix_d = tap % 3 - 1;
+        }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < AR; ++i) {
             uint4 v = make_uint4(0, 0, 0, 0);
-            if (aval[i] && k < K) {
+            if (aval[i] && kin) {
                 if (!CONV) {
                     const T* src = (p.k_split > 0 && k >= p.k_split) ? A1 + aoff[i] + (k - p.k_split) : A0 + aoff[i] + k;
                     v = *(const uint4*)src;
                 } else {
-                    int iy = ay[i], ix = ax[i], ci = k;
-                    if (p.conv_k3) {
-                        const int tap = k / p.conv_cin;
-                        ci = k - tap * p.conv_cin;
-                        iy += tap / 3 - 1;
-                        ix += tap % 3 - 1;
-                    }
+                    const int iy = ay[i] + iy_d, ix = ax[i] + ix_d;
                     if (iy >= 0 && ix >= 0 && iy < ch && ix < ch) {
                         const int64_t pix = aoff[i] + (int64_t)(iy / cup) * hi + (ix / cup);
                         v = *(const uint4*)(A0 + pix * p.lda + ci);
                     }
                 }
             }
-            ra[i] = v;
+            s.a[i] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < BR; ++i) {
             uint4 w = make_uint4(0, 0, 0, 0);
-            if (bval[i] && k < K) w = *(const uint4*)(W + boff[i] + k);
-            rb[i] = w;
+            if (bval[i] && kin) w = *(const uint4*)(W + boff[i] + k);
+            s.b[i] = w;
         }
     };
-    auto store_tile = [&](int buf) {
+    auto store_tile = [&](int buf, const Stage& s) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < AR; ++i) {
             const int row = (tid >> 3) + 32 * i;
-            lds[buf][row * NCH + (c ^ (row & 7))] = ra[i];
-            lds[buf][(BM + row) * NCH + (c ^ (row & 7))] = rb[i];
+            lds[buf][row * NCH + (c ^ (row & 7))] = s.a[i];
+        }
+#pragma unroll
+        for (int i = 0; i < BR; ++i) {
+            const int row = (tid >> 3) + 32 * i;
+            lds[buf][(BM + row) * NCH + (c ^ (row & 7))] = s.b[i];
         }
     };
 
-    f32x4 acc[4][4];
+    f32x4 acc[MT][NTL];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MT; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < NTL; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    const int nk = (K + KT - 1) / KT;
-    load_tile(0);
-    store_tile(0);
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-        const int cur = kt & 1;
-        if (kt + 1 < nk) load_tile(kt + 1);
-        const uint4* L = lds[cur];
+    auto compute = [&](int buf) {
+        const uint4* L = lds[buf];
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
             const int sw = (4 * t + lg) ^ (lane & 7);
-            uint4 af[4], bfr[4];
+            uint4 af[MT], bfr[NTL];
 #pragma unroll
-            for (int mt = 0; mt < 4; ++mt) af[mt] = L[(wr * 64 + mt * 16 + l16) * NCH + sw];
+            for (int mt = 0; mt < MT; ++mt) af[mt] = L[(wr * WM + mt * 16 + l16) * NCH + sw];
 #pragma unroll
-            for (int nt = 0; nt < 4; ++nt) bfr[nt] = L[(BM + wc * 64 + nt * 16 + l16) * NCH + sw];
+            for (int nt = 0; nt < NTL; ++nt) bfr[nt] = L[(BM + wc * WN + nt * 16 + l16) * NCH + sw];
 #pragma unroll
-            for (int mt = 0; mt < 4; ++mt)
+            for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-                for (int nt = 0; nt < 4; ++nt) {
+                for (int nt = 0; nt < NTL; ++nt) {
                     if constexpr (sizeof(T) == 2) {
                         acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                             __builtin_bit_cast(bf16x8, af[mt]), __builtin_bit_cast(bf16x8, bfr[nt]), acc[mt][nt], 0, 0, 0);
@@ -145,8 +152,25 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const mmt_gemm_params p) {
                     }
                 }
         }
-        if (kt + 1 < nk) store_tile(cur ^ 1);
-        __syncthreads();
+    };
+
+    // ---- K loop: ring of DEPTH register stages, double-buffered LDS, one barrier per K-step
+    const int nk = (K + KT - 1) / KT;
+    Stage st[DEPTH];
+#pragma unroll
+    for (int j = 0; j < DEPTH; ++j)
+        if (j < nk) load_tile(j, st[j]);
+    for (int k0 = 0; k0 < nk; k0 += DEPTH) {
+#pragma unroll
+        for (int j = 0; j < DEPTH; ++j) {
+            const int kt = k0 + j;
+            if (kt < nk) {
+                store_tile(kt & 1, st[j]);
+                __syncthreads();
+                if (kt + DEPTH < nk) load_tile(kt + DEPTH, st[j]);
+                compute(kt & 1);
+            }
+        }
     }
 
     // ---- epilogue
@@ -156,15 +180,15 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const mmt_gemm_params p) {
     char* C2 = (char*)p.c2[g];
     const int osz = p.c_f32 ? 4 : (int)sizeof(T);
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-            const int n = n0 + wc * 64 + nt * 16 + l16;
+        for (int nt = 0; nt < NTL; ++nt) {
+            const int n = n0 + wc * WN + nt * 16 + l16;
             if (n >= N) continue;
             const float bn = bias ? bias[n] : 0.f;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int m = m0 + wr * 64 + mt * 16 + lg * 4 + r;
+                const int m = m0 + wr * WM + mt * 16 + lg * 4 + r;
                 if (m >= M) continue;
                 float v = acc[mt][nt][r] + bn;
                 if (p.act == 1) v = gelu_erf(v);
@@ -192,6 +216,19 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const mmt_gemm_params p) {
         }
 }
 
+template <typename T, bool CONV>
+void launch_tiles(const mmt_gemm_params& p, hipStream_t st) {
+    auto blocks = [&](int bm, int bn) { return (int64_t)((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn) * p.groups; };
+    // Large problems: 128x128 (best MFMA:LDS ratio).  Otherwise 64x64 to put work on every CU.
+    if (blocks(128, 128) >= 512) {
+        dim3 grid((unsigned)(blocks(128, 128) / p.groups), 1, p.groups);
+        hipLaunchKernelGGL((gemm_kernel<T, CONV, 128, 128>), grid, dim3(NT), 0, st, p);
+    } else {
+        dim3 grid((unsigned)(blocks(64, 64) / p.groups), 1, p.groups);
+        hipLaunchKernelGGL((gemm_kernel<T, CONV, 64, 64>), grid, dim3(NT), 0, st, p);
+    }
+}
+
 template <typename T>
 int launch_gemm(const mmt_gemm_params& p, hipStream_t st) {
     const int EPC = 16 / (int)sizeof(T);
@@ -213,10 +250,8 @@ int launch_gemm(const mmt_gemm_params& p, hipStream_t st) {
         if (p.k_split > 0 && p.conv_h == 0 && (!p.a1[g] || ((uintptr_t)p.a1[g] & 15))) return MMT_EBADARG;
         if (p.c2[g] && !p.r[g]) return MMT_EBADARG;
     }
-    const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-    dim3 grid(tiles, 1, p.groups);
-    if (p.conv_h > 0) hipLaunchKernelGGL((gemm_kernel<T, true>), grid, dim3(NT), 0, st, p);
-    else hipLaunchKernelGGL((gemm_kernel<T, false>), grid, dim3(NT), 0, st, p);
+    if (p.conv_h > 0) launch_tiles<T, true>(p, st);
+    else launch_tiles<T, false>(p, st);
     return launch_status();
 }
 

@@ -12,62 +12,97 @@
 
 namespace {
 
+// 8 lanes per output pixel, each summing a strided slice of the 9*cin/EPC 16-byte chunks.
 template <typename T>
 __global__ __launch_bounds__(256) void conv3x3_c1_kernel(const T* __restrict__ in, const T* __restrict__ w,
                                                          const float* __restrict__ bias, float* __restrict__ out, int B,
                                                          int h, int cin, int64_t in_stride) {
+    constexpr int EPC = 16 / (int)sizeof(T);
     const int g = blockIdx.y;
     const int64_t npx = (int64_t)B * h * h;
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= npx) return;
-    const int b = idx / (h * h), rem = idx % (h * h), y = rem / h, x = rem % h;
-    const T* ib = in + (int64_t)g * npx * in_stride + (int64_t)b * h * h * in_stride;
-    const T* wg = w + (int64_t)g * 9 * cin;
-    float acc = bias[g];
-    for (int ky = 0; ky < 3; ++ky) {
-        const int iy = y + ky - 1;
-        if (iy < 0 || iy >= h) continue;
-        for (int kx = 0; kx < 3; ++kx) {
-            const int ix = x + kx - 1;
-            if (ix < 0 || ix >= h) continue;
-            const T* px = ib + ((int64_t)iy * h + ix) * in_stride;
-            const T* wt = wg + (ky * 3 + kx) * cin;
-            for (int ci = 0; ci < cin; ++ci) acc += to_f<T>(px[ci]) * to_f<T>(wt[ci]);
+    const int64_t idx = (int64_t)blockIdx.x * 32 + (threadIdx.x >> 3);
+    const int sl = threadIdx.x & 7;
+    const int nch = cin / EPC;
+    float acc = 0.f;
+    if (idx < npx) {
+        const int b = idx / (h * h), rem = idx % (h * h), y = rem / h, x = rem % h;
+        const T* ib = in + (int64_t)g * npx * in_stride + (int64_t)b * h * h * in_stride;
+        const T* wg = w + (int64_t)g * 9 * cin;
+        for (int u = sl; u < 9 * nch; u += 8) {
+            const int tap = u / nch, cc = u - tap * nch;
+            const int iy = y + tap / 3 - 1, ix = x + tap % 3 - 1;
+            if (iy < 0 || iy >= h || ix < 0 || ix >= h) continue;
+            const uint4 xv = *(const uint4*)(ib + ((int64_t)iy * h + ix) * in_stride + cc * EPC);
+            const uint4 wv = *(const uint4*)(wg + tap * cin + cc * EPC);
+            if constexpr (sizeof(T) == 2) {
+                const uint32_t xa[4] = {xv.x, xv.y, xv.z, xv.w}, wa[4] = {wv.x, wv.y, wv.z, wv.w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    acc += __uint_as_float(xa[j] << 16) * __uint_as_float(wa[j] << 16);
+                    acc += __uint_as_float(xa[j] & 0xffff0000u) * __uint_as_float(wa[j] & 0xffff0000u);
+                }
+            } else {
+                const f32x4 xf = __builtin_bit_cast(f32x4, xv), wf = __builtin_bit_cast(f32x4, wv);
+                acc += xf[0] * wf[0] + xf[1] * wf[1] + xf[2] * wf[2] + xf[3] * wf[3];
+            }
         }
     }
-    out[(int64_t)g * npx + idx] = fmaxf(acc, 0.f);
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+    acc += __shfl_xor(acc, 4, 64);
+    if (idx < npx && sl == 0) out[(int64_t)g * npx + idx] = fmaxf(acc + bias[g], 0.f);
 }
 
+// score(p) for both corners: conv5 (1x1, c4 -> 1) + up4(adjust3) + up2(adjust4); one thread per pixel.
 template <typename T>
-__global__ __launch_bounds__(256) void corner_softargmax_kernel(const T* __restrict__ x4, const float* __restrict__ w5,
-                                                                const float* __restrict__ b5, const float* __restrict__ a3,
-                                                                const float* __restrict__ a4, float* __restrict__ cxcywh,
-                                                                float* __restrict__ xyxy, float* __restrict__ rois,
-                                                                float roi_scale, int B, int fh, int c4, int stride) {
-    extern __shared__ float sc[];  // fh*fh scores
+__global__ __launch_bounds__(256) void corner_score_kernel(const T* __restrict__ x4, const float* __restrict__ w5,
+                                                           const float* __restrict__ b5, const float* __restrict__ a3,
+                                                           const float* __restrict__ a4, float* __restrict__ maps, int B,
+                                                           int fh, int c4) {
+    constexpr int EPC = 16 / (int)sizeof(T);
+    const int g = blockIdx.y;
+    const int np = fh * fh, f4 = fh / 4, f2 = fh / 2;
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (int64_t)B * np) return;
+    const int b = idx / np, p = idx % np, y = p / fh, x = p % fh;
+    const T* px = x4 + ((int64_t)g * B * np + idx) * c4;
+    const float* wg = w5 + g * c4;
+    float s = 0.f;
+    for (int cc = 0; cc < c4; cc += EPC) {
+        const uint4 v = *(const uint4*)(px + cc);
+        if constexpr (sizeof(T) == 2) {
+            const uint32_t va[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                s += __uint_as_float(va[j] << 16) * wg[cc + 2 * j];
+                s += __uint_as_float(va[j] & 0xffff0000u) * wg[cc + 2 * j + 1];
+            }
+        } else {
+            const f32x4 f = __builtin_bit_cast(f32x4, v);
+            s += f[0] * wg[cc] + f[1] * wg[cc + 1] + f[2] * wg[cc + 2] + f[3] * wg[cc + 3];
+        }
+    }
+    s = (s + b5[g]) + a3[((int64_t)g * B + b) * f4 * f4 + (y / 4) * f4 + x / 4] +
+        a4[((int64_t)g * B + b) * f2 * f2 + (y / 2) * f2 + x / 2];
+    maps[((int64_t)g * B + b) * np + p] = s;
+}
+
+// softmax over each fh x fh map + expectation of the coordinate grids; one workgroup per frame.
+__global__ __launch_bounds__(256) void softargmax_kernel(const float* __restrict__ maps, float* __restrict__ cxcywh,
+                                                         float* __restrict__ xyxy, float* __restrict__ rois,
+                                                         float roi_scale, int B, int fh, int stride) {
     __shared__ float red[4];
     const int b = blockIdx.x;
-    const int np = fh * fh, f4 = fh / 4, f2 = fh / 2;
+    const int np = fh * fh;
     float res[4];
     for (int g = 0; g < 2; ++g) {
-        const T* xb = x4 + ((int64_t)g * B + b) * np * c4;
-        const float* wg = w5 + g * c4;
-        const float* a3b = a3 + ((int64_t)g * B + b) * f4 * f4;
-        const float* a4b = a4 + ((int64_t)g * B + b) * f2 * f2;
+        const float* m = maps + ((int64_t)g * B + b) * np;
         float mx = -INFINITY;
-        for (int p = threadIdx.x; p < np; p += 256) {
-            const int y = p / fh, x = p % fh;
-            const T* px = xb + (int64_t)p * c4;
-            float s = 0.f;
-            for (int ci = 0; ci < c4; ++ci) s += to_f<T>(px[ci]) * wg[ci];
-            s = (s + b5[g]) + a3b[(y / 4) * f4 + x / 4] + a4b[(y / 2) * f2 + x / 2];
-            sc[p] = s;
-            mx = fmaxf(mx, s);
-        }
+        for (int p = threadIdx.x; p < np; p += 256) mx = fmaxf(mx, m[p]);
         mx = block_max<256>(mx, red);
         float se = 0.f, sx = 0.f, sy = 0.f;
         for (int p = threadIdx.x; p < np; p += 256) {
-            const float e = expf(sc[p] - mx);
+            const float e = expf(m[p] - mx);
             se += e;
             sx += e * (float)(stride * (p % fh));
             sy += e * (float)(stride * (p / fh));
@@ -78,7 +113,6 @@ __global__ __launch_bounds__(256) void corner_softargmax_kernel(const T* __restr
         const float img = (float)(fh * stride);
         res[2 * g] = (sx / se) / img;
         res[2 * g + 1] = (sy / se) / img;
-        __syncthreads();
     }
     if (threadIdx.x == 0) {
         if (xyxy) {
@@ -188,9 +222,11 @@ __global__ __launch_bounds__(64) void spm_attention_kernel(const float* __restri
 
 extern "C" int mmt_conv3x3_c1(const void* in, const void* w, const float* bias, float* out, int G, int B, int h, int cin,
                               int64_t in_stride, int dtype, void* stream) {
-    if (!in || !w || !bias || !out || G <= 0 || B <= 0 || h <= 0 || cin <= 0) return MMT_EBADARG;
+    const int epc = dtype == MMT_BF16 ? 8 : 4;
+    if (!in || !w || !bias || !out || G <= 0 || B <= 0 || h <= 0 || cin <= 0 || cin % epc || in_stride % epc)
+        return MMT_EBADARG;
     const int64_t npx = (int64_t)B * h * h;
-    dim3 grid((unsigned)((npx + 255) / 256), G);
+    dim3 grid((unsigned)((npx + 31) / 32), G);
     hipStream_t st = (hipStream_t)stream;
     if (dtype == MMT_BF16)
         hipLaunchKernelGGL(conv3x3_c1_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)in, (const bf16_t*)w, bias,
@@ -203,19 +239,23 @@ extern "C" int mmt_conv3x3_c1(const void* in, const void* w, const float* bias, 
 }
 
 extern "C" int mmt_corner_softargmax(const void* x4, const float* w5, const float* b5, const float* a3, const float* a4,
-                                     float* boxes_cxcywh, float* boxes_xyxy, float* rois, float roi_scale, int B, int fh,
-                                     int c4, int stride, int dtype, void* stream) {
-    if (!x4 || !w5 || !b5 || !a3 || !a4 || !boxes_cxcywh || B <= 0 || fh <= 0 || fh % 4 || c4 <= 0) return MMT_EBADARG;
-    const size_t lds = (size_t)fh * fh * sizeof(float);
-    if (lds > 60000) return MMT_EBADARG;
+                                     float* score_maps, float* boxes_cxcywh, float* boxes_xyxy, float* rois,
+                                     float roi_scale, int B, int fh, int c4, int stride, int dtype, void* stream) {
+    const int epc = dtype == MMT_BF16 ? 8 : 4;
+    if (!x4 || !w5 || !b5 || !a3 || !a4 || !score_maps || !boxes_cxcywh || B <= 0 || fh <= 0 || fh % 4 || c4 <= 0 ||
+        c4 % epc)
+        return MMT_EBADARG;
     hipStream_t st = (hipStream_t)stream;
+    dim3 grid((unsigned)(((int64_t)B * fh * fh + 255) / 256), 2);
     if (dtype == MMT_BF16)
-        hipLaunchKernelGGL(corner_softargmax_kernel<bf16_t>, dim3(B), dim3(256), lds, st, (const bf16_t*)x4, w5, b5, a3,
-                           a4, boxes_cxcywh, boxes_xyxy, rois, roi_scale, B, fh, c4, stride);
+        hipLaunchKernelGGL(corner_score_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)x4, w5, b5, a3, a4,
+                           score_maps, B, fh, c4);
     else if (dtype == MMT_F32)
-        hipLaunchKernelGGL(corner_softargmax_kernel<float>, dim3(B), dim3(256), lds, st, (const float*)x4, w5, b5, a3,
-                           a4, boxes_cxcywh, boxes_xyxy, rois, roi_scale, B, fh, c4, stride);
+        hipLaunchKernelGGL(corner_score_kernel<float>, grid, dim3(256), 0, st, (const float*)x4, w5, b5, a3, a4,
+                           score_maps, B, fh, c4);
     else return MMT_EBADARG;
+    hipLaunchKernelGGL(softargmax_kernel, dim3(B), dim3(256), 0, st, score_maps, boxes_cxcywh, boxes_xyxy, rois,
+                       roi_scale, B, fh, stride);
     return launch_status();
 }
 

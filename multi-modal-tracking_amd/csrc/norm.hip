@@ -67,35 +67,68 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
     }
 }
 
-// GroupNorm: one block per (instance, group); two passes for the statistics (torch's numerics:
-// mean first, then mean of squared deviations), one pass to write.
+// GroupNorm: one 512-thread workgroup per (instance, group); the group's values (P positions x cg
+// channels, float4 granules) stay in registers, so the input is read once; two-pass statistics
+// (mean, then mean of squared deviations) as torch computes them.
+constexpr int GN_THREADS = 512, GN_VMAX = 12;
+
 template <typename T>
-__global__ __launch_bounds__(256) void groupnorm_kernel(const float* __restrict__ in, float* out_f32, T* out_t,
-                                                        const float* g0, const float* b0, const float* g1,
-                                                        const float* b1, int inst_per_set, int P, int Ctot, int groups,
-                                                        float eps) {
-    __shared__ float red[4];
+__global__ __launch_bounds__(GN_THREADS) void groupnorm_kernel(const float* __restrict__ in, float* out_f32, T* out_t,
+                                                               const float* g0, const float* b0, const float* g1,
+                                                               const float* b1, int inst_per_set, int P, int Ctot,
+                                                               int groups, float eps) {
+    __shared__ float red[GN_THREADS / 64];
     const int inst = blockIdx.y, grp = blockIdx.x;
-    const int cg = Ctot / groups;
-    const int n = P * cg;
-    const float* x = in + (int64_t)inst * P * Ctot + grp * cg;
+    const int cg = Ctot / groups, q = cg / 4, items = P * q;
+    const int64_t base = (int64_t)inst * P * Ctot + grp * cg;
+    float4 v[GN_VMAX];
     float s = 0.f;
-    for (int i = threadIdx.x; i < n; i += 256) s += x[(int64_t)(i / cg) * Ctot + (i % cg)];
-    const float mean = block_sum<256>(s, red) / n;
-    float q = 0.f;
-    for (int i = threadIdx.x; i < n; i += 256) {
-        const float d = x[(int64_t)(i / cg) * Ctot + (i % cg)] - mean;
-        q += d * d;
+#pragma unroll
+    for (int i = 0; i < GN_VMAX; ++i) {
+        const int it = threadIdx.x + GN_THREADS * i;
+        if (it < items) {
+            v[i] = *(const float4*)(in + base + (int64_t)(it / q) * Ctot + 4 * (it % q));
+            s += v[i].x + v[i].y + v[i].z + v[i].w;
+        }
     }
-    const float rstd = rsqrtf(block_sum<256>(q, red) / n + eps);
+    const float n = (float)(P * cg);
+    const float mean = block_sum<GN_THREADS>(s, red) / n;
+    float sq = 0.f;
+#pragma unroll
+    for (int i = 0; i < GN_VMAX; ++i) {
+        const int it = threadIdx.x + GN_THREADS * i;
+        if (it < items) {
+            const float dx = v[i].x - mean, dy = v[i].y - mean, dz = v[i].z - mean, dw = v[i].w - mean;
+            sq += dx * dx + dy * dy + dz * dz + dw * dw;
+        }
+    }
+    const float rstd = rsqrtf(block_sum<GN_THREADS>(sq, red) / n + eps);
     const bool second = g1 && inst >= inst_per_set;
     const float* gg = (second ? g1 : g0) + grp * cg;
     const float* bb = (second ? b1 : b0) + grp * cg;
-    for (int i = threadIdx.x; i < n; i += 256) {
-        const int64_t off = (int64_t)inst * P * Ctot + (int64_t)(i / cg) * Ctot + grp * cg + (i % cg);
-        const float y = (in[off] - mean) * rstd * gg[i % cg] + bb[i % cg];
-        if (out_f32) out_f32[off] = y;
-        if (out_t) out_t[off] = from_f<T>(y);
+#pragma unroll
+    for (int i = 0; i < GN_VMAX; ++i) {
+        const int it = threadIdx.x + GN_THREADS * i;
+        if (it < items) {
+            const int c4 = 4 * (it % q);
+            const int64_t off = base + (int64_t)(it / q) * Ctot + c4;
+            float4 y;
+            y.x = (v[i].x - mean) * rstd * gg[c4 + 0] + bb[c4 + 0];
+            y.y = (v[i].y - mean) * rstd * gg[c4 + 1] + bb[c4 + 1];
+            y.z = (v[i].z - mean) * rstd * gg[c4 + 2] + bb[c4 + 2];
+            y.w = (v[i].w - mean) * rstd * gg[c4 + 3] + bb[c4 + 3];
+            if (out_f32) *(float4*)(out_f32 + off) = y;
+            if (out_t) {
+                if constexpr (sizeof(T) == 2) {
+                    uint2 pk;
+                    pk.x = (uint32_t)f2bf(y.x) | ((uint32_t)f2bf(y.y) << 16);
+                    pk.y = (uint32_t)f2bf(y.z) | ((uint32_t)f2bf(y.w) << 16);
+                    *(uint2*)(out_t + off) = pk;
+                } else {
+                    *(float4*)(out_t + off) = y;
+                }
+            }
+        }
     }
 }
 
@@ -181,14 +214,15 @@ extern "C" int mmt_groupnorm(const float* in, float* out_f32, void* out_t, const
                              const float* gamma1, const float* beta1, int n_inst, int inst_per_set, int P, int Ctot,
                              int groups, float eps, int dtype, void* stream) {
     if (!in || !gamma0 || !beta0 || n_inst <= 0 || P <= 0 || groups <= 0 || Ctot % groups) return MMT_EBADARG;
+    if ((Ctot / groups) % 4 || (int64_t)P * (Ctot / groups / 4) > (int64_t)GN_THREADS * GN_VMAX) return MMT_EBADARG;
     if (inst_per_set <= 0) inst_per_set = n_inst;
     dim3 grid(groups, n_inst);
     hipStream_t st = (hipStream_t)stream;
     if (dtype == MMT_BF16)
-        hipLaunchKernelGGL((groupnorm_kernel<bf16_t>), grid, dim3(256), 0, st, in, out_f32, (bf16_t*)out_t, gamma0,
+        hipLaunchKernelGGL((groupnorm_kernel<bf16_t>), grid, dim3(GN_THREADS), 0, st, in, out_f32, (bf16_t*)out_t, gamma0,
                            beta0, gamma1, beta1, inst_per_set, P, Ctot, groups, eps);
     else if (dtype == MMT_F32)
-        hipLaunchKernelGGL((groupnorm_kernel<float>), grid, dim3(256), 0, st, in, out_f32, (float*)out_t, gamma0,
+        hipLaunchKernelGGL((groupnorm_kernel<float>), grid, dim3(GN_THREADS), 0, st, in, out_f32, (float*)out_t, gamma0,
                            beta0, gamma1, beta1, inst_per_set, P, Ctot, groups, eps);
     else return MMT_EBADARG;
     return launch_status();

@@ -222,6 +222,7 @@ class MixFormerRGBTRuntime:
             "A3a": e(2, B * ns, hc // 4), "A3b": e(2, B * ns, hc // 8), "A3": e(2, B, ns, t=f32),
             "A4a": e(2, B * 4 * ns, hc // 8), "A4": e(2, B, 4 * ns, t=f32),
             "BOX": e(B, 4, t=f32), "XYXY": e(B, 4, t=f32), "ROIS": e(B, 5, t=f32),
+            "MAPS": e(2, B, d.fh * d.fh, t=f32),
         }
         pos = self.w["pos_sine"]  # [ns][512]
         le = self.w["level_embed"]
@@ -396,7 +397,7 @@ class MixFormerRGBTRuntime:
         plan.append((LIB.mmt_conv3x3_c1, (P(ws["A4a"]), P(W["a4c1.w"]), P(W["a4c1.b"]), P(ws["A4"]), 2, B, 2 * gs, h8,
                                           h8, cdt), "head_adjust4_1", None))
         plan.append((LIB.mmt_corner_softargmax, (P(X4), P(W["c5.w"]), P(W["c5.b"]), P(ws["A3"]), P(ws["A4"]),
-                                                 P(ws["BOX"]), P(ws["XYXY"]), P(ws["ROIS"]) if score else None,
+                                                 P(ws["MAPS"]), P(ws["BOX"]), P(ws["XYXY"]), P(ws["ROIS"]) if score else None,
                                                  float(gs), B, d.fh, h8, 4, cdt), "corner_softargmax", None))
         if score:
             self._plan_spm(plan, ws)

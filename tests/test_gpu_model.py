@@ -46,6 +46,12 @@ def test_model_matches_reference(variant, B, dname, tol):
     err = np.abs(box.cpu().numpy() - gold["pred_boxes"].reshape(B, 4)).max()
     print("%s B=%d %s box err %.3g" % (variant, B, dname, err))
     assert err <= tol, err
+    maps = rt.workspace(B)["MAPS"].cpu().numpy()  # [2][B][80*80] corner score maps
+    for g, nm in enumerate(("score_map_tl", "score_map_br")):
+        ref = gold[nm].reshape(B, -1)
+        merr = np.abs(maps[g] - ref).max() / max(1.0, np.abs(ref).max())
+        print("%s rel map err %.3g" % (nm, merr))
+        assert merr <= (1e-4 if dname == "f32" else 5e-2), merr
     if score:
         serr = np.abs(sc.cpu().numpy() - gold["pred_scores"].reshape(-1)).max()
         print("score err %.3g" % serr)
