@@ -6,8 +6,9 @@
 // The qkv Linear output is consumed in place ([seq][token][3][head][64], no permute) and the
 // result is written as [seq][token][head*64], i.e. exactly the proj GEMM's A operand.
 //
-// One workgroup = 2 waves = 64 queries of one (sequence, head); each wave owns 32 queries (two
-// 16-query MFMA tiles that share every K/V fragment read).  Keys stream through a double-buffered
+// One workgroup = 64 queries of one (sequence, head): 2 waves x 32 queries (two 16-query MFMA
+// tiles sharing every K/V fragment read) for large grids, or 4 waves x 16 queries when the grid
+// is small (batch-1 tracking) so that more SIMDs get a wave.  Keys stream through a double-buffered
 // LDS ring in 64-key tiles (register-staged: the next tile's global loads are in flight during
 // the current tile's matrix work).  Scores are computed transposed (S^T = K Q^T) so that each
 // lane owns one query column: the online-softmax max/sum/rescale need only two cross-lane
@@ -19,7 +20,7 @@
 
 namespace {
 
-constexpr int D = 64, KB = 64, NTH = 128;
+constexpr int D = 64, KB = 64;
 
 template <typename T>
 struct AttnCfg {
@@ -29,11 +30,13 @@ struct AttnCfg {
     static constexpr int VROW = BF ? 160 : 272;          // padded V row (bytes)
 };
 
-template <typename T>
-__global__ __launch_bounds__(NTH) void mam_attention_kernel(const mmt_attn_params p) {
+// QT = 16-query MFMA tiles per wave (1: 4 waves x 16 queries, for small grids; 2: 2 waves x 32).
+template <typename T, int QT>
+__global__ __launch_bounds__(256 / QT) void mam_attention_kernel(const mmt_attn_params p) {
+    constexpr int NTH = 256 / QT;
     using Cfg = AttnCfg<T>;
     constexpr int KCH = Cfg::KCH, QCH = Cfg::QCH, VROW = Cfg::VROW;
-    __shared__ uint4 kl[2][KB * KCH];
+    __shared__ u32x4 kl[2][KB * KCH];
     __shared__ __attribute__((aligned(16))) char vl[2][KB * VROW];
 
     const int qb = blockIdx.x, h = blockIdx.y, s = blockIdx.z;
@@ -52,17 +55,13 @@ __global__ __launch_bounds__(NTH) void mam_attention_kernel(const mmt_attn_param
     const int l16 = lane & 15, lg = lane >> 4;
 
     // ---- Q fragments (B operand of S^T = K Q^T)
-    uint4 qf[2][QCH];
+    u32x4 qf[QT][QCH];
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-        const int q = q0 + 32 * w + 16 * qt + l16;
-        const T* qp = qkv + ((int64_t)s * ntok + q) * rs + h * D;
+    for (int qt = 0; qt < QT; ++qt) {
+        const int q = q0 + 16 * QT * w + 16 * qt + l16;
+        const T* qp = qkv + ((int64_t)s * ntok + min(q, qend - 1)) * rs + h * D;  // clamped, never stored
 #pragma unroll
-        for (int t = 0; t < QCH; ++t) {
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (q < qend) v = *(const uint4*)(qp + (4 * t + lg) * (16 / (int)sizeof(T)));
-            qf[qt][t] = v;
-        }
+        for (int t = 0; t < QCH; ++t) qf[qt][t] = *(const u32x4*)(qp + (4 * t + lg) * (16 / (int)sizeof(T)));
     }
 
     // ---- K/V staging
@@ -77,20 +76,17 @@ __global__ __launch_bounds__(NTH) void mam_attention_kernel(const mmt_attn_param
         }
         return qkv + ((int64_t)seq * ntok + row) * rs + h * D;
     };
-    uint4 rk[PER], rv[PER];
+    // K/V loads are unconditional (rows past Lk re-read key Lk-1 and are masked in the scores;
+    // their V rows are multiplied by p = 0): a guarded load would make hipcc drain vmcnt(0).
+    u32x4 rk[PER], rv[PER];
     auto load_kv = [&](int kt) {
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const int row = (tid + NTH * i) / KCH;
-            const int kk = kt * KB + row;
-            uint4 a = make_uint4(0, 0, 0, 0), b = a;
-            if (kk < Lk) {
-                const T* kp = key_ptr(kk) + ch * (16 / (int)sizeof(T));
-                a = *(const uint4*)(kp + C);
-                b = *(const uint4*)(kp + 2 * C);
-            }
-            rk[i] = a;
-            rv[i] = b;
+            const int kk = min(kt * KB + row, Lk - 1);
+            const T* kp = key_ptr(kk) + ch * (16 / (int)sizeof(T));
+            rk[i] = *(const u32x4*)(kp + C);
+            rv[i] = *(const u32x4*)(kp + 2 * C);
         }
     };
     auto store_kv = [&](int buf) {
@@ -98,35 +94,42 @@ __global__ __launch_bounds__(NTH) void mam_attention_kernel(const mmt_attn_param
         for (int i = 0; i < PER; ++i) {
             const int row = (tid + NTH * i) / KCH;
             kl[buf][row * KCH + (ch ^ (row & 7))] = rk[i];
-            *(uint4*)(vl[buf] + row * VROW + ch * 16) = rv[i];
+            *(u32x4*)(vl[buf] + row * VROW + ch * 16) = rv[i];
         }
     };
 
     const float cexp = p.scale * 1.4426950408889634f;
-    float m_run[2] = {-1e30f, -1e30f}, l_run[2] = {0.f, 0.f};
-    f32x4 o[4][2];
+    float m_run[QT], l_run[QT];
+    f32x4 o[4][QT];
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) o[dt][0] = o[dt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int qt = 0; qt < QT; ++qt) {
+        m_run[qt] = -1e30f;
+        l_run[qt] = 0.f;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[dt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
 
     const int nkt = (Lk + KB - 1) / KB;
     load_kv(0);
     store_kv(0);
-    __syncthreads();
+    lds_barrier();
     for (int kt = 0; kt < nkt; ++kt) {
         const int cur = kt & 1;
         if (kt + 1 < nkt) load_kv(kt + 1);
 
         // S^T tiles: sacc[kt16][qt], lane: query l16, keys 16*kt16 + 4*lg + r
-        f32x4 sacc[4][2];
+        f32x4 sacc[4][QT];
 #pragma unroll
-        for (int a = 0; a < 4; ++a) sacc[a][0] = sacc[a][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) sacc[a][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kt16 = 0; kt16 < 4; ++kt16) {
 #pragma unroll
             for (int t = 0; t < QCH; ++t) {
-                const uint4 kf = kl[cur][(kt16 * 16 + l16) * KCH + ((4 * t + lg) ^ (l16 & 7))];
+                const u32x4 kf = kl[cur][(kt16 * 16 + l16) * KCH + ((4 * t + lg) ^ (l16 & 7))];
 #pragma unroll
-                for (int qt = 0; qt < 2; ++qt) {
+                for (int qt = 0; qt < QT; ++qt) {
                     if constexpr (Cfg::BF) {
                         sacc[kt16][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                             __builtin_bit_cast(bf16x8, kf), __builtin_bit_cast(bf16x8, qf[qt][t]), sacc[kt16][qt], 0, 0, 0);
@@ -145,11 +148,13 @@ __global__ __launch_bounds__(NTH) void mam_attention_kernel(const mmt_attn_param
             for (int kt16 = 0; kt16 < 4; ++kt16)
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    if (kt * KB + kt16 * 16 + 4 * lg + r >= Lk) sacc[kt16][0][r] = sacc[kt16][1][r] = -1e30f;
+                    if (kt * KB + kt16 * 16 + 4 * lg + r >= Lk)
+#pragma unroll
+                        for (int qt = 0; qt < QT; ++qt) sacc[kt16][qt][r] = -1e30f;
         }
         // online softmax (per query column)
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) {
+        for (int qt = 0; qt < QT; ++qt) {
             float mx = -1e30f;
 #pragma unroll
             for (int kt16 = 0; kt16 < 4; ++kt16)
@@ -178,9 +183,9 @@ __global__ __launch_bounds__(NTH) void mam_attention_kernel(const mmt_attn_param
         if constexpr (Cfg::BF) {
 #pragma unroll
             for (int kk = 0; kk < 2; ++kk) {
-                bf16x8 pf[2];
+                bf16x8 pf[QT];
 #pragma unroll
-                for (int qt = 0; qt < 2; ++qt) {
+                for (int qt = 0; qt < QT; ++qt) {
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         pf[qt][j] = (__bf16)sacc[2 * kk][qt][j];
@@ -198,7 +203,7 @@ __global__ __launch_bounds__(NTH) void mam_attention_kernel(const mmt_attn_param
                     const uint2 ua = __builtin_bit_cast(uint2, va), ub = __builtin_bit_cast(uint2, vb);
                     const bf16x8 vf = __builtin_bit_cast(bf16x8, make_uint4(ua.x, ua.y, ub.x, ub.y));
 #pragma unroll
-                    for (int qt = 0; qt < 2; ++qt)
+                    for (int qt = 0; qt < QT; ++qt)
                         o[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qt], o[dt][qt], 0, 0, 0);
                 }
             }
@@ -213,24 +218,24 @@ __global__ __launch_bounds__(NTH) void mam_attention_kernel(const mmt_attn_param
                     for (int dt = 0; dt < 4; ++dt) {
                         const float va = vf[key * (VROW / 4) + dt * 16 + l16];
 #pragma unroll
-                        for (int qt = 0; qt < 2; ++qt)
+                        for (int qt = 0; qt < QT; ++qt)
                             o[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x4f32(va, sacc[kt16][qt][r], o[dt][qt], 0, 0, 0);
                     }
                 }
         }
         if (kt + 1 < nkt) store_kv(cur ^ 1);
-        __syncthreads();
+        lds_barrier();
     }
 
     // ---- normalise and store: lane holds O[q = l16][d = dt*16 + 4*lg + r]
     T* out = (T*)p.out;
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
+    for (int qt = 0; qt < QT; ++qt) {
         float l = l_run[qt];
         l += __shfl_xor(l, 16, 64);
         l += __shfl_xor(l, 32, 64);
         const float inv = 1.f / l;
-        const int q = q0 + 32 * w + 16 * qt + l16;
+        const int q = q0 + 16 * QT * w + 16 * qt + l16;
         if (q >= qend) continue;
         T* op = out + ((int64_t)s * ntok + q) * C + h * D;
 #pragma unroll
@@ -254,7 +259,9 @@ int launch_attn(const mmt_attn_params& p, hipStream_t st) {
     if (((uintptr_t)p.qkv | (uintptr_t)p.out) & 15) return MMT_EBADARG;
     const int nqb = (p.n_t + 63) / 64 + (p.ntok - p.n_t + 63) / 64;
     dim3 grid(nqb, p.H, p.S);
-    hipLaunchKernelGGL((mam_attention_kernel<T>), grid, dim3(NTH), 0, st, p);
+    // small grids (batch-1 tracking): 4 waves x 16 queries per workgroup to occupy more SIMDs
+    if ((int64_t)nqb * p.H * p.S < 1024) hipLaunchKernelGGL((mam_attention_kernel<T, 1>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((mam_attention_kernel<T, 2>), grid, dim3(128), 0, st, p);
     return launch_status();
 }
 

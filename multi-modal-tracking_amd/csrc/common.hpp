@@ -9,6 +9,7 @@ typedef uint16_t bf16_t;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 #define MMT_DEV __device__ __forceinline__
 
@@ -60,6 +61,12 @@ MMT_DEV float block_max(float v, float* red) {
     for (int i = 0; i < NT / 64; ++i) t = fmaxf(t, red[i]);
     return t;
 }
+
+// Workgroup barrier for LDS hand-offs that leaves global loads in flight: waits only for this
+// wave's LDS operations (lgkmcnt), unlike __syncthreads(), whose fence makes hipcc drain vmcnt(0)
+// and so serialises any register prefetch ring.  The "memory" clobber keeps LDS accesses on
+// their side of the barrier.
+MMT_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 static inline int hip_status(hipError_t e) { return e == hipSuccess ? 0 : -(int)e; }
 static inline int launch_status() { return hip_status(hipGetLastError()); }

@@ -19,21 +19,32 @@
 
 namespace {
 
-constexpr int NCH = 8, NT = 256, DEPTH = 3;
+constexpr int NCH = 8, DEPTH = 3;
 
-template <typename T, bool CONV, int BM, int BN>
-__global__ __launch_bounds__(NT) void gemm_kernel(const mmt_gemm_params p) {
+// KS = wave groups splitting the K-steps inside the workgroup (4 waves each): group kg takes
+// K-steps kg, kg+KS, ...; the partial accumulators are summed through LDS at the end.  KS = 2
+// doubles the waves per SIMD for the small-M (batch-1) GEMMs without any global reduction.
+template <typename T, bool CONV, int BM, int BN, int KS>
+__global__ __launch_bounds__(256 * KS) void gemm_kernel(const mmt_gemm_params p) {
     constexpr int EPC = 16 / (int)sizeof(T);
     constexpr int KT = NCH * EPC;
     constexpr int AR = BM / 32, BR = BN / 32;  // staged 16-B chunks per thread per K-step
     constexpr int WM = BM / 2, WN = BN / 2, MT = WM / 16, NTL = WN / 16;
-    __shared__ uint4 lds[2][(BM + BN) * NCH];
+    __shared__ u32x4 lds[2][KS][(BM + BN) * NCH];
 
-    const int g = blockIdx.z;
+    // XCD-aware bijective remap (workgroups are dealt round-robin over the 8 XCDs): give each XCD
+    // a contiguous run of (tile, group) ids, tm fastest, so the W column-slices and A rows a run
+    // re-reads stay in that XCD's L2.  Placement only changes speed, never results.
+    const int nwg = gridDim.x * gridDim.z;
+    const int orig = blockIdx.x + gridDim.x * blockIdx.z;
+    const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+    const int g = lin / gridDim.x, tile = lin - g * gridDim.x;
     const int tiles_m = (p.M + BM - 1) / BM;
-    const int tm = blockIdx.x % tiles_m, tn = blockIdx.x / tiles_m;
+    const int tm = tile % tiles_m, tn = tile / tiles_m;
     const int m0 = tm * BM, n0 = tn * BN;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int lane = threadIdx.x & 63, kg = threadIdx.x >> 8;
+    const int tid = threadIdx.x & 255, wid = tid >> 6;  // thread / wave within the k-group
     const int wr = wid >> 1, wc = wid & 1;
     const int l16 = lane & 15, lg = lane >> 4;
     const int c = tid & 7;
@@ -49,8 +60,9 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const mmt_gemm_params p) {
     const int ch = p.conv_h, cup = p.conv_up > 0 ? p.conv_up : 1, hi = CONV ? p.conv_h / cup : 0;
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
-        const int m = m0 + (tid >> 3) + 32 * i;
-        aval[i] = m < M;
+        const int mr = m0 + (tid >> 3) + 32 * i;
+        aval[i] = mr < M;
+        const int m = aval[i] ? mr : M - 1;  // clamped: always a valid address
         if (!CONV) {
             const int64_t seg = m / p.a_seg_rows;
             aoff[i] = (seg % p.a_segs_a) * p.a_stride_a + (seg / p.a_segs_a) * p.a_stride_b + (m % p.a_seg_rows) * p.lda;
@@ -67,58 +79,61 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const mmt_gemm_params p) {
     for (int i = 0; i < BR; ++i) {
         const int n = n0 + (tid >> 3) + 32 * i;
         bval[i] = n < N;
-        boff[i] = (int64_t)n * K;
+        boff[i] = (int64_t)(bval[i] ? n : N - 1) * K;
     }
 
-    struct Stage {
-        uint4 a[AR], b[BR];
-    };
-    auto load_tile = [&](int kt, Stage& s) {
-        const int k = kt * KT + c * EPC;
-        const bool kin = k < K;
-        int iy_d = 0, ix_d = 0, ci = k;
-        if (CONV && p.conv_k3) {
-            const int tap = k / p.conv_cin;
-            ci = k - tap * p.conv_cin;
-            iy_d = tap / 3 - 1;
-            ix_d = tap % 3 - 1;
-        }
-#pragma unroll
-        for (int i = 0; i < AR; ++i) {
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (aval[i] && kin) {
-                if (!CONV) {
-                    const T* src = (p.k_split > 0 && k >= p.k_split) ? A1 + aoff[i] + (k - p.k_split) : A0 + aoff[i] + k;
-                    v = *(const uint4*)src;
-                } else {
-                    const int iy = ay[i] + iy_d, ix = ax[i] + ix_d;
-                    if (iy >= 0 && ix >= 0 && iy < ch && ix < ch) {
-                        const int64_t pix = aoff[i] + (int64_t)(iy / cup) * hi + (ix / cup);
-                        v = *(const uint4*)(A0 + pix * p.lda + ci);
-                    }
-                }
-            }
-            s.a[i] = v;
-        }
-#pragma unroll
-        for (int i = 0; i < BR; ++i) {
-            uint4 w = make_uint4(0, 0, 0, 0);
-            if (bval[i] && kin) w = *(const uint4*)(W + boff[i] + k);
-            s.b[i] = w;
-        }
-    };
-    auto store_tile = [&](int buf, const Stage& s) {
-#pragma unroll
-        for (int i = 0; i < AR; ++i) {
-            const int row = (tid >> 3) + 32 * i;
-            lds[buf][row * NCH + (c ^ (row & 7))] = s.a[i];
-        }
-#pragma unroll
-        for (int i = 0; i < BR; ++i) {
-            const int row = (tid >> 3) + 32 * i;
-            lds[buf][(BM + row) * NCH + (c ^ (row & 7))] = s.b[i];
-        }
-    };
+    // Loads are never predicated: out-of-range rows / K-columns / padding taps read a clamped,
+    // in-bounds address and are zeroed when written to LDS.  (A guarded load becomes an
+    // s_and_saveexec branch and hipcc then drains vmcnt(0) before every barrier, which serialises
+    // the whole prefetch ring.)  The ring's three stages are plain named register arrays: a stage
+    // struct passed by reference is demoted to scratch by hipcc.
+#define MMT_LOAD_TILE(KTV, SA, SB, SOK)                                                                  \
+    {                                                                                                    \
+        const int kraw_ = (KTV) * KT + c * EPC;                                                          \
+        const bool kin_ = kraw_ < K;                                                                     \
+        const int k_ = kin_ ? kraw_ : 0;                                                                 \
+        int iyd_ = 0, ixd_ = 0, ci_ = k_;                                                                \
+        if (CONV && p.conv_k3) {                                                                         \
+            const int tap_ = k_ / p.conv_cin;                                                            \
+            ci_ = k_ - tap_ * p.conv_cin;                                                                \
+            iyd_ = tap_ / 3 - 1;                                                                         \
+            ixd_ = tap_ % 3 - 1;                                                                         \
+        }                                                                                                \
+        uint32_t ok_ = 0;                                                                                \
+        _Pragma("unroll") for (int i = 0; i < AR; ++i) {                                                 \
+            bool v_ = aval[i] && kin_;                                                                   \
+            const T* src_;                                                                               \
+            if (!CONV) {                                                                                 \
+                const bool hp_ = p.k_split > 0 && k_ >= p.k_split;                                      \
+                src_ = (hp_ ? A1 : A0) + aoff[i] + (hp_ ? k_ - p.k_split : k_);                          \
+            } else {                                                                                     \
+                int iy_ = ay[i] + iyd_, ix_ = ax[i] + ixd_;                                              \
+                v_ = v_ && iy_ >= 0 && ix_ >= 0 && iy_ < ch && ix_ < ch;                                 \
+                iy_ = min(max(iy_, 0), ch - 1);                                                          \
+                ix_ = min(max(ix_, 0), ch - 1);                                                          \
+                src_ = A0 + (aoff[i] + (int64_t)(iy_ / cup) * hi + (ix_ / cup)) * p.lda + ci_;            \
+            }                                                                                            \
+            SA[i] = *(const u32x4*)src_;                                                                 \
+            ok_ |= (uint32_t)v_ << i;                                                                    \
+        }                                                                                                \
+        _Pragma("unroll") for (int i = 0; i < BR; ++i) {                                                 \
+            SB[i] = *(const u32x4*)(W + boff[i] + k_);                                                   \
+            ok_ |= (uint32_t)(bval[i] && kin_) << (AR + i);                                              \
+        }                                                                                                \
+        SOK = ok_;                                                                                       \
+    }
+#define MMT_STORE_TILE(BUF, SA, SB, SOK)                                                                 \
+    {                                                                                                    \
+        const u32x4 z_ = {0u, 0u, 0u, 0u};                                                               \
+        _Pragma("unroll") for (int i = 0; i < AR; ++i) {                                                 \
+            const int row_ = (tid >> 3) + 32 * i;                                                        \
+            lds[BUF][kg][row_ * NCH + (c ^ (row_ & 7))] = (((SOK) >> i) & 1) ? SA[i] : z_;               \
+        }                                                                                                \
+        _Pragma("unroll") for (int i = 0; i < BR; ++i) {                                                 \
+            const int row_ = (tid >> 3) + 32 * i;                                                        \
+            lds[BUF][kg][(BM + row_) * NCH + (c ^ (row_ & 7))] = (((SOK) >> (AR + i)) & 1) ? SB[i] : z_; \
+        }                                                                                                \
+    }
 
     f32x4 acc[MT][NTL];
 #pragma unroll
@@ -127,11 +142,11 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const mmt_gemm_params p) {
         for (int j = 0; j < NTL; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     auto compute = [&](int buf) {
-        const uint4* L = lds[buf];
+        const u32x4* L = lds[buf][kg];
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
             const int sw = (4 * t + lg) ^ (lane & 7);
-            uint4 af[MT], bfr[NTL];
+            u32x4 af[MT], bfr[NTL];
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt) af[mt] = L[(wr * WM + mt * 16 + l16) * NCH + sw];
 #pragma unroll
@@ -155,22 +170,54 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const mmt_gemm_params p) {
     };
 
     // ---- K loop: ring of DEPTH register stages, double-buffered LDS, one barrier per K-step
+    // Three named stages; the tail issues clamped re-loads of the last K-step instead of branching
+    // around the loads.
+    // Step s covers K-steps s*KS .. s*KS+KS-1 (one per k-group); K-steps past the end load a
+    // clamped address and are masked to zero.
     const int nk = (K + KT - 1) / KT;
-    Stage st[DEPTH];
+    const int ns = (nk + KS - 1) / KS;
+    static_assert(DEPTH == 3, "ring is written out for three stages");
+    u32x4 sa0[AR], sb0[BR], sa1[AR], sb1[BR], sa2[AR], sb2[BR];
+    uint32_t ok0, ok1, ok2;
+    MMT_LOAD_TILE(kg, sa0, sb0, ok0);
+    MMT_LOAD_TILE(min(1, ns - 1) * KS + kg, sa1, sb1, ok1);
+    MMT_LOAD_TILE(min(2, ns - 1) * KS + kg, sa2, sb2, ok2);
+#define MMT_STEP(SV, SA, SB, SOK)                                        \
+    {                                                                    \
+        MMT_STORE_TILE((SV) & 1, SA, SB, SOK);                           \
+        lds_barrier();                                                   \
+        MMT_LOAD_TILE(min((SV) + DEPTH, ns - 1) * KS + kg, SA, SB, SOK); \
+        compute((SV) & 1);                                               \
+    }
+    int st = 0;
+    for (; st + DEPTH <= ns; st += DEPTH) {
+        MMT_STEP(st, sa0, sb0, ok0);
+        MMT_STEP(st + 1, sa1, sb1, ok1);
+        MMT_STEP(st + 2, sa2, sb2, ok2);
+    }
+    if (st < ns) MMT_STEP(st, sa0, sb0, ok0);
+    if (st + 1 < ns) MMT_STEP(st + 1, sa1, sb1, ok1);
+#undef MMT_STEP
+#undef MMT_LOAD_TILE
+#undef MMT_STORE_TILE
+
+    if constexpr (KS > 1) {  // sum the k-groups' partial tiles through LDS
+        static_assert(KS == 2, "k-group reduction written for two groups");
+        static_assert((size_t)4 * MT * NTL * 64 * 16 <= sizeof(lds), "reduction buffer");
+        __syncthreads();
+        f32x4* red = (f32x4*)&lds[0][0][0];
+        if (kg == 1) {
 #pragma unroll
-    for (int j = 0; j < DEPTH; ++j)
-        if (j < nk) load_tile(j, st[j]);
-    for (int k0 = 0; k0 < nk; k0 += DEPTH) {
+            for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int j = 0; j < DEPTH; ++j) {
-            const int kt = k0 + j;
-            if (kt < nk) {
-                store_tile(kt & 1, st[j]);
-                __syncthreads();
-                if (kt + DEPTH < nk) load_tile(kt + DEPTH, st[j]);
-                compute(kt & 1);
-            }
+                for (int nt = 0; nt < NTL; ++nt) red[((wid * MT + mt) * NTL + nt) * 64 + lane] = acc[mt][nt];
         }
+        __syncthreads();
+        if (kg == 1) return;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < NTL; ++nt) acc[mt][nt] += red[((wid * MT + mt) * NTL + nt) * 64 + lane];
     }
 
     // ---- epilogue
@@ -219,13 +266,18 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const mmt_gemm_params p) {
 template <typename T, bool CONV>
 void launch_tiles(const mmt_gemm_params& p, hipStream_t st) {
     auto blocks = [&](int bm, int bn) { return (int64_t)((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn) * p.groups; };
-    // Large problems: 128x128 (best MFMA:LDS ratio).  Otherwise 64x64 to put work on every CU.
+    const int nk64 = (p.K + 16 / (int)sizeof(T) * NCH - 1) / (16 / (int)sizeof(T) * NCH);
+    // Large problems: 128x128 (best MFMA:LDS ratio).  Otherwise 64x64 to put work on every CU,
+    // with two k-groups per tile when there are enough K-steps to share.
     if (blocks(128, 128) >= 512) {
         dim3 grid((unsigned)(blocks(128, 128) / p.groups), 1, p.groups);
-        hipLaunchKernelGGL((gemm_kernel<T, CONV, 128, 128>), grid, dim3(NT), 0, st, p);
+        hipLaunchKernelGGL((gemm_kernel<T, CONV, 128, 128, 1>), grid, dim3(256), 0, st, p);
+    } else if (nk64 >= 8) {
+        dim3 grid((unsigned)(blocks(64, 64) / p.groups), 1, p.groups);
+        hipLaunchKernelGGL((gemm_kernel<T, CONV, 64, 64, 2>), grid, dim3(512), 0, st, p);
     } else {
         dim3 grid((unsigned)(blocks(64, 64) / p.groups), 1, p.groups);
-        hipLaunchKernelGGL((gemm_kernel<T, CONV, 64, 64>), grid, dim3(NT), 0, st, p);
+        hipLaunchKernelGGL((gemm_kernel<T, CONV, 64, 64, 1>), grid, dim3(256), 0, st, p);
     }
 }
 

@@ -474,6 +474,34 @@ class MixFormerRGBTRuntime:
             self.run_plan(ws["plan_score"] if score else ws["plan"])
         return ws["BOX"], (ws["SC"].view(-1) if score else None)
 
+    def plan_for_inputs(self, template, online_template, search, run_score_head=False):
+        """The plan of batch B with its patch staging reading the given device tensors directly
+        (zero-copy: for frames already resident in HBM, e.g. written there by the preprocessing)."""
+        B = template[0].shape[0]
+        ws = self.workspace(B)
+        score = bool(run_score_head) and self.variant == "asym_online"
+        base = ws["plan_score"] if score else ws["plan"]
+        fn, args, name, keep = base[0]
+        assert name == "patch_im2col"
+        srcs = list(template) + list(online_template) + list(search)
+        for src, dst in zip(srcs, ws["in_t"] + ws["in_o"] + ws["in_s"]):
+            if src.shape != dst.shape or src.dtype != torch.float32 or not src.is_contiguous() or src.device != dst.device:
+                raise ValueError("zero-copy inputs must be contiguous fp32 %s tensors on %s" % (tuple(dst.shape), dst.device))
+        new_args = tuple(_ptr(x) for x in srcs) + args[6:]
+        return [(fn, new_args, name, srcs)] + base[1:]
+
+    def capture_plan(self, plan):
+        """Record an arbitrary plan as one hipGraph (returned; caller keeps the inputs alive)."""
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self.run_plan(plan)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.run_plan(plan)
+        return g
+
     def capture(self, B, score=False):
         """Record the plan of batch B as one hipGraph (inputs are the workspace's static buffers)."""
         ws = self.workspace(B)

@@ -81,3 +81,16 @@ def test_batch_rows_independent():
     b1, _ = rt.forward([x[1:2] for x in t], [x[1:2] for x in o], [x[1:2] for x in s])
     torch.cuda.synchronize()
     assert (b2[1] - b1[0]).abs().max().item() < 1e-5
+
+
+def test_zero_copy_plan_matches_copy_path():
+    """Graph of a plan whose patch staging reads resident frames in place == the copying forward."""
+    rt = _runtime("rgbt", torch.bfloat16)
+    t, o, s = _inputs(1)
+    b0, _ = rt.forward(t, o, s)
+    b0 = b0.clone()
+    g = rt.capture_plan(rt.plan_for_inputs(t, o, s))
+    rt.workspace(1)["BOX"].zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(b0, rt.workspace(1)["BOX"])
