@@ -120,6 +120,7 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--dump-plan", default=None, help="write the plan's launch names (JSON) to this path")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -174,6 +175,9 @@ def main():
 
     ws = rt.workspace(B)
     plan = ws["plan_score"] if score else ws["plan"]
+    if args.dump_plan and rank == 0:
+        with open(args.dump_plan, "w") as f:
+            json.dump([e[2] for e in plan], f)
     times = kernel_profile(rt, plan)
     dom, mam, dev_ms, by = roofline(rt, plan, times, args.dtype)
 

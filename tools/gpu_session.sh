@@ -29,8 +29,11 @@ if [ $rc -ne 0 ]; then exit $rc; fi
 export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o trace --output-format csv -- \
-    python3 "$ROOT/bench.py" --no-cpu-baseline --steps 100 --warmup 10 "$@" > "$OUT/bench_prof.log" 2>&1
+    python3 "$ROOT/bench.py" --no-cpu-baseline --steps 100 --warmup 10 --dump-plan "$OUT/plan_names.json" "$@" \
+    > "$OUT/bench_prof.log" 2>&1
 rc=$?
 echo "rocprof rc=$rc"
+python3 "$ROOT/tools/trace_breakdown.py" "$OUT/prof/trace_kernel_trace.csv" "$OUT/plan_names.json" > "$OUT/breakdown.txt" 2>&1
+head -40 "$OUT/breakdown.txt"
 find "$OUT/prof" -name "*stats*" | head
 exit $rc
