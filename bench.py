@@ -120,6 +120,7 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--gemm-impl", type=int, default=0, help="mmt_gemm_params.impl for every GEMM (A/B)")
     ap.add_argument("--dump-plan", default=None, help="write the plan's launch names (JSON) to this path")
     args = ap.parse_args()
 
@@ -137,6 +138,7 @@ def main():
     keys = state_dict_keys(args.variant)
     sd = {k: torch.from_numpy(v) for k, v in synthetic.synth_state_dict(keys).items()}
     rt = MixFormerRGBTRuntime(sd, args.variant, dtype=dtype)
+    rt.gemm_impl = args.gemm_impl
     B = args.batch
     score = args.variant == "asym_online"
     pool = []

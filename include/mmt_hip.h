@@ -76,7 +76,10 @@ typedef struct {
     int32_t r_mode, r_p0, r_p1;
     int32_t conv_h, conv_up, conv_cin, conv_k3;
     int32_t groups;
-    int32_t r_t; /* 1: R is stored in `dtype` instead of fp32 */
+    int32_t r_t;  /* 1: R is stored in `dtype` instead of fp32 */
+    int32_t impl; /* kernel choice, results identical up to fp32 summation order: 0 auto;
+                     -1 register-staged 64/128 tiles; 1 / 2 / 3 LDS-DMA 128x128 / 128x64 (K split
+                     over 2 wave groups) / 64x64 (K split 2), bf16 with K % 64 == 0 only */
 } mmt_gemm_params;
 
 int mmt_gemm(const mmt_gemm_params* p, int dtype, void* stream);

@@ -10,6 +10,8 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
 #define MMT_DEV __device__ __forceinline__
 
@@ -23,7 +25,20 @@ template <typename T> MMT_DEV T from_f(float v);
 template <> MMT_DEV float from_f<float>(float v) { return v; }
 template <> MMT_DEV bf16_t from_f<bf16_t>(float v) { return f2bf(v); }
 
-MMT_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f)); }
+// Two floats -> packed bf16 pair (RNE), lo in bits 0-15.  Whole-vector conversion: a per-element
+// bit_cast between 16-bit types has been seen to miscompile.
+MMT_DEV uint32_t pack_bf16x2(float lo, float hi) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{lo, hi}, bf16x2));
+}
+
+// GELU(x) = x/2 (1 + erf(x/sqrt2)) with a branch-free erf (Abramowitz-Stegun 7.1.26, |error| <=
+// 1.5e-7): libm erff branches on |x|, which in a 64-value epilogue means 64 divergent regions.
+MMT_DEV float erf_fast(float x) {
+    const float a = fabsf(x), t = 1.0f / (1.0f + 0.3275911f * a);
+    const float y = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+    return copysignf(1.0f - y * __expf(-a * a), x);
+}
+MMT_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752440f)); }
 
 MMT_DEV float wave_sum(float v) {
 #pragma unroll
@@ -66,7 +81,14 @@ MMT_DEV float block_max(float v, float* red) {
 // wave's LDS operations (lgkmcnt), unlike __syncthreads(), whose fence makes hipcc drain vmcnt(0)
 // and so serialises any register prefetch ring.  The "memory" clobber keeps LDS accesses on
 // their side of the barrier.
-MMT_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// The wait is the s_waitcnt builtin (gfx9 encoding: lgkmcnt 0, vmcnt / expcnt at their maximum)
+// rather than inline asm so that hipcc's wait-count tracking knows the LDS reads are retired (it
+// otherwise re-waits for them later, and with >15 newer LDS reads outstanding it can only
+// express that as lgkmcnt(0)).
+MMT_DEV void lds_barrier() {
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    asm volatile("s_barrier" ::: "memory");
+}
 
 static inline int hip_status(hipError_t e) { return e == hipSuccess ? 0 : -(int)e; }
 static inline int launch_status() { return hip_status(hipGetLastError()); }

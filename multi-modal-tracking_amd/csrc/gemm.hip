@@ -16,6 +16,7 @@
 // Epilogue: bias, GELU(erf)/ReLU, residual with a row map (identity, modulo, or down-sampled conv
 // map; fp32 or compute dtype), optional second output (C2 = C + R).
 #include "common.hpp"
+#include "gemm_internal.hpp"
 
 namespace {
 
@@ -285,6 +286,7 @@ template <typename T>
 int launch_gemm(const mmt_gemm_params& p, hipStream_t st) {
     const int EPC = 16 / (int)sizeof(T);
     if (p.M <= 0 || p.N <= 0 || p.K <= 0 || p.groups < 1 || p.groups > MMT_MAX_GROUPS) return MMT_EBADARG;
+    if (p.impl < -1 || p.impl > 3) return MMT_EBADARG;
     if (p.K % EPC || p.lda % EPC) return MMT_EBADARG;
     if (p.conv_h > 0) {
         if (p.conv_cin % EPC || p.conv_up < 1 || p.conv_h % p.conv_up) return MMT_EBADARG;
@@ -302,6 +304,7 @@ int launch_gemm(const mmt_gemm_params& p, hipStream_t st) {
         if (p.k_split > 0 && p.conv_h == 0 && (!p.a1[g] || ((uintptr_t)p.a1[g] & 15))) return MMT_EBADARG;
         if (p.c2[g] && !p.r[g]) return MMT_EBADARG;
     }
+    if (sizeof(T) == 2 && mmt_gemm_glds_bf16(p, st, p.impl) == 0) return launch_status();
     if (p.conv_h > 0) launch_tiles<T, true>(p, st);
     else launch_tiles<T, false>(p, st);
     return launch_status();

@@ -9,7 +9,9 @@ import os
 
 import torch  # noqa: F401  (loads the HIP runtime the kernels must share)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmmt_hip.so")
+# MMT_HIP_LIB may name another build of the same library (A/B or ablation builds of tools/).
+LIB_PATH = os.environ.get("MMT_HIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib",
+                                                         "libmmt_hip.so")
 
 MMT_F32, MMT_BF16, MMT_F64 = 0, 1, 2
 MAX_GROUPS = 2
@@ -30,7 +32,7 @@ class GemmParams(ctypes.Structure):
         ("act", i32), ("c_f32", i32),
         ("r_mode", i32), ("r_p0", i32), ("r_p1", i32),
         ("conv_h", i32), ("conv_up", i32), ("conv_cin", i32), ("conv_k3", i32),
-        ("groups", i32), ("r_t", i32),
+        ("groups", i32), ("r_t", i32), ("impl", i32),
     ]
 
 

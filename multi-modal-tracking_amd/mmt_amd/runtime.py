@@ -64,6 +64,8 @@ class Dims:
 class MixFormerRGBTRuntime:
     """Compiled forward of one of the four hot-path variants on the current CUDA (HIP) device."""
 
+    gemm_impl = 0  # mmt_gemm_params.impl of every plan GEMM (0 = library's choice; A/B knob)
+
     def __init__(self, state_dict, variant, dtype=torch.bfloat16, device="cuda"):
         if variant not in VARIANTS:
             raise ValueError("unknown variant %r" % (variant,))
@@ -263,6 +265,7 @@ class MixFormerRGBTRuntime:
             p.conv_h, p.conv_up, p.conv_cin, p.conv_k3 = conv
         p.groups = G
         p.r_t = r_t
+        p.impl = self.gemm_impl
         plan.append((LIB.mmt_gemm, (ctypes_byref(p), self.cdt if dtype is None else dtype), name, p))
 
     def _build_plan(self, ws, score):

@@ -43,6 +43,7 @@ def _gemm(a, w, c, M, N, K, lda, ldc, dtype, **kw):
         p.conv_h, p.conv_up, p.conv_cin, p.conv_k3 = kw["conv"]
     p.groups = G
     p.r_t = kw.get("r_t", 0)
+    p.impl = kw.get("impl", 0)
     L.check(L.LIB.mmt_gemm(p, L.MMT_BF16 if dtype == torch.bfloat16 else L.MMT_F32,
                            torch.cuda.current_stream().cuda_stream), "mmt_gemm")
 
@@ -61,9 +62,10 @@ def test_gemm_plain(dname, M, N, K, act):
     b = torch.randn(N, generator=g)
     R = torch.randn(M, N, generator=g)
     Ad, Wd = A.to(dt).cuda(), W.to(dt).cuda()
+    bd, Rd = b.cuda(), R.cuda()  # held: a temporary's memory could be recycled before the launch
     out = torch.empty(M, N, device="cuda")
-    _gemm([Ad.data_ptr()], [Wd.data_ptr()], [out.data_ptr()], M, N, K, K, N, dt, bias=[b.cuda().data_ptr()],
-          r=[R.cuda().data_ptr()], ldr=N, act=act, c_f32=1)
+    _gemm([Ad.data_ptr()], [Wd.data_ptr()], [out.data_ptr()], M, N, K, K, N, dt, bias=[bd.data_ptr()],
+          r=[Rd.data_ptr()], ldr=N, act=act, c_f32=1)
     torch.cuda.synchronize()
     ref = A.to(dt).float() @ W.to(dt).float().t() + b
     ref = {0: ref, 1: F.gelu(ref), 2: F.relu(ref)}[act] + R
@@ -96,6 +98,62 @@ def test_gemm_groups_segments_ksplit(dname):
         assert err <= _tol(dt) * ref.abs().max().item(), (grp, err)
 
 
+@pytest.mark.parametrize("impl", [-1, 1, 2, 3])
+@pytest.mark.parametrize("M,N,K", [(528, 768, 768), (77, 196, 64), (300, 132, 192), (1056, 256, 3072)])
+def test_gemm_bf16_tile_paths(impl, M, N, K):
+    """Every bf16 GEMM kernel (impl: register-staged / LDS-DMA 128x128, 128x64 K-split, 64x64
+    K-split) on ragged M/N, odd K-step counts (the K-split's empty last step) and each epilogue:
+    GELU + fp32 residual into an fp32 C; bf16 C + C2 = C + bf16 residual (r_t) with a modulo row
+    map; two groups with segmented rows and a split K source."""
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    A = torch.randn(2, M, K, generator=g)
+    W = torch.randn(2, N, K, generator=g) / math.sqrt(K)
+    b = torch.randn(2, N, generator=g)
+    R = torch.randn(2, M, N, generator=g)
+    Ab, Wb = A.bfloat16(), W.bfloat16()
+    Ad, Wd, bd, Rd = Ab.cuda(), Wb.cuda(), b.cuda(), R.cuda()
+    ref = torch.einsum("gmk,gnk->gmn", Ab.float(), Wb.float()) + b[:, None]
+    # (1) GELU + fp32 residual, fp32 out, two groups
+    out = torch.empty(2, M, N, device="cuda")
+    _gemm([Ad[0].data_ptr(), Ad[1].data_ptr()], [Wd[0].data_ptr(), Wd[1].data_ptr()],
+          [out[0].data_ptr(), out[1].data_ptr()], M, N, K, K, N, torch.bfloat16,
+          bias=[bd[0].data_ptr(), bd[1].data_ptr()], r=[Rd[0].data_ptr(), Rd[1].data_ptr()], ldr=N, act=1, c_f32=1,
+          impl=impl)
+    torch.cuda.synchronize()
+    r1 = F.gelu(ref) + R
+    err = (out.cpu() - r1).abs().max().item()
+    assert err <= 1e-3 * r1.abs().max().item() + 1e-4, err
+    # (2) bf16 out + C2 with a bf16 residual read at row m % 5
+    Rt = R[0, :5].bfloat16().cuda()
+    c1 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    c2 = torch.empty_like(c1)
+    _gemm([Ad[0].data_ptr()], [Wd[0].data_ptr()], [c1.data_ptr()], M, N, K, K, N, torch.bfloat16,
+          bias=[bd[0].data_ptr()], r=[Rt.data_ptr()], ldr=N, r_t=1, r_mode=1, r_p0=5, c2=[c2.data_ptr()], impl=impl)
+    torch.cuda.synchronize()
+    rr = Rt.float().cpu()[torch.arange(M) % 5]
+    tol = 1e-2 * (ref[0].abs().max().item() + 4)
+    assert (c1.float().cpu() - ref[0]).abs().max().item() <= tol
+    assert (c2.float().cpu() - (ref[0] + rr)).abs().max().item() <= tol
+    # (3) segmented rows (runs of 7 rows, 3 per A block) + K split between two sources
+    if K >= 128:
+        ks = K // 2 + 8 if K % 128 else K // 2  # both sources use row stride lda = ks
+        src0 = torch.randn(2, M + 64, ks, generator=g).bfloat16()
+        src1 = torch.randn(2, M + 64, ks, generator=g).bfloat16()
+        s0, s1 = src0.cuda(), src1.cuda()
+        o3 = torch.empty(2, M, N, device="cuda")
+        _gemm([s0[0].data_ptr(), s0[1].data_ptr()], [Wd[0].data_ptr(), Wd[1].data_ptr()],
+              [o3[0].data_ptr(), o3[1].data_ptr()], M, N, K, ks, N, torch.bfloat16, c_f32=1, impl=impl,
+              a1=[s1[0].data_ptr(), s1[1].data_ptr()], k_split=ks, seg=(7, 3, 8 * ks, 0))
+        torch.cuda.synchronize()
+        # segment seg: rows (seg % 3) * 8 + (m % 7) of source block seg // 3 (a_stride_b = 0)
+        rows = [(m // 7 % 3) * 8 + m % 7 for m in range(M)]
+        for grp in range(2):
+            Ag = torch.cat([src0[grp, rows].float(), src1[grp, rows, :K - ks].float()], 1)
+            r3 = Ag @ Wb[grp].float().t()
+            e3 = (o3[grp].cpu() - r3).abs().max().item()
+            assert e3 <= 1e-3 * r3.abs().max().item() + 1e-4, (grp, e3)
+
+
 @pytest.mark.parametrize("dname", ["f32", "bf16"])
 @pytest.mark.parametrize("h,up,cin,cout", [(20, 1, 64, 96), (40, 2, 32, 48), (10, 1, 16, 200)])
 def test_conv3x3_implicit_gemm(dname, h, up, cin, cout):
@@ -112,8 +170,9 @@ def test_conv3x3_implicit_gemm(dname, h, up, cin, cout):
     rr = res.permute(0, 2, 3, 1).contiguous().cuda()
     out = torch.empty(B * h * h, cout, device="cuda", dtype=dt)
     out2 = torch.empty_like(out)
+    bd = b.cuda()
     _gemm([xin.data_ptr()], [wk.data_ptr()], [out.data_ptr()], B * h * h, cout, 9 * cin, cin, cout, dt,
-          bias=[b.cuda().data_ptr()], act=2, conv=(h, up, cin, 1), c2=[out2.data_ptr()], r=[rr.data_ptr()], ldr=cout,
+          bias=[bd.data_ptr()], act=2, conv=(h, up, cin, 1), c2=[out2.data_ptr()], r=[rr.data_ptr()], ldr=cout,
           r_mode=2, r_p0=h, r_p1=up)
     torch.cuda.synchronize()
     xu = F.interpolate(x.to(dt).float(), scale_factor=up) if up > 1 else x.to(dt).float()
@@ -195,7 +254,8 @@ def test_layernorm_groups_and_add(dname, C):
     of = torch.empty(rows, C, device="cuda")
     ot = torch.empty(rows, C, device="cuda", dtype=dt)
     gs = [t.cuda() for t in (ga, ba, gb, bb)]
-    L.check(L.LIB.mmt_layernorm(xd.data_ptr(), add.cuda().data_ptr(), rpg, of.data_ptr(), ot.data_ptr(),
+    addd = add.cuda()
+    L.check(L.LIB.mmt_layernorm(xd.data_ptr(), addd.data_ptr(), rpg, of.data_ptr(), ot.data_ptr(),
                                 *[t.data_ptr() for t in gs], rows, rpg, C, 1e-5,
                                 L.MMT_BF16 if dt == torch.bfloat16 else L.MMT_F32,
                                 torch.cuda.current_stream().cuda_stream), "ln")
@@ -214,7 +274,8 @@ def test_groupnorm():
     ga, ba, gb, bb = (torch.randn(Ct, generator=g) for _ in range(4))
     out = torch.empty(n, P, Ct, device="cuda")
     gs = [t.cuda() for t in (ga, ba, gb, bb)]
-    L.check(L.LIB.mmt_groupnorm(x.cuda().data_ptr(), out.data_ptr(), None, *[t.data_ptr() for t in gs], n, 2, P, Ct, G,
+    xd = x.cuda()
+    L.check(L.LIB.mmt_groupnorm(xd.data_ptr(), out.data_ptr(), None, *[t.data_ptr() for t in gs], n, 2, P, Ct, G,
                                 1e-5, L.MMT_F32, torch.cuda.current_stream().cuda_stream), "gn")
     torch.cuda.synchronize()
     xin = x.permute(0, 2, 1)
@@ -282,7 +343,8 @@ def test_msda_bimodal_vs_oracle(dname):
     offw = torch.randn(B * nq, 192, generator=g)
     offw[:, :128] *= 3.0
     out = torch.empty(B * nq, 512, device="cuda", dtype=dt)
-    L.check(L.LIB.mmt_msda_bimodal(offw.cuda().data_ptr(), value.to(dt).cuda().data_ptr(), out.data_ptr(), B, hw,
+    offd, vald = offw.cuda(), value.to(dt).cuda()
+    L.check(L.LIB.mmt_msda_bimodal(offd.data_ptr(), vald.data_ptr(), out.data_ptr(), B, hw,
                                    L.MMT_BF16 if dt == torch.bfloat16 else L.MMT_F32,
                                    torch.cuda.current_stream().cuda_stream), "msda_bimodal")
     torch.cuda.synchronize()
@@ -306,8 +368,8 @@ def test_prroi_known_answer():
     feat = torch.rand(4, 16, 24, 32, generator=g)
     rois = torch.tensor([[0, 0, 0, 14, 14], [1, 14, 14, 28, 28]], dtype=torch.float32)
     out = torch.empty(2, 16, 7, 7, device="cuda")
-    fd = feat.cuda()
-    L.check(L.LIB.mmt_prroi_pool_forward(fd.data_ptr(), rois.cuda().data_ptr(), out.data_ptr(), 2, 16, 24, 32,
+    fd, rd = feat.cuda(), rois.cuda()
+    L.check(L.LIB.mmt_prroi_pool_forward(fd.data_ptr(), rd.data_ptr(), out.data_ptr(), 2, 16, 24, 32,
                                          16 * 24 * 32, 24 * 32, 32, 1, 7, 7, 0.5, 16 * 49, 49, 1,
                                          torch.cuda.current_stream().cuda_stream), "prroi")
     torch.cuda.synchronize()
@@ -325,7 +387,8 @@ def test_prroi_fractional_vs_oracle():
     feat = torch.randn(2, 8, 20, 20, generator=g)
     rois = torch.tensor([[0, 1.3, 2.7, 15.2, 9.9], [1, -2.0, 3.5, 7.25, 21.0], [0, 5.0, 5.0, 5.0, 9.0]])
     out = torch.empty(3, 8, 4, 4, device="cuda")
-    L.check(L.LIB.mmt_prroi_pool_forward(feat.cuda().data_ptr(), rois.cuda().data_ptr(), out.data_ptr(), 3, 8, 20, 20,
+    fd, rd = feat.cuda(), rois.cuda()
+    L.check(L.LIB.mmt_prroi_pool_forward(fd.data_ptr(), rd.data_ptr(), out.data_ptr(), 3, 8, 20, 20,
                                          8 * 400, 400, 20, 1, 4, 4, 1.0, 8 * 16, 16, 1,
                                          torch.cuda.current_stream().cuda_stream), "prroi")
     torch.cuda.synchronize()

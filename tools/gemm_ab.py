@@ -1,0 +1,100 @@
+#!/usr/bin/env python3
+"""A/B timing of the bf16 GEMM kernels (mmt_gemm impl -1 / 1 / 2 / 3 / auto) against torch.bmm
+(hipBLASLt) on the hot path's GEMM shapes: back-to-back launches captured in a hipGraph and timed
+with HIP events (device time, no host launch cost).
+
+usage: python tools/gemm_ab.py [--reps 200]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "multi-modal-tracking_amd"))
+import torch  # noqa: E402
+
+from mmt_amd import _lib as L  # noqa: E402
+
+# (name, groups, M per group, N, K, act, residual) at B = 1: rgbt two-stream (groups = modalities)
+SHAPES = [("qkv", 2, 528, 2304, 768, 0, 0), ("proj", 2, 528, 768, 768, 0, 1), ("fc1", 2, 528, 3072, 768, 1, 0),
+          ("fc2", 2, 528, 768, 3072, 0, 1), ("qkv_B4", 2, 2112, 2304, 768, 0, 0), ("fc2_B4", 2, 2112, 768, 3072, 0, 1)]
+
+
+def run(name, G, M, N, K, act, res, impl, reps):
+    A = torch.randn(G, M, K, device="cuda").bfloat16()
+    W = (torch.randn(G, N, K, device="cuda") / K ** 0.5).bfloat16()
+    b = torch.randn(G, N, device="cuda")
+    R = torch.randn(G, M, N, device="cuda")
+    C = torch.empty(G, M, N, device="cuda", dtype=torch.float32 if res else torch.bfloat16)
+    p = L.GemmParams()
+    for g in range(G):
+        p.a[g], p.w[g], p.c[g], p.bias[g] = A[g].data_ptr(), W[g].data_ptr(), C[g].data_ptr(), b[g].data_ptr()
+        p.r[g] = R[g].data_ptr() if res else None
+    p.lda, p.ldc, p.ldr = K, N, N
+    p.a_seg_rows, p.a_segs_a = M, 1
+    p.M, p.N, p.K, p.act, p.c_f32, p.groups, p.impl = M, N, K, act, 1 if res else 0, G, impl
+    fn = lambda: L.check(L.LIB.mmt_gemm(L.ctypes.byref(p), L.MMT_BF16,  # noqa: E731
+                                        torch.cuda.current_stream().cuda_stream), name)
+    us = graph_time(fn, reps)
+    ref = torch.baddbmm(b[:, None, :], A.float(), W.float().transpose(1, 2))
+    if act:
+        ref = torch.nn.functional.gelu(ref)
+    if res:
+        ref = ref + R
+    err = ((C.float() - ref).abs().max() / ref.abs().max()).item()
+    return us, err
+
+
+def torch_ref(G, M, N, K, reps):
+    A = torch.randn(G, M, K, device="cuda").bfloat16()
+    Wt = (torch.randn(G, K, N, device="cuda") / K ** 0.5).bfloat16()
+    out = torch.empty(G, M, N, device="cuda", dtype=torch.bfloat16)
+    return graph_time(lambda: torch.bmm(A, Wt, out=out), reps)
+
+
+def graph_time(fn, reps, per_graph=20):
+    """Device time per call: `per_graph` back-to-back calls captured in one hipGraph, replayed."""
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(per_graph):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n = max(1, reps // per_graph)
+    e0.record(s)
+    for _ in range(n):
+        g.replay()
+    e1.record(s)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / (n * per_graph)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=200)
+    ap.add_argument("--impls", default="-1,1,2,3,0")
+    ap.add_argument("--no-torch", action="store_true")
+    args = ap.parse_args()
+    impls = [int(x) for x in args.impls.split(",")]
+    rows = []
+    for name, G, M, N, K, act, res in SHAPES:
+        fl = 2.0 * G * M * N * K
+        row = {"gemm": name, "G": G, "M": M, "N": N, "K": K}
+        for impl in impls:
+            us, err = run(name, G, M, N, K, act, res, impl, args.reps)
+            row["impl%d" % impl] = {"us": round(us, 2), "tflops": round(fl / us / 1e6, 1), "relerr": float("%.2e" % err)}
+        if not args.no_torch:
+            tu = torch_ref(G, M, N, K, args.reps)
+            row["torch_bmm"] = {"us": round(tu, 2), "tflops": round(fl / tu / 1e6, 1)}
+        rows.append(row)
+        print(json.dumps(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()
