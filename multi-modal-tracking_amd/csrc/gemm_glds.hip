@@ -28,6 +28,26 @@
 #define MMT_GEMM_ABLATE 0
 #endif
 
+// MMT_GEMM_STAMP (measurement builds only, tools/build_ablate.sh): workgroup-leader timestamps
+// per phase, read back with mmt_gemm_stamps() (tools/gemm_stamps.py).
+#ifndef MMT_GEMM_STAMP
+#define MMT_GEMM_STAMP 0
+#endif
+#if MMT_GEMM_STAMP
+__device__ unsigned long long g_mmt_stamps[16384 * 6];
+#define MMT_STAMP(I, INSN)                                                                          \
+    if (threadIdx.x == 0) {                                                                        \
+        unsigned long long t_;                                                                     \
+        asm volatile(INSN " %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                      \
+        g_mmt_stamps[(blockIdx.x + gridDim.x * blockIdx.z) * 6 + (I)] = t_;                        \
+    }
+extern "C" int mmt_gemm_stamps(unsigned long long* host, int n) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_mmt_stamps), sizeof(unsigned long long) * n);
+}
+#else
+#define MMT_STAMP(I, INSN)
+#endif
+
 namespace {
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -62,6 +82,8 @@ __global__ __launch_bounds__(256 * KS) __attribute__((amdgpu_waves_per_eu(KS, KS
     static_assert(KS * ST * STAGE <= 160 * 1024, "LDS budget");
     static_assert(KS == 1 || BM * BN * 4 <= KS * ST * STAGE, "k-group reduction buffer");
     __shared__ __attribute__((aligned(1024))) unsigned char lds[KS * ST * STAGE];
+    MMT_STAMP(0, "s_memrealtime");
+    MMT_STAMP(1, "s_memtime");
 
     // XCD-aware bijective remap (see gemm.hip): each XCD gets a contiguous run of (group, tile)
     // ids, tm fastest, so a run's W column slices and A rows stay in that XCD's L2.
@@ -159,6 +181,7 @@ __global__ __launch_bounds__(256 * KS) __attribute__((amdgpu_waves_per_eu(KS, KS
     for (int j = 0; j < ST - 1 && j < ns; ++j) issue(j);
     if (MMT_GEMM_ABLATE == 1) wait_vm<0>();
     sync_for(0);
+    MMT_STAMP(2, "s_memtime");
     MMT_READ(ring, fa0, fb0);
     // Every k-group has a real K-step at j < ns-1; only the last can be empty (KS = 2 with an odd
     // step count).  Keeping that test out of the loop keeps the accumulators in place (a
@@ -183,6 +206,7 @@ __global__ __launch_bounds__(256 * KS) __attribute__((amdgpu_waves_per_eu(KS, KS
     }
 #undef MMT_READ
 #undef MMT_MMA
+    MMT_STAMP(3, "s_memtime");
 
     if constexpr (KS > 1) {  // sum the k-groups' partial tiles through LDS
         static_assert(KS == 2, "k-group reduction written for two groups");
@@ -271,6 +295,11 @@ __global__ __launch_bounds__(256 * KS) __attribute__((amdgpu_waves_per_eu(KS, KS
             }
         }
     }
+#if MMT_GEMM_STAMP
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    MMT_STAMP(4, "s_memtime");
+    MMT_STAMP(5, "s_memrealtime");
 }
 
 template <int BM, int BN, int KS, int ST>

@@ -72,15 +72,17 @@ def test_graph_replay_is_bitwise_eager(variant):
         assert torch.equal(s0, s1)
 
 
-def test_batch_rows_independent():
-    """Frame b of a batch equals the same frame run alone (no cross-batch leakage)."""
-    rt = _runtime("asym", torch.bfloat16)
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 5e-3)])
+def test_batch_rows_independent(dtype, tol):
+    """Frame b of a batch equals the same frame run alone (no cross-batch leakage).  Not bitwise:
+    the GEMM tile shape (hence the fp32 summation order) is chosen per M, i.e. per batch size."""
+    rt = _runtime("asym", dtype)
     t, o, s = _inputs(2)
     b2, _ = rt.forward(t, o, s)
     b2 = b2.clone()
     b1, _ = rt.forward([x[1:2] for x in t], [x[1:2] for x in o], [x[1:2] for x in s])
     torch.cuda.synchronize()
-    assert (b2[1] - b1[0]).abs().max().item() < 1e-5
+    assert (b2[1] - b1[0]).abs().max().item() < tol
 
 
 def test_zero_copy_plan_matches_copy_path():

@@ -1,10 +1,15 @@
 #!/bin/bash
-# Builds measurement-only variants of libmmt_hip.so with the LDS-DMA GEMM's K loop ablated
-# (MMT_GEMM_ABLATE=1: no DMA after the prologue; 2: no MFMA).  Results are wrong by design; use
-# with MMT_HIP_LIB=... python tools/gemm_ab.py --no-check.
+# Measurement-only variants of libmmt_hip.so (never the product):
+#   ablate1: LDS-DMA GEMM K loop without DMA after the prologue (MMT_GEMM_ABLATE=1)
+#   ablate2: LDS-DMA GEMM K loop without MFMA work          (MMT_GEMM_ABLATE=2)
+#   stamp:   LDS-DMA GEMM with per-phase workgroup timestamps (MMT_GEMM_STAMP=1)
+# Use with MMT_HIP_LIB=multi-modal-tracking_amd/mmt_amd/_lib/<variant>/libmmt_hip.so.
 set -e
 cd "$(dirname "$0")/../multi-modal-tracking_amd/csrc"
-for a in 1 2; do
-  make -s OUT=../mmt_amd/_lib/ablate$a OBJDIR=../mmt_amd/_lib/ablate$a/obj \
-       CXXFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 -DMMT_GEMM_ABLATE=$a"
-done
+build() {
+  make -s OUT=../mmt_amd/_lib/$1 OBJDIR=../mmt_amd/_lib/$1/obj \
+       CXXFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 $2"
+}
+build ablate1 -DMMT_GEMM_ABLATE=1
+build ablate2 -DMMT_GEMM_ABLATE=2
+build stamp -DMMT_GEMM_STAMP=1

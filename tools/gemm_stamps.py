@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""Per-phase timing of the LDS-DMA GEMM from in-kernel timestamps (stamp build of tools/build_ablate.sh).
+
+Phases per workgroup (leader thread): prologue = start -> first K-step landed (DMA latency + address
+setup); loop = the K loop; epilogue = loop end -> stores retired.  Cycle counts come from s_memtime;
+start / end skew across workgroups from s_memrealtime (100 MHz).
+
+usage: MMT_HIP_LIB=.../_lib/stamp/libmmt_hip.so python tools/gemm_stamps.py
+"""
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "multi-modal-tracking_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from mmt_amd import _lib as L  # noqa: E402
+
+SHAPES = [("qkv", 2, 528, 2304, 768, 0, 0), ("proj", 2, 528, 768, 768, 0, 1), ("fc1", 2, 528, 3072, 768, 1, 0),
+          ("fc2", 2, 528, 768, 3072, 0, 1), ("k64", 2, 528, 768, 64, 0, 1), ("k256", 2, 528, 768, 256, 0, 1)]
+TILES = {1: (128, 128), 2: (128, 64), 3: (64, 64)}
+
+
+def main():
+    L.LIB.mmt_gemm_stamps.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+    for name, G, M, N, K, act, res in SHAPES:
+        A = torch.randn(G, M, K, device="cuda").bfloat16()
+        W = (torch.randn(G, N, K, device="cuda") / K ** 0.5).bfloat16()
+        b = torch.randn(G, N, device="cuda")
+        R = torch.randn(G, M, N, device="cuda")
+        C = torch.empty(G, M, N, device="cuda", dtype=torch.float32 if res else torch.bfloat16)
+        for impl in (1, 2, 3):
+            p = L.GemmParams()
+            for g in range(G):
+                p.a[g], p.w[g], p.c[g], p.bias[g] = A[g].data_ptr(), W[g].data_ptr(), C[g].data_ptr(), b[g].data_ptr()
+                p.r[g] = R[g].data_ptr() if res else None
+            p.lda, p.ldc, p.ldr = K, N, N
+            p.a_seg_rows, p.a_segs_a = M, 1
+            p.M, p.N, p.K, p.act, p.c_f32, p.groups, p.impl = M, N, K, act, 1 if res else 0, G, impl
+            s = torch.cuda.current_stream().cuda_stream
+            for _ in range(10):
+                L.check(L.LIB.mmt_gemm(ctypes.byref(p), L.MMT_BF16, s), name)
+            torch.cuda.synchronize()
+            bm, bn = TILES[impl]
+            nwg = ((M + bm - 1) // bm) * ((N + bn - 1) // bn) * G
+            buf = (ctypes.c_ulonglong * (nwg * 6))()
+            L.check(L.LIB.mmt_gemm_stamps(buf, nwg * 6), "stamps")
+            st = np.frombuffer(buf, dtype=np.uint64).reshape(nwg, 6).astype(np.int64)
+            rt0, c0, c1, c2, c3, rt1 = st.T
+            freq = np.median((c3 - c0) / np.maximum(rt1 - rt0, 1)) * 100.0  # MHz (realtime = 100 MHz)
+            row = {"gemm": name, "impl": impl, "nwg": nwg, "clock_mhz": round(float(freq), 0),
+                   "prologue_us": round(float(np.median(c1 - c0)) / freq, 2),
+                   "loop_us": round(float(np.median(c2 - c1)) / freq, 2),
+                   "epilogue_us": round(float(np.median(c3 - c2)) / freq, 2),
+                   "wg_total_us_med": round(float(np.median(c3 - c0)) / freq, 2),
+                   "wg_total_us_max": round(float(np.max(c3 - c0)) / freq, 2),
+                   "start_spread_us": round(float(rt0.max() - rt0.min()) / 100.0, 2),
+                   "span_us": round(float(rt1.max() - rt0.min()) / 100.0, 2)}
+            print(json.dumps(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()
