@@ -78,8 +78,9 @@ typedef struct {
     int32_t groups;
     int32_t r_t;  /* 1: R is stored in `dtype` instead of fp32 */
     int32_t impl; /* kernel choice, results identical up to fp32 summation order: 0 auto;
-                     -1 register-staged 64/128 tiles; 1 / 2 / 3 LDS-DMA 128x128 / 128x64 (K split
-                     over 2 wave groups) / 64x64 (K split 2), bf16 with K % 64 == 0 only */
+                     -1 register-staged 64/128 tiles; LDS-DMA (bf16, K % 64 == 0 only): 1 128x128
+                     (8 waves), 2 128x64 (K split over 2 wave groups), 3 64x64 (K split 2),
+                     4 128x128 (4 waves) */
 } mmt_gemm_params;
 
 int mmt_gemm(const mmt_gemm_params* p, int dtype, void* stream);

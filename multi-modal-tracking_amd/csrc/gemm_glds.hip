@@ -72,13 +72,18 @@ MMT_DEV void wait_stages(int ahead) {
     else wait_vm<(ST >= 4 ? 3 * L : L)>();
 }
 
-template <int BM, int BN, int KS, int ST>
-__global__ __launch_bounds__(256 * KS) __attribute__((amdgpu_waves_per_eu(KS, KS))) void gemm_glds_kernel(const mmt_gemm_params p) {
-    constexpr int KT = 64;                    // bf16 elements of K per step: 128-B rows
-    constexpr int STAGE = (BM + BN) * 128;    // bytes of one stage image (A rows, then W rows)
-    constexpr int PA = BM / 32, PB = BN / 32; // 1-KiB pieces per wave per stage (4 waves)
-    constexpr int L = PA + PB;                // DMA instructions per wave per stage
-    constexpr int WM = BM / 2, WN = BN / 2, MT = WM / 16, NT = WN / 16;
+// WGM x WGN waves per k-group own WM x WN sub-tiles; KS k-groups split the K-steps.
+template <int BM, int BN, int WGM, int WGN, int KS, int ST>
+__global__ __launch_bounds__(64 * WGM * WGN * KS)
+    __attribute__((amdgpu_waves_per_eu(WGM * WGN * KS / 4, WGM * WGN * KS / 4))) void gemm_glds_kernel(
+        const mmt_gemm_params p) {
+    constexpr int NW = WGM * WGN, TPG = 64 * NW;  // waves / threads per k-group
+    constexpr int KT = 64;                        // bf16 elements of K per step: 128-B rows
+    constexpr int STAGE = (BM + BN) * 128;        // bytes of one stage image (A rows, then W rows)
+    constexpr int PA = BM / 8 / NW, PB = BN / 8 / NW;  // 1-KiB pieces per wave per stage
+    static_assert(PA * 8 * NW == BM && PB * 8 * NW == BN, "pieces divide evenly over the waves");
+    constexpr int L = PA + PB;  // DMA instructions per wave per stage
+    constexpr int WM = BM / WGM, WN = BN / WGN, MT = WM / 16, NT = WN / 16;
     static_assert(KS * ST * STAGE <= 160 * 1024, "LDS budget");
     static_assert(KS == 1 || BM * BN * 4 <= KS * ST * STAGE, "k-group reduction buffer");
     __shared__ __attribute__((aligned(1024))) unsigned char lds[KS * ST * STAGE];
@@ -95,8 +100,8 @@ __global__ __launch_bounds__(256 * KS) __attribute__((amdgpu_waves_per_eu(KS, KS
     const int tiles_m = (p.M + BM - 1) / BM;
     const int tm = tile % tiles_m, tn = tile / tiles_m;
     const int m0 = tm * BM, n0 = tn * BN;
-    const int lane = threadIdx.x & 63, kg = threadIdx.x >> 8;
-    const int wid = (threadIdx.x & 255) >> 6, wr = wid >> 1, wc = wid & 1;
+    const int lane = threadIdx.x & 63, kg = threadIdx.x / TPG;
+    const int wid = (threadIdx.x % TPG) >> 6, wr = wid / WGN, wc = wid % WGN;
     const int l16 = lane & 15, lg = lane >> 4;
     const int M = p.M, N = p.N, K = p.K;
 
@@ -208,89 +213,112 @@ __global__ __launch_bounds__(256 * KS) __attribute__((amdgpu_waves_per_eu(KS, KS
 #undef MMT_MMA
     MMT_STAMP(3, "s_memtime");
 
-    if constexpr (KS > 1) {  // sum the k-groups' partial tiles through LDS
-        static_assert(KS == 2, "k-group reduction written for two groups");
-        lds_barrier();
-        f32x4* red = (f32x4*)lds;
-        if (kg == 1) {
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-                for (int mt = 0; mt < MT; ++mt) red[((wid * NT + nt) * MT + mt) * 64 + lane] = acc[nt][mt];
-        }
-        lds_barrier();
-        if (kg == 1) return;
+    // ---- epilogue through LDS.  Fragment-shaped stores (16 rows x 32 B per wave-instruction) ran
+    // at a fraction of the store path's rate (5-8 us of a 15-19 us launch, per in-kernel stamps),
+    // so the fp32 tile is first assembled in LDS (summing the two k-groups when KS = 2) and then
+    // every thread owns 8 consecutive columns of RPP-row strips: bias / residual loads and C / C2
+    // stores are whole 256-512-B row segments per wave-instruction.
+    constexpr int TP = BN + 4;  // tile row pitch (floats); +4 keeps the fragment writes 2-way
+    static_assert(BM * TP * 4 <= KS * ST * STAGE, "epilogue tile fits in the stage ring");
+    float* ctile = (float*)lds;
+    lds_barrier();  // every wave is past its last fragment read (the DMA ring is drained: vmcnt(0))
+    if (KS == 1 || kg == 1) {
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt) acc[nt][mt] += red[((wid * NT + nt) * MT + mt) * 64 + lane];
+            for (int mt = 0; mt < MT; ++mt)
+                *(f32x4*)(ctile + (wr * WM + mt * 16 + l16) * TP + wc * WN + nt * 16 + lg * 4) = acc[nt][mt];
     }
+    if constexpr (KS == 2) {
+        lds_barrier();
+        if (kg == 0) {
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt) {
+                    f32x4* t4 = (f32x4*)(ctile + (wr * WM + mt * 16 + l16) * TP + wc * WN + nt * 16 + lg * 4);
+                    *t4 = *t4 + acc[nt][mt];
+                }
+        }
+    }
+    static_assert(KS <= 2, "k-group reduction written for up to two groups");
+    lds_barrier();
 
-    // ---- epilogue: 4 consecutive columns per lane.  Bias / residual loads are issued first and
-    // unconditionally (clamped row / column); only the stores are predicated.  (Loads inside a
-    // lane-divergent guard make hipcc wait vmcnt(0) per fragment: MT*NT serial round trips.)
+    // 8-column strips: one 16-B store per lane for a bf16 C (two for fp32); dwordx2 stores were
+    // store-issue-bound.
+    constexpr int NTHR = TPG * KS, TPR = BN / 8, RPP = NTHR / TPR, NPASS = BM / RPP;
+    static_assert(NTHR % TPR == 0 && BM % RPP == 0, "strip geometry");
     const float* bias = p.bias[g];
     const float* R = p.r[g];
     char* C = (char*)p.c[g];
     char* C2 = (char*)p.c2[g];
-    int nc[NT];
-    f32x4 bn[NT];
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-        nc[nt] = min(n0 + wc * WN + nt * 16 + lg * 4, N - 4);
-        bn[nt] = bias ? *(const f32x4*)(bias + nc[nt]) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const int tc = (threadIdx.x % TPR) * 8, tr = threadIdx.x / TPR;
+    const int n = n0 + tc, nc = min(n, N - 8);
+    f32x4 bn0 = {0.f, 0.f, 0.f, 0.f}, bn1 = bn0;
+    if (bias) {
+        bn0 = *(const f32x4*)(bias + nc);
+        bn1 = *(const f32x4*)(bias + nc + 4);
     }
-    int64_t rbase[MT];
+    constexpr int PG = NPASS < 4 ? NPASS : 4;  // passes whose residual loads are in flight together
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-        const int m = min(m0 + wr * WM + mt * 16 + l16, M - 1);
-        int64_t rr = m;
-        if (p.r_mode == 1) rr = m % p.r_p0;
-        else if (p.r_mode == 2) {
-            const int hw = p.r_p0 * p.r_p0, b = m / hw, rem = m - b * hw;
-            const int y = rem / p.r_p0, x = rem - y * p.r_p0, hs = p.r_p0 / p.r_p1;
-            rr = (int64_t)b * hs * hs + (int64_t)(y / p.r_p1) * hs + (x / p.r_p1);
-        }
-        rbase[mt] = rr * p.ldr;
-    }
-    f32x4 rv[NT][MT];  // every residual load in flight at once: one round trip, not NT
+    for (int p0 = 0; p0 < NPASS; p0 += PG) {
+        f32x4 ra[PG], rb[PG];
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-            rv[nt][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (R) {  // wave-uniform
+        for (int i = 0; i < PG; ++i) {
+            ra[i] = rb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (R) {  // wave-uniform; loads unconditional from a clamped row
+                const int m = min(m0 + tr + (p0 + i) * RPP, M - 1);
+                int64_t rr = m;
+                if (p.r_mode == 1) rr = m % p.r_p0;
+                else if (p.r_mode == 2) {
+                    const int hw = p.r_p0 * p.r_p0, b = m / hw, rem = m - b * hw;
+                    const int y = rem / p.r_p0, x = rem - y * p.r_p0, hs = p.r_p0 / p.r_p1;
+                    rr = (int64_t)b * hs * hs + (int64_t)(y / p.r_p1) * hs + (x / p.r_p1);
+                }
                 if (p.r_t) {
-                    const uint2 u = *(const uint2*)((const bf16_t*)R + rbase[mt] + nc[nt]);
-                    rv[nt][mt] = f32x4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
-                                       __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
+                    const u32x4 u = *(const u32x4*)((const bf16_t*)R + rr * p.ldr + nc);
+                    ra[i] = f32x4{__uint_as_float(u[0] << 16), __uint_as_float(u[0] & 0xffff0000u),
+                                  __uint_as_float(u[1] << 16), __uint_as_float(u[1] & 0xffff0000u)};
+                    rb[i] = f32x4{__uint_as_float(u[2] << 16), __uint_as_float(u[2] & 0xffff0000u),
+                                  __uint_as_float(u[3] << 16), __uint_as_float(u[3] & 0xffff0000u)};
                 } else {
-                    rv[nt][mt] = *(const f32x4*)(R + rbase[mt] + nc[nt]);
+                    ra[i] = *(const f32x4*)(R + rr * p.ldr + nc);
+                    rb[i] = *(const f32x4*)(R + rr * p.ldr + nc + 4);
                 }
             }
         }
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-        const int n = n0 + wc * WN + nt * 16 + lg * 4;
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-            const int m = m0 + wr * WM + mt * 16 + l16;
-            f32x4 v = acc[nt][mt] + bn[nt];
+        for (int i = 0; i < PG; ++i) {
+            const int r = tr + (p0 + i) * RPP, m = m0 + r;
+            f32x4 va = *(const f32x4*)(ctile + r * TP + tc) + bn0;
+            f32x4 vb = *(const f32x4*)(ctile + r * TP + tc + 4) + bn1;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                if (p.act == 1) v[j] = gelu_erf(v[j]);
-                else if (p.act == 2) v[j] = fmaxf(v[j], 0.f);
+                if (p.act == 1) {
+                    va[j] = gelu_erf(va[j]);
+                    vb[j] = gelu_erf(vb[j]);
+                } else if (p.act == 2) {
+                    va[j] = fmaxf(va[j], 0.f);
+                    vb[j] = fmaxf(vb[j], 0.f);
+                }
             }
-            const f32x4 o1 = C2 ? v : v + rv[nt][mt];
-            const f32x4 o2 = v + rv[nt][mt];
+            const f32x4 sa = va + ra[i], sb = vb + rb[i];  // + residual
+            const f32x4 oa = C2 ? va : sa, ob = C2 ? vb : sb;
             if (m < M && n < N) {
                 const int64_t e = (int64_t)m * p.ldc + n;
                 if (p.c_f32) {
-                    *(f32x4*)((float*)C + e) = o1;
-                    if (C2) *(f32x4*)((float*)C2 + e) = o2;
+                    *(f32x4*)((float*)C + e) = oa;
+                    *(f32x4*)((float*)C + e + 4) = ob;
+                    if (C2) {
+                        *(f32x4*)((float*)C2 + e) = sa;
+                        *(f32x4*)((float*)C2 + e + 4) = sb;
+                    }
                 } else {
-                    *(uint2*)((bf16_t*)C + e) = make_uint2(pack_bf16x2(o1[0], o1[1]), pack_bf16x2(o1[2], o1[3]));
-                    if (C2) *(uint2*)((bf16_t*)C2 + e) = make_uint2(pack_bf16x2(o2[0], o2[1]), pack_bf16x2(o2[2], o2[3]));
+                    *(u32x4*)((bf16_t*)C + e) = u32x4{pack_bf16x2(oa[0], oa[1]), pack_bf16x2(oa[2], oa[3]),
+                                                      pack_bf16x2(ob[0], ob[1]), pack_bf16x2(ob[2], ob[3])};
+                    if (C2)
+                        *(u32x4*)((bf16_t*)C2 + e) = u32x4{pack_bf16x2(sa[0], sa[1]), pack_bf16x2(sa[2], sa[3]),
+                                                           pack_bf16x2(sb[0], sb[1]), pack_bf16x2(sb[2], sb[3])};
                 }
             }
         }
@@ -302,10 +330,11 @@ __global__ __launch_bounds__(256 * KS) __attribute__((amdgpu_waves_per_eu(KS, KS
     MMT_STAMP(5, "s_memrealtime");
 }
 
-template <int BM, int BN, int KS, int ST>
+template <int BM, int BN, int WGM, int WGN, int KS, int ST>
 void launch(const mmt_gemm_params& p, hipStream_t st) {
     const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, KS, ST>), dim3(tiles, 1, p.groups), dim3(256 * KS), 0, st, p);
+    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, KS, ST>), dim3(tiles, 1, p.groups),
+                       dim3(64 * WGM * WGN * KS), 0, st, p);
 }
 
 bool aligned(const void* ptr, int bytes) { return ((uintptr_t)ptr & (uintptr_t)(bytes - 1)) == 0; }
@@ -315,28 +344,30 @@ bool aligned(const void* ptr, int bytes) { return ((uintptr_t)ptr & (uintptr_t)(
 // Returns 1 when the shape / layout is not one this kernel takes (caller uses gemm.hip's kernel).
 int mmt_gemm_glds_bf16(const mmt_gemm_params& p, hipStream_t st, int force) {
     if (force < 0) return 1;
-    if (p.conv_h > 0 || p.K % 64 || p.N % 4 || p.ldc % 4 || (p.r[0] && p.ldr % 4)) return 1;
+    if (p.conv_h > 0 || p.K % 64 || p.N % 8 || p.ldc % 8 || (p.r[0] && p.ldr % 8)) return 1;
     if (p.lda % 8 || p.a_stride_a % 8 || p.a_stride_b % 8 || p.k_split % 8) return 1;
     if (p.a_seg_rows > INT32_MAX || p.a_segs_a > INT32_MAX) return 1;
     for (int g = 0; g < p.groups; ++g) {
-        const int cb = p.c_f32 ? 16 : 8;
-        if (!aligned(p.c[g], cb) || (p.c2[g] && !aligned(p.c2[g], cb))) return 1;
+        if (!aligned(p.c[g], 16) || (p.c2[g] && !aligned(p.c2[g], 16))) return 1;
         if (p.bias[g] && !aligned(p.bias[g], 16)) return 1;
-        if (p.r[g] && !aligned(p.r[g], p.r_t ? 8 : 16)) return 1;
+        if (p.r[g] && !aligned(p.r[g], 16)) return 1;
     }
     auto blocks = [&](int bm, int bn) { return (int64_t)((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn) * p.groups; };
     const int nk = p.K / 64;
     int cfg = force;
     if (cfg == 0) {
+        // measured at batch 1 (tools/gemm_ab.py, tools/gemm_stamps.py): 128x128 / 8 waves once the
+        // grid has >= 128 tiles (qkv, fc1); below that (N = 768: proj, fc2) 64x64 with the K steps
+        // split over two wave groups, which keeps ~216 CUs streaming.
         if (blocks(128, 128) >= 128) cfg = 1;
-        else if (blocks(128, 64) >= 64 && nk >= 4) cfg = 2;
         else if (nk >= 4) cfg = 3;
         else return 1;
     }
     switch (cfg) {
-        case 1: launch<128, 128, 1, 4>(p, st); break;
-        case 2: launch<128, 64, 2, 3>(p, st); break;
-        case 3: launch<64, 64, 2, 4>(p, st); break;
+        case 1: launch<128, 128, 2, 4, 1, 4>(p, st); break;
+        case 2: launch<128, 64, 2, 2, 2, 3>(p, st); break;
+        case 3: launch<64, 64, 2, 2, 2, 4>(p, st); break;
+        case 4: launch<128, 128, 2, 2, 1, 4>(p, st); break;
         default: return 1;
     }
     return 0;

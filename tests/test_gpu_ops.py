@@ -98,7 +98,7 @@ def test_gemm_groups_segments_ksplit(dname):
         assert err <= _tol(dt) * ref.abs().max().item(), (grp, err)
 
 
-@pytest.mark.parametrize("impl", [-1, 1, 2, 3])
+@pytest.mark.parametrize("impl", [-1, 1, 2, 3, 4])
 @pytest.mark.parametrize("M,N,K", [(528, 768, 768), (77, 196, 64), (300, 132, 192), (1056, 256, 3072)])
 def test_gemm_bf16_tile_paths(impl, M, N, K):
     """Every bf16 GEMM kernel (impl: register-staged / LDS-DMA 128x128, 128x64 K-split, 64x64

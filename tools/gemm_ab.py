@@ -78,7 +78,7 @@ def graph_time(fn, reps, per_graph=20):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=200)
-    ap.add_argument("--impls", default="-1,1,2,3,0")
+    ap.add_argument("--impls", default="-1,1,2,3,4,0")
     ap.add_argument("--no-torch", action="store_true")
     args = ap.parse_args()
     impls = [int(x) for x in args.impls.split(",")]

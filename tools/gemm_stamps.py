@@ -22,7 +22,7 @@ from mmt_amd import _lib as L  # noqa: E402
 
 SHAPES = [("qkv", 2, 528, 2304, 768, 0, 0), ("proj", 2, 528, 768, 768, 0, 1), ("fc1", 2, 528, 3072, 768, 1, 0),
           ("fc2", 2, 528, 768, 3072, 0, 1), ("k64", 2, 528, 768, 64, 0, 1), ("k256", 2, 528, 768, 256, 0, 1)]
-TILES = {1: (128, 128), 2: (128, 64), 3: (64, 64)}
+TILES = {1: (128, 128), 2: (128, 64), 3: (64, 64), 4: (128, 128)}
 
 
 def main():
@@ -33,7 +33,7 @@ def main():
         b = torch.randn(G, N, device="cuda")
         R = torch.randn(G, M, N, device="cuda")
         C = torch.empty(G, M, N, device="cuda", dtype=torch.float32 if res else torch.bfloat16)
-        for impl in (1, 2, 3):
+        for impl in (1, 2, 3, 4):
             p = L.GemmParams()
             for g in range(G):
                 p.a[g], p.w[g], p.c[g], p.bias[g] = A[g].data_ptr(), W[g].data_ptr(), C[g].data_ptr(), b[g].data_ptr()
