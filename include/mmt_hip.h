@@ -96,6 +96,8 @@ typedef struct {
     void* out;
     int32_t S, Bm, ntok, n_t, C, H, asym;
     float scale;
+    int32_t impl; /* bf16 kernel choice (identical results up to fp32 summation order): 0 auto,
+                     2 / 4 = key tiles split over 2 / 4 groups of 4 waves */
 } mmt_attn_params;
 
 int mmt_mam_attention(const mmt_attn_params* p, int dtype, void* stream);

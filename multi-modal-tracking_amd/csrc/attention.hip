@@ -288,13 +288,66 @@ MMT_DEV void attn_lds_wait() {
     __builtin_amdgcn_sched_barrier(0);  // keep the MFMAs that consume the asm reads below the wait
 }
 
+#if MMT_STAMP_BUILD
+__device__ unsigned long long g_mmt_attn_stamps[16384 * 6];
+extern "C" int mmt_attn_stamps(unsigned long long* host, int n) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_mmt_attn_stamps), sizeof(unsigned long long) * n);
+}
+#endif
+#define MMT_ASTAMP(I, INSN) MMT_STAMP_AT(g_mmt_attn_stamps, I, INSN)
+
 constexpr int ANS = 8;              // K/V tile slots in the ring
 constexpr int ATILE = 2 * KB * 128; // bytes of one slot: K image then V image
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void mam_attention_glds_kernel(
+// Cross-lane reductions over the 4 lane groups (lanes l, l^16, l^32, l^48) that hold the 64 keys
+// of one query column: gfx950 v_permlane32_swap / v_permlane16_swap (VALU) instead of
+// ds_bpermute round trips through the LDS pipe.
+MMT_DEV float lanegroup_max(float v) {
+    auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+    auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+MMT_DEV float lanegroup_sum(float v) {
+    auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+MMT_DEV void attn_wait_dyn(int n) {
+    switch (n) {
+        case 0: attn_wait_vm<0>(); break;
+        case 1: attn_wait_vm<1>(); break;
+        case 2: attn_wait_vm<2>(); break;
+        case 3: attn_wait_vm<3>(); break;
+        case 4: attn_wait_vm<4>(); break;
+        case 5: attn_wait_vm<5>(); break;
+        case 6: attn_wait_vm<6>(); break;
+        case 7: attn_wait_vm<7>(); break;
+        case 8: attn_wait_vm<8>(); break;
+        case 9: attn_wait_vm<9>(); break;
+        case 10: attn_wait_vm<10>(); break;
+        case 11: attn_wait_vm<11>(); break;
+        default: attn_wait_vm<12>(); break;
+    }
+}
+
+// KG key groups of 4 waves: the WG's 64 queries (16 per wave) are shared, the key tiles are dealt
+// round-robin over the groups (tile t -> group t % KG), each group keeps its own online-softmax
+// state, and the states are merged through LDS at the end.  At batch 1 the grid is ~216 WGs, one
+// per CU: splitting the keys puts 4*KG waves on the CU to hide the per-tile dependency chain
+// (LDS read -> MFMA -> max -> exp -> MFMA) that one wave per SIMD exposed in full.
+template <int KG>
+__global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(KG, KG))) void mam_attention_glds_kernel(
     const mmt_attn_params p) {
+    constexpr int NWV = 4 * KG, PPW = 16 / NWV;  // waves; K/V pieces per wave per tile
+    constexpr int R = ANS / KG;                    // rounds (KG tiles each) held by the ring
+    static_assert(R >= 2 && PPW >= 1, "ring geometry");
     __shared__ __attribute__((aligned(1024))) char lds[ANS * ATILE + 64 * 128];
     char* qimg = lds + ANS * ATILE;
+    MMT_ASTAMP(0, "s_memrealtime");
+    MMT_ASTAMP(1, "s_memtime");
 
     const int qb = blockIdx.x, h = blockIdx.y, s = blockIdx.z;
     const int n_t = p.n_t, ntok = p.ntok, C = p.C;
@@ -309,6 +362,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const int sV = s % p.Bm, sI = sV + p.Bm;
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int kg = w >> 2, qw = w & 3;  // key group, 16-query sub-block
     const int l16 = lane & 15, lg = lane >> 4;
     const int prow = lane >> 3, pcol = lane & 7;  // this lane's row / position in a 1-KiB piece
 
@@ -321,26 +375,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
         return qkv + ((int64_t)seq * ntok + row) * rs + h * D;
     };
-    // Tile kt into slot kt % ANS: wave w stages K pieces 2w, 2w+1 and V pieces 2w, 2w+1.
-    const int nkt = (Lk + KB - 1) / KB;
-    auto issue = [&](int kt) {
-        char* slot = lds + (kt % ANS) * ATILE;
+    const int nkt = (Lk + KB - 1) / KB, nr = (nkt + KG - 1) / KG;
+    // Tile t into slot t % ANS: its 16 pieces (8 K, 8 V) are dealt over the waves, PPW each.
+    auto issue_tile = [&](int t) {
+        char* slot = lds + (t % ANS) * ATILE;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int piece = 2 * w + i, r = piece * 8 + prow;  // r & 7 == prow
-            const bf16_t* src = key_row(min(kt * KB + r, Lk - 1));
-            attn_glds16(src + C + ((pcol ^ prow) * 8), slot + piece * 1024);
-            attn_glds16(src + 2 * C + ((pcol ^ (prow & 6)) * 8), slot + KB * 128 + piece * 1024);
+        for (int i = 0; i < PPW; ++i) {
+            const int piece = w * PPW + i, isv = piece >> 3, pk = piece & 7, r = pk * 8 + prow;
+            const bf16_t* src = key_row(min(t * KB + r, Lk - 1)) + (isv ? 2 * C : C);
+            const int sw = isv ? (pcol ^ (prow & 6)) : (pcol ^ prow);
+            attn_glds16(src + sw * 8, slot + isv * KB * 128 + pk * 1024);
         }
     };
-    // Q image: wave w stages pieces 2w, 2w+1 (rows past the block's end re-read the last query)
+    auto tiles_in = [&](int r) { return min(KG, nkt - r * KG); };  // valid tiles of round r
+    auto issue_round = [&](int r) {
+        for (int j = 0; j < tiles_in(r); ++j) issue_tile(r * KG + j);
+    };
+    // Q image: 8 pieces over the first 8 waves (rows past the block's end re-read the last query)
+    if (w < 8) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int piece = 2 * w + i, r = piece * 8 + prow;
-        const bf16_t* src = qkv + ((int64_t)s * ntok + min(q0 + r, qend - 1)) * rs + h * D;
-        attn_glds16(src + ((pcol ^ prow) * 8), qimg + piece * 1024);
+        for (int i = 0; i < (NWV >= 8 ? 1 : 8 / NWV); ++i) {
+            const int piece = NWV >= 8 ? w : w * (8 / NWV) + i, r = piece * 8 + prow;
+            const bf16_t* src = qkv + ((int64_t)s * ntok + min(q0 + r, qend - 1)) * rs + h * D;
+            attn_glds16(src + ((pcol ^ prow) * 8), qimg + piece * 1024);
+        }
     }
-    for (int kt = 0; kt < ANS - 1 && kt < nkt; ++kt) issue(kt);
+    for (int r = 0; r < R - 1 && r < nr; ++r) issue_round(r);
 
     const float cexp = p.scale * 1.4426950408889634f;
     float m_run = -1e30f, l_run = 0.f;
@@ -348,32 +408,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
     u32x4 qf[2];
+    const int qr = l16 >> 2, pc = l16 & 3;
 
-    for (int kt = 0; kt < nkt; ++kt) {
-        // this wave's DMA of tile kt (and of Q, issued first) has landed once at most `ahead`
-        // later tiles (4 instructions each) are outstanding
-        const int ahead = min(nkt - 1, kt + ANS - 2) - kt;
-        switch (ahead) {
-            case 0: attn_wait_vm<0>(); break;
-            case 1: attn_wait_vm<4>(); break;
-            case 2: attn_wait_vm<8>(); break;
-            case 3: attn_wait_vm<12>(); break;
-            case 4: attn_wait_vm<16>(); break;
-            case 5: attn_wait_vm<20>(); break;
-            default: attn_wait_vm<24>(); break;
-        }
-        lds_barrier();  // every wave's pieces of tile kt landed; every wave is done with tile kt-1
-        if (kt + ANS - 1 < nkt) issue(kt + ANS - 1);  // refills the slot tile kt-1 used
-        if (kt == 0) {
+    for (int r = 0; r < nr; ++r) {
+        // this wave's DMA of round r (and of Q, issued first) has landed once at most the pieces
+        // of the rounds issued after it are outstanding
+        int after = 0;
+        for (int r2 = r + 1; r2 <= min(nr - 1, r + R - 2); ++r2) after += PPW * tiles_in(r2);
+        attn_wait_dyn(after);
+        lds_barrier();  // every wave's pieces of round r landed; every wave is done with round r-1
+        if (r + R - 1 < nr) issue_round(r + R - 1);  // refills the slots of round r-1
+        if (r == 0) {
+            MMT_ASTAMP(2, "s_memtime");
 #pragma unroll
             for (int t = 0; t < 2; ++t)
-                qf[t] = *(const u32x4*)(qimg + ((16 * w + l16) * 8 + ((4 * t + lg) ^ (l16 & 7))) * 16);
+                qf[t] = *(const u32x4*)(qimg + ((16 * qw + l16) * 8 + ((4 * t + lg) ^ (l16 & 7))) * 16);
         }
+        const int kt = r * KG + kg;
+        if (kt >= nkt) continue;  // wave-uniform: this group has no tile in the last round
         const char* kimg = lds + (kt % ANS) * ATILE;
         const char* vimg = kimg + KB * 128;
         // V^T fragments for the PV product, issued first so they land behind the QK^T work:
         // vt[kk][dt] = keys 32kk + 4lg + qr (+16), d = dt*16 + 4pc..+3
-        const int qr = l16 >> 2, pc = l16 & 3;
         uint2 vt[2][4][2];
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
@@ -385,45 +441,47 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                 vt[kk][dt][1] = attn_tr16<16 * 128>(b1);
             }
         }
-
         // S^T tiles: sacc[kt16], lane: query l16, keys 16*kt16 + 4*lg + r
-        f32x4 sacc[4];
-#pragma unroll
-        for (int a = 0; a < 4; ++a) sacc[a] = f32x4{0.f, 0.f, 0.f, 0.f};
+        u32x4 kf[4][2];
 #pragma unroll
         for (int kt16 = 0; kt16 < 4; ++kt16)
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                const u32x4 kf = *(const u32x4*)(kimg + ((kt16 * 16 + l16) * 8 + ((4 * t + lg) ^ (l16 & 7))) * 16);
-                sacc[kt16] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kf),
+            for (int t = 0; t < 2; ++t)
+                kf[kt16][t] = *(const u32x4*)(kimg + ((kt16 * 16 + l16) * 8 + ((4 * t + lg) ^ (l16 & 7))) * 16);
+        f32x4 sacc[4];
+#pragma unroll
+        for (int kt16 = 0; kt16 < 4; ++kt16) {
+            sacc[kt16] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+                sacc[kt16] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kf[kt16][t]),
                                                                      __builtin_bit_cast(bf16x8, qf[t]), sacc[kt16], 0, 0, 0);
-            }
+        }
         if (kt * KB + KB > Lk) {  // mask the tail of the key range (clamped rows)
 #pragma unroll
             for (int kt16 = 0; kt16 < 4; ++kt16)
 #pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    if (kt * KB + kt16 * 16 + 4 * lg + r >= Lk) sacc[kt16][r] = -1e30f;
+                for (int j = 0; j < 4; ++j)
+                    if (kt * KB + kt16 * 16 + 4 * lg + j >= Lk) sacc[kt16][j] = -1e30f;
         }
         // online softmax (per query column)
         float mx = -1e30f;
 #pragma unroll
         for (int kt16 = 0; kt16 < 4; ++kt16)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) mx = fmaxf(mx, sacc[kt16][r]);
-        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+            for (int j = 0; j < 4; ++j) mx = fmaxf(mx, sacc[kt16][j]);
+        mx = lanegroup_max(mx);
         const float mnew = fmaxf(m_run, mx);
-        const float alpha = exp2f((m_run - mnew) * cexp);
+        const float alpha = __builtin_amdgcn_exp2f((m_run - mnew) * cexp);
         m_run = mnew;
         const float mc = mnew * cexp;
         float ls = 0.f;
 #pragma unroll
         for (int kt16 = 0; kt16 < 4; ++kt16)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float e = exp2f(sacc[kt16][r] * cexp - mc);
-                sacc[kt16][r] = e;
+            for (int j = 0; j < 4; ++j) {
+                const float e = __builtin_amdgcn_exp2f(sacc[kt16][j] * cexp - mc);
+                sacc[kt16][j] = e;
                 ls += e;
             }
         l_run = l_run * alpha + ls;
@@ -433,12 +491,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         attn_lds_wait();
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
-            bf16x8 pf;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                pf[j] = (__bf16)sacc[2 * kk][j];
-                pf[4 + j] = (__bf16)sacc[2 * kk + 1][j];
-            }
+            const bf16x8 pf = __builtin_bit_cast(
+                bf16x8, u32x4{pack_bf16x2(sacc[2 * kk][0], sacc[2 * kk][1]), pack_bf16x2(sacc[2 * kk][2], sacc[2 * kk][3]),
+                              pack_bf16x2(sacc[2 * kk + 1][0], sacc[2 * kk + 1][1]),
+                              pack_bf16x2(sacc[2 * kk + 1][2], sacc[2 * kk + 1][3])});
 #pragma unroll
             for (int dt = 0; dt < 4; ++dt) {
                 const uint2 ua = vt[kk][dt][0], ub = vt[kk][dt][1];
@@ -447,13 +503,44 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             }
         }
     }
+    MMT_ASTAMP(3, "s_memtime");
+
+    // ---- merge the key groups' states (m, partial l, O) through LDS, group 0 finishes
+    if constexpr (KG > 1) {
+        float* mg = (float*)lds;  // [KG][4 waves][64 lanes][20]: m, l, -, -, O (16-B aligned)
+        constexpr int ST = 20;
+        lds_barrier();                           // ring no longer read by anyone
+        float* mine = mg + ((kg * 4 + qw) * 64 + lane) * ST;
+        if (kg > 0) {
+            mine[0] = m_run;
+            mine[1] = l_run;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) *(f32x4*)(mine + 4 + 4 * dt) = o[dt];
+        }
+        lds_barrier();
+        if (kg > 0) return;
+        float mall = m_run;
+#pragma unroll
+        for (int g2 = 1; g2 < KG; ++g2) mall = fmaxf(mall, mg[((g2 * 4 + qw) * 64 + lane) * ST]);
+        const float a0 = __builtin_amdgcn_exp2f((m_run - mall) * cexp);
+        l_run *= a0;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[dt] *= a0;
+#pragma unroll
+        for (int g2 = 1; g2 < KG; ++g2) {
+            const float* src = mg + ((g2 * 4 + qw) * 64 + lane) * ST;
+            const float ag = __builtin_amdgcn_exp2f((src[0] - mall) * cexp);
+            l_run += src[1] * ag;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) o[dt][j] += src[4 + 4 * dt + j] * ag;
+        }
+    }
 
     // ---- normalise and store: lane holds O[q = l16][d = dt*16 + 4*lg + r]
-    float l = l_run;
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
-    const float inv = 1.f / l;
-    const int q = q0 + 16 * w + l16;
+    const float inv = 1.f / lanegroup_sum(l_run);
+    const int q = q0 + 16 * qw + l16;
     if (q < qend) {
         bf16_t* op = (bf16_t*)p.out + ((int64_t)s * ntok + q) * C + h * D;
 #pragma unroll
@@ -461,17 +548,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             *(uint2*)(op + dt * 16 + 4 * lg) =
                 make_uint2(pack_bf16x2(o[dt][0] * inv, o[dt][1] * inv), pack_bf16x2(o[dt][2] * inv, o[dt][3] * inv));
     }
+#if MMT_STAMP_BUILD
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    MMT_ASTAMP(4, "s_memtime");
+    MMT_ASTAMP(5, "s_memrealtime");
 }
 
 template <typename T>
 int launch_attn(const mmt_attn_params& p, hipStream_t st) {
+    if (p.impl != 0 && p.impl != 2 && p.impl != 4) return MMT_EBADARG;
     if (!p.qkv || !p.out || p.H <= 0 || p.C != p.H * D || p.S <= 0 || p.ntok <= p.n_t || p.n_t <= 0) return MMT_EBADARG;
     if (p.asym && (p.Bm <= 0 || p.S != 2 * p.Bm)) return MMT_EBADARG;
     if (((uintptr_t)p.qkv | (uintptr_t)p.out) & 15) return MMT_EBADARG;
     const int nqb = (p.n_t + 63) / 64 + (p.ntok - p.n_t + 63) / 64;
     dim3 grid(nqb, p.H, p.S);
-    if constexpr (sizeof(T) == 2) {  // bf16: LDS-DMA kernel, 4 waves x 16 queries per workgroup
-        hipLaunchKernelGGL(mam_attention_glds_kernel, grid, dim3(256), 0, st, p);
+    if constexpr (sizeof(T) == 2) {  // bf16: LDS-DMA kernel, 64 queries x KG key groups per workgroup
+        const int kg = p.impl > 0 ? p.impl : 4;
+        if (kg == 2) hipLaunchKernelGGL(mam_attention_glds_kernel<2>, grid, dim3(512), 0, st, p);
+        else hipLaunchKernelGGL(mam_attention_glds_kernel<4>, grid, dim3(1024), 0, st, p);
     } else {  // fp32 (parity path); small grids: 4 waves x 16 queries to occupy more SIMDs
         if ((int64_t)nqb * p.H * p.S < 1024) hipLaunchKernelGGL((mam_attention_kernel<T, 1>), grid, dim3(256), 0, st, p);
         else hipLaunchKernelGGL((mam_attention_kernel<T, 2>), grid, dim3(128), 0, st, p);

@@ -90,5 +90,22 @@ MMT_DEV void lds_barrier() {
     asm volatile("s_barrier" ::: "memory");
 }
 
+// Measurement builds only (tools/build_ablate.sh, MMT_STAMP_BUILD=1): the leader thread of each
+// workgroup records clock stamps into a per-kernel __device__ array, read back by an exported
+// mmt_*_stamps() (tools/gemm_stamps.py, tools/attn_stamps.py).  Compiled out of the product.
+#ifndef MMT_STAMP_BUILD
+#define MMT_STAMP_BUILD 0
+#endif
+#if MMT_STAMP_BUILD
+#define MMT_STAMP_AT(BUF, I, INSN)                                                                  \
+    if (threadIdx.x == 0) {                                                                        \
+        unsigned long long t_;                                                                     \
+        asm volatile(INSN " %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                      \
+        BUF[(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 6 + (I)] = t_;       \
+    }
+#else
+#define MMT_STAMP_AT(BUF, I, INSN)
+#endif
+
 static inline int hip_status(hipError_t e) { return e == hipSuccess ? 0 : -(int)e; }
 static inline int launch_status() { return hip_status(hipGetLastError()); }

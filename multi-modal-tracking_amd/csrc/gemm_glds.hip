@@ -28,25 +28,14 @@
 #define MMT_GEMM_ABLATE 0
 #endif
 
-// MMT_GEMM_STAMP (measurement builds only, tools/build_ablate.sh): workgroup-leader timestamps
-// per phase, read back with mmt_gemm_stamps() (tools/gemm_stamps.py).
-#ifndef MMT_GEMM_STAMP
-#define MMT_GEMM_STAMP 0
-#endif
-#if MMT_GEMM_STAMP
+// Stamp build (MMT_STAMP_BUILD): per-phase workgroup timestamps, read with mmt_gemm_stamps().
+#if MMT_STAMP_BUILD
 __device__ unsigned long long g_mmt_stamps[16384 * 6];
-#define MMT_STAMP(I, INSN)                                                                          \
-    if (threadIdx.x == 0) {                                                                        \
-        unsigned long long t_;                                                                     \
-        asm volatile(INSN " %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                      \
-        g_mmt_stamps[(blockIdx.x + gridDim.x * blockIdx.z) * 6 + (I)] = t_;                        \
-    }
 extern "C" int mmt_gemm_stamps(unsigned long long* host, int n) {
     return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_mmt_stamps), sizeof(unsigned long long) * n);
 }
-#else
-#define MMT_STAMP(I, INSN)
 #endif
+#define MMT_STAMP(I, INSN) MMT_STAMP_AT(g_mmt_stamps, I, INSN)
 
 namespace {
 
@@ -323,7 +312,7 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
             }
         }
     }
-#if MMT_GEMM_STAMP
+#if MMT_STAMP_BUILD
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
     MMT_STAMP(4, "s_memtime");

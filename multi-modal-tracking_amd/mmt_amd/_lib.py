@@ -38,7 +38,7 @@ class GemmParams(ctypes.Structure):
 
 class AttnParams(ctypes.Structure):
     _fields_ = [("qkv", vp), ("out", vp), ("S", i32), ("Bm", i32), ("ntok", i32), ("n_t", i32), ("C", i32),
-                ("H", i32), ("asym", i32), ("scale", f32)]
+                ("H", i32), ("asym", i32), ("scale", f32), ("impl", i32)]
 
 
 _PROTOS = {

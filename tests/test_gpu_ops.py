@@ -202,10 +202,12 @@ def _attn_ref(qkv, S, Bm, ntok, n_t, C, H, asym):
     return out.permute(0, 2, 1, 3).reshape(S, ntok, C)
 
 
-@pytest.mark.parametrize("dname", ["f32", "bf16"])
+@pytest.mark.parametrize("dname,impl", [("f32", 0), ("bf16", 2), ("bf16", 4)])
 @pytest.mark.parametrize("asym", [0, 1])
-@pytest.mark.parametrize("Bm,ntok,n_t,H", [(1, 528, 128, 12), (2, 100, 36, 2), (1, 70, 8, 1)])
-def test_mam_attention(dname, asym, Bm, ntok, n_t, H):
+@pytest.mark.parametrize("Bm,ntok,n_t,H", [(1, 528, 128, 12), (2, 100, 36, 2), (1, 70, 8, 1), (1, 864, 288, 2)])
+def test_mam_attention(dname, impl, asym, Bm, ntok, n_t, H):
+    """impl = key groups of the bf16 kernel (2 / 4); (1, 864, 288) is the ViT-L 192/384 shape
+    (14 / 18 key tiles: more tiles than ring slots)."""
     dt = DT[dname]
     L = _lib()
     S, C = 2 * Bm, 64 * H
@@ -215,6 +217,7 @@ def test_mam_attention(dname, asym, Bm, ntok, n_t, H):
     out = torch.empty(S, ntok, C, device="cuda", dtype=dt)
     p = L.AttnParams()
     p.qkv, p.out, p.S, p.Bm, p.ntok, p.n_t, p.C, p.H, p.asym, p.scale = qd.data_ptr(), out.data_ptr(), S, Bm, ntok, n_t, C, H, asym, 0.125
+    p.impl = impl
     L.check(L.LIB.mmt_mam_attention(p, L.MMT_BF16 if dt == torch.bfloat16 else L.MMT_F32,
                                     torch.cuda.current_stream().cuda_stream), "attn")
     torch.cuda.synchronize()
@@ -223,21 +226,26 @@ def test_mam_attention(dname, asym, Bm, ntok, n_t, H):
     assert err <= (1.5e-2 if dt == torch.bfloat16 else 2e-5), err
 
 
-def test_mam_attention_rescale_branch():
-    """Online-softmax rescale forced: one key per query block carries a huge score in a late tile."""
+@pytest.mark.parametrize("dname,impl", [("f32", 0), ("bf16", 2), ("bf16", 4)])
+def test_mam_attention_rescale_branch(dname, impl):
+    """Online-softmax rescale forced: one key per query block carries a huge score in a late tile
+    (bf16: and in a different key group than the first tile, so the group merge rescales)."""
+    dt = DT[dname]
     L = _lib()
     S, Bm, ntok, n_t, H, C = 2, 1, 528, 128, 1, 64
     g = torch.Generator().manual_seed(9)
     qkv = torch.randn(S, ntok, 3 * C, generator=g) * 0.5
     qkv[:, 500, C:2 * C] = qkv[:, 300, :C] * 6  # key 500 aligned with query 300
-    qd = qkv.cuda()
-    out = torch.empty(S, ntok, C, device="cuda")
+    qd = qkv.to(dt).cuda()
+    out = torch.empty(S, ntok, C, device="cuda", dtype=dt)
     p = L.AttnParams()
     p.qkv, p.out, p.S, p.Bm, p.ntok, p.n_t, p.C, p.H, p.asym, p.scale = qd.data_ptr(), out.data_ptr(), S, Bm, ntok, n_t, C, H, 0, 0.125
-    L.check(L.LIB.mmt_mam_attention(p, L.MMT_F32, torch.cuda.current_stream().cuda_stream), "attn")
+    p.impl = impl
+    L.check(L.LIB.mmt_mam_attention(p, L.MMT_BF16 if dt == torch.bfloat16 else L.MMT_F32,
+                                    torch.cuda.current_stream().cuda_stream), "attn")
     torch.cuda.synchronize()
-    ref = _attn_ref(qkv.double(), S, Bm, ntok, n_t, C, H, 0).float()
-    assert (out.cpu() - ref).abs().max().item() < 5e-5
+    ref = _attn_ref(qkv.to(dt).double(), S, Bm, ntok, n_t, C, H, 0).float()
+    assert (out.float().cpu() - ref).abs().max().item() < (1.5e-2 if dt == torch.bfloat16 else 5e-5)
 
 
 @pytest.mark.parametrize("dname", ["f32", "bf16"])

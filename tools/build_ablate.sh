@@ -2,7 +2,7 @@
 # Measurement-only variants of libmmt_hip.so (never the product):
 #   ablate1: LDS-DMA GEMM K loop without DMA after the prologue (MMT_GEMM_ABLATE=1)
 #   ablate2: LDS-DMA GEMM K loop without MFMA work          (MMT_GEMM_ABLATE=2)
-#   stamp:   LDS-DMA GEMM with per-phase workgroup timestamps (MMT_GEMM_STAMP=1)
+#   stamp:   per-phase workgroup timestamps in the GEMM / attention kernels (MMT_STAMP_BUILD=1)
 # Use with MMT_HIP_LIB=multi-modal-tracking_amd/mmt_amd/_lib/<variant>/libmmt_hip.so.
 set -e
 cd "$(dirname "$0")/../multi-modal-tracking_amd/csrc"
@@ -12,4 +12,4 @@ build() {
 }
 build ablate1 -DMMT_GEMM_ABLATE=1
 build ablate2 -DMMT_GEMM_ABLATE=2
-build stamp -DMMT_GEMM_STAMP=1
+build stamp -DMMT_STAMP_BUILD=1
