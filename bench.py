@@ -1,16 +1,23 @@
 #!/usr/bin/env python3
 """Tracker FPS benchmark of the MI355X MixFormer RGB-T forward path (BASELINE.json `metric`).
 
-A step = one template+search forward (both modalities, boxes out) of B frames per GPU on
-synthetic inputs resident in HBM (fresh frames rotated from a pool each step, copied into the
-static input buffers), replayed as one hipGraph.  N>1: one process per GPU (torchrun), each an
-independent replica tracking its own sequences ("replicas only": the path has no exchange step),
-so scaling is weak and value = frames of all ranks / max-over-ranks time.
+A step = one template+search forward (both modalities, boxes out) of B frames per GPU on synthetic
+inputs resident in HBM.  Four distinct input sets are rotated; each has its own captured hipGraph
+whose patch-staging kernel reads that set in place, so a step is one graph replay.  N>1: one
+process per GPU (torchrun), each an independent replica tracking its own sequences ("replicas
+only": the path has no exchange step), so scaling is weak and value = frames of all ranks /
+max-over-ranks time.
 
-Extra fields: `roofline` for the kernel with the largest share of device time and `roofline_mam`
-for the MAM attention kernel (algorithmic FLOPs per launch / average launch time measured with HIP
-events in an eager pass over the same plan), and `cpu_baseline` = the oracle's fp32 CPU forward
-(oracle/forward.py, a restatement of the reference) on a bounded sample, rank 0 at N=1 only.
+Extra fields:
+  kernels        device time per launch of every plan entry (graph-replayed back-to-back launches
+                 timed with HIP events on the launch stream, after the timed region)
+  roofline       the kernel with the largest share of device time: algorithmic FLOPs per launch /
+                 that average launch time; `traffic` = HBM bytes per launch from the PMC pass in
+                 profiles/pmc_traffic.json (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction) when it
+                 was measured for this workload, else null
+  roofline_mam   the same for the MAM attention kernel
+  cpu_baseline   the oracle's fp32 CPU forward (oracle/forward.py, a restatement of the reference)
+                 on a bounded sample, rank 0 at N=1 only
 """
 import argparse
 import json
@@ -50,25 +57,45 @@ def plan_flops(rt, entry):
     return 4.0 * 64 * keep.H * keep.S * (d.n_t * d.n_t + d.ns * lk_s)
 
 
-def kernel_profile(rt, plan, reps=20):
-    """Average device time per plan entry, HIP events around each launch on the launch stream."""
+def kernel_profile(rt, plan, per_graph=20, replays=5):
+    """Average device time per launch of each plan entry name: `per_graph` back-to-back launches of
+    the name's first entry captured in one hipGraph on the launch stream and replayed, timed with
+    HIP events on that stream (launch gaps excluded, as in a rocprofv3 kernel trace).  Run after
+    the timed region: repeated in-place launches leave the workspace scrambled."""
     s = torch.cuda.current_stream()
-    n = len(plan)
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(n + 1)] for _ in range(reps)]
-    for r in range(reps):
-        for i, (fn, args, name, _) in enumerate(plan):
-            ev[r][i].record(s)
-            fn(*args, s.cuda_stream)
-        ev[r][n].record(s)
-    torch.cuda.synchronize()
-    tot = [0.0] * n
-    for r in range(reps):
-        for i in range(n):
-            tot[i] += ev[r][i].elapsed_time(ev[r][i + 1])
-    return [t / reps for t in tot]  # ms per launch
+    first = {}
+    for e in plan:
+        first.setdefault(e[2], e)
+    per_name = {}
+    for nm, (fn, args, _, _) in first.items():
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(per_graph):
+                fn(*args, torch.cuda.current_stream().cuda_stream)
+        g.replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(replays):
+            g.replay()
+        e1.record(s)
+        torch.cuda.synchronize()
+        per_name[nm] = e0.elapsed_time(e1) / (replays * per_graph)
+        del g
+    return [per_name[e[2]] for e in plan]  # ms per launch
 
 
-def roofline(rt, plan, times, dtype):
+def load_traffic(variant, B, dtype):
+    """HBM bytes per launch by plan-entry name, from the committed PMC pass (tools/pmc_traffic.py)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get("%s/B%d/%s" % (variant, B, dtype), {})
+    except (OSError, ValueError):
+        return {}
+
+
+def roofline(rt, plan, times, dtype, traffic=None):
+    traffic = traffic or {}
     by = {}
     for e, t in zip(plan, times):
         nm = e[2]
@@ -83,8 +110,10 @@ def roofline(rt, plan, times, dtype):
         a = by[nm]
         avg_ms = a["t"] / a["n"]
         ach = (a["flops"] / a["n"]) / (avg_ms * 1e-3) / 1e12
+        tb = traffic.get(nm, {}).get("traffic_bytes")
         return {"kernel": nm, "bound": "mfma", "achieved": round(ach, 2), "peak": PEAK[dtype], "unit": "TFLOP/s",
-                "frac": round(ach / PEAK[dtype], 4), "traffic": None, "avg_launch_us": round(avg_ms * 1e3, 2),
+                "frac": round(ach / PEAK[dtype], 4), "traffic": tb, "traffic_unit": "bytes/launch (HBM, PMC)",
+                "flops_per_launch": a["flops"] / a["n"], "avg_launch_us": round(avg_ms * 1e3, 2),
                 "launches_per_step": a["n"], "share_of_device_time": round(a["t"] / total, 4)}
 
     return obj(dom), obj("mam_attention"), total, by
@@ -121,6 +150,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--gemm-impl", type=int, default=0, help="mmt_gemm_params.impl for every GEMM (A/B)")
+    ap.add_argument("--no-kernel-profile", action="store_true",
+                    help="skip the per-kernel timing (profiler runs that map dispatches to plan entries)")
     ap.add_argument("--dump-plan", default=None, help="write the plan's launch names (JSON) to this path")
     args = ap.parse_args()
 
@@ -180,8 +211,12 @@ def main():
     if args.dump_plan and rank == 0:
         with open(args.dump_plan, "w") as f:
             json.dump([e[2] for e in plan], f)
-    times = kernel_profile(rt, plan)
-    dom, mam, dev_ms, by = roofline(rt, plan, times, args.dtype)
+    if args.no_kernel_profile:
+        dom = mam = by = None
+        dev_ms = None
+    else:
+        times = kernel_profile(rt, plan)
+        dom, mam, dev_ms, by = roofline(rt, plan, times, args.dtype, load_traffic(args.variant, B, args.dtype))
 
     if rank == 0:
         frames = world * B * args.steps
@@ -195,10 +230,10 @@ def main():
                        "variant": args.variant, "batch_per_gpu": B, "template": 128, "search": 320,
                        "parallelism": "replicas" if world > 1 else "single", "hip_graph": use_graph},
             "roofline": dom, "roofline_mam": mam,
-            "device_ms_per_step_eager": round(dev_ms, 4), "launches_per_step": len(plan),
+            "device_ms_per_step_sum": round(dev_ms, 4) if dev_ms else None, "launches_per_step": len(plan),
             "kernels": {k: {"us": round(a["t"] * 1e3 / a["n"], 2), "n": a["n"],
                             "tflops": round(a["flops"] / a["n"] / (a["t"] / a["n"] * 1e-3) / 1e12, 1) if a["flops"] else None}
-                        for k, a in sorted(by.items(), key=lambda kv: -kv[1]["t"])},
+                        for k, a in sorted(by.items(), key=lambda kv: -kv[1]["t"])} if by else None,
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.variant, B)

@@ -61,8 +61,14 @@ MMT_DEV void wait_stages(int ahead) {
     else wait_vm<(ST >= 4 ? 3 * L : L)>();
 }
 
-// WGM x WGN waves per k-group own WM x WN sub-tiles; KS k-groups split the K-steps.
-template <int BM, int BN, int WGM, int WGN, int KS, int ST>
+// Zero source for A chunks outside the operand: conv padding taps and the K tail past K (a glds
+// lane cannot zero its LDS bytes, so it loads zeros instead).
+__device__ __attribute__((aligned(64))) const uint32_t g_zero_chunk[16] = {0};
+
+// WGM x WGN waves per k-group own WM x WN sub-tiles; KS k-groups split the K-steps.  CONV: A is
+// the implicit im2col of an NHWC 3x3/pad-1 (conv_k3) or 1x1 convolution, input read through the
+// nearest-upsample index map (gemm.hip's conv mode).
+template <int BM, int BN, int WGM, int WGN, int KS, int ST, bool CONV>
 __global__ __launch_bounds__(64 * WGM * WGN * KS)
     __attribute__((amdgpu_waves_per_eu(WGM * WGN * KS / 4, WGM * WGN * KS / 4))) void gemm_glds_kernel(
         const mmt_gemm_params p) {
@@ -101,31 +107,64 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
     // This lane stages row (piece*8 + prow), logical chunk pch, into byte 16*lane of the piece:
     // position (lane & 7) of row prow holds chunk (lane & 7) ^ prow  (the read-side XOR).
     const int prow = lane >> 3, pch = (lane & 7) ^ prow;
-    int64_t aoff[PA], boff[PB];
-    const int segr = (int)p.a_seg_rows, sega = (int)p.a_segs_a;
+    int64_t aoff[PA], boff[PB];  // GEMM: row offset of A; conv: input-image base pixel
+    int ay[PA], ax[PA];           // conv: output pixel of the row
+    const int ch = p.conv_h, cup = CONV ? p.conv_up : 1, hi = CONV ? p.conv_h / cup : 0;
+    if constexpr (!CONV) {
+        const int segr = (int)p.a_seg_rows, sega = (int)p.a_segs_a;
 #pragma unroll
-    for (int i = 0; i < PA; ++i) {
-        const int m = min(m0 + (wid * PA + i) * 8 + prow, M - 1);
-        const int seg = m / segr, sa = seg % sega;  // 32-bit: the launcher checks the ranges
-        aoff[i] = sa * p.a_stride_a + (int64_t)((seg - sa) / sega) * p.a_stride_b + (int64_t)(m - seg * segr) * p.lda +
-                  pch * 8;
+        for (int i = 0; i < PA; ++i) {
+            const int m = min(m0 + (wid * PA + i) * 8 + prow, M - 1);
+            const int seg = m / segr, sa = seg % sega;  // 32-bit: the launcher checks the ranges
+            aoff[i] = sa * p.a_stride_a + (int64_t)((seg - sa) / sega) * p.a_stride_b + (int64_t)(m - seg * segr) * p.lda;
+            ay[i] = ax[i] = 0;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < PA; ++i) {
+            const int m = min(m0 + (wid * PA + i) * 8 + prow, M - 1);
+            const int b = m / (ch * ch), rem = m - b * ch * ch;
+            ay[i] = rem / ch;
+            ax[i] = rem - ay[i] * ch;
+            aoff[i] = (int64_t)b * hi * hi;
+        }
     }
 #pragma unroll
-    for (int i = 0; i < PB; ++i) boff[i] = (int64_t)min(n0 + (wid * PB + i) * 8 + prow, N - 1) * K + pch * 8;
-    const int ks = p.k_split;
+    for (int i = 0; i < PB; ++i) boff[i] = (int64_t)min(n0 + (wid * PB + i) * 8 + prow, N - 1) * K;
+    const int ks = p.k_split, cin = p.conv_cin, k3 = p.conv_k3;
 
     unsigned char* ring = lds + kg * ST * STAGE;
-    const int nk = K / KT, ns = (nk + KS - 1) / KS;
+    const int nk = (K + KT - 1) / KT, ns = (nk + KS - 1) / KS;
 
     auto issue = [&](int s) {  // this k-group's step s -> ring slot s % ST
-        const int k0 = min(s * KS + kg, nk - 1) * KT;
+        const int k = min(s * KS + kg, nk - 1) * KT + pch * 8;  // this lane's 8-element chunk
+        const bool kin = k < K;
         unsigned char* base = ring + (s % ST) * STAGE;
-        const bool hp = ks > 0 && k0 + pch * 8 >= ks;
-        const bf16_t* ab = hp ? A1 - ks : A0;
+        if constexpr (!CONV) {
+            const bool hp = ks > 0 && k >= ks;
+            const bf16_t* ab = (hp ? A1 - ks : A0) + k;
 #pragma unroll
-        for (int i = 0; i < PA; ++i) glds16(ab + aoff[i] + k0, base + (wid * PA + i) * 1024);
+            for (int i = 0; i < PA; ++i)
+                glds16(kin ? (const void*)(ab + aoff[i]) : (const void*)g_zero_chunk, base + (wid * PA + i) * 1024);
+        } else {
+            int dy = 0, dx = 0, ci = k;
+            if (k3) {  // k = (ky*3 + kx)*cin + ci
+                const int tap = k / cin;
+                ci = k - tap * cin;
+                dy = tap / 3 - 1;
+                dx = tap - (tap / 3) * 3 - 1;
+            }
 #pragma unroll
-        for (int i = 0; i < PB; ++i) glds16(W + boff[i] + k0, base + BM * 128 + (wid * PB + i) * 1024);
+            for (int i = 0; i < PA; ++i) {
+                const int iy = ay[i] + dy, ix = ax[i] + dx;
+                const bool ok = kin && iy >= 0 && ix >= 0 && iy < ch && ix < ch;
+                const bf16_t* src = A0 + (aoff[i] + (int64_t)(iy / cup) * hi + ix / cup) * p.lda + ci;
+                glds16(ok ? (const void*)src : (const void*)g_zero_chunk, base + (wid * PA + i) * 1024);
+            }
+        }
+        const int kw = kin ? k : 0;  // past K: any in-bounds W bytes (they meet zero A chunks)
+#pragma unroll
+        for (int i = 0; i < PB; ++i) glds16(W + boff[i] + kw, base + BM * 128 + (wid * PB + i) * 1024);
     };
 
     f32x4 acc[NT][MT];  // acc[nt][mt] = (C^T) fragment: rows n, columns m
@@ -322,8 +361,12 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
 template <int BM, int BN, int WGM, int WGN, int KS, int ST>
 void launch(const mmt_gemm_params& p, hipStream_t st) {
     const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, KS, ST>), dim3(tiles, 1, p.groups),
-                       dim3(64 * WGM * WGN * KS), 0, st, p);
+    if (p.conv_h > 0)
+        hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, KS, ST, true>), dim3(tiles, 1, p.groups),
+                           dim3(64 * WGM * WGN * KS), 0, st, p);
+    else
+        hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, KS, ST, false>), dim3(tiles, 1, p.groups),
+                           dim3(64 * WGM * WGN * KS), 0, st, p);
 }
 
 bool aligned(const void* ptr, int bytes) { return ((uintptr_t)ptr & (uintptr_t)(bytes - 1)) == 0; }
@@ -333,7 +376,7 @@ bool aligned(const void* ptr, int bytes) { return ((uintptr_t)ptr & (uintptr_t)(
 // Returns 1 when the shape / layout is not one this kernel takes (caller uses gemm.hip's kernel).
 int mmt_gemm_glds_bf16(const mmt_gemm_params& p, hipStream_t st, int force) {
     if (force < 0) return 1;
-    if (p.conv_h > 0 || p.K % 64 || p.N % 8 || p.ldc % 8 || (p.r[0] && p.ldr % 8)) return 1;
+    if (p.K % 8 || p.N % 8 || p.ldc % 8 || (p.r[0] && p.ldr % 8)) return 1;
     if (p.lda % 8 || p.a_stride_a % 8 || p.a_stride_b % 8 || p.k_split % 8) return 1;
     if (p.a_seg_rows > INT32_MAX || p.a_segs_a > INT32_MAX) return 1;
     for (int g = 0; g < p.groups; ++g) {
@@ -342,15 +385,22 @@ int mmt_gemm_glds_bf16(const mmt_gemm_params& p, hipStream_t st, int force) {
         if (p.r[g] && !aligned(p.r[g], 16)) return 1;
     }
     auto blocks = [&](int bm, int bn) { return (int64_t)((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn) * p.groups; };
-    const int nk = p.K / 64;
+    const int nk = (p.K + 63) / 64;
     int cfg = force;
     if (cfg == 0) {
-        // measured at batch 1 (tools/gemm_ab.py, tools/gemm_stamps.py): 128x128 / 8 waves once the
-        // grid has >= 128 tiles (qkv, fc1); below that (N = 768: proj, fc2) 64x64 with the K steps
-        // split over two wave groups, which keeps ~216 CUs streaming.
-        if (blocks(128, 128) >= 128) cfg = 1;
-        else if (nk >= 4) cfg = 3;
-        else return 1;
+        // Cost model fitted to in-kernel stamps at batch 1 (tools/gemm_stamps.py): one workgroup per
+        // CU (>= 128 KiB of LDS each), so time ~ rounds of 256 workgroups x (fixed prologue +
+        // epilogue + K-steps per workgroup x time per step).  Per-step times are per-CU LDS-fill
+        // bound: 128x128 (32 KiB/step) ~0.52 us, 128x64 with 2 k-groups ~0.52 us per pair of
+        // steps, 64x64 with 2 k-groups ~0.33 us per pair.
+        struct Cand { int cfg, bm, bn, ks; float fixed_us, step_us; };
+        const Cand cands[3] = {{1, 128, 128, 1, 6.0f, 0.52f}, {2, 128, 64, 2, 5.0f, 0.52f}, {3, 64, 64, 2, 3.2f, 0.33f}};
+        float best = 1e30f;
+        for (const Cand& c : cands) {
+            const int64_t wg = blocks(c.bm, c.bn);
+            const float t = (float)((wg + 255) / 256) * (c.fixed_us + (float)((nk + c.ks - 1) / c.ks) * c.step_us);
+            if (t < best) best = t, cfg = c.cfg;
+        }
     }
     switch (cfg) {
         case 1: launch<128, 128, 2, 4, 1, 4>(p, st); break;

@@ -88,33 +88,81 @@ __global__ __launch_bounds__(256) void corner_score_kernel(const T* __restrict__
 }
 
 // softmax over each fh x fh map + expectation of the coordinate grids; one workgroup per frame.
-__global__ __launch_bounds__(256) void softargmax_kernel(const float* __restrict__ maps, float* __restrict__ cxcywh,
-                                                         float* __restrict__ xyxy, float* __restrict__ rois,
-                                                         float roi_scale, int B, int fh, int stride) {
-    __shared__ float red[4];
-    const int b = blockIdx.x;
+// One 1024-thread block per frame handles both corner maps.  All map reads are issued up front
+// (independent, unrolled: SA_PER per thread per map) so the kernel pays one memory round trip, not
+// one per strided-loop iteration (the 256-thread loop version took ~20 us at batch 1).
+constexpr int SA_NT = 1024, SA_PER = 8;  // fh*fh <= SA_NT*SA_PER (80x80 = 6400 at 320/4)
+__global__ __launch_bounds__(SA_NT) void softargmax_kernel(const float* __restrict__ maps, float* __restrict__ cxcywh,
+                                                           float* __restrict__ xyxy, float* __restrict__ rois,
+                                                           float roi_scale, int B, int fh, int stride) {
+    __shared__ float red[2][3][SA_NT / 64];
+    __shared__ float mred[2][SA_NT / 64];
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int np = fh * fh;
-    float res[4];
+    float v[2][SA_PER];
+#pragma unroll
     for (int g = 0; g < 2; ++g) {
         const float* m = maps + ((int64_t)g * B + b) * np;
-        float mx = -INFINITY;
-        for (int p = threadIdx.x; p < np; p += 256) mx = fmaxf(mx, m[p]);
-        mx = block_max<256>(mx, red);
-        float se = 0.f, sx = 0.f, sy = 0.f;
-        for (int p = threadIdx.x; p < np; p += 256) {
-            const float e = expf(m[p] - mx);
-            se += e;
-            sx += e * (float)(stride * (p % fh));
-            sy += e * (float)(stride * (p / fh));
+#pragma unroll
+        for (int i = 0; i < SA_PER; ++i) {
+            const int p = tid + SA_NT * i;
+            v[g][i] = m[min(p, np - 1)];  // clamped read, masked below
         }
-        se = block_sum<256>(se, red);
-        sx = block_sum<256>(sx, red);
-        sy = block_sum<256>(sy, red);
-        const float img = (float)(fh * stride);
-        res[2 * g] = (sx / se) / img;
-        res[2 * g + 1] = (sy / se) / img;
     }
-    if (threadIdx.x == 0) {
+    float mx[2];
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        float t = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < SA_PER; ++i)
+            if (tid + SA_NT * i < np) t = fmaxf(t, v[g][i]);
+        t = wave_max(t);
+        if (lane == 0) mred[g][w] = t;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        float t = mred[g][0];
+#pragma unroll
+        for (int i = 1; i < SA_NT / 64; ++i) t = fmaxf(t, mred[g][i]);
+        mx[g] = t;
+    }
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        float se = 0.f, sx = 0.f, sy = 0.f;
+#pragma unroll
+        for (int i = 0; i < SA_PER; ++i) {
+            const int p = tid + SA_NT * i;
+            if (p < np) {
+                const float e = expf(v[g][i] - mx[g]);
+                se += e;
+                sx += e * (float)(stride * (p % fh));
+                sy += e * (float)(stride * (p / fh));
+            }
+        }
+        se = wave_sum(se);
+        sx = wave_sum(sx);
+        sy = wave_sum(sy);
+        if (lane == 0) {
+            red[g][0][w] = se;
+            red[g][1][w] = sx;
+            red[g][2][w] = sy;
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        float res[4];
+        const float img = (float)(fh * stride);
+        for (int g = 0; g < 2; ++g) {
+            float se = 0.f, sx = 0.f, sy = 0.f;
+            for (int i = 0; i < SA_NT / 64; ++i) {
+                se += red[g][0][i];
+                sx += red[g][1][i];
+                sy += red[g][2][i];
+            }
+            res[2 * g] = (sx / se) / img;
+            res[2 * g + 1] = (sy / se) / img;
+        }
         if (xyxy) {
             xyxy[b * 4 + 0] = res[0]; xyxy[b * 4 + 1] = res[1];
             xyxy[b * 4 + 2] = res[2]; xyxy[b * 4 + 3] = res[3];
@@ -243,7 +291,7 @@ extern "C" int mmt_corner_softargmax(const void* x4, const float* w5, const floa
                                      float roi_scale, int B, int fh, int c4, int stride, int dtype, void* stream) {
     const int epc = dtype == MMT_BF16 ? 8 : 4;
     if (!x4 || !w5 || !b5 || !a3 || !a4 || !score_maps || !boxes_cxcywh || B <= 0 || fh <= 0 || fh % 4 || c4 <= 0 ||
-        c4 % epc)
+        c4 % epc || fh * fh > SA_NT * SA_PER)
         return MMT_EBADARG;
     hipStream_t st = (hipStream_t)stream;
     dim3 grid((unsigned)(((int64_t)B * fh * fh + 255) / 256), 2);
@@ -254,7 +302,7 @@ extern "C" int mmt_corner_softargmax(const void* x4, const float* w5, const floa
         hipLaunchKernelGGL(corner_score_kernel<float>, grid, dim3(256), 0, st, (const float*)x4, w5, b5, a3, a4,
                            score_maps, B, fh, c4);
     else return MMT_EBADARG;
-    hipLaunchKernelGGL(softargmax_kernel, dim3(B), dim3(256), 0, st, score_maps, boxes_cxcywh, boxes_xyxy, rois,
+    hipLaunchKernelGGL(softargmax_kernel, dim3(B), dim3(SA_NT), 0, st, score_maps, boxes_cxcywh, boxes_xyxy, rois,
                        roi_scale, B, fh, stride);
     return launch_status();
 }

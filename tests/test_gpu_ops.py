@@ -99,7 +99,7 @@ def test_gemm_groups_segments_ksplit(dname):
 
 
 @pytest.mark.parametrize("impl", [-1, 1, 2, 3, 4])
-@pytest.mark.parametrize("M,N,K", [(528, 768, 768), (77, 196, 64), (300, 132, 192), (1056, 256, 3072)])
+@pytest.mark.parametrize("M,N,K", [(528, 768, 768), (77, 200, 64), (300, 136, 192), (1056, 256, 3072), (300, 136, 200)])
 def test_gemm_bf16_tile_paths(impl, M, N, K):
     """Every bf16 GEMM kernel (impl: register-staged / LDS-DMA 128x128, 128x64 K-split, 64x64
     K-split) on ragged M/N, odd K-step counts (the K-split's empty last step) and each epilogue:
@@ -136,7 +136,7 @@ def test_gemm_bf16_tile_paths(impl, M, N, K):
     assert (c2.float().cpu() - (ref[0] + rr)).abs().max().item() <= tol
     # (3) segmented rows (runs of 7 rows, 3 per A block) + K split between two sources
     if K >= 128:
-        ks = K // 2 + 8 if K % 128 else K // 2  # both sources use row stride lda = ks
+        ks = (K // 2) // 8 * 8 + 8 if K % 128 else K // 2  # both sources use row stride lda = ks (k_split % 8 == 0)
         src0 = torch.randn(2, M + 64, ks, generator=g).bfloat16()
         src1 = torch.randn(2, M + 64, ks, generator=g).bfloat16()
         s0, s1 = src0.cuda(), src1.cuda()
@@ -154,9 +154,11 @@ def test_gemm_bf16_tile_paths(impl, M, N, K):
             assert e3 <= 1e-3 * r3.abs().max().item() + 1e-4, (grp, e3)
 
 
-@pytest.mark.parametrize("dname", ["f32", "bf16"])
-@pytest.mark.parametrize("h,up,cin,cout", [(20, 1, 64, 96), (40, 2, 32, 48), (10, 1, 16, 200)])
-def test_conv3x3_implicit_gemm(dname, h, up, cin, cout):
+@pytest.mark.parametrize("dname,impl", [("f32", 0), ("bf16", -1), ("bf16", 1), ("bf16", 2), ("bf16", 3)])
+@pytest.mark.parametrize("h,up,cin,cout", [(20, 1, 64, 96), (40, 2, 32, 48), (10, 1, 16, 200), (20, 1, 96, 48)])
+def test_conv3x3_implicit_gemm(dname, impl, h, up, cin, cout):
+    """3x3/pad-1 conv as implicit GEMM on every kernel (impl); K = 9*cin is not a multiple of the
+    64-deep K-step for cin = 16 / 32 / 96 (zero-filled K tail)."""
     dt = DT[dname]
     B = 2
     g = torch.Generator().manual_seed(h + cin)
@@ -173,7 +175,7 @@ def test_conv3x3_implicit_gemm(dname, h, up, cin, cout):
     bd = b.cuda()
     _gemm([xin.data_ptr()], [wk.data_ptr()], [out.data_ptr()], B * h * h, cout, 9 * cin, cin, cout, dt,
           bias=[bd.data_ptr()], act=2, conv=(h, up, cin, 1), c2=[out2.data_ptr()], r=[rr.data_ptr()], ldr=cout,
-          r_mode=2, r_p0=h, r_p1=up)
+          r_mode=2, r_p0=h, r_p1=up, impl=impl)
     torch.cuda.synchronize()
     xu = F.interpolate(x.to(dt).float(), scale_factor=up) if up > 1 else x.to(dt).float()
     ref = F.relu(F.conv2d(xu, w.to(dt).float(), b, padding=1))

@@ -29,7 +29,7 @@ if [ $rc -ne 0 ]; then exit $rc; fi
 export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o trace --output-format csv -- \
-    python3 "$ROOT/bench.py" --no-cpu-baseline --steps 100 --warmup 10 --dump-plan "$OUT/plan_names.json" "$@" \
+    python3 "$ROOT/bench.py" --no-cpu-baseline --no-kernel-profile --steps 100 --warmup 10 --dump-plan "$OUT/plan_names.json" "$@" \
     > "$OUT/bench_prof.log" 2>&1
 rc=$?
 echo "rocprof rc=$rc"
