@@ -56,7 +56,8 @@ extern "C" {
  *   conv producing a conv_h x conv_h map; the input map is conv_h/conv_up square, pixel stride
  *   lda (channels are contiguous, conv_cin of them), k = (ky*3+kx)*conv_cin + ci.
  * Epilogue: v = act(acc + bias) with act 0 none / 1 GELU(erf) / 2 ReLU;
- *   c2 == NULL: C = v (+ R if r != NULL);  c2 != NULL: C = v, C2 = v + R.
+ *   c2 == NULL: C = v (+ R if r != NULL);  c2 != NULL: C = v, C2 = v + R (c2_copy: C = v (+ R),
+ *   C2 = the same values in `dtype`).
  *   R row index: r_mode 0 -> m, 1 -> m % r_p0, 2 -> conv map m=(b,y,x) of an r_p0 x r_p0 map read
  *   at (y / r_p1, x / r_p1) of an (r_p0/r_p1)^2 map.  R is fp32 (or dtype if r_t); C/C2 are fp32
  *   if c_f32 else dtype.
@@ -78,9 +79,18 @@ typedef struct {
     int32_t groups;
     int32_t r_t;  /* 1: R is stored in `dtype` instead of fp32 */
     int32_t impl; /* kernel choice, results identical up to fp32 summation order: 0 auto;
-                     -1 register-staged 64/128 tiles; LDS-DMA (bf16, K % 64 == 0 only): 1 128x128
+                     -1 register-staged 64/128 tiles; LDS-DMA (bf16, K % 8 == 0): 1 128x128
                      (8 waves), 2 128x64 (K split over 2 wave groups), 3 64x64 (K split 2),
                      4 128x128 (4 waves) */
+    /* LayerNorm folded into the GEMM (bf16 LDS-DMA kernels, GEMM mode): A holds the raw rows x
+     * (K = the LayerNorm width), W = W_lin * gamma (per column k), and the epilogue's v is
+     *   rstd_m * (acc - mu_m * ln_colsum[g][n]) + bias[g][n],   mu / rstd over the K values of row m
+     * with ln_colsum[n] = sum_k W[n][k] and bias = b_lin + W_lin beta, i.e. Linear(LayerNorm(x)). */
+    int32_t ln_fold;
+    float ln_eps;
+    const float* ln_colsum[MMT_MAX_GROUPS];
+    /* 1: C2 receives a copy of C (the value C holds, in `dtype`) instead of C = v, C2 = v + R */
+    int32_t c2_copy;
 } mmt_gemm_params;
 
 int mmt_gemm(const mmt_gemm_params* p, int dtype, void* stream);

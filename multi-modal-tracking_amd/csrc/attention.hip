@@ -299,22 +299,6 @@ extern "C" int mmt_attn_stamps(unsigned long long* host, int n) {
 constexpr int ANS = 8;              // K/V tile slots in the ring
 constexpr int ATILE = 2 * KB * 128; // bytes of one slot: K image then V image
 
-// Cross-lane reductions over the 4 lane groups (lanes l, l^16, l^32, l^48) that hold the 64 keys
-// of one query column: gfx950 v_permlane32_swap / v_permlane16_swap (VALU) instead of
-// ds_bpermute round trips through the LDS pipe.
-MMT_DEV float lanegroup_max(float v) {
-    auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
-    auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
-}
-MMT_DEV float lanegroup_sum(float v) {
-    auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
-    auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
-}
-
 MMT_DEV void attn_wait_dyn(int n) {
     switch (n) {
         case 0: attn_wait_vm<0>(); break;

@@ -51,6 +51,22 @@ MMT_DEV float wave_max(float v) {
     return v;
 }
 
+// Reductions over the 4 lane groups (lanes l, l^16, l^32, l^48) of an MFMA 16x16 fragment layout:
+// gfx950 v_permlane32_swap / v_permlane16_swap (VALU) instead of ds_bpermute round trips through
+// the LDS pipe.
+MMT_DEV float lanegroup_max(float v) {
+    auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+    auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+MMT_DEV float lanegroup_sum(float v) {
+    auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
 // Block-wide sum for blockDim.x == NT (multiple of 64); `red` needs NT/64 floats of LDS.
 template <int NT>
 MMT_DEV float block_sum(float v, float* red) {

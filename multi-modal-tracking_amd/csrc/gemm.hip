@@ -305,6 +305,7 @@ int launch_gemm(const mmt_gemm_params& p, hipStream_t st) {
         if (p.c2[g] && !p.r[g]) return MMT_EBADARG;
     }
     if (sizeof(T) == 2 && mmt_gemm_glds_bf16(p, st, p.impl) == 0) return launch_status();
+    if (p.ln_fold || p.c2_copy) return MMT_EBADARG;  // LDS-DMA kernel features only
     if (p.conv_h > 0) launch_tiles<T, true>(p, st);
     else launch_tiles<T, false>(p, st);
     return launch_status();

@@ -67,8 +67,11 @@ __device__ __attribute__((aligned(64))) const uint32_t g_zero_chunk[16] = {0};
 
 // WGM x WGN waves per k-group own WM x WN sub-tiles; KS k-groups split the K-steps.  CONV: A is
 // the implicit im2col of an NHWC 3x3/pad-1 (conv_k3) or 1x1 convolution, input read through the
-// nearest-upsample index map (gemm.hip's conv mode).
-template <int BM, int BN, int WGM, int WGN, int KS, int ST, bool CONV>
+// nearest-upsample index map (gemm.hip's conv mode).  LNF: LayerNorm folded into the GEMM
+// (mmt_gemm_params.ln_fold): the row statistics of A are accumulated from the A fragments the
+// waves already hold for the MFMAs (wave column wc sums fragment rows mt = wc, wc + WGN, ...), so
+// the normalised operand never exists in memory and the LayerNorm launch disappears.
+template <int BM, int BN, int WGM, int WGN, int KS, int ST, bool CONV, bool LNF>
 __global__ __launch_bounds__(64 * WGM * WGN * KS)
     __attribute__((amdgpu_waves_per_eu(WGM * WGN * KS / 4, WGM * WGN * KS / 4))) void gemm_glds_kernel(
         const mmt_gemm_params p) {
@@ -167,6 +170,11 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
         for (int i = 0; i < PB; ++i) glds16(W + boff[i] + kw, base + BM * 128 + (wid * PB + i) * 1024);
     };
 
+    constexpr int MTW = (MT + WGN - 1) / WGN;  // LNF: fragment rows whose statistics this wave sums
+    const int wc_u = __builtin_amdgcn_readfirstlane(wc);  // (v_dot2_f32_bf16 was tried for these sums: inexact)
+    float lsx[MTW], lsxx[MTW];
+#pragma unroll
+    for (int j = 0; j < MTW; ++j) lsx[j] = lsxx[j] = 0.f;
     f32x4 acc[NT][MT];  // acc[nt][mt] = (C^T) fragment: rows n, columns m
 #pragma unroll
     for (int i = 0; i < NT; ++i)
@@ -188,6 +196,22 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
     }
 #define MMT_MMA(AF, BF)                                                                                          \
     {                                                                                                            \
+        if constexpr (LNF) { /* compile-time fragment index, scalar (wave-uniform) wave-column test */            \
+            _Pragma("unroll") for (int mt_ = 0; mt_ < MT; ++mt_) {                                               \
+                if (mt_ % WGN == wc_u) {                                                                         \
+                    float sx_ = 0.f, sxx_ = 0.f;                                                                 \
+                    _Pragma("unroll") for (int t = 0; t < 2; ++t)                                                \
+                    _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                              \
+                        const float lo_ = __uint_as_float(AF[t][mt_][e] << 16);                                  \
+                        const float hi_ = __uint_as_float(AF[t][mt_][e] & 0xffff0000u);                          \
+                        sx_ += lo_ + hi_;                                                                        \
+                        sxx_ = fmaf(lo_, lo_, fmaf(hi_, hi_, sxx_));                                             \
+                    }                                                                                            \
+                    lsx[mt_ / WGN] += sx_;                                                                       \
+                    lsxx[mt_ / WGN] += sxx_;                                                                     \
+                }                                                                                                \
+            }                                                                                                    \
+        }                                                                                                        \
         if (MMT_GEMM_ABLATE == 2) {                                                                              \
             acc[0][0] += __builtin_bit_cast(f32x4, AF[0][0]) + __builtin_bit_cast(f32x4, BF[1][NT - 1]);         \
         } else {                                                                                                 \
@@ -247,9 +271,21 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
     // every thread owns 8 consecutive columns of RPP-row strips: bias / residual loads and C / C2
     // stores are whole 256-512-B row segments per wave-instruction.
     constexpr int TP = BN + 4;  // tile row pitch (floats); +4 keeps the fragment writes 2-way
-    static_assert(BM * TP * 4 <= KS * ST * STAGE, "epilogue tile fits in the stage ring");
+    static_assert(BM * TP * 4 + KS * BM * 8 <= KS * ST * STAGE, "epilogue tile fits in the stage ring");
     float* ctile = (float*)lds;
+    float* rstat = ctile + BM * TP;  // LNF: [KS][BM][2] partial (sum x, sum x^2) per k-group
     lds_barrier();  // every wave is past its last fragment read (the DMA ring is drained: vmcnt(0))
+    if constexpr (LNF) {
+#pragma unroll
+        for (int j = 0; j < MTW; ++j) {
+            const int mt = wc + j * WGN;
+            const float sx = lanegroup_sum(lsx[j]), sxx = lanegroup_sum(lsxx[j]);
+            if (mt < MT && lg == 0) {
+                rstat[(kg * BM + wr * WM + mt * 16 + l16) * 2] = sx;
+                rstat[(kg * BM + wr * WM + mt * 16 + l16) * 2 + 1] = sxx;
+            }
+        }
+    }
     if (KS == 1 || kg == 1) {
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
@@ -282,11 +318,16 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
     char* C2 = (char*)p.c2[g];
     const int tc = (threadIdx.x % TPR) * 8, tr = threadIdx.x / TPR;
     const int n = n0 + tc, nc = min(n, N - 8);
-    f32x4 bn0 = {0.f, 0.f, 0.f, 0.f}, bn1 = bn0;
+    f32x4 bn0 = {0.f, 0.f, 0.f, 0.f}, bn1 = bn0, cs0 = bn0, cs1 = bn0;
     if (bias) {
         bn0 = *(const f32x4*)(bias + nc);
         bn1 = *(const f32x4*)(bias + nc + 4);
     }
+    if constexpr (LNF) {
+        cs0 = *(const f32x4*)(p.ln_colsum[g] + nc);
+        cs1 = *(const f32x4*)(p.ln_colsum[g] + nc + 4);
+    }
+    const float inv_k = 1.f / (float)K;
     constexpr int PG = NPASS < 4 ? NPASS : 4;  // passes whose residual loads are in flight together
 #pragma unroll
     for (int p0 = 0; p0 < NPASS; p0 += PG) {
@@ -318,8 +359,22 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
 #pragma unroll
         for (int i = 0; i < PG; ++i) {
             const int r = tr + (p0 + i) * RPP, m = m0 + r;
-            f32x4 va = *(const f32x4*)(ctile + r * TP + tc) + bn0;
-            f32x4 vb = *(const f32x4*)(ctile + r * TP + tc + 4) + bn1;
+            f32x4 va = *(const f32x4*)(ctile + r * TP + tc);
+            f32x4 vb = *(const f32x4*)(ctile + r * TP + tc + 4);
+            if constexpr (LNF) {  // Linear(LayerNorm(x)) = rstd * (x.W' - mu * colsum(W')) + b'
+                float sx = 0.f, sxx = 0.f;
+#pragma unroll
+                for (int q = 0; q < KS; ++q) {
+                    sx += rstat[(q * BM + r) * 2];
+                    sxx += rstat[(q * BM + r) * 2 + 1];
+                }
+                const float mu = sx * inv_k, var = fmaxf(sxx * inv_k - mu * mu, 0.f);
+                const float rstd = rsqrtf(var + p.ln_eps);
+                va = (va - mu * cs0) * rstd;
+                vb = (vb - mu * cs1) * rstd;
+            }
+            va += bn0;
+            vb += bn1;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 if (p.act == 1) {
@@ -331,13 +386,17 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
                 }
             }
             const f32x4 sa = va + ra[i], sb = vb + rb[i];  // + residual
-            const f32x4 oa = C2 ? va : sa, ob = C2 ? vb : sb;
+            const bool split_c2 = C2 && !p.c2_copy;           // C = v, C2 = v + R
+            const f32x4 oa = split_c2 ? va : sa, ob = split_c2 ? vb : sb;
             if (m < M && n < N) {
                 const int64_t e = (int64_t)m * p.ldc + n;
                 if (p.c_f32) {
                     *(f32x4*)((float*)C + e) = oa;
                     *(f32x4*)((float*)C + e + 4) = ob;
-                    if (C2) {
+                    if (C2 && p.c2_copy) {  // compute-dtype copy of C (the next LayerNorm-folded GEMM's A)
+                        *(u32x4*)((bf16_t*)C2 + e) = u32x4{pack_bf16x2(sa[0], sa[1]), pack_bf16x2(sa[2], sa[3]),
+                                                           pack_bf16x2(sb[0], sb[1]), pack_bf16x2(sb[2], sb[3])};
+                    } else if (C2) {
                         *(f32x4*)((float*)C2 + e) = sa;
                         *(f32x4*)((float*)C2 + e + 4) = sb;
                     }
@@ -362,10 +421,13 @@ template <int BM, int BN, int WGM, int WGN, int KS, int ST>
 void launch(const mmt_gemm_params& p, hipStream_t st) {
     const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
     if (p.conv_h > 0)
-        hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, KS, ST, true>), dim3(tiles, 1, p.groups),
+        hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, KS, ST, true, false>), dim3(tiles, 1, p.groups),
+                           dim3(64 * WGM * WGN * KS), 0, st, p);
+    else if (p.ln_fold)
+        hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, KS, ST, false, true>), dim3(tiles, 1, p.groups),
                            dim3(64 * WGM * WGN * KS), 0, st, p);
     else
-        hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, KS, ST, false>), dim3(tiles, 1, p.groups),
+        hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, KS, ST, false, false>), dim3(tiles, 1, p.groups),
                            dim3(64 * WGM * WGN * KS), 0, st, p);
 }
 
@@ -377,12 +439,14 @@ bool aligned(const void* ptr, int bytes) { return ((uintptr_t)ptr & (uintptr_t)(
 int mmt_gemm_glds_bf16(const mmt_gemm_params& p, hipStream_t st, int force) {
     if (force < 0) return 1;
     if (p.K % 8 || p.N % 8 || p.ldc % 8 || (p.r[0] && p.ldr % 8)) return 1;
+    if (p.ln_fold && p.conv_h > 0) return 1;
     if (p.lda % 8 || p.a_stride_a % 8 || p.a_stride_b % 8 || p.k_split % 8) return 1;
     if (p.a_seg_rows > INT32_MAX || p.a_segs_a > INT32_MAX) return 1;
     for (int g = 0; g < p.groups; ++g) {
         if (!aligned(p.c[g], 16) || (p.c2[g] && !aligned(p.c2[g], 16))) return 1;
         if (p.bias[g] && !aligned(p.bias[g], 16)) return 1;
         if (p.r[g] && !aligned(p.r[g], 16)) return 1;
+        if (p.ln_fold && (!p.ln_colsum[g] || !aligned(p.ln_colsum[g], 16))) return 1;
     }
     auto blocks = [&](int bm, int bn) { return (int64_t)((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn) * p.groups; };
     const int nk = (p.K + 63) / 64;

@@ -33,6 +33,7 @@ class GemmParams(ctypes.Structure):
         ("r_mode", i32), ("r_p0", i32), ("r_p1", i32),
         ("conv_h", i32), ("conv_up", i32), ("conv_cin", i32), ("conv_k3", i32),
         ("groups", i32), ("r_t", i32), ("impl", i32),
+        ("ln_fold", i32), ("ln_eps", f32), ("ln_colsum", vp * MAX_GROUPS), ("c2_copy", i32),
     ]
 
 

@@ -66,7 +66,11 @@ class MixFormerRGBTRuntime:
 
     gemm_impl = 0  # mmt_gemm_params.impl of every plan GEMM (0 = library's choice; A/B knob)
 
-    def __init__(self, state_dict, variant, dtype=torch.bfloat16, device="cuda"):
+    def __init__(self, state_dict, variant, dtype=torch.bfloat16, device="cuda", fold_ln=None):
+        """fold_ln (default: on for bf16): the ViT's LayerNorms are folded into the qkv / fc1 GEMMs
+        (mmt_gemm_params.ln_fold) and the residual-producing GEMMs also write the bf16 copy of the
+        residual stream those GEMMs read, so no LayerNorm launch or normalised tensor remains.
+        The fp32 path keeps the explicit LayerNorm kernels."""
         if variant not in VARIANTS:
             raise ValueError("unknown variant %r" % (variant,))
         if dtype not in (torch.bfloat16, torch.float32):
@@ -74,6 +78,9 @@ class MixFormerRGBTRuntime:
         self.variant = variant
         self.dtype = dtype
         self.cdt = MMT_BF16 if dtype == torch.bfloat16 else MMT_F32
+        self.fold_ln = (dtype == torch.bfloat16) if fold_ln is None else bool(fold_ln)
+        if self.fold_ln and dtype != torch.bfloat16:
+            raise ValueError("the LayerNorm fold needs the bf16 (LDS-DMA) GEMM kernels")
         self.device = torch.device(device)
         sd = {k: v.detach() for k, v in state_dict.items()}
         self.d = Dims(sd, variant)
@@ -126,6 +133,21 @@ class MixFormerRGBTRuntime:
                     for nm in ("norm1", "norm2"):
                         blk[nm + "_v"] = (self._F(sd[b + nm + "_v.weight"]), self._F(sd[b + nm + "_v.bias"]))
                         blk[nm + "_i"] = (self._F(sd[b + nm + "_i.weight"]), self._F(sd[b + nm + "_i.bias"]))
+                if self.fold_ln:
+                    # Linear(LayerNorm(x)) = rstd*(x.W' - mu*colsum(W')) + b', W' = W*gamma (per k),
+                    # b' = b + W.beta; one (W', colsum, b') per norm (two-stream: this backbone's;
+                    # shared: norm*_v / norm*_i -> one GEMM group per modality)
+                    norms = ["", ] if self.variant == "rgbt" else ["_v", "_i"]
+                    for lin, nm in (("attn.qkv", "norm1"), ("mlp.fc1", "norm2")):
+                        w64, b64 = sd[b + lin + ".weight"].double(), sd[b + lin + ".bias"].double()
+                        fw, fc, fb = [], [], []
+                        for suf in norms:
+                            gam, bet = sd[b + nm + suf + ".weight"].double(), sd[b + nm + suf + ".bias"].double()
+                            wt = self._T(w64 * gam[None, :])
+                            fw.append(wt)
+                            fc.append(self._F(wt.double().sum(1)))
+                            fb.append(self._F(b64 + w64 @ bet))
+                        blk[lin + ".fw"], blk[lin + ".fcs"], blk[lin + ".fb"] = fw, fc, fb
                 bb["blocks"].append(blk)
             W["bb"].append(bb)
         # fusion
@@ -242,7 +264,8 @@ class MixFormerRGBTRuntime:
 
     # ------------------------------------------------------------------ plan construction
     def _gemm(self, plan, name, *, a, w, c, M, N, K, lda, ldc, bias=None, r=None, ldr=0, c2=None, a1=None,
-              k_split=0, act=0, c_f32=0, seg=None, r_mode=0, r_p0=0, r_p1=1, conv=None, r_t=0, dtype=None):
+              k_split=0, act=0, c_f32=0, seg=None, r_mode=0, r_p0=0, r_p1=1, conv=None, r_t=0, dtype=None,
+              ln_colsum=None, ln_eps=0.0, c2_copy=0):
         p = GemmParams()
         G = len(a)
         for g in range(G):
@@ -266,6 +289,11 @@ class MixFormerRGBTRuntime:
         p.groups = G
         p.r_t = r_t
         p.impl = self.gemm_impl
+        if ln_colsum is not None:
+            p.ln_fold, p.ln_eps = 1, ln_eps
+            for g in range(G):
+                p.ln_colsum[g] = ln_colsum[g]
+        p.c2_copy = c2_copy
         plan.append((LIB.mmt_gemm, (ctypes_byref(p), self.cdt if dtype is None else dtype), name, p))
 
     def _build_plan(self, ws, score):
@@ -278,28 +306,34 @@ class MixFormerRGBTRuntime:
         P = _ptr
         X, XN, QKV, AO, HID = ws["X"], ws["XN"], ws["QKV"], ws["AO"], ws["HID"]
         cdt = self.cdt
-        # --- patch embed (im2col + GEMM, + bias + pos-embed) -> X
+        # --- patch embed (im2col + GEMM, + bias + pos-embed) -> X  (fold: + its bf16 copy XN)
+        fold = self.fold_ln
         plan.append((LIB.mmt_patch_im2col, tuple(P(t) for t in ws["in_t"]) + tuple(P(t) for t in ws["in_o"])
                      + tuple(P(t) for t in ws["in_s"]) + (P(ws["PATCH"]), B, d.ht, d.hs, d.patch, cdt), "patch_im2col", None))
         KP = 3 * d.patch * d.patch
+        gm = B * ntok
+        cp = dict(c2_copy=1) if fold else {}
         if two:
-            gm = B * ntok
+            if fold:
+                cp["c2"] = [P(XN), P(XN, gm * C)]
             self._gemm(plan, "patch_gemm", a=[P(ws["PATCH"]), P(ws["PATCH"], gm * KP)],
                        w=[P(W["bb"][g]["patch_w"]) for g in range(2)], c=[P(X), P(X, gm * C)], M=gm, N=C, K=KP,
                        lda=KP, ldc=C, bias=[P(W["bb"][g]["patch_b"]) for g in range(2)],
-                       r=[P(W["bb"][g]["pos"]) for g in range(2)], ldr=C, r_mode=1, r_p0=ntok, c_f32=1)
+                       r=[P(W["bb"][g]["pos"]) for g in range(2)], ldr=C, r_mode=1, r_p0=ntok, c_f32=1, **cp)
         else:
+            if fold:
+                cp["c2"] = [P(XN)]
             self._gemm(plan, "patch_gemm", a=[P(ws["PATCH"])], w=[P(W["bb"][0]["patch_w"])], c=[P(X)], M=R, N=C, K=KP,
                        lda=KP, ldc=C, bias=[P(W["bb"][0]["patch_b"])], r=[P(W["bb"][0]["pos"])], ldr=C, r_mode=1,
-                       r_p0=ntok, c_f32=1)
+                       r_p0=ntok, c_f32=1, **cp)
         # --- transformer blocks
-        gm = B * ntok
         for i in range(d.depth):
             if two:
                 blks = [W["bb"][g]["blocks"][i] for g in range(2)]
                 n1 = [blks[0]["norm1"], blks[1]["norm1"]]
                 n2 = [blks[0]["norm2"], blks[1]["norm2"]]
                 wl = lambda nm: [P(blks[g][nm]) for g in range(2)]  # noqa: E731
+                fl = lambda nm: [P(blks[g][nm][0]) for g in range(2)]  # noqa: E731
                 rows = lambda t, k: [P(t), P(t, gm * k)]  # noqa: E731
                 Mg = gm
             else:
@@ -307,27 +341,42 @@ class MixFormerRGBTRuntime:
                 n1 = [blk["norm1_v"], blk["norm1_i"]]
                 n2 = [blk["norm2_v"], blk["norm2_i"]]
                 wl = lambda nm: [P(blk[nm])]  # noqa: E731
+                fl = lambda nm: [P(blk[nm][m]) for m in range(2)]  # noqa: E731
                 rows = lambda t, k: [P(t)]  # noqa: E731
                 Mg = R
-            plan.append((LIB.mmt_layernorm, (P(X), None, 0, None, P(XN), P(n1[0][0]), P(n1[0][1]), P(n1[1][0]),
-                                             P(n1[1][1]), R, gm, C, 1e-6, cdt), "ln1", None))
-            self._gemm(plan, "qkv", a=rows(XN, C), w=wl("attn.qkv.w"), c=rows(QKV, 3 * C), M=Mg, N=3 * C, K=C,
-                       lda=C, ldc=3 * C, bias=wl("attn.qkv.b"))
+            rows2 = lambda t, k: [P(t), P(t, gm * k)]  # noqa: E731  (one group per modality)
+            if fold:  # LayerNorm 1 folded into qkv: A = XN = bf16 copy of the residual stream X
+                self._gemm(plan, "qkv", a=rows2(XN, C), w=fl("attn.qkv.fw"), c=rows2(QKV, 3 * C), M=gm, N=3 * C,
+                           K=C, lda=C, ldc=3 * C, bias=fl("attn.qkv.fb"), ln_colsum=fl("attn.qkv.fcs"), ln_eps=1e-6)
+            else:
+                plan.append((LIB.mmt_layernorm, (P(X), None, 0, None, P(XN), P(n1[0][0]), P(n1[0][1]), P(n1[1][0]),
+                                                 P(n1[1][1]), R, gm, C, 1e-6, cdt), "ln1", None))
+                self._gemm(plan, "qkv", a=rows(XN, C), w=wl("attn.qkv.w"), c=rows(QKV, 3 * C), M=Mg, N=3 * C, K=C,
+                           lda=C, ldc=3 * C, bias=wl("attn.qkv.b"))
             ap = AttnParams()
             ap.qkv, ap.out, ap.S, ap.Bm, ap.ntok, ap.n_t, ap.C, ap.H = P(QKV), P(AO), S, B, ntok, d.n_t, C, d.H
             ap.asym = 1 if self.variant in ("asym", "asym_online") else 0
             ap.scale = (C // d.H) ** -0.5
             plan.append((LIB.mmt_mam_attention, (ctypes_byref(ap), cdt), "mam_attention", ap))
+            cpx = dict(c2=rows(XN, C), c2_copy=1) if fold else {}
             self._gemm(plan, "proj", a=rows(AO, C), w=wl("attn.proj.w"), c=rows(X, C), M=Mg, N=C, K=C, lda=C,
-                       ldc=C, bias=wl("attn.proj.b"), r=rows(X, C), ldr=C, c_f32=1)
-            plan.append((LIB.mmt_layernorm, (P(X), None, 0, None, P(XN), P(n2[0][0]), P(n2[0][1]), P(n2[1][0]),
-                                             P(n2[1][1]), R, gm, C, 1e-6, cdt), "ln2", None))
-            self._gemm(plan, "fc1", a=rows(XN, C), w=wl("mlp.fc1.w"), c=rows(HID, d.hidden), M=Mg, N=d.hidden, K=C,
-                       lda=C, ldc=d.hidden, bias=wl("mlp.fc1.b"), act=1)
+                       ldc=C, bias=wl("attn.proj.b"), r=rows(X, C), ldr=C, c_f32=1, **cpx)
+            if fold:
+                self._gemm(plan, "fc1", a=rows2(XN, C), w=fl("mlp.fc1.fw"), c=rows2(HID, d.hidden), M=gm, N=d.hidden,
+                           K=C, lda=C, ldc=d.hidden, bias=fl("mlp.fc1.fb"), act=1, ln_colsum=fl("mlp.fc1.fcs"),
+                           ln_eps=1e-6)
+            else:
+                plan.append((LIB.mmt_layernorm, (P(X), None, 0, None, P(XN), P(n2[0][0]), P(n2[0][1]), P(n2[1][0]),
+                                                 P(n2[1][1]), R, gm, C, 1e-6, cdt), "ln2", None))
+                self._gemm(plan, "fc1", a=rows(XN, C), w=wl("mlp.fc1.w"), c=rows(HID, d.hidden), M=Mg, N=d.hidden,
+                           K=C, lda=C, ldc=d.hidden, bias=wl("mlp.fc1.b"), act=1)
             self._gemm(plan, "fc2", a=rows(HID, d.hidden), w=wl("mlp.fc2.w"), c=rows(X, C), M=Mg, N=C, K=d.hidden,
-                       lda=d.hidden, ldc=C, bias=wl("mlp.fc2.b"), r=rows(X, C), ldr=C, c_f32=1)
-        XT = ws["XT"]
-        plan.append((LIB.mmt_add_cast, (P(X), None, 0, None, P(XT), R * C, cdt), "cast_x", None))
+                       lda=d.hidden, ldc=C, bias=wl("mlp.fc2.b"), r=rows(X, C), ldr=C, c_f32=1, **cpx)
+        if fold:
+            XT = XN  # the last fc2 already wrote the bf16 copy of the backbone output
+        else:
+            XT = ws["XT"]
+            plan.append((LIB.mmt_add_cast, (P(X), None, 0, None, P(XT), R * C, cdt), "cast_x", None))
         # --- fusion: adjust_v / adjust_i (1x1 conv on the search tokens) + GroupNorm
         Y1, SRC, SRCT, QS, VAL = ws["Y1"], ws["SRC"], ws["SRCT"], ws["QS"], ws["VAL"]
         Mf = B * ns

@@ -16,14 +16,14 @@ CASES = [("rgbt", 1), ("shared", 1), ("asym", 1), ("asym_online", 1), ("shared",
 _RT = {}
 
 
-def _runtime(variant, dtype):
-    key = (variant, dtype)
+def _runtime(variant, dtype, fold_ln=None):
+    key = (variant, dtype, fold_ln)
     if key not in _RT:
         from mmt_amd import synthetic
         from mmt_amd.runtime import MixFormerRGBTRuntime
         keys = json.load(open(GOLDEN + "/state_dict_%s.json" % variant))
         sd = {k: torch.from_numpy(v) for k, v in synthetic.synth_state_dict(keys).items()}
-        _RT[key] = MixFormerRGBTRuntime(sd, variant, dtype=dtype)
+        _RT[key] = MixFormerRGBTRuntime(sd, variant, dtype=dtype, fold_ln=fold_ln)
     return _RT[key]
 
 
@@ -96,3 +96,20 @@ def test_zero_copy_plan_matches_copy_path():
     g.replay()
     torch.cuda.synchronize()
     assert torch.equal(b0, rt.workspace(1)["BOX"])
+
+
+@pytest.mark.parametrize("variant", ["rgbt", "asym"])
+def test_bf16_layernorm_fold_vs_explicit(variant):
+    """bf16 plan with the ViT LayerNorms folded into qkv / fc1 (default) against the plan with the
+    explicit LayerNorm kernels: both within the bf16 bound of the golden boxes, and of each other."""
+    t, o, s = _inputs(1)
+    gold = np.load(GOLDEN + "/model_%s_b1.npz" % variant)["pred_boxes"].reshape(1, 4)
+    boxes = []
+    for fold in (True, False):
+        rt = _runtime(variant, torch.bfloat16, fold_ln=fold)
+        assert any(e[2] == "ln1" for e in rt.workspace(1)["plan"]) != fold
+        box, _ = rt.forward(t, o, s)
+        torch.cuda.synchronize()
+        boxes.append(box.cpu().numpy().copy())
+        assert np.abs(boxes[-1] - gold).max() <= 1e-2
+    assert np.abs(boxes[0] - boxes[1]).max() <= 1e-2

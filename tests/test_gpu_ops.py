@@ -44,6 +44,7 @@ def _gemm(a, w, c, M, N, K, lda, ldc, dtype, **kw):
     p.groups = G
     p.r_t = kw.get("r_t", 0)
     p.impl = kw.get("impl", 0)
+    p.c2_copy = kw.get("c2_copy", 0)
     L.check(L.LIB.mmt_gemm(p, L.MMT_BF16 if dtype == torch.bfloat16 else L.MMT_F32,
                            torch.cuda.current_stream().cuda_stream), "mmt_gemm")
 
@@ -152,6 +153,51 @@ def test_gemm_bf16_tile_paths(impl, M, N, K):
             r3 = Ag @ Wb[grp].float().t()
             e3 = (o3[grp].cpu() - r3).abs().max().item()
             assert e3 <= 1e-3 * r3.abs().max().item() + 1e-4, (grp, e3)
+
+
+@pytest.mark.parametrize("impl", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("M,N,K", [(528, 2304, 768), (300, 136, 512)])
+def test_gemm_layernorm_fold(impl, M, N, K):
+    """Linear(LayerNorm(x)) as one GEMM (ln_fold): A = bf16 rows of x with a nonzero mean, W' =
+    W * gamma, colsum / bias' precomputed as the runtime does; two groups (modalities) with their
+    own gamma / beta.  Also the producer side: c2_copy writes the bf16 copy of an fp32 C + R."""
+    L = _lib()
+    g = torch.Generator().manual_seed(M + K)
+    x = torch.randn(2, M, K, generator=g) * 2 + 0.7
+    W = torch.randn(N, K, generator=g) / math.sqrt(K)
+    b = torch.randn(N, generator=g)
+    gam = 1 + 0.3 * torch.randn(2, K, generator=g)
+    bet = 0.2 * torch.randn(2, K, generator=g)
+    xb = x.bfloat16()
+    Wp = (W[None] * gam[:, None, :]).bfloat16()                      # [2][N][K]
+    colsum = Wp.float().sum(-1).contiguous()                         # [2][N]
+    bp = (b[None] + torch.einsum("nk,gk->gn", W, bet)).contiguous()  # [2][N]
+    xd, Wd, cd, bd = xb.cuda(), Wp.cuda(), colsum.cuda(), bp.cuda()
+    out = torch.empty(2, M, N, device="cuda")
+    p = L.GemmParams()
+    for q in range(2):
+        p.a[q], p.w[q], p.c[q], p.bias[q], p.ln_colsum[q] = (xd[q].data_ptr(), Wd[q].data_ptr(), out[q].data_ptr(),
+                                                             bd[q].data_ptr(), cd[q].data_ptr())
+    p.lda, p.ldc = K, N
+    p.a_seg_rows, p.a_segs_a = M, 1
+    p.M, p.N, p.K, p.c_f32, p.groups, p.impl, p.ln_fold, p.ln_eps = M, N, K, 1, 2, impl, 1, 1e-6
+    L.check(L.LIB.mmt_gemm(p, L.MMT_BF16, torch.cuda.current_stream().cuda_stream), "gemm_ln")
+    torch.cuda.synchronize()
+    for q in range(2):
+        ref = F.layer_norm(xb[q].float(), (K,), gam[q], bet[q], 1e-6) @ W.t() + b
+        err = (out[q].cpu() - ref).abs().max().item()
+        assert err <= 1e-2 * ref.abs().max().item(), (q, err)
+    # producer: C (fp32) = A W^T + bias + R and C2 = bf16 copy of C
+    R = torch.randn(M, N, generator=g)
+    Rd = R.cuda()
+    c1 = torch.empty(M, N, device="cuda")
+    c2 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    _gemm([xd[0].data_ptr()], [Wd[0].data_ptr()], [c1.data_ptr()], M, N, K, K, N, torch.bfloat16,
+          bias=[bd[0].data_ptr()], r=[Rd.data_ptr()], ldr=N, c_f32=1, c2=[c2.data_ptr()], impl=impl, c2_copy=1)
+    torch.cuda.synchronize()
+    ref = xb[0].float() @ Wp[0].float().t() + bp[0] + R
+    assert (c1.cpu() - ref).abs().max().item() <= 1e-3 * ref.abs().max().item() + 1e-4
+    assert torch.equal(c2.cpu(), c1.cpu().bfloat16())
 
 
 @pytest.mark.parametrize("dname,impl", [("f32", 0), ("bf16", -1), ("bf16", 1), ("bf16", 2), ("bf16", 3)])

@@ -21,7 +21,7 @@ import torch  # noqa: E402
 from mmt_amd import _lib as L  # noqa: E402
 
 SHAPES = [("qkv", 2, 528, 2304, 768, 0, 0), ("proj", 2, 528, 768, 768, 0, 1), ("fc1", 2, 528, 3072, 768, 1, 0),
-          ("fc2", 2, 528, 768, 3072, 0, 1), ("k64", 2, 528, 768, 64, 0, 1), ("k256", 2, 528, 768, 256, 0, 1)]
+          ("fc2", 2, 528, 768, 3072, 0, 1), ("qkv_ln", 2, 528, 2304, 768, 0, 0), ("fc1_ln", 2, 528, 3072, 768, 1, 0)]
 TILES = {1: (128, 128), 2: (128, 64), 3: (64, 64), 4: (128, 128)}
 
 
@@ -41,6 +41,10 @@ def main():
             p.lda, p.ldc, p.ldr = K, N, N
             p.a_seg_rows, p.a_segs_a = M, 1
             p.M, p.N, p.K, p.act, p.c_f32, p.groups, p.impl = M, N, K, act, 1 if res else 0, G, impl
+            if name.endswith("_ln"):
+                p.ln_fold, p.ln_eps = 1, 1e-6
+                for g in range(G):
+                    p.ln_colsum[g] = b[g].data_ptr()
             s = torch.cuda.current_stream().cuda_stream
             for _ in range(10):
                 L.check(L.LIB.mmt_gemm(ctypes.byref(p), L.MMT_BF16, s), name)
