@@ -30,6 +30,10 @@
  *       head.py:191-212, mixformer.py:419-432
  *   mmt_conv3x3_c1              the 1-channel conv-BN-ReLU of adjust3/adjust4, head.py:115-120
  *   mmt_spm_attention           ScoreDecoder single-query attention, score_decoder.py:55-61
+ *   mmt_sample_target           the trackers' host crop + preprocessing, processing_utils.py:15-77,
+ *       tracker_utils.py:24-48 (cv2 crop/pad/resize, colour map, normalise)
+ *   mmt_track_update            map_box_back + clip_box, lib/test/tracker/mixformer_vit_rgbt.py:92-95,
+ *       :124-131, lib/utils/box_ops.py:155-164
  */
 #ifndef MMT_HIP_H_
 #define MMT_HIP_H_
@@ -180,6 +184,41 @@ int mmt_prroi_pool_forward(const float* features, const float* rois, float* out,
  * H heads of C/H (= 64), scale; out [B][C] fp32 (dtype copy optional via out_t). */
 int mmt_spm_attention(const float* q, int64_t q_stride, const float* kv, float* out, int B, int Lk, int C, int H,
                       float scale, void* stream);
+
+/* ---------------------------------------------------------------- tracker pre/post-processing
+ * mmt_sample_target replaces the per-frame host path of the RGB-T trackers
+ *   sample_target (lib/train/data/processing_utils.py:15-77, cv2.copyMakeBorder + cv2.resize) +
+ *   Preprocessor_wo_mask / Preprocessor_Multimodal.process (lib/test/tracker/tracker_utils.py:24-48)
+ * for n (<= MMT_MAX_CROPS) crops of equal out_sz in one launch.  The crop box comes from the
+ * device-resident box (x, y, w, h) in fp64, exactly as the tracker state: crop_sz =
+ * ceil(sqrt(w*h)*factor), x1 = round-half-even(x + w/2 - crop_sz/2).  out: [3][out_sz][out_sz] fp32
+ * = ((v / 255) - mean) / std of the resized uint8 crop v (after the colour map `lut` if non-NULL:
+ * BGR2GRAY then lut[gray][c], the cv2.applyColorMap(COLORMAP_JET) step).  Optional: patch
+ * [out_sz][out_sz][3] uint8 (sample_target's crop), crop [4] fp64 = (x1, y1, crop_sz,
+ * resize_factor = out_sz / crop_sz).
+ */
+#define MMT_MAX_CROPS 4
+typedef struct {
+    const uint8_t* image; /* [H][W][3] uint8 frame (HWC, as the tracker receives it) */
+    int32_t H, W;
+    const double* box;  /* [4] x, y, w, h */
+    double factor;      /* search_area_factor (template_factor / search_factor) */
+    int32_t out_sz;     /* output_sz */
+    const uint8_t* lut; /* NULL or [256][3] */
+    float mean[3], std[3];
+    float* out;
+    uint8_t* patch;
+    double* crop;
+} mmt_crop_params;
+
+int mmt_sample_target(const mmt_crop_params* p, int n, void* stream);
+
+/* Box post-processing of the trackers (lib/test/tracker/mixformer_vit_rgbt.py:92-95, :124-131;
+ * lib/utils/box_ops.py:155-164): for each of n trackers, pred = pred_cxcywh[i] * search_size /
+ * resize_factor (fp32, as torch computes it), map_box_back against state[i] (fp64 x, y, w, h) and
+ * crop[i][3] = resize_factor, clip_box(H, W, margin); the result replaces state[i]. */
+int mmt_track_update(const float* pred_cxcywh, const double* crop, double* state, int n, int H, int W,
+                     int search_size, double margin, void* stream);
 
 /* Library version string (for diagnostics). */
 const char* mmt_version(void);

@@ -1,0 +1,70 @@
+"""Shared body of the four RGB-T tracker entry points (drop-in for lib/test/tracker/
+mixformer_vit_rgbt.py, mixformer_vit_rgbt_shared.py, asymmetric_shared.py,
+asymmetric_shared_online.py; each defines `MixFormer` and `get_tracker_class()`).
+
+Same constructor, `initialize(image, info)` and `track(image, info)` contract as the reference
+(mixformer_vit_rgbt.py:13-121): `params` carries cfg, template_factor, template_size,
+search_factor, search_size, checkpoint, save_all_boxes; `image` is [image_v, image_i] (H, W, 3)
+uint8 frames (numpy, or torch uint8 tensors already on the device); `track` returns
+{"target_bbox": [x, y, w, h]}.  The per-frame crop, preprocessing, forward and box
+post-processing run on the MI355X as one hipGraph (mmt_amd.tracking.RGBTTrackerCore).
+"""
+import torch
+
+from mmt_amd.tracking import RGBTTrackerCore
+
+from .basetracker import BaseTracker
+
+
+def _update_intervals(cfg, dataset_name):
+    """mixformer_vit_rgbt.py:39-44: per-dataset template update intervals."""
+    name = dataset_name.upper()
+    ui = cfg.TEST.UPDATE_INTERVALS
+    if hasattr(ui, name) or (isinstance(ui, dict) and name in ui):
+        return ui[name]
+    return cfg.DATA.MAX_SAMPLE_INTERVAL
+
+
+def make_tracker_class(builder, multimodal, online_score=False):
+    class MixFormer(BaseTracker):
+        def __init__(self, params, dataset_name):
+            super().__init__(params)
+            network = builder(params.cfg, train=False)
+            if getattr(params, "checkpoint", None):
+                ck = torch.load(params.checkpoint, map_location="cpu", weights_only=True)
+                network.load_state_dict(ck["net"], strict=True)
+            self.cfg = params.cfg
+            self.network = network.cuda()
+            self.network.eval()
+            self.save_all_boxes = getattr(params, "save_all_boxes", False)
+            self.update_intervals = _update_intervals(self.cfg, dataset_name)
+            self.core = RGBTTrackerCore(self.network, params.template_factor, params.template_size,
+                                        params.search_factor, params.search_size, self.update_intervals,
+                                        multimodal=multimodal, online_score=online_score)
+            self.state = None
+            self.frame_id = 0
+
+        def initialize(self, image, info: dict):
+            """image: [image_v, image_i]; info["init_bbox"]: (bbox_v, bbox_i), the RGB box is used."""
+            self.core.initialize(image, info["init_bbox"][0])
+            self.state = [float(v) for v in info["init_bbox"][0]]
+            self.frame_id = 0
+            if self.save_all_boxes:
+                return {"all_boxes": info["init_bbox"] * self.cfg.MODEL.NUM_OBJECT_QUERIES}
+
+        def track(self, image, info: dict = None):
+            self.frame_id += 1
+            self.state = self.core.track(image)
+            if self.save_all_boxes:  # one query: all boxes = the tracked box (mixformer_vit_rgbt.py:114-117)
+                return {"target_bbox": self.state, "all_boxes": list(self.state)}
+            return {"target_bbox": self.state}
+
+        def map_box_back(self, pred_box: list, resize_factor: float):
+            """mixformer_vit_rgbt.py:124-131 (host form; the tracking step runs it on the device)."""
+            cx_prev, cy_prev = self.state[0] + 0.5 * self.state[2], self.state[1] + 0.5 * self.state[3]
+            cx, cy, w, h = pred_box
+            half_side = 0.5 * self.params.search_size / resize_factor
+            cx_real, cy_real = cx + (cx_prev - half_side), cy + (cy_prev - half_side)
+            return [cx_real - 0.5 * w, cy_real - 0.5 * h, w, h]
+
+    return MixFormer

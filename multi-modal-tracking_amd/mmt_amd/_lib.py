@@ -42,6 +42,16 @@ class AttnParams(ctypes.Structure):
                 ("H", i32), ("asym", i32), ("scale", f32), ("impl", i32)]
 
 
+MAX_CROPS = 4
+f64 = ctypes.c_double
+u8p = ctypes.c_void_p
+
+
+class CropParams(ctypes.Structure):
+    _fields_ = [("image", vp), ("H", i32), ("W", i32), ("box", vp), ("factor", f64), ("out_sz", i32),
+                ("lut", vp), ("mean", f32 * 3), ("std", f32 * 3), ("out", vp), ("patch", vp), ("crop", vp)]
+
+
 _PROTOS = {
     "mmt_gemm": [ctypes.POINTER(GemmParams), i32, vp],
     "mmt_mam_attention": [ctypes.POINTER(AttnParams), i32, vp],
@@ -55,6 +65,8 @@ _PROTOS = {
     "mmt_corner_softargmax": [vp, vp, vp, vp, vp, vp, vp, vp, vp, f32, i32, i32, i32, i32, i32, vp],
     "mmt_prroi_pool_forward": [vp, vp, vp, i32, i32, i32, i32, i64, i64, i64, i64, i32, i32, f32, i64, i64, i64, vp],
     "mmt_spm_attention": [vp, i64, vp, vp, i32, i32, i32, i32, f32, vp],
+    "mmt_sample_target": [ctypes.POINTER(CropParams), i32, vp],
+    "mmt_track_update": [vp, vp, vp, i32, i32, i32, i32, f64, vp],
 }
 
 
