@@ -95,6 +95,18 @@ typedef struct {
     const float* ln_colsum[MMT_MAX_GROUPS];
     /* 1: C2 receives a copy of C (the value C holds, in `dtype`) instead of C = v, C2 = v + R */
     int32_t c2_copy;
+    /* Split-K over workgroups (bf16 LDS-DMA kernel, GEMM and conv modes, not with ln_fold): each
+     * output tile's K-steps are cut into `splitk` slices computed by separate workgroups; every
+     * slice stores its fp32 partial tile in sk_ws, and the tile's last-arriving workgroup sums the
+     * partials in slice order (bitwise deterministic) and runs the epilogue.  splitk: 0 auto (cost
+     * model), 1 off, n >= 2 forced.  sk_ws: fp32 slab workspace of sk_ws_floats floats; sk_cnt:
+     * sk_cnt_n uint32 arrival tickets, zero before the first launch and left zero by every launch.
+     * Without both buffers (or when they are too small for the choice) no split is made. */
+    int32_t splitk;
+    float* sk_ws;
+    int64_t sk_ws_floats;
+    uint32_t* sk_cnt;
+    int64_t sk_cnt_n;
 } mmt_gemm_params;
 
 int mmt_gemm(const mmt_gemm_params* p, int dtype, void* stream);

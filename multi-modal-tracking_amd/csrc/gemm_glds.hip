@@ -22,6 +22,8 @@
 #include "common.hpp"
 #include "gemm_internal.hpp"
 
+#include <algorithm>
+
 // MMT_GEMM_ABLATE (measurement builds only, tools/build_ablate.sh): 1 = no DMA after the prologue
 // (MFMA + LDS reads + barriers alone), 2 = no MFMA work (DMA pipeline alone).
 #ifndef MMT_GEMM_ABLATE
@@ -88,13 +90,18 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
     MMT_STAMP(0, "s_memrealtime");
     MMT_STAMP(1, "s_memtime");
 
-    // XCD-aware bijective remap (see gemm.hip): each XCD gets a contiguous run of (group, tile)
-    // ids, tm fastest, so a run's W column slices and A rows stay in that XCD's L2.
-    const int nwg = gridDim.x * gridDim.z;
-    const int orig = blockIdx.x + gridDim.x * blockIdx.z;
+    // XCD-aware bijective remap (see gemm.hip): each XCD gets a contiguous run of (group, tile,
+    // K-slice) ids, slice fastest then tm, so a run's W column slices and A rows stay in that XCD's
+    // L2 and a tile's split-K partials are mostly written and summed on one XCD (speed only: the
+    // hand-off below is correct for any placement).
+    const int nsk = gridDim.y;  // split-K slices per tile
+    const int nwg = gridDim.x * gridDim.y * gridDim.z;
+    const int orig = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
     const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
     const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-    const int g = lin / gridDim.x, tile = lin - g * gridDim.x;
+    const int per_g = gridDim.x * nsk;
+    const int g = lin / per_g, rem_t = lin - g * per_g;
+    const int tile = rem_t / nsk, slice = rem_t - tile * nsk;
     const int tiles_m = (p.M + BM - 1) / BM;
     const int tm = tile % tiles_m, tn = tile / tiles_m;
     const int m0 = tm * BM, n0 = tn * BN;
@@ -137,10 +144,12 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
     const int ks = p.k_split, cin = p.conv_cin, k3 = p.conv_k3;
 
     unsigned char* ring = lds + kg * ST * STAGE;
-    const int nk = (K + KT - 1) / KT, ns = (nk + KS - 1) / KS;
+    // this slice's K-steps [kb0, kb0 + nk) of the nk_all 64-deep steps (the launcher keeps nk >= KS)
+    const int nk_all = (K + KT - 1) / KT, kb0 = slice * nk_all / nsk;
+    const int nk = (slice + 1) * nk_all / nsk - kb0, ns = (nk + KS - 1) / KS;
 
     auto issue = [&](int s) {  // this k-group's step s -> ring slot s % ST
-        const int k = min(s * KS + kg, nk - 1) * KT + pch * 8;  // this lane's 8-element chunk
+        const int k = (min(s * KS + kg, nk - 1) + kb0) * KT + pch * 8;  // this lane's 8-element chunk
         const bool kin = k < K;
         unsigned char* base = ring + (s % ST) * STAGE;
         if constexpr (!CONV) {
@@ -271,7 +280,8 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
     // every thread owns 8 consecutive columns of RPP-row strips: bias / residual loads and C / C2
     // stores are whole 256-512-B row segments per wave-instruction.
     constexpr int TP = BN + 4;  // tile row pitch (floats); +4 keeps the fragment writes 2-way
-    static_assert(BM * TP * 4 + KS * BM * 8 <= KS * ST * STAGE, "epilogue tile fits in the stage ring");
+    constexpr int FLAG_OFF = BM * TP * 4 + KS * BM * 8;  // split-K "this workgroup sums" word
+    static_assert(FLAG_OFF + 16 <= KS * ST * STAGE, "epilogue tile fits in the stage ring");
     float* ctile = (float*)lds;
     float* rstat = ctile + BM * TP;  // LNF: [KS][BM][2] partial (sum x, sum x^2) per k-group
     lds_barrier();  // every wave is past its last fragment read (the DMA ring is drained: vmcnt(0))
@@ -317,6 +327,70 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
     char* C = (char*)p.c[g];
     char* C2 = (char*)p.c2[g];
     const int tc = (threadIdx.x % TPR) * 8, tr = threadIdx.x / TPR;
+
+    // ---- split-K hand-off (cdna_hip_programming.md Guideline 16, form R1 in its counter variant):
+    // every slice stores its fp32 partial tile (the strips this thread owns below) WRITE-THROUGH
+    // (buffer_store ... sc1, so no release fence), every wave drains its stores, and after a
+    // workgroup barrier lane 0 takes an agent-scope arrival ticket.  The workgroup that draws the
+    // last ticket resets it and reads the other slices' partials with sc1 loads only (so no acquire
+    // either), summing the nsk partials in SLICE order (its own from LDS): the result does not
+    // depend on which slice arrives last.  It alone runs the epilogue.
+    if (nsk > 1) {
+        const int64_t tix = (int64_t)g * gridDim.x + tile;
+        constexpr int SLAB = BM * BN * 4;  // bytes of one partial tile
+        const __amdgpu_buffer_rsrc_t slabs = __builtin_amdgcn_make_buffer_rsrc(
+            p.sk_ws + tix * nsk * (BM * BN), (short)0, nsk * SLAB, 0x00020000);
+#pragma unroll
+        for (int ps = 0; ps < NPASS; ++ps) {
+            const int r = tr + ps * RPP, off = slice * SLAB + (r * BN + tc) * 4;
+            __builtin_amdgcn_raw_buffer_store_b128(*(const u32x4*)(ctile + r * TP + tc), slabs, off, 0, 16);
+            __builtin_amdgcn_raw_buffer_store_b128(*(const u32x4*)(ctile + r * TP + tc + 4), slabs, off + 16, 0, 16);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+        __syncthreads();
+        int* flag = (int*)(lds + FLAG_OFF);
+        if (threadIdx.x == 0) {
+            const uint32_t old = __hip_atomic_fetch_add(p.sk_cnt + tix, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int last = old == (uint32_t)(nsk - 1);
+            if (last) __hip_atomic_store(p.sk_cnt + tix, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            *flag = last;
+        }
+        __syncthreads();
+        if (!*flag) return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below
+#pragma unroll
+        for (int ps = 0; ps < NPASS; ++ps) {
+            const int r = tr + ps * RPP, off = (r * BN + tc) * 4;
+            f32x4 sa = {0.f, 0.f, 0.f, 0.f}, sb = sa;
+#pragma unroll
+            for (int q0 = 0; q0 < 8; q0 += 4) {  // 4 slices' loads in flight together, summed in order
+                u32x4 pa[4], pb[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int q = q0 + j;
+                    if (q < nsk && q != slice) {
+                        pa[j] = __builtin_amdgcn_raw_buffer_load_b128(slabs, q * SLAB + off, 0, 16);
+                        pb[j] = __builtin_amdgcn_raw_buffer_load_b128(slabs, q * SLAB + off + 16, 0, 16);
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int q = q0 + j;
+                    if (q < nsk) {
+                        if (q == slice) {
+                            sa += *(const f32x4*)(ctile + r * TP + tc);
+                            sb += *(const f32x4*)(ctile + r * TP + tc + 4);
+                        } else {
+                            sa += __builtin_bit_cast(f32x4, pa[j]);
+                            sb += __builtin_bit_cast(f32x4, pb[j]);
+                        }
+                    }
+                }
+            }
+            *(f32x4*)(ctile + r * TP + tc) = sa;  // this thread's own strip: no barrier needed
+            *(f32x4*)(ctile + r * TP + tc + 4) = sb;
+        }
+    }
     const int n = n0 + tc, nc = min(n, N - 8);
     f32x4 bn0 = {0.f, 0.f, 0.f, 0.f}, bn1 = bn0, cs0 = bn0, cs1 = bn0;
     if (bias) {
@@ -418,17 +492,15 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
 }
 
 template <int BM, int BN, int WGM, int WGN, int KS, int ST>
-void launch(const mmt_gemm_params& p, hipStream_t st) {
+void launch(const mmt_gemm_params& p, int nsk, hipStream_t st) {
     const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+    const dim3 grid(tiles, nsk, p.groups), block(64 * WGM * WGN * KS);
     if (p.conv_h > 0)
-        hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, KS, ST, true, false>), dim3(tiles, 1, p.groups),
-                           dim3(64 * WGM * WGN * KS), 0, st, p);
+        hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, KS, ST, true, false>), grid, block, 0, st, p);
     else if (p.ln_fold)
-        hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, KS, ST, false, true>), dim3(tiles, 1, p.groups),
-                           dim3(64 * WGM * WGN * KS), 0, st, p);
+        hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, KS, ST, false, true>), grid, block, 0, st, p);
     else
-        hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, KS, ST, false, false>), dim3(tiles, 1, p.groups),
-                           dim3(64 * WGM * WGN * KS), 0, st, p);
+        hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, KS, ST, false, false>), grid, block, 0, st, p);
 }
 
 bool aligned(const void* ptr, int bytes) { return ((uintptr_t)ptr & (uintptr_t)(bytes - 1)) == 0; }
@@ -448,29 +520,61 @@ int mmt_gemm_glds_bf16(const mmt_gemm_params& p, hipStream_t st, int force) {
         if (p.r[g] && !aligned(p.r[g], 16)) return 1;
         if (p.ln_fold && (!p.ln_colsum[g] || !aligned(p.ln_colsum[g], 16))) return 1;
     }
-    auto blocks = [&](int bm, int bn) { return (int64_t)((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn) * p.groups; };
+    auto tiles_of = [&](int bm, int bn) { return (int64_t)((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn); };
     const int nk = (p.K + 63) / 64;
-    int cfg = force;
+    struct Cand { int cfg, bm, bn, ks; float fixed_us, step_us; };
+    // Cost model fitted to in-kernel stamps at batch 1 (tools/gemm_stamps.py): one workgroup per
+    // CU (>= 128 KiB of LDS each), so time ~ rounds of 256 workgroups x (fixed prologue +
+    // epilogue + K-steps per workgroup x time per step).  Per-step times are per-CU LDS-fill
+    // bound: 128x128 (32 KiB/step) ~0.52 us, 128x64 with 2 k-groups ~0.52 us per pair of
+    // steps, 64x64 with 2 k-groups ~0.33 us per pair.  A K split into n slices adds the partial
+    // tile round trip of the last-arriving slice (~0.8 us + 0.5 us per 64 KiB slab it reads).
+    const Cand cands[4] = {{1, 128, 128, 1, 6.0f, 0.52f}, {2, 128, 64, 2, 5.0f, 0.52f}, {3, 64, 64, 2, 3.2f, 0.33f},
+                           {4, 128, 128, 1, 6.0f, 0.60f}};
+    // largest split the workspace allows for a candidate (each slice keeps >= ks K-steps)
+    auto max_split = [&](const Cand& c) -> int {
+        if (p.ln_fold || !p.sk_ws || !p.sk_cnt) return 1;
+        const int64_t t = tiles_of(c.bm, c.bn) * p.groups;
+        if (t > p.sk_cnt_n) return 1;
+        int n = 8;
+        while (n > 1 && ((int64_t)n * c.ks > nk || t * n * c.bm * c.bn > p.sk_ws_floats)) --n;
+        return n;
+    };
+    auto cost = [&](const Cand& c, int n) {
+        const int64_t wg = tiles_of(c.bm, c.bn) * p.groups * n;
+        const int steps = (nk + n - 1) / n;
+        const float red = n > 1 ? 0.8f + 0.5f * (float)(n - 1) * (float)(c.bm * c.bn) / 16384.f : 0.f;
+        return (float)((wg + 255) / 256) * (c.fixed_us + (float)((steps + c.ks - 1) / c.ks) * c.step_us) + red;
+    };
+    int cfg = force, nsk = 1;
     if (cfg == 0) {
-        // Cost model fitted to in-kernel stamps at batch 1 (tools/gemm_stamps.py): one workgroup per
-        // CU (>= 128 KiB of LDS each), so time ~ rounds of 256 workgroups x (fixed prologue +
-        // epilogue + K-steps per workgroup x time per step).  Per-step times are per-CU LDS-fill
-        // bound: 128x128 (32 KiB/step) ~0.52 us, 128x64 with 2 k-groups ~0.52 us per pair of
-        // steps, 64x64 with 2 k-groups ~0.33 us per pair.
-        struct Cand { int cfg, bm, bn, ks; float fixed_us, step_us; };
-        const Cand cands[3] = {{1, 128, 128, 1, 6.0f, 0.52f}, {2, 128, 64, 2, 5.0f, 0.52f}, {3, 64, 64, 2, 3.2f, 0.33f}};
         float best = 1e30f;
-        for (const Cand& c : cands) {
-            const int64_t wg = blocks(c.bm, c.bn);
-            const float t = (float)((wg + 255) / 256) * (c.fixed_us + (float)((nk + c.ks - 1) / c.ks) * c.step_us);
-            if (t < best) best = t, cfg = c.cfg;
+        for (int ci = 0; ci < 3; ++ci) {
+            const Cand& c = cands[ci];
+            const int nmax = p.splitk >= 1 ? std::min(p.splitk, max_split(c)) : max_split(c);
+            for (int n = (p.splitk >= 2 ? nmax : 1); n <= nmax; ++n) {
+                // a split must win clearly: the model prices the partial round trip loosely
+                const float t = cost(c, n) * (n > 1 && p.splitk == 0 ? 1.15f : 1.f);
+                if (t < best) best = t, cfg = c.cfg, nsk = n;
+            }
+        }
+    } else if (cfg >= 1 && cfg <= 4) {
+        const Cand& c = cands[cfg - 1];
+        if (p.splitk >= 2) {
+            nsk = std::min(p.splitk, max_split(c));
+        } else if (p.splitk == 0) {
+            float best = 1e30f;
+            for (int n = 1; n <= max_split(c); ++n) {
+                const float t = cost(c, n) * (n > 1 ? 1.15f : 1.f);
+                if (t < best) best = t, nsk = n;
+            }
         }
     }
     switch (cfg) {
-        case 1: launch<128, 128, 2, 4, 1, 4>(p, st); break;
-        case 2: launch<128, 64, 2, 2, 2, 3>(p, st); break;
-        case 3: launch<64, 64, 2, 2, 2, 4>(p, st); break;
-        case 4: launch<128, 128, 2, 2, 1, 4>(p, st); break;
+        case 1: launch<128, 128, 2, 4, 1, 4>(p, nsk, st); break;
+        case 2: launch<128, 64, 2, 2, 2, 3>(p, nsk, st); break;
+        case 3: launch<64, 64, 2, 2, 2, 4>(p, nsk, st); break;
+        case 4: launch<128, 128, 2, 2, 1, 4>(p, nsk, st); break;
         default: return 1;
     }
     return 0;

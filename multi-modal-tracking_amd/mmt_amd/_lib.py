@@ -34,6 +34,7 @@ class GemmParams(ctypes.Structure):
         ("conv_h", i32), ("conv_up", i32), ("conv_cin", i32), ("conv_k3", i32),
         ("groups", i32), ("r_t", i32), ("impl", i32),
         ("ln_fold", i32), ("ln_eps", f32), ("ln_colsum", vp * MAX_GROUPS), ("c2_copy", i32),
+        ("splitk", i32), ("sk_ws", vp), ("sk_ws_floats", i64), ("sk_cnt", vp), ("sk_cnt_n", i64),
     ]
 
 

@@ -65,6 +65,9 @@ class MixFormerRGBTRuntime:
     """Compiled forward of one of the four hot-path variants on the current CUDA (HIP) device."""
 
     gemm_impl = 0  # mmt_gemm_params.impl of every plan GEMM (0 = library's choice; A/B knob)
+    gemm_splitk = 0  # mmt_gemm_params.splitk of every plan GEMM (0 = library's choice, 1 = off)
+    SPLITK_FLOATS = 8 << 20  # fp32 split-K partial-tile workspace (32 MiB), shared by every plan GEMM
+    SPLITK_TICKETS = 1 << 16
 
     def __init__(self, state_dict, variant, dtype=torch.bfloat16, device="cuda", fold_ln=None):
         """fold_ln (default: on for bf16): the ViT's LayerNorms are folded into the qkv / fc1 GEMMs
@@ -90,6 +93,10 @@ class MixFormerRGBTRuntime:
         self._prepare(sd)
         self._ws = {}
         self._graphs = {}
+        # split-K hand-off buffers: the plan's GEMMs run one after another on one stream, so one
+        # slab workspace serves them all; the tickets start at zero and every launch leaves them so
+        self._sk_ws = torch.empty(self.SPLITK_FLOATS, device=self.device, dtype=torch.float32)
+        self._sk_cnt = torch.zeros(self.SPLITK_TICKETS, device=self.device, dtype=torch.int32)
 
     # ------------------------------------------------------------------ weights
     def _T(self, x):
@@ -294,6 +301,9 @@ class MixFormerRGBTRuntime:
             for g in range(G):
                 p.ln_colsum[g] = ln_colsum[g]
         p.c2_copy = c2_copy
+        p.splitk = self.gemm_splitk
+        p.sk_ws, p.sk_ws_floats = self._sk_ws.data_ptr(), self._sk_ws.numel()
+        p.sk_cnt, p.sk_cnt_n = self._sk_cnt.data_ptr(), self._sk_cnt.numel()
         plan.append((LIB.mmt_gemm, (ctypes_byref(p), self.cdt if dtype is None else dtype), name, p))
 
     def _build_plan(self, ws, score):

@@ -45,6 +45,9 @@ def _gemm(a, w, c, M, N, K, lda, ldc, dtype, **kw):
     p.r_t = kw.get("r_t", 0)
     p.impl = kw.get("impl", 0)
     p.c2_copy = kw.get("c2_copy", 0)
+    if kw.get("sk"):  # (splitk, slab workspace, tickets)
+        n, ws, cnt = kw["sk"]
+        p.splitk, p.sk_ws, p.sk_ws_floats, p.sk_cnt, p.sk_cnt_n = n, ws.data_ptr(), ws.numel(), cnt.data_ptr(), cnt.numel()
     L.check(L.LIB.mmt_gemm(p, L.MMT_BF16 if dtype == torch.bfloat16 else L.MMT_F32,
                            torch.cuda.current_stream().cuda_stream), "mmt_gemm")
 
@@ -153,6 +156,64 @@ def test_gemm_bf16_tile_paths(impl, M, N, K):
             r3 = Ag @ Wb[grp].float().t()
             e3 = (o3[grp].cpu() - r3).abs().max().item()
             assert e3 <= 1e-3 * r3.abs().max().item() + 1e-4, (grp, e3)
+
+
+@pytest.mark.parametrize("impl", [1, 2, 3, 4])
+@pytest.mark.parametrize("splitk", [2, 3, 5])
+@pytest.mark.parametrize("M,N,K", [(528, 768, 3072), (77, 200, 1024), (400, 192, 640)])
+def test_gemm_splitk(impl, splitk, M, N, K):
+    """Split-K over workgroups (slices summed in slice order by the last-arriving workgroup): matches
+    the reference, repeats bitwise across launches (no dependence on arrival order), handles an
+    in-place fp32 residual (C = R, the residual stream's X += ...) and a bf16 C2 copy, and leaves
+    every ticket at zero."""
+    g = torch.Generator().manual_seed(M + N + K + splitk)
+    A = torch.randn(2, M, K, generator=g).bfloat16()
+    W = (torch.randn(2, N, K, generator=g) / math.sqrt(K)).bfloat16()
+    b = torch.randn(2, N, generator=g)
+    X0 = torch.randn(2, M, N, generator=g)
+    Ad, Wd, bd = A.cuda(), W.cuda(), b.cuda()
+    ws = torch.empty(8 << 20, device="cuda")
+    cnt = torch.zeros(1 << 16, device="cuda", dtype=torch.int32)
+    ref = torch.einsum("gmk,gnk->gmn", A.float(), W.float()) + b[:, None] + X0
+    outs = []
+    for rep in range(3):
+        X = X0.cuda()
+        c2 = torch.empty(2, M, N, device="cuda", dtype=torch.bfloat16)
+        _gemm([Ad[0].data_ptr(), Ad[1].data_ptr()], [Wd[0].data_ptr(), Wd[1].data_ptr()],
+              [X[0].data_ptr(), X[1].data_ptr()], M, N, K, K, N, torch.bfloat16,
+              bias=[bd[0].data_ptr(), bd[1].data_ptr()], r=[X[0].data_ptr(), X[1].data_ptr()], ldr=N, c_f32=1,
+              c2=[c2[0].data_ptr(), c2[1].data_ptr()], c2_copy=1, impl=impl, sk=(splitk, ws, cnt))
+        torch.cuda.synchronize()
+        outs.append((X.cpu(), c2.cpu()))
+    err = (outs[0][0] - ref).abs().max().item()
+    assert err <= 1e-3 * ref.abs().max().item() + 1e-4, err
+    assert torch.equal(outs[0][1], outs[0][0].bfloat16())
+    for X, c2 in outs[1:]:
+        assert torch.equal(X, outs[0][0]) and torch.equal(c2, outs[0][1])
+    assert int(cnt.abs().sum()) == 0
+
+
+def test_gemm_splitk_conv():
+    """Split-K on the implicit-GEMM 3x3 conv (K = 9 * 96 = 864, a zero-filled K tail)."""
+    B, h, cin, cout = 2, 20, 96, 48
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(B, cin, h, h, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) / math.sqrt(9 * cin)
+    b = torch.randn(cout, generator=g)
+    xin = x.permute(0, 2, 3, 1).contiguous().bfloat16().cuda()
+    wk = w.permute(0, 2, 3, 1).reshape(cout, -1).contiguous().bfloat16().cuda()
+    bd = b.cuda()
+    ws = torch.empty(8 << 20, device="cuda")
+    cnt = torch.zeros(1 << 16, device="cuda", dtype=torch.int32)
+    ref = F.relu(F.conv2d(x.bfloat16().float(), w.bfloat16().float(), b, padding=1))
+    for impl, n in ((1, 4), (3, 3), (2, 2)):
+        out = torch.empty(B * h * h, cout, device="cuda")
+        _gemm([xin.data_ptr()], [wk.data_ptr()], [out.data_ptr()], B * h * h, cout, 9 * cin, cin, cout, torch.bfloat16,
+              bias=[bd.data_ptr()], act=2, conv=(h, 1, cin, 1), c_f32=1, impl=impl, sk=(n, ws, cnt))
+        torch.cuda.synchronize()
+        o = out.cpu().reshape(B, h, h, cout).permute(0, 3, 1, 2)
+        assert (o - ref).abs().max().item() <= 1e-3 * ref.abs().max().item() + 1e-4, (impl, n)
+    assert int(cnt.abs().sum()) == 0
 
 
 @pytest.mark.parametrize("impl", [0, 1, 2, 3, 4])

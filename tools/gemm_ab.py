@@ -18,10 +18,18 @@ from mmt_amd import _lib as L  # noqa: E402
 
 # (name, groups, M per group, N, K, act, residual) at B = 1: rgbt two-stream (groups = modalities)
 SHAPES = [("qkv_ln", 2, 528, 2304, 768, 0, 0), ("fc1_ln", 2, 528, 3072, 768, 1, 0), ("qkv", 2, 528, 2304, 768, 0, 0), ("proj", 2, 528, 768, 768, 0, 1), ("fc1", 2, 528, 3072, 768, 1, 0),
-          ("fc2", 2, 528, 768, 3072, 0, 1), ("qkv_B4", 2, 2112, 2304, 768, 0, 0), ("fc2_B4", 2, 2112, 768, 3072, 0, 1)]
+          ("fc2", 2, 528, 768, 3072, 0, 1), ("qkv_B4", 2, 2112, 2304, 768, 0, 0), ("fc2_B4", 2, 2112, 768, 3072, 0, 1),
+          ("head1_like", 1, 400, 1344, 6912, 2, 0), ("enc_lin2_like", 1, 800, 512, 2048, 0, 1),
+          ("conv2_like", 2, 400, 192, 3456, 2, 0)]
 
 
-def run(name, G, M, N, K, act, res, impl, reps):
+SK_WS = None
+
+
+def run(name, G, M, N, K, act, res, impl, reps, splitk=1):
+    global SK_WS
+    if SK_WS is None:
+        SK_WS = (torch.empty(8 << 20, device="cuda"), torch.zeros(1 << 16, device="cuda", dtype=torch.int32))
     A = torch.randn(G, M, K, device="cuda").bfloat16()
     W = (torch.randn(G, N, K, device="cuda") / K ** 0.5).bfloat16()
     b = torch.randn(G, N, device="cuda")
@@ -34,16 +42,24 @@ def run(name, G, M, N, K, act, res, impl, reps):
     p.lda, p.ldc, p.ldr = K, N, N
     p.a_seg_rows, p.a_segs_a = M, 1
     p.M, p.N, p.K, p.act, p.c_f32, p.groups, p.impl = M, N, K, act, 1 if res else 0, G, impl
+    p.splitk, p.sk_ws, p.sk_ws_floats = splitk, SK_WS[0].data_ptr(), SK_WS[0].numel()
+    p.sk_cnt, p.sk_cnt_n = SK_WS[1].data_ptr(), SK_WS[1].numel()
     if name.endswith("_ln"):  # LayerNorm folded (timing only: colsum = bias, reference check skipped)
         p.ln_fold, p.ln_eps = 1, 1e-6
         for g in range(G):
             p.ln_colsum[g] = b[g].data_ptr()
     fn = lambda: L.check(L.LIB.mmt_gemm(L.ctypes.byref(p), L.MMT_BF16,  # noqa: E731
                                         torch.cuda.current_stream().cuda_stream), name)
+    fn()
+    torch.cuda.synchronize()
+    first = C.clone()
     us = graph_time(fn, reps)
+    assert torch.equal(first, C), "%s impl %d splitk %d: repeated calls differ" % (name, impl, splitk)
     ref = torch.baddbmm(b[:, None, :], A.float(), W.float().transpose(1, 2))
-    if act:
+    if act == 1:
         ref = torch.nn.functional.gelu(ref)
+    elif act == 2:
+        ref = torch.relu(ref)
     if res:
         ref = ref + R
     err = ((C.float() - ref).abs().max() / ref.abs().max()).item() if not name.endswith("_ln") else float("nan")
@@ -82,17 +98,20 @@ def graph_time(fn, reps, per_graph=20):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=200)
-    ap.add_argument("--impls", default="-1,1,2,3,4,0")
+    ap.add_argument("--impls", default="-1,1,2,3,4,0", help="impl[:splitk] list, e.g. 1:1,1:4,0:0")
+    ap.add_argument("--only", default="", help="comma list of shape names")
     ap.add_argument("--no-torch", action="store_true")
     args = ap.parse_args()
-    impls = [int(x) for x in args.impls.split(",")]
+    impls = [tuple(int(v) for v in (x.split(":") + ["1"])[:2]) for x in args.impls.split(",")]
     rows = []
     for name, G, M, N, K, act, res in SHAPES:
+        if args.only and name not in args.only.split(","):
+            continue
         fl = 2.0 * G * M * N * K
         row = {"gemm": name, "G": G, "M": M, "N": N, "K": K}
-        for impl in impls:
-            us, err = run(name, G, M, N, K, act, res, impl, args.reps)
-            row["impl%d" % impl] = {"us": round(us, 2), "tflops": round(fl / us / 1e6, 1), "relerr": float("%.2e" % err)}
+        for impl, sk in impls:
+            us, err = run(name, G, M, N, K, act, res, impl, args.reps, sk)
+            row["impl%d:%d" % (impl, sk)] = {"us": round(us, 2), "tflops": round(fl / us / 1e6, 1), "relerr": float("%.2e" % err)}
         if not args.no_torch:
             tu = torch_ref(G, M, N, K, args.reps)
             row["torch_bmm"] = {"us": round(tu, 2), "tflops": round(fl / tu / 1e6, 1)}
