@@ -16,6 +16,8 @@ Extra fields:
                  profiles/pmc_traffic.json (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction) when it
                  was measured for this workload, else null
   roofline_mam   the same for the MAM attention kernel
+  roofline_mam_batched  the MAM attention kernel alone at the batched-inference size (SURVEY §8(e)
+                 C3: 32 frames per GPU, the grid where the throughput kernel runs), same definition
   cpu_baseline   the oracle's fp32 CPU forward (oracle/forward.py, a restatement of the reference)
                  on a bounded sample, rank 0 at N=1 only
 """
@@ -119,6 +121,40 @@ def roofline(rt, plan, times, dtype, traffic=None):
     return obj(dom), obj("mam_attention"), total, by
 
 
+def mam_batched(rt, B=32, per_graph=20, replays=5):
+    """Roofline of the MAM attention launch at B frames (2B sequences) on random bf16 q/k/v in the
+    runtime's convention (q pre-scaled), timed like kernel_profile."""
+    import ctypes
+    from mmt_amd._lib import LIB, AttnParams, MMT_BF16, check
+    d = rt.d
+    S = 2 * B
+    qkv = (torch.randn(S, d.ntok, 3 * d.C, device="cuda") * 0.5).bfloat16()
+    out = torch.empty(S, d.ntok, d.C, device="cuda", dtype=torch.bfloat16)
+    p = AttnParams()
+    p.qkv, p.out, p.S, p.Bm, p.ntok, p.n_t, p.C, p.H = qkv.data_ptr(), out.data_ptr(), S, B, d.ntok, d.n_t, d.C, d.H
+    p.asym = 1 if rt.variant in ("asym", "asym_online") else 0
+    p.scale, p.impl = 1.0 / 1.4426950408889634, 0
+    st = torch.cuda.current_stream()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(per_graph):
+            check(LIB.mmt_mam_attention(ctypes.byref(p), MMT_BF16, torch.cuda.current_stream().cuda_stream), "attn")
+    g.replay()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(replays):
+        g.replay()
+    e1.record(st)
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / (replays * per_graph)
+    lk_s = d.ntok + (d.n_t if p.asym else 0)
+    fl = 4.0 * 64 * d.H * S * (d.n_t * d.n_t + d.ns * lk_s)
+    ach = fl / (us * 1e-6) / 1e12
+    return {"kernel": "mam_attention", "bound": "mfma", "achieved": round(ach, 2), "peak": PEAK["bf16"],
+            "unit": "TFLOP/s", "frac": round(ach / PEAK["bf16"], 4), "traffic": None, "frames": B,
+            "flops_per_launch": fl, "avg_launch_us": round(us, 2)}
+
+
 def cpu_baseline(variant, B, budget_s=12.0):
     """Oracle (fp32 CPU restatement of the reference forward), bounded sample."""
     from mmt_amd import synthetic
@@ -153,6 +189,7 @@ def main():
     ap.add_argument("--no-kernel-profile", action="store_true",
                     help="skip the per-kernel timing (profiler runs that map dispatches to plan entries)")
     ap.add_argument("--dump-plan", default=None, help="write the plan's launch names (JSON) to this path")
+    ap.add_argument("--no-mam-batched", action="store_true", help="skip the batched MAM attention roofline")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -235,6 +272,8 @@ def main():
                             "tflops": round(a["flops"] / a["n"] / (a["t"] / a["n"] * 1e-3) / 1e12, 1) if a["flops"] else None}
                         for k, a in sorted(by.items(), key=lambda kv: -kv[1]["t"])} if by else None,
         }
+        if args.dtype == "bf16" and not args.no_kernel_profile and not args.no_mam_batched:
+            out["roofline_mam_batched"] = mam_batched(rt)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.variant, B)
         else:

@@ -122,8 +122,12 @@ typedef struct {
     void* out;
     int32_t S, Bm, ntok, n_t, C, H, asym;
     float scale;
-    int32_t impl; /* bf16 kernel choice (identical results up to fp32 summation order): 0 auto,
-                     2 / 4 = key tiles split over 2 / 4 groups of 4 waves */
+    int32_t impl; /* bf16 kernel choice (results equal within bf16 rounding): 0 auto (latency
+                     kernel for small grids, throughput kernel from ~200 of its workgroups);
+                     2 / 4 = latency kernel, key tiles split over 2 / 4 groups of 4 waves;
+                     8 = throughput kernel (128 queries per workgroup, 3 workgroups per CU);
+                     9 = throughput kernel, 3-deep ring, 2 workgroups per CU.  q may arrive
+                     pre-multiplied by scale*log2(e); then pass scale = 1/log2(e). */
 } mmt_attn_params;
 
 int mmt_mam_attention(const mmt_attn_params* p, int dtype, void* stream);

@@ -539,15 +539,260 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(KG, KG
     MMT_ASTAMP(5, "s_memrealtime");
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Throughput kernel for large grids (batched inference): one workgroup = 4 waves x 32 queries =
+// 128 queries of one (sequence, head), OCC workgroups per CU.  Each K / V fragment read from LDS
+// feeds two 16-query MFMA tiles (half the LDS traffic per FLOP of the latency kernel), and the
+// softmax is trimmed to one transcendental + ~1 other VALU op per score, since at d = 64 the VALU
+// work per score is as long as its 256 MFMA FLOPs:
+//   - Q arrives pre-multiplied by scale*log2(e) (folded into the qkv weights by the runtime, or
+//     applied here once if scale*log2(e) != 1), and the QK^T accumulators start at -m (the running
+//     maximum) instead of 0, so exp2 of the accumulator IS the unnormalised probability;
+//   - the running maximum is the first key tile's maximum and is raised only when a later tile's
+//     scores exceed it by more than FA_THR (log2 units; then that tile rescales O and l), so most
+//     tiles skip the rescale entirely (a wave-uniform branch);
+//   - the row sums l come from one extra MFMA per 32 keys against an all-ones operand (the same
+//     bf16 P that multiplies V), not from per-score adds.
+// K / V tiles stream through an FNS-deep LDS-DMA ring (counted vmcnt + raw barrier, one barrier
+// per tile).  The MFMA / VALU overlap comes from the OCC co-resident workgroups (a software-
+// pipelined variant with one workgroup per CU measured 2.6x slower).  When the key segments are
+// 64-aligned (n_t % 64 == 0) a tile never straddles a segment and its DMA source is one
+// wave-uniform row base plus per-lane constant offsets.
+constexpr int FQ = 128, FTILE = 2 * KB * 128;
+#ifndef MMT_ATTN_FA_MIN_WG
+#define MMT_ATTN_FA_MIN_WG 200  // workgroups of the throughput kernel from which it is chosen
+#endif
+constexpr float FA_THR = 8.f;
+
+template <int FNS, int OCC>  // ring depth, workgroups per CU
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void mam_attention_fa_kernel(
+    const mmt_attn_params p) {
+    __shared__ __attribute__((aligned(1024))) char lds[FNS * FTILE + FQ * 128];
+    char* qimg = lds + FNS * FTILE;
+
+    const int qb = blockIdx.x, h = blockIdx.y, s = blockIdx.z;
+    const int n_t = p.n_t, ntok = p.ntok, C = p.C;
+    const int nqb_t = (n_t + FQ - 1) / FQ;
+    const bool tmpl = qb < nqb_t;
+    const int q0 = tmpl ? qb * FQ : n_t + (qb - nqb_t) * FQ;
+    const int qend = tmpl ? n_t : ntok;
+    const int Lk = tmpl ? n_t : (p.asym ? ntok + n_t : ntok);
+    const bool cross = p.asym && !tmpl;
+    const int64_t rs = 3 * (int64_t)C;
+    const bf16_t* qkv = (const bf16_t*)p.qkv;
+    const int sV = s % p.Bm, sI = sV + p.Bm;
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int l16 = lane & 15, lg = lane >> 4;
+    const int prow = lane >> 3, pcol = lane & 7;
+    const int qr = l16 >> 2, pc = l16 & 3;
+
+    // ---- K / V DMA.  This wave's 4 pieces of a tile: piece w*4+i (waves 0-1: K, 2-3: V), rows
+    // pk*8 + prow of the tile, this lane's swizzled 16-B chunk.
+    const int isv = w >> 1;
+    const int64_t col = (isv ? 2 * C : C) + h * D + (isv ? (pcol ^ (prow & 6)) : (pcol ^ prow)) * 8;
+    auto key_row = [&](int kk) -> const bf16_t* {
+        int seq = s, row = kk;
+        if (cross) {
+            if (kk < n_t) seq = sV;
+            else if (kk < 2 * n_t) { seq = sI; row = kk - n_t; }
+            else row = kk - n_t;
+        }
+        return qkv + ((int64_t)seq * ntok + row) * rs;
+    };
+    const bool aligned = n_t % KB == 0;  // every tile lies in one key segment
+    const int nkt = (Lk + KB - 1) / KB;
+    auto issue_tile = [&](int t) {
+        char* slot = lds + (t % FNS) * FTILE + isv * KB * 128;
+        if (aligned && t * KB + KB <= Lk) {
+            const bf16_t* base = key_row(t * KB);  // wave-uniform
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int pk = (w & 1) * 4 + i;
+                attn_glds16(base + (int64_t)(pk * 8 + prow) * rs + col, slot + pk * 1024);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int pk = (w & 1) * 4 + i;
+                attn_glds16(key_row(min(t * KB + pk * 8 + prow, Lk - 1)) + col, slot + pk * 1024);
+            }
+        }
+    };
+    // Q image: 128 rows (16 pieces, 4 per wave); rows past the block's end re-read the last query
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int piece = w * 4 + i, r = piece * 8 + prow;
+        const bf16_t* src = qkv + ((int64_t)s * ntok + min(q0 + r, qend - 1)) * rs + h * D;
+        attn_glds16(src + ((pcol ^ prow) * 8), qimg + piece * 1024);
+    }
+    for (int t = 0; t < FNS - 1 && t < nkt; ++t) issue_tile(t);
+
+    const bool active = q0 + 32 * w < qend;  // wave-uniform: this wave has queries
+    const float cexp = p.scale * 1.4426950408889634f;
+    const bool prescale = fabsf(cexp - 1.f) > 1e-6f;
+    float mr[2] = {0.f, 0.f};
+    f32x4 o[4][2], lsum[2];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+        lsum[qt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[dt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4{0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u});
+    u32x4 qf[2][2];
+
+    for (int kt = 0; kt < nkt; ++kt) {
+        attn_wait_dyn(4 * (min(nkt - 1, kt + FNS - 2) - kt));
+        lds_barrier();  // every wave's pieces of tile kt landed; every wave is done with tile kt-1
+        if (kt + FNS - 1 < nkt) issue_tile(kt + FNS - 1);
+        if (kt == 0) {
+#pragma unroll
+            for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int row = 32 * w + 16 * qt + l16;
+                    qf[qt][u] = *(const u32x4*)(qimg + (row * 8 + ((4 * u + lg) ^ (l16 & 7))) * 16);
+                    if (prescale) {
+                        u32x4 v = qf[qt][u];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            v[e] = pack_bf16x2(__uint_as_float(v[e] << 16) * cexp,
+                                               __uint_as_float(v[e] & 0xffff0000u) * cexp);
+                        qf[qt][u] = v;
+                    }
+                }
+        }
+        if (!active) continue;
+        const char* kimg = lds + (kt % FNS) * FTILE;
+        const char* vimg = kimg + KB * 128;
+        uint2 vt[2][4][2];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int row = 32 * kk + 4 * lg + qr;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) {
+                const char* b1 = vimg + row * 128 + (((2 * dt + (pc >> 1)) ^ (row & 6)) * 16) + (pc & 1) * 8;
+                vt[kk][dt][0] = attn_tr16<0>(b1);
+                vt[kk][dt][1] = attn_tr16<16 * 128>(b1);
+            }
+        }
+        u32x4 kf[4][2];
+#pragma unroll
+        for (int kt16 = 0; kt16 < 4; ++kt16)
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+                kf[kt16][u] = *(const u32x4*)(kimg + ((kt16 * 16 + l16) * 8 + ((4 * u + lg) ^ (l16 & 7))) * 16);
+        // S^T - m: the accumulators start at -m (per query column = per lane)
+        f32x4 sacc[4][2];
+#pragma unroll
+        for (int kt16 = 0; kt16 < 4; ++kt16)
+#pragma unroll
+            for (int qt = 0; qt < 2; ++qt) {
+                sacc[kt16][qt] = f32x4{-mr[qt], -mr[qt], -mr[qt], -mr[qt]};
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+                    sacc[kt16][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kf[kt16][u]),
+                                                                             __builtin_bit_cast(bf16x8, qf[qt][u]),
+                                                                             sacc[kt16][qt], 0, 0, 0);
+            }
+        if (kt * KB + KB > Lk) {
+#pragma unroll
+            for (int kt16 = 0; kt16 < 4; ++kt16)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (kt * KB + kt16 * 16 + 4 * lg + j >= Lk) sacc[kt16][0][j] = sacc[kt16][1][j] = -1e30f;
+        }
+        float mx[2];
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
+            float m = sacc[0][qt][0];
+#pragma unroll
+            for (int kt16 = 0; kt16 < 4; ++kt16)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) m = fmaxf(m, sacc[kt16][qt][j]);
+            mx[qt] = lanegroup_max(m);
+        }
+        if (kt == 0 || __any(mx[0] > FA_THR || mx[1] > FA_THR)) {  // (re)base the running maximum
+#pragma unroll
+            for (int qt = 0; qt < 2; ++qt) {
+                const float d = kt == 0 ? mx[qt] : fmaxf(mx[qt], 0.f);
+                mr[qt] += d;
+                const float alpha = __builtin_amdgcn_exp2f(-d);
+#pragma unroll
+                for (int kt16 = 0; kt16 < 4; ++kt16) sacc[kt16][qt] -= d;
+#pragma unroll
+                for (int dt = 0; dt < 4; ++dt) o[dt][qt] *= alpha;
+                lsum[qt] *= alpha;
+            }
+        }
+#pragma unroll
+        for (int kt16 = 0; kt16 < 4; ++kt16)
+#pragma unroll
+            for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) sacc[kt16][qt][j] = __builtin_amdgcn_exp2f(sacc[kt16][qt][j]);
+        attn_lds_wait();
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            bf16x8 pf[2];
+#pragma unroll
+            for (int qt = 0; qt < 2; ++qt)
+                pf[qt] = __builtin_bit_cast(
+                    bf16x8, u32x4{pack_bf16x2(sacc[2 * kk][qt][0], sacc[2 * kk][qt][1]),
+                                  pack_bf16x2(sacc[2 * kk][qt][2], sacc[2 * kk][qt][3]),
+                                  pack_bf16x2(sacc[2 * kk + 1][qt][0], sacc[2 * kk + 1][qt][1]),
+                                  pack_bf16x2(sacc[2 * kk + 1][qt][2], sacc[2 * kk + 1][qt][3])});
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) {
+                const uint2 ua = vt[kk][dt][0], ub = vt[kk][dt][1];
+                const bf16x8 vf = __builtin_bit_cast(bf16x8, make_uint4(ua.x, ua.y, ub.x, ub.y));
+#pragma unroll
+                for (int qt = 0; qt < 2; ++qt) o[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qt], o[dt][qt], 0, 0, 0);
+            }
+#pragma unroll
+            for (int qt = 0; qt < 2; ++qt) lsum[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[qt], lsum[qt], 0, 0, 0);
+        }
+    }
+
+    // ---- normalise and store: lane holds O[q = l16][d = dt*16 + 4*lg + r]; every row of lsum = l
+    if (!active) return;
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+        const float inv = 1.f / lsum[qt][0];
+        const int q = q0 + 32 * w + 16 * qt + l16;
+        if (q < qend) {
+            bf16_t* op = (bf16_t*)p.out + ((int64_t)s * ntok + q) * C + h * D;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+                *(uint2*)(op + dt * 16 + 4 * lg) = make_uint2(pack_bf16x2(o[dt][qt][0] * inv, o[dt][qt][1] * inv),
+                                                              pack_bf16x2(o[dt][qt][2] * inv, o[dt][qt][3] * inv));
+        }
+    }
+}
+
 template <typename T>
 int launch_attn(const mmt_attn_params& p, hipStream_t st) {
-    if (p.impl != 0 && p.impl != 2 && p.impl != 4) return MMT_EBADARG;
+    if (p.impl != 0 && p.impl != 2 && p.impl != 4 && (p.impl < 8 || p.impl > 9)) return MMT_EBADARG;
     if (!p.qkv || !p.out || p.H <= 0 || p.C != p.H * D || p.S <= 0 || p.ntok <= p.n_t || p.n_t <= 0) return MMT_EBADARG;
     if (p.asym && (p.Bm <= 0 || p.S != 2 * p.Bm)) return MMT_EBADARG;
     if (((uintptr_t)p.qkv | (uintptr_t)p.out) & 15) return MMT_EBADARG;
     const int nqb = (p.n_t + 63) / 64 + (p.ntok - p.n_t + 63) / 64;
     dim3 grid(nqb, p.H, p.S);
-    if constexpr (sizeof(T) == 2) {  // bf16: LDS-DMA kernel, 64 queries x KG key groups per workgroup
+    if constexpr (sizeof(T) == 2) {
+        // large grids: the throughput kernel (128 queries per workgroup, 2 workgroups per CU);
+        // small grids (batch-1 tracking): the latency kernel (64 queries x KG key groups)
+        const int nfa = (p.n_t + FQ - 1) / FQ + (p.ntok - p.n_t + FQ - 1) / FQ;
+        const dim3 fgrid(nfa, p.H, p.S);
+        if (p.impl == 8 || (p.impl == 0 && (int64_t)nfa * p.H * p.S >= MMT_ATTN_FA_MIN_WG)) {
+            hipLaunchKernelGGL((mam_attention_fa_kernel<2, 3>), fgrid, dim3(256), 0, st, p);
+            return launch_status();
+        }
+        if (p.impl == 9) {  // ring-depth / occupancy variant (A/B): 3-deep ring, 2 workgroups per CU
+            hipLaunchKernelGGL((mam_attention_fa_kernel<3, 2>), fgrid, dim3(256), 0, st, p);
+            return launch_status();
+        }
         const int kg = p.impl > 0 ? p.impl : 4;
         if (kg == 2) hipLaunchKernelGGL(mam_attention_glds_kernel<2>, grid, dim3(512), 0, st, p);
         else hipLaunchKernelGGL(mam_attention_glds_kernel<4>, grid, dim3(1024), 0, st, p);

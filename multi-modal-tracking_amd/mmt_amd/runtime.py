@@ -31,6 +31,9 @@ from ._lib import LIB, GemmParams, AttnParams, check, MMT_F32, MMT_BF16
 VARIANTS = ("rgbt", "shared", "asym", "asym_online")
 
 
+LOG2E = 1.4426950408889634
+
+
 def _ptr(t, off=0):
     return t.data_ptr() + off * t.element_size()
 
@@ -90,6 +93,8 @@ class MixFormerRGBTRuntime:
         if self.d.C % 256 or self.d.d_model != 512 or self.d.C // 64 * 64 != self.d.C:
             raise ValueError("unsupported dims C=%d d_model=%d" % (self.d.C, self.d.d_model))
         self.w = {}
+        head_dim = self.d.C // self.d.H
+        self.q_scale = head_dim ** -0.5 * LOG2E if self.fold_ln else 1.0  # folded into the q weights
         self._prepare(sd)
         self._ws = {}
         self._graphs = {}
@@ -147,6 +152,12 @@ class MixFormerRGBTRuntime:
                     norms = ["", ] if self.variant == "rgbt" else ["_v", "_i"]
                     for lin, nm in (("attn.qkv", "norm1"), ("mlp.fc1", "norm2")):
                         w64, b64 = sd[b + lin + ".weight"].double(), sd[b + lin + ".bias"].double()
+                        if lin == "attn.qkv":
+                            # the q rows carry the attention scale * log2(e), so the MAM kernels'
+                            # exp2 takes the scores as they come (mmt_attn_params.scale = 1/log2(e))
+                            qs = torch.ones(3 * C, dtype=torch.float64, device=w64.device)
+                            qs[:C] = self.q_scale
+                            w64, b64 = w64 * qs[:, None], b64 * qs
                         fw, fc, fb = [], [], []
                         for suf in norms:
                             gam, bet = sd[b + nm + suf + ".weight"].double(), sd[b + nm + suf + ".bias"].double()
@@ -366,7 +377,7 @@ class MixFormerRGBTRuntime:
             ap = AttnParams()
             ap.qkv, ap.out, ap.S, ap.Bm, ap.ntok, ap.n_t, ap.C, ap.H = P(QKV), P(AO), S, B, ntok, d.n_t, C, d.H
             ap.asym = 1 if self.variant in ("asym", "asym_online") else 0
-            ap.scale = (C // d.H) ** -0.5
+            ap.scale = 1.0 / LOG2E if self.fold_ln else (C // d.H) ** -0.5  # see q_scale
             plan.append((LIB.mmt_mam_attention, (ctypes_byref(ap), cdt), "mam_attention", ap))
             cpx = dict(c2=rows(XN, C), c2_copy=1) if fold else {}
             self._gemm(plan, "proj", a=rows(AO, C), w=wl("attn.proj.w"), c=rows(X, C), M=Mg, N=C, K=C, lda=C,

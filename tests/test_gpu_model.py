@@ -113,3 +113,28 @@ def test_bf16_layernorm_fold_vs_explicit(variant):
         boxes.append(box.cpu().numpy().copy())
         assert np.abs(boxes[-1] - gold).max() <= 1e-2
     assert np.abs(boxes[0] - boxes[1]).max() <= 1e-2
+
+
+@pytest.mark.parametrize("variant", ["rgbt", "asym_online"])
+def test_module_api_after_cuda(variant):
+    """The drop-in path a tracker takes (mixformer_vit_rgbt.py:16-24): build -> load_state_dict ->
+    .cuda() -> .eval() -> forward([rgb, tir] lists) under no_grad, with the weights already on the
+    device when the HIP runtime prepares them."""
+    from mmt_amd import model as M
+    from mmt_amd import synthetic
+    builder = {"rgbt": M.build_mixformer_vit_rgbt, "asym_online": M.build_asymmetric_shared_online_score}[variant]
+    net = builder(M.hot_path_cfg(), train=False)
+    keys = json.load(open(GOLDEN + "/state_dict_%s.json" % variant))
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic.synth_state_dict(keys).items()}, strict=True)
+    net = net.cuda().eval()
+    t, o, s = _inputs(1)
+    score = variant == "asym_online"
+    with torch.no_grad():
+        out, coord = net(t, o, s, run_score_head=score)
+    torch.cuda.synchronize()
+    gold = np.load(GOLDEN + "/model_%s_b1.npz" % variant)
+    err = np.abs(out["pred_boxes"].cpu().numpy().reshape(1, 4) - gold["pred_boxes"].reshape(1, 4)).max()
+    assert err <= 1e-2, err
+    assert coord.shape == (1, 1, 4)
+    if score:
+        assert out["pred_scores"].shape == (1,)

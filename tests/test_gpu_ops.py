@@ -311,7 +311,7 @@ def _attn_ref(qkv, S, Bm, ntok, n_t, C, H, asym):
     return out.permute(0, 2, 1, 3).reshape(S, ntok, C)
 
 
-@pytest.mark.parametrize("dname,impl", [("f32", 0), ("bf16", 2), ("bf16", 4)])
+@pytest.mark.parametrize("dname,impl", [("f32", 0), ("bf16", 2), ("bf16", 4), ("bf16", 8), ("bf16", 9)])
 @pytest.mark.parametrize("asym", [0, 1])
 @pytest.mark.parametrize("Bm,ntok,n_t,H", [(1, 528, 128, 12), (2, 100, 36, 2), (1, 70, 8, 1), (1, 864, 288, 2)])
 def test_mam_attention(dname, impl, asym, Bm, ntok, n_t, H):
@@ -335,7 +335,7 @@ def test_mam_attention(dname, impl, asym, Bm, ntok, n_t, H):
     assert err <= (1.5e-2 if dt == torch.bfloat16 else 2e-5), err
 
 
-@pytest.mark.parametrize("dname,impl", [("f32", 0), ("bf16", 2), ("bf16", 4)])
+@pytest.mark.parametrize("dname,impl", [("f32", 0), ("bf16", 2), ("bf16", 4), ("bf16", 8), ("bf16", 9)])
 def test_mam_attention_rescale_branch(dname, impl):
     """Online-softmax rescale forced: one key per query block carries a huge score in a late tile
     (bf16: and in a different key group than the first tile, so the group merge rescales)."""
@@ -355,6 +355,33 @@ def test_mam_attention_rescale_branch(dname, impl):
     torch.cuda.synchronize()
     ref = _attn_ref(qkv.to(dt).double(), S, Bm, ntok, n_t, C, H, 0).float()
     assert (out.float().cpu() - ref).abs().max().item() < (1.5e-2 if dt == torch.bfloat16 else 5e-5)
+
+
+@pytest.mark.parametrize("impl", [2, 4, 8, 9])
+@pytest.mark.parametrize("asym", [0, 1])
+def test_mam_attention_prescaled_q(impl, asym):
+    """The runtime's convention (bf16): q arrives multiplied by scale * log2(e) (folded into the qkv
+    weights) and mmt_attn_params.scale = 1 / log2(e); both bf16 kernels must give softmax(q k^T * scale) v."""
+    L = _lib()
+    Bm, ntok, n_t, H = 3, 528, 128, 4
+    S, C = 2 * Bm, 64 * H
+    g = torch.Generator().manual_seed(77 + asym)
+    qkv = torch.randn(S, ntok, 3 * C, generator=g)
+    c = 0.125 * 1.4426950408889634
+    qs = qkv.clone()
+    qs[..., :C] *= c
+    qd = qs.bfloat16().cuda()
+    out = torch.empty(S, ntok, C, device="cuda", dtype=torch.bfloat16)
+    p = L.AttnParams()
+    p.qkv, p.out, p.S, p.Bm, p.ntok, p.n_t, p.C, p.H, p.asym = qd.data_ptr(), out.data_ptr(), S, Bm, ntok, n_t, C, H, asym
+    p.scale, p.impl = 1.0 / 1.4426950408889634, impl
+    L.check(L.LIB.mmt_mam_attention(p, L.MMT_BF16, torch.cuda.current_stream().cuda_stream), "attn")
+    torch.cuda.synchronize()
+    qr = qs.bfloat16().float()
+    qr[..., :C] /= c
+    ref = _attn_ref(qr, S, Bm, ntok, n_t, C, H, asym)
+    err = (out.float().cpu() - ref).abs().max().item()
+    assert err <= 1.5e-2, err
 
 
 @pytest.mark.parametrize("dname", ["f32", "bf16"])
