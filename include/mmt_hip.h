@@ -22,6 +22,7 @@
  *       head.py:7-20,159-198, score_decoder.py (implicit GEMM, fused epilogues)
  *   mmt_mam_attention           Attention.forward MAM softmax(QK^T)V, mixformer.py:52-78 /
  *       asymmetric_shared.py:55-104
+ *   mmt_mam_attention_bwd       its autograd (training step, train_script_mixformer*.py)
  *   mmt_layernorm / mmt_groupnorm  nn.LayerNorm / nn.GroupNorm on the hot path
  *   mmt_patch_im2col            PatchEmbed conv input staging, mixformer.py:29-34
  *   mmt_msda_bimodal            MSDeformAttn_Bimodal.forward middle part (offset/weight softmax,
@@ -128,9 +129,29 @@ typedef struct {
                      8 = throughput kernel (128 queries per workgroup, 3 workgroups per CU);
                      9 = throughput kernel, 3-deep ring, 2 workgroups per CU.  q may arrive
                      pre-multiplied by scale*log2(e); then pass scale = 1/log2(e). */
+    float* lse;   /* NULL, or [S][H][ntok] fp32: per query the log2-sum-exp2 of its pre-scaled scores
+                     (training forward; selects the throughput kernel, bf16 only) */
 } mmt_attn_params;
 
 int mmt_mam_attention(const mmt_attn_params* p, int dtype, void* stream);
+
+/* MAM attention backward (training, two-stream / shared layout: asym must be 0; bf16).  qkv / out
+ * as in the forward (q NOT pre-scaled: pass the natural `scale`), dout = dL/dout [S][ntok][C], lse
+ * from the forward with the same qkv and scale; delta: [S][H][ntok] fp32 workspace; dqkv:
+ * [S][ntok][3C] = (dL/dq, dL/dk, dL/dv) in the qkv layout.  Deterministic (no atomics).
+ * Replaces the autograd of Attention.forward, mixformer.py:52-78. */
+typedef struct {
+    const void* qkv;
+    const void* out;
+    const void* dout;
+    const float* lse;
+    float* delta;
+    void* dqkv;
+    int32_t S, Bm, ntok, n_t, C, H, asym;
+    float scale;
+} mmt_attn_bwd_params;
+
+int mmt_mam_attention_bwd(const mmt_attn_bwd_params* p, int dtype, void* stream);
 
 /* ---------------------------------------------------------------- norms / elementwise
  * LayerNorm over the last dim C (C % 256 == 0) of fp32 rows; x = in[row] (+ add[row % add_rows]);

@@ -762,6 +762,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     for (int qt = 0; qt < 2; ++qt) {
         const float inv = 1.f / lsum[qt][0];
         const int q = q0 + 32 * w + 16 * qt + l16;
+        if (q < qend && p.lse && lg == 0)  // training: log2-sum-exp2 of the pre-scaled scores
+            p.lse[((int64_t)s * p.H + h) * ntok + q] = mr[qt] + __builtin_amdgcn_logf(lsum[qt][0]);
         if (q < qend) {
             bf16_t* op = (bf16_t*)p.out + ((int64_t)s * ntok + q) * C + h * D;
 #pragma unroll
@@ -775,6 +777,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 template <typename T>
 int launch_attn(const mmt_attn_params& p, hipStream_t st) {
     if (p.impl != 0 && p.impl != 2 && p.impl != 4 && (p.impl < 8 || p.impl > 9)) return MMT_EBADARG;
+    if (p.lse && (sizeof(T) != 2 || p.impl == 9)) return MMT_EBADARG;
     if (!p.qkv || !p.out || p.H <= 0 || p.C != p.H * D || p.S <= 0 || p.ntok <= p.n_t || p.n_t <= 0) return MMT_EBADARG;
     if (p.asym && (p.Bm <= 0 || p.S != 2 * p.Bm)) return MMT_EBADARG;
     if (((uintptr_t)p.qkv | (uintptr_t)p.out) & 15) return MMT_EBADARG;
@@ -785,7 +788,7 @@ int launch_attn(const mmt_attn_params& p, hipStream_t st) {
         // small grids (batch-1 tracking): the latency kernel (64 queries x KG key groups)
         const int nfa = (p.n_t + FQ - 1) / FQ + (p.ntok - p.n_t + FQ - 1) / FQ;
         const dim3 fgrid(nfa, p.H, p.S);
-        if (p.impl == 8 || (p.impl == 0 && (int64_t)nfa * p.H * p.S >= MMT_ATTN_FA_MIN_WG)) {
+        if (p.impl == 8 || p.lse || (p.impl == 0 && (int64_t)nfa * p.H * p.S >= MMT_ATTN_FA_MIN_WG)) {
             hipLaunchKernelGGL((mam_attention_fa_kernel<2, 3>), fgrid, dim3(256), 0, st, p);
             return launch_status();
         }

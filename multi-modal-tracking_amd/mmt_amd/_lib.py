@@ -40,7 +40,13 @@ class GemmParams(ctypes.Structure):
 
 class AttnParams(ctypes.Structure):
     _fields_ = [("qkv", vp), ("out", vp), ("S", i32), ("Bm", i32), ("ntok", i32), ("n_t", i32), ("C", i32),
-                ("H", i32), ("asym", i32), ("scale", f32), ("impl", i32)]
+                ("H", i32), ("asym", i32), ("scale", f32), ("impl", i32), ("lse", vp)]
+
+
+class AttnBwdParams(ctypes.Structure):
+    _fields_ = [("qkv", vp), ("out", vp), ("dout", vp), ("lse", vp), ("delta", vp), ("dqkv", vp),
+                ("S", i32), ("Bm", i32), ("ntok", i32), ("n_t", i32), ("C", i32), ("H", i32), ("asym", i32),
+                ("scale", f32)]
 
 
 MAX_CROPS = 4
@@ -56,6 +62,7 @@ class CropParams(ctypes.Structure):
 _PROTOS = {
     "mmt_gemm": [ctypes.POINTER(GemmParams), i32, vp],
     "mmt_mam_attention": [ctypes.POINTER(AttnParams), i32, vp],
+    "mmt_mam_attention_bwd": [ctypes.POINTER(AttnBwdParams), i32, vp],
     "mmt_layernorm": [vp, vp, i64, vp, vp, vp, vp, vp, vp, i64, i64, i32, f32, i32, vp],
     "mmt_groupnorm": [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, f32, i32, vp],
     "mmt_add_cast": [vp, vp, i64, vp, vp, i64, i32, vp],
