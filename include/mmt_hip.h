@@ -23,6 +23,7 @@
  *   mmt_mam_attention           Attention.forward MAM softmax(QK^T)V, mixformer.py:52-78 /
  *       asymmetric_shared.py:55-104
  *   mmt_mam_attention_bwd       its autograd (training step, train_script_mixformer*.py)
+ *   mmt_transpose_bf16          operand transposes of the Linear backward (nn.Linear autograd)
  *   mmt_layernorm / mmt_groupnorm  nn.LayerNorm / nn.GroupNorm on the hot path
  *   mmt_patch_im2col            PatchEmbed conv input staging, mixformer.py:29-34
  *   mmt_msda_bimodal            MSDeformAttn_Bimodal.forward middle part (offset/weight softmax,
@@ -256,6 +257,13 @@ int mmt_sample_target(const mmt_crop_params* p, int n, void* stream);
  * crop[i][3] = resize_factor, clip_box(H, W, margin); the result replaces state[i]. */
 int mmt_track_update(const float* pred_cxcywh, const double* crop, double* state, int n, int H, int W,
                      int search_size, double margin, void* stream);
+
+/* ---------------------------------------------------------------- training-step helpers
+ * bf16 transpose: out[b][c][r] = in[b][r][c] for a rows x cols matrix (leading dimensions ld_in /
+ * ld_out in elements, `batch` matrices stride_in / stride_out elements apart).  Feeds the Linear
+ * backward's dX = dY W and dW = dY^T X GEMMs (both contract over a non-contiguous dimension). */
+int mmt_transpose_bf16(const void* in, void* out, int rows, int cols, int64_t ld_in, int64_t ld_out, int batch,
+                       int64_t stride_in, int64_t stride_out, void* stream);
 
 /* Library version string (for diagnostics). */
 const char* mmt_version(void);

@@ -1,0 +1,410 @@
+"""Training step of the two-stream MixFormer RGB-T tracker on the MI355X (BASELINE
+config 4): forward with autograd, the reference's box loss, backward, data-parallel gradient
+all-reduce over RCCL (DistributedDataParallel) and the AdamW update with the reference's parameter
+groups and gradient clipping.
+
+Reference: lib/train/train_script_mixformer.py:105-140 (DDP, SyncBN, MixFormerRGBTActor),
+lib/train/actors/mixformer_rgbt.py:33-168 (forward pass, CIoU + L1 loss on xyxy boxes),
+lib/utils/box_ops.py:100-152 (ciou_loss), lib/train/base_functions.py:362-400 (rgbt strategy:
+parameter groups with per-group lr multipliers, pos_embed frozen), lib/train/trainers/
+ltr_trainer.py (clip_grad_norm_ with TRAIN.GRAD_CLIP_NORM).
+
+What runs where.  The ViT backbones (≈ 85 % of the step's FLOPs) run on libmmt_hip.so through two
+autograd Functions: every Linear (patch embed as a GEMM on the unfolded patches, qkv, proj, fc1,
+fc2) forward and backward on the LDS-DMA bf16 GEMM (dX = dY W and dW = dY^T X after bf16
+transposes, fp32 accumulation, fp32 master weights), and the MAM attention forward (throughput
+kernel, log-sum-exp kept) and backward (mmt_mam_attention_bwd).  LayerNorm / GELU / residual adds,
+the deformable fusion encoder and the corner head run as PyTorch-ROCm ops on the same module tree
+(`nn.Conv2d`, `nn.GroupNorm`, `SyncBatchNorm` under DDP, `F.grid_sample` for the deformable
+sampling as the reference's ms_deform_attn_core_pytorch), in bf16 autocast like the reference's AMP
+path.  The backbone ops are injected (`ops`), so the data-parallel plumbing can be exercised on CPU
+with stand-in ops in tests; the product's ops are `HipOps` and have no CPU path.
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+LOG2E = 1.4426950408889634
+
+
+# ----------------------------------------------------------------------------- HIP backbone ops
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _transpose(x, rows, cols, ld_out=None):
+    """[rows][cols] bf16 -> [cols][ld_out] (mmt_transpose_bf16); columns rows..ld_out-1 are zero
+    (the GEMM's K must be a multiple of 8)."""
+    from ._lib import LIB, check
+    ld_out = ld_out or rows
+    alloc = torch.empty if ld_out == rows else torch.zeros
+    out = alloc(cols, ld_out, device=x.device, dtype=torch.bfloat16)
+    check(LIB.mmt_transpose_bf16(x.data_ptr(), out.data_ptr(), rows, cols, cols, ld_out, 1, 0, 0, _stream()),
+          "mmt_transpose_bf16")
+    return out
+
+
+def _gemm(a, w, M, N, K, bias=None, out_f32=False):
+    """C[M][N] = A[M][K] W[N][K]^T (+ bias), bf16 operands, fp32 accumulation (mmt_gemm)."""
+    from ._lib import LIB, GemmParams, MMT_BF16, check
+    c = torch.empty(M, N, device=a.device, dtype=torch.float32 if out_f32 else torch.bfloat16)
+    p = GemmParams()
+    p.a[0], p.w[0], p.c[0] = a.data_ptr(), w.data_ptr(), c.data_ptr()
+    p.bias[0] = bias.data_ptr() if bias is not None else None
+    p.lda, p.ldc = K, N
+    p.a_seg_rows, p.a_segs_a = M, 1
+    p.M, p.N, p.K, p.groups, p.c_f32 = M, N, K, 1, 1 if out_f32 else 0
+    check(LIB.mmt_gemm(p, MMT_BF16, _stream()), "mmt_gemm")
+    return c
+
+
+class _HipLinear(torch.autograd.Function):
+    """y = x W^T + b (nn.Linear) with bf16 operands; x [M][K] bf16, W [N][K] fp32 master, b [N]."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        M, K = x.shape
+        N = w.shape[0]
+        x = x.contiguous()
+        wb = w.detach().to(torch.bfloat16).contiguous()
+        y = _gemm(x, wb, M, N, K, bias=b.detach().float().contiguous())
+        ctx.save_for_backward(x, wb)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wb = ctx.saved_tensors
+        M, K = x.shape
+        N = wb.shape[0]
+        dy = dy.to(torch.bfloat16).contiguous()
+        dx = _gemm(dy, _transpose(wb, N, K), M, K, N) if ctx.needs_input_grad[0] else None
+        Mp = (M + 7) // 8 * 8  # contraction over tokens, zero-padded to the GEMM's K granule
+        dw = _gemm(_transpose(dy, M, N, Mp), _transpose(x, M, K, Mp), N, K, Mp, out_f32=True)
+        db = dy.float().sum(0)
+        return dx, dw, db
+
+
+class _HipMamAttention(torch.autograd.Function):
+    """MAM softmax attention (mixformer.py:52-78) over qkv [S][ntok][3C] bf16 -> [S][ntok][C] bf16."""
+
+    @staticmethod
+    def forward(ctx, qkv, n_t, heads):
+        from ._lib import LIB, AttnParams, MMT_BF16, check
+        S, ntok, C3 = qkv.shape
+        C = C3 // 3
+        qkv = qkv.contiguous()
+        out = torch.empty(S, ntok, C, device=qkv.device, dtype=torch.bfloat16)
+        lse = torch.empty(S, heads, ntok, device=qkv.device, dtype=torch.float32)
+        p = AttnParams()
+        p.qkv, p.out, p.S, p.Bm, p.ntok, p.n_t, p.C, p.H, p.asym = (qkv.data_ptr(), out.data_ptr(), S, S, ntok, n_t, C,
+                                                                 heads, 0)
+        p.scale, p.impl, p.lse = (C // heads) ** -0.5, 0, lse.data_ptr()
+        check(LIB.mmt_mam_attention(p, MMT_BF16, _stream()), "mmt_mam_attention")
+        ctx.save_for_backward(qkv, out, lse)
+        ctx.n_t, ctx.heads = n_t, heads
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        from ._lib import LIB, AttnBwdParams, MMT_BF16, check
+        qkv, out, lse = ctx.saved_tensors
+        S, ntok, C3 = qkv.shape
+        C = C3 // 3
+        dout = dout.to(torch.bfloat16).contiguous()
+        delta = torch.empty_like(lse)
+        dqkv = torch.empty_like(qkv)
+        p = AttnBwdParams()
+        p.qkv, p.out, p.dout, p.lse, p.delta, p.dqkv = (qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(),
+                                                        delta.data_ptr(), dqkv.data_ptr())
+        p.S, p.Bm, p.ntok, p.n_t, p.C, p.H, p.asym, p.scale = S, S, ntok, ctx.n_t, C, ctx.heads, 0, (C // ctx.heads) ** -0.5
+        check(LIB.mmt_mam_attention_bwd(p, MMT_BF16, _stream()), "mmt_mam_attention_bwd")
+        return dqkv, None, None
+
+
+class HipOps:
+    """The backbone's matrix work on libmmt_hip.so (bf16 in, bf16 out)."""
+
+    dtype = torch.bfloat16  # activation dtype of the GEMM / attention operands
+
+    @staticmethod
+    def linear(x, weight, bias):
+        return _HipLinear.apply(x, weight, bias)
+
+    @staticmethod
+    def mam_attention(qkv, n_t, heads):
+        return _HipMamAttention.apply(qkv, n_t, heads)
+
+
+# ----------------------------------------------------------------------------- forward
+DROP_PATH_RATE = 0.1  # get_mixformer_vit drop_path_rate (mixformer.py:311, :324); timm linear per-block schedule
+
+
+def _drop_path(x, p, training):
+    """timm DropPath: per-sample stochastic depth, survivors scaled by 1/(1-p)."""
+    if not training or p <= 0.0:
+        return x
+    keep = x.new_empty((x.shape[0],) + (1,) * (x.dim() - 1)).bernoulli_(1.0 - p)
+    return x * keep / (1.0 - p)
+
+
+def backbone_forward(bb, t, o, s, ops):
+    """VisionTransformer.forward (mixformer.py:231-259) for one modality: returns the search
+    features (B, C, gs, gs) fp32.  Tokens [template | online | search], pre-LN blocks; in training
+    mode the blocks' residual branches use stochastic depth (mixformer.py:129-138)."""
+    B = t.shape[0]
+    C = bb.pos_embed_s.shape[-1]
+    H = C // 64
+    gt, gs = bb.grid_size_t, bb.grid_size_s
+    ntok, n_t = 2 * gt * gt + gs * gs, 2 * gt * gt
+    patches = torch.cat([F.unfold(x, 16, stride=16).transpose(1, 2) for x in (t, o, s)], 1)  # (B, ntok, 3*256)
+    w = bb.patch_embed.proj.weight
+    x = ops.linear(patches.reshape(B * ntok, -1).to(ops.dtype), w.reshape(w.shape[0], -1), bb.patch_embed.proj.bias)
+    pos = torch.cat([bb.pos_embed_t, bb.pos_embed_t, bb.pos_embed_s], 1)
+    x = x.float().view(B, ntok, C) + pos
+    depth = len(bb.blocks)
+    for li, blk in enumerate(bb.blocks):
+        dp = DROP_PATH_RATE * li / max(depth - 1, 1)
+        xn = F.layer_norm(x, (C,), blk.norm1.weight, blk.norm1.bias, 1e-6).to(ops.dtype)
+        qkv = ops.linear(xn.view(B * ntok, C), blk.attn.qkv.weight, blk.attn.qkv.bias).view(B, ntok, 3 * C)
+        a = ops.mam_attention(qkv, n_t, H).view(B * ntok, C)
+        x = x + _drop_path(ops.linear(a, blk.attn.proj.weight, blk.attn.proj.bias).float().view(B, ntok, C), dp,
+                           bb.training)
+        xn = F.layer_norm(x, (C,), blk.norm2.weight, blk.norm2.bias, 1e-6).to(ops.dtype)
+        h = ops.linear(xn.view(B * ntok, C), blk.mlp.fc1.weight, blk.mlp.fc1.bias)
+        h = F.gelu(h.float()).to(ops.dtype)
+        x = x + _drop_path(ops.linear(h, blk.mlp.fc2.weight, blk.mlp.fc2.bias).float().view(B, ntok, C), dp,
+                           bb.training)
+    xs = x[:, n_t:]
+    return xs.transpose(1, 2).reshape(B, C, gs, gs)
+
+
+def _sine_pos(B, C, H, W, device):
+    """PositionEmbeddingSine(C/2, normalize=True) on an all-valid mask (position_encoding.py:34-54)."""
+    npf = C // 2
+    ones = torch.ones(B, H, W, device=device)
+    y = ones.cumsum(1)
+    x = ones.cumsum(2)
+    y = (y - 0.5) / (y[:, -1:, :] + 1e-6) * (2 * math.pi)
+    x = (x - 0.5) / (x[:, :, -1:] + 1e-6) * (2 * math.pi)
+    dim_t = 10000 ** (2 * (torch.arange(npf, device=device, dtype=torch.float32) // 2) / npf)
+    px, py = x[..., None] / dim_t, y[..., None] / dim_t
+    px = torch.stack((px[..., 0::2].sin(), px[..., 1::2].cos()), dim=4).flatten(3)
+    py = torch.stack((py[..., 0::2].sin(), py[..., 1::2].cos()), dim=4).flatten(3)
+    return torch.cat((py, px), dim=3).permute(0, 3, 1, 2)
+
+
+def _ref_points(H, W, B, L, device):
+    """get_reference_points (deformable_encoder_lnspecific.py:170-186), valid ratios 1."""
+    ry, rx = torch.meshgrid(torch.linspace(0.5, H - 0.5, H, device=device), torch.linspace(0.5, W - 0.5, W, device=device),
+                            indexing="ij")
+    ref = torch.stack((rx.reshape(-1) / W, ry.reshape(-1) / H), -1)
+    ref = torch.cat([ref] * L, 0)[None].expand(B, -1, -1)
+    return ref[:, :, None].expand(B, ref.shape[1], L, 2)
+
+
+def _msda_core(value, hw, loc, aw):
+    """ms_deform_attn_core_pytorch (ms_deform_attn_func.py:41-61): bilinear, zero padding,
+    align_corners=False; value (N, L*hw*hw, M, D), loc (N, Lq, M, L, P, 2), aw (N, Lq, M, L, P)."""
+    N, _, M, D = value.shape
+    _, Lq, _, L, P, _ = loc.shape
+    vl = value.split([hw * hw] * L, dim=1)
+    grids = 2 * loc - 1
+    outs = []
+    for lid in range(L):
+        v = vl[lid].flatten(2).transpose(1, 2).reshape(N * M, D, hw, hw)
+        g = grids[:, :, :, lid].transpose(1, 2).flatten(0, 1)
+        outs.append(F.grid_sample(v, g, mode="bilinear", padding_mode="zeros", align_corners=False))
+    aw = aw.transpose(1, 2).reshape(N * M, 1, Lq, L * P)
+    out = (torch.stack(outs, dim=-2).flatten(-2) * aw).sum(-1).view(N, M * D, Lq)
+    return out.transpose(1, 2)
+
+
+def fusion_forward(fu, s_v, s_i):
+    """Attention_Fusion_Bimodal_LNSpecific.forward (fusion_utils.py:270-279) with the deformable
+    encoder (deformable_encoder_lnspecific.py:131-160) and MSDeformAttn_Bimodal
+    (ms_deform_attn_bimodal.py:83-130)."""
+    b, _, h, w = s_v.shape
+    av, ai = fu.adjust_v(s_v), fu.adjust_i(s_i)
+    d = av.shape[1]
+    fa = fu.fusion_attention
+    pos = _sine_pos(b, d, h, w, s_v.device).flatten(2).transpose(1, 2)
+    src = torch.cat([av.flatten(2).transpose(1, 2), ai.flatten(2).transpose(1, 2)], 1)
+    lpos = torch.cat([pos + fa.level_embed[0].view(1, 1, -1), pos + fa.level_embed[1].view(1, 1, -1)], 1)
+    ref = _ref_points(h, w, b, 2, s_v.device)
+    nl = 2 * h * w
+    for layer in fa.encoder.layers:
+        sa = layer.self_attn
+        query = src + lpos
+        q_bi = torch.cat(torch.chunk(query, 2, 1), dim=2)
+        value = sa.value_proj(src).view(b, nl, sa.n_heads, d // sa.n_heads)
+        off = sa.sampling_offsets(q_bi).view(b, nl // 2, sa.n_heads, sa.n_levels, sa.n_points, 2)
+        off = torch.cat([off, off], 1)
+        aw = sa.attention_weights(q_bi).view(b, nl // 2, sa.n_heads, sa.n_levels * sa.n_points)
+        aw = F.softmax(torch.cat([aw, aw], 1).float(), -1).view(b, nl, sa.n_heads, sa.n_levels, sa.n_points)
+        loc = ref[:, :, None, :, None, :] + off.float() / torch.tensor([w, h], device=src.device, dtype=torch.float32)
+        src2 = sa.output_proj(_msda_core(value.float(), h, loc, aw))
+        src = src + layer.dropout1(src2)
+        s1, s2 = torch.chunk(src, 2, 1)
+        src = torch.cat([layer.norm1_v(s1), layer.norm1_i(s2)], 1)
+        src = src + layer.dropout3(layer.linear2(layer.dropout2(F.relu(layer.linear1(src)))))
+        s1, s2 = torch.chunk(src, 2, 1)
+        src = torch.cat([layer.norm2_v(s1), layer.norm2_i(s2)], 1)
+    o_v, o_i = torch.chunk(src, 2, 1)
+    o_v = o_v.permute(0, 2, 1).reshape(b, -1, h, w)
+    o_i = o_i.permute(0, 2, 1).reshape(b, -1, h, w)
+    return fu.adjust_cat(torch.cat([o_v, o_i], 1))
+
+
+def _soft_argmax(score_map, stride):
+    """head.py:200-212, coord grids :138-145 (x = stride * col, y = stride * row)."""
+    B, _, H, W = score_map.shape
+    idx = torch.arange(0, H, device=score_map.device).view(-1, 1) * stride
+    coord_x = idx.repeat((H, 1)).view((H * W,)).float()
+    coord_y = idx.repeat((1, H)).view((H * W,)).float()
+    prob = F.softmax(score_map.float().view(-1, H * W), dim=1)
+    return (coord_x * prob).sum(1), (coord_y * prob).sum(1)
+
+
+def head_forward(hd, x):
+    """Pyramid_Corner_Predictor.forward / get_score_map (head.py:147-212) -> (B, 4) xyxy in [0, 1]."""
+    up = lambda t, f: F.interpolate(t, scale_factor=f)  # noqa: E731
+    coords = []
+    for br in ("tl", "br"):
+        g = lambda n: getattr(hd, n + "_" + br)  # noqa: E731
+        x1 = g("conv1")(x)
+        x2 = g("conv2")(x1)
+        x3 = g("conv3")(up(g("adjust1")(x), 2) + up(x2, 2))
+        x4 = g("conv4")(up(g("adjust2")(x), 4) + up(x3, 2))
+        sm = g("conv5")(x4) + up(g("adjust3")(x2), 4) + up(g("adjust4")(x3), 2)
+        coords += list(_soft_argmax(sm, hd.stride))
+    return torch.stack(coords, dim=1) / hd.img_sz
+
+
+def forward_boxes(net, template, online_template, search, ops):
+    """MixFormer_RGBT.forward (mixformer.py:366-395) + forward_box_head (:419-432): pred_boxes
+    (B, 1, 4) cxcywh."""
+    s_v = backbone_forward(net.backbone_v, template[0], online_template[0], search[0], ops)
+    s_i = backbone_forward(net.backbone_i, template[1], online_template[1], search[1], ops)
+    with torch.autocast(s_v.device.type, dtype=torch.bfloat16, enabled=s_v.device.type == "cuda"):
+        fused = fusion_forward(net.fusion_vi, s_v, s_i)
+        xyxy = head_forward(net.box_head, fused)
+    x0, y0, x1, y1 = xyxy.float().unbind(-1)
+    return torch.stack([(x0 + x1) / 2, (y0 + y1) / 2, (x1 - x0), (y1 - y0)], -1).view(-1, 1, 4)
+
+
+# ----------------------------------------------------------------------------- loss / optimizer
+def ciou_loss(b1, b2):
+    """lib/utils/box_ops.py:100-152 for equal-length (N, 4) xyxy sets: (mean(1 - ciou), iou)."""
+    w1, h1 = b1[:, 2] - b1[:, 0], b1[:, 3] - b1[:, 1]
+    w2, h2 = b2[:, 2] - b2[:, 0], b2[:, 3] - b2[:, 1]
+    cx1, cy1 = (b1[:, 0] + b1[:, 2]) / 2.0, (b1[:, 1] + b1[:, 3]) / 2.0
+    cx2, cy2 = (b2[:, 0] + b2[:, 2]) / 2.0, (b2[:, 1] + b2[:, 3]) / 2.0
+    il, ir = torch.max(cx1 - w1 / 2, cx2 - w2 / 2), torch.min(cx1 + w1 / 2, cx2 + w2 / 2)
+    it, ib = torch.max(cy1 - h1 / 2, cy2 - h2 / 2), torch.min(cy1 + h1 / 2, cy2 + h2 / 2)
+    inter = torch.clamp(ir - il, min=0) * torch.clamp(ib - it, min=0)
+    cl, cr = torch.min(cx1 - w1 / 2, cx2 - w2 / 2), torch.max(cx1 + w1 / 2, cx2 + w2 / 2)
+    ct, cb = torch.min(cy1 - h1 / 2, cy2 - h2 / 2), torch.max(cy1 + h1 / 2, cy2 + h2 / 2)
+    inter_diag = (cx2 - cx1) ** 2 + (cy2 - cy1) ** 2
+    c_diag = torch.clamp(cr - cl, min=0) ** 2 + torch.clamp(cb - ct, min=0) ** 2
+    union = w1 * h1 + w2 * h2 - inter
+    u = inter_diag / c_diag
+    iou = inter / union
+    v = (4 / (math.pi ** 2)) * torch.pow(torch.atan(w2 / h2) - torch.atan(w1 / h1), 2)
+    with torch.no_grad():
+        alpha = (iou > 0.5).float() * v / (1 - iou + v)
+    cious = torch.clamp(iou - u - alpha * v, min=-1.0, max=1.0)
+    return torch.mean(1 - cious), iou
+
+
+def box_loss(pred_cxcywh, gt_xywh, iou_weight=2.0, l1_weight=5.0):
+    """MixFormerRGBTActor.compute_losses (actors/mixformer_rgbt.py:127-168)."""
+    xc, yc, w, h = pred_cxcywh.view(-1, 4).unbind(-1)
+    pred = torch.stack([xc - 0.5 * w, yc - 0.5 * h, xc + 0.5 * w, yc + 0.5 * h], -1)
+    x, y, gw, gh = gt_xywh.unbind(-1)
+    gt = torch.stack([x, y, x + gw, y + gh], -1).clamp(min=0.0, max=1.0)
+    ciou, iou = ciou_loss(pred, gt)
+    l1 = F.l1_loss(pred, gt)
+    return iou_weight * ciou + l1_weight * l1, {"ciou": ciou.detach(), "l1": l1.detach(), "iou": iou.detach().mean()}
+
+
+def param_groups(net, lr):
+    """base_functions.py:362-400 (rgbt strategy): pos_embed frozen; backbone_i 0.1 lr, backbone_v
+    0.02 lr, box_head 0.02 lr, fusion 1.0 lr except sampling_offsets / reference_points 0.1 lr."""
+    named = list(net.named_parameters())
+    for n, p in named:
+        p.requires_grad = "pos_embed" not in n
+    proj = ("reference_points", "sampling_offsets")
+    sel = lambda f: [p for n, p in named if p.requires_grad and f(n)]  # noqa: E731
+    return [
+        {"params": sel(lambda n: "backbone_i" in n), "lr": 0.1 * lr},
+        {"params": sel(lambda n: "backbone_v" in n), "lr": 0.02 * lr},
+        {"params": sel(lambda n: "box_head" in n), "lr": 0.02 * lr},
+        {"params": sel(lambda n: "fusion_vi" in n and not any(k in n for k in proj))},
+        {"params": sel(lambda n: "fusion_vi" in n and any(k in n for k in proj)), "lr": 0.1 * lr},
+    ]
+
+
+def synthetic_batch(B, device, generator=None, template=128, search=320):
+    """LaSOT-shaped synthetic pairs: N(0,1) images, search box label xywh with the
+    centre at 0.5 +- 0.1 and the size in [0.1, 0.5] (normalised to the search crop)."""
+    g = generator
+    t = [torch.randn(B, 3, template, template, generator=g).to(device) for _ in range(2)]
+    o = [torch.randn(B, 3, template, template, generator=g).to(device) for _ in range(2)]
+    s = [torch.randn(B, 3, search, search, generator=g).to(device) for _ in range(2)]
+    wh = 0.1 + 0.4 * torch.rand(B, 2, generator=g)
+    c = 0.5 + 0.2 * (torch.rand(B, 2, generator=g) - 0.5)
+    return t, o, s, torch.cat([c - wh / 2, wh], 1).to(device)
+
+
+class TrainStep:
+    """One optimisation step: forward, loss, backward, (DDP all-reduce), clip, AdamW.
+
+    net: the two-stream model (mmt_amd.model.build_mixformer_vit_rgbt) on the device, or its DDP
+    wrapper's module; ddp: the DistributedDataParallel wrapper when world > 1 (its forward is the
+    hook point of the gradient all-reduce)."""
+
+    def __init__(self, net, ops, lr=1e-4, weight_decay=1e-4, grad_clip=0.1, iou_weight=2.0, l1_weight=5.0,
+                 ddp=False):
+        self.net = net
+        self.ops = ops
+        self.grad_clip, self.iou_weight, self.l1_weight = grad_clip, iou_weight, l1_weight
+        self.opt = torch.optim.AdamW(param_groups(net, lr), lr=lr, weight_decay=weight_decay)
+        if ddp and next(net.parameters()).is_cuda:  # train_script_mixformer.py:105
+            net = self.net = torch.nn.SyncBatchNorm.convert_sync_batchnorm(net)
+        if ddp:
+            self.model = torch.nn.parallel.DistributedDataParallel(_Wrapped(net, ops), broadcast_buffers=False)
+        else:
+            self.model = _Wrapped(net, ops)
+
+    def backward(self, t, o, s, gt_xywh):
+        """Forward, loss and backward; under DDP the gradient all-reduce runs inside backward()."""
+        self.opt.zero_grad(set_to_none=True)
+        pred = self.model(t, o, s)
+        loss, stats = box_loss(pred, gt_xywh, self.iou_weight, self.l1_weight)
+        loss.backward()
+        stats["loss"] = loss.detach()
+        return stats
+
+    def apply(self):
+        """Gradient clipping (TRAIN.GRAD_CLIP_NORM) and the AdamW update."""
+        if self.grad_clip > 0:
+            torch.nn.utils.clip_grad_norm_(self.net.parameters(), self.grad_clip)
+        self.opt.step()
+
+    def __call__(self, t, o, s, gt_xywh):
+        stats = self.backward(t, o, s, gt_xywh)
+        self.apply()
+        return stats
+
+
+class _Wrapped(torch.nn.Module):
+    """nn.Module view of forward_boxes (DDP needs a module whose forward runs the graph)."""
+
+    def __init__(self, net, ops):
+        super().__init__()
+        self.net = net
+        self.ops = ops
+
+    def forward(self, t, o, s):
+        return forward_boxes(self.net, t, o, s, self.ops)

@@ -88,3 +88,103 @@ def test_attention_backward_deterministic():
     a = _run_fwd_bwd(qkv, dout, S, ntok, n_t, H)
     b = _run_fwd_bwd(qkv, dout, S, ntok, n_t, H)
     assert all(torch.equal(x, y) for x, y in zip(a, b))
+
+
+@pytest.mark.parametrize("rows,cols", [(64, 64), (528, 768), (1056, 2304), (37, 200), (300, 13)])
+def test_transpose_bf16_bit_exact(rows, cols):
+    from mmt_amd.train import _transpose
+    x = torch.randn(rows, cols, generator=torch.Generator().manual_seed(rows * cols)).bfloat16().cuda()
+    y = _transpose(x, rows, cols)
+    torch.cuda.synchronize()
+    assert torch.equal(y.cpu(), x.cpu().t().contiguous())
+
+
+@pytest.mark.parametrize("M,N,K", [(1056, 2304, 768), (1056, 768, 3072), (130, 96, 768)])
+def test_hip_linear_autograd(M, N, K):
+    """_HipLinear (bf16 operands, fp32 accumulation) against fp32 autograd on the same bf16 values."""
+    from mmt_amd.train import HipOps
+    g = torch.Generator().manual_seed(M + N + K)
+    x = torch.randn(M, K, generator=g).bfloat16()
+    w = (torch.randn(N, K, generator=g) * K ** -0.5)
+    b = torch.randn(N, generator=g)
+    dy = torch.randn(M, N, generator=g).bfloat16()
+    xg = x.cuda().requires_grad_(True)
+    wg, bg = w.cuda().requires_grad_(True), b.cuda().requires_grad_(True)
+    y = HipOps.linear(xg, wg, bg)
+    y.backward(dy.cuda())
+    xr = x.float().requires_grad_(True)
+    wr, br = w.bfloat16().float().requires_grad_(True), b.clone().requires_grad_(True)
+    yr = torch.nn.functional.linear(xr, wr, br)
+    yr.backward(dy.float())
+    for got, ref, nm in ((y, yr, "y"), (xg.grad, xr.grad, "dx"), (wg.grad, wr.grad, "dw"), (bg.grad, br.grad, "db")):
+        err = (got.float().cpu() - ref.detach()).abs().max().item() / ref.detach().abs().max().item()
+        print("%s rel err %.3g" % (nm, err))
+        assert err <= 1e-2, (nm, err)
+
+
+class _TorchBf16Ops:
+    """Same bf16 roundings as HipOps, PyTorch-ROCm ops (hipBLASLt GEMMs, fp32 softmax): measures
+    how far bf16 alone moves the gradients from fp32, so the HIP path is held to that bar."""
+
+    dtype = torch.bfloat16
+
+    @staticmethod
+    def linear(x, weight, bias):
+        return torch.nn.functional.linear(x.bfloat16(), weight.bfloat16(), bias.bfloat16())
+
+    @staticmethod
+    def mam_attention(qkv, n_t, heads):
+        import sys
+        import os
+        sys.path.insert(0, os.path.dirname(__file__))
+        from test_train import TorchOps
+        return TorchOps.mam_attention(qkv.float(), n_t, heads).bfloat16()
+
+
+def test_train_step_gpu_matches_fp32_grads():
+    """One two-stream training step at the bench shapes (128/320, B=2): HIP backbone ops in bf16 vs
+    the fp32 stand-in on the CPU.  Loss within 2e-2; each parameter group's gradient within
+    max(5e-2, 1.5 x the PyTorch-bf16 path's own distance from fp32) (relative L2); then a few steps
+    on the fixed batch lower the loss."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_train import TorchOps
+    from mmt_amd.model import build_mixformer_vit_rgbt, hot_path_cfg
+    from mmt_amd.train import HipOps, TrainStep, synthetic_batch
+    torch.manual_seed(0)
+    net = build_mixformer_vit_rgbt(hot_path_cfg(), train=False)
+    with torch.no_grad():
+        for br in ("tl", "br"):
+            getattr(net.box_head, "conv5_" + br).weight.mul_(30.0)
+    net.eval()
+    batch = synthetic_batch(2, "cpu", torch.Generator().manual_seed(7))
+    ref_step = TrainStep(net, TorchOps)
+    ref_stats = ref_step.backward(*batch)
+    ref_grads = {n: p.grad.clone() for n, p in net.named_parameters() if p.grad is not None}
+    net.cuda()
+    gb = [[x.cuda() for x in batch[i]] for i in range(3)] + [batch[3].cuda()]
+    tb_stats = TrainStep(net, _TorchBf16Ops).backward(*gb)
+    tb_grads = {n: p.grad.float().cpu() for n, p in net.named_parameters() if p.grad is not None}
+    step = TrainStep(net, HipOps)
+    stats = step.backward(*gb)
+    torch.cuda.synchronize()
+    print("loss hip %.5f torch-bf16 %.5f fp32 %.5f" % (stats["loss"].item(), tb_stats["loss"].item(),
+                                                      ref_stats["loss"].item()))
+    assert abs(stats["loss"].item() - ref_stats["loss"].item()) <= 2e-2
+    params = dict(net.named_parameters())
+    bad = []
+    for grp in ("backbone_v", "backbone_i", "fusion_vi", "box_head"):
+        names = [n for n in ref_grads if n.startswith(grp)]
+        ref = torch.cat([ref_grads[n].flatten() for n in names])
+        got = torch.cat([params[n].grad.float().cpu().flatten() for n in names])
+        tb = torch.cat([tb_grads[n].flatten() for n in names])
+        rel, rel_tb = ((got - ref).norm() / ref.norm()).item(), ((tb - ref).norm() / ref.norm()).item()
+        print("%s grad rel L2: hip %.3g, torch-bf16 %.3g" % (grp, rel, rel_tb))
+        if rel > max(5e-2, 1.5 * rel_tb):
+            bad.append((grp, rel, rel_tb))
+    assert not bad, bad
+    step.apply()
+    losses = [step(*gb)["loss"].item() for _ in range(4)]
+    print("losses", losses)
+    assert losses[-1] < stats["loss"].item(), losses

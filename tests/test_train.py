@@ -1,0 +1,146 @@
+"""Training step on CPU: the step's autograd graph against the oracle's, and the
+data-parallel gradient exchange over a world_size-2 gloo group.
+
+The backbone's matrix work is injected (`ops`); here it is a plain fp32 PyTorch stand-in (test
+infrastructure, like the oracle), so these tests check the step's structure — forward, box loss
+(actors/mixformer_rgbt.py:127-168), parameter groups (base_functions.py:362-400), DDP averaging,
+clip + AdamW — while tests/test_gpu_train.py checks the HIP ops themselves on the MI355X.
+Small images (64 px search, 32 px template) keep the full-width ViT-B step within seconds."""
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import ROOT
+
+SEARCH, TEMPLATE = 64, 32
+
+
+class TorchOps:
+    """fp32 stand-in for HipOps: nn.Linear and the MAM softmax attention (mixformer.py:52-78)."""
+
+    dtype = torch.float32
+
+    @staticmethod
+    def linear(x, weight, bias):
+        return F.linear(x, weight, bias)
+
+    @staticmethod
+    def mam_attention(qkv, n_t, heads):
+        S, ntok, C3 = qkv.shape
+        C = C3 // 3
+        q, k, v = qkv.view(S, ntok, 3, heads, C // heads).permute(2, 0, 3, 1, 4)
+        sc = (C // heads) ** -0.5
+        ot = torch.softmax(q[:, :, :n_t] @ k[:, :, :n_t].transpose(-1, -2) * sc, -1) @ v[:, :, :n_t]
+        os_ = torch.softmax(q[:, :, n_t:] @ k.transpose(-1, -2) * sc, -1) @ v
+        return torch.cat([ot, os_], 2).transpose(1, 2).reshape(S, ntok, C)
+
+
+def _net(seed=0):
+    from mmt_amd.model import build_mixformer_vit_rgbt, hot_path_cfg
+    torch.manual_seed(seed)
+    net = build_mixformer_vit_rgbt(hot_path_cfg(search=SEARCH, template=TEMPLATE), train=False)
+    with torch.no_grad():  # non-trivial corner heatmaps (default init is near-flat)
+        for br in ("tl", "br"):
+            getattr(net.box_head, "conv5_" + br).weight.mul_(30.0)
+    return net.eval()  # BatchNorm on running statistics (SyncBN needs a GPU)
+
+
+def _batch(B, seed):
+    from mmt_amd.train import synthetic_batch
+    return synthetic_batch(B, "cpu", torch.Generator().manual_seed(seed), TEMPLATE, SEARCH)
+
+
+def test_forward_and_grads_match_oracle():
+    from mmt_amd.train import box_loss, forward_boxes
+    from oracle.forward import forward as oracle_forward
+    torch.set_num_threads(8)
+    net = _net()
+    t, o, s, gt = _batch(2, 1)
+    pred = forward_boxes(net, t, o, s, TorchOps)
+    loss, _ = box_loss(pred, gt)
+    loss.backward()
+
+    sd = {k: v.detach().clone() for k, v in net.state_dict().items()}
+    leaves = {k: sd[k].requires_grad_() for k, p in net.named_parameters() if p.requires_grad}
+    ref, _ = oracle_forward.__wrapped__(sd, "rgbt", t, o, s)  # undecorated: autograd on
+    ref_loss, _ = box_loss(ref["pred_boxes"], gt)
+    ref_loss.backward()
+    assert (pred - ref["pred_boxes"]).abs().max().item() < 1e-5
+    assert abs(loss.item() - ref_loss.item()) < 1e-5
+    for k, p in net.named_parameters():
+        if not p.requires_grad:
+            continue
+        g, rg = p.grad, leaves[k].grad
+        assert g is not None and rg is not None, k
+        # 1e-3 of the tensor's largest gradient; the 1e-6 floor covers the corner-map biases, whose
+        # exact gradient is 0 (softmax is shift-invariant) and whose computed one is rounding noise.
+        assert (g - rg).abs().max().item() <= 1e-3 * rg.abs().max().item() + 1e-6, k
+
+
+def test_param_groups_follow_reference():
+    from mmt_amd.train import param_groups
+    net = _net()
+    groups = param_groups(net, 1e-4)
+    lrs = [g.get("lr", 1e-4) for g in groups]
+    assert lrs == pytest.approx([1e-5, 2e-6, 2e-6, 1e-4, 1e-5])
+    grouped = {id(p) for g in groups for p in g["params"]}
+    for n, p in net.named_parameters():
+        assert (id(p) in grouped) == ("pos_embed" not in n), n
+        assert p.requires_grad == ("pos_embed" not in n), n
+
+
+def test_train_step_reduces_loss_on_fixed_batch():
+    from mmt_amd.train import TrainStep
+    torch.set_num_threads(8)
+    net = _net()
+    step = TrainStep(net, TorchOps, lr=1e-4)
+    batch = _batch(2, 3)
+    losses = [step(*batch)["loss"].item() for _ in range(4)]
+    assert losses[-1] < losses[0], losses
+
+
+def _ddp_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+    from mmt_amd.train import TrainStep
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(4)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        net = _net()
+        step = TrainStep(net, TorchOps, lr=1e-4, ddp=True)
+        t, o, s, gt = _batch(2, 5)
+        sl = slice(rank, rank + 1)  # each rank its own sequence of the global batch of 2
+        step.backward([x[sl] for x in t], [x[sl] for x in o], [x[sl] for x in s], gt[sl])
+        grads = {n: p.grad.clone() for n, p in net.named_parameters() if p.grad is not None}
+        step.apply()
+        params = {n: p.detach().clone() for n, p in net.named_parameters()}
+        torch.save({"grads": grads, "params": params}, os.path.join(out_dir, "rank%d.pt" % rank))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ddp_gloo_two_ranks_matches_full_batch(tmp_path):
+    import socket
+    import torch.multiprocessing as mp
+    from mmt_amd.train import TrainStep
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    mp.spawn(_ddp_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
+
+    torch.set_num_threads(8)
+    net = _net()
+    step = TrainStep(net, TorchOps, lr=1e-4)
+    step.backward(*_batch(2, 5))
+    full = {n: p.grad for n, p in net.named_parameters() if p.grad is not None}
+    assert set(full) == set(r0["grads"]) == set(r1["grads"])
+    for n, g in full.items():
+        assert torch.equal(r0["grads"][n], r1["grads"][n]), n  # all-reduced: identical on both ranks
+        scale = g.abs().max().item() + 1e-12
+        assert (r0["grads"][n] - g).abs().max().item() <= 1e-4 * scale + 1e-6, n  # mean over ranks == batch mean
+    for n in r0["params"]:
+        assert torch.equal(r0["params"][n], r1["params"][n]), n  # replicas stay in lockstep
