@@ -56,7 +56,8 @@ def plan_flops(rt, entry):
         return 2.0 * keep.M * keep.N * keep.K * keep.groups
     d = rt.d
     lk_s = d.ntok + (d.n_t if keep.asym else 0)
-    return 4.0 * 64 * keep.H * keep.S * (d.n_t * d.n_t + d.ns * lk_s)
+    qpart = getattr(keep, "q_part", 0)
+    return 4.0 * 64 * keep.H * keep.S * ((d.n_t * d.n_t if qpart != 2 else 0) + (d.ns * lk_s if qpart != 1 else 0))
 
 
 def kernel_profile(rt, plan, per_graph=20, replays=5):
@@ -155,6 +156,37 @@ def mam_batched(rt, B=32, per_graph=20, replays=5):
             "flops_per_launch": fl, "avg_launch_us": round(us, 2)}
 
 
+def kv_cache_tracking(rt, pool, score, steps, warmup):
+    """Tracking-loop rate with the template K/V cache: per frame only the search
+    pass (one graph replay per resident input set, zero-copy); the template pass runs once per
+    template update (every 200 frames in the reference's TEST.UPDATE_INTERVALS) and is timed
+    separately.  Returns frames/s of the search pass, its ms, and the template pass's ms."""
+    t0_, o0_, _ = pool[0]
+    tplan = rt.plan_for_inputs(t0_, o0_, None, part="t")
+    tg = rt.capture_plan(tplan)
+    sg = [rt.capture_plan(rt.plan_for_inputs(None, None, s, run_score_head=score, part="s")) for _, _, s in pool]
+    tg.replay()
+    for i in range(warmup):
+        sg[i % len(sg)].replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        sg[i % len(sg)].replay()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    n_t = 20
+    t1 = time.perf_counter()
+    for _ in range(n_t):
+        tg.replay()
+    torch.cuda.synchronize()
+    tel = time.perf_counter() - t1
+    B = t0_[0].shape[0]
+    return {"value": round(B * steps / el, 2), "unit": "frames/s", "ms_per_step": round(el / steps * 1e3, 4),
+            "template_pass_ms": round(tel / n_t * 1e3, 4),
+            "note": "search-only pass per frame against the cached template K/V (template pass once per "
+                    "template update); not the headline `value`, which runs the full template+search forward"}
+
+
 def cpu_baseline(variant, B, budget_s=12.0):
     """Oracle (fp32 CPU restatement of the reference forward), bounded sample."""
     from mmt_amd import synthetic
@@ -190,6 +222,7 @@ def main():
                     help="skip the per-kernel timing (profiler runs that map dispatches to plan entries)")
     ap.add_argument("--dump-plan", default=None, help="write the plan's launch names (JSON) to this path")
     ap.add_argument("--no-mam-batched", action="store_true", help="skip the batched MAM attention roofline")
+    ap.add_argument("--no-kv-cache", action="store_true", help="skip the template K/V cache tracking-rate line")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -274,6 +307,8 @@ def main():
         }
         if args.dtype == "bf16" and not args.no_kernel_profile and not args.no_mam_batched:
             out["roofline_mam_batched"] = mam_batched(rt)
+        if use_graph and not args.no_kv_cache:
+            out["tracking_kv_cache"] = kv_cache_tracking(rt, pool, score, args.steps, args.warmup)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.variant, B)
         else:

@@ -109,6 +109,11 @@ typedef struct {
     int64_t sk_ws_floats;
     uint32_t* sk_cnt;
     int64_t sk_cnt_n;
+    /* Output row map (GEMM mode): c_seg_rows > 0 stores logical row m at physical row
+     * (m / c_seg_rows) * c_seg_pitch + m % c_seg_rows of C and C2, and reads R there when
+     * r_mode == 0 -- e.g. the search rows [n_t, ntok) of every sequence of a [S][ntok] stream
+     * (c, c2, r offset by n_t rows; c_seg_rows = ntok - n_t, c_seg_pitch = ntok). 0: identity. */
+    int64_t c_seg_rows, c_seg_pitch;
 } mmt_gemm_params;
 
 int mmt_gemm(const mmt_gemm_params* p, int dtype, void* stream);
@@ -132,6 +137,10 @@ typedef struct {
                      pre-multiplied by scale*log2(e); then pass scale = 1/log2(e). */
     float* lse;   /* NULL, or [S][H][ntok] fp32: per query the log2-sum-exp2 of its pre-scaled scores
                      (training forward; selects the throughput kernel, bf16 only) */
+    int32_t q_part; /* 0: all queries; 1: template queries [0,n_t) only; 2: search queries
+                       [n_t,ntok) only -- the template K/V cache: template rows of qkv computed
+                       once per template update, only the search rows per frame.  Rows of `out`
+                       outside the part are not written. */
 } mmt_attn_params;
 
 int mmt_mam_attention(const mmt_attn_params* p, int dtype, void* stream);

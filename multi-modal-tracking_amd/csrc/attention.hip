@@ -39,9 +39,9 @@ __global__ __launch_bounds__(256 / QT) void mam_attention_kernel(const mmt_attn_
     __shared__ u32x4 kl[2][KB * KCH];
     __shared__ __attribute__((aligned(16))) char vl[2][KB * VROW];
 
-    const int qb = blockIdx.x, h = blockIdx.y, s = blockIdx.z;
     const int n_t = p.n_t, ntok = p.ntok, C = p.C;
     const int nqb_t = (n_t + 63) / 64;
+    const int qb = blockIdx.x + (p.q_part == 2 ? nqb_t : 0), h = blockIdx.y, s = blockIdx.z;
     const bool tmpl = qb < nqb_t;
     const int q0 = tmpl ? qb * 64 : n_t + (qb - nqb_t) * 64;
     const int qend = tmpl ? n_t : ntok;
@@ -333,9 +333,9 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(KG, KG
     MMT_ASTAMP(0, "s_memrealtime");
     MMT_ASTAMP(1, "s_memtime");
 
-    const int qb = blockIdx.x, h = blockIdx.y, s = blockIdx.z;
     const int n_t = p.n_t, ntok = p.ntok, C = p.C;
     const int nqb_t = (n_t + 63) / 64;
+    const int qb = blockIdx.x + (p.q_part == 2 ? nqb_t : 0), h = blockIdx.y, s = blockIdx.z;
     const bool tmpl = qb < nqb_t;
     const int q0 = tmpl ? qb * 64 : n_t + (qb - nqb_t) * 64;
     const int qend = tmpl ? n_t : ntok;
@@ -571,9 +571,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     __shared__ __attribute__((aligned(1024))) char lds[FNS * FTILE + FQ * 128];
     char* qimg = lds + FNS * FTILE;
 
-    const int qb = blockIdx.x, h = blockIdx.y, s = blockIdx.z;
     const int n_t = p.n_t, ntok = p.ntok, C = p.C;
     const int nqb_t = (n_t + FQ - 1) / FQ;
+    const int qb = blockIdx.x + (p.q_part == 2 ? nqb_t : 0), h = blockIdx.y, s = blockIdx.z;
     const bool tmpl = qb < nqb_t;
     const int q0 = tmpl ? qb * FQ : n_t + (qb - nqb_t) * FQ;
     const int qend = tmpl ? n_t : ntok;
@@ -781,12 +781,18 @@ int launch_attn(const mmt_attn_params& p, hipStream_t st) {
     if (!p.qkv || !p.out || p.H <= 0 || p.C != p.H * D || p.S <= 0 || p.ntok <= p.n_t || p.n_t <= 0) return MMT_EBADARG;
     if (p.asym && (p.Bm <= 0 || p.S != 2 * p.Bm)) return MMT_EBADARG;
     if (((uintptr_t)p.qkv | (uintptr_t)p.out) & 15) return MMT_EBADARG;
-    const int nqb = (p.n_t + 63) / 64 + (p.ntok - p.n_t + 63) / 64;
+    if (p.q_part < 0 || p.q_part > 2) return MMT_EBADARG;
+    // q_part: 0 all queries, 1 template queries only, 2 search queries only (template K/V cache)
+    auto qblocks = [&](int qt) {
+        const int t = (p.n_t + qt - 1) / qt, sr = (p.ntok - p.n_t + qt - 1) / qt;
+        return p.q_part == 1 ? t : p.q_part == 2 ? sr : t + sr;
+    };
+    const int nqb = qblocks(64);
     dim3 grid(nqb, p.H, p.S);
     if constexpr (sizeof(T) == 2) {
         // large grids: the throughput kernel (128 queries per workgroup, 2 workgroups per CU);
         // small grids (batch-1 tracking): the latency kernel (64 queries x KG key groups)
-        const int nfa = (p.n_t + FQ - 1) / FQ + (p.ntok - p.n_t + FQ - 1) / FQ;
+        const int nfa = qblocks(FQ);
         const dim3 fgrid(nfa, p.H, p.S);
         if (p.impl == 8 || p.lse || (p.impl == 0 && (int64_t)nfa * p.H * p.S >= MMT_ATTN_FA_MIN_WG)) {
             hipLaunchKernelGGL((mam_attention_fa_kernel<2, 3>), fgrid, dim3(256), 0, st, p);

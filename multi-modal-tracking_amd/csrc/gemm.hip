@@ -242,8 +242,9 @@ __global__ __launch_bounds__(256 * KS) void gemm_kernel(const mmt_gemm_params p)
                 if (p.act == 1) v = gelu_erf(v);
                 else if (p.act == 2) v = fmaxf(v, 0.f);
                 float rv = 0.f;
+                const int64_t cm = p.c_seg_rows > 0 ? (m / p.c_seg_rows) * p.c_seg_pitch + m % p.c_seg_rows : m;
                 if (R) {
-                    int64_t rr = m;
+                    int64_t rr = cm;
                     if (p.r_mode == 1) rr = m % p.r_p0;
                     else if (p.r_mode == 2) {
                         const int hw = p.r_p0 * p.r_p0, b = m / hw, rem = m - b * hw;
@@ -252,7 +253,7 @@ __global__ __launch_bounds__(256 * KS) void gemm_kernel(const mmt_gemm_params p)
                     }
                     rv = p.r_t ? to_f<T>(((const T*)R)[rr * p.ldr + n]) : R[rr * p.ldr + n];
                 }
-                const int64_t off = ((int64_t)m * p.ldc + n) * osz;
+                const int64_t off = (cm * p.ldc + n) * osz;
                 const float out1 = C2 ? v : v + rv;
                 if (p.c_f32) *(float*)(C + off) = out1;
                 else *(T*)(C + off) = from_f<T>(out1);
@@ -298,6 +299,7 @@ int launch_gemm(const mmt_gemm_params& p, hipStream_t st) {
     }
     if (p.r_mode == 2 && (p.r_p1 < 1 || p.r_p0 % p.r_p1)) return MMT_EBADARG;
     if (p.r_mode == 1 && p.r_p0 < 1) return MMT_EBADARG;
+    if (p.c_seg_rows < 0 || (p.c_seg_rows > 0 && (p.conv_h > 0 || p.c_seg_pitch < p.c_seg_rows))) return MMT_EBADARG;
     for (int g = 0; g < p.groups; ++g) {
         if (!p.a[g] || !p.w[g] || !p.c[g]) return MMT_EBADARG;
         if (((uintptr_t)p.a[g] | (uintptr_t)p.w[g]) & 15) return MMT_EBADARG;

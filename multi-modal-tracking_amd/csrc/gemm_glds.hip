@@ -402,6 +402,9 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
         cs1 = *(const f32x4*)(p.ln_colsum[g] + nc + 4);
     }
     const float inv_k = 1.f / (float)K;
+    // output row map (template K/V cache: search rows of a [S][ntok] stream); identity if c_seg_rows == 0
+    const int64_t csr = p.c_seg_rows > 0 ? p.c_seg_rows : INT64_MAX, csp = p.c_seg_pitch;
+    auto crow = [&](int m) -> int64_t { return csr == INT64_MAX ? (int64_t)m : (m / csr) * csp + m % csr; };
     constexpr int PG = NPASS < 4 ? NPASS : 4;  // passes whose residual loads are in flight together
 #pragma unroll
     for (int p0 = 0; p0 < NPASS; p0 += PG) {
@@ -411,7 +414,7 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
             ra[i] = rb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
             if (R) {  // wave-uniform; loads unconditional from a clamped row
                 const int m = min(m0 + tr + (p0 + i) * RPP, M - 1);
-                int64_t rr = m;
+                int64_t rr = crow(m);
                 if (p.r_mode == 1) rr = m % p.r_p0;
                 else if (p.r_mode == 2) {
                     const int hw = p.r_p0 * p.r_p0, b = m / hw, rem = m - b * hw;
@@ -463,7 +466,7 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
             const bool split_c2 = C2 && !p.c2_copy;           // C = v, C2 = v + R
             const f32x4 oa = split_c2 ? va : sa, ob = split_c2 ? vb : sb;
             if (m < M && n < N) {
-                const int64_t e = (int64_t)m * p.ldc + n;
+                const int64_t e = crow(m) * p.ldc + n;
                 if (p.c_f32) {
                     *(f32x4*)((float*)C + e) = oa;
                     *(f32x4*)((float*)C + e + 4) = ob;

@@ -35,12 +35,13 @@ class GemmParams(ctypes.Structure):
         ("groups", i32), ("r_t", i32), ("impl", i32),
         ("ln_fold", i32), ("ln_eps", f32), ("ln_colsum", vp * MAX_GROUPS), ("c2_copy", i32),
         ("splitk", i32), ("sk_ws", vp), ("sk_ws_floats", i64), ("sk_cnt", vp), ("sk_cnt_n", i64),
+        ("c_seg_rows", i64), ("c_seg_pitch", i64),
     ]
 
 
 class AttnParams(ctypes.Structure):
     _fields_ = [("qkv", vp), ("out", vp), ("S", i32), ("Bm", i32), ("ntok", i32), ("n_t", i32), ("C", i32),
-                ("H", i32), ("asym", i32), ("scale", f32), ("impl", i32), ("lse", vp)]
+                ("H", i32), ("asym", i32), ("scale", f32), ("impl", i32), ("lse", vp), ("q_part", i32)]
 
 
 class AttnBwdParams(ctypes.Structure):

@@ -219,12 +219,14 @@ class _HipTracker(nn.Module):
         super().__init__()
         self.head_type = head_type
         self._rt = None
+        self._online_batch = None
         self.compute_dtype = torch.bfloat16 if os.environ.get("MMT_DTYPE", "bf16") == "bf16" else torch.float32
         self.use_hip_graph = True
         self.register_load_state_dict_post_hook(lambda m, keys: m.refresh_kernels())
 
     def refresh_kernels(self):
         self._rt = None
+        self._online_batch = None
 
     def set_compute_dtype(self, dtype):
         self.compute_dtype = dtype
@@ -233,6 +235,7 @@ class _HipTracker(nn.Module):
 
     def _apply(self, fn, *args, **kwargs):
         self._rt = None
+        self._online_batch = None
         return super()._apply(fn, *args, **kwargs)
 
     def _runtime(self, device):
@@ -270,6 +273,39 @@ class _HipTracker(nn.Module):
             feats = X.permute(0, 1, 3, 2).reshape(2, B, d.C, d.gs, d.gs).clone()
             fused = ws["FUS"].view(B, d.ns, d.C).permute(0, 2, 1).reshape(B, d.C, d.gs, d.gs).clone()
             return out, coord, feats[0], feats[1], fused
+
+    # ------------------------------------------------------------------ template K/V cache
+    # The RGB MixFormer's online API (lib/models/mixformer_vit/mixformer.py:308-323: set_online
+    # caches the template tokens' qkv in every block, forward_test runs only the search tokens),
+    # defined for the RGB-T models whose own versions are broken (reference defect D2).  Both
+    # take [rgb, tir] lists; the result equals forward() on the same template / search.
+    def set_online(self, template, online_template):
+        for nm, x in (("template", template), ("online_template", online_template)):
+            if not isinstance(x, (list, tuple)) or len(x) != 2:
+                raise ValueError("%s must be a list [rgb, tir] of (B,3,H,W) tensors" % nm)
+        dev = template[0].device
+        if dev.type != "cuda":
+            raise RuntimeError("the MI355X forward needs the inputs on the HIP device (got %s); there is no CPU path" % dev)
+        rt = self._runtime(dev)
+        with torch.cuda.device(dev):
+            rt.set_template(template, online_template)
+        self._online_batch = template[0].shape[0]
+
+    def forward_test(self, search, run_score_head=False, gt_bboxes=None):
+        if not isinstance(search, (list, tuple)) or len(search) != 2:
+            raise ValueError("search must be a list [rgb, tir] of (B,3,H,W) tensors")
+        if getattr(self, "_online_batch", None) != search[0].shape[0]:
+            raise RuntimeError("forward_test needs set_online() with the same batch size first")
+        dev = search[0].device
+        rt = self._runtime(dev)
+        score = bool(run_score_head) and self.variant == "asym_online"
+        with torch.cuda.device(dev):
+            box, sc = rt.forward_search(search, run_score_head=score)
+            coord = box.clone().view(-1, 1, 4)
+            out = {"pred_boxes": coord}
+            if score:
+                out["pred_scores"] = sc.clone()
+            return out, coord
 
 
 class MixFormer_RGBT(_HipTracker):

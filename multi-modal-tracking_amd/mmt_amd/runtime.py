@@ -283,7 +283,7 @@ class MixFormerRGBTRuntime:
     # ------------------------------------------------------------------ plan construction
     def _gemm(self, plan, name, *, a, w, c, M, N, K, lda, ldc, bias=None, r=None, ldr=0, c2=None, a1=None,
               k_split=0, act=0, c_f32=0, seg=None, r_mode=0, r_p0=0, r_p1=1, conv=None, r_t=0, dtype=None,
-              ln_colsum=None, ln_eps=0.0, c2_copy=0):
+              ln_colsum=None, ln_eps=0.0, c2_copy=0, cmap=None):
         p = GemmParams()
         G = len(a)
         for g in range(G):
@@ -312,50 +312,76 @@ class MixFormerRGBTRuntime:
             for g in range(G):
                 p.ln_colsum[g] = ln_colsum[g]
         p.c2_copy = c2_copy
+        if cmap is not None:
+            p.c_seg_rows, p.c_seg_pitch = cmap
         p.splitk = self.gemm_splitk
         p.sk_ws, p.sk_ws_floats = self._sk_ws.data_ptr(), self._sk_ws.numel()
         p.sk_cnt, p.sk_cnt_n = self._sk_cnt.data_ptr(), self._sk_cnt.numel()
         plan.append((LIB.mmt_gemm, (ctypes_byref(p), self.cdt if dtype is None else dtype), name, p))
 
     def _build_plan(self, ws, score):
-        d, W, B = self.d, self.w, ws["B"]
         plan = []
-        C, ntok, ns, nt1, dm = d.C, d.ntok, d.ns, d.nt1, d.d_model
+        self._plan_backbone(plan, ws, None)
+        self._plan_tail(plan, ws, score)
+        return plan
+
+    def _plan_backbone(self, plan, ws, part, qkv_layers=None):
+        """Patch embed + the ViT blocks over the token rows of `part`: None = all rows; "t" = the
+        template rows [0, n_t) of every sequence; "s" = the search rows [n_t, ntok).  A part's GEMMs
+        address their rows in the [S][ntok] streams through the A segment map and the output row
+        map (c_seg_rows / c_seg_pitch), and its attention launch takes the matching query part.
+        Template queries never attend search keys (the MAM is asymmetric, mixformer.py:61-76), so
+        the "t" pass run once per template update followed by "s" passes per frame equals the full
+        forward exactly, provided each layer's qkv rows persist: qkv_layers gives one
+        [S*ntok][3C] buffer per layer (None: the one QKV buffer, reused by every layer)."""
+        d, W, B = self.d, self.w, ws["B"]
+        C, ntok = d.C, d.ntok
         S = 2 * B
         R = S * ntok
         two = self.variant == "rgbt"
         P = _ptr
-        X, XN, QKV, AO, HID = ws["X"], ws["XN"], ws["QKV"], ws["AO"], ws["HID"]
+        X, XN, AO, HID = ws["X"], ws["XN"], ws["AO"], ws["HID"]
         cdt = self.cdt
+        off, nr = {None: (0, ntok), "t": (0, d.n_t), "s": (d.n_t, d.ns)}[part]
+
+        def rmap(ld):  # A segment map + output row map of the part's rows (identity for part None)
+            if part is None:
+                return {}
+            return dict(seg=(nr, 1 << 30, ntok * ld, 0), cmap=(nr, ntok))
+
+        def at(t, ld, g=0):  # first row of the part in group g's block of B sequences
+            return P(t, (g * B * ntok + off) * ld)
         # --- patch embed (im2col + GEMM, + bias + pos-embed) -> X  (fold: + its bf16 copy XN)
         fold = self.fold_ln
         plan.append((LIB.mmt_patch_im2col, tuple(P(t) for t in ws["in_t"]) + tuple(P(t) for t in ws["in_o"])
                      + tuple(P(t) for t in ws["in_s"]) + (P(ws["PATCH"]), B, d.ht, d.hs, d.patch, cdt), "patch_im2col", None))
         KP = 3 * d.patch * d.patch
-        gm = B * ntok
+        gm = B * nr  # rows per modality group
         cp = dict(c2_copy=1) if fold else {}
+        pos_at = lambda g: P(W["bb"][g]["pos"], off * C)  # noqa: E731  (pos rows of the part)
         if two:
             if fold:
-                cp["c2"] = [P(XN), P(XN, gm * C)]
-            self._gemm(plan, "patch_gemm", a=[P(ws["PATCH"]), P(ws["PATCH"], gm * KP)],
-                       w=[P(W["bb"][g]["patch_w"]) for g in range(2)], c=[P(X), P(X, gm * C)], M=gm, N=C, K=KP,
+                cp["c2"] = [at(XN, C, 0), at(XN, C, 1)]
+            self._gemm(plan, "patch_gemm", a=[at(ws["PATCH"], KP, 0), at(ws["PATCH"], KP, 1)],
+                       w=[P(W["bb"][g]["patch_w"]) for g in range(2)], c=[at(X, C, 0), at(X, C, 1)], M=gm, N=C, K=KP,
                        lda=KP, ldc=C, bias=[P(W["bb"][g]["patch_b"]) for g in range(2)],
-                       r=[P(W["bb"][g]["pos"]) for g in range(2)], ldr=C, r_mode=1, r_p0=ntok, c_f32=1, **cp)
+                       r=[pos_at(g) for g in range(2)], ldr=C, r_mode=1, r_p0=nr, c_f32=1, **cp, **rmap(KP))
         else:
             if fold:
-                cp["c2"] = [P(XN)]
-            self._gemm(plan, "patch_gemm", a=[P(ws["PATCH"])], w=[P(W["bb"][0]["patch_w"])], c=[P(X)], M=R, N=C, K=KP,
-                       lda=KP, ldc=C, bias=[P(W["bb"][0]["patch_b"])], r=[P(W["bb"][0]["pos"])], ldr=C, r_mode=1,
-                       r_p0=ntok, c_f32=1, **cp)
+                cp["c2"] = [at(XN, C)]
+            self._gemm(plan, "patch_gemm", a=[at(ws["PATCH"], KP)], w=[P(W["bb"][0]["patch_w"])], c=[at(X, C)],
+                       M=S * nr, N=C, K=KP, lda=KP, ldc=C, bias=[P(W["bb"][0]["patch_b"])], r=[pos_at(0)], ldr=C,
+                       r_mode=1, r_p0=nr, c_f32=1, **cp, **rmap(KP))
         # --- transformer blocks
         for i in range(d.depth):
+            QKV = ws["QKV"] if qkv_layers is None else qkv_layers[i]
             if two:
                 blks = [W["bb"][g]["blocks"][i] for g in range(2)]
                 n1 = [blks[0]["norm1"], blks[1]["norm1"]]
                 n2 = [blks[0]["norm2"], blks[1]["norm2"]]
                 wl = lambda nm: [P(blks[g][nm]) for g in range(2)]  # noqa: E731
                 fl = lambda nm: [P(blks[g][nm][0]) for g in range(2)]  # noqa: E731
-                rows = lambda t, k: [P(t), P(t, gm * k)]  # noqa: E731
+                rows = lambda t, k: [at(t, k, 0), at(t, k, 1)]  # noqa: E731
                 Mg = gm
             else:
                 blk = W["bb"][0]["blocks"][i]
@@ -363,36 +389,49 @@ class MixFormerRGBTRuntime:
                 n2 = [blk["norm2_v"], blk["norm2_i"]]
                 wl = lambda nm: [P(blk[nm])]  # noqa: E731
                 fl = lambda nm: [P(blk[nm][m]) for m in range(2)]  # noqa: E731
-                rows = lambda t, k: [P(t)]  # noqa: E731
-                Mg = R
-            rows2 = lambda t, k: [P(t), P(t, gm * k)]  # noqa: E731  (one group per modality)
+                rows = lambda t, k: [at(t, k)]  # noqa: E731
+                Mg = S * nr
+            rows2 = lambda t, k: [at(t, k, 0), at(t, k, 1)]  # noqa: E731  (one group per modality)
             if fold:  # LayerNorm 1 folded into qkv: A = XN = bf16 copy of the residual stream X
                 self._gemm(plan, "qkv", a=rows2(XN, C), w=fl("attn.qkv.fw"), c=rows2(QKV, 3 * C), M=gm, N=3 * C,
-                           K=C, lda=C, ldc=3 * C, bias=fl("attn.qkv.fb"), ln_colsum=fl("attn.qkv.fcs"), ln_eps=1e-6)
-            else:
+                           K=C, lda=C, ldc=3 * C, bias=fl("attn.qkv.fb"), ln_colsum=fl("attn.qkv.fcs"), ln_eps=1e-6,
+                           **rmap(C))
+            else:  # (the fp32 LayerNorm runs over all rows; rows outside the part are not read)
                 plan.append((LIB.mmt_layernorm, (P(X), None, 0, None, P(XN), P(n1[0][0]), P(n1[0][1]), P(n1[1][0]),
-                                                 P(n1[1][1]), R, gm, C, 1e-6, cdt), "ln1", None))
+                                                 P(n1[1][1]), R, B * ntok, C, 1e-6, cdt), "ln1", None))
                 self._gemm(plan, "qkv", a=rows(XN, C), w=wl("attn.qkv.w"), c=rows(QKV, 3 * C), M=Mg, N=3 * C, K=C,
-                           lda=C, ldc=3 * C, bias=wl("attn.qkv.b"))
+                           lda=C, ldc=3 * C, bias=wl("attn.qkv.b"), **rmap(C))
             ap = AttnParams()
             ap.qkv, ap.out, ap.S, ap.Bm, ap.ntok, ap.n_t, ap.C, ap.H = P(QKV), P(AO), S, B, ntok, d.n_t, C, d.H
             ap.asym = 1 if self.variant in ("asym", "asym_online") else 0
             ap.scale = 1.0 / LOG2E if self.fold_ln else (C // d.H) ** -0.5  # see q_scale
+            ap.q_part = {None: 0, "t": 1, "s": 2}[part]
             plan.append((LIB.mmt_mam_attention, (ctypes_byref(ap), cdt), "mam_attention", ap))
             cpx = dict(c2=rows(XN, C), c2_copy=1) if fold else {}
             self._gemm(plan, "proj", a=rows(AO, C), w=wl("attn.proj.w"), c=rows(X, C), M=Mg, N=C, K=C, lda=C,
-                       ldc=C, bias=wl("attn.proj.b"), r=rows(X, C), ldr=C, c_f32=1, **cpx)
+                       ldc=C, bias=wl("attn.proj.b"), r=rows(X, C), ldr=C, c_f32=1, **cpx, **rmap(C))
             if fold:
                 self._gemm(plan, "fc1", a=rows2(XN, C), w=fl("mlp.fc1.fw"), c=rows2(HID, d.hidden), M=gm, N=d.hidden,
                            K=C, lda=C, ldc=d.hidden, bias=fl("mlp.fc1.fb"), act=1, ln_colsum=fl("mlp.fc1.fcs"),
-                           ln_eps=1e-6)
+                           ln_eps=1e-6, **rmap(C))
             else:
                 plan.append((LIB.mmt_layernorm, (P(X), None, 0, None, P(XN), P(n2[0][0]), P(n2[0][1]), P(n2[1][0]),
-                                                 P(n2[1][1]), R, gm, C, 1e-6, cdt), "ln2", None))
+                                                 P(n2[1][1]), R, B * ntok, C, 1e-6, cdt), "ln2", None))
                 self._gemm(plan, "fc1", a=rows(XN, C), w=wl("mlp.fc1.w"), c=rows(HID, d.hidden), M=Mg, N=d.hidden,
-                           K=C, lda=C, ldc=d.hidden, bias=wl("mlp.fc1.b"), act=1)
+                           K=C, lda=C, ldc=d.hidden, bias=wl("mlp.fc1.b"), act=1, **rmap(C))
             self._gemm(plan, "fc2", a=rows(HID, d.hidden), w=wl("mlp.fc2.w"), c=rows(X, C), M=Mg, N=C, K=d.hidden,
-                       lda=d.hidden, ldc=C, bias=wl("mlp.fc2.b"), r=rows(X, C), ldr=C, c_f32=1, **cpx)
+                       lda=d.hidden, ldc=C, bias=wl("mlp.fc2.b"), r=rows(X, C), ldr=C, c_f32=1, **cpx,
+                       **rmap(d.hidden))
+
+    def _plan_tail(self, plan, ws, score):
+        """Fusion, corner head (and score head) on the backbone output's search rows."""
+        d, W, B = self.d, self.w, ws["B"]
+        C, ntok, ns, dm = d.C, d.ntok, d.ns, d.d_model
+        R = 2 * B * ntok
+        P = _ptr
+        X, XN = ws["X"], ws["XN"]
+        cdt = self.cdt
+        fold = self.fold_ln
         if fold:
             XT = XN  # the last fc2 already wrote the bf16 copy of the backbone output
         else:
@@ -403,7 +442,7 @@ class MixFormerRGBTRuntime:
         Mf = B * ns
         self._gemm(plan, "fusion_adjust", a=[P(XT, d.n_t * C), P(XT, B * ntok * C + d.n_t * C)],
                    w=[P(W["adj_v.w"]), P(W["adj_i.w"])], c=[P(Y1), P(Y1, Mf * dm)], M=Mf, N=dm, K=C, lda=C, ldc=dm,
-                   bias=[P(W["adj_v.b"]), P(W["adj_i.b"])], seg=(ns, 1 << 40, ntok * C, 0), c_f32=1)
+                   bias=[P(W["adj_v.b"]), P(W["adj_i.b"])], seg=(ns, 1 << 30, ntok * C, 0), c_f32=1)
         plan.append((LIB.mmt_groupnorm, (P(Y1), P(SRC), P(SRCT), P(W["adj_v.gn"][0]), P(W["adj_v.gn"][1]),
                                          P(W["adj_i.gn"][0]), P(W["adj_i.gn"][1]), 2 * B, B, ns, dm, 32, 1e-5, cdt),
                      "fusion_gn", None))
@@ -547,15 +586,70 @@ class MixFormerRGBTRuntime:
             self.run_plan(ws["plan_score"] if score else ws["plan"])
         return ws["BOX"], (ws["SC"].view(-1) if score else None)
 
-    def plan_for_inputs(self, template, online_template, search, run_score_head=False):
-        """The plan of batch B with its patch staging reading the given device tensors directly
-        (zero-copy: for frames already resident in HBM, e.g. written there by the preprocessing)."""
-        B = template[0].shape[0]
+    # ------------------------------------------------------------------ template K/V cache
+    def cache_workspace(self, B):
+        """Workspace of batch B plus the template K/V cache (the RGB MixFormer's
+        set_online / forward_test, mixformer_vit/mixformer.py:308-323, which the RGB-T models
+        lack, reference defect D2): one qkv buffer per layer, whose template rows the template
+        pass ("plan_t") fills once per template update and whose search rows each frame's pass
+        ("plan_s"; "plan_s_score" with the score head) fills before the layer's attention reads
+        all of them.  Template queries attend template keys only, so template + search passes
+        reproduce the full forward (same kernels, same per-row arithmetic)."""
         ws = self.workspace(B)
+        if "plan_t" not in ws:
+            d = self.d
+            ws["QKVL"] = [torch.empty(2 * B * d.ntok, 3 * d.C, device=self.device, dtype=self.dtype)
+                          for _ in range(d.depth)]
+            ws["plan_t"] = []
+            self._plan_backbone(ws["plan_t"], ws, "t", ws["QKVL"])
+            for score in ((False, True) if self.variant == "asym_online" else (False,)):
+                plan = []
+                self._plan_backbone(plan, ws, "s", ws["QKVL"])
+                self._plan_tail(plan, ws, score)
+                ws["plan_s_score" if score else "plan_s"] = plan
+        return ws
+
+    def set_template(self, template, online_template):
+        """Template pass: template + online template ([rgb, tir] lists of (B,3,h,h) fp32 device
+        tensors) through the backbone, filling the per-layer K/V cache (and the final template
+        token states the score head reads)."""
+        B = template[0].shape[0]
+        ws = self.cache_workspace(B)
+        for dst, src in zip(ws["in_t"] + ws["in_o"], list(template) + list(online_template)):
+            if src.shape != dst.shape:
+                raise ValueError("input shape %s, expected %s" % (tuple(src.shape), tuple(dst.shape)))
+            dst.copy_(src, non_blocking=True)
+        self.run_plan(ws["plan_t"])
+
+    def forward_search(self, search, run_score_head=False):
+        """Search pass against the cached template (set_template first, same batch size): boxes
+        (B,4) cxcywh and scores as forward() returns them."""
+        B = search[0].shape[0]
+        ws = self.cache_workspace(B)
         score = bool(run_score_head) and self.variant == "asym_online"
-        base = ws["plan_score"] if score else ws["plan"]
+        for dst, src in zip(ws["in_s"], list(search)):
+            if src.shape != dst.shape:
+                raise ValueError("input shape %s, expected %s" % (tuple(src.shape), tuple(dst.shape)))
+            dst.copy_(src, non_blocking=True)
+        self.run_plan(ws["plan_s_score"] if score else ws["plan_s"])
+        return ws["BOX"], (ws["SC"].view(-1) if score else None)
+
+    def plan_for_inputs(self, template, online_template, search, run_score_head=False, part=None):
+        """The plan of batch B with its patch staging reading the given device tensors directly
+        (zero-copy: for frames already resident in HBM, e.g. written there by the preprocessing).
+        part None: the full forward; "t": the template pass (search may be None); "s": the search
+        pass against the cache (template / online_template may be None)."""
+        B = (search if part == "s" else template)[0].shape[0]
+        ws = self.workspace(B) if part is None else self.cache_workspace(B)
+        score = bool(run_score_head) and self.variant == "asym_online"
+        key = {None: "plan", "t": "plan_t", "s": "plan_s"}[part]
+        base = ws[key + "_score" if score and part != "t" else key]
         fn, args, name, keep = base[0]
         assert name == "patch_im2col"
+        if part == "t":
+            search = ws["in_s"]
+        elif part == "s":
+            template, online_template = ws["in_t"], ws["in_o"]
         srcs = list(template) + list(online_template) + list(search)
         for src, dst in zip(srcs, ws["in_t"] + ws["in_o"] + ws["in_s"]):
             if src.shape != dst.shape or src.dtype != torch.float32 or not src.is_contiguous() or src.device != dst.device:

@@ -81,8 +81,13 @@ class RGBTTrackerCore:
     asymmetric_shared_online tracker's score-gated online-template update."""
 
     def __init__(self, network, template_factor, template_size, search_factor, search_size, update_intervals,
-                 multimodal, online_score=False, use_graph=True):
+                 multimodal, online_score=False, use_graph=True, kv_cache=True):
         self.net = network
+        # kv_cache: the template tokens' per-layer qkv are computed once per template update (a
+        # separate template pass) and each frame runs only the search tokens (runtime.cache_workspace)
+        self.kv_cache = bool(kv_cache)
+        self._tmpl_dirty = True
+        self._tmpl_graph = self._tmpl_plan = None
         self.tf, self.ts, self.sf, self.ss = float(template_factor), int(template_size), float(search_factor), int(search_size)
         self.update_intervals = list(update_intervals)
         self.online_score = bool(online_score)
@@ -134,8 +139,14 @@ class RGBTTrackerCore:
         self._keep = [crop_params(self.frames[m], self.state, self.sf, self.ss, out=self.search[m].view(-1),
                                   crop=self.search_crop[m], lut=self.lut if m == 1 else None) for m in range(2)]
         arr = (CropParams * 2)(*self._keep)
-        model_plan = rt.plan_for_inputs(self.template, self.online_template, self.search, run_score_head=score)
+        part = "s" if self.kv_cache else None
+        model_plan = rt.plan_for_inputs(self.template, self.online_template, self.search, run_score_head=score,
+                                        part=part)
         ws = rt.workspace(1)
+        if self.kv_cache:
+            self._tmpl_plan = rt.plan_for_inputs(self.template, self.online_template, None, part="t")
+            self._tmpl_graph = rt.capture_plan(self._tmpl_plan) if self.use_graph else None
+            self._tmpl_dirty = True
         self._ws = ws
         plan = [(LIB.mmt_sample_target, (arr, 2), "track_sample_target", arr)]
         plan += model_plan
@@ -154,6 +165,12 @@ class RGBTTrackerCore:
     def _step(self):
         if self._plan is None or (self.use_graph and self._graph is None):
             self._build_step()
+        if self.kv_cache and self._tmpl_dirty:  # template pass after a template / online-template change
+            if self._tmpl_graph is not None:
+                self._tmpl_graph.replay()
+            else:
+                self.net._runtime(self.dev).run_plan(self._tmpl_plan)
+            self._tmpl_dirty = False
         if self._graph is not None:
             self._graph.replay()
         else:
@@ -172,6 +189,7 @@ class RGBTTrackerCore:
             self.online_max_template[m].copy_(self.template[m])
         self.frame_id = 0
         self.max_pred_score = -1.0
+        self._tmpl_dirty = True
         self._check_crop(self.tmpl_crop)
 
     def track(self, image):
@@ -190,10 +208,12 @@ class RGBTTrackerCore:
                         self.online_template[m].copy_(self.online_max_template[m])
                         self.online_max_template[m].copy_(self.template[m])
                     self.max_pred_score = -1
+                    self._tmpl_dirty = True
         else:
             for update_i in self.update_intervals:
                 if self.frame_id % update_i == 0:
                     self._crop_templates(self.online_template, self.state)
+                    self._tmpl_dirty = True
         vals = torch.cat([self.state, self.search_crop[:, 2]]).tolist()  # the step's one host round trip
         if min(vals[4:]) < 1:
             raise Exception("Too small bounding box.")  # processing_utils.py:36-37

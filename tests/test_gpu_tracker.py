@@ -170,13 +170,16 @@ def _seq(n, H=360, W=480):
     return frames, [200.0, 150.0, 48.0, 48.0]
 
 
+@pytest.mark.parametrize("kv_cache", [True, False])
 @pytest.mark.parametrize("variant,module,multimodal", [("rgbt", "mixformer_vit_rgbt", False),
                                                         ("asym", "asymmetric_shared", True)])
-def test_tracking_loop_matches_oracle(variant, module, multimodal):
+def test_tracking_loop_matches_oracle(variant, module, multimodal, kv_cache):
     """Each frame: the HIP tracker's new box vs the oracle's tracking step started from the HIP
-    tracker's previous box (teacher forcing, so bf16/fp32 rounding cannot compound)."""
+    tracker's previous box (teacher forcing, so bf16/fp32 rounding cannot compound).  kv_cache:
+    template pass on template updates + search-only frames (the default) or the full forward."""
     from oracle.forward import forward as oracle_forward
     trk, sd = _tracker(variant, module)
+    trk.core.kv_cache = kv_cache
     frames, init = _seq(5)
     lut = pp.jet_lut() if multimodal else None
     trk.initialize(frames[0], {"init_bbox": [init, init]})
