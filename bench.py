@@ -36,6 +36,9 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "tracker FPS (template+search fwd) MixViT-B RGB-T @320px, 1/2/4/8 MI355X"
 PEAK = {"bf16": 2500.0, "f32": 157.3}  # dense MFMA TFLOP/s, MI355X_MICROARCH.md
+# model geometry: ViT-B 128/320 (configs 2-4) and ViT-L 192/384 (config 5; fusion width = HIDDEN_DIM, defect D1)
+GEO_B = {"hidden": 768, "depth": 12, "search": 320, "template": 128}
+GEO_L = {"hidden": 1024, "depth": 24, "search": 384, "template": 192}
 VARIANT_NAMES = {"rgbt": "mixformer_vit_rgbt (two-stream)", "shared": "mixformer_vit_rgbt_shared",
                  "asym": "asymmetric_shared", "asym_online": "asymmetric_shared_online_score"}
 
@@ -187,14 +190,15 @@ def kv_cache_tracking(rt, pool, score, steps, warmup):
                     "template update); not the headline `value`, which runs the full template+search forward"}
 
 
-def cpu_baseline(variant, B, budget_s=12.0):
+def cpu_baseline(variant, B, budget_s=12.0, geo=None):
     """Oracle (fp32 CPU restatement of the reference forward), bounded sample."""
+    geo = geo or GEO_B
     from mmt_amd import synthetic
     from oracle.forward import forward as oracle_forward, state_dict_to_torch
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
     torch.set_num_threads(threads)
-    sd = state_dict_to_torch(synthetic.synth_state_dict(state_dict_keys(variant)))
-    t, o, s = synthetic.synth_inputs(B)
+    sd = state_dict_to_torch(synthetic.synth_state_dict(state_dict_keys(variant, **geo)))
+    t, o, s = synthetic.synth_inputs(B, geo["template"], geo["search"])
     oracle_forward(sd, variant, t, o, s)
     n, t0 = 0, time.perf_counter()
     while n < 3 or time.perf_counter() - t0 < budget_s:
@@ -204,7 +208,8 @@ def cpu_baseline(variant, B, budget_s=12.0):
             break
     dt = time.perf_counter() - t0
     return {"value": round(n * B / dt, 3), "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": "%d fp32 CPU forwards of B=%d (%s, 128/320), %.1f s, oracle/forward.py" % (n, B, variant, dt)}
+            "sample": "%d fp32 CPU forwards of B=%d (%s, %d/%d), %.1f s, oracle/forward.py"
+                      % (n, B, variant, geo["template"], geo["search"], dt)}
 
 
 def main():
@@ -223,6 +228,8 @@ def main():
     ap.add_argument("--dump-plan", default=None, help="write the plan's launch names (JSON) to this path")
     ap.add_argument("--no-mam-batched", action="store_true", help="skip the batched MAM attention roofline")
     ap.add_argument("--no-kv-cache", action="store_true", help="skip the template K/V cache tracking-rate line")
+    ap.add_argument("--vitl", action="store_true",
+                    help="BASELINE config 5 geometry: ViT-L (1024 wide, 24 blocks), 192px templates / 384px search")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -236,7 +243,8 @@ def main():
     from mmt_amd.runtime import MixFormerRGBTRuntime
 
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
-    keys = state_dict_keys(args.variant)
+    geo = GEO_L if args.vitl else GEO_B
+    keys = state_dict_keys(args.variant, **geo)
     sd = {k: torch.from_numpy(v) for k, v in synthetic.synth_state_dict(keys).items()}
     rt = MixFormerRGBTRuntime(sd, args.variant, dtype=dtype)
     rt.gemm_impl = args.gemm_impl
@@ -244,7 +252,7 @@ def main():
     score = args.variant == "asym_online"
     pool = []
     for i in range(4):  # distinct frames per rank, resident in HBM before timing
-        t, o, s = synthetic.synth_inputs(B, seed=1 + 4 * rank + i)
+        t, o, s = synthetic.synth_inputs(B, geo["template"], geo["search"], seed=1 + 4 * rank + i)
         pool.append(([x.cuda() for x in t], [x.cuda() for x in o], [x.cuda() for x in s]))
     use_graph = not args.no_graph
     # one hipGraph per resident input set: the patch staging reads that set in place (zero-copy)
@@ -295,9 +303,11 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic N(0,1) frames (seeded), seed-hash random-init weights (mmt-synth-v1)",
-            "config": {"workload": "%s ViT-B 128px template x2 + 320px search, RGB+TIR, %d frame(s)/GPU/step%s"
-                                   % (VARIANT_NAMES[args.variant], B, ", score head on" if score else ""),
-                       "variant": args.variant, "batch_per_gpu": B, "template": 128, "search": 320,
+            "config": {"workload": "%s %s %dpx template x2 + %dpx search, RGB+TIR, %d frame(s)/GPU/step%s"
+                                   % (VARIANT_NAMES[args.variant], "ViT-L" if args.vitl else "ViT-B", geo["template"],
+                                      geo["search"], B, ", score head on" if score else ""),
+                       "variant": args.variant, "batch_per_gpu": B, "template": geo["template"],
+                       "search": geo["search"], "hidden": geo["hidden"], "depth": geo["depth"],
                        "parallelism": "replicas" if world > 1 else "single", "hip_graph": use_graph},
             "roofline": dom, "roofline_mam": mam,
             "device_ms_per_step_sum": round(dev_ms, 4) if dev_ms else None, "launches_per_step": len(plan),
@@ -310,7 +320,7 @@ def main():
         if use_graph and not args.no_kv_cache:
             out["tracking_kv_cache"] = kv_cache_tracking(rt, pool, score, args.steps, args.warmup)
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.variant, B)
+            out["cpu_baseline"] = cpu_baseline(args.variant, B, budget_s=20.0 if args.vitl else 12.0, geo=geo)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

@@ -91,7 +91,8 @@ __global__ __launch_bounds__(256) void corner_score_kernel(const T* __restrict__
 // One 1024-thread block per frame handles both corner maps.  All map reads are issued up front
 // (independent, unrolled: SA_PER per thread per map) so the kernel pays one memory round trip, not
 // one per strided-loop iteration (the 256-thread loop version took ~20 us at batch 1).
-constexpr int SA_NT = 1024, SA_PER = 8;  // fh*fh <= SA_NT*SA_PER (80x80 = 6400 at 320/4)
+constexpr int SA_NT = 1024;  // fh*fh <= SA_NT*SA_PER: SA_PER 8 for 80x80 (320/4), 16 for 96x96 (384/4)
+template <int SA_PER>
 __global__ __launch_bounds__(SA_NT) void softargmax_kernel(const float* __restrict__ maps, float* __restrict__ cxcywh,
                                                            float* __restrict__ xyxy, float* __restrict__ rois,
                                                            float roi_scale, int B, int fh, int stride) {
@@ -291,7 +292,7 @@ extern "C" int mmt_corner_softargmax(const void* x4, const float* w5, const floa
                                      float roi_scale, int B, int fh, int c4, int stride, int dtype, void* stream) {
     const int epc = dtype == MMT_BF16 ? 8 : 4;
     if (!x4 || !w5 || !b5 || !a3 || !a4 || !score_maps || !boxes_cxcywh || B <= 0 || fh <= 0 || fh % 4 || c4 <= 0 ||
-        c4 % epc || fh * fh > SA_NT * SA_PER)
+        c4 % epc || fh * fh > SA_NT * 16)
         return MMT_EBADARG;
     hipStream_t st = (hipStream_t)stream;
     dim3 grid((unsigned)(((int64_t)B * fh * fh + 255) / 256), 2);
@@ -302,8 +303,12 @@ extern "C" int mmt_corner_softargmax(const void* x4, const float* w5, const floa
         hipLaunchKernelGGL(corner_score_kernel<float>, grid, dim3(256), 0, st, (const float*)x4, w5, b5, a3, a4,
                            score_maps, B, fh, c4);
     else return MMT_EBADARG;
-    hipLaunchKernelGGL(softargmax_kernel, dim3(B), dim3(SA_NT), 0, st, score_maps, boxes_cxcywh, boxes_xyxy, rois,
-                       roi_scale, B, fh, stride);
+    if (fh * fh <= SA_NT * 8)
+        hipLaunchKernelGGL(softargmax_kernel<8>, dim3(B), dim3(SA_NT), 0, st, score_maps, boxes_cxcywh, boxes_xyxy,
+                           rois, roi_scale, B, fh, stride);
+    else
+        hipLaunchKernelGGL(softargmax_kernel<16>, dim3(B), dim3(SA_NT), 0, st, score_maps, boxes_cxcywh, boxes_xyxy,
+                           rois, roi_scale, B, fh, stride);
     return launch_status();
 }
 

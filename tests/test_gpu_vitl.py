@@ -1,0 +1,48 @@
+"""BASELINE config 5 geometry on the GPU: ViT-L (C = 1024, 24 blocks, 16 heads), 192 px templates and
+384 px search (ntok = 2*144 + 576 = 864, head maps 96x96), asymmetric shared backbone with the online
+score head (asymmetric_shared_online.py:351-413), fusion width = HIDDEN_DIM (reference defect D1,
+mixformer.py:443 hard-codes 768 so the reference cannot build this model).
+
+The reference has no fixture at this size, so the check is against the oracle (oracle/forward.py, the
+fp32 CPU restatement pinned by the ViT-B golden vectors): boxes within 1e-3 (fp32 path) / 1e-2 (bf16
+path), the score logit within the same bound relative to its magnitude (north_star tolerances)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+GEO = {"hidden": 1024, "depth": 24, "search": 384, "template": 192}
+_CACHE = {}
+
+
+def _setup():
+    if "sd" not in _CACHE:
+        from mmt_amd import synthetic
+        from mmt_amd.model import reference_state_dict_shapes
+        from oracle.forward import forward as oracle_forward, state_dict_to_torch
+        keys = reference_state_dict_shapes("asym_online", **GEO)
+        sd = state_dict_to_torch(synthetic.synth_state_dict(keys))
+        t, o, s = synthetic.synth_inputs(1, GEO["template"], GEO["search"])
+        torch.set_num_threads(min(16, torch.get_num_threads()))
+        with torch.no_grad():
+            out, _ = oracle_forward(sd, "asym_online", t, o, s, run_score_head=True)
+        _CACHE.update(sd=sd, inputs=(t, o, s), box=out["pred_boxes"].reshape(4).numpy(),
+                      score=float(out["pred_scores"].reshape(-1)[0]))
+    return _CACHE
+
+
+@pytest.mark.parametrize("dname,tol", [("f32", 1e-3), ("bf16", 1e-2)])
+def test_vit_large_matches_oracle(dname, tol):
+    from mmt_amd.runtime import MixFormerRGBTRuntime
+    c = _setup()
+    rt = MixFormerRGBTRuntime(c["sd"], "asym_online", dtype=torch.float32 if dname == "f32" else torch.bfloat16)
+    assert (rt.d.C, rt.d.depth, rt.d.ntok, rt.d.n_t) == (1024, 24, 864, 288)
+    t, o, s = [[x.cuda() for x in grp] for grp in c["inputs"]]
+    box, sc = rt.forward(t, o, s, run_score_head=True)
+    torch.cuda.synchronize()
+    err = np.abs(box.cpu().numpy().reshape(4) - c["box"]).max()
+    serr = abs(float(sc.cpu().reshape(-1)[0]) - c["score"])
+    print("ViT-L %s box err %.3g score err %.3g (score %.4g)" % (dname, err, serr, c["score"]))
+    assert err <= tol, err
+    assert serr <= tol * max(1.0, abs(c["score"])), serr
