@@ -14,9 +14,13 @@
  *   mmt_ms_deform_attn_forward  pybind `MultiScaleDeformableAttention.ms_deform_attn_forward`
  *       lib/models/mixformer_vit_rgbt/deformable_attention/ops/src/vision.cpp:13-16,
  *       ms_deform_attn_cuda.cu:20-80 (same tensor meaning; fp64/fp32/bf16)
+ *   mmt_ms_deform_attn_backward pybind `MultiScaleDeformableAttention.ms_deform_attn_backward`
+ *       (ops/src/vision.cpp:13-16, ms_deform_attn_cuda.cu:83-153, ms_deform_im2col_cuda.cuh:86-235)
  *   mmt_prroi_pool_forward      `_prroi_pooling.prroi_pooling_forward_cuda`
  *       external/PreciseRoIPooling/pytorch/prroi_pool/src/prroi_pooling_gpu.c:22-50,
  *       prroi_pooling_gpu_impl.cu:149-212, 388-400 (plus explicit feature strides)
+ *   mmt_prroi_pool_backward / mmt_prroi_pool_coor_backward  `prroi_pooling_backward_cuda`,
+ *       `prroi_pooling_coor_backward_cuda` (prroi_pooling_gpu.c:52-113, _impl.cu:214-378)
  *   mmt_gemm                    the eager nn.Linear / 1x1-conv / 3x3-conv (+BN+ReLU) / patch-embed
  *       calls of mixformer.py:26-76, :137-138, fusion_utils.py:252-278, deformable_encoder*.py,
  *       head.py:7-20,159-198, score_decoder.py (implicit GEMM, fused epilogues)
@@ -198,6 +202,15 @@ int mmt_ms_deform_attn_forward(const void* value, const int64_t* spatial_shapes,
                                const void* sampling_loc, const void* attn_weight, void* out, int N, int S,
                                int M, int D, int Lq, int L, int P, int dtype, void* stream);
 
+/* Reference-op replacement for `ms_deform_attn_backward` (ops/src/vision.cpp:13-16,
+ * ms_deform_attn_cuda.cu:83-153): same tensors as the forward plus grad_output (N,Lq,M*D); writes
+ * grad_value (N,S,M,D; zeroed here, then accumulated by atomics), grad_loc (N,Lq,M,L,P,2) and
+ * grad_attn (N,Lq,M,L,P).  dtype MMT_F64 / MMT_F32 (the reference's dispatch). */
+int mmt_ms_deform_attn_backward(const void* value, const int64_t* spatial_shapes, const int64_t* level_start,
+                                const void* sampling_loc, const void* attn_weight, const void* grad_output,
+                                void* grad_value, void* grad_loc, void* grad_attn, int N, int S, int M, int D,
+                                int Lq, int L, int P, int dtype, void* stream);
+
 /* Bimodal encoder layer core (ms_deform_attn_bimodal.py:97-128) for nq queries per modality on an
  * hw x hw map, 8 heads x 64 ch, 2 levels x 4 points: offw[b*nq+q][192] fp32 = [sampling_offsets
  * (128) | attention logits (64)] from the [q_v | q_i] Linear; value [2][B][nq][512] (dtype);
@@ -226,6 +239,16 @@ int mmt_corner_softargmax(const void* x4, const float* w5, const float* b5, cons
 int mmt_prroi_pool_forward(const float* features, const float* rois, float* out, int R, int C, int H, int W,
                            int64_t s_b, int64_t s_c, int64_t s_h, int64_t s_w, int ph, int pw,
                            float spatial_scale, int64_t o_r, int64_t o_c, int64_t o_p, void* stream);
+
+/* `prroi_pooling_backward_cuda` / `prroi_pooling_coor_backward_cuda` (prroi_pooling_gpu.c:52-107,
+ * prroi_pooling_gpu_impl.cu:214-378): contiguous NCHW features (B,C,H,W) fp32, rois (R,5).
+ * _backward zeroes grad_features (B,C,H,W) and accumulates it by atomics; _coor_backward writes
+ * grad_rois (R,5) (column 0 = 0) from the forward's output `out` (R,C,ph,pw). */
+int mmt_prroi_pool_backward(const float* rois, const float* grad_out, float* grad_features, int B, int R, int C, int H,
+                            int W, int ph, int pw, float spatial_scale, void* stream);
+int mmt_prroi_pool_coor_backward(const float* features, const float* rois, const float* out, const float* grad_out,
+                                 float* grad_rois, int R, int C, int H, int W, int ph, int pw, float spatial_scale,
+                                 void* stream);
 
 /* ScoreDecoder attention: q [B][C] fp32 (one query per batch), kv [B][Lk][2C] fp32 (k | v),
  * H heads of C/H (= 64), scale; out [B][C] fp32 (dtype copy optional via out_t). */

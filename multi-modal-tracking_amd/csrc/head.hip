@@ -243,6 +243,127 @@ __global__ __launch_bounds__(256) void prroi_kernel(const float* __restrict__ fe
     *dst = sum / win;
 }
 
+// ---- PrRoIPool backward (prroi_pooling_gpu_impl.cu:214-378), contiguous NCHW features, (R,5) rois.
+// PrRoIPoolingDistributeDiff / MatDistributeDiff (:108-147): the four corner terms of one cell,
+// each an atomic add of top_diff * coeff where the tap lies inside the map.
+MMT_DEV void prroi_dist(float* g, float v, int h, int w, int H, int W) {
+    if (h >= 0 && w >= 0 && h < H && w < W) atomicAdd(g + (int64_t)h * W + w, v);
+}
+MMT_DEV void prroi_mat_dist(float* g, float top, int s_h, int s_w, int e_h, int e_w, float y0, float x0, float y1,
+                            float x1, int H, int W) {
+    float alpha = x0 - (float)s_w, beta = y0 - (float)s_h, la = x1 - (float)s_w, lb = y1 - (float)s_h;
+    prroi_dist(g, top * prroi_term(alpha, beta, la, lb), s_h, s_w, H, W);
+    alpha = (float)e_w - x1;
+    la = (float)e_w - x0;
+    prroi_dist(g, top * prroi_term(alpha, beta, la, lb), s_h, e_w, H, W);
+    alpha = x0 - (float)s_w;
+    beta = (float)e_h - y1;
+    la = x1 - (float)s_w;
+    lb = (float)e_h - y0;
+    prroi_dist(g, top * prroi_term(alpha, beta, la, lb), e_h, s_w, H, W);
+    alpha = (float)e_w - x1;
+    la = (float)e_w - x0;
+    prroi_dist(g, top * prroi_term(alpha, beta, la, lb), e_h, e_w, H, W);
+}
+
+// PrRoIPoolingBackward (:214-270): one thread per pooled element (n, c, ph, pw)
+__global__ __launch_bounds__(256) void prroi_bwd_kernel(const float* __restrict__ rois, const float* __restrict__ gout,
+                                                        float* __restrict__ gfeat, int R, int C, int H, int W, int PH,
+                                                        int PW, float scale) {
+    const int64_t total = (int64_t)R * C * PH * PW;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const int pw = idx % PW, ph = (idx / PW) % PH;
+    const int c = (idx / PW / PH) % C;
+    const int n = idx / PW / PH / C;
+    const float* roi = rois + n * 5;
+    const int bi = (int)roi[0];
+    const float x0 = roi[1] * scale, y0 = roi[2] * scale, x1 = roi[3] * scale, y1 = roi[4] * scale;
+    const float bh = fmaxf(y1 - y0, 0.f) / (float)PH, bw = fmaxf(x1 - x0, 0.f) / (float)PW;
+    const float ws = x0 + bw * pw, hs = y0 + bh * ph, we = ws + bw, he = hs + bh;
+    const float win = fmaxf(0.f, bw * bh);
+    const float top = win == 0.f ? 0.f : gout[idx] / win;
+    float* g = gfeat + ((int64_t)bi * C + c) * H * W;
+    const int sw_ = (int)floorf(ws), ew = (int)ceilf(we), sh_ = (int)floorf(hs), eh = (int)ceilf(he);
+    for (int wi = sw_; wi < ew; ++wi)
+        for (int hi = sh_; hi < eh; ++hi)
+            prroi_mat_dist(g, top, hi, wi, hi + 1, wi + 1, fmaxf(hs, (float)hi), fmaxf(ws, (float)wi),
+                           fminf(he, (float)hi + 1.f), fminf(we, (float)(wi + 1)), H, W);
+}
+
+// PrRoIPoolingInterpolation / SingleCoorIntegral (:44-69)
+MMT_DEV float prroi_interp(const float* d, float h, float w, int H, int W) {
+    const int h1 = (int)floorf(h), w1 = (int)floorf(w);
+    float r = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int hh = h1 + (k & 1), ww = w1 + (k >> 1);
+        const float v = (hh < 0 || ww < 0 || hh >= H || ww >= W) ? 0.f : d[(int64_t)hh * W + ww];
+        r += v * (1.f - fabsf(h - (float)hh)) * (1.f - fabsf(w - (float)ww));
+    }
+    return r;
+}
+MMT_DEV float prroi_coor_int(float s, float t, float c1, float c2) {
+    return 0.5f * (t * t - s * s) * c2 + (t - 0.5f * t * t - s + 0.5f * s * s) * c1;
+}
+
+// PrRoIPoolingCoorBackward (:272-378): one workgroup per ROI sums the (c, ph, pw) contributions
+// in registers + LDS and stores the 5 coordinate gradients once (the reference adds them with
+// 4 atomics per pooled element into the same 4 words).
+__global__ __launch_bounds__(256) void prroi_coor_bwd_kernel(const float* __restrict__ feat, const float* __restrict__ rois,
+                                                             const float* __restrict__ out, const float* __restrict__ gout,
+                                                             float* __restrict__ groi, int C, int H, int W, int PH, int PW,
+                                                             float scale) {
+    __shared__ float red[4][4];
+    const int n = blockIdx.x, tid = threadIdx.x;
+    const float* roi = rois + n * 5;
+    const int bi = (int)roi[0];
+    const float x0 = roi[1] * scale, y0 = roi[2] * scale, x1 = roi[3] * scale, y1 = roi[4] * scale;
+    const float bh = fmaxf(y1 - y0, 0.f) / (float)PH, bw = fmaxf(x1 - x0, 0.f) / (float)PW;
+    const float win = fmaxf(0.f, bw * bh);
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    const int per = C * PH * PW;
+    for (int e = tid; e < per; e += 256) {
+        const int pw = e % PW, ph = (e / PW) % PH, c = e / (PW * PH);
+        const int64_t idx = (int64_t)n * per + e;
+        const float go = gout[idx];
+        const float sum_out = win == 0.f ? 0.f : go / win;
+        if (sum_out == 0.f) continue;  // the reference's early return (:318)
+        const float ws = x0 + bw * pw, hs = y0 + bh * ph, we = ws + bw, he = hs + bh;
+        const float* d = feat + ((int64_t)bi * C + c) * H * W;
+        const int sw_ = (int)floorf(ws), ew = (int)ceilf(we), sh_ = (int)floorf(hs), eh = (int)ceilf(he);
+        float gx1 = 0.f, gx2 = 0.f, gy1 = 0.f, gy2 = 0.f;
+        for (int hi = sh_; hi < eh; ++hi) {
+            const float a = fmaxf(hs, (float)hi) - hi, b = fminf(he, (float)(hi + 1)) - hi;
+            gx1 += prroi_coor_int(a, b, prroi_interp(d, hi, ws, H, W), prroi_interp(d, hi + 1, ws, H, W));
+            gx2 += prroi_coor_int(a, b, prroi_interp(d, hi, we, H, W), prroi_interp(d, hi + 1, we, H, W));
+        }
+        for (int wi = sw_; wi < ew; ++wi) {
+            const float a = fmaxf(ws, (float)wi) - wi, b = fminf(we, (float)(wi + 1)) - wi;
+            gy1 += prroi_coor_int(a, b, prroi_interp(d, hs, wi, H, W), prroi_interp(d, hs, wi + 1, H, W));
+            gy2 += prroi_coor_int(a, b, prroi_interp(d, he, wi, H, W), prroi_interp(d, he, wi + 1, H, W));
+        }
+        const float top = out[idx];
+        const float px1 = (-gx1 + (he - hs) * top) / win * scale, py1 = (-gy1 + (we - ws) * top) / win * scale;
+        const float px2 = (gx2 - (he - hs) * top) / win * scale, py2 = (gy2 - (we - ws) * top) / win * scale;
+        acc[0] += (px1 * (1.f - (float)pw / PW) + px2 * (1.f - (float)(pw + 1) / PW)) * go;
+        acc[1] += (py1 * (1.f - (float)ph / PH) + py2 * (1.f - (float)(ph + 1) / PH)) * go;
+        acc[2] += (px2 * (float)(pw + 1) / PW + px1 * (float)pw / PW) * go;
+        acc[3] += (py2 * (float)(ph + 1) / PH + py1 * (float)ph / PH) * go;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float v = wave_sum(acc[k]);
+        if ((tid & 63) == 0) red[k][tid >> 6] = v;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        groi[n * 5] = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) groi[n * 5 + 1 + k] = red[k][0] + red[k][1] + red[k][2] + red[k][3];
+    }
+}
+
 // one wave per (batch, head); lane = channel within the head (64)
 __global__ __launch_bounds__(64) void spm_attention_kernel(const float* __restrict__ q, int64_t q_stride,
                                                            const float* __restrict__ kv, float* __restrict__ out, int Lk,
@@ -320,6 +441,32 @@ extern "C" int mmt_prroi_pool_forward(const float* features, const float* rois, 
     const int64_t total = (int64_t)R * C * ph * pw;
     hipLaunchKernelGGL(prroi_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, features,
                        rois, out, R, C, H, W, s_b, s_c, s_h, s_w, ph, pw, spatial_scale, o_r, o_c, o_p);
+    return launch_status();
+}
+
+extern "C" int mmt_prroi_pool_backward(const float* rois, const float* grad_out, float* grad_features, int B, int R,
+                                       int C, int H, int W, int ph, int pw, float spatial_scale, void* stream) {
+    if (!rois || !grad_out || !grad_features || B <= 0 || R < 0 || C <= 0 || H <= 0 || W <= 0 || ph <= 0 || pw <= 0)
+        return MMT_EBADARG;
+    hipStream_t st = (hipStream_t)stream;
+    const hipError_t e = hipMemsetAsync(grad_features, 0, sizeof(float) * (size_t)B * C * H * W, st);
+    if (e != hipSuccess) return -(int)e;
+    if (R == 0) return 0;
+    const int64_t total = (int64_t)R * C * ph * pw;
+    hipLaunchKernelGGL(prroi_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, rois, grad_out,
+                       grad_features, R, C, H, W, ph, pw, spatial_scale);
+    return launch_status();
+}
+
+extern "C" int mmt_prroi_pool_coor_backward(const float* features, const float* rois, const float* out,
+                                            const float* grad_out, float* grad_rois, int R, int C, int H, int W, int ph,
+                                            int pw, float spatial_scale, void* stream) {
+    if (!features || !rois || !out || !grad_out || !grad_rois || R < 0 || C <= 0 || H <= 0 || W <= 0 || ph <= 0 ||
+        pw <= 0)
+        return MMT_EBADARG;
+    if (R == 0) return 0;
+    hipLaunchKernelGGL(prroi_coor_bwd_kernel, dim3((unsigned)R), dim3(256), 0, (hipStream_t)stream, features, rois, out,
+                       grad_out, grad_rois, C, H, W, ph, pw, spatial_scale);
     return launch_status();
 }
 

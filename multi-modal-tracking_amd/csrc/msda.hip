@@ -14,6 +14,15 @@
 //   400 bimodal queries onto both 400-query halves and its reference points are per cell, so both
 //   halves produce identical rows; this kernel computes them once (B*nq rows, not 2*B*nq).
 //   Layout: one 512-thread workgroup per (batch, query) = 8 waves = 8 heads, lane = channel.
+//
+// mmt_ms_deform_attn_backward — drop-in for `ms_deform_attn_backward` (vision.cpp:13-16 ->
+//   ms_deform_attn_cuda.cu:83-153 -> ms_deformable_col2im kernels, ms_deform_im2col_cuda.cuh:86-235
+//   for the per-tap arithmetic): grad_value by float atomics at the four taps (w_k * g * a),
+//   grad_attn = sum_c g * bilinear, grad_loc = (W * dbil/dw, H * dbil/dh) * g * a summed over the
+//   channels.  One wave per (n, q, m) sample row, lanes over channels: the channel sums of
+//   grad_loc / grad_attn are wave reductions with one plain store each (the reference's
+//   blocksize-aware shared-memory reductions and their atomics are not needed), and samples the
+//   forward skipped (outside (-1, H) x (-1, W)) keep zero gradients, as the reference's zeros_like.
 #include "common.hpp"
 
 namespace {
@@ -114,7 +123,94 @@ __global__ __launch_bounds__(512) void msda_bimodal_kernel(const float* __restri
     out[(int64_t)row * CM + m * DH + c] = from_f<T>(col);
 }
 
+template <typename A> MMT_DEV A wave_sum_t(A v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void msda_bwd_kernel(const T* __restrict__ value, const int64_t* __restrict__ shapes,
+                                                       const int64_t* __restrict__ lstart, const T* __restrict__ loc,
+                                                       const T* __restrict__ aw, const T* __restrict__ gout,
+                                                       T* __restrict__ gvalue, T* __restrict__ gloc, T* __restrict__ gaw,
+                                                       int S, int M, int D, int Lq, int L, int P, int64_t nsamp) {
+    using A = T;  // fp32 / fp64 only, as the reference's dispatch
+    const int64_t samp = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // (n, q, m)
+    if (samp >= nsamp) return;                                           // wave-uniform
+    const int lane = threadIdx.x & 63;
+    const int m = samp % M;
+    const int n = (int)(samp / ((int64_t)M * Lq));
+    const T* g = gout + samp * D;
+    int64_t wi = samp * L * P;
+    for (int l = 0; l < L; ++l) {
+        const int H = (int)shapes[2 * l], W = (int)shapes[2 * l + 1];
+        const int64_t base = (((int64_t)n * S + lstart[l]) * M + m) * D;
+        const int64_t ws = (int64_t)M * D, hs = (int64_t)W * ws;
+        for (int p = 0; p < P; ++p, ++wi) {
+            const A lx = loc[2 * wi], ly = loc[2 * wi + 1], a = aw[wi];
+            const A h = ly * (A)H - (A)0.5, w = lx * (A)W - (A)0.5;
+            A sx = 0, sy = 0, sa = 0;
+            if (h > (A)-1 && w > (A)-1 && h < (A)H && w < (A)W) {  // sample-uniform, so wave-uniform
+                const int hl = (int)floor(h), wl = (int)floor(w), hh_ = hl + 1, wh_ = wl + 1;
+                const A lh = h - (A)hl, lw = w - (A)wl, hh = (A)1 - lh, hw = (A)1 - lw;
+                const A w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
+                const bool k1 = hl >= 0 && wl >= 0, k2 = hl >= 0 && wh_ <= W - 1;
+                const bool k3 = hh_ <= H - 1 && wl >= 0, k4 = hh_ <= H - 1 && wh_ <= W - 1;
+                const int64_t o1 = hl * hs + wl * ws, o2 = o1 + ws, o3 = o1 + hs, o4 = o3 + ws;
+                for (int c = lane; c < D; c += 64) {
+                    const A tg = g[c], tgv = tg * a;
+                    const T* v = value + base + c;
+                    T* gv = gvalue + base + c;
+                    A gh = 0, gw = 0, v1 = 0, v2 = 0, v3 = 0, v4 = 0;
+                    if (k1) { v1 = v[o1]; gh -= hw * v1; gw -= hh * v1; atomicAdd(gv + o1, w1 * tgv); }
+                    if (k2) { v2 = v[o2]; gh -= lw * v2; gw += hh * v2; atomicAdd(gv + o2, w2 * tgv); }
+                    if (k3) { v3 = v[o3]; gh += hw * v3; gw -= lh * v3; atomicAdd(gv + o3, w3 * tgv); }
+                    if (k4) { v4 = v[o4]; gh += lw * v4; gw += lh * v4; atomicAdd(gv + o4, w4 * tgv); }
+                    sa += tg * (w1 * v1 + w2 * v2 + w3 * v3 + w4 * v4);
+                    sx += (A)W * gw * tgv;
+                    sy += (A)H * gh * tgv;
+                }
+                sa = wave_sum_t<A>(sa);
+                sx = wave_sum_t<A>(sx);
+                sy = wave_sum_t<A>(sy);
+            }
+            if (lane == 0) {
+                gaw[wi] = sa;
+                gloc[2 * wi] = sx;
+                gloc[2 * wi + 1] = sy;
+            }
+        }
+    }
+}
+
 }  // namespace
+
+extern "C" int mmt_ms_deform_attn_backward(const void* value, const int64_t* spatial_shapes, const int64_t* level_start,
+                                           const void* sampling_loc, const void* attn_weight, const void* grad_output,
+                                           void* grad_value, void* grad_loc, void* grad_attn, int N, int S, int M, int D,
+                                           int Lq, int L, int P, int dtype, void* stream) {
+    if (!value || !spatial_shapes || !level_start || !sampling_loc || !attn_weight || !grad_output || !grad_value ||
+        !grad_loc || !grad_attn)
+        return MMT_EBADARG;
+    if (N <= 0 || S <= 0 || M <= 0 || D <= 0 || Lq <= 0 || L <= 0 || P <= 0) return MMT_EBADARG;
+    const size_t esz = dtype == MMT_F64 ? 8 : dtype == MMT_F32 ? 4 : 0;
+    if (!esz) return MMT_EBADARG;
+    hipStream_t st = (hipStream_t)stream;
+    // grad_value accumulates by atomics; grad_loc / grad_attn are fully written by the kernel
+    const hipError_t e = hipMemsetAsync(grad_value, 0, (size_t)N * S * M * D * esz, st);
+    if (e != hipSuccess) return -(int)e;
+    const int64_t nsamp = (int64_t)N * Lq * M;
+    dim3 grid((unsigned)((nsamp + 3) / 4));
+#define MSDA_BWD_CASE(T)                                                                                          \
+    hipLaunchKernelGGL((msda_bwd_kernel<T>), grid, dim3(256), 0, st, (const T*)value, spatial_shapes, level_start, \
+                       (const T*)sampling_loc, (const T*)attn_weight, (const T*)grad_output, (T*)grad_value,       \
+                       (T*)grad_loc, (T*)grad_attn, S, M, D, Lq, L, P, nsamp)
+    if (dtype == MMT_F32) MSDA_BWD_CASE(float);
+    else MSDA_BWD_CASE(double);
+#undef MSDA_BWD_CASE
+    return launch_status();
+}
 
 extern "C" int mmt_ms_deform_attn_forward(const void* value, const int64_t* spatial_shapes, const int64_t* level_start,
                                           const void* sampling_loc, const void* attn_weight, void* out, int N, int S,

@@ -70,10 +70,13 @@ _PROTOS = {
     "mmt_add_cast": [vp, vp, i64, vp, vp, i64, i32, vp],
     "mmt_patch_im2col": [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp],
     "mmt_ms_deform_attn_forward": [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp],
+    "mmt_ms_deform_attn_backward": [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp],
     "mmt_msda_bimodal": [vp, vp, vp, i32, i32, i32, vp],
     "mmt_conv3x3_c1": [vp, vp, vp, vp, i32, i32, i32, i32, i64, i32, vp],
     "mmt_corner_softargmax": [vp, vp, vp, vp, vp, vp, vp, vp, vp, f32, i32, i32, i32, i32, i32, vp],
     "mmt_prroi_pool_forward": [vp, vp, vp, i32, i32, i32, i32, i64, i64, i64, i64, i32, i32, f32, i64, i64, i64, vp],
+    "mmt_prroi_pool_backward": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, f32, vp],
+    "mmt_prroi_pool_coor_backward": [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, f32, vp],
     "mmt_spm_attention": [vp, i64, vp, vp, i32, i32, i32, i32, f32, vp],
     "mmt_sample_target": [ctypes.POINTER(CropParams), i32, vp],
     "mmt_track_update": [vp, vp, vp, i32, i32, i32, i32, f64, vp],

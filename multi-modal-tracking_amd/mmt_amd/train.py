@@ -14,10 +14,10 @@ autograd Functions: every Linear (patch embed as a GEMM on the unfolded patches,
 fc2) forward and backward on the LDS-DMA bf16 GEMM (dX = dY W and dW = dY^T X after bf16
 transposes, fp32 accumulation, fp32 master weights), and the MAM attention forward (throughput
 kernel, log-sum-exp kept) and backward (mmt_mam_attention_bwd).  LayerNorm / GELU / residual adds,
-the deformable fusion encoder and the corner head run as PyTorch-ROCm ops on the same module tree
-(`nn.Conv2d`, `nn.GroupNorm`, `SyncBatchNorm` under DDP, `F.grid_sample` for the deformable
-sampling as the reference's ms_deform_attn_core_pytorch), in bf16 autocast like the reference's AMP
-path.  The backbone ops are injected (`ops`), so the data-parallel plumbing can be exercised on CPU
+the fusion encoder's deformable sampling runs on mmt_ms_deform_attn_forward / _backward
+(mmt_amd.functional.MSDeformAttnFunction, the reference's MSDeformAttnFunction), and the rest of the
+fusion and the corner head run as PyTorch-ROCm ops on the same module tree (`nn.Conv2d`,
+`nn.GroupNorm`, `SyncBatchNorm` under DDP), in bf16 autocast like the reference's AMP path.  The backbone ops are injected (`ops`), so the data-parallel plumbing can be exercised on CPU
 with stand-in ops in tests; the product's ops are `HipOps` and have no CPU path.
 """
 import math
@@ -135,6 +135,16 @@ class HipOps:
     def mam_attention(qkv, n_t, heads):
         return _HipMamAttention.apply(qkv, n_t, heads)
 
+    @staticmethod
+    def ms_deform_attn(value, hw, loc, aw):
+        """MSDeformAttnFunction (ms_deform_attn_func.py:22-38) on mmt_ms_deform_attn_forward / _backward,
+        fp32 as the reference op; L levels of hw x hw."""
+        from .functional import MSDeformAttnFunction
+        L = loc.shape[3]
+        shapes = torch.tensor([[hw, hw]] * L, dtype=torch.long, device=value.device)
+        starts = torch.arange(L, dtype=torch.long, device=value.device) * (hw * hw)
+        return MSDeformAttnFunction.apply(value, shapes, starts, loc, aw, 64)
+
 
 # ----------------------------------------------------------------------------- forward
 DROP_PATH_RATE = 0.1  # get_mixformer_vit drop_path_rate (mixformer.py:311, :324); timm linear per-block schedule
@@ -203,24 +213,7 @@ def _ref_points(H, W, B, L, device):
     return ref[:, :, None].expand(B, ref.shape[1], L, 2)
 
 
-def _msda_core(value, hw, loc, aw):
-    """ms_deform_attn_core_pytorch (ms_deform_attn_func.py:41-61): bilinear, zero padding,
-    align_corners=False; value (N, L*hw*hw, M, D), loc (N, Lq, M, L, P, 2), aw (N, Lq, M, L, P)."""
-    N, _, M, D = value.shape
-    _, Lq, _, L, P, _ = loc.shape
-    vl = value.split([hw * hw] * L, dim=1)
-    grids = 2 * loc - 1
-    outs = []
-    for lid in range(L):
-        v = vl[lid].flatten(2).transpose(1, 2).reshape(N * M, D, hw, hw)
-        g = grids[:, :, :, lid].transpose(1, 2).flatten(0, 1)
-        outs.append(F.grid_sample(v, g, mode="bilinear", padding_mode="zeros", align_corners=False))
-    aw = aw.transpose(1, 2).reshape(N * M, 1, Lq, L * P)
-    out = (torch.stack(outs, dim=-2).flatten(-2) * aw).sum(-1).view(N, M * D, Lq)
-    return out.transpose(1, 2)
-
-
-def fusion_forward(fu, s_v, s_i):
+def fusion_forward(fu, s_v, s_i, ops):
     """Attention_Fusion_Bimodal_LNSpecific.forward (fusion_utils.py:270-279) with the deformable
     encoder (deformable_encoder_lnspecific.py:131-160) and MSDeformAttn_Bimodal
     (ms_deform_attn_bimodal.py:83-130)."""
@@ -243,7 +236,7 @@ def fusion_forward(fu, s_v, s_i):
         aw = sa.attention_weights(q_bi).view(b, nl // 2, sa.n_heads, sa.n_levels * sa.n_points)
         aw = F.softmax(torch.cat([aw, aw], 1).float(), -1).view(b, nl, sa.n_heads, sa.n_levels, sa.n_points)
         loc = ref[:, :, None, :, None, :] + off.float() / torch.tensor([w, h], device=src.device, dtype=torch.float32)
-        src2 = sa.output_proj(_msda_core(value.float(), h, loc, aw))
+        src2 = sa.output_proj(ops.ms_deform_attn(value.float().contiguous(), h, loc.contiguous(), aw.contiguous()))
         src = src + layer.dropout1(src2)
         s1, s2 = torch.chunk(src, 2, 1)
         src = torch.cat([layer.norm1_v(s1), layer.norm1_i(s2)], 1)
@@ -287,7 +280,7 @@ def forward_boxes(net, template, online_template, search, ops):
     s_v = backbone_forward(net.backbone_v, template[0], online_template[0], search[0], ops)
     s_i = backbone_forward(net.backbone_i, template[1], online_template[1], search[1], ops)
     with torch.autocast(s_v.device.type, dtype=torch.bfloat16, enabled=s_v.device.type == "cuda"):
-        fused = fusion_forward(net.fusion_vi, s_v, s_i)
+        fused = fusion_forward(net.fusion_vi, s_v, s_i, ops)
         xyxy = head_forward(net.box_head, fused)
     x0, y0, x1, y1 = xyxy.float().unbind(-1)
     return torch.stack([(x0 + x1) / 2, (y0 + y1) / 2, (x1 - x0), (y1 - y0)], -1).view(-1, 1, 4)
@@ -408,3 +401,85 @@ class _Wrapped(torch.nn.Module):
 
     def forward(self, t, o, s):
         return forward_boxes(self.net, t, o, s, self.ops)
+
+
+# ----------------------------------------------------------------------------- score-head training
+def score_decoder_forward(sb, search_feat, template_feat, box_xyxy):
+    """ScoreDecoder.forward (lib/models/mixformer_cvt/score_decoder.py:32-66) with autograd; the ROI
+    features come from PrRoIPool on libmmt_hip.so (mmt_amd.functional.prroi_pool2d, whose backward
+    is mmt_prroi_pool_backward / _coor_backward).  search_feat (b,C,h,w) fp32, template_feat
+    (b,C,2*ht,wt), box_xyxy (b,4) normalised -> logits (b,)."""
+    from .functional import prroi_pool2d
+    b, c, h, w = search_feat.shape
+    H = sb.num_heads
+    bb = (box_xyxy.clone() * w).view(-1, 4).float()
+    rois = torch.cat([torch.arange(bb.shape[0], dtype=torch.float32, device=bb.device).view(-1, 1), bb], 1)
+    x = sb.norm1(sb.score_token.expand(b, -1, -1))
+    roi = prroi_pool2d(search_feat.float().contiguous(), rois.contiguous(), sb.pool_size, sb.pool_size, 1.0)
+    mem = [roi.flatten(2).transpose(1, 2), template_feat.float().flatten(2).transpose(1, 2)]
+    for i in range(2):
+        q = sb.proj_q[i](x).view(b, -1, H, c // H).transpose(1, 2)
+        k = sb.proj_k[i](mem[i]).view(b, -1, H, c // H).transpose(1, 2)
+        v = sb.proj_v[i](mem[i]).view(b, -1, H, c // H).transpose(1, 2)
+        a = torch.softmax(q @ k.transpose(-1, -2) * sb.scale, dim=-1)
+        x = (a @ v).transpose(1, 2).reshape(b, -1, c)
+        x = sb.norm2[i](sb.proj[i](x))
+    n = len(sb.score_head.layers)
+    for i, layer in enumerate(sb.score_head.layers):
+        x = layer(x)
+        if i < n - 1:
+            x = F.relu(x)
+    return x.view(-1)
+
+
+class ScoreTrainStep:
+    """The TRAIN.TRAIN_SCORE stage of the online-score model (asymmetric_shared_online): only the
+    parameters whose name contains "score" learn (base_functions.py:300-308), the loss is
+    BCEWithLogits(pred_scores, labels) * TRAIN.SCORE_WEIGHT (train_script_mixformer.py:138-140,
+    actors/mixformer_rgbt.py:150-152), clip TRAIN.GRAD_CLIP_NORM, AdamW (lr 1e-4, wd 1e-4).
+
+    The frozen trunk (backbone, fusion, box head) runs on the HIP inference runtime `rt` (no
+    autograd is needed through it); its search feature, template tokens and predicted boxes feed
+    the score decoder, which runs with autograd.  The reference builds the ROI from the predicted
+    boxes (asymmetric_shared_online.py:398-413: forward_head is called without gt_bboxes)."""
+
+    def __init__(self, net, rt, lr=1e-4, weight_decay=1e-4, grad_clip=0.1, score_weight=1.0):
+        self.net, self.rt = net, rt
+        for n, p in net.named_parameters():
+            p.requires_grad = "score" in n
+        self.params = [p for n, p in net.named_parameters() if "score" in n]
+        self.opt = torch.optim.AdamW([{"params": self.params}], lr=lr, weight_decay=weight_decay)
+        self.grad_clip, self.score_weight = grad_clip, score_weight
+        self.loss_fn = torch.nn.BCEWithLogitsLoss()
+
+    @torch.no_grad()
+    def trunk(self, t, o, s):
+        """-> search feature (B,C,gs,gs), template feature (B,C,2*gt,gt), boxes xyxy (B,4)."""
+        rt, d = self.rt, self.rt.d
+        box, _ = rt.forward(t, o, s, run_score_head=False)
+        B = box.shape[0]
+        ws = rt.workspace(B)
+        fused = ws["FUS"].view(B, d.ns, d.C).permute(0, 2, 1).reshape(B, d.C, d.gs, d.gs).float()
+        X = ws["X"].view(2, B, d.ntok, d.C)[:, :, :d.nt1]  # first template's tokens, RGB then TIR
+        templ = torch.cat([X[0], X[1]], 1).transpose(1, 2).reshape(B, d.C, 2 * d.gt, d.gt).float()
+        cx, cy, w, h = box.float().unbind(-1)
+        xyxy = torch.stack([cx - 0.5 * w, cy - 0.5 * h, cx + 0.5 * w, cy + 0.5 * h], -1)
+        return fused.clone(), templ.clone(), xyxy
+
+    def backward(self, t, o, s, labels):
+        self.opt.zero_grad(set_to_none=True)
+        fused, templ, xyxy = self.trunk(t, o, s)
+        scores = score_decoder_forward(self.net.score_branch, fused, templ, xyxy)
+        loss = self.loss_fn(scores, labels.float().view(-1)) * self.score_weight
+        loss.backward()
+        return {"loss": loss.detach(), "scores": scores.detach()}
+
+    def apply(self):
+        if self.grad_clip > 0:
+            torch.nn.utils.clip_grad_norm_(self.params, self.grad_clip)
+        self.opt.step()
+
+    def __call__(self, t, o, s, labels):
+        stats = self.backward(t, o, s, labels)
+        self.apply()
+        return stats

@@ -9,6 +9,13 @@ Restates the reference CUDA op, not its grid_sample debug path:
 The reference's own pure-PyTorch core (ops/functions/ms_deform_attn_func.py:41-61) is the
 same function via grid_sample(align_corners=False, padding zeros); the golden vectors are made
 with that core and pin this restatement.
+
+Backward (ms_deform_attn_backward, ms_deform_attn_cuda.cu:83-153; per-tap arithmetic
+ms_deform_im2col_cuda.cuh:86-150 ms_deform_attn_col2im_bilinear): autograd of the restatement
+above.  floor() has zero derivative, so d/dloc flows only through lh / lw, exactly the
+reference's grad_h_weight / grad_w_weight sums scaled by H / W; taps outside the map and skipped
+samples contribute zero, as the reference's zero-initialised gradients.  Pinned by a numerical
+gradient check in float64 (the reference's ops/test.py check_gradient_numerical).
 """
 import torch
 
@@ -61,3 +68,15 @@ def ms_deform_attn(value, spatial_shapes, level_start_index, sampling_locations,
             val = w1 * v1 + w2 * v2 + w3 * v3 + w4 * v4
             out = out + torch.where(inside.unsqueeze(-1), val * w.unsqueeze(-1), torch.zeros((), dtype=dt))
     return out.reshape(N, Lq, M * D)
+
+
+def ms_deform_attn_backward(value, spatial_shapes, level_start_index, sampling_locations, attention_weights,
+                            grad_output):
+    """-> (grad_value, grad_sampling_loc, grad_attn_weight), same shapes/dtypes as the inputs."""
+    v = value.detach().clone().requires_grad_(True)
+    loc = sampling_locations.detach().clone().requires_grad_(True)
+    aw = attention_weights.detach().clone().requires_grad_(True)
+    with torch.enable_grad():
+        out = ms_deform_attn(v, spatial_shapes, level_start_index, loc, aw)
+        gv, gl, ga = torch.autograd.grad(out, (v, loc, aw), grad_output)
+    return gv, gl, ga

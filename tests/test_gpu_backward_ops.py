@@ -1,0 +1,108 @@
+"""HIP backward kernels of the reference's native ops vs the oracle.
+
+* mmt_ms_deform_attn_backward (through mmt_amd.functional.MSDeformAttnFunction) vs autograd of the
+  oracle restatement (tests/test_oracle_backward.py pins it by a float64 numerical gradient check):
+  float64 within 1e-10 of the largest gradient; float32 within 1e-4 (atomics reorder the sums);
+  at the reference's op-test shapes and at the bimodal encoder's training shape
+  (N 2, 800 keys / queries, 8 heads x 64, 2 levels of 20x20, 4 points).
+* mmt_prroi_pool_backward / _coor_backward (PrRoIPool2DFunction) vs the oracle's numpy
+  restatement of prroi_pooling_gpu_impl.cu:214-378, fp32, within 1e-4 relative, including the
+  score head's shape (768 channels, 20x20 map, 4x4 bins, scale 1)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _msda_case(N, Lq, M, D, shapes, P, dtype, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    S = sum(h * w for h, w in shapes)
+    L = len(shapes)
+    starts = np.cumsum([0] + [h * w for h, w in shapes])[:-1].tolist()
+    v = torch.rand(N, S, M, D, generator=g, dtype=torch.float64)
+    loc = torch.rand(N, Lq, M, L, P, 2, generator=g, dtype=torch.float64) * 1.3 - 0.15  # some samples outside
+    # grad_loc is discontinuous where h_im / w_im crosses an integer (the tap cell and the inside test
+    # change): keep samples 1e-3 away from those points, so fp32 and fp64 take the same branches
+    for lv, (h, wd) in enumerate(shapes):
+        for k, ext in ((0, wd), (1, h)):
+            im = loc[:, :, :, lv, :, k] * ext - 0.5
+            fr = im - im.floor()
+            loc[:, :, :, lv, :, k] += torch.where((fr < 1e-3) | (fr > 1 - 1e-3), 2e-3 / ext, 0.0)
+    w = torch.rand(N, Lq, M, L, P, generator=g, dtype=torch.float64) + 1e-5
+    w = w / w.sum((-1, -2), keepdim=True)
+    go = torch.randn(N, Lq, M * D, generator=g, dtype=torch.float64)
+    return [x.to(dtype) for x in (v, loc, w, go)], shapes, starts
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float64, 1e-10), (torch.float32, 1e-4)])
+@pytest.mark.parametrize("N,Lq,M,D,shapes,P", [(1, 2, 2, 2, [(6, 4), (3, 2)], 2), (2, 7, 2, 71, [(6, 4), (3, 2)], 3),
+                                               (1, 5, 3, 130, [(5, 5)], 4), (2, 800, 8, 64, [(20, 20), (20, 20)], 4)])
+def test_msda_backward_matches_oracle(N, Lq, M, D, shapes, P, dtype, tol):
+    from mmt_amd.functional import MSDeformAttnFunction
+    from oracle.msda import ms_deform_attn_backward
+    (v, loc, w, go), shapes, starts = _msda_case(N, Lq, M, D, shapes, P, dtype)
+    ref = ms_deform_attn_backward(v.double(), shapes, starts, loc.double(), w.double(), go.double())
+    vc, lc, wc = (x.cuda().requires_grad_(True) for x in (v, loc, w))
+    sh = torch.tensor(shapes, dtype=torch.long, device="cuda")
+    st = torch.tensor(starts, dtype=torch.long, device="cuda")
+    out = MSDeformAttnFunction.apply(vc, sh, st, lc, wc, 64)
+    out.backward(go.cuda())
+    for got, want, nm in zip((vc.grad, lc.grad, wc.grad), ref, ("value", "loc", "attn")):
+        scale = max(1.0, float(want.abs().max()))
+        err = float((got.double().cpu() - want).abs().max()) / scale
+        print("%s grad_%s err %.3g" % (dtype, nm, err))
+        assert err <= tol, (nm, err)
+
+
+def test_msda_backward_zero_for_skipped_samples():
+    from mmt_amd.functional import MSDeformAttnFunction
+    (v, loc, w, go), shapes, starts = _msda_case(1, 3, 2, 8, [(6, 4), (3, 2)], 2, torch.float32)
+    loc[0, 1] = 1.6  # every sample of query 1 lies outside its map -> skipped by the forward
+    vc, lc, wc = (x.cuda().requires_grad_(True) for x in (v, loc, w))
+    out = MSDeformAttnFunction.apply(vc, torch.tensor(shapes, device="cuda"), torch.tensor(starts, device="cuda"),
+                                     lc, wc, 64)
+    assert float(out[0, 1].abs().max()) == 0.0
+    out.backward(go.cuda())
+    assert float(lc.grad[0, 1].abs().max()) == 0.0 and float(wc.grad[0, 1].abs().max()) == 0.0
+
+
+def test_msda_rejects_non_contiguous():
+    from mmt_amd.functional import MSDeformAttnFunction
+    (v, loc, w, _), shapes, starts = _msda_case(1, 2, 2, 4, [(6, 4), (3, 2)], 2, torch.float32)
+    vt = v.cuda().transpose(2, 3)
+    with pytest.raises(RuntimeError):
+        MSDeformAttnFunction.apply(vt, torch.tensor(shapes, device="cuda"), torch.tensor(starts, device="cuda"),
+                                   loc.cuda(), w.cuda(), 64)
+
+
+def _prroi_case(B, C, H, W, seed=0):
+    rng = np.random.default_rng(seed)
+    feats = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    rois = []
+    for r in range(2 * B + 1):
+        x0, y0 = rng.uniform(-1.5, W * 0.6), rng.uniform(-1.5, H * 0.6)
+        rois.append([r % B, x0, y0, x0 + rng.uniform(0.0, W * 0.7), y0 + rng.uniform(0.0, H * 0.7)])
+    rois.append([0, 2.0, 3.0, 2.0, 7.0])  # zero-width ROI: empty bins, zero gradients
+    return feats, np.array(rois, dtype=np.float32)
+
+
+@pytest.mark.parametrize("B,C,H,W,ph,scale", [(2, 5, 9, 8, 7, 0.5), (2, 16, 20, 20, 4, 1.0), (1, 768, 20, 20, 4, 1.0)])
+def test_prroi_backward_matches_oracle(B, C, H, W, ph, scale):
+    from mmt_amd.functional import prroi_pool2d
+    from oracle.prroi import prroi_pool2d as ref_fwd, prroi_pool2d_backward, prroi_pool2d_coor_backward
+    feats, rois = _prroi_case(B, C, H, W)
+    g = np.random.default_rng(7).standard_normal((rois.shape[0], C, ph, ph)).astype(np.float32)
+    fc = torch.from_numpy(feats).cuda().requires_grad_(True)
+    rc = torch.from_numpy(rois).cuda().requires_grad_(True)
+    out = prroi_pool2d(fc, rc, ph, ph, scale)
+    ref_out = ref_fwd(feats, rois, ph, ph, scale)
+    assert np.abs(out.detach().cpu().numpy() - ref_out).max() <= 1e-4 * max(1.0, np.abs(ref_out).max())
+    out.backward(torch.from_numpy(g).cuda())
+    gf_ref = prroi_pool2d_backward(feats.shape, rois, g, ph, ph, scale)
+    gr_ref = prroi_pool2d_coor_backward(feats, rois, ref_out, g, ph, ph, scale)
+    ef = np.abs(fc.grad.cpu().numpy() - gf_ref).max() / max(1.0, np.abs(gf_ref).max())
+    er = np.abs(rc.grad.cpu().numpy() - gr_ref).max() / max(1.0, np.abs(gr_ref).max())
+    print("prroi grad feat err %.3g roi err %.3g" % (ef, er))
+    assert ef <= 1e-4 and er <= 1e-4, (ef, er)
+    assert float(rc.grad[-1].abs().max()) == 0.0  # the zero-width ROI

@@ -140,6 +140,14 @@ class _TorchBf16Ops:
         from test_train import TorchOps
         return TorchOps.mam_attention(qkv.float(), n_t, heads).bfloat16()
 
+    @staticmethod
+    def ms_deform_attn(value, hw, loc, aw):
+        import sys
+        import os
+        sys.path.insert(0, os.path.dirname(__file__))
+        from test_train import TorchOps
+        return TorchOps.ms_deform_attn(value, hw, loc, aw)
+
 
 def test_train_step_gpu_matches_fp32_grads():
     """One two-stream training step at the bench shapes (128/320, B=2): HIP backbone ops in bf16 vs
@@ -188,3 +196,55 @@ def test_train_step_gpu_matches_fp32_grads():
     losses = [step(*gb)["loss"].item() for _ in range(4)]
     print("losses", losses)
     assert losses[-1] < stats["loss"].item(), losses
+
+
+def test_score_train_step_matches_oracle_grads():
+    """TRAIN_SCORE stage on the online-score model: the frozen trunk on the HIP runtime (fp32), the
+    score decoder with autograd over the HIP PrRoIPool.  Logits and every score-branch gradient
+    vs autograd through the oracle's ScoreDecoder restatement on the CPU (same trunk outputs):
+    within 1e-3 (relative L2); only "score" parameters receive gradients; AdamW steps lower the loss."""
+    import json
+    from conftest import GOLDEN
+    from mmt_amd import synthetic
+    from mmt_amd.model import build_asymmetric_shared_online_score, hot_path_cfg
+    from mmt_amd.runtime import MixFormerRGBTRuntime
+    from mmt_amd.train import ScoreTrainStep
+    from oracle.forward import score_decoder
+    keys = json.load(open(GOLDEN + "/state_dict_asym_online.json"))
+    sd = {k: torch.from_numpy(v) for k, v in synthetic.synth_state_dict(keys).items()}
+    net = build_asymmetric_shared_online_score(hot_path_cfg(), train=False)
+    net.load_state_dict(sd, strict=True)
+    net = net.cuda().eval()
+    rt = MixFormerRGBTRuntime(sd, "asym_online", dtype=torch.float32)
+    step = ScoreTrainStep(net, rt)
+    B = 3
+    t, o, s = synthetic.synth_inputs(B)
+    t, o, s = [x.cuda() for x in t], [x.cuda() for x in o], [x.cuda() for x in s]
+    labels = torch.tensor([1.0, 0.0, 1.0], device="cuda")
+    stats = step.backward(t, o, s, labels)
+    fused, templ, xyxy = step.trunk(t, o, s)
+    leaf = {k: v.detach().cpu().float().requires_grad_(k.startswith("score_branch.")) for k, v in
+            net.state_dict().items() if k.startswith("score_branch.")}
+    ref = score_decoder(leaf, "score_branch.", fused.cpu(), templ.cpu(), xyxy.cpu(), num_heads=fused.shape[1] // 64)
+    loss = torch.nn.functional.binary_cross_entropy_with_logits(ref.view(-1), labels.cpu())
+    loss.backward()
+    serr = (stats["scores"].cpu() - ref.view(-1).detach()).abs().max().item()
+    print("score logits err %.3g, loss hip %.6f oracle %.6f" % (serr, stats["loss"].item(), loss.item()))
+    assert serr <= 1e-3 and abs(stats["loss"].item() - loss.item()) <= 1e-4
+    named = dict(net.named_parameters())
+    for n, p in named.items():
+        if "score" not in n:
+            assert p.grad is None, n
+    # proj_k biases get mathematically zero gradients (softmax is shift-invariant): measure each
+    # gradient against max(its own norm, 1e-4 x the largest one) so rounding noise there is not a ratio
+    gmax = max(v.grad.norm().item() for v in leaf.values() if v.grad is not None)
+    for k, v in leaf.items():
+        if v.grad is None:
+            continue
+        got = named[k].grad.float().cpu()
+        rel = ((got - v.grad).norm() / max(v.grad.norm().item(), 1e-4 * gmax)).item()
+        assert rel <= 1e-3, (k, rel)
+    step.apply()
+    losses = [step(t, o, s, labels)["loss"].item() for _ in range(5)]
+    print("score losses", stats["loss"].item(), losses)
+    assert losses[-1] < stats["loss"].item()

@@ -36,6 +36,27 @@ class TorchOps:
         os_ = torch.softmax(q[:, :, n_t:] @ k.transpose(-1, -2) * sc, -1) @ v
         return torch.cat([ot, os_], 2).transpose(1, 2).reshape(S, ntok, C)
 
+    @staticmethod
+    def ms_deform_attn(value, hw, loc, aw):
+        return _msda_core(value, hw, loc, aw)
+
+
+def _msda_core(value, hw, loc, aw):
+    """ms_deform_attn_core_pytorch (ms_deform_attn_func.py:41-61): bilinear, zero padding,
+    align_corners=False; value (N, L*hw*hw, M, D), loc (N, Lq, M, L, P, 2), aw (N, Lq, M, L, P)."""
+    N, _, M, D = value.shape
+    _, Lq, _, L, P, _ = loc.shape
+    vl = value.split([hw * hw] * L, dim=1)
+    grids = 2 * loc - 1
+    outs = []
+    for lid in range(L):
+        v = vl[lid].flatten(2).transpose(1, 2).reshape(N * M, D, hw, hw)
+        g = grids[:, :, :, lid].transpose(1, 2).flatten(0, 1)
+        outs.append(F.grid_sample(v, g, mode="bilinear", padding_mode="zeros", align_corners=False))
+    aw = aw.transpose(1, 2).reshape(N * M, 1, Lq, L * P)
+    out = (torch.stack(outs, dim=-2).flatten(-2) * aw).sum(-1).view(N, M * D, Lq)
+    return out.transpose(1, 2)
+
 
 def _net(seed=0):
     from mmt_amd.model import build_mixformer_vit_rgbt, hot_path_cfg
