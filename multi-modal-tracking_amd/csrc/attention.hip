@@ -22,6 +22,29 @@ namespace {
 
 constexpr int D = 64, KB = 64;
 
+// XCD-aware bijective block remap (as gemm.hip): workgroups are dealt round-robin over the 8 XCDs,
+// so consecutive (query block, head, sequence) ids would put the query blocks of one (sequence,
+// head) on different XCDs, each fetching the same K / V rows into its own L2.  Giving each XCD a
+// contiguous run of ids (query block fastest) keeps those re-reads in one L2.  Speed only; applied
+// to grids larger than the chip (batched inference: B = 8 / 32 throughput kernel 33 -> 29 / 90 ->
+// 84 us), not to the single-wave batch-1 grid.
+MMT_DEV void attn_block_ids(int& bx, int& by, int& bz) {
+    const int nbx = gridDim.x, nby = gridDim.y, nwg = nbx * nby * gridDim.z;
+    if (nwg <= 256) {
+        bx = blockIdx.x;
+        by = blockIdx.y;
+        bz = blockIdx.z;
+        return;
+    }
+    const int orig = blockIdx.x + nbx * (blockIdx.y + nby * blockIdx.z);
+    const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+    bx = lin % nbx;
+    by = (lin / nbx) % nby;
+    bz = lin / (nbx * nby);
+}
+
+
 template <typename T>
 struct AttnCfg {
     static constexpr bool BF = sizeof(T) == 2;
@@ -41,7 +64,9 @@ __global__ __launch_bounds__(256 / QT) void mam_attention_kernel(const mmt_attn_
 
     const int n_t = p.n_t, ntok = p.ntok, C = p.C;
     const int nqb_t = (n_t + 63) / 64;
-    const int qb = blockIdx.x + (p.q_part == 2 ? nqb_t : 0), h = blockIdx.y, s = blockIdx.z;
+    int bx, h, s;
+    attn_block_ids(bx, h, s);
+    const int qb = bx + (p.q_part == 2 ? nqb_t : 0);
     const bool tmpl = qb < nqb_t;
     const int q0 = tmpl ? qb * 64 : n_t + (qb - nqb_t) * 64;
     const int qend = tmpl ? n_t : ntok;
@@ -335,7 +360,9 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(KG, KG
 
     const int n_t = p.n_t, ntok = p.ntok, C = p.C;
     const int nqb_t = (n_t + 63) / 64;
-    const int qb = blockIdx.x + (p.q_part == 2 ? nqb_t : 0), h = blockIdx.y, s = blockIdx.z;
+    int bx, h, s;
+    attn_block_ids(bx, h, s);
+    const int qb = bx + (p.q_part == 2 ? nqb_t : 0);
     const bool tmpl = qb < nqb_t;
     const int q0 = tmpl ? qb * 64 : n_t + (qb - nqb_t) * 64;
     const int qend = tmpl ? n_t : ntok;
@@ -573,7 +600,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 
     const int n_t = p.n_t, ntok = p.ntok, C = p.C;
     const int nqb_t = (n_t + FQ - 1) / FQ;
-    const int qb = blockIdx.x + (p.q_part == 2 ? nqb_t : 0), h = blockIdx.y, s = blockIdx.z;
+    int bx, h, s;
+    attn_block_ids(bx, h, s);
+    const int qb = bx + (p.q_part == 2 ? nqb_t : 0);
     const bool tmpl = qb < nqb_t;
     const int q0 = tmpl ? qb * FQ : n_t + (qb - nqb_t) * FQ;
     const int qend = tmpl ? n_t : ntok;
@@ -774,10 +803,227 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Throughput kernel on 32x32x16 MFMAs (impl 10-12): same workgroup geometry, DMA ring and softmax
+// tricks as mam_attention_fa_kernel, but each wave's 32 queries are ONE MFMA column block:
+//   S^T[32 keys][32 queries] = K Q^T: 4 v_mfma_f32_32x32x16_bf16 per 32-key block, C = the running
+//     -m broadcast (a persistent 16-register block, rewritten only when the maximum is rebased);
+//   lane l owns query l%32 and 16 keys of the block (rows 8*(r/4) + 4*(l/32) + r%4), so the row
+//     maximum is 32 v_max per 64-key tile + one permlane32 swap (no permlane16 stage), and the row
+//     sum is kept per half-wave and combined once at the end;
+//   O^T[64 d][32 queries] += V^T P^T: 2 d-blocks x 4 16-key steps; the 8 keys a lane contributes to
+//     a step are {4h..4h+3, 8+4h..8+4h+3}, so the V^T operand is two ds_read_b64_tr_b16 (rows base +
+//     qr and base + 8 + qr) and P needs no permlane.
+// Half the MFMA instructions of the 16x16x32 kernel for the same FLOPs (each 32x32x16 holds the
+// SIMD's VALU issue 8 of its 32 cycles instead of 8 of 16), which leaves the VALU for the softmax.
+// Measured SLOWER than impl 8 as compiled (B = 32: 100.5 vs 84.0 us): hipcc copies the -m block
+// into each accumulator (8 v_mov_b64 per block) and drains lgkmcnt(0) right after the first K
+// reads; kept as an A/B variant (parity-tested) for a hand-scheduled version.
+// V image swizzle: chunk c of row r at c ^ (r & 6) ^ ((r & 2) << 1): the 4 rows x 4 chunks a
+// half-wave reads per tr instruction then cover all 64 banks once.
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+MMT_DEV int attn_vswz(int row) { return (row & 6) ^ ((row & 2) << 1); }
+
+template <int FNS, int OCC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void mam_attention_fa32_kernel(
+    const mmt_attn_params p) {
+    __shared__ __attribute__((aligned(1024))) char lds[FNS * FTILE + FQ * 128];
+    char* qimg = lds + FNS * FTILE;
+
+    const int n_t = p.n_t, ntok = p.ntok, C = p.C;
+    const int nqb_t = (n_t + FQ - 1) / FQ;
+    int bx, h, s;
+    attn_block_ids(bx, h, s);
+    const int qb = bx + (p.q_part == 2 ? nqb_t : 0);
+    const bool tmpl = qb < nqb_t;
+    const int q0 = tmpl ? qb * FQ : n_t + (qb - nqb_t) * FQ;
+    const int qend = tmpl ? n_t : ntok;
+    const int Lk = tmpl ? n_t : (p.asym ? ntok + n_t : ntok);
+    const bool cross = p.asym && !tmpl;
+    const int64_t rs = 3 * (int64_t)C;
+    const bf16_t* qkv = (const bf16_t*)p.qkv;
+    const int sV = s % p.Bm, sI = sV + p.Bm;
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int l32 = lane & 31, hf = lane >> 5;
+    const int prow = lane >> 3, pcol = lane & 7;
+
+    // ---- K / V DMA (waves 0-1: K, 2-3: V), 4 pieces of 8 rows per wave per tile
+    const int isv = w >> 1;
+    const int64_t col = (isv ? 2 * C : C) + h * D + (isv ? (pcol ^ attn_vswz(prow)) : (pcol ^ prow)) * 8;
+    auto key_row = [&](int kk) -> const bf16_t* {
+        int seq = s, row = kk;
+        if (cross) {
+            if (kk < n_t) seq = sV;
+            else if (kk < 2 * n_t) { seq = sI; row = kk - n_t; }
+            else row = kk - n_t;
+        }
+        return qkv + ((int64_t)seq * ntok + row) * rs;
+    };
+    const bool aligned = n_t % KB == 0;
+    const int nkt = (Lk + KB - 1) / KB;
+    auto issue_tile = [&](int t) {
+        char* slot = lds + (t % FNS) * FTILE + isv * KB * 128;
+        if (aligned && t * KB + KB <= Lk) {
+            const bf16_t* base = key_row(t * KB);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int pk = (w & 1) * 4 + i;
+                attn_glds16(base + (int64_t)(pk * 8 + prow) * rs + col, slot + pk * 1024);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int pk = (w & 1) * 4 + i;
+                attn_glds16(key_row(min(t * KB + pk * 8 + prow, Lk - 1)) + col, slot + pk * 1024);
+            }
+        }
+    };
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int piece = w * 4 + i, r = piece * 8 + prow;
+        const bf16_t* src = qkv + ((int64_t)s * ntok + min(q0 + r, qend - 1)) * rs + h * D;
+        attn_glds16(src + ((pcol ^ prow) * 8), qimg + piece * 1024);
+    }
+    for (int t = 0; t < FNS - 1 && t < nkt; ++t) issue_tile(t);
+
+    const bool active = q0 + 32 * w < qend;
+    const float cexp = p.scale * 1.4426950408889634f;
+    const bool prescale = fabsf(cexp - 1.f) > 1e-6f;
+    float mr = 0.f, lsum = 0.f;
+    f32x16 o[2], negm;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { o[0][r] = 0.f; o[1][r] = 0.f; negm[r] = 0.f; }
+    u32x4 qf[4];
+    // this lane's K fragment rows (32kb + l32) and V^T read offsets (rows 4*hf + qr (+8), chunk 4db + 2*dsub + pc/2)
+    const int kpos = ((l32 & 7) * 16);
+    const int li = lane & 15, qr = li >> 2, pc = li & 3, dsub = (lane >> 4) & 1;
+
+    for (int kt = 0; kt < nkt; ++kt) {
+        attn_wait_dyn(4 * (min(nkt - 1, kt + FNS - 2) - kt));
+        lds_barrier();
+        if (kt + FNS - 1 < nkt) issue_tile(kt + FNS - 1);
+        if (kt == 0) {
+            const int row = 32 * w + l32;
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) {
+                qf[ks] = *(const u32x4*)(qimg + row * 128 + (((2 * ks + hf) ^ (row & 7)) * 16));
+                if (prescale) {
+                    u32x4 v = qf[ks];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        v[e] = pack_bf16x2(__uint_as_float(v[e] << 16) * cexp, __uint_as_float(v[e] & 0xffff0000u) * cexp);
+                    qf[ks] = v;
+                }
+            }
+        }
+        if (!active) continue;
+        const char* kimg = lds + (kt % FNS) * FTILE;
+        const char* vimg = kimg + KB * 128;
+        f32x16 sacc[2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            const char* krow = kimg + (32 * kb + l32) * 128;
+            u32x4 kf[4];
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) kf[ks] = *(const u32x4*)(krow + ((((2 * ks + hf) * 16) ^ kpos)));
+            sacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kf[0]),
+                                                               __builtin_bit_cast(bf16x8, qf[0]), negm, 0, 0, 0);
+#pragma unroll
+            for (int ks = 1; ks < 4; ++ks)
+                sacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kf[ks]),
+                                                                   __builtin_bit_cast(bf16x8, qf[ks]), sacc[kb], 0, 0, 0);
+        }
+        // V^T fragments, issued behind the QK^T MFMAs
+        uint2 vt[4][2][2];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int row = 16 * j + 4 * hf + qr;
+#pragma unroll
+            for (int db = 0; db < 2; ++db) {
+                const char* b1 = vimg + row * 128 + (((4 * db + 2 * dsub + (pc >> 1)) ^ attn_vswz(row)) * 16) + (pc & 1) * 8;
+                vt[j][db][0] = attn_tr16<0>(b1);
+                vt[j][db][1] = attn_tr16<8 * 128>(b1);
+            }
+        }
+        if (kt * KB + KB > Lk) {
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if (kt * KB + 32 * kb + 8 * (r >> 2) + 4 * hf + (r & 3) >= Lk) sacc[kb][r] = -1e30f;
+        }
+        float mx = fmaxf(sacc[0][0], sacc[0][1]);
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = (kb == 0 ? 2 : 0); r < 16; r += 2) mx = __builtin_fmaxf(mx, __builtin_fmaxf(sacc[kb][r], sacc[kb][r + 1]));
+        {
+            auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+            mx = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+        }
+        if (kt == 0 || __any(mx > FA_THR)) {
+            const float d = kt == 0 ? mx : fmaxf(mx, 0.f);
+            mr += d;
+            const float alpha = __builtin_amdgcn_exp2f(-d);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                sacc[0][r] -= d;
+                sacc[1][r] -= d;
+                o[0][r] *= alpha;
+                o[1][r] *= alpha;
+                negm[r] = -mr;
+            }
+            lsum *= alpha;
+        }
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                sacc[kb][r] = __builtin_amdgcn_exp2f(sacc[kb][r]);
+                lsum += sacc[kb][r];
+            }
+        attn_lds_wait();
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int kb = j >> 1, rb = 8 * (j & 1);
+            const bf16x8 pf = __builtin_bit_cast(
+                bf16x8, u32x4{pack_bf16x2(sacc[kb][rb], sacc[kb][rb + 1]), pack_bf16x2(sacc[kb][rb + 2], sacc[kb][rb + 3]),
+                              pack_bf16x2(sacc[kb][rb + 4], sacc[kb][rb + 5]), pack_bf16x2(sacc[kb][rb + 6], sacc[kb][rb + 7])});
+#pragma unroll
+            for (int db = 0; db < 2; ++db) {
+                const uint2 ua = vt[j][db][0], ub = vt[j][db][1];
+                const bf16x8 vf = __builtin_bit_cast(bf16x8, make_uint4(ua.x, ua.y, ub.x, ub.y));
+                o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[db], 0, 0, 0);
+            }
+        }
+    }
+
+    if (!active) return;
+    {
+        auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(lsum), __float_as_uint(lsum), false, false);
+        lsum = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    }
+    const float inv = 1.f / lsum;
+    const int q = q0 + 32 * w + l32;
+    if (q < qend) {
+        if (p.lse && hf == 0) p.lse[((int64_t)s * p.H + h) * ntok + q] = mr + __builtin_amdgcn_logf(lsum);
+        bf16_t* op = (bf16_t*)p.out + ((int64_t)s * ntok + q) * C + h * D;
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                *(uint2*)(op + 32 * db + 8 * g + 4 * hf) =
+                    make_uint2(pack_bf16x2(o[db][4 * g] * inv, o[db][4 * g + 1] * inv),
+                               pack_bf16x2(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv));
+    }
+}
+
 template <typename T>
 int launch_attn(const mmt_attn_params& p, hipStream_t st) {
-    if (p.impl != 0 && p.impl != 2 && p.impl != 4 && (p.impl < 8 || p.impl > 9)) return MMT_EBADARG;
-    if (p.lse && (sizeof(T) != 2 || p.impl == 9)) return MMT_EBADARG;
+    if (p.impl != 0 && p.impl != 2 && p.impl != 4 && (p.impl < 8 || p.impl > 12)) return MMT_EBADARG;
+    if (p.lse && (sizeof(T) != 2 || p.impl == 9 || p.impl > 9)) return MMT_EBADARG;
     if (!p.qkv || !p.out || p.H <= 0 || p.C != p.H * D || p.S <= 0 || p.ntok <= p.n_t || p.n_t <= 0) return MMT_EBADARG;
     if (p.asym && (p.Bm <= 0 || p.S != 2 * p.Bm)) return MMT_EBADARG;
     if (((uintptr_t)p.qkv | (uintptr_t)p.out) & 15) return MMT_EBADARG;
@@ -800,6 +1046,12 @@ int launch_attn(const mmt_attn_params& p, hipStream_t st) {
         }
         if (p.impl == 9) {  // ring-depth / occupancy variant (A/B): 3-deep ring, 2 workgroups per CU
             hipLaunchKernelGGL((mam_attention_fa_kernel<3, 2>), fgrid, dim3(256), 0, st, p);
+            return launch_status();
+        }
+        if (p.impl >= 10) {  // 32x32x16 throughput kernel (A/B): 10 = ring 2 / 2 WG per CU, 11 = 3 / 2, 12 = 2 / 3
+            if (p.impl == 10) hipLaunchKernelGGL((mam_attention_fa32_kernel<2, 2>), fgrid, dim3(256), 0, st, p);
+            else if (p.impl == 11) hipLaunchKernelGGL((mam_attention_fa32_kernel<3, 2>), fgrid, dim3(256), 0, st, p);
+            else hipLaunchKernelGGL((mam_attention_fa32_kernel<2, 3>), fgrid, dim3(256), 0, st, p);
             return launch_status();
         }
         const int kg = p.impl > 0 ? p.impl : 4;

@@ -311,7 +311,7 @@ def _attn_ref(qkv, S, Bm, ntok, n_t, C, H, asym):
     return out.permute(0, 2, 1, 3).reshape(S, ntok, C)
 
 
-@pytest.mark.parametrize("dname,impl", [("f32", 0), ("bf16", 2), ("bf16", 4), ("bf16", 8), ("bf16", 9)])
+@pytest.mark.parametrize("dname,impl", [("f32", 0), ("bf16", 2), ("bf16", 4), ("bf16", 8), ("bf16", 9), ("bf16", 10), ("bf16", 11), ("bf16", 12)])
 @pytest.mark.parametrize("asym", [0, 1])
 @pytest.mark.parametrize("Bm,ntok,n_t,H", [(1, 528, 128, 12), (2, 100, 36, 2), (1, 70, 8, 1), (1, 864, 288, 2)])
 def test_mam_attention(dname, impl, asym, Bm, ntok, n_t, H):
@@ -335,7 +335,7 @@ def test_mam_attention(dname, impl, asym, Bm, ntok, n_t, H):
     assert err <= (1.5e-2 if dt == torch.bfloat16 else 2e-5), err
 
 
-@pytest.mark.parametrize("dname,impl", [("f32", 0), ("bf16", 2), ("bf16", 4), ("bf16", 8), ("bf16", 9)])
+@pytest.mark.parametrize("dname,impl", [("f32", 0), ("bf16", 2), ("bf16", 4), ("bf16", 8), ("bf16", 9), ("bf16", 10), ("bf16", 11), ("bf16", 12)])
 def test_mam_attention_rescale_branch(dname, impl):
     """Online-softmax rescale forced: one key per query block carries a huge score in a late tile
     (bf16: and in a different key group than the first tile, so the group merge rescales)."""
@@ -357,7 +357,7 @@ def test_mam_attention_rescale_branch(dname, impl):
     assert (out.float().cpu() - ref).abs().max().item() < (1.5e-2 if dt == torch.bfloat16 else 5e-5)
 
 
-@pytest.mark.parametrize("impl", [2, 4, 8, 9])
+@pytest.mark.parametrize("impl", [2, 4, 8, 9, 10, 12])
 @pytest.mark.parametrize("asym", [0, 1])
 def test_mam_attention_prescaled_q(impl, asym):
     """The runtime's convention (bf16): q arrives multiplied by scale * log2(e) (folded into the qkv
