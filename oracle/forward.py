@@ -27,7 +27,8 @@ import torch.nn.functional as F
 from .msda import ms_deform_attn
 from .prroi import prroi_pool2d
 
-VARIANTS = ("rgbt", "shared", "asym", "asym_online")
+VARIANTS = ("rgbt", "shared", "asym", "asym_online", "asym_ce")
+CE_LOC, CE_KEEP = (3, 6, 9), (0.7, 0.7, 0.7)  # lib/config/asymmetric_shared_ce/config.py:23-24
 
 
 # ----------------------------------------------------------------------------- helpers
@@ -163,6 +164,72 @@ def backbone_asym(sd, pre, t, o, s):
         res = res + _mlp(sd, b + "mlp", xn)
         x_v, x_i = res[:Bh], res[Bh:]
     return _split_out(torch.cat([x_v, x_i], 0), B2, C, gt, gs)
+
+
+def ce_attn_mean(q_v, q_i, k_v, k_i, n_t, scale):
+    """attn_t2s of Asym_Attention.forward(return_attention=True) (asymmetric_shared_ce.py:198-202),
+    averaged over template queries and heads (candidate_elimination :83-89, mask None):
+    softmax over [k_s_V | k_s_I] of [q_mt_V; q_mt_I], -> (B, 2 * lens_s) [RGB | TIR]."""
+    q = torch.cat([q_v[:, :, :n_t], q_i[:, :, :n_t]], 2)
+    k = torch.cat([k_v[:, :, n_t:], k_i[:, :, n_t:]], 2)
+    a = ((q @ k.transpose(-2, -1)) * scale).softmax(dim=-1)
+    return a.mean(dim=2).mean(dim=1)
+
+
+def ce_select(attn_mean, x, n_t, keep_ratio, gidx):
+    """get_token_from_attn (asymmetric_shared_ce.py:22-46) for one modality: sort the search tokens'
+    mean attention descending, keep the first ceil(keep_ratio * lens_s) (in that order) after the
+    template tokens; gidx tracks their original search positions."""
+    lens_s = x.shape[1] - n_t
+    keep = math.ceil(keep_ratio * lens_s)
+    if keep == lens_s:
+        return x, gidx
+    order = torch.sort(attn_mean, dim=1, descending=True)[1][:, :keep]
+    xs = x[:, n_t:].gather(1, order.unsqueeze(-1).expand(-1, -1, x.shape[2]))
+    return torch.cat([x[:, :n_t], xs], 1), gidx.gather(1, order)
+
+
+def backbone_asym_ce(sd, pre, t, o, s, stages=None):
+    """asymmetric_shared_ce.py:228-282 (CE_Block_Shared), :372-424 (VisionTransformer.forward with
+    _recover_search).  The elimination runs after a CE block's attention residual, before its MLP;
+    pruned search positions come back as zero tokens.  `stages` (a list) receives the kept indices."""
+    C, H, depth, gt, gs = _vit_dims(sd, pre)
+    x = _tokens(sd, pre, t, o, s)
+    B2 = x.shape[0]
+    Bh = B2 // 2
+    n_t = 2 * gt * gt
+    N = gs * gs
+    gidx = [torch.arange(N).repeat(Bh, 1), torch.arange(N).repeat(Bh, 1)]
+    x_v, x_i = x[:Bh], x[Bh:]
+    scale = (C // H) ** -0.5
+    for i in range(depth):
+        b = pre + "blocks.%d." % i
+        n = x_v.shape[1]
+        res = torch.cat([x_v, x_i], 0)
+        xn_v, xn_i = _ln(sd, b + "norm1_v", x_v, 1e-6), _ln(sd, b + "norm1_i", x_i, 1e-6)
+        a_v, a_i = mam_attention_asym(sd[b + "attn.qkv.weight"], sd[b + "attn.qkv.bias"], sd[b + "attn.proj.weight"],
+                                      sd[b + "attn.proj.bias"], xn_v, xn_i, n_t, H)
+        res = res + torch.cat([a_v, a_i], 0)
+        x_v, x_i = res[:Bh], res[Bh:]
+        if i in CE_LOC:
+            qkv = F.linear(torch.cat([xn_v, xn_i], 0), sd[b + "attn.qkv.weight"], sd[b + "attn.qkv.bias"])
+            q, k, _ = _heads(qkv, B2, n, H).unbind(0)
+            am = ce_attn_mean(q[:Bh], q[Bh:], k[:Bh], k[Bh:], n_t, scale)
+            ls = n - n_t
+            x_v, gidx[0] = ce_select(am[:, :ls], x_v, n_t, CE_KEEP[CE_LOC.index(i)], gidx[0])
+            x_i, gidx[1] = ce_select(am[:, ls:], x_i, n_t, CE_KEEP[CE_LOC.index(i)], gidx[1])
+            if stages is not None:
+                stages.append((am, gidx[0].clone(), gidx[1].clone()))
+        res = torch.cat([x_v, x_i], 0)
+        xn = torch.cat([_ln(sd, b + "norm2_v", x_v, 1e-6), _ln(sd, b + "norm2_i", x_i, 1e-6)], 0)
+        res = res + _mlp(sd, b + "mlp", xn)
+        x_v, x_i = res[:Bh], res[Bh:]
+    outs = []
+    for xm, gm in ((x_v, gidx[0]), (x_i, gidx[1])):  # _recover_search: scatter back, zeros where pruned
+        full = torch.zeros(Bh, N, C, dtype=xm.dtype)
+        full.scatter_(1, gm.unsqueeze(-1).expand(-1, -1, C), xm[:, n_t:])
+        outs.append(torch.cat([xm[:, :n_t], full], 1))
+    return _split_out(torch.cat(outs, 0), B2, C, gt, gs)
 
 
 # ----------------------------------------------------------------------------- fusion
@@ -361,8 +428,10 @@ def forward(sd, variant, template, online_template, search, run_score_head=False
         ti, oi, si = backbone_two_stream(sd, "backbone_i.", template[1], online_template[1], search[1])
         t_all = torch.cat([tv, ti], 0)
     else:
-        fn = backbone_shared if variant == "shared" else backbone_asym
-        t_all, _, s_all = fn(sd, "backbone.", torch.cat(template, 0), torch.cat(online_template, 0), torch.cat(search, 0))
+        fn = {"shared": backbone_shared, "asym_ce": backbone_asym_ce}.get(variant, backbone_asym)
+        kw = {"stages": aux.setdefault("ce_stages", [])} if variant == "asym_ce" else {}
+        t_all, _, s_all = fn(sd, "backbone.", torch.cat(template, 0), torch.cat(online_template, 0), torch.cat(search, 0),
+                             **kw)
         Bh = s_all.shape[0] // 2
         sv, si = s_all[:Bh], s_all[Bh:]
     aux["search_v"], aux["search_i"] = sv, si

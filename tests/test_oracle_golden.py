@@ -134,3 +134,28 @@ def test_oracle_prroi_empty_and_outside():
     assert np.all(out[0] == 0)          # zero-width RoI -> empty bins
     assert np.all(out[1] == 0)          # fully outside -> zero-padded integral
     assert 0 < out[2, 0, 1, 1] <= 1.0   # partially outside -> partial mass
+
+
+@pytest.mark.parametrize("B", [1, 2])
+def test_oracle_candidate_elimination_matches_reference(B):
+    """asymmetric_shared_ce: boxes, maps and features, plus every elimination
+    stage's mean template->search attention and kept token indices (reference order), vs the
+    reference's own forward (tests/golden/make_golden_ce.py)."""
+    from mmt_amd import synthetic
+    from oracle import forward as of
+    torch.set_num_threads(8)
+    g = np.load(GOLDEN + "/model_asym_ce_b%d.npz" % B)
+    sd = of.state_dict_to_torch(synthetic.synth_state_dict(json.load(open(GOLDEN + "/state_dict_asym_ce.json"))))
+    t, o, s = synthetic.synth_inputs(B)
+    out, coord, aux = of.forward(sd, "asym_ce", t, o, s, return_aux=True)
+    assert np.abs(out["pred_boxes"].numpy() - g["pred_boxes"]).max() < 1e-5
+    for nm in ("score_map_tl", "score_map_br"):
+        assert np.abs(aux[nm].numpy() - g[nm]).max() < 1e-4 * max(1.0, np.abs(g[nm]).max())
+    for nm in ("search_v", "search_i", "fused"):
+        sub, sums = _sub(aux[nm])
+        assert np.abs(sub - g[nm + "_sub"]).max() < 1e-4 * max(1.0, np.abs(g[nm + "_sub"]).max())
+    assert len(aux["ce_stages"]) == 3
+    for k, (am, kv, ki) in enumerate(aux["ce_stages"]):
+        assert np.abs(am.numpy() - g["ce%d_attn_mean" % k]).max() <= 1e-6 * np.abs(g["ce%d_attn_mean" % k]).max()
+        assert np.array_equal(kv.numpy(), g["ce%d_keep_v" % k]) and np.array_equal(ki.numpy(), g["ce%d_keep_i" % k])
+    assert [g["ce%d_keep_v" % k].shape[1] for k in range(3)] == [280, 196, 138]
