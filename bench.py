@@ -40,7 +40,8 @@ PEAK = {"bf16": 2500.0, "f32": 157.3}  # dense MFMA TFLOP/s, MI355X_MICROARCH.md
 GEO_B = {"hidden": 768, "depth": 12, "search": 320, "template": 128}
 GEO_L = {"hidden": 1024, "depth": 24, "search": 384, "template": 192}
 VARIANT_NAMES = {"rgbt": "mixformer_vit_rgbt (two-stream)", "shared": "mixformer_vit_rgbt_shared",
-                 "asym": "asymmetric_shared", "asym_online": "asymmetric_shared_online_score"}
+                 "asym": "asymmetric_shared", "asym_online": "asymmetric_shared_online_score",
+                 "asym_ce": "asymmetric_shared_ce (candidate elimination 3/6/9 x0.7)"}
 
 
 def state_dict_keys(variant, hidden=768, depth=12, search=320, template=128, fusion_layers=2):
@@ -58,9 +59,10 @@ def plan_flops(rt, entry):
     if hasattr(keep, "K"):
         return 2.0 * keep.M * keep.N * keep.K * keep.groups
     d = rt.d
-    lk_s = d.ntok + (d.n_t if keep.asym else 0)
+    ntok = keep.ntok  # < d.ntok after a candidate-elimination stage
+    lk_s = ntok + (d.n_t if keep.asym else 0)
     qpart = getattr(keep, "q_part", 0)
-    return 4.0 * 64 * keep.H * keep.S * ((d.n_t * d.n_t if qpart != 2 else 0) + (d.ns * lk_s if qpart != 1 else 0))
+    return 4.0 * 64 * keep.H * keep.S * ((d.n_t * d.n_t if qpart != 2 else 0) + ((ntok - d.n_t) * lk_s if qpart != 1 else 0))
 
 
 def kernel_profile(rt, plan, per_graph=20, replays=5):
@@ -317,7 +319,7 @@ def main():
         }
         if args.dtype == "bf16" and not args.no_kernel_profile and not args.no_mam_batched:
             out["roofline_mam_batched"] = mam_batched(rt)
-        if use_graph and not args.no_kv_cache:
+        if use_graph and not args.no_kv_cache and args.variant != "asym_ce":  # no template cache with CE
             out["tracking_kv_cache"] = kv_cache_tracking(rt, pool, score, args.steps, args.warmup)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.variant, B, budget_s=20.0 if args.vitl else 12.0, geo=geo)

@@ -36,6 +36,8 @@
  *       head.py:191-212, mixformer.py:419-432
  *   mmt_conv3x3_c1              the 1-channel conv-BN-ReLU of adjust3/adjust4, head.py:115-120
  *   mmt_spm_attention           ScoreDecoder single-query attention, score_decoder.py:55-61
+ *   mmt_ce_t2s_attention / mmt_ce_select / mmt_ce_gather / mmt_ce_recover  candidate elimination
+ *       of asymmetric_shared_ce.py:22-102, :198-202, :426-447 (attn_t2s mean, sorted top-k, recover)
  *   mmt_sample_target           the trackers' host crop + preprocessing, processing_utils.py:15-77,
  *       tracker_utils.py:24-48 (cv2 crop/pad/resize, colour map, normalise)
  *   mmt_track_update            map_box_back + clip_box, lib/test/tracker/mixformer_vit_rgbt.py:92-95,
@@ -145,6 +147,9 @@ typedef struct {
                        [n_t,ntok) only -- the template K/V cache: template rows of qkv computed
                        once per template update, only the search rows per frame.  Rows of `out`
                        outside the part are not written. */
+    int32_t tok_pitch; /* rows between consecutive sequences in qkv / out; 0 = ntok.  Candidate
+                       elimination keeps each sequence's rows at the original pitch and runs on
+                       its first ntok (template + surviving search) rows (not with lse). */
 } mmt_attn_params;
 
 int mmt_mam_attention(const mmt_attn_params* p, int dtype, void* stream);
@@ -210,6 +215,32 @@ int mmt_ms_deform_attn_backward(const void* value, const int64_t* spatial_shapes
                                 const void* sampling_loc, const void* attn_weight, const void* grad_output,
                                 void* grad_value, void* grad_loc, void* grad_attn, int N, int S, int M, int D,
                                 int Lq, int L, int P, int dtype, void* stream);
+
+/* ---------------------------------------------------------------- candidate elimination
+ * asymmetric_shared_ce.py (CE_Block_Shared :228-282, candidate_elimination :52-102,
+ * get_token_from_attn :22-46, _recover_search :426-447).  Token streams are [S][tok_pitch][C]
+ * with S = 2*Bm sequences, modality-major; a stage keeps each sequence's first n_t + keep rows.
+ *   mmt_ce_t2s_attention: partial[Bm][H][2*n_t/QB][2*n_s] (QB = 16 for MMT_BF16, 8 for MMT_F32)
+ *     column sums of the template->search
+ *     softmax (qkv [S][tok_pitch][3C], q/k in place; scale in natural-log units, i.e. 1/log2(e)
+ *     when q carries scale*log2(e) already);
+ *   mmt_ce_select: sums the partials (into each frame's first partial row, so `partial` is
+ *     overwritten) and ranks each modality's n_s tokens by the sum (desc, ties by index)
+ *     and keeps `keep`: order[S][ns_full] (slot -> current row - n_t), gidx_out = original search
+ *     positions (gidx_in NULL = identity), attn_mean[Bm][2*n_s] = sums * mean_scale (NULL = not
+ *     written);
+ *   mmt_ce_gather: xc rows [0, n_t + keep) of every sequence = x's template rows then the kept
+ *     rows in order (xn, if not NULL, gets the same rows cast to xn_dtype);
+ *   mmt_ce_recover: out rows [n_t, n_t + ns_full) = x's surviving rows (slots [0, keep) of the
+ *     final gidx) at their original positions, zeros where pruned (dtype MMT_BF16 / MMT_F32). */
+int mmt_ce_t2s_attention(const void* qkv, float* partial, int Bm, int tok_pitch, int n_t, int n_s, int C, int H,
+                         float scale, int dtype, void* stream);
+int mmt_ce_select(float* partial, int nparts, int Bm, int n_s, int keep, int ns_full, const int* gidx_in,
+                  int* gidx_out, int* order, float* attn_mean, float mean_scale, void* stream);
+int mmt_ce_gather(const float* x, float* xc, void* xn, const int* order, int S, int tok_pitch, int n_t, int keep,
+                  int ns_full, int C, int xn_dtype, void* stream);
+int mmt_ce_recover(const float* x, const int* gidx, int keep, void* out, int S, int tok_pitch, int n_t, int ns_full,
+                   int C, int dtype, void* stream);
 
 /* Bimodal encoder layer core (ms_deform_attn_bimodal.py:97-128) for nq queries per modality on an
  * hw x hw map, 8 heads x 64 ch, 2 levels x 4 points: offw[b*nq+q][192] fp32 = [sampling_offsets

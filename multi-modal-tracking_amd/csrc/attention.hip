@@ -63,6 +63,7 @@ __global__ __launch_bounds__(256 / QT) void mam_attention_kernel(const mmt_attn_
     __shared__ __attribute__((aligned(16))) char vl[2][KB * VROW];
 
     const int n_t = p.n_t, ntok = p.ntok, C = p.C;
+    const int64_t pitch = p.tok_pitch > 0 ? p.tok_pitch : ntok;  // rows between sequences
     const int nqb_t = (n_t + 63) / 64;
     int bx, h, s;
     attn_block_ids(bx, h, s);
@@ -84,7 +85,7 @@ __global__ __launch_bounds__(256 / QT) void mam_attention_kernel(const mmt_attn_
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) {
         const int q = q0 + 16 * QT * w + 16 * qt + l16;
-        const T* qp = qkv + ((int64_t)s * ntok + min(q, qend - 1)) * rs + h * D;  // clamped, never stored
+        const T* qp = qkv + ((int64_t)s * pitch + min(q, qend - 1)) * rs + h * D;  // clamped, never stored
 #pragma unroll
         for (int t = 0; t < QCH; ++t) qf[qt][t] = *(const u32x4*)(qp + (4 * t + lg) * (16 / (int)sizeof(T)));
     }
@@ -99,7 +100,7 @@ __global__ __launch_bounds__(256 / QT) void mam_attention_kernel(const mmt_attn_
             else if (kk < 2 * n_t) { seq = sI; row = kk - n_t; }
             else row = kk - n_t;
         }
-        return qkv + ((int64_t)seq * ntok + row) * rs + h * D;
+        return qkv + ((int64_t)seq * pitch + row) * rs + h * D;
     };
     // K/V loads are unconditional (rows past Lk re-read key Lk-1 and are masked in the scores;
     // their V rows are multiplied by p = 0): a guarded load would make hipcc drain vmcnt(0).
@@ -262,7 +263,7 @@ __global__ __launch_bounds__(256 / QT) void mam_attention_kernel(const mmt_attn_
         const float inv = 1.f / l;
         const int q = q0 + 16 * QT * w + 16 * qt + l16;
         if (q >= qend) continue;
-        T* op = out + ((int64_t)s * ntok + q) * C + h * D;
+        T* op = out + ((int64_t)s * pitch + q) * C + h * D;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) {
             if constexpr (Cfg::BF) {
@@ -359,6 +360,7 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(KG, KG
     MMT_ASTAMP(1, "s_memtime");
 
     const int n_t = p.n_t, ntok = p.ntok, C = p.C;
+    const int64_t pitch = p.tok_pitch > 0 ? p.tok_pitch : ntok;  // rows between sequences
     const int nqb_t = (n_t + 63) / 64;
     int bx, h, s;
     attn_block_ids(bx, h, s);
@@ -384,7 +386,7 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(KG, KG
             else if (kk < 2 * n_t) { seq = sI; row = kk - n_t; }
             else row = kk - n_t;
         }
-        return qkv + ((int64_t)seq * ntok + row) * rs + h * D;
+        return qkv + ((int64_t)seq * pitch + row) * rs + h * D;
     };
     const int nkt = (Lk + KB - 1) / KB, nr = (nkt + KG - 1) / KG;
     // Tile t into slot t % ANS: its 16 pieces (8 K, 8 V) are dealt over the waves, PPW each.
@@ -407,7 +409,7 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(KG, KG
 #pragma unroll
         for (int i = 0; i < (NWV >= 8 ? 1 : 8 / NWV); ++i) {
             const int piece = NWV >= 8 ? w : w * (8 / NWV) + i, r = piece * 8 + prow;
-            const bf16_t* src = qkv + ((int64_t)s * ntok + min(q0 + r, qend - 1)) * rs + h * D;
+            const bf16_t* src = qkv + ((int64_t)s * pitch + min(q0 + r, qend - 1)) * rs + h * D;
             attn_glds16(src + ((pcol ^ prow) * 8), qimg + piece * 1024);
         }
     }
@@ -553,7 +555,7 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(KG, KG
     const float inv = 1.f / lanegroup_sum(l_run);
     const int q = q0 + 16 * qw + l16;
     if (q < qend) {
-        bf16_t* op = (bf16_t*)p.out + ((int64_t)s * ntok + q) * C + h * D;
+        bf16_t* op = (bf16_t*)p.out + ((int64_t)s * pitch + q) * C + h * D;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt)
             *(uint2*)(op + dt * 16 + 4 * lg) =
@@ -599,6 +601,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     char* qimg = lds + FNS * FTILE;
 
     const int n_t = p.n_t, ntok = p.ntok, C = p.C;
+    const int64_t pitch = p.tok_pitch > 0 ? p.tok_pitch : ntok;  // rows between sequences
     const int nqb_t = (n_t + FQ - 1) / FQ;
     int bx, h, s;
     attn_block_ids(bx, h, s);
@@ -628,7 +631,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
             else if (kk < 2 * n_t) { seq = sI; row = kk - n_t; }
             else row = kk - n_t;
         }
-        return qkv + ((int64_t)seq * ntok + row) * rs;
+        return qkv + ((int64_t)seq * pitch + row) * rs;
     };
     const bool aligned = n_t % KB == 0;  // every tile lies in one key segment
     const int nkt = (Lk + KB - 1) / KB;
@@ -653,7 +656,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int piece = w * 4 + i, r = piece * 8 + prow;
-        const bf16_t* src = qkv + ((int64_t)s * ntok + min(q0 + r, qend - 1)) * rs + h * D;
+        const bf16_t* src = qkv + ((int64_t)s * pitch + min(q0 + r, qend - 1)) * rs + h * D;
         attn_glds16(src + ((pcol ^ prow) * 8), qimg + piece * 1024);
     }
     for (int t = 0; t < FNS - 1 && t < nkt; ++t) issue_tile(t);
@@ -794,7 +797,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
         if (q < qend && p.lse && lg == 0)  // training: log2-sum-exp2 of the pre-scaled scores
             p.lse[((int64_t)s * p.H + h) * ntok + q] = mr[qt] + __builtin_amdgcn_logf(lsum[qt][0]);
         if (q < qend) {
-            bf16_t* op = (bf16_t*)p.out + ((int64_t)s * ntok + q) * C + h * D;
+            bf16_t* op = (bf16_t*)p.out + ((int64_t)s * pitch + q) * C + h * D;
 #pragma unroll
             for (int dt = 0; dt < 4; ++dt)
                 *(uint2*)(op + dt * 16 + 4 * lg) = make_uint2(pack_bf16x2(o[dt][qt][0] * inv, o[dt][qt][1] * inv),
@@ -832,6 +835,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     char* qimg = lds + FNS * FTILE;
 
     const int n_t = p.n_t, ntok = p.ntok, C = p.C;
+    const int64_t pitch = p.tok_pitch > 0 ? p.tok_pitch : ntok;  // rows between sequences
     const int nqb_t = (n_t + FQ - 1) / FQ;
     int bx, h, s;
     attn_block_ids(bx, h, s);
@@ -859,7 +863,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
             else if (kk < 2 * n_t) { seq = sI; row = kk - n_t; }
             else row = kk - n_t;
         }
-        return qkv + ((int64_t)seq * ntok + row) * rs;
+        return qkv + ((int64_t)seq * pitch + row) * rs;
     };
     const bool aligned = n_t % KB == 0;
     const int nkt = (Lk + KB - 1) / KB;
@@ -883,7 +887,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int piece = w * 4 + i, r = piece * 8 + prow;
-        const bf16_t* src = qkv + ((int64_t)s * ntok + min(q0 + r, qend - 1)) * rs + h * D;
+        const bf16_t* src = qkv + ((int64_t)s * pitch + min(q0 + r, qend - 1)) * rs + h * D;
         attn_glds16(src + ((pcol ^ prow) * 8), qimg + piece * 1024);
     }
     for (int t = 0; t < FNS - 1 && t < nkt; ++t) issue_tile(t);
@@ -1009,7 +1013,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     const int q = q0 + 32 * w + l32;
     if (q < qend) {
         if (p.lse && hf == 0) p.lse[((int64_t)s * p.H + h) * ntok + q] = mr + __builtin_amdgcn_logf(lsum);
-        bf16_t* op = (bf16_t*)p.out + ((int64_t)s * ntok + q) * C + h * D;
+        bf16_t* op = (bf16_t*)p.out + ((int64_t)s * pitch + q) * C + h * D;
 #pragma unroll
         for (int db = 0; db < 2; ++db)
 #pragma unroll
@@ -1025,6 +1029,7 @@ int launch_attn(const mmt_attn_params& p, hipStream_t st) {
     if (p.impl != 0 && p.impl != 2 && p.impl != 4 && (p.impl < 8 || p.impl > 12)) return MMT_EBADARG;
     if (p.lse && (sizeof(T) != 2 || p.impl == 9 || p.impl > 9)) return MMT_EBADARG;
     if (!p.qkv || !p.out || p.H <= 0 || p.C != p.H * D || p.S <= 0 || p.ntok <= p.n_t || p.n_t <= 0) return MMT_EBADARG;
+    if (p.tok_pitch != 0 && (p.tok_pitch < p.ntok || p.lse)) return MMT_EBADARG;
     if (p.asym && (p.Bm <= 0 || p.S != 2 * p.Bm)) return MMT_EBADARG;
     if (((uintptr_t)p.qkv | (uintptr_t)p.out) & 15) return MMT_EBADARG;
     if (p.q_part < 0 || p.q_part > 2) return MMT_EBADARG;

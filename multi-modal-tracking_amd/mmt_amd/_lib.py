@@ -41,7 +41,8 @@ class GemmParams(ctypes.Structure):
 
 class AttnParams(ctypes.Structure):
     _fields_ = [("qkv", vp), ("out", vp), ("S", i32), ("Bm", i32), ("ntok", i32), ("n_t", i32), ("C", i32),
-                ("H", i32), ("asym", i32), ("scale", f32), ("impl", i32), ("lse", vp), ("q_part", i32)]
+                ("H", i32), ("asym", i32), ("scale", f32), ("impl", i32), ("lse", vp), ("q_part", i32),
+                ("tok_pitch", i32)]
 
 
 class AttnBwdParams(ctypes.Structure):
@@ -78,6 +79,10 @@ _PROTOS = {
     "mmt_prroi_pool_backward": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, f32, vp],
     "mmt_prroi_pool_coor_backward": [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, f32, vp],
     "mmt_spm_attention": [vp, i64, vp, vp, i32, i32, i32, i32, f32, vp],
+    "mmt_ce_t2s_attention": [vp, vp, i32, i32, i32, i32, i32, i32, f32, i32, vp],
+    "mmt_ce_select": [vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, f32, vp],
+    "mmt_ce_gather": [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp],
+    "mmt_ce_recover": [vp, vp, i32, vp, i32, i32, i32, i32, i32, i32, vp],
     "mmt_sample_target": [ctypes.POINTER(CropParams), i32, vp],
     "mmt_track_update": [vp, vp, vp, i32, i32, i32, i32, f64, vp],
 }

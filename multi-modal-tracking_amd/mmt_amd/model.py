@@ -269,7 +269,8 @@ class _HipTracker(nn.Module):
                 return out, coord
             ws = rt.workspace(B)
             d = rt.d
-            X = ws["X"].view(2, B, d.ntok, d.C)[:, :, d.n_t:]
+            # backbone output rows (candidate elimination: the recovered rows the fusion reads)
+            X = ws.get("XOUT", ws["X"]).view(2, B, d.ntok, d.C)[:, :, d.n_t:].float()
             feats = X.permute(0, 1, 3, 2).reshape(2, B, d.C, d.gs, d.gs).clone()
             fused = ws["FUS"].view(B, d.ns, d.C).permute(0, 2, 1).reshape(B, d.C, d.gs, d.gs).clone()
             return out, coord, feats[0], feats[1], fused
@@ -337,6 +338,33 @@ class MixFormer_RGBT_Asymmetric(MixFormer_RGBT_Shared):
     """Cross-modal asymmetric MAM (asymmetric_shared.py:336-368)."""
 
     variant = "asym"
+
+
+class MixFormer_RGBT_CE(MixFormer_RGBT_Shared):
+    """Asymmetric model with candidate elimination (asymmetric_shared_ce.py:543-608): the search
+    tokens are pruned to ceil(keep * n) after the attention of the CE_LOC blocks (by the template
+    queries' mean attention) and restored as zero tokens after the last block.  Same parameters as
+    the asymmetric model."""
+
+    variant = "asym_ce"
+
+    def __init__(self, backbone, box_head, fusion_vi, head_type="CORNER_UP", ce_loc=(3, 6, 9),
+                 ce_keep_ratio=(0.7, 0.7, 0.7)):
+        super().__init__(backbone, box_head, fusion_vi, head_type)
+        if len(ce_loc) != len(ce_keep_ratio):
+            raise ValueError("CE_LOC and CE_KEEP_RATIO differ in length")
+        self.ce_loc, self.ce_keep_ratio = tuple(int(i) for i in ce_loc), tuple(float(r) for r in ce_keep_ratio)
+
+    def _runtime(self, device):
+        if self._rt is None:
+            from .runtime import MixFormerRGBTRuntime
+            with torch.cuda.device(device):
+                self._rt = MixFormerRGBTRuntime(self.state_dict(), self.variant, dtype=self.compute_dtype,
+                                                device=device, ce=(self.ce_loc, self.ce_keep_ratio))
+        return self._rt
+
+    def set_online(self, template, online_template):
+        raise NotImplementedError("the template K/V cache is not defined for candidate elimination")
 
 
 class MixFormer_RGBT_OnlineScore(_HipTracker):
@@ -478,8 +506,24 @@ def build_asymmetric_shared_online_score(cfg, train=True):
     return model
 
 
+def build_asymmetric_shared_ce(cfg, train=True):
+    """build_asymmetric_shared_ce (asymmetric_shared_ce.py:611-675); MODEL.BACKBONE.CE_LOC /
+    CE_KEEP_RATIO as lib/config/asymmetric_shared_ce/config.py:23-24."""
+    _check_cfg(cfg)
+    bb = _backbone(cfg, True)
+    if train:
+        _load_mae(bb, cfg, True)
+    ce_loc = getattr(cfg.MODEL.BACKBONE, "CE_LOC", None) or (3, 6, 9)
+    ce_keep = getattr(cfg.MODEL.BACKBONE, "CE_KEEP_RATIO", None) or (0.7, 0.7, 0.7)
+    model = MixFormer_RGBT_CE(bb, _head(cfg), _fusion(cfg), cfg.MODEL.HEAD_TYPE, ce_loc, ce_keep)
+    if train and getattr(cfg.MODEL, "RGBT_PRETRAINED_PATH", ""):
+        _load_rgb_tracker(model, cfg.MODEL.RGBT_PRETRAINED_PATH, False)
+    return model
+
+
 BUILDERS = {"rgbt": build_mixformer_vit_rgbt, "shared": build_mixformer_vit_rgbt_shared,
-            "asym": build_asymmetric_shared, "asym_online": build_asymmetric_shared_online_score}
+            "asym": build_asymmetric_shared, "asym_online": build_asymmetric_shared_online_score,
+            "asym_ce": build_asymmetric_shared_ce}
 
 
 def hot_path_cfg(vit="base_patch16", search=320, template=128, fusion_layers=2, hidden=None):

@@ -28,7 +28,7 @@ import torch
 from . import _lib
 from ._lib import LIB, GemmParams, AttnParams, check, MMT_F32, MMT_BF16
 
-VARIANTS = ("rgbt", "shared", "asym", "asym_online")
+VARIANTS = ("rgbt", "shared", "asym", "asym_online", "asym_ce")
 
 
 LOG2E = 1.4426950408889634
@@ -72,7 +72,7 @@ class MixFormerRGBTRuntime:
     SPLITK_FLOATS = 8 << 20  # fp32 split-K partial-tile workspace (32 MiB), shared by every plan GEMM
     SPLITK_TICKETS = 1 << 16
 
-    def __init__(self, state_dict, variant, dtype=torch.bfloat16, device="cuda", fold_ln=None):
+    def __init__(self, state_dict, variant, dtype=torch.bfloat16, device="cuda", fold_ln=None, ce=None):
         """fold_ln (default: on for bf16): the ViT's LayerNorms are folded into the qkv / fc1 GEMMs
         (mmt_gemm_params.ln_fold) and the residual-producing GEMMs also write the bf16 copy of the
         residual stream those GEMMs read, so no LayerNorm launch or normalised tensor remains.
@@ -82,6 +82,9 @@ class MixFormerRGBTRuntime:
         if dtype not in (torch.bfloat16, torch.float32):
             raise ValueError("dtype must be torch.bfloat16 or torch.float32")
         self.variant = variant
+        # candidate elimination (asym_ce): {block: keep ratio}, lib/config/asymmetric_shared_ce/config.py:23-24
+        ce = ce if ce is not None else ((3, 6, 9), (0.7, 0.7, 0.7))
+        self.ce = dict(zip(ce[0], ce[1])) if variant == "asym_ce" else {}
         self.dtype = dtype
         self.cdt = MMT_BF16 if dtype == torch.bfloat16 else MMT_F32
         self.fold_ln = (dtype == torch.bfloat16) if fold_ln is None else bool(fold_ln)
@@ -274,6 +277,11 @@ class MixFormerRGBTRuntime:
             ws.update({"ROIT": e(B * 16, C, t=f32), "KV0": e(B * 16, 2 * C, t=f32), "AT": e(B, C, t=f32),
                        "XS": e(B, C, t=f32), "Q1": e(B, C, t=f32), "KV1": e(B * d.n_t, 2 * C, t=f32),
                        "M1": e(B, C, t=f32), "M2": e(B, C, t=f32), "SC": e(B, 1, t=f32)})
+        if self.ce:
+            nparts = d.H * (2 * d.n_t // 8)  # (bf16 uses 16-query blocks: half of it)
+            ws.update({"XC": e(R, C, t=f32), "CEP": e(B * nparts * 2 * ns, t=f32),
+                       "CEG": [e(S, ns, t=torch.int32) for _ in self.ce], "CEO": e(S, ns, t=torch.int32),
+                       "CEM": [e(B, 2 * ns, t=f32) for _ in self.ce]})
         ws["plan"] = self._build_plan(ws, False)
         if self.variant == "asym_online":
             ws["plan_score"] = self._build_plan(ws, True)
@@ -321,8 +329,8 @@ class MixFormerRGBTRuntime:
 
     def _build_plan(self, ws, score):
         plan = []
-        self._plan_backbone(plan, ws, None)
-        self._plan_tail(plan, ws, score)
+        xf = self._plan_backbone(plan, ws, None)
+        self._plan_tail(plan, ws, score, xf)
         return plan
 
     def _plan_backbone(self, plan, ws, part, qkv_layers=None):
@@ -344,8 +352,8 @@ class MixFormerRGBTRuntime:
         cdt = self.cdt
         off, nr = {None: (0, ntok), "t": (0, d.n_t), "s": (d.n_t, d.ns)}[part]
 
-        def rmap(ld):  # A segment map + output row map of the part's rows (identity for part None)
-            if part is None:
+        def rmap(ld):  # A segment map + output row map of the part's rows (identity for all rows)
+            if part is None and nr == ntok:
                 return {}
             return dict(seg=(nr, 1 << 30, ntok * ld, 0), cmap=(nr, ntok))
 
@@ -373,7 +381,11 @@ class MixFormerRGBTRuntime:
                        M=S * nr, N=C, K=KP, lda=KP, ldc=C, bias=[P(W["bb"][0]["patch_b"])], r=[pos_at(0)], ldr=C,
                        r_mode=1, r_p0=nr, c_f32=1, **cp, **rmap(KP))
         # --- transformer blocks
+        if self.ce and part is not None:
+            raise NotImplementedError("the template K/V cache is not defined for candidate elimination")
+        stage = 0
         for i in range(d.depth):
+            gm = B * nr  # rows per modality group (nr shrinks after each elimination stage)
             QKV = ws["QKV"] if qkv_layers is None else qkv_layers[i]
             if two:
                 blks = [W["bb"][g]["blocks"][i] for g in range(2)]
@@ -403,13 +415,36 @@ class MixFormerRGBTRuntime:
                            lda=C, ldc=3 * C, bias=wl("attn.qkv.b"), **rmap(C))
             ap = AttnParams()
             ap.qkv, ap.out, ap.S, ap.Bm, ap.ntok, ap.n_t, ap.C, ap.H = P(QKV), P(AO), S, B, ntok, d.n_t, C, d.H
-            ap.asym = 1 if self.variant in ("asym", "asym_online") else 0
+            if part is None and nr != ntok:  # after an elimination stage: first nr rows of each sequence
+                ap.ntok, ap.tok_pitch = nr, ntok
+            ap.asym = 1 if self.variant in ("asym", "asym_online", "asym_ce") else 0
             ap.scale = 1.0 / LOG2E if self.fold_ln else (C // d.H) ** -0.5  # see q_scale
             ap.q_part = {None: 0, "t": 1, "s": 2}[part]
             plan.append((LIB.mmt_mam_attention, (ctypes_byref(ap), cdt), "mam_attention", ap))
             cpx = dict(c2=rows(XN, C), c2_copy=1) if fold else {}
             self._gemm(plan, "proj", a=rows(AO, C), w=wl("attn.proj.w"), c=rows(X, C), M=Mg, N=C, K=C, lda=C,
                        ldc=C, bias=wl("attn.proj.b"), r=rows(X, C), ldr=C, c_f32=1, **cpx, **rmap(C))
+            if i in self.ce:  # candidate elimination after the attention residual, before the MLP
+                k = nr - d.n_t
+                keep = math.ceil(self.ce[i] * k)
+                if keep < k:
+                    nparts = d.H * (2 * d.n_t // (16 if cdt == MMT_BF16 else 8))  # mmt_ce_t2s_attention blocks
+                    plan.append((LIB.mmt_ce_t2s_attention, (P(QKV), P(ws["CEP"]), B, ntok, d.n_t, k, C, d.H, ap.scale,
+                                                            cdt), "ce_t2s", None))
+                    plan.append((LIB.mmt_ce_select, (P(ws["CEP"]), nparts, B, k, keep, d.ns,
+                                                     P(ws["CEG"][stage - 1]) if stage else None, P(ws["CEG"][stage]),
+                                                     P(ws["CEO"]), P(ws["CEM"][stage]),
+                                                     1.0 / (d.H * 2 * d.n_t)), "ce_select", None))
+                    Xn = ws["XC"] if X is ws["X"] else ws["X"]
+                    plan.append((LIB.mmt_ce_gather, (P(X), P(Xn), P(XN) if fold else None, P(ws["CEO"]), S, ntok,
+                                                     d.n_t, keep, d.ns, C, cdt), "ce_gather", None))
+                    X = Xn
+                    nr = d.n_t + keep
+                    ws["CE_FINAL"] = (ws["CEG"][stage], keep)
+                    stage += 1
+                    Mg = gm = B * nr
+                    if not two:
+                        Mg = S * nr
             if fold:
                 self._gemm(plan, "fc1", a=rows2(XN, C), w=fl("mlp.fc1.fw"), c=rows2(HID, d.hidden), M=gm, N=d.hidden,
                            K=C, lda=C, ldc=d.hidden, bias=fl("mlp.fc1.fb"), act=1, ln_colsum=fl("mlp.fc1.fcs"),
@@ -422,9 +457,11 @@ class MixFormerRGBTRuntime:
             self._gemm(plan, "fc2", a=rows(HID, d.hidden), w=wl("mlp.fc2.w"), c=rows(X, C), M=Mg, N=C, K=d.hidden,
                        lda=d.hidden, ldc=C, bias=wl("mlp.fc2.b"), r=rows(X, C), ldr=C, c_f32=1, **cpx,
                        **rmap(d.hidden))
+        return (X, stage)
 
-    def _plan_tail(self, plan, ws, score):
-        """Fusion, corner head (and score head) on the backbone output's search rows."""
+    def _plan_tail(self, plan, ws, score, xf=None):
+        """Fusion, corner head (and score head) on the backbone output's search rows.  xf = (the fp32
+        stream holding the backbone output, elimination stages run) from _plan_backbone."""
         d, W, B = self.d, self.w, ws["B"]
         C, ntok, ns, dm = d.C, d.ntok, d.ns, d.d_model
         R = 2 * B * ntok
@@ -432,7 +469,15 @@ class MixFormerRGBTRuntime:
         X, XN = ws["X"], ws["XN"]
         cdt = self.cdt
         fold = self.fold_ln
-        if fold:
+        if xf is not None and xf[1] > 0:
+            # _recover_search (asymmetric_shared_ce.py:426-447): surviving rows back to their original
+            # search positions, zeros where pruned, in the dtype the fusion reads
+            XT = XN if fold else ws["XT"]
+            gf, kf = ws["CE_FINAL"]
+            plan.append((LIB.mmt_ce_recover, (P(xf[0]), P(gf), kf, P(XT), 2 * B, ntok, d.n_t, ns, C, cdt),
+                         "ce_recover", None))
+            ws["XOUT"] = XT
+        elif fold:
             XT = XN  # the last fc2 already wrote the bf16 copy of the backbone output
         else:
             XT = ws["XT"]

@@ -176,20 +176,27 @@ def ce_attn_mean(q_v, q_i, k_v, k_i, n_t, scale):
     return a.mean(dim=2).mean(dim=1)
 
 
-def ce_select(attn_mean, x, n_t, keep_ratio, gidx):
+def ce_select(attn_mean, x, n_t, keep_ratio, gidx, forced=None):
     """get_token_from_attn (asymmetric_shared_ce.py:22-46) for one modality: sort the search tokens'
     mean attention descending, keep the first ceil(keep_ratio * lens_s) (in that order) after the
-    template tokens; gidx tracks their original search positions."""
+    template tokens; gidx tracks their original search positions.  forced (B, keep): original
+    positions to keep instead (test hook: replays another implementation's discrete choices)."""
     lens_s = x.shape[1] - n_t
     keep = math.ceil(keep_ratio * lens_s)
     if keep == lens_s:
         return x, gidx
-    order = torch.sort(attn_mean, dim=1, descending=True)[1][:, :keep]
+    if forced is None:
+        order = torch.sort(attn_mean, dim=1, descending=True)[1][:, :keep]
+    else:
+        inv = torch.full((gidx.shape[0], int(gidx.max()) + 1), -1, dtype=torch.long)
+        inv.scatter_(1, gidx.long(), torch.arange(lens_s).repeat(gidx.shape[0], 1))
+        order = inv.gather(1, torch.as_tensor(forced, dtype=torch.long)[:, :keep])
+        assert bool((order >= 0).all()), "forced selection keeps a token pruned earlier"
     xs = x[:, n_t:].gather(1, order.unsqueeze(-1).expand(-1, -1, x.shape[2]))
     return torch.cat([x[:, :n_t], xs], 1), gidx.gather(1, order)
 
 
-def backbone_asym_ce(sd, pre, t, o, s, stages=None):
+def backbone_asym_ce(sd, pre, t, o, s, stages=None, forced=None):
     """asymmetric_shared_ce.py:228-282 (CE_Block_Shared), :372-424 (VisionTransformer.forward with
     _recover_search).  The elimination runs after a CE block's attention residual, before its MLP;
     pruned search positions come back as zero tokens.  `stages` (a list) receives the kept indices."""
@@ -216,8 +223,10 @@ def backbone_asym_ce(sd, pre, t, o, s, stages=None):
             q, k, _ = _heads(qkv, B2, n, H).unbind(0)
             am = ce_attn_mean(q[:Bh], q[Bh:], k[:Bh], k[Bh:], n_t, scale)
             ls = n - n_t
-            x_v, gidx[0] = ce_select(am[:, :ls], x_v, n_t, CE_KEEP[CE_LOC.index(i)], gidx[0])
-            x_i, gidx[1] = ce_select(am[:, ls:], x_i, n_t, CE_KEEP[CE_LOC.index(i)], gidx[1])
+            st = CE_LOC.index(i)
+            fv, fi = forced[st] if forced is not None else (None, None)
+            x_v, gidx[0] = ce_select(am[:, :ls], x_v, n_t, CE_KEEP[st], gidx[0], fv)
+            x_i, gidx[1] = ce_select(am[:, ls:], x_i, n_t, CE_KEEP[st], gidx[1], fi)
             if stages is not None:
                 stages.append((am, gidx[0].clone(), gidx[1].clone()))
         res = torch.cat([x_v, x_i], 0)
@@ -417,7 +426,7 @@ def score_decoder(sd, pre, search, template, box_xyxy, num_heads=12):
 
 # ----------------------------------------------------------------------------- models
 @torch.no_grad()
-def forward(sd, variant, template, online_template, search, run_score_head=False, return_aux=False):
+def forward(sd, variant, template, online_template, search, run_score_head=False, return_aux=False, ce_forced=None):
     """Reference-equivalent forward.  template / online_template / search are [rgb, tir] lists
     of (B,3,H,W) fp32 CPU tensors.  Returns (out_dict, outputs_coord) like the reference;
     with return_aux also a dict of intermediates."""
@@ -429,7 +438,7 @@ def forward(sd, variant, template, online_template, search, run_score_head=False
         t_all = torch.cat([tv, ti], 0)
     else:
         fn = {"shared": backbone_shared, "asym_ce": backbone_asym_ce}.get(variant, backbone_asym)
-        kw = {"stages": aux.setdefault("ce_stages", [])} if variant == "asym_ce" else {}
+        kw = {"stages": aux.setdefault("ce_stages", []), "forced": ce_forced} if variant == "asym_ce" else {}
         t_all, _, s_all = fn(sd, "backbone.", torch.cat(template, 0), torch.cat(online_template, 0), torch.cat(search, 0),
                              **kw)
         Bh = s_all.shape[0] // 2

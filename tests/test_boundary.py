@@ -9,7 +9,7 @@ import torch
 from conftest import GOLDEN
 
 
-@pytest.mark.parametrize("variant", ["rgbt", "shared", "asym", "asym_online"])
+@pytest.mark.parametrize("variant", ["rgbt", "shared", "asym", "asym_online", "asym_ce"])
 def test_state_dict_keys_match_reference(variant):
     from mmt_amd.model import reference_state_dict_shapes
     ref = json.load(open(GOLDEN + "/state_dict_%s.json" % variant))
@@ -33,6 +33,19 @@ def test_lib_package_shim_exports_builders():
     from lib.models.mixformer_vit_rgbt import build_mixformer_vit_rgbt, build_mixformer_vit_rgbt_shared  # noqa: F401
     from lib.models.mixformer_vit_rgbt.asymmetric_shared import build_asymmetric_shared  # noqa: F401
     from lib.models.mixformer_vit_rgbt.asymmetric_shared_online import build_asymmetric_shared_online_score  # noqa: F401
+    from lib.models.mixformer_vit_rgbt.asymmetric_shared_ce import build_asymmetric_shared_ce
+
+
+def test_ce_builder_reads_reference_config():
+    """MODEL.BACKBONE.CE_LOC / CE_KEEP_RATIO (lib/config/asymmetric_shared_ce/config.py:23-24)."""
+    from mmt_amd.model import build_asymmetric_shared_ce, hot_path_cfg
+    cfg = hot_path_cfg()
+    m = build_asymmetric_shared_ce(cfg, train=False)
+    assert m.ce_loc == (3, 6, 9) and m.ce_keep_ratio == (0.7, 0.7, 0.7)
+    cfg.MODEL.BACKBONE.CE_LOC = [2, 5]
+    cfg.MODEL.BACKBONE.CE_KEEP_RATIO = [0.5, 0.8]
+    m = build_asymmetric_shared_ce(cfg, train=False)
+    assert m.ce_loc == (2, 5) and m.ce_keep_ratio == (0.5, 0.8)
 
 
 def test_forward_refuses_cpu_inputs():
