@@ -1,6 +1,6 @@
 """Shared body of the four RGB-T tracker entry points (drop-in for lib/test/tracker/
 mixformer_vit_rgbt.py, mixformer_vit_rgbt_shared.py, asymmetric_shared.py,
-asymmetric_shared_online.py; each defines `MixFormer` and `get_tracker_class()`).
+asymmetric_shared_online.py, asymmetric_shared_ce.py; each defines `MixFormer` and `get_tracker_class()`).
 
 Same constructor, `initialize(image, info)` and `track(image, info)` contract as the reference
 (mixformer_vit_rgbt.py:13-121): `params` carries cfg, template_factor, template_size,
@@ -25,7 +25,7 @@ def _update_intervals(cfg, dataset_name):
     return cfg.DATA.MAX_SAMPLE_INTERVAL
 
 
-def make_tracker_class(builder, multimodal, online_score=False):
+def make_tracker_class(builder, multimodal, online_score=False, kv_cache=True):
     class MixFormer(BaseTracker):
         def __init__(self, params, dataset_name):
             super().__init__(params)
@@ -40,7 +40,7 @@ def make_tracker_class(builder, multimodal, online_score=False):
             self.update_intervals = _update_intervals(self.cfg, dataset_name)
             self.core = RGBTTrackerCore(self.network, params.template_factor, params.template_size,
                                         params.search_factor, params.search_size, self.update_intervals,
-                                        multimodal=multimodal, online_score=online_score)
+                                        multimodal=multimodal, online_score=online_score, kv_cache=kv_cache)
             self.state = None
             self.frame_id = 0
 

@@ -170,9 +170,10 @@ def _seq(n, H=360, W=480):
     return frames, [200.0, 150.0, 48.0, 48.0]
 
 
-@pytest.mark.parametrize("kv_cache", [True, False])
-@pytest.mark.parametrize("variant,module,multimodal", [("rgbt", "mixformer_vit_rgbt", False),
-                                                        ("asym", "asymmetric_shared", True)])
+@pytest.mark.parametrize("variant,module,multimodal,kv_cache", [
+    ("rgbt", "mixformer_vit_rgbt", False, True), ("rgbt", "mixformer_vit_rgbt", False, False),
+    ("asym", "asymmetric_shared", True, True), ("asym", "asymmetric_shared", True, False),
+    ("asym_ce", "asymmetric_shared_ce", True, False)])
 def test_tracking_loop_matches_oracle(variant, module, multimodal, kv_cache):
     """Each frame: the HIP tracker's new box vs the oracle's tracking step started from the HIP
     tracker's previous box (teacher forcing, so bf16/fp32 rounding cannot compound).  kv_cache:
