@@ -283,6 +283,44 @@ void launch_tiles(const mmt_gemm_params& p, hipStream_t st) {
     }
 }
 
+// GEMV path for a handful of rows (the score head's single-token Linears, M = batch; its 16 ROI tokens): one wave per
+// output column n, lanes stride K with 16-B loads of the W row and the M activation rows, wave-sum,
+// + bias, activation.  The tiled kernels would stream W through one K loop per 64-column tile (a few
+// workgroups for the whole launch).  Plain fp32 GEMMs only: no residual / row maps / conv / split.
+constexpr int GEMV_MAXM = 16;
+__global__ __launch_bounds__(256) void gemv_f32_kernel(const float* __restrict__ a, const float* __restrict__ w,
+                                                       const float* __restrict__ bias, float* __restrict__ c, int M,
+                                                       int N, int K, int64_t lda, int64_t ldc, int act) {
+    const int n = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (n >= N) return;  // wave-uniform
+    const float* wr = w + (int64_t)n * K;
+    float acc[GEMV_MAXM];
+#pragma unroll
+    for (int m = 0; m < GEMV_MAXM; ++m) acc[m] = 0.f;
+    for (int k = lane * 4; k < K; k += 256) {
+        const float4 wv = *(const float4*)(wr + k);
+#pragma unroll
+        for (int m = 0; m < GEMV_MAXM; ++m) {
+            if (m < M) {
+                const float4 av = *(const float4*)(a + m * lda + k);
+                acc[m] = fmaf(wv.x, av.x, fmaf(wv.y, av.y, fmaf(wv.z, av.z, fmaf(wv.w, av.w, acc[m]))));
+            }
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < GEMV_MAXM; ++m) {
+        if (m < M) {
+            float v = wave_sum(acc[m]);
+            if (lane == 0) {
+                if (bias) v += bias[n];
+                if (act == 1) v = gelu_erf(v);
+                else if (act == 2) v = fmaxf(v, 0.f);
+                c[m * ldc + n] = v;
+            }
+        }
+    }
+}
+
 template <typename T>
 int launch_gemm(const mmt_gemm_params& p, hipStream_t st) {
     const int EPC = 16 / (int)sizeof(T);
@@ -305,6 +343,14 @@ int launch_gemm(const mmt_gemm_params& p, hipStream_t st) {
         if (((uintptr_t)p.a[g] | (uintptr_t)p.w[g]) & 15) return MMT_EBADARG;
         if (p.k_split > 0 && p.conv_h == 0 && (!p.a1[g] || ((uintptr_t)p.a1[g] & 15))) return MMT_EBADARG;
         if (p.c2[g] && !p.r[g]) return MMT_EBADARG;
+    }
+    if (sizeof(T) == 4 && p.M <= GEMV_MAXM && p.groups == 1 && p.conv_h == 0 && !p.r[0] && !p.c2[0] && p.c_f32 &&
+        p.k_split == 0 && !p.ln_fold && p.splitk == 0 && p.c_seg_rows == 0 && p.a_seg_rows >= p.M && p.K % 4 == 0 &&
+        p.lda % 4 == 0 && p.impl <= 0) {
+        hipLaunchKernelGGL(gemv_f32_kernel, dim3((unsigned)((p.N + 3) / 4)), dim3(256), 0, st, (const float*)p.a[0],
+                           (const float*)p.w[0], (const float*)p.bias[0], (float*)p.c[0], p.M, p.N, p.K, p.lda, p.ldc,
+                           p.act);
+        return launch_status();
     }
     if (sizeof(T) == 2 && mmt_gemm_glds_bf16(p, st, p.impl) == 0) return launch_status();
     if (p.ln_fold || p.c2_copy) return MMT_EBADARG;  // LDS-DMA kernel features only

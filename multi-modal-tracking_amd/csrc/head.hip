@@ -364,28 +364,56 @@ __global__ __launch_bounds__(256) void prroi_coor_bwd_kernel(const float* __rest
     }
 }
 
-// one wave per (batch, head); lane = channel within the head (64)
-__global__ __launch_bounds__(64) void spm_attention_kernel(const float* __restrict__ q, int64_t q_stride,
-                                                           const float* __restrict__ kv, float* __restrict__ out, int Lk,
-                                                           int C, float scale) {
-    extern __shared__ float sc[];  // Lk
-    const int h = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
-    const float qd = q[b * q_stride + h * 64 + d];
-    const float* kb = kv + (int64_t)b * Lk * 2 * C + h * 64 + d;
-    float mx = -INFINITY;
-    for (int t = 0; t < Lk; ++t) {
-        const float s = wave_sum(qd * kb[(int64_t)t * 2 * C]) * scale;
-        if (d == 0) sc[t] = s;
-        mx = fmaxf(mx, s);
-    }
+// ScoreDecoder single-query attention (score_decoder.py:55-61): one 256-thread workgroup per (batch,
+// head).  Scores: thread t takes keys t, t+256, .. (64-wide dot with the query in LDS, the key row by
+// 16-B loads); softmax statistics by block reduction; output: lane = channel, the 4 waves take
+// interleaved keys, partial sums combined through LDS.
+constexpr int SPM_MAXK = 2048;  // keys (16 ROI tokens; 2 x 64 / 2 x 144 template tokens)
+__global__ __launch_bounds__(256) void spm_attention_kernel(const float* __restrict__ q, int64_t q_stride,
+                                                            const float* __restrict__ kv, float* __restrict__ out,
+                                                            int Lk, int C, float scale) {
+    __shared__ float sc[SPM_MAXK];  // Lk scores
+    __shared__ __attribute__((aligned(16))) float qs[64];
+    __shared__ float red[4];
+    __shared__ float part[4][64];
+    const int h = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid < 64) qs[tid] = q[b * q_stride + h * 64 + tid];
     __syncthreads();
-    float se = 0.f, acc = 0.f;
-    for (int t = 0; t < Lk; ++t) {
-        const float e = expf(sc[t] - mx);
-        se += e;
-        acc += e * kb[(int64_t)t * 2 * C + C];
+    const float* kb = kv + (int64_t)b * Lk * 2 * C + h * 64;
+    float mx = -INFINITY;
+    for (int t = tid; t < Lk; t += 256) {
+        const float* kr = kb + (int64_t)t * 2 * C;
+        float acc = 0.f;
+#pragma unroll
+        for (int d = 0; d < 64; d += 4) {
+            const float4 kv4 = *(const float4*)(kr + d);
+            const float4 q4 = *(const float4*)(qs + d);
+            acc = fmaf(q4.x, kv4.x, fmaf(q4.y, kv4.y, fmaf(q4.z, kv4.z, fmaf(q4.w, kv4.w, acc))));
+        }
+        acc *= scale;
+        sc[t] = acc;
+        mx = fmaxf(mx, acc);
     }
-    out[(int64_t)b * C + h * 64 + d] = acc / se;
+    mx = wave_max(mx);
+    if (lane == 0) red[w] = mx;
+    __syncthreads();
+    mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    __syncthreads();
+    float se = 0.f;
+    for (int t = tid; t < Lk; t += 256) {
+        const float e = expf(sc[t] - mx);
+        sc[t] = e;
+        se += e;
+    }
+    se = wave_sum(se);
+    if (lane == 0) red[w] = se;
+    __syncthreads();
+    const float inv = 1.f / (red[0] + red[1] + red[2] + red[3]);
+    float acc = 0.f;
+    for (int t = w; t < Lk; t += 4) acc = fmaf(sc[t], kb[(int64_t)t * 2 * C + C + lane], acc);
+    part[w][lane] = acc;
+    __syncthreads();
+    if (w == 0) out[(int64_t)b * C + h * 64 + lane] = (part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane]) * inv;
 }
 
 }  // namespace
@@ -472,8 +500,9 @@ extern "C" int mmt_prroi_pool_coor_backward(const float* features, const float* 
 
 extern "C" int mmt_spm_attention(const float* q, int64_t q_stride, const float* kv, float* out, int B, int Lk, int C,
                                  int H, float scale, void* stream) {
-    if (!q || !kv || !out || B <= 0 || Lk <= 0 || Lk > 8192 || C != H * 64) return MMT_EBADARG;
-    hipLaunchKernelGGL(spm_attention_kernel, dim3(H, B), dim3(64), Lk * sizeof(float), (hipStream_t)stream, q, q_stride,
+    if (!q || !kv || !out || B <= 0 || Lk <= 0 || Lk > SPM_MAXK || C != H * 64) return MMT_EBADARG;
+    if (((uintptr_t)kv & 15) || (C & 3) || ((uintptr_t)q & 3)) return MMT_EBADARG;
+    hipLaunchKernelGGL(spm_attention_kernel, dim3(H, B), dim3(256), 0, (hipStream_t)stream, q, q_stride,
                        kv, out, Lk, C, scale);
     return launch_status();
 }

@@ -459,7 +459,7 @@ class MixFormerRGBTRuntime:
                        **rmap(d.hidden))
         return (X, stage)
 
-    def _plan_tail(self, plan, ws, score, xf=None):
+    def _plan_tail(self, plan, ws, score, xf=None, spm_kv1=True):
         """Fusion, corner head (and score head) on the backbone output's search rows.  xf = (the fp32
         stream holding the backbone output, elimination stages run) from _plan_backbone."""
         d, W, B = self.d, self.w, ws["B"]
@@ -557,11 +557,20 @@ class MixFormerRGBTRuntime:
                                                  P(ws["MAPS"]), P(ws["BOX"]), P(ws["XYXY"]), P(ws["ROIS"]) if score else None,
                                                  float(gs), B, d.fh, h8, 4, cdt), "corner_softargmax", None))
         if score:
-            self._plan_spm(plan, ws)
+            self._plan_spm(plan, ws, spm_kv1)
         return plan
 
-    def _plan_spm(self, plan, ws):
-        """ScoreDecoder (score_decoder.py:32-66), fp32."""
+    def _plan_spm_kv1(self, plan, ws):
+        """K/V of the score decoder's second memory: the first template's tokens of both modalities
+        (the template pass computes it once per template update when the K/V cache is used)."""
+        d, W, B, P, C = self.d, self.w, ws["B"], _ptr, self.d.C
+        self._gemm(plan, "spm_kv1", a=[P(ws["X"])], w=[P(W["spm.kv1.w"])], c=[P(ws["KV1"])], M=B * 2 * d.nt1, N=2 * C,
+                   K=C, lda=C, ldc=2 * C, bias=[P(W["spm.kv1.b"])], seg=(d.nt1, 2, B * d.ntok * C, d.ntok * C),
+                   c_f32=1, dtype=MMT_F32)
+
+    def _plan_spm(self, plan, ws, kv1=True):
+        """ScoreDecoder (score_decoder.py:32-66), fp32.  kv1=False: the template memory's K/V are
+        already in KV1 (template pass)."""
         d, W, B = self.d, self.w, ws["B"]
         P, C, ns, gs = _ptr, d.C, d.ns, d.gs
         F32 = MMT_F32
@@ -581,9 +590,8 @@ class MixFormerRGBTRuntime:
         self._gemm(plan, "spm_q1", a=[P(ws["XS"])], w=[P(W["spm.q1.w"])], c=[P(ws["Q1"])], M=B, N=C, K=C, lda=C, ldc=C,
                    bias=[P(W["spm.q1.b"])], c_f32=1, dtype=F32)
         # template tokens of both modalities from the fp32 residual stream: [b][m][t]
-        self._gemm(plan, "spm_kv1", a=[P(ws["X"])], w=[P(W["spm.kv1.w"])], c=[P(ws["KV1"])], M=B * 2 * d.nt1, N=2 * C,
-                   K=C, lda=C, ldc=2 * C, bias=[P(W["spm.kv1.b"])], seg=(d.nt1, 2, B * d.ntok * C, d.ntok * C),
-                   c_f32=1, dtype=F32)
+        if kv1:
+            self._plan_spm_kv1(plan, ws)
         plan.append((LIB.mmt_spm_attention, (P(ws["Q1"]), C, P(ws["KV1"]), P(ws["AT"]), B, 2 * d.nt1, C, d.H, scale),
                      "spm_attn1", None))
         self._gemm(plan, "spm_proj1", a=[P(ws["AT"])], w=[P(W["spm.proj1.w"])], c=[P(ws["XS"])], M=B, N=C, K=C, lda=C,
@@ -647,10 +655,12 @@ class MixFormerRGBTRuntime:
                           for _ in range(d.depth)]
             ws["plan_t"] = []
             self._plan_backbone(ws["plan_t"], ws, "t", ws["QKVL"])
+            if self.variant == "asym_online":  # the score head's template K/V: once per template update
+                self._plan_spm_kv1(ws["plan_t"], ws)
             for score in ((False, True) if self.variant == "asym_online" else (False,)):
                 plan = []
                 self._plan_backbone(plan, ws, "s", ws["QKVL"])
-                self._plan_tail(plan, ws, score)
+                self._plan_tail(plan, ws, score, spm_kv1=False)
                 ws["plan_s_score" if score else "plan_s"] = plan
         return ws
 

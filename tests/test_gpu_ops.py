@@ -538,3 +538,41 @@ def test_prroi_fractional_vs_oracle():
     torch.cuda.synchronize()
     ref = torch.from_numpy(prroi_pool2d(feat.numpy(), rois.numpy(), 4, 4, 1.0))
     assert (out.cpu() - ref).abs().max().item() < 1e-5
+
+
+@pytest.mark.parametrize("M,N,K,act", [(1, 768, 768, 0), (3, 1024, 1024, 2), (8, 1, 768, 0), (2, 100, 64, 1),
+                                       (16, 1536, 768, 0)])
+def test_gemv_small_m_fp32(M, N, K, act):
+    """fp32 GEMMs with M <= 8 (the score head's single-token Linears) take the GEMV path: vs torch fp64."""
+    g = torch.Generator().manual_seed(M * 7 + N)
+    a, w, b = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g) * 0.05, torch.randn(N, generator=g)
+    ad, wd, bd = a.cuda(), w.cuda(), b.cuda()
+    c = torch.empty(M, N, device="cuda")
+    _gemm([ad.data_ptr()], [wd.data_ptr()], [c.data_ptr()], M, N, K, K, N, torch.float32, bias=[bd.data_ptr()], act=act,
+          c_f32=1)
+    torch.cuda.synchronize()
+    ref = a.double() @ w.double().T + b.double()
+    ref = F.gelu(ref) if act == 1 else (F.relu(ref) if act == 2 else ref)
+    assert (c.cpu().double() - ref).abs().max().item() <= 1e-4 * max(1.0, ref.abs().max().item())
+
+
+@pytest.mark.parametrize("B,Lk,H", [(1, 16, 12), (2, 128, 12), (1, 288, 16), (3, 300, 2)])
+def test_spm_attention(B, Lk, H):
+    """ScoreDecoder single-query multi-head attention (score_decoder.py:55-61) vs torch fp64."""
+    L = _lib()
+    C = 64 * H
+    g = torch.Generator().manual_seed(Lk + H)
+    q, kv = torch.randn(B, C, generator=g), torch.randn(B, Lk, 2 * C, generator=g)
+    out = torch.empty(B, C, device="cuda")
+    scale = C ** -0.5
+    qd, kvd = q.cuda(), kv.cuda()  # keep the device copies alive across the launch
+    L.check(L.LIB.mmt_spm_attention(qd.data_ptr(), C, kvd.data_ptr(), out.data_ptr(), B, Lk, C, H, scale,
+                                    torch.cuda.current_stream().cuda_stream), "spm_attention")
+    torch.cuda.synchronize()
+    qh = q.double().view(B, H, 1, 64)
+    k = kv[:, :, :C].double().view(B, Lk, H, 64).transpose(1, 2)
+    v = kv[:, :, C:].double().view(B, Lk, H, 64).transpose(1, 2)
+    ref = (torch.softmax(qh @ k.transpose(-1, -2) * scale, -1) @ v).view(B, C)
+    err = (out.cpu().double() - ref).abs().view(B, H, 64).amax(-1)
+    print("spm per (b, h) err", err)
+    assert err.max().item() <= 1e-5
