@@ -143,8 +143,17 @@ __global__ __launch_bounds__(256) void ce_t2s_kernel(const T* __restrict__ qkv, 
 // queries] blocks = K Q^T with v_mfma_f32_16x16x32_bf16 (A = key rows, B = query rows, 16-B
 // fragments read straight from the qkv rows, all of a wave's key blocks loaded up front); lane l
 // holds query l%16 against keys 4*(l/16)..+3 of each block.  Row max / sum: over the lane's values,
-// the 4 lanes of the query (xor 16, 32) and the 4 waves (LDS); column sums over the 16 queries:
-// xor-butterflies inside each 16-lane group.  No score matrix in LDS.
+// the 4 lanes of the query (permlane swaps) and the 4 waves (LDS); column sums over the 16 queries:
+// DPP row scans inside each 16-lane group.  No score matrix in LDS.
+// inclusive sum over the 16 lanes of a DPP row (row_shr 1, 2, 4, 8; lanes shifted in from outside the
+// row add 0): lane 15 of each row holds the row's total
+MMT_DEV float ce_row16_sum(float v) {
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xf, 0xf, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x112, 0xf, 0xf, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x114, 0xf, 0xf, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x118, 0xf, 0xf, false));
+    return v;
+}
 constexpr int CE_QBM = 16, CE_MAXI = 18;  // key blocks per wave: 2k <= 4 * 18 * 16 = 1152 (ViT-L 384 px)
 __global__ __launch_bounds__(256) void ce_t2s_mfma_kernel(const bf16_t* __restrict__ qkv, float* __restrict__ part,
                                                           int Bm, int pitch, int n_t, int k, int C, float scale) {
@@ -188,8 +197,7 @@ __global__ __launch_bounds__(256) void ce_t2s_mfma_kernel(const bf16_t* __restri
             sc[i] = acc;
         }
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = lanegroup_max(mx);  // the 4 lanes of the query (l, l^16, l^32, l^48)
     if (lg == 0) red[0][w][l16] = mx;
     __syncthreads();
     mx = fmaxf(fmaxf(red[0][0][l16], red[0][1][l16]), fmaxf(red[0][2][l16], red[0][3][l16]));
@@ -204,8 +212,7 @@ __global__ __launch_bounds__(256) void ce_t2s_mfma_kernel(const bf16_t* __restri
             }
         }
     }
-    se += __shfl_xor(se, 16, 64);
-    se += __shfl_xor(se, 32, 64);
+    se = lanegroup_sum(se);
     if (lg == 0) red[1][w][l16] = se;
     __syncthreads();
     const float inv = 1.f / ((red[1][0][l16] + red[1][1][l16]) + (red[1][2][l16] + red[1][3][l16]));
@@ -216,14 +223,12 @@ __global__ __launch_bounds__(256) void ce_t2s_mfma_kernel(const bf16_t* __restri
         if (kb < nkb) {
             float v[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                float t = sc[i][r] * inv;
+            for (int r = 0; r < 4; ++r) v[r] = ce_row16_sum(sc[i][r] * inv);  // sum over the 16 queries
+            if (l16 == 15) {
 #pragma unroll
-                for (int o = 1; o < 16; o <<= 1) t += __shfl_xor(t, o, 64);  // sum over the 16 queries
-                v[r] = t;
+                for (int r = 0; r < 4; ++r)
+                    if (kb * 16 + 4 * lg + r < nk) dst[kb * 16 + 4 * lg + r] = v[r];
             }
-            const int key = kb * 16 + 4 * lg + (l16 & 3);
-            if (l16 < 4 && key < nk) dst[key] = v[l16 & 3];
         }
     }
 }
