@@ -214,6 +214,34 @@ def cpu_baseline(variant, B, budget_s=12.0, geo=None):
                       % (n, B, variant, geo["template"], geo["search"], dt)}
 
 
+def timed_steps(step, steps, world, sync, device):
+    """The contract's timed region: barrier + sync, exactly `steps` steps, barrier + sync, and the MAX of
+    the ranks' elapsed times (the slowest replica sets the job's rate)."""
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = tt.item()
+    return elapsed
+
+
+def frame_seeds(rank, n=4):
+    """Seeds of the resident input sets of one rank: disjoint across ranks (each replica tracks its own
+    frames, SURVEY §8(e): single-stream tracking shards by sequence, no data-path collective)."""
+    return [1 + n * rank + i for i in range(n)]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -253,8 +281,8 @@ def main():
     B = args.batch
     score = args.variant == "asym_online"
     pool = []
-    for i in range(4):  # distinct frames per rank, resident in HBM before timing
-        t, o, s = synthetic.synth_inputs(B, geo["template"], geo["search"], seed=1 + 4 * rank + i)
+    for seed in frame_seeds(rank):  # distinct frames per rank, resident in HBM before timing
+        t, o, s = synthetic.synth_inputs(B, geo["template"], geo["search"], seed=seed)
         pool.append(([x.cuda() for x in t], [x.cuda() for x in o], [x.cuda() for x in s]))
     use_graph = not args.no_graph
     # one hipGraph per resident input set: the patch staging reads that set in place (zero-copy)
@@ -269,22 +297,7 @@ def main():
 
     for i in range(args.warmup):
         step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = tt.item()
+    elapsed = timed_steps(step, args.steps, world, torch.cuda.synchronize, "cuda")
 
     ws = rt.workspace(B)
     plan = ws["plan_score"] if score else ws["plan"]
