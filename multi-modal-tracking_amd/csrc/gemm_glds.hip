@@ -142,6 +142,8 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
 #pragma unroll
     for (int i = 0; i < PB; ++i) boff[i] = (int64_t)min(n0 + (wid * PB + i) * 8 + prow, N - 1) * K;
     const int ks = p.k_split, cin = p.conv_cin, k3 = p.conv_k3;
+    const float inv_cin = CONV && k3 ? 1.f / (float)cin : 0.f;
+    const int cup_sh = CONV ? 31 - __builtin_clz(cup) : 0;
 
     unsigned char* ring = lds + kg * ST * STAGE;
     // this slice's K-steps [kb0, kb0 + nk) of the nk_all 64-deep steps (the launcher keeps nk >= KS)
@@ -159,18 +161,25 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
             for (int i = 0; i < PA; ++i)
                 glds16(kin ? (const void*)(ab + aoff[i]) : (const void*)g_zero_chunk, base + (wid * PA + i) * 1024);
         } else {
+            // Per-step address math stays off the integer-division path (a runtime-divisor division
+            // is ~35 VALU; at 9 per step it held the DMA issue back by ~0.3 us per K-step): the tap
+            // comes from a float reciprocal (exact: k < 2^24 and (k + 0.5) / cin sits >= 0.5 / cin
+            // from an integer), the upsample factor is a power of two (shift), and the element
+            // offset fits 32 bits (both checked by the launcher).
             int dy = 0, dx = 0, ci = k;
             if (k3) {  // k = (ky*3 + kx)*cin + ci
-                const int tap = k / cin;
-                ci = k - tap * cin;
-                dy = tap / 3 - 1;
-                dx = tap - (tap / 3) * 3 - 1;
+                const uint32_t tap = (uint32_t)(((float)k + 0.5f) * inv_cin);
+                ci = k - (int)tap * cin;
+                const int ty = (int)(tap / 3u);
+                dy = ty - 1;
+                dx = (int)tap - ty * 3 - 1;
             }
 #pragma unroll
             for (int i = 0; i < PA; ++i) {
                 const int iy = ay[i] + dy, ix = ax[i] + dx;
                 const bool ok = kin && iy >= 0 && ix >= 0 && iy < ch && ix < ch;
-                const bf16_t* src = A0 + (aoff[i] + (int64_t)(iy / cup) * hi + ix / cup) * p.lda + ci;
+                const uint32_t pix = (uint32_t)aoff[i] + (uint32_t)((iy >> cup_sh) * hi + (ix >> cup_sh));
+                const bf16_t* src = A0 + (pix * (uint32_t)p.lda + (uint32_t)ci);
                 glds16(ok ? (const void*)src : (const void*)g_zero_chunk, base + (wid * PA + i) * 1024);
             }
         }
@@ -515,6 +524,12 @@ int mmt_gemm_glds_bf16(const mmt_gemm_params& p, hipStream_t st, int force) {
     if (force < 0) return 1;
     if (p.K % 8 || p.N % 8 || p.ldc % 8 || (p.r[0] && p.ldr % 8)) return 1;
     if (p.ln_fold && p.conv_h > 0) return 1;
+    if (p.conv_h > 0) {  // the kernel's conv addressing: power-of-two upsample, 32-bit element offsets
+        const int cup = p.conv_up, hi = p.conv_up > 0 ? p.conv_h / p.conv_up : 0;
+        if (cup <= 0 || (cup & (cup - 1)) || hi * cup != p.conv_h) return 1;
+        const int64_t imgs = (p.M + (int64_t)p.conv_h * p.conv_h - 1) / ((int64_t)p.conv_h * p.conv_h);
+        if ((imgs * hi * hi * (int64_t)p.lda + p.K) >= ((int64_t)1 << 32) || p.K >= (1 << 24)) return 1;
+    }
     if (p.lda % 8 || p.a_stride_a % 8 || p.a_stride_b % 8 || p.k_split % 8) return 1;
     if (p.a_seg_rows > INT32_MAX || p.a_segs_a > INT32_MAX) return 1;
     for (int g = 0; g < p.groups; ++g) {

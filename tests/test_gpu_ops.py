@@ -262,7 +262,7 @@ def test_gemm_layernorm_fold(impl, M, N, K):
 
 
 @pytest.mark.parametrize("dname,impl", [("f32", 0), ("bf16", -1), ("bf16", 1), ("bf16", 2), ("bf16", 3)])
-@pytest.mark.parametrize("h,up,cin,cout", [(20, 1, 64, 96), (40, 2, 32, 48), (10, 1, 16, 200), (20, 1, 96, 48)])
+@pytest.mark.parametrize("h,up,cin,cout", [(20, 1, 64, 96), (40, 2, 32, 48), (10, 1, 16, 200), (20, 1, 96, 48), (80, 4, 48, 32)])
 def test_conv3x3_implicit_gemm(dname, impl, h, up, cin, cout):
     """3x3/pad-1 conv as implicit GEMM on every kernel (impl); K = 9*cin is not a multiple of the
     64-deep K-step for cin = 16 / 32 / 96 (zero-filled K tail)."""
