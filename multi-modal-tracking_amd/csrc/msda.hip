@@ -79,16 +79,22 @@ __global__ __launch_bounds__(256) void msda_generic_kernel(const T* __restrict__
     }
 }
 
-// 8 heads x 2 levels x 4 points, 64 channels per head.
+// 8 heads x 2 levels x 4 points, 64 channels per head.  Each lane owns 16 bytes of channels (8 bf16 /
+// 4 fp32) of one head, so one wave (bf16) or two (fp32) cover a query (one query per workgroup) and
+// every corner gather is a 16-byte load.  A level's 16 corner loads are issued before any is used:
+// out-of-map corners and samples read a clamped in-map pixel with weight 0, which leaves each
+// channel's sum exactly as the reference's skip / zero-corner form (cuh:33-84) computes it.
 template <typename T>
-__global__ __launch_bounds__(512) void msda_bimodal_kernel(const float* __restrict__ offw, const T* __restrict__ value,
-                                                           T* __restrict__ out, int B, int hw) {
+__global__ __launch_bounds__(64 * (int)sizeof(T) / 2) void msda_bimodal_kernel(const float* __restrict__ offw,
+                                                                              const T* __restrict__ value,
+                                                                              T* __restrict__ out, int B, int hw) {
     constexpr int NH = 8, NL = 2, NP = 4, DH = 64, CM = NH * DH;
-    const int row = blockIdx.x;  // b * nq + q
+    constexpr int EPL = 16 / (int)sizeof(T), LPH = DH / EPL;  // one query per workgroup: 8 * LPH threads
     const int nq = hw * hw;
-    const int b = row / nq, q = row % nq;
-    const int m = threadIdx.x >> 6, c = threadIdx.x & 63;
-    const float* ow = offw + (int64_t)row * (NH * NL * NP * 3);
+    const int64_t row = blockIdx.x;  // b * nq + q
+    const int t = threadIdx.x, m = t / LPH, c0 = (t % LPH) * EPL;
+    const int b = (int)(row / nq), q = (int)(row % nq);
+    const float* ow = offw + row * (NH * NL * NP * 3);
     // softmax over the 8 logits of this head (fp32, max-subtracted)
     float lg[NL * NP];
     float mx = -INFINITY;
@@ -106,21 +112,63 @@ __global__ __launch_bounds__(512) void msda_bimodal_kernel(const float* __restri
     const float inv = 1.f / sum;
     const float rx = ((float)(q % hw) + 0.5f) / (float)hw;
     const float ry = ((float)(q / hw) + 0.5f) / (float)hw;
-    float col = 0.f;
+    float col[EPL];
 #pragma unroll
-    for (int l = 0; l < NL; ++l) {
-        const T* vb = value + ((int64_t)(l * B + b) * nq) * CM + m * DH + c;
+    for (int j = 0; j < EPL; ++j) col[j] = 0.f;
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {  // per level: 16 corner loads in flight, then their math
+        uint4 raw[NP][4];
+        float wt[NP][4], at[NP];
+        const T* vb = value + ((int64_t)(l * B + b) * nq) * CM + m * DH + c0;
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
             const int oi = ((m * NL + l) * NP + p) * 2;
             const float lx = rx + ow[oi] / (float)hw;
             const float ly = ry + ow[oi + 1] / (float)hw;
             const float h_im = ly * (float)hw - 0.5f, w_im = lx * (float)hw - 0.5f;
-            if (h_im > -1.f && w_im > -1.f && h_im < (float)hw && w_im < (float)hw)
-                col += bilinear<T, float>(vb, hw, hw, CM, h_im, w_im) * (lg[l * NP + p] * inv);
+            const bool in = h_im > -1.f && w_im > -1.f && h_im < (float)hw && w_im < (float)hw;
+            const float hf = floorf(h_im), wf = floorf(w_im);
+            const int hl = (int)hf, wl = (int)wf, hh_ = hl + 1, wh_ = wl + 1;
+            const float lh = h_im - hf, lw = w_im - wf, hh = 1.f - lh, hwt = 1.f - lw;
+            const bool y0 = hl >= 0, y1 = hh_ <= hw - 1, x0 = wl >= 0, x1 = wh_ <= hw - 1;
+            wt[p][0] = in && y0 && x0 ? hh * hwt : 0.f;
+            wt[p][1] = in && y0 && x1 ? hh * lw : 0.f;
+            wt[p][2] = in && y1 && x0 ? lh * hwt : 0.f;
+            wt[p][3] = in && y1 && x1 ? lh * lw : 0.f;
+            at[p] = in ? lg[l * NP + p] * inv : 0.f;
+            const int ya = min(max(hl, 0), hw - 1), yb = min(max(hh_, 0), hw - 1);
+            const int xa = min(max(wl, 0), hw - 1), xb = min(max(wh_, 0), hw - 1);
+            raw[p][0] = *(const uint4*)(vb + (ya * hw + xa) * CM);
+            raw[p][1] = *(const uint4*)(vb + (ya * hw + xb) * CM);
+            raw[p][2] = *(const uint4*)(vb + (yb * hw + xa) * CM);
+            raw[p][3] = *(const uint4*)(vb + (yb * hw + xb) * CM);
+        }
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+            float v[4][EPL];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t w4[4] = {raw[p][k].x, raw[p][k].y, raw[p][k].z, raw[p][k].w};
+#pragma unroll
+                for (int j = 0; j < EPL; ++j) {
+                    if constexpr (sizeof(T) == 2)
+                        v[k][j] = (j & 1) ? __uint_as_float(w4[j >> 1] & 0xffff0000u) : __uint_as_float(w4[j >> 1] << 16);
+                    else
+                        v[k][j] = __uint_as_float(w4[j]);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < EPL; ++j)
+                col[j] += (wt[p][0] * v[0][j] + wt[p][1] * v[1][j] + wt[p][2] * v[2][j] + wt[p][3] * v[3][j]) * at[p];
         }
     }
-    out[(int64_t)row * CM + m * DH + c] = from_f<T>(col);
+    T* o = out + row * CM + m * DH + c0;
+    if constexpr (sizeof(T) == 2) {
+        *(uint4*)o = uint4{pack_bf16x2(col[0], col[1]), pack_bf16x2(col[2], col[3]), pack_bf16x2(col[4], col[5]),
+                           pack_bf16x2(col[6], col[7])};
+    } else {
+        *(f32x4*)o = f32x4{col[0], col[1], col[2], col[3]};
+    }
 }
 
 template <typename A> MMT_DEV A wave_sum_t(A v) {
@@ -236,14 +284,15 @@ extern "C" int mmt_ms_deform_attn_forward(const void* value, const int64_t* spat
 extern "C" int mmt_msda_bimodal(const float* offw, const void* value, void* out, int B, int hw, int dtype,
                                 void* stream) {
     if (!offw || !value || !out || B <= 0 || hw <= 0) return MMT_EBADARG;
-    dim3 grid((unsigned)(B * hw * hw));
+    if (((uintptr_t)value | (uintptr_t)out) & 15) return MMT_EBADARG;  // 16-byte channel vectors
+    const int64_t rows = (int64_t)B * hw * hw;
     hipStream_t st = (hipStream_t)stream;
-    if (dtype == MMT_BF16)
-        hipLaunchKernelGGL((msda_bimodal_kernel<bf16_t>), grid, dim3(512), 0, st, offw, (const bf16_t*)value,
-                           (bf16_t*)out, B, hw);
+    if (dtype == MMT_BF16)  // one query per workgroup: one wave (bf16) / two (fp32)
+        hipLaunchKernelGGL((msda_bimodal_kernel<bf16_t>), dim3((unsigned)rows), dim3(64), 0, st, offw,
+                           (const bf16_t*)value, (bf16_t*)out, B, hw);
     else if (dtype == MMT_F32)
-        hipLaunchKernelGGL((msda_bimodal_kernel<float>), grid, dim3(512), 0, st, offw, (const float*)value,
-                           (float*)out, B, hw);
+        hipLaunchKernelGGL((msda_bimodal_kernel<float>), dim3((unsigned)rows), dim3(128), 0, st, offw,
+                           (const float*)value, (float*)out, B, hw);
     else return MMT_EBADARG;
     return launch_status();
 }
