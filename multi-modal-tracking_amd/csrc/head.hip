@@ -28,12 +28,19 @@ __global__ __launch_bounds__(256) void conv3x3_c1_kernel(const T* __restrict__ i
         const int b = idx / (h * h), rem = idx % (h * h), y = rem / h, x = rem % h;
         const T* ib = in + (int64_t)g * npx * in_stride + (int64_t)b * h * h * in_stride;
         const T* wg = w + (int64_t)g * 9 * cin;
+        // (tap, chunk) advance incrementally (no per-iteration division) and the body is branch-free
+        // (clamped pixel, zeroed value) so the unrolled iterations' loads issue together
+        int tap = sl / nch, cc = sl - tap * nch;
+#pragma unroll 4
         for (int u = sl; u < 9 * nch; u += 8) {
-            const int tap = u / nch, cc = u - tap * nch;
-            const int iy = y + tap / 3 - 1, ix = x + tap % 3 - 1;
-            if (iy < 0 || iy >= h || ix < 0 || ix >= h) continue;
-            const uint4 xv = *(const uint4*)(ib + ((int64_t)iy * h + ix) * in_stride + cc * EPC);
+            const int ty = (tap * 11) >> 5;  // tap / 3 for tap < 9
+            const int iy = y + ty - 1, ix = x + (tap - 3 * ty) - 1;
+            const bool ok = iy >= 0 && iy < h && ix >= 0 && ix < h;
+            const int cy = min(max(iy, 0), h - 1), cx = min(max(ix, 0), h - 1);
+            uint4 xv = *(const uint4*)(ib + ((int64_t)cy * h + cx) * in_stride + cc * EPC);
             const uint4 wv = *(const uint4*)(wg + tap * cin + cc * EPC);
+            if (!ok) xv = uint4{0u, 0u, 0u, 0u};
+            for (cc += 8; cc >= nch; cc -= nch) ++tap;
             if constexpr (sizeof(T) == 2) {
                 const uint32_t xa[4] = {xv.x, xv.y, xv.z, xv.w}, wa[4] = {wv.x, wv.y, wv.z, wv.w};
 #pragma unroll

@@ -81,13 +81,23 @@ __global__ __launch_bounds__(GN_THREADS) void groupnorm_kernel(const float* __re
     const int inst = blockIdx.y, grp = blockIdx.x;
     const int cg = Ctot / groups, q = cg / 4, items = P * q;
     const int64_t base = (int64_t)inst * P * Ctot + grp * cg;
+    // item -> (pixel, 4-channel chunk) without a runtime-divisor division per item: the float
+    // quotient is exact (items < 2^24; (it + 0.5) / q sits >= 0.5 / q from an integer)
+    const float inv_q = 1.f / (float)q;
+    int pix[GN_VMAX], c4s[GN_VMAX];
+#pragma unroll
+    for (int i = 0; i < GN_VMAX; ++i) {
+        const int it = threadIdx.x + GN_THREADS * i;
+        pix[i] = (int)(((float)it + 0.5f) * inv_q);
+        c4s[i] = 4 * (it - pix[i] * q);
+    }
     float4 v[GN_VMAX];
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < GN_VMAX; ++i) {
         const int it = threadIdx.x + GN_THREADS * i;
         if (it < items) {
-            v[i] = *(const float4*)(in + base + (int64_t)(it / q) * Ctot + 4 * (it % q));
+            v[i] = *(const float4*)(in + base + (int64_t)pix[i] * Ctot + c4s[i]);
             s += v[i].x + v[i].y + v[i].z + v[i].w;
         }
     }
@@ -110,8 +120,8 @@ __global__ __launch_bounds__(GN_THREADS) void groupnorm_kernel(const float* __re
     for (int i = 0; i < GN_VMAX; ++i) {
         const int it = threadIdx.x + GN_THREADS * i;
         if (it < items) {
-            const int c4 = 4 * (it % q);
-            const int64_t off = base + (int64_t)(it / q) * Ctot + c4;
+            const int c4 = c4s[i];
+            const int64_t off = base + (int64_t)pix[i] * Ctot + c4;
             float4 y;
             y.x = (v[i].x - mean) * rstd * gg[c4 + 0] + bb[c4 + 0];
             y.y = (v[i].y - mean) * rstd * gg[c4 + 1] + bb[c4 + 1];

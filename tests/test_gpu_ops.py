@@ -576,3 +576,30 @@ def test_spm_attention(B, Lk, H):
     err = (out.cpu().double() - ref).abs().view(B, H, 64).amax(-1)
     print("spm per (b, h) err", err)
     assert err.max().item() <= 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dname", ["f32", "bf16"])
+@pytest.mark.parametrize("h,cin,pad", [(20, 48, 0), (40, 48, 16), (10, 16, 0), (16, 96, 8)])
+def test_conv3x3_c1_vs_torch(dname, h, cin, pad):
+    """mmt_conv3x3_c1 (adjust3 / adjust4 closing conv, head.py:115-120): Cout = 1 3x3/pad-1 conv +
+    bias + ReLU on NHWC [G][B][h*h][cin] with pixel stride cin + pad, vs F.conv2d in fp32."""
+    L = _lib()
+    dt = DT[dname]
+    G, B = 2, 2
+    g = torch.Generator().manual_seed(h * 1000 + cin + pad)
+    x = torch.randn(G, B, h, h, cin + pad, generator=g)
+    w = torch.randn(G, 9, cin, generator=g) / math.sqrt(9 * cin)
+    b = torch.randn(G, generator=g) * 0.1
+    xd, wd, bd = x.to(dt).cuda(), w.to(dt).cuda(), b.cuda()
+    out = torch.empty(G, B, h * h, device="cuda")
+    L.check(L.LIB.mmt_conv3x3_c1(xd.data_ptr(), wd.data_ptr(), bd.data_ptr(), out.data_ptr(), G, B, h, cin, cin + pad,
+                                 L.MMT_BF16 if dt == torch.bfloat16 else L.MMT_F32,
+                                 torch.cuda.current_stream().cuda_stream), "conv3x3_c1")
+    torch.cuda.synchronize()
+    xr = x.to(dt).float()[..., :cin]
+    wr = w.to(dt).float()
+    for gi in range(G):
+        ref = F.relu(F.conv2d(xr[gi].permute(0, 3, 1, 2), wr[gi].t().reshape(1, cin, 3, 3), b[gi:gi + 1], padding=1))
+        got = out[gi].cpu().reshape(B, 1, h, h)
+        assert (got - ref).abs().max().item() <= 1e-4 * (1 + ref.abs().max().item())
