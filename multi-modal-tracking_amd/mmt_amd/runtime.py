@@ -196,6 +196,21 @@ class MixFormerRGBTRuntime:
                 e[nm] = (self._F(sd[lp + nm + ".weight"]), self._F(sd[lp + nm + ".bias"]))
             W["enc"].append(e)
         W["pos_sine"] = self._F(_sine_pos(d.gs, d.d_model))  # [ns][512]
+        # The encoder query is src + (pos + level_embed[l]) per modality l (deformable_transformer
+        # with_pos_embed), and it only feeds the sampling-offset / attention-weight Linear, so that
+        # Linear splits as src.W^T + [(pos + le[l]).W_l^T summed over l + b]: the bracket is a
+        # per-cell constant folded here (float64 on the host), added by the GEMM's row-mapped
+        # residual, and the query tensor and its add kernel disappear.
+        pos64 = _sine_pos(d.gs, d.d_model).double()
+        le64 = sd[fa + "level_embed"].detach().cpu().double()
+        for li, e in enumerate(W["enc"]):
+            sa = fa + "encoder.layers.%d.self_attn." % li
+            w64 = torch.cat([sd[sa + "sampling_offsets.weight"], sd[sa + "attention_weights.weight"]], 0)
+            b64 = torch.cat([sd[sa + "sampling_offsets.bias"], sd[sa + "attention_weights.bias"]], 0)
+            w64, b64 = w64.detach().cpu().double(), b64.detach().cpu().double()
+            dm = d.d_model
+            pw = sum((pos64 + le64[l]) @ w64[:, l * dm:(l + 1) * dm].t() for l in range(2)) + b64
+            e["offw.pos"] = self._F(pw.float())  # [ns][192]
         # corner head
         h = "box_head."
         ws, bs = [], []
@@ -259,7 +274,7 @@ class MixFormerRGBTRuntime:
             "PATCH": e(R, 3 * d.patch * d.patch), "X": e(R, C, t=f32), "XN": e(R, C), "QKV": e(R, 3 * C),
             "AO": e(R, C), "HID": e(R, d.hidden), "XT": e(R, C),
             "Y1": e(2, B * ns, dm, t=f32), "SRC": e(2, B * ns, dm, t=f32), "SRCT": e(2, B * ns, dm),
-            "QS": e(2, B * ns, dm), "VAL": e(2, B * ns, dm), "OFFW": e(B * ns, 192, t=f32), "MS": e(B * ns, dm),
+            "VAL": e(2, B * ns, dm), "OFFW": e(B * ns, 192, t=f32), "MS": e(B * ns, dm),
             "SRC2": e(B * ns, dm, t=f32), "H2": e(2 * B * ns, d.ffn), "Y2": e(B * ns, C, t=f32),
             "FUS": e(B * ns, C, t=f32), "FUST": e(B * ns, C),
             "H0": e(B * ns, 2 * hc + hc + hc // 2), "X2": e(2, B * ns, hc // 2), "S1": e(2, B * ns, hc // 2),
@@ -269,10 +284,6 @@ class MixFormerRGBTRuntime:
             "BOX": e(B, 4, t=f32), "XYXY": e(B, 4, t=f32), "ROIS": e(B, 5, t=f32),
             "MAPS": e(2, B, d.fh * d.fh, t=f32),
         }
-        pos = self.w["pos_sine"]  # [ns][512]
-        le = self.w["level_embed"]
-        ws["POSE"] = torch.stack([(pos + le[l]).unsqueeze(0).expand(B, ns, dm).reshape(B * ns, dm)
-                                  for l in range(2)]).contiguous()
         if self.variant == "asym_online":
             ws.update({"ROIT": e(B * 16, C, t=f32), "KV0": e(B * 16, 2 * C, t=f32), "AT": e(B, C, t=f32),
                        "XS": e(B, C, t=f32), "Q1": e(B, C, t=f32), "KV1": e(B * d.n_t, 2 * C, t=f32),
@@ -483,7 +494,7 @@ class MixFormerRGBTRuntime:
             XT = ws["XT"]
             plan.append((LIB.mmt_add_cast, (P(X), None, 0, None, P(XT), R * C, cdt), "cast_x", None))
         # --- fusion: adjust_v / adjust_i (1x1 conv on the search tokens) + GroupNorm
-        Y1, SRC, SRCT, QS, VAL = ws["Y1"], ws["SRC"], ws["SRCT"], ws["QS"], ws["VAL"]
+        Y1, SRC, SRCT, VAL = ws["Y1"], ws["SRC"], ws["SRCT"], ws["VAL"]
         Mf = B * ns
         self._gemm(plan, "fusion_adjust", a=[P(XT, d.n_t * C), P(XT, B * ntok * C + d.n_t * C)],
                    w=[P(W["adj_v.w"]), P(W["adj_i.w"])], c=[P(Y1), P(Y1, Mf * dm)], M=Mf, N=dm, K=C, lda=C, ldc=dm,
@@ -492,12 +503,12 @@ class MixFormerRGBTRuntime:
                                          P(W["adj_i.gn"][0]), P(W["adj_i.gn"][1]), 2 * B, B, ns, dm, 32, 1e-5, cdt),
                      "fusion_gn", None))
         for e in W["enc"]:
-            plan.append((LIB.mmt_add_cast, (P(SRC), P(ws["POSE"]), 2 * Mf * dm, None, P(QS), 2 * Mf * dm, cdt),
-                         "enc_query", None))
             self._gemm(plan, "enc_value", a=[P(SRCT)], w=[P(e["value.w"])], c=[P(VAL)], M=2 * Mf, N=dm, K=dm, lda=dm,
                        ldc=dm, bias=[P(e["value.b"])])
-            self._gemm(plan, "enc_offw", a=[P(QS)], a1=[P(QS, Mf * dm)], k_split=dm, w=[P(e["offw.w"])],
-                       c=[P(ws["OFFW"])], M=Mf, N=192, K=2 * dm, lda=dm, ldc=192, bias=[P(e["offw.b"])], c_f32=1)
+            # offsets / logits of the query src + pos: src . W^T + the folded per-cell pos term
+            self._gemm(plan, "enc_offw", a=[P(SRCT)], a1=[P(SRCT, Mf * dm)], k_split=dm, w=[P(e["offw.w"])],
+                       c=[P(ws["OFFW"])], M=Mf, N=192, K=2 * dm, lda=dm, ldc=192, r=[P(e["offw.pos"])], ldr=192,
+                       r_mode=1, r_p0=ns, c_f32=1)
             plan.append((LIB.mmt_msda_bimodal, (P(ws["OFFW"]), P(VAL), P(ws["MS"]), B, d.gs, cdt), "msda_bimodal", None))
             self._gemm(plan, "enc_outproj", a=[P(ws["MS"])], w=[P(e["out.w"])], c=[P(ws["SRC2"])], M=Mf, N=dm, K=dm,
                        lda=dm, ldc=dm, bias=[P(e["out.b"])], c_f32=1)
