@@ -135,6 +135,20 @@ __global__ __launch_bounds__(SA_NT) void softargmax_kernel(const float* __restri
         for (int i = 1; i < SA_NT / 64; ++i) t = fmaxf(t, mred[g][i]);
         mx[g] = t;
     }
+    // grid coordinates of this thread's pixels, stepped by SA_NT without a division per pixel
+    int px[SA_PER], py[SA_PER];
+    {
+        const int dq = SA_NT / fh, dr = SA_NT - dq * fh;
+        int y = tid / fh, x = tid - y * fh;
+#pragma unroll
+        for (int i = 0; i < SA_PER; ++i) {
+            px[i] = x;
+            py[i] = y;
+            x += dr;
+            y += dq;
+            if (x >= fh) x -= fh, ++y;
+        }
+    }
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
         float se = 0.f, sx = 0.f, sy = 0.f;
@@ -144,8 +158,8 @@ __global__ __launch_bounds__(SA_NT) void softargmax_kernel(const float* __restri
             if (p < np) {
                 const float e = expf(v[g][i] - mx[g]);
                 se += e;
-                sx += e * (float)(stride * (p % fh));
-                sy += e * (float)(stride * (p / fh));
+                sx += e * (float)(stride * px[i]);
+                sy += e * (float)(stride * py[i]);
             }
         }
         se = wave_sum(se);
