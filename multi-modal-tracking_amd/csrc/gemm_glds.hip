@@ -122,11 +122,16 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
     const int ch = p.conv_h, cup = CONV ? p.conv_up : 1, hi = CONV ? p.conv_h / cup : 0;
     if constexpr (!CONV) {
         const int segr = (int)p.a_seg_rows, sega = (int)p.a_segs_a;
+        const bool plain = segr >= M;  // one segment (wave-uniform): no divisions ahead of the first DMA
 #pragma unroll
         for (int i = 0; i < PA; ++i) {
             const int m = min(m0 + (wid * PA + i) * 8 + prow, M - 1);
-            const int seg = m / segr, sa = seg % sega;  // 32-bit: the launcher checks the ranges
-            aoff[i] = sa * p.a_stride_a + (int64_t)((seg - sa) / sega) * p.a_stride_b + (int64_t)(m - seg * segr) * p.lda;
+            if (plain) {
+                aoff[i] = (int64_t)m * p.lda;
+            } else {
+                const int seg = m / segr, sa = seg % sega;  // 32-bit: the launcher checks the ranges
+                aoff[i] = sa * p.a_stride_a + (int64_t)((seg - sa) / sega) * p.a_stride_b + (int64_t)(m - seg * segr) * p.lda;
+            }
             ay[i] = ax[i] = 0;
         }
     } else {
