@@ -41,6 +41,29 @@ MMT_DEV float erf_fast(float x) {
 }
 MMT_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752440f)); }
 
+// gelu_erf on two values at once: the same approximation with the polynomial, the exponent
+// argument and the final scale as packed fp32 ops (v_pk_fma_f32 / v_pk_mul_f32 issue two lanes'
+// worth of fp32 per slot), leaving only v_rcp / v_exp per element.  The GEMM epilogue evaluates 64
+// of these per thread with one wave per SIMD, so its VALU issue count is what the fc1 tail costs.
+MMT_DEV f32x2 gelu_erf2(f32x2 x) {
+    const f32x2 z = x * 0.70710678118654752440f;
+    const f32x2 a = __builtin_elementwise_abs(z);
+    const f32x2 d = __builtin_elementwise_fma(a, f32x2(0.3275911f), f32x2(1.0f));
+    const f32x2 t = {__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+    f32x2 y = __builtin_elementwise_fma(t, f32x2(1.061405429f), f32x2(-1.453152027f));
+    y = __builtin_elementwise_fma(y, t, f32x2(1.421413741f));
+    y = __builtin_elementwise_fma(y, t, f32x2(-0.284496736f));
+    y = __builtin_elementwise_fma(y, t, f32x2(0.254829592f));
+    y = y * t;
+    const f32x2 q = a * (a * -1.44269504088896340736f);  // -a^2 log2(e)
+    const f32x2 e = {__builtin_amdgcn_exp2f(q[0]), __builtin_amdgcn_exp2f(q[1])};
+    const f32x2 r = __builtin_elementwise_fma(-y, e, f32x2(1.0f));  // erf(|z|)
+    const f32x2 h = x * 0.5f;
+    // GELU = h (1 + sign(z) erf|z|); sign(z) = sign(x)
+    const f32x2 s = {copysignf(r[0], x[0]), copysignf(r[1], x[1])};
+    return __builtin_elementwise_fma(h, s, h);
+}
+
 MMT_DEV float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

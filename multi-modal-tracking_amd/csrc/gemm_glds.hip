@@ -466,12 +466,15 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
             }
             va += bn0;
             vb += bn1;
+            if (p.act == 1) {
+                va.xy = gelu_erf2(va.xy);
+                va.zw = gelu_erf2(va.zw);
+                vb.xy = gelu_erf2(vb.xy);
+                vb.zw = gelu_erf2(vb.zw);
+            }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                if (p.act == 1) {
-                    va[j] = gelu_erf(va[j]);
-                    vb[j] = gelu_erf(vb[j]);
-                } else if (p.act == 2) {
+                if (p.act == 2) {
                     va[j] = fmaxf(va[j], 0.f);
                     vb[j] = fmaxf(vb[j], 0.f);
                 }
