@@ -219,22 +219,6 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
     }
 #define MMT_MMA(AF, BF)                                                                                          \
     {                                                                                                            \
-        if constexpr (LNF) { /* compile-time fragment index, scalar (wave-uniform) wave-column test */            \
-            _Pragma("unroll") for (int mt_ = 0; mt_ < MT; ++mt_) {                                               \
-                if (mt_ % WGN == wc_u) {                                                                         \
-                    float sx_ = 0.f, sxx_ = 0.f;                                                                 \
-                    _Pragma("unroll") for (int t = 0; t < 2; ++t)                                                \
-                    _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                              \
-                        const float lo_ = __uint_as_float(AF[t][mt_][e] << 16);                                  \
-                        const float hi_ = __uint_as_float(AF[t][mt_][e] & 0xffff0000u);                          \
-                        sx_ += lo_ + hi_;                                                                        \
-                        sxx_ = fmaf(lo_, lo_, fmaf(hi_, hi_, sxx_));                                             \
-                    }                                                                                            \
-                    lsx[mt_ / WGN] += sx_;                                                                       \
-                    lsxx[mt_ / WGN] += sxx_;                                                                     \
-                }                                                                                                \
-            }                                                                                                    \
-        }                                                                                                        \
         if (MMT_GEMM_ABLATE == 2) {                                                                              \
             acc[0][0] += __builtin_bit_cast(f32x4, AF[0][0]) + __builtin_bit_cast(f32x4, BF[1][NT - 1]);         \
         } else {                                                                                                 \
@@ -243,6 +227,23 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
             _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) acc[nt][mt] =                                      \
                 __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, BF[t][nt]),                   \
                                                         __builtin_bit_cast(bf16x8, AF[t][mt]), acc[nt][mt], 0, 0, 0); \
+        }                                                                                                        \
+        if constexpr (LNF) { /* compile-time fragment index, scalar (wave-uniform) wave-column test; */          \
+            /* packed fp32 sums (v_pk_add / v_pk_fma on the {lo, hi} bf16 pair), issued after the MFMAs */       \
+            _Pragma("unroll") for (int mt_ = 0; mt_ < MT; ++mt_) {                                               \
+                if (mt_ % WGN == wc_u) {                                                                         \
+                    f32x2 sx_ = {0.f, 0.f}, sxx_ = {0.f, 0.f};                                                   \
+                    _Pragma("unroll") for (int t = 0; t < 2; ++t)                                                \
+                    _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                              \
+                        const f32x2 v_ = {__uint_as_float(AF[t][mt_][e] << 16),                                  \
+                                          __uint_as_float(AF[t][mt_][e] & 0xffff0000u)};                         \
+                        sx_ += v_;                                                                               \
+                        sxx_ = __builtin_elementwise_fma(v_, v_, sxx_);                                          \
+                    }                                                                                            \
+                    lsx[mt_ / WGN] += sx_[0] + sx_[1];                                                           \
+                    lsxx[mt_ / WGN] += sxx_[0] + sxx_[1];                                                        \
+                }                                                                                                \
+            }                                                                                                    \
         }                                                                                                        \
     }
 
