@@ -57,7 +57,8 @@ def _tol(dt):
 
 
 @pytest.mark.parametrize("dname", ["f32", "bf16"])
-@pytest.mark.parametrize("M,N,K,act", [(300, 200, 192, 0), (1056, 2304, 768, 0), (128, 128, 64, 1), (77, 192, 1024, 2)])
+@pytest.mark.parametrize("M,N,K,act", [(300, 200, 192, 0), (1056, 2304, 768, 0), (128, 128, 64, 1), (77, 192, 1024, 2),
+                                       (1056, 3072, 768, 1)])  # the last: fc1 shape, packed GELU epilogue
 def test_gemm_plain(dname, M, N, K, act):
     dt = DT[dname]
     g = torch.Generator().manual_seed(M + N + K)
