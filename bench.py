@@ -3,10 +3,20 @@
 
 A step = one template+search forward (both modalities, boxes out) of B frames per GPU on synthetic
 inputs resident in HBM.  Four distinct input sets are rotated; each has its own captured hipGraph
-whose patch-staging kernel reads that set in place, so a step is one graph replay.  N>1: one
-process per GPU (torchrun), each an independent replica tracking its own sequences ("replicas
-only": the path has no exchange step), so scaling is weak and value = frames of all ranks /
-max-over-ranks time.
+whose patch-staging kernel reads that set in place, so a step is one graph replay.
+
+Multi-GPU (one process per GPU, no data-path collective):
+  default          single-stream tracking (config 2): every rank is an independent replica tracking
+                   its own sequences at B frames per step ("replicas only": each frame depends on the
+                   previous box, nothing to exchange); scaling "weak", value = frames of all ranks /
+                   max-over-ranks time.
+  --total-seqs T   batched multi-sequence inference (config 3, e.g. `--variant shared --total-seqs 64`):
+                   the T sequences are sharded over the ranks, T/N per rank (rank r owns sequences
+                   [r*T/N, (r+1)*T/N), each sequence's frames seeded by its global index, so the union
+                   of the shards is exactly the single-process batch); scaling "strong".
+  `python bench.py --gpus N` with no WORLD_SIZE in the environment starts N worker processes itself
+  (before any GPU call), each with RANK / LOCAL_RANK / WORLD_SIZE set; under torchrun, WORLD_SIZE must
+  equal --gpus.
 
 Extra fields:
   kernels        device time per launch of every plan entry (graph-replayed back-to-back launches
@@ -24,6 +34,8 @@ Extra fields:
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -242,6 +254,56 @@ def frame_seeds(rank, n=4):
     return [1 + n * rank + i for i in range(n)]
 
 
+def shard_range(total, world, rank):
+    """Sequences [lo, hi) of rank `rank` when `total` sequences are sharded over `world` ranks
+    (the reference's running.py:134-141 deals whole sequences to workers)."""
+    if total % world:
+        raise SystemExit("bench.py: --total-seqs %d is not divisible by %d ranks" % (total, world))
+    per = total // world
+    return rank * per, (rank + 1) * per
+
+
+def sequence_inputs(seqs, set_idx, template=128, search=320):
+    """Synthetic frames of the global sequences `seqs` for input set `set_idx`: each sequence's frame is
+    drawn from its own seed (1 + 1000 * set_idx + global index), so a rank's shard is the same data the
+    single-process run holds for those sequences."""
+    from mmt_amd import synthetic
+    parts = [synthetic.synth_inputs(1, template, search, seed=1 + 1000 * set_idx + q) for q in seqs]
+    cat = lambda i, m: torch.cat([p[i][m] for p in parts], 0)  # noqa: E731
+    return tuple([cat(i, 0), cat(i, 1)] for i in range(3))
+
+
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_workers(nprocs, argv, script=None):
+    """Start `nprocs` copies of this script, one per GPU (RANK = LOCAL_RANK = i, WORLD_SIZE = nprocs,
+    rendezvous on 127.0.0.1), wait for all of them and return the worst exit status.  Runs before
+    anything touches the GPU; the workers are children, never an exec of this process."""
+    script = script or os.path.abspath(__file__)
+    port = str(free_port())
+    procs = []
+    for r in range(nprocs):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nprocs), LOCAL_WORLD_SIZE=str(nprocs),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+def resolve_world(gpus):
+    """(world, rank, local_rank) from the launcher's environment; refuses a world size that disagrees
+    with --gpus (the line's n_gpus must be what ran)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != gpus:
+        raise SystemExit("bench.py: WORLD_SIZE=%d but --gpus %d" % (world, gpus))
+    return world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -260,11 +322,34 @@ def main():
     ap.add_argument("--no-kv-cache", action="store_true", help="skip the template K/V cache tracking-rate line")
     ap.add_argument("--vitl", action="store_true",
                     help="BASELINE config 5 geometry: ViT-L (1024 wide, 24 blocks), 192px templates / 384px search")
+    ap.add_argument("--total-seqs", type=int, default=0,
+                    help="batched multi-sequence inference (config 3): shard this many sequences over the ranks")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="harness check without a GPU: resolve ranks and shards over gloo, print them, exit")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:  # self-launch: one worker process per GPU
+        sys.exit(launch_workers(args.gpus, sys.argv[1:]))
+    world, rank, local = resolve_world(args.gpus)
+    sharded = args.total_seqs > 0
+    if sharded:
+        lo, hi = shard_range(args.total_seqs, world, rank)
+        args.batch = hi - lo
+    if args.dry_run:
+        if world > 1:
+            dist.init_process_group("gloo")
+        shard = [lo, hi] if sharded else None
+        shards = [None] * world
+        if world > 1:
+            dist.all_gather_object(shards, shard)
+        else:
+            shards = [shard]
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "batch_per_gpu": args.batch, "shards": shards,
+                              "scaling": "strong" if sharded else "weak"}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -281,8 +366,11 @@ def main():
     B = args.batch
     score = args.variant == "asym_online"
     pool = []
-    for seed in frame_seeds(rank):  # distinct frames per rank, resident in HBM before timing
-        t, o, s = synthetic.synth_inputs(B, geo["template"], geo["search"], seed=seed)
+    for i, seed in enumerate(frame_seeds(rank)):  # distinct frames per rank, resident in HBM before timing
+        if sharded:  # this rank's slice of the global batch
+            t, o, s = sequence_inputs(range(lo, hi), i, geo["template"], geo["search"])
+        else:
+            t, o, s = synthetic.synth_inputs(B, geo["template"], geo["search"], seed=seed)
         pool.append(([x.cuda() for x in t], [x.cuda() for x in o], [x.cuda() for x in s]))
     use_graph = not args.no_graph
     # one hipGraph per resident input set: the patch staging reads that set in place (zero-copy)
@@ -313,17 +401,26 @@ def main():
 
     if rank == 0:
         frames = world * B * args.steps
+        if sharded:
+            load = "%d sequences sharded over %d GPU(s) (%d per GPU), one frame each per step" % (
+                args.total_seqs, world, B)
+        else:
+            load = "%d frame(s)/GPU/step" % B
         out = {
             "metric": METRIC, "value": round(frames / elapsed, 2), "unit": "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+            "higher_is_better": True, "scaling": "strong" if sharded else "weak", "vs_baseline": None,
+            "dtype": args.dtype,
             "data": "synthetic N(0,1) frames (seeded), seed-hash random-init weights (mmt-synth-v1)",
-            "config": {"workload": "%s %s %dpx template x2 + %dpx search, RGB+TIR, %d frame(s)/GPU/step%s"
+            "config": {"workload": "%s %s %dpx template x2 + %dpx search, RGB+TIR, %s%s"
                                    % (VARIANT_NAMES[args.variant], "ViT-L" if args.vitl else "ViT-B", geo["template"],
-                                      geo["search"], B, ", score head on" if score else ""),
-                       "variant": args.variant, "batch_per_gpu": B, "template": geo["template"],
-                       "search": geo["search"], "hidden": geo["hidden"], "depth": geo["depth"],
-                       "parallelism": "replicas" if world > 1 else "single", "hip_graph": use_graph},
+                                      geo["search"], load, ", score head on" if score else ""),
+                       "variant": args.variant, "batch_per_gpu": B, "total_sequences": args.total_seqs or None,
+                       "template": geo["template"], "search": geo["search"], "hidden": geo["hidden"],
+                       "depth": geo["depth"],
+                       "parallelism": ("dp%d sharded sequences" % world if sharded else
+                                       "replicas x%d" % world if world > 1 else "single"),
+                       "hip_graph": use_graph},
             "roofline": dom, "roofline_mam": mam,
             "device_ms_per_step_sum": round(dev_ms, 4) if dev_ms else None, "launches_per_step": len(plan),
             "kernels": {k: {"us": round(a["t"] * 1e3 / a["n"], 2), "n": a["n"],

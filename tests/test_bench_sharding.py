@@ -1,0 +1,104 @@
+"""bench.py's multi-GPU harness on CPU (no GPU touched):
+
+* `python bench.py --gpus 2` with no WORLD_SIZE starts two worker processes itself and the line reports
+  n_gpus 2; a WORLD_SIZE that disagrees with --gpus is refused;
+* batched sharded inference (reference running.py:134-141, 223-232 deals whole
+  sequences to workers): rank r owns sequences [r*T/N, (r+1)*T/N) and its inputs are exactly those
+  sequences' rows of the single-process batch, so the gathered per-rank outputs equal one process
+  running all T sequences (checked through the oracle's forward on a 2-block shared backbone over
+  gloo, world size 2).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _clean_env():
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return env
+
+
+def _last_json(out):
+    return json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
+
+
+def test_gpus_flag_spawns_workers_and_reports_world():
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dry-run", "--total-seqs", "64"],
+                       env=_clean_env(), capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr
+    line = _last_json(r.stdout)
+    assert line["n_gpus"] == 2 and line["batch_per_gpu"] == 32 and line["scaling"] == "strong"
+    assert line["shards"] == [[0, 32], [32, 64]]
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dry-run"], env=_clean_env(),
+                       capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr
+    line = _last_json(r.stdout)
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
+
+
+def test_world_size_mismatch_refused():
+    env = dict(_clean_env(), WORLD_SIZE="3")
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dry-run"], env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=3" in r.stderr
+
+
+def test_shard_ranges_partition():
+    sys.path.insert(0, ROOT)
+    import bench
+    for world in (1, 2, 4, 8):
+        got = [bench.shard_range(64, world, r) for r in range(world)]
+        assert got[0][0] == 0 and got[-1][1] == 64
+        assert all(a[1] == b[0] for a, b in zip(got, got[1:]))
+
+
+def _sd():
+    from mmt_amd import synthetic
+    from mmt_amd.model import reference_state_dict_shapes
+    from oracle.forward import state_dict_to_torch
+    return state_dict_to_torch(synthetic.synth_state_dict(reference_state_dict_shapes("shared", depth=2)))
+
+
+def _worker(rank, world, port, total, out):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    from oracle.forward import forward
+    lo, hi = bench.shard_range(total, world, rank)
+    t, o, s = bench.sequence_inputs(range(lo, hi), 0)
+    res, _ = forward(_sd(), "shared", t, o, s)
+    boxes = res["pred_boxes"].contiguous()
+    gathered = [torch.empty_like(boxes) for _ in range(world)]
+    dist.all_gather(gathered, boxes)  # the optional (B,4) box gather to rank 0
+    if rank == 0:
+        out["boxes"] = torch.cat(gathered, 0).numpy()
+    dist.destroy_process_group()
+
+
+def test_sharded_slices_equal_single_process():
+    sys.path.insert(0, ROOT)
+    import bench
+    from oracle.forward import forward
+    total, world, port = 4, 2, 29641
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_worker, args=(world, port, total, out), nprocs=world, join=True)
+        sharded = torch.from_numpy(out["boxes"])
+    torch.set_num_threads(4)
+    t, o, s = bench.sequence_inputs(range(total), 0)
+    full, _ = forward(_sd(), "shared", t, o, s)
+    assert sharded.shape == full["pred_boxes"].shape == (total, 1, 4)
+    assert torch.allclose(sharded, full["pred_boxes"], atol=1e-5, rtol=0), (sharded - full["pred_boxes"]).abs().max()
