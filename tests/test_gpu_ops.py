@@ -312,7 +312,10 @@ def _attn_ref(qkv, S, Bm, ntok, n_t, C, H, asym):
     return out.permute(0, 2, 1, 3).reshape(S, ntok, C)
 
 
-@pytest.mark.parametrize("dname,impl", [("f32", 0), ("bf16", 2), ("bf16", 4), ("bf16", 8), ("bf16", 9), ("bf16", 10), ("bf16", 11), ("bf16", 12)])
+ATTN_BF16_IMPLS = [2, 4, 8, 9, 10, 11, 12, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25]
+
+
+@pytest.mark.parametrize("dname,impl", [("f32", 0), ("bf16", 0)] + [("bf16", i) for i in ATTN_BF16_IMPLS])
 @pytest.mark.parametrize("asym", [0, 1])
 @pytest.mark.parametrize("Bm,ntok,n_t,H", [(1, 528, 128, 12), (2, 100, 36, 2), (1, 70, 8, 1), (1, 864, 288, 2)])
 def test_mam_attention(dname, impl, asym, Bm, ntok, n_t, H):
@@ -336,7 +339,7 @@ def test_mam_attention(dname, impl, asym, Bm, ntok, n_t, H):
     assert err <= (1.5e-2 if dt == torch.bfloat16 else 2e-5), err
 
 
-@pytest.mark.parametrize("dname,impl", [("f32", 0), ("bf16", 2), ("bf16", 4), ("bf16", 8), ("bf16", 9), ("bf16", 10), ("bf16", 11), ("bf16", 12)])
+@pytest.mark.parametrize("dname,impl", [("f32", 0), ("bf16", 0)] + [("bf16", i) for i in ATTN_BF16_IMPLS])
 def test_mam_attention_rescale_branch(dname, impl):
     """Online-softmax rescale forced: one key per query block carries a huge score in a late tile
     (bf16: and in a different key group than the first tile, so the group merge rescales)."""
@@ -358,7 +361,7 @@ def test_mam_attention_rescale_branch(dname, impl):
     assert (out.float().cpu() - ref).abs().max().item() < (1.5e-2 if dt == torch.bfloat16 else 5e-5)
 
 
-@pytest.mark.parametrize("impl", [2, 4, 8, 9, 10, 12])
+@pytest.mark.parametrize("impl", [0, 2, 4, 8, 9, 10, 12, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25])
 @pytest.mark.parametrize("asym", [0, 1])
 def test_mam_attention_prescaled_q(impl, asym):
     """The runtime's convention (bf16): q arrives multiplied by scale * log2(e) (folded into the qkv
@@ -383,6 +386,34 @@ def test_mam_attention_prescaled_q(impl, asym):
     ref = _attn_ref(qr, S, Bm, ntok, n_t, C, H, asym)
     err = (out.float().cpu() - ref).abs().max().item()
     assert err <= 1.5e-2, err
+
+
+@pytest.mark.parametrize("impl", [0, 4, 8, 16, 17, 20, 21, 22, 23, 24, 25])
+@pytest.mark.parametrize("asym", [0, 1])
+def test_mam_attention_extreme_scores(impl, asym):
+    """Scores far outside the fp32 exponent range of exp2 without a reference point: a key that
+    overflows it for one query (key 500 = 60 x query 300) and a query whose every score is huge in
+    magnitude (query 310 x 40: both signs).  The range-checked kernels (16, 17) must detect this in
+    their epilogue and take the exact two-pass fallback; every kernel must match the fp64 softmax."""
+    L = _lib()
+    Bm, ntok, n_t, H = 2, 528, 128, 2
+    S, C = 2 * Bm, 64 * H
+    g = torch.Generator().manual_seed(5 + asym)
+    qkv = torch.randn(S, ntok, 3 * C, generator=g) * 0.5
+    qkv[:, 500, C:2 * C] = qkv[:, 300, :C] * 60
+    qkv[:, 310, :C] *= 40
+    qkv[:, 40, :C] *= 40  # a template query too
+    qd = qkv.bfloat16().cuda()
+    out = torch.empty(S, ntok, C, device="cuda", dtype=torch.bfloat16)
+    p = L.AttnParams()
+    p.qkv, p.out, p.S, p.Bm, p.ntok, p.n_t, p.C, p.H, p.asym, p.scale = qd.data_ptr(), out.data_ptr(), S, Bm, ntok, n_t, C, H, asym, 0.125
+    p.impl = impl
+    L.check(L.LIB.mmt_mam_attention(p, L.MMT_BF16, torch.cuda.current_stream().cuda_stream), "attn")
+    torch.cuda.synchronize()
+    ref = _attn_ref(qkv.bfloat16().double(), S, Bm, ntok, n_t, C, H, asym).float()
+    o = out.float().cpu()
+    assert torch.isfinite(o).all()
+    assert (o - ref).abs().max().item() < 2.5e-2 * max(1.0, ref.abs().max().item())
 
 
 @pytest.mark.parametrize("dname", ["f32", "bf16"])

@@ -2,14 +2,23 @@
 # Measurement-only variants of libmmt_hip.so (never the product):
 #   ablate1: LDS-DMA GEMM K loop without DMA after the prologue (MMT_GEMM_ABLATE=1)
 #   ablate2: LDS-DMA GEMM K loop without MFMA work          (MMT_GEMM_ABLATE=2)
+#   aab1/2/3: range-checked MAM attention without K/V DMA after the prologue / without matrix and
+#            softmax work / without exponentials / without exponentials and bf16 packing
+#            (MMT_ATTN_ABLATE=1/2/3/4)
 #   stamp:   per-phase workgroup timestamps in the GEMM / attention kernels (MMT_STAMP_BUILD=1)
 # Use with MMT_HIP_LIB=multi-modal-tracking_amd/mmt_amd/_lib/<variant>/libmmt_hip.so.
 set -e
+ONLY=${1:-}
 cd "$(dirname "$0")/../multi-modal-tracking_amd/csrc"
 build() {
+  if [ -n "$ONLY" ] && [ "$ONLY" != "$1" ]; then return; fi
   make -s OUT=../mmt_amd/_lib/$1 OBJDIR=../mmt_amd/_lib/$1/obj \
        CXXFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 $2"
 }
 build ablate1 -DMMT_GEMM_ABLATE=1
 build ablate2 -DMMT_GEMM_ABLATE=2
 build stamp -DMMT_STAMP_BUILD=1
+build aab1 -DMMT_ATTN_ABLATE=1
+build aab2 -DMMT_ATTN_ABLATE=2
+build aab3 -DMMT_ATTN_ABLATE=3
+build aab4 -DMMT_ATTN_ABLATE=4
