@@ -55,12 +55,16 @@ def make_tracker_class(builder, multimodal, online_score=False, kv_cache=True):
         def track(self, image, info: dict = None):
             self.frame_id += 1
             self.state = self.core.track(image)
-            if self.save_all_boxes:  # one query: all boxes = the tracked box (mixformer_vit_rgbt.py:114-117)
-                return {"target_bbox": self.state, "all_boxes": list(self.state)}
+            if self.save_all_boxes:  # mixformer_vit_rgbt.py:131-134: the unclipped box mapped back
+                rf = self.params.search_size / self.core.last_crop_sz
+                box = [v * self.params.search_size / rf for v in self.core.last_pred_box()]
+                return {"target_bbox": self.state, "all_boxes": self.map_box_back(box, rf)}
             return {"target_bbox": self.state}
 
         def map_box_back(self, pred_box: list, resize_factor: float):
-            """mixformer_vit_rgbt.py:124-131 (host form; the tracking step runs it on the device)."""
+            """mixformer_vit_rgbt.py:124-131 (host form; the tracking step runs it on the device).  Like
+            the reference's map_box_back_batch for all_boxes (:133-139), it reads the current state,
+            which at that point is already this frame's (clipped) result."""
             cx_prev, cy_prev = self.state[0] + 0.5 * self.state[2], self.state[1] + 0.5 * self.state[3]
             cx, cy, w, h = pred_box
             half_side = 0.5 * self.params.search_size / resize_factor

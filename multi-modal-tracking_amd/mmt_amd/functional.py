@@ -72,6 +72,7 @@ class MSDeformAttnFunction(torch.autograd.Function):
 class PrRoIPool2DFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, features, rois, pooled_height, pooled_width, spatial_scale):
+        ctx.dtypes = (features.dtype, rois.dtype)  # gradients go back in the inputs' dtypes
         features = features.contiguous().float()
         rois = rois.contiguous().float()
         _need(features, "features", (torch.float32,))
@@ -95,15 +96,19 @@ class PrRoIPool2DFunction(torch.autograd.Function):
         R = rois.shape[0]
         g = grad_output.contiguous().float()
         gf = gr = None
-        if features.requires_grad:
+        # needs_input_grad, not the saved copies' requires_grad: forward's .float() copies of
+        # non-fp32 inputs are made with grad mode off and never require grad
+        if ctx.needs_input_grad[0]:
             gf = torch.empty_like(features)
             check(LIB.mmt_prroi_pool_backward(rois.data_ptr(), g.data_ptr(), gf.data_ptr(), B, R, C, H, W, ph, pw, sc,
                                               _stream()), "mmt_prroi_pool_backward")
-        if rois.requires_grad:
+            gf = gf.to(ctx.dtypes[0])
+        if ctx.needs_input_grad[1]:
             gr = torch.empty_like(rois)
             check(LIB.mmt_prroi_pool_coor_backward(features.data_ptr(), rois.data_ptr(), out.data_ptr(), g.data_ptr(),
                                                    gr.data_ptr(), R, C, H, W, ph, pw, sc, _stream()),
                   "mmt_prroi_pool_coor_backward")
+            gr = gr.to(ctx.dtypes[1])
         return gf, gr, None, None, None
 
 

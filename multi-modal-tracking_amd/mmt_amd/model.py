@@ -211,9 +211,12 @@ class ScoreDecoder(nn.Module):
 
 # ----------------------------------------------------------------------------- HIP-backed models
 class _HipTracker(nn.Module):
-    """Common forward: prepares mmt_amd.runtime from this module's parameters, runs the plan."""
+    """Common forward: prepares mmt_amd.runtime from this module's parameters, runs the plan
+    (inference); in train() mode under autograd, mmt_amd.train.module_forward."""
 
     variant = None
+    train_ops = None  # None = mmt_amd.train.HipOps (the product); tests on CPU inject a stand-in
+    drop_path_rate = 0.1  # the backbone's stochastic depth in training (mixformer.py:311, :324)
 
     def __init__(self, head_type="CORNER_UP"):
         super().__init__()
@@ -251,16 +254,27 @@ class _HipTracker(nn.Module):
             if not isinstance(x, (list, tuple)) or len(x) != 2:
                 raise ValueError("%s must be a list [rgb, tir] of (B,3,H,W) tensors" % nm)
         dev = search[0].device
+        if self.training and torch.is_grad_enabled():
+            # training (the reference actor, DDP + SyncBN wrap this module unchanged): autograd over
+            # the HIP ops of mmt_amd.train; `train_ops` may be replaced only by test stand-ins
+            from .train import HipOps, module_forward
+            ops = self.train_ops or HipOps
+            if ops is HipOps and dev.type != "cuda":
+                raise RuntimeError("the MI355X forward needs the inputs on the HIP device (got %s); there is no CPU path"
+                                   % dev)
+            return module_forward(self, template, online_template, search, ops, run_score_head=run_score_head,
+                                  gt_bboxes=gt_bboxes)
         if dev.type != "cuda":
             raise RuntimeError("the MI355X forward needs the inputs on the HIP device (got %s); there is no CPU path" % dev)
-        if self.training and torch.is_grad_enabled():
-            raise NotImplementedError("training forward (autograd) is not implemented on the HIP path yet; "
-                                      "call .eval() / torch.no_grad() for tracking")
         rt = self._runtime(dev)
         score = bool(run_score_head) and self.variant == "asym_online"
+        on_gt = score and gt_bboxes is not None
         with torch.cuda.device(dev):
-            box, sc = rt.forward(template, online_template, search, run_score_head=score, use_graph=self.use_hip_graph)
+            box, sc = rt.forward(template, online_template, search, run_score_head=score and not on_gt,
+                                 use_graph=self.use_hip_graph)
             B = box.shape[0]
+            if on_gt:  # the ROI is the given box, not the prediction (asymmetric_shared_online.py:405-410)
+                sc = rt.score_on_boxes(B, gt_bboxes.to(device=dev, dtype=torch.float32))
             coord = box.clone().view(B, 1, 4)
             out = {"pred_boxes": coord}
             if score:
@@ -358,10 +372,33 @@ class MixFormer_RGBT_CE(MixFormer_RGBT_Shared):
     def _runtime(self, device):
         if self._rt is None:
             from .runtime import MixFormerRGBTRuntime
+            keep = self.ce_keep_ratio if self._keep_override is None else (self._keep_override,) * len(self.ce_loc)
             with torch.cuda.device(device):
                 self._rt = MixFormerRGBTRuntime(self.state_dict(), self.variant, dtype=self.compute_dtype,
-                                                device=device, ce=(self.ce_loc, self.ce_keep_ratio))
+                                                device=device, ce=(self.ce_loc, keep))
         return self._rt
+
+    _keep_override = None
+
+    def forward(self, template, online_template, search, run_score_head=False, gt_bboxes=None, ce_template_mask=None,
+                ce_keep_rate=None, return_features=False):
+        """asymmetric_shared_ce.py:557-587 signature.  ce_keep_rate (the actor's keep-rate schedule,
+        actors/mixformer_rgbt.py:70-89) replaces every CE layer's keep ratio; >= 1 disables the
+        elimination (asymmetric_shared_ce.py:249-252).  ce_template_mask (generate_mask_cond) must be
+        None or select every template token: the CE kernels average the attention of all template
+        queries."""
+        if ce_template_mask is not None and not bool(torch.as_tensor(ce_template_mask).all()):
+            raise NotImplementedError("ce_template_mask restricted to part of the template (CE_TEMPLATE_RANGE other "
+                                      "than ALL) is not supported by the candidate-elimination kernels")
+        if self.training and torch.is_grad_enabled():
+            raise NotImplementedError("training forward of asymmetric_shared_ce (candidate elimination with autograd) "
+                                      "is not built; its inference forward runs under eval() / no_grad()")
+        rate = None if ce_keep_rate is None else float(ce_keep_rate)
+        if rate != self._keep_override:
+            self._keep_override = rate
+            self.refresh_kernels()
+        return super().forward(template, online_template, search, run_score_head=run_score_head, gt_bboxes=gt_bboxes,
+                               return_features=return_features)
 
     def set_online(self, template, online_template):
         raise NotImplementedError("the template K/V cache is not defined for candidate elimination")

@@ -296,6 +296,8 @@ class MixFormerRGBTRuntime:
         ws["plan"] = self._build_plan(ws, False)
         if self.variant == "asym_online":
             ws["plan_score"] = self._build_plan(ws, True)
+            ws["plan_spm"] = []  # the score decoder alone, on ROIS as given (forward with gt_bboxes)
+            self._plan_spm(ws["plan_spm"], ws)
         self._ws[B] = ws
         return ws
 
@@ -649,6 +651,18 @@ class MixFormerRGBTRuntime:
         else:
             self.run_plan(ws["plan_score"] if score else ws["plan"])
         return ws["BOX"], (ws["SC"].view(-1) if score else None)
+
+    def score_on_boxes(self, B, boxes_xyxy):
+        """The score head on given boxes (asymmetric_shared_online.py:405-410: gt_bboxes, xyxy
+        normalised to the search crop, instead of the predicted box) after forward() of batch B:
+        ROIs = [b, box * feature size] into the workspace, then the ScoreDecoder plan."""
+        ws = self.workspace(B)
+        gs = float(self.d.gs)
+        rois = ws["ROIS"]
+        rois[:, 0] = torch.arange(B, device=rois.device, dtype=rois.dtype)
+        rois[:, 1:] = boxes_xyxy.reshape(B, 4).to(rois.dtype) * gs
+        self.run_plan(ws["plan_spm"])
+        return ws["SC"].view(-1)
 
     # ------------------------------------------------------------------ template K/V cache
     def cache_workspace(self, B):

@@ -106,6 +106,8 @@ class RGBTTrackerCore:
         self.frames = None
         self._graph = None
         self._plan = None
+        self._rt = None
+        self._tmpl_graph = None
         self.frame_id = 0
         self.max_pred_score = -1.0
 
@@ -134,6 +136,9 @@ class RGBTTrackerCore:
     # ------------------------------------------------------------------ per-frame plan
     def _build_step(self):
         rt = self.net._runtime(self.dev)
+        # the captured graphs hold raw pointers into this runtime's weights and workspace: keep it
+        # alive, and rebuild when the network swaps it (load_state_dict / .to() / refresh_kernels)
+        self._rt = rt
         score = self.online_score
         H, W = self.frames[0].shape[:2]
         self._keep = [crop_params(self.frames[m], self.state, self.sf, self.ss, out=self.search[m].view(-1),
@@ -163,18 +168,21 @@ class RGBTTrackerCore:
             self._graph = None
 
     def _step(self):
+        if self._plan is not None and self.net._runtime(self.dev) is not self._rt:
+            self._graph = self._plan = self._tmpl_graph = None  # weights reloaded: re-plan, re-capture
+            self._tmpl_dirty = True
         if self._plan is None or (self.use_graph and self._graph is None):
             self._build_step()
         if self.kv_cache and self._tmpl_dirty:  # template pass after a template / online-template change
             if self._tmpl_graph is not None:
                 self._tmpl_graph.replay()
             else:
-                self.net._runtime(self.dev).run_plan(self._tmpl_plan)
+                self._rt.run_plan(self._tmpl_plan)
             self._tmpl_dirty = False
         if self._graph is not None:
             self._graph.replay()
         else:
-            self.net._runtime(self.dev).run_plan(self._plan)
+            self._rt.run_plan(self._plan)
 
     # ------------------------------------------------------------------ tracker API
     def initialize(self, image, init_bbox):
@@ -217,7 +225,12 @@ class RGBTTrackerCore:
         vals = torch.cat([self.state, self.search_crop[:, 2]]).tolist()  # the step's one host round trip
         if min(vals[4:]) < 1:
             raise Exception("Too small bounding box.")  # processing_utils.py:36-37
+        self.last_crop_sz = vals[4]  # this frame's RGB search crop side (resize factor = search_size / it)
         return vals[:4]
+
+    def last_pred_box(self):
+        """This frame's network box (cx, cy, w, h), normalised to the search crop (one extra host copy)."""
+        return self._ws["BOX"].view(-1, 4)[0].tolist()
 
     def _check_crop(self, crop):
         if float(crop[:, 2].min()) < 1:

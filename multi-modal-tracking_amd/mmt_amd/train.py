@@ -136,6 +136,10 @@ class HipOps:
         return _HipMamAttention.apply(qkv, n_t, heads)
 
     @staticmethod
+    def mam_attention_asym(qkv, Bh, n_t, heads):
+        return asym_attention_from_mam(HipOps.mam_attention, qkv, Bh, n_t, heads)
+
+    @staticmethod
     def ms_deform_attn(value, hw, loc, aw):
         """MSDeformAttnFunction (ms_deform_attn_func.py:22-38) on mmt_ms_deform_attn_forward / _backward,
         fp32 as the reference op; L levels of hw x hw."""
@@ -144,6 +148,26 @@ class HipOps:
         shapes = torch.tensor([[hw, hw]] * L, dtype=torch.long, device=value.device)
         starts = torch.arange(L, dtype=torch.long, device=value.device) * (hw * hw)
         return MSDeformAttnFunction.apply(value, shapes, starts, loc, aw, 64)
+
+
+def asym_attention_from_mam(mam, qkv, Bh, n_t, heads):
+    """Cross-modal asymmetric MAM (asymmetric_shared.py:55-104) composed from two standard MAM
+    attentions, so that training reuses the standard kernel pair (forward with log-sum-exp,
+    mmt_mam_attention_bwd) and autograd routes the gradients back into qkv:
+      - template queries of every sequence attend its own template keys: the standard attention of
+        the sequence itself, template rows kept;
+      - search queries of modality m attend [template_V | template_I | search_m]: the standard
+        attention of the built sequence [tV | tI | s_m] with 2 n_t "template" rows, search rows kept.
+    qkv: (2 Bh, ntok, 3C), RGB sequences first.  The discarded rows cost extra arithmetic (about 1.6x
+    the attention FLOPs of the fused inference kernel) but no accuracy: their outputs get zero
+    gradients, which contribute nothing to dq / dk / dv."""
+    ntok = qkv.shape[1]
+    own = mam(qkv, n_t, heads)
+    t_v, t_i = qkv[:Bh, :n_t], qkv[Bh:, :n_t]
+    tt = torch.cat([t_v, t_i], 1)  # (Bh, 2 n_t, 3C)
+    built = torch.cat([torch.cat([tt, qkv[:Bh, n_t:]], 1), torch.cat([tt, qkv[Bh:, n_t:]], 1)], 0)
+    cross = mam(built.contiguous(), 2 * n_t, heads)
+    return torch.cat([own[:, :n_t], cross[:, 2 * n_t:]], 1)
 
 
 # ----------------------------------------------------------------------------- forward
@@ -158,7 +182,7 @@ def _drop_path(x, p, training):
     return x * keep / (1.0 - p)
 
 
-def backbone_forward(bb, t, o, s, ops):
+def backbone_forward(bb, t, o, s, ops, drop_path_rate=DROP_PATH_RATE):
     """VisionTransformer.forward (mixformer.py:231-259) for one modality: returns the search
     features (B, C, gs, gs) fp32.  Tokens [template | online | search], pre-LN blocks; in training
     mode the blocks' residual branches use stochastic depth (mixformer.py:129-138)."""
@@ -174,7 +198,7 @@ def backbone_forward(bb, t, o, s, ops):
     x = x.float().view(B, ntok, C) + pos
     depth = len(bb.blocks)
     for li, blk in enumerate(bb.blocks):
-        dp = DROP_PATH_RATE * li / max(depth - 1, 1)
+        dp = drop_path_rate * li / max(depth - 1, 1)
         xn = F.layer_norm(x, (C,), blk.norm1.weight, blk.norm1.bias, 1e-6).to(ops.dtype)
         qkv = ops.linear(xn.view(B * ntok, C), blk.attn.qkv.weight, blk.attn.qkv.bias).view(B, ntok, 3 * C)
         a = ops.mam_attention(qkv, n_t, H).view(B * ntok, C)
@@ -187,6 +211,43 @@ def backbone_forward(bb, t, o, s, ops):
                            bb.training)
     xs = x[:, n_t:]
     return xs.transpose(1, 2).reshape(B, C, gs, gs)
+
+
+def backbone_forward_stacked(bb, t, o, s, ops, asym=False, drop_path_rate=DROP_PATH_RATE):
+    """Shared-backbone forward with the modalities stacked on the batch ([rgb; tir], 2B):
+    mixformer_shared.py:143-159, :253-282 (per-modality LayerNorms, shared weights, standard MAM) or,
+    asym, asymmetric_shared.py:137-154, :236-266 (cross-modal MAM).  Returns the search features
+    (2B, C, gs, gs) and the first template's tokens (2B, gt*gt, C) (the score decoder's memory)."""
+    B2 = t.shape[0]
+    Bh = B2 // 2
+    C = bb.pos_embed_s.shape[-1]
+    H = C // 64
+    gt, gs = bb.grid_size_t, bb.grid_size_s
+    ntok, n_t = 2 * gt * gt + gs * gs, 2 * gt * gt
+    patches = torch.cat([F.unfold(x, 16, stride=16).transpose(1, 2) for x in (t, o, s)], 1)
+    w = bb.patch_embed.proj.weight
+    x = ops.linear(patches.reshape(B2 * ntok, -1).to(ops.dtype), w.reshape(w.shape[0], -1), bb.patch_embed.proj.bias)
+    pos = torch.cat([bb.pos_embed_t, bb.pos_embed_t, bb.pos_embed_s], 1)
+    x = x.float().view(B2, ntok, C) + pos
+    depth = len(bb.blocks)
+
+    def ln2(x, a, b):  # norm*_v on the RGB half, norm*_i on the TIR half
+        return torch.cat([F.layer_norm(x[:Bh], (C,), a.weight, a.bias, 1e-6),
+                          F.layer_norm(x[Bh:], (C,), b.weight, b.bias, 1e-6)], 0).to(ops.dtype)
+
+    for li, blk in enumerate(bb.blocks):
+        dp = drop_path_rate * li / max(depth - 1, 1)
+        xn = ln2(x, blk.norm1_v, blk.norm1_i)
+        qkv = ops.linear(xn.view(B2 * ntok, C), blk.attn.qkv.weight, blk.attn.qkv.bias).view(B2, ntok, 3 * C)
+        a = ops.mam_attention_asym(qkv, Bh, n_t, H) if asym else ops.mam_attention(qkv, n_t, H)
+        x = x + _drop_path(ops.linear(a.reshape(B2 * ntok, C), blk.attn.proj.weight, blk.attn.proj.bias).float()
+                           .view(B2, ntok, C), dp, bb.training)
+        xn = ln2(x, blk.norm2_v, blk.norm2_i)
+        h = ops.linear(xn.view(B2 * ntok, C), blk.mlp.fc1.weight, blk.mlp.fc1.bias)
+        h = F.gelu(h.float()).to(ops.dtype)
+        x = x + _drop_path(ops.linear(h, blk.mlp.fc2.weight, blk.mlp.fc2.bias).float().view(B2, ntok, C), dp,
+                           bb.training)
+    return x[:, n_t:].transpose(1, 2).reshape(B2, C, gs, gs), x[:, :gt * gt]
 
 
 def _sine_pos(B, C, H, W, device):
@@ -284,6 +345,47 @@ def forward_boxes(net, template, online_template, search, ops):
         xyxy = head_forward(net.box_head, fused)
     x0, y0, x1, y1 = xyxy.float().unbind(-1)
     return torch.stack([(x0 + x1) / 2, (y0 + y1) / 2, (x1 - x0), (y1 - y0)], -1).view(-1, 1, 4)
+
+
+def module_forward(net, template, online_template, search, ops, run_score_head=False, gt_bboxes=None):
+    """The drop-in module's forward with autograd (net.train() under grad mode; what the reference's
+    MixFormerRGBTActor calls, actors/mixformer_rgbt.py:82-98, possibly wrapped in DDP + SyncBN,
+    train_script_mixformer.py:105-110): MixFormer_RGBT.forward (mixformer.py:366-395),
+    mixformer_shared.py:400-424, asymmetric_shared.py:349-368 and asymmetric_shared_online.py:351-413
+    (score head on gt_bboxes when given, else on the predicted boxes).  Returns
+    ({"pred_boxes": (B,1,4)[, "pred_scores": (B,)]}, (B,1,4))."""
+    variant = net.variant
+    dpr = getattr(net, "drop_path_rate", DROP_PATH_RATE)
+    if variant == "rgbt":
+        s_v = backbone_forward(net.backbone_v, template[0], online_template[0], search[0], ops, dpr)
+        s_i = backbone_forward(net.backbone_i, template[1], online_template[1], search[1], ops, dpr)
+        tok = None
+    elif variant in ("shared", "asym", "asym_online"):
+        feats, tok = backbone_forward_stacked(net.backbone, torch.cat(template, 0), torch.cat(online_template, 0),
+                                              torch.cat(search, 0), ops, asym=variant != "shared", drop_path_rate=dpr)
+        s_v, s_i = feats.chunk(2, 0)
+    else:
+        raise NotImplementedError("training forward of %s (candidate elimination with autograd) is not built; "
+                                  "its inference forward runs under eval() / no_grad()" % variant)
+    with torch.autocast(s_v.device.type, dtype=torch.bfloat16, enabled=s_v.device.type == "cuda"):
+        fused = fusion_forward(net.fusion_vi, s_v, s_i, ops)
+        xyxy = head_forward(net.box_head, fused)
+    x0, y0, x1, y1 = xyxy.float().unbind(-1)
+    coord = torch.stack([(x0 + x1) / 2, (y0 + y1) / 2, (x1 - x0), (y1 - y0)], -1).view(-1, 1, 4)
+    out = {"pred_boxes": coord}
+    if run_score_head and variant == "asym_online":
+        B = coord.shape[0]
+        gt = tok.shape[1]
+        g = int(round(gt ** 0.5))
+        C = tok.shape[-1]
+        t_v, t_i = tok[:B].transpose(1, 2).reshape(B, C, g, g), tok[B:].transpose(1, 2).reshape(B, C, g, g)
+        templ = torch.cat([t_v, t_i], 2)
+        if gt_bboxes is None:  # box_cxcywh_to_xyxy(outputs_coord.clone())
+            xc, yc, w, h = coord.clone().view(-1, 4).unbind(-1)
+            gt_bboxes = torch.stack([xc - 0.5 * w, yc - 0.5 * h, xc + 0.5 * w, yc + 0.5 * h], -1)
+        out["pred_scores"] = score_decoder_forward(net.score_branch, fused.float(), templ.float(),
+                                                   gt_bboxes.view(-1, 4).float())
+    return out, coord
 
 
 # ----------------------------------------------------------------------------- loss / optimizer

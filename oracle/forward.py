@@ -426,7 +426,8 @@ def score_decoder(sd, pre, search, template, box_xyxy, num_heads=12):
 
 # ----------------------------------------------------------------------------- models
 @torch.no_grad()
-def forward(sd, variant, template, online_template, search, run_score_head=False, return_aux=False, ce_forced=None):
+def forward(sd, variant, template, online_template, search, run_score_head=False, return_aux=False, ce_forced=None,
+            gt_bboxes=None):
     """Reference-equivalent forward.  template / online_template / search are [rgb, tir] lists
     of (B,3,H,W) fp32 CPU tensors.  Returns (out_dict, outputs_coord) like the reference;
     with return_aux also a dict of intermediates."""
@@ -458,7 +459,8 @@ def forward(sd, variant, template, online_template, search, run_score_head=False
     if variant == "asym_online" and run_score_head:
         Bh = t_all.shape[0] // 2
         templ = torch.cat([t_all[:Bh], t_all[Bh:]], dim=2)
-        gt = cxcywh_to_xyxy(coord.clone().view(-1, 4))
+        # forward_head, asymmetric_shared_online.py:405-410: the ROI is gt_bboxes when given
+        gt = cxcywh_to_xyxy(coord.clone().view(-1, 4)) if gt_bboxes is None else gt_bboxes.view(-1, 4).float()
         out["pred_scores"] = score_decoder(sd, "score_branch.", fused, templ, gt,
                                            num_heads=fused.shape[1] // 64).view(-1)
     if return_aux:

@@ -98,3 +98,17 @@ def test_synthetic_weights_are_deterministic():
     # pinned values: the generator must not drift between rounds / machines
     assert abs(float(synthetic.uniform("backbone.blocks.0.attn.qkv.weight", (3,))[0]) - float(
         synthetic.uniform("backbone.blocks.0.attn.qkv.weight", (5,))[0])) == 0.0
+
+
+def test_ce_partial_template_mask_raises():
+    """A CE template mask restricted to part of the template (CE_TEMPLATE_RANGE CTR_POINT) is refused
+    explicitly rather than ignored (the kernels average every template query's attention)."""
+    import pytest
+    import torch
+    from mmt_amd import model as M
+    net = M.build_asymmetric_shared_ce(M.hot_path_cfg(), train=False).eval()
+    mask = torch.zeros(1, 256, dtype=torch.bool)
+    mask[:, 27] = True
+    x = [torch.zeros(1, 3, 128, 128)] * 2
+    with pytest.raises(NotImplementedError):
+        net(x, x, [torch.zeros(1, 3, 320, 320)] * 2, ce_template_mask=mask, ce_keep_rate=0.7)

@@ -106,3 +106,23 @@ def test_prroi_backward_matches_oracle(B, C, H, W, ph, scale):
     print("prroi grad feat err %.3g roi err %.3g" % (ef, er))
     assert ef <= 1e-4 and er <= 1e-4, (ef, er)
     assert float(rc.grad[-1].abs().max()) == 0.0  # the zero-width ROI
+
+
+def test_prroi_backward_non_fp32_and_strided_inputs():
+    """Gradients reach leaves that are not fp32 / not contiguous (forward works on fp32 copies):
+    returned in the inputs' dtypes and equal to the fp32 path's."""
+    from mmt_amd.functional import prroi_pool2d
+    feats, rois = _prroi_case(2, 8, 12, 12)
+    g = torch.from_numpy(np.random.default_rng(3).standard_normal((rois.shape[0], 8, 4, 4)).astype(np.float32)).cuda()
+    f32 = torch.from_numpy(feats).cuda().requires_grad_(True)
+    r32 = torch.from_numpy(rois).cuda().requires_grad_(True)
+    prroi_pool2d(f32, r32, 4, 4, 1.0).backward(g)
+    f64 = torch.from_numpy(feats).double().cuda().requires_grad_(True)
+    base = torch.from_numpy(np.ascontiguousarray(feats.transpose(0, 1, 3, 2))).cuda()
+    ft = base.transpose(2, 3).requires_grad_(True)  # non-contiguous view
+    r64 = torch.from_numpy(rois).double().cuda().requires_grad_(True)
+    prroi_pool2d(f64, r64, 4, 4, 1.0).backward(g)
+    prroi_pool2d(ft, r32.detach(), 4, 4, 1.0).backward(g)
+    assert f64.grad is not None and f64.grad.dtype == torch.float64 and r64.grad.dtype == torch.float64
+    assert torch.allclose(f64.grad.float(), f32.grad, atol=1e-6) and torch.allclose(r64.grad.float(), r32.grad, atol=1e-5)
+    assert ft.grad is not None and torch.allclose(ft.grad, f32.grad, atol=1e-6)

@@ -138,3 +138,47 @@ def test_module_api_after_cuda(variant):
     assert coord.shape == (1, 1, 4)
     if score:
         assert out["pred_scores"].shape == (1,)
+
+
+def test_score_head_on_given_boxes_matches_oracle():
+    """asymmetric_shared_online.py:405-410: with run_score_head and gt_bboxes the score decoder pools
+    the given boxes (the actor's validation call), not the prediction; fp32 vs the oracle."""
+    from mmt_amd import synthetic
+    from oracle.forward import forward as oracle_forward
+    rt = _runtime("asym_online", torch.float32)
+    keys = json.load(open(GOLDEN + "/state_dict_asym_online.json"))
+    sd = {k: torch.from_numpy(v) for k, v in synthetic.synth_state_dict(keys).items()}
+    B = 2
+    t, o, s = synthetic.synth_inputs(B, seed=11)
+    gt = torch.tensor([[0.30, 0.35, 0.62, 0.70], [0.12, 0.20, 0.48, 0.41]])
+    rt.forward([x.cuda() for x in t], [x.cuda() for x in o], [x.cuda() for x in s], run_score_head=False)
+    sc = rt.score_on_boxes(B, gt.cuda()).cpu()
+    ref, _ = oracle_forward(sd, "asym_online", t, o, s, run_score_head=True, gt_bboxes=gt)
+    pred, _ = oracle_forward(sd, "asym_online", t, o, s, run_score_head=True)
+    err = (sc - ref["pred_scores"]).abs().max().item()
+    print("score on given boxes err %.3g (vs predicted-box score %.3g)" % (err, (ref["pred_scores"] - pred["pred_scores"]).abs().max()))
+    assert err <= 1e-3 * max(1.0, ref["pred_scores"].abs().max().item())
+
+
+def test_ce_keep_rate_argument():
+    """asymmetric_shared_ce.py:557-567 signature: ce_keep_rate >= 1 disables the elimination (the
+    result is the asymmetric model's), the configured rate gives the default forward; a template
+    mask over every token is accepted."""
+    from mmt_amd import model as M
+    from mmt_amd import synthetic
+    net = M.build_asymmetric_shared_ce(M.hot_path_cfg(), train=False)
+    keys = [(k, list(v.shape)) for k, v in net.state_dict().items()]
+    sd = {k: torch.from_numpy(v) for k, v in synthetic.synth_state_dict(keys).items()}
+    net.load_state_dict(sd, strict=True)
+    net = net.cuda().eval().set_compute_dtype(torch.float32)
+    asym = M.build_asymmetric_shared(M.hot_path_cfg(), train=False)
+    asym.load_state_dict(sd, strict=True)
+    asym = asym.cuda().eval().set_compute_dtype(torch.float32)
+    t, o, s = _inputs(1)
+    with torch.no_grad():
+        full, _ = net(t, o, s, False, None, torch.ones(1, 256, dtype=torch.bool), 1.0)
+        ref, _ = asym(t, o, s)
+        b_def, _ = net(t, o, s)
+        b_07, _ = net(t, o, s, ce_keep_rate=0.7)
+    assert (full["pred_boxes"] - ref["pred_boxes"]).abs().max().item() <= 1e-5
+    assert torch.equal(b_def["pred_boxes"], b_07["pred_boxes"])

@@ -263,3 +263,28 @@ def test_online_score_tracking_loop_matches_oracle(kv_cache):
             for m in range(2):
                 assert torch.equal(trk.core.online_template[m].cpu(), online[m])
     print("candidate crops taken:", took)
+
+
+def test_weights_reloaded_mid_sequence():
+    """The tracker's captured graphs point into the network's runtime: after load_state_dict mid
+    sequence the next frame must re-plan on the new weights (not replay against freed memory).
+    A tracker reloaded with weights W2 tracks exactly like a fresh tracker built on W2."""
+    from mmt_amd import synthetic
+    trk, sd = _tracker("rgbt", "mixformer_vit_rgbt")
+    frames, init = _seq(4)
+    keys = [(k, list(v.shape)) for k, v in sd.items()]
+    sd2 = {k: torch.from_numpy(v) for k, v in synthetic.synth_state_dict(keys, seed=5).items()}
+    trk.initialize(frames[0], {"init_bbox": [init, init]})
+    trk.track(frames[1], {})
+    state = list(trk.core.state.cpu().tolist())
+    trk.network.load_state_dict(sd2, strict=True)
+    trk.network.set_compute_dtype(torch.float32)
+    got = [trk.track(frames[f], {})["target_bbox"] for f in (2, 3)]
+    fresh, _ = _tracker("rgbt", "mixformer_vit_rgbt")
+    fresh.network.load_state_dict(sd2, strict=True)
+    fresh.network.set_compute_dtype(torch.float32)
+    fresh.initialize(frames[0], {"init_bbox": [init, init]})
+    fresh.core.state.copy_(torch.tensor(state, dtype=torch.float64))
+    ref = [fresh.track(frames[f], {})["target_bbox"] for f in (2, 3)]
+    for a, b in zip(got, ref):
+        assert max(abs(x - y) for x, y in zip(a, b)) <= 1e-6, (got, ref)

@@ -141,6 +141,11 @@ class _TorchBf16Ops:
         return TorchOps.mam_attention(qkv.float(), n_t, heads).bfloat16()
 
     @staticmethod
+    def mam_attention_asym(qkv, Bh, n_t, heads):
+        from mmt_amd.train import asym_attention_from_mam
+        return asym_attention_from_mam(_TorchBf16Ops.mam_attention, qkv, Bh, n_t, heads)
+
+    @staticmethod
     def ms_deform_attn(value, hw, loc, aw):
         import sys
         import os
@@ -248,3 +253,61 @@ def test_score_train_step_matches_oracle_grads():
     losses = [step(t, o, s, labels)["loss"].item() for _ in range(5)]
     print("score losses", stats["loss"].item(), losses)
     assert losses[-1] < stats["loss"].item()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["rgbt", "shared", "asym"])
+def test_module_forward_training_gpu_grads(variant):
+    """The drop-in module itself in train() mode (boundary b2: what the reference actor and DDP call,
+    actors/mixformer_rgbt.py:82-98): net(t, o, s, gt_bboxes=...) on the HIP ops (bf16) at the bench
+    shapes, B = 2.  Box loss within 2e-2 of the fp32 stand-in on the CPU, each parameter group's
+    gradient within max(5e-2, 1.5 x the PyTorch-bf16 path's distance from fp32) (relative L2)."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_train import TorchOps
+    import mmt_amd.model as M
+    from mmt_amd.train import box_loss, synthetic_batch
+    builders = {"rgbt": M.build_mixformer_vit_rgbt, "shared": M.build_mixformer_vit_rgbt_shared,
+                "asym": M.build_asymmetric_shared}
+    torch.manual_seed(0)
+    net = builders[variant](M.hot_path_cfg(), train=False)
+    with torch.no_grad():
+        for br in ("tl", "br"):
+            getattr(net.box_head, "conv5_" + br).weight.mul_(30.0)
+    net.train()
+    net.drop_path_rate = 0.0
+    for m in net.modules():
+        if isinstance(m, torch.nn.Dropout):
+            m.p = 0.0
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.eval()
+    t, o, s, gt = synthetic_batch(2, "cpu", torch.Generator().manual_seed(7))
+
+    def run(ops, dev):
+        net.zero_grad(set_to_none=True)
+        net.train_ops = ops
+        args = [[x.to(dev) for x in z] for z in (t, o, s)]
+        _, coord = net(*args, gt_bboxes=None)
+        loss, _ = box_loss(coord, gt.to(dev))
+        loss.backward()
+        return loss.item(), {n: p.grad.float().cpu().clone() for n, p in net.named_parameters() if p.grad is not None}
+
+    ref_loss, ref = run(TorchOps, "cpu")
+    net.cuda()
+    tb_loss, tb = run(_TorchBf16Ops, "cuda")
+    hip_loss, hip = run(None, "cuda")  # None = HipOps, the product path
+    print("%s loss hip %.5f torch-bf16 %.5f fp32 %.5f" % (variant, hip_loss, tb_loss, ref_loss))
+    assert abs(hip_loss - ref_loss) <= 2e-2
+    groups = ("backbone_v", "backbone_i", "fusion_vi", "box_head") if variant == "rgbt" else ("backbone", "fusion_vi", "box_head")
+    bad = []
+    for grp in groups:
+        names = [n for n in ref if n.startswith(grp + ".")]
+        r = torch.cat([ref[n].flatten() for n in names])
+        g = torch.cat([hip[n].flatten() for n in names])
+        b = torch.cat([tb[n].flatten() for n in names])
+        rel, rel_tb = ((g - r).norm() / r.norm()).item(), ((b - r).norm() / r.norm()).item()
+        print("%s %s grad rel L2: hip %.3g, torch-bf16 %.3g" % (variant, grp, rel, rel_tb))
+        if rel > max(5e-2, 1.5 * rel_tb):
+            bad.append((grp, rel, rel_tb))
+    assert not bad, bad

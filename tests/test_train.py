@@ -37,6 +37,11 @@ class TorchOps:
         return torch.cat([ot, os_], 2).transpose(1, 2).reshape(S, ntok, C)
 
     @staticmethod
+    def mam_attention_asym(qkv, Bh, n_t, heads):
+        from mmt_amd.train import asym_attention_from_mam
+        return asym_attention_from_mam(TorchOps.mam_attention, qkv, Bh, n_t, heads)
+
+    @staticmethod
     def ms_deform_attn(value, hw, loc, aw):
         return _msda_core(value, hw, loc, aw)
 
@@ -165,3 +170,120 @@ def test_ddp_gloo_two_ranks_matches_full_batch(tmp_path):
         assert (r0["grads"][n] - g).abs().max().item() <= 1e-4 * scale + 1e-6, n  # mean over ranks == batch mean
     for n in r0["params"]:
         assert torch.equal(r0["params"][n], r1["params"][n]), n  # replicas stay in lockstep
+
+
+# ----------------------------------------------------------------------------- module-level autograd
+BUILDERS = {"rgbt": "build_mixformer_vit_rgbt", "shared": "build_mixformer_vit_rgbt_shared", "asym": "build_asymmetric_shared"}
+
+
+def _train_net(variant, seed=0):
+    """The drop-in module in train() mode with the test's fp32 op stand-in; stochastic depth and
+    dropout off and BatchNorm on running statistics, so that the forward is deterministic."""
+    import mmt_amd.model as M
+    torch.manual_seed(seed)
+    net = getattr(M, BUILDERS[variant])(M.hot_path_cfg(search=SEARCH, template=TEMPLATE), train=False)
+    with torch.no_grad():
+        for br in ("tl", "br"):
+            getattr(net.box_head, "conv5_" + br).weight.mul_(30.0)
+    net.train()
+    net.train_ops = TorchOps
+    net.drop_path_rate = 0.0
+    for m in net.modules():
+        if isinstance(m, torch.nn.Dropout):
+            m.p = 0.0
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.eval()
+    return net
+
+
+@pytest.mark.parametrize("variant", ["rgbt", "shared", "asym"])
+def test_module_forward_autograd_matches_oracle(variant):
+    """net.train(); out, coord = net(t, o, s, gt_bboxes=...) builds the autograd graph (the reference
+    actor's call, actors/mixformer_rgbt.py:82-98): boxes and every parameter gradient of the box loss
+    equal autograd through the oracle's restatement of the same variant.  For the cross-modal variant
+    this also pins the training path's asymmetric attention (two standard attentions composed) against
+    the oracle's direct formula (asymmetric_shared.py:55-104)."""
+    from mmt_amd.train import box_loss
+    from oracle.forward import forward as oracle_forward
+    torch.set_num_threads(8)
+    net = _train_net(variant)
+    t, o, s, gt = _batch(2, 3)
+    gt_xyxy = torch.cat([gt[:, :2], gt[:, :2] + gt[:, 2:]], 1)
+    out, coord = net(t, o, s, run_score_head=False, gt_bboxes=gt_xyxy)
+    assert out["pred_boxes"] is coord and coord.requires_grad
+    loss, _ = box_loss(coord, gt)
+    loss.backward()
+    sd = {k: v.detach().clone() for k, v in net.state_dict().items()}
+    leaves = {k: sd[k].requires_grad_() for k, p in net.named_parameters() if p.requires_grad}
+    ref, _ = oracle_forward.__wrapped__(sd, variant, t, o, s)
+    ref_loss, _ = box_loss(ref["pred_boxes"], gt)
+    ref_loss.backward()
+    assert (coord - ref["pred_boxes"]).abs().max().item() < 1e-5
+    n = 0
+    for k, p in net.named_parameters():
+        if not p.requires_grad or leaves[k].grad is None:
+            continue
+        g, rg = p.grad, leaves[k].grad
+        assert g is not None, k
+        assert (g - rg).abs().max().item() <= 1e-3 * rg.abs().max().item() + 1e-6, k
+        n += 1
+    assert n > 100
+
+
+def test_module_forward_eval_still_refuses_cpu():
+    """Outside training (or with the product ops) the module has no CPU path."""
+    net = _train_net("rgbt").eval()
+    t, o, s, _ = _batch(1, 4)
+    with pytest.raises(RuntimeError):
+        net(t, o, s)
+    net.train()
+    net.train_ops = None
+    with pytest.raises(RuntimeError):
+        net(t, o, s)
+
+
+def _ddp_module_worker(rank, world, port, out_dir):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from mmt_amd.train import box_loss
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.set_num_threads(2)
+        net = _train_net("rgbt")
+        ddp = torch.nn.parallel.DistributedDataParallel(net)  # the reference's wrap, unchanged
+        t, o, s, gt = _batch(2, 5)
+        sl = slice(rank, rank + 1)
+        out, coord = ddp([x[sl] for x in t], [x[sl] for x in o], [x[sl] for x in s], gt_bboxes=None)
+        loss, _ = box_loss(coord, gt[sl])
+        loss.backward()
+        grads = {n: p.grad.clone() for n, p in net.named_parameters() if p.grad is not None}
+        torch.save({"grads": grads}, os.path.join(out_dir, "mrank%d.pt" % rank))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ddp_gloo_two_ranks_through_module_forward(tmp_path):
+    """DistributedDataParallel wraps the drop-in module itself (not a training wrapper): two gloo
+    ranks with one sample each all-reduce to the full-batch gradient of the module's own forward."""
+    import socket
+    import torch.multiprocessing as mp
+    from mmt_amd.train import box_loss
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    mp.spawn(_ddp_module_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    r0 = torch.load(tmp_path / "mrank0.pt", weights_only=True)["grads"]
+    r1 = torch.load(tmp_path / "mrank1.pt", weights_only=True)["grads"]
+    torch.set_num_threads(8)
+    net = _train_net("rgbt")
+    t, o, s, gt = _batch(2, 5)
+    _, coord = net(t, o, s)
+    loss, _ = box_loss(coord, gt)
+    loss.backward()
+    full = {n: p.grad for n, p in net.named_parameters() if p.grad is not None}
+    assert set(full) == set(r0) == set(r1)
+    for n, g in full.items():
+        assert torch.equal(r0[n], r1[n]), n
+        assert (r0[n] - g).abs().max().item() <= 1e-4 * (g.abs().max().item() + 1e-12) + 1e-6, n
