@@ -204,8 +204,26 @@ def kv_cache_tracking(rt, pool, score, steps, warmup):
                     "template update); not the headline `value`, which runs the full template+search forward"}
 
 
+def host_cpu():
+    """lscpu model / sockets / cores / SMT of the host the CPU baseline ran on."""
+    info = {}
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        keys = {"Model name": "model", "Socket(s)": "sockets", "Core(s) per socket": "cores_per_socket",
+                "Thread(s) per core": "threads_per_core", "CPU(s)": "logical_cpus"}
+        for ln in out.splitlines():
+            k, _, v = ln.partition(":")
+            if k.strip() in keys:
+                info[keys[k.strip()]] = v.strip()
+    except Exception:  # lscpu absent: report what the OS says
+        info["logical_cpus"] = str(os.cpu_count())
+    return info
+
+
 def cpu_baseline(variant, B, budget_s=12.0, geo=None):
-    """Oracle (fp32 CPU restatement of the reference forward), bounded sample."""
+    """Oracle (fp32 CPU restatement of the reference forward; within +-15 % of the reference's own
+    CPU time on the same threads, tools/cpu_baseline_check.py -> profiles/cpu_baseline_check.json):
+    3 warm-up forwards, then the median of >= 10 timed forwards or as many as fit the budget."""
     geo = geo or GEO_B
     from mmt_amd import synthetic
     from oracle.forward import forward as oracle_forward, state_dict_to_torch
@@ -213,17 +231,20 @@ def cpu_baseline(variant, B, budget_s=12.0, geo=None):
     torch.set_num_threads(threads)
     sd = state_dict_to_torch(synthetic.synth_state_dict(state_dict_keys(variant, **geo)))
     t, o, s = synthetic.synth_inputs(B, geo["template"], geo["search"])
-    oracle_forward(sd, variant, t, o, s)
-    n, t0 = 0, time.perf_counter()
-    while n < 3 or time.perf_counter() - t0 < budget_s:
+    for _ in range(3):
         oracle_forward(sd, variant, t, o, s)
-        n += 1
-        if n >= 200:
+    times, t0 = [], time.perf_counter()
+    while len(times) < 10 or time.perf_counter() - t0 < budget_s:
+        t1 = time.perf_counter()
+        oracle_forward(sd, variant, t, o, s)
+        times.append(time.perf_counter() - t1)
+        if len(times) >= 200 or (len(times) >= 3 and time.perf_counter() - t0 > 4 * budget_s):
             break
-    dt = time.perf_counter() - t0
-    return {"value": round(n * B / dt, 3), "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": "%d fp32 CPU forwards of B=%d (%s, %d/%d), %.1f s, oracle/forward.py"
-                      % (n, B, variant, geo["template"], geo["search"], dt)}
+    med = sorted(times)[len(times) // 2]
+    return {"value": round(B / med, 3), "unit": "frames/s", "cores": threads, "kind": "port",
+            "host": host_cpu(),
+            "sample": "median of %d fp32 CPU forwards of B=%d after 3 warm-up (%s, %d/%d), %.1f s, oracle/forward.py"
+                      % (len(times), B, variant, geo["template"], geo["search"], sum(times))}
 
 
 def timed_steps(step, steps, world, sync, device):
