@@ -1331,510 +1331,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Whole-sequence kernel (impl 20; the default for large grids at the ViT-B shapes).  The kernels
-// above give a (sequence, head) 4-5 workgroups, each streaming the whole key range through its
-// own LDS ring: at batch 32 that is 1.77 MB of L2 -> LDS traffic per CU, and the DMA alone (no
-// matrix work) measured 41 us of the 86 us launch.  Here ONE workgroup of 8 waves owns every
-// query of a (sequence, head), so its keys and values cross L2 -> LDS exactly once:
-//   - the key stream ([0, Lk), 64-key tiles) is DMA'd into a 9-slot LDS ring (144 KiB, one
-//     workgroup per CU; the two-stream / shared key range, 9 tiles, is resident at once), 2 pieces
-//     per wave per tile, one barrier per tile;
-//   - the queries are cut into 32-column blocks (13 search + 4 template at 528 tokens) and each
-//     wave holds two blocks' Q / O / row-sum state, sharing every K and V^T fragment it reads
-//     between the two (half the LDS reads per FLOP of a one-block wave, two independent MFMA
-//     chains): waves 0-5 search blocks (2w, 2w+1), wave 6 (S12, T0), wave 7 (T1, T2) and then T3,
-//     which it runs "deferred" two tiles later on the template tiles still in the ring (the ring
-//     refill lags the consumer by 1 + n_t/64 tiles so that those slots are kept);
-//   - per block the arithmetic is that of mam_attention_lz_kernel (32x32x16 MFMAs, exp2 with no
-//     reference point and the range-checked exact fallback, row sums from the selector MFMA).
-// Waves w and w+4 share a SIMD (the dispatcher deals a workgroup's waves 0 -> 2 -> 1 -> 3), so the
-// busiest SIMD carries 4 search blocks: 87 % balance at 17 blocks.  Template queries of the
-// cross-modal variant read their own template keys, tiles [n_t/64, 2 n_t/64) of the I stream.
-constexpr int WS_NSLOT = 9;
-
-#if MMT_STAMP_BUILD
-// stamp build: per workgroup, waves 0 and 4 (one SIMD's pair) record [realtime start, memtime start,
-// after the first barrier, after each of the first 12 tiles ..., memtime end, realtime end]
-__device__ unsigned long long g_mmt_ws_stamps[4096 * 2 * 16];
-extern "C" int mmt_ws_stamps(unsigned long long* host, int n) {
-    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_mmt_ws_stamps), sizeof(unsigned long long) * n);
-}
-#define MMT_WSTAMP(I, INSN)                                                                          \
-    if ((threadIdx.x & 255) == 0 && (blockIdx.x + gridDim.x * blockIdx.y) < 4096) {                 \
-        unsigned long long t_;                                                                      \
-        asm volatile(INSN " %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                      \
-        g_mmt_ws_stamps[((blockIdx.x + gridDim.x * blockIdx.y) * 2 + (threadIdx.x >> 8)) * 16 + (I)] = t_; \
-    }
-#else
-#define MMT_WSTAMP(I, INSN)
-#endif
-
-struct ws_blk {
-    int q0, nq, lo, hi;  // query rows [q0, q0 + nq), key tiles [lo, hi) of the stream
-};
-
-// G = key tiles per barrier (the waves run free between barriers; G must not exceed WS_NSLOT - 1 -
-// n_t/64 when the stream is longer than the ring)
-// Exact two-pass fp32 softmax for the 32 queries [q0, q0 + nq) of (sequence s, head h) over the keys
-// [k_lo, k_hi) of s's stream (the whole-sequence kernel's range-check fallback; rare, run after the
-// pair loop so that its registers stay out of the loop's).  Lane (query l%32, half hf) owns d = 32hf .. 32hf+31
-// of the dot products and of O; K / V come straight from global memory.
-MMT_DEV void ws_exact(const mmt_attn_params& p, int s, int h, int q0, int nq, int k_lo, int k_hi) {
-    const int lane = threadIdx.x & 63, l32 = lane & 31, hf = lane >> 5;
-    const int n_t = p.n_t, ntok = p.ntok, C = p.C;
-    const int64_t pitch = p.tok_pitch > 0 ? p.tok_pitch : ntok, rs = 3 * (int64_t)C;
-    const bf16_t* qkv = (const bf16_t*)p.qkv;
-    const float cexp = p.scale * 1.4426950408889634f;
-    auto key_row = [&](int kk) -> const bf16_t* {
-        int seq = s, row = kk;
-        if (p.asym) {
-            const int v = s % p.Bm;
-            if (kk < n_t) seq = v;
-            else if (kk < 2 * n_t) { seq = v + p.Bm; row = kk - n_t; }
-            else row = kk - n_t;
-        }
-        return qkv + ((int64_t)seq * pitch + row) * rs;
-    };
-    const int q = q0 + l32;
-    bf16_t* op = (bf16_t*)p.out + ((int64_t)s * pitch + q) * C + h * D;
-    float qv[32], acc[32];
-    {
-        const bf16_t* qp = qkv + ((int64_t)s * pitch + q0 + min(l32, nq - 1)) * rs + h * D + 32 * hf;
-#pragma unroll
-        for (int i = 0; i < 32; ++i) qv[i] = bf2f(qp[i]) * cexp;
-    }
-    auto score = [&](int kk) {
-        const bf16_t* kp = key_row(kk) + C + h * D + 32 * hf;
-        float d0 = 0.f;
-#pragma unroll
-        for (int i = 0; i < 32; ++i) d0 += qv[i] * bf2f(kp[i]);
-        return d0 + __shfl_xor(d0, 32, 64);
-    };
-    float m = -INFINITY;
-    for (int kk = k_lo; kk < k_hi; ++kk) m = fmaxf(m, score(kk));
-    float lf = 0.f;
-#pragma unroll
-    for (int i = 0; i < 32; ++i) acc[i] = 0.f;
-    for (int kk = k_lo; kk < k_hi; ++kk) {
-        const float e = __builtin_amdgcn_exp2f(score(kk) - m);
-        lf += e;
-        const bf16_t* vp = key_row(kk) + 2 * C + h * D + 32 * hf;
-#pragma unroll
-        for (int i = 0; i < 32; ++i) acc[i] += e * bf2f(vp[i]);
-    }
-    if (l32 < nq) {
-        const float inv = 1.f / lf;
-        if (p.lse && hf == 0) p.lse[((int64_t)s * p.H + h) * ntok + q] = m + __builtin_amdgcn_logf(lf);
-#pragma unroll
-        for (int i = 0; i < 32; i += 8)
-            *(u32x4*)(op + 32 * hf + i) =
-                u32x4{pack_bf16x2(acc[i] * inv, acc[i + 1] * inv), pack_bf16x2(acc[i + 2] * inv, acc[i + 3] * inv),
-                      pack_bf16x2(acc[i + 4] * inv, acc[i + 5] * inv), pack_bf16x2(acc[i + 6] * inv, acc[i + 7] * inv)};
-    }
-}
-
-// NW = waves per workgroup: 8 (two query blocks per wave, as described above) or 16 (one block per
-// wave, 4 waves per SIMD: waves 0-12 the search blocks, 13-14 T0-T1, 15 T2 then T3 deferred).
-// PERSIST: a grid of one workgroup per CU walks the (sequence, head) pairs blockIdx.x, + gridDim.x,
-// ...; the K / V tile stream runs on across the pairs, so the next pair's first tiles land during
-// the current pair's last ones (otherwise every workgroup's first K / V tiles, ~10 us at batch 32,
-// are exposed: one 144 KiB workgroup per CU leaves no other workgroup to overlap them with).
-template <int G, int NW, bool PERSIST>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4, NW / 4))) void mam_attention_ws_kernel(
-    const mmt_attn_params p) {
-    constexpr int PPW = 16 / NW;  // DMA pieces per wave per tile
-    MMT_WSTAMP(0, "s_memrealtime");
-    MMT_WSTAMP(1, "s_memtime");
-    __shared__ __attribute__((aligned(1024))) char lds[WS_NSLOT * FTILE];
-
-    const int n_t = p.n_t, ntok = p.ntok, C = p.C, ns = ntok - n_t;
-    const int64_t pitch = p.tok_pitch > 0 ? p.tok_pitch : ntok;  // rows between sequences
-    const int64_t rs = 3 * (int64_t)C;
-    const bf16_t* qkv = (const bf16_t*)p.qkv;
-    const bool cross = p.asym;
-    const int Lk = p.asym ? ntok + n_t : ntok;  // the search key stream
-    const int nkt = (Lk + KB - 1) / KB;
-    const int ntt = n_t / KB;  // template tiles
-    // this workgroup's pairs (pair = h + H * s): pr0, pr0 + pstep, ... (np_loc of them)
-    const int npairs = p.H * p.S;
-    const int pr0 = PERSIST ? (int)blockIdx.x : (int)(blockIdx.x + gridDim.x * blockIdx.y);
-    const int pstep = PERSIST ? (int)gridDim.x : npairs;
-    const int np_loc = (npairs - pr0 + pstep - 1) / pstep;
-    const int total = np_loc * nkt;  // tiles in this workgroup's stream
-    int h = pr0 % p.H, s = pr0 / p.H, sV = s % p.Bm, sI = sV + p.Bm;
-    int ta = (p.asym && s >= p.Bm) ? ntt : 0;  // first tile of this sequence's own template keys
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int l32 = lane & 31, hf = lane >> 5;
-    const int prow = lane >> 3, pcol = lane & 7;
-
-    // ---- this wave's query blocks
-    auto sblk = [&](int j) {
-        const int nq = max(0, min(32, ns - 32 * j));
-        return ws_blk{n_t + 32 * j, nq, 0, nq ? nkt : 0};
-    };
-    auto tblk = [&](int j) {
-        const int nq = p.q_part == 2 ? 0 : max(0, min(32, n_t - 32 * j));
-        return ws_blk{32 * j, nq, ta, nq ? ta + ntt : 0};
-    };
-    ws_blk b0, b1, bd;
-    auto plan = [&]() {
-        b1 = bd = ws_blk{0, 0, 0, 0};
-        if constexpr (NW == 8) {
-            if (w < 6) { b0 = sblk(2 * w); b1 = sblk(2 * w + 1); }
-            else if (w == 6) { b0 = sblk(12); b1 = tblk(0); }
-            else { b0 = tblk(1); b1 = tblk(2); bd = tblk(3); }
-        } else {
-            if (w < 13) b0 = sblk(w);
-            else if (w < 15) b0 = tblk(w - 13);
-            else { b0 = tblk(2); bd = tblk(3); }
-        }
-        if (!b0.nq) { b0 = b1; b1 = ws_blk{0, 0, 0, 0}; }  // a lone block lives in slot 0
-        if (!b0.nq) { b0 = bd; bd = ws_blk{0, 0, 0, 0}; }
-    };
-    plan();
-    int d0 = 0;  // slot 0 runs d0 tiles behind the stream (the deferred template block)
-
-    // ---- K / V DMA: tile t into slot t % WS_NSLOT; the first half of the waves the K image, the
-    // second half the V image, PPW pieces (8 rows x 128 B) each
-    const int isv = w / (NW / 2);
-    const int64_t col = (isv ? 2 * C : C) + (isv ? (pcol ^ attn_vswz(prow)) : (pcol ^ prow)) * 8;
-    auto key_row_of = [&](int seq_s, int kk) -> const bf16_t* {  // key kk of sequence seq_s's stream
-        int seq = seq_s, row = kk;
-        if (cross) {
-            const int v = seq_s % p.Bm;
-            if (kk < n_t) seq = v;
-            else if (kk < 2 * n_t) { seq = v + p.Bm; row = kk - n_t; }
-            else row = kk - n_t;
-        }
-        return qkv + ((int64_t)seq * pitch + row) * rs;
-    };
-    auto key_row = [&](int kk) { return key_row_of(s, kk); };
-    // stream tile u: tile u % nkt of this workgroup's pair u / nkt, into slot u % WS_NSLOT
-    auto issue_tile = [&](int u) {
-        const int pr = pr0 + (u / nkt) * pstep, t = u % nkt;
-        const int us = pr / p.H, uh = pr % p.H;
-        char* slot = lds + (u % WS_NSLOT) * FTILE + isv * KB * 128;
-        if (t * KB + KB <= Lk) {  // n_t % 64 == 0: a full tile lies in one key segment
-            const bf16_t* base = key_row_of(us, t * KB) + uh * D;
-#pragma unroll
-            for (int i = 0; i < PPW; ++i) {
-                const int pk = (w % (NW / 2)) * PPW + i;
-                attn_glds16(base + (int64_t)(pk * 8 + prow) * rs + col, slot + pk * 1024);
-            }
-        } else {
-#pragma unroll
-            for (int i = 0; i < PPW; ++i) {
-                const int pk = (w % (NW / 2)) * PPW + i;
-                attn_glds16(key_row_of(us, min(t * KB + pk * 8 + prow, Lk - 1)) + uh * D + col, slot + pk * 1024);
-            }
-        }
-    };
-
-    const float cexp = p.scale * 1.4426950408889634f;
-    const bool prescale = fabsf(cexp - 1.f) > 1e-6f;
-    // B operand of S^T = K Q^T: query q0 + l32 (clamped), loaded by inline asm (invisible to hipcc's
-    // wait-count tracking, which would otherwise wait for vmcnt(0) behind the K / V DMA issued next);
-    // the explicit wait below covers them
-    auto load_q = [&](const ws_blk& b, u32x4* qf) {
-        const bf16_t* qp = qkv + ((int64_t)s * pitch + b.q0 + min(l32, max(b.nq, 1) - 1)) * rs + h * D + 8 * hf;
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qf[ks]) : "v"(qp + 16 * ks) : "memory");
-    };
-    auto scale_q = [&](u32x4* qf) {
-        if (prescale) {  // natural-scale q (training / A/B callers): to log2 units
-#pragma unroll
-            for (int ks = 0; ks < 4; ++ks) {
-                u32x4 v = qf[ks];
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    v[e] = pack_bf16x2(__uint_as_float(v[e] << 16) * cexp, __uint_as_float(v[e] & 0xffff0000u) * cexp);
-                qf[ks] = v;
-            }
-        }
-    };
-    // every Q this wave will use is loaded (and waited for) here: a global load consumed inside
-    // the tile loop would make hipcc wait for vmcnt(0), i.e. for the whole in-flight K / V ring
-    u32x4 qf0[4], qf1[4], qfd[4];
-    load_q(b0, qf0);
-    if constexpr (NW == 8) load_q(b1, qf1);
-    load_q(bd, qfd);
-#pragma unroll
-    for (int t = 0; t < WS_NSLOT; ++t) issue_tile(t);  // the launcher guarantees nkt >= WS_NSLOT
-    int issued = WS_NSLOT;
-    // the Q loads are older than the PPW * WS_NSLOT DMA pieces: wait for them only
-    if constexpr (NW == 8) {
-        asm volatile("s_waitcnt vmcnt(%12)"
-                     : "+v"(qf0[0]), "+v"(qf0[1]), "+v"(qf0[2]), "+v"(qf0[3]), "+v"(qf1[0]), "+v"(qf1[1]), "+v"(qf1[2]),
-                       "+v"(qf1[3]), "+v"(qfd[0]), "+v"(qfd[1]), "+v"(qfd[2]), "+v"(qfd[3])
-                     : "n"(PPW * WS_NSLOT)
-                     : "memory");
-        scale_q(qf1);
-    } else {
-        asm volatile("s_waitcnt vmcnt(%8)"
-                     : "+v"(qf0[0]), "+v"(qf0[1]), "+v"(qf0[2]), "+v"(qf0[3]), "+v"(qfd[0]), "+v"(qfd[1]), "+v"(qfd[2]),
-                       "+v"(qfd[3])
-                     : "n"(PPW * WS_NSLOT)
-                     : "memory");
-    }
-    scale_q(qf0);
-    scale_q(qfd);
-    const int lag = 1 + ntt;  // ring slots stay readable this many tiles behind the stream
-
-    f32x16 o0[2], o1[2];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { o0[0][r] = o0[1][r] = o1[0][r] = o1[1][r] = 0.f; }
-    f32x4 la0 = f32x4{0.f, 0.f, 0.f, 0.f}, la1 = la0;  // row sums: every element = this lane's query
-    const float one_or_zero = (((lane & 15) >> 2) & 1) == ((lane >> 4) & 1) ? 1.f : 0.f;
-    const uint32_t sel_w = pack_bf16x2(one_or_zero, one_or_zero);
-    const bf16x8 sel = __builtin_bit_cast(bf16x8, u32x4{sel_w, sel_w, sel_w, sel_w});
-    const int kpos = (l32 & 7) * 16;
-    const int li = lane & 15, qr = li >> 2, pc = li & 3, dsub = (lane >> 4) & 1;
-
-    // one 32-key block kb of a tile for NB (1: slot 0; 2: slots 0 and 1) query blocks; NJ 16-key
-    // steps; MASK = zero P past the nv valid keys of the tile
-    // K fragments of the next 32-key block are read during this block's exponentials (kfp), so
-    // only the first block of a tile waits for its K reads
-    u32x4 kfp[4];
-    auto read_k = [&](const char* kimg, int kb) {
-        const char* krow = kimg + (32 * kb + l32) * 128;
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) kfp[ks] = *(const u32x4*)(krow + ((((2 * ks + hf) * 16) ^ kpos)));
-    };
-    // one 32-key block kb of a tile for NB (1: slot 0; 2: slots 0 and 1) query blocks; NJ 16-key
-    // steps; MASK = zero P past the nv valid keys of the tile; PRE = read the K fragments of block 1
-    // of the same tile behind this block's exponentials
-    auto sub = [&](const char* kimg, int kb, int nv, auto NJc, auto MASKc, auto NBc, auto PREc) {
-        constexpr int NJ = decltype(NJc)::value;
-        constexpr bool MASK = decltype(MASKc)::value;
-        constexpr int NB = decltype(NBc)::value;
-        constexpr bool PRE = decltype(PREc)::value;
-        const char* vimg = kimg + KB * 128;
-        __builtin_amdgcn_sched_barrier(0);  // one 32-key block at a time: bounds the live registers
-        // V^T fragments first: their LDS latency hides behind the QK^T MFMAs
-        uint2 vt[NJ][2][2];
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const int row = 32 * kb + 16 * j + 4 * hf + qr;
-#pragma unroll
-            for (int db = 0; db < 2; ++db) {
-                const char* b1 = vimg + row * 128 + (((4 * db + 2 * dsub + (pc >> 1)) ^ attn_vswz(row)) * 16) + (pc & 1) * 8;
-                vt[j][db][0] = attn_tr16<0>(b1);
-                vt[j][db][1] = attn_tr16<8 * 128>(b1);
-            }
-        }
-        f32x16 sa[NB];
-#pragma unroll
-        for (int b = 0; b < NB; ++b) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) sa[b][r] = 0.f;
-#pragma unroll
-            for (int ks = 0; ks < 4; ++ks)
-                sa[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kfp[ks]),
-                                                               __builtin_bit_cast(bf16x8, b ? qf1[ks] : qf0[ks]), sa[b], 0, 0, 0);
-        }
-        if constexpr (PRE) read_k(kimg, kb + 1);
-#pragma unroll
-        for (int b = 0; b < NB; ++b)
-#pragma unroll
-            for (int r = 0; r < 8 * NJ; ++r) {
-                float e = MMT_ATTN_ABLATE >= 3 ? sa[b][r] : __builtin_amdgcn_exp2f(sa[b][r]);
-                if constexpr (MASK) {
-                    if (32 * kb + 8 * (r >> 2) + 4 * hf + (r & 3) >= nv) e = 0.f;
-                }
-                sa[b][r] = e;
-            }
-        // the V^T reads have landed once at most the PRE K reads (issued after them) are pending
-        if constexpr (PRE) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const int rb = 8 * j;
-#pragma unroll
-            for (int b = 0; b < NB; ++b) {
-                const bf16x8 pf = MMT_ATTN_ABLATE == 4
-                    ? __builtin_bit_cast(bf16x8, u32x4{__float_as_uint(sa[b][rb]), __float_as_uint(sa[b][rb + 2]),
-                                                       __float_as_uint(sa[b][rb + 4]), __float_as_uint(sa[b][rb + 6])})
-                    : __builtin_bit_cast(
-                    bf16x8, u32x4{pack_bf16x2(sa[b][rb], sa[b][rb + 1]), pack_bf16x2(sa[b][rb + 2], sa[b][rb + 3]),
-                                  pack_bf16x2(sa[b][rb + 4], sa[b][rb + 5]), pack_bf16x2(sa[b][rb + 6], sa[b][rb + 7])});
-#pragma unroll
-                for (int db = 0; db < 2; ++db) {
-                    const uint2 ua = vt[j][db][0], ub = vt[j][db][1];
-                    const bf16x8 vf = __builtin_bit_cast(bf16x8, make_uint4(ua.x, ua.y, ub.x, ub.y));
-                    if (b) o1[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o1[db], 0, 0, 0);
-                    else o0[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o0[db], 0, 0, 0);
-                }
-                if (b) la1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pf, la1, 0, 0, 0);
-                else la0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pf, la0, 0, 0, 0);
-            }
-        }
-    };
-    auto tile = [&](const char* kimg, int nv, auto NBc) {
-        read_k(kimg, 0);
-        if (nv == KB) {
-            sub(kimg, 0, nv, attn_ic<2>{}, attn_ic<0>{}, NBc, attn_ic<1>{});
-            sub(kimg, 1, nv, attn_ic<2>{}, attn_ic<0>{}, NBc, attn_ic<0>{});
-        } else {  // the stream's tail tile: only the 16-key steps that hold valid keys
-            if (nv > 32) {
-                sub(kimg, 0, nv, attn_ic<2>{}, attn_ic<1>{}, NBc, attn_ic<1>{});
-                if (nv > 48) sub(kimg, 1, nv, attn_ic<2>{}, attn_ic<1>{}, NBc, attn_ic<0>{});
-                else sub(kimg, 1, nv, attn_ic<1>{}, attn_ic<1>{}, NBc, attn_ic<0>{});
-            } else if (nv > 16) sub(kimg, 0, nv, attn_ic<2>{}, attn_ic<1>{}, NBc, attn_ic<0>{});
-            else sub(kimg, 0, nv, attn_ic<1>{}, attn_ic<1>{}, NBc, attn_ic<0>{});
-        }
-    };
-
-    // normalise and store one block; false = the range check failed (the block is redone exactly
-    // after the loop, when the registers are free)
-    auto finish = [&](const ws_blk& b, f32x16* o, f32x4 la) -> bool {
-        const float l = la[0];
-        float chk = 0.f;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) chk += o[0][r] * 0.f + o[1][r] * 0.f;
-        const bool ok = (l >= LZ_LO && l <= LZ_HI && chk == 0.f) || MMT_ATTN_ABLATE != 0;
-        if (!__all(ok)) return false;
-        const int q = b.q0 + l32;
-        bf16_t* op = (bf16_t*)p.out + ((int64_t)s * pitch + q) * C + h * D;
-        const float inv = 1.f / l;
-        if (l32 < b.nq) {
-            if (p.lse && hf == 0) p.lse[((int64_t)s * p.H + h) * ntok + q] = __builtin_amdgcn_logf(l);
-#pragma unroll
-            for (int db = 0; db < 2; ++db)
-#pragma unroll
-                for (int g = 0; g < 4; ++g)
-                    *(uint2*)(op + 32 * db + 8 * g + 4 * hf) =
-                        make_uint2(pack_bf16x2(o[db][4 * g] * inv, o[db][4 * g + 1] * inv),
-                                   pack_bf16x2(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv));
-        }
-        return true;
-    };
-    auto exact = [&](const ws_blk& b) { ws_exact(p, s, h, b.q0, b.nq, b.lo * KB, min(b.hi * KB, Lk)); };
-
-    // at stream tiles u = 0, G, 2G, ...: every wave's pieces of tiles [u, u + G) landed (this wave:
-    // counted vmcnt; all waves: the barrier), every wave is done with the tiles before u; refill
-    auto sync = [&](int u) {
-        if (u % G) return;
-        attn_wait_dyn(PPW * (issued - min(u + G, issued)));
-        lds_barrier();
-        if (MMT_ATTN_ABLATE != 1)
-            while (issued < total && issued < u - lag + WS_NSLOT) issue_tile(issued++);
-    };
-    const int nfull = Lk / KB;  // full tiles; the stream's last Lk % 64 keys form a tail tile
-    uint64_t redo_all = 0;      // 3 bits per pair: blocks that need the exact path
-    for (int k = 0; k < np_loc; ++k) {
-        const int u0 = k * nkt;  // this pair's first stream tile
-        if (k > 0) {  // next pair: its (sequence, head), block plan and Q
-            const int pr = pr0 + k * pstep;
-            h = pr % p.H;
-            s = pr / p.H;
-            sV = s % p.Bm;
-            sI = sV + p.Bm;
-            ta = (p.asym && s >= p.Bm) ? ntt : 0;
-            plan();
-            d0 = 0;
-            sync(u0);
-            load_q(b0, qf0);
-            if constexpr (NW == 8) load_q(b1, qf1);
-            load_q(bd, qfd);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // only the Q loads and older DMA pieces
-            scale_q(qf0);
-            if constexpr (NW == 8) scale_q(qf1);
-            scale_q(qfd);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) { o0[0][r] = o0[1][r] = o1[0][r] = o1[1][r] = 0.f; }
-            la0 = la1 = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-        int redo = 0;  // bit i: block i of the pair's plan {b0, b1, bd} needs the exact path
-        for (int t = 0; t < nfull; ++t) {
-            if (k == 0 || t > 0) sync(u0 + t);
-            if (k == 0 && t == 0) MMT_WSTAMP(2, "s_memtime");
-            if (MMT_ATTN_ABLATE == 2) continue;
-            const int t0 = t - d0;
-            const bool a0 = b0.nq && t0 >= b0.lo && t0 < b0.hi;
-            const bool a1 = NW == 8 && b1.nq && t >= b1.lo && t < b1.hi;
-            if (NW == 8 && a0 && a1) {  // d0 == 0 whenever both slots are live
-                const char* kimg = lds + ((u0 + t) % WS_NSLOT) * FTILE;
-                read_k(kimg, 0);
-                sub(kimg, 0, KB, attn_ic<2>{}, attn_ic<0>{}, attn_ic<2>{}, attn_ic<1>{});
-                sub(kimg, 1, KB, attn_ic<2>{}, attn_ic<0>{}, attn_ic<2>{}, attn_ic<0>{});
-            } else if (a0) {
-                const char* kimg = lds + ((u0 + t0) % WS_NSLOT) * FTILE;
-                read_k(kimg, 0);
-                sub(kimg, 0, KB, attn_ic<2>{}, attn_ic<0>{}, attn_ic<1>{}, attn_ic<1>{});
-                sub(kimg, 1, KB, attn_ic<2>{}, attn_ic<0>{}, attn_ic<1>{}, attn_ic<0>{});
-            }
-            // template blocks end inside the stream; the search blocks end after the tail below
-            if (a0 && b0.hi < nkt && t0 == b0.hi - 1) {
-                if (!finish(b0, o0, la0)) redo |= d0 ? 4 : 1;
-                if (bd.nq) {  // slot 0 takes the deferred block: the same tiles, b0.hi - bd.lo tiles later
-                    d0 = b0.hi - bd.lo;
-                    b0 = bd;
-                    bd = ws_blk{0, 0, 0, 0};
-#pragma unroll
-                    for (int ks = 0; ks < 4; ++ks) qf0[ks] = qfd[ks];
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) o0[0][r] = o0[1][r] = 0.f;
-                    la0 = f32x4{0.f, 0.f, 0.f, 0.f};
-                }
-            }
-            if constexpr (NW == 8)
-                if (a1 && b1.hi < nkt && t == b1.hi - 1 && !finish(b1, o1, la1)) redo |= 2;
-            if (k == 0 && t < 11) MMT_WSTAMP(3 + t, "s_memtime");
-        }
-        if (nfull < nkt) {  // the tail tile: only the 16-key steps that hold valid keys
-            sync(u0 + nfull);
-            const int nv = Lk - nfull * KB;
-            const char* kimg = lds + ((u0 + nfull) % WS_NSLOT) * FTILE;
-            const bool a0 = b0.nq && b0.hi == nkt, a1 = NW == 8 && b1.nq && b1.hi == nkt;  // d0 == 0 here
-            if (NW == 8 && MMT_ATTN_ABLATE != 2 && a0 && a1) tile(kimg, nv, attn_ic<2>{});
-            else if (MMT_ATTN_ABLATE != 2 && a0) tile(kimg, nv, attn_ic<1>{});
-        }
-        if (b0.nq && b0.hi == nkt && !finish(b0, o0, la0)) redo |= 1;
-        if constexpr (NW == 8)
-            if (b1.nq && b1.hi == nkt && !finish(b1, o1, la1)) redo |= 2;
-        redo_all |= (uint64_t)redo << (3 * k);
-    }
-    if (__builtin_expect(redo_all != 0, 0)) {  // the launcher keeps np_loc <= 21
-        for (int k = 0; k < np_loc; ++k) {
-            const int m = (int)(redo_all >> (3 * k)) & 7;
-            if (!m) continue;
-            const int pr = pr0 + k * pstep;
-            h = pr % p.H;
-            s = pr / p.H;
-            ta = (p.asym && s >= p.Bm) ? ntt : 0;
-            plan();
-            if (m & 1) exact(b0);
-            if (m & 2) exact(b1);
-            if (m & 4) exact(bd);
-        }
-    }
-#if MMT_STAMP_BUILD
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-    MMT_WSTAMP(14, "s_memtime");
-    MMT_WSTAMP(15, "s_memrealtime");
-}
-
-// compute units of the current device (the persistent kernel's grid), queried once per device
-int attn_cu_count() {
-    static int cache[64] = {0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    if (!cache[dev]) {
-        int n = 0;
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-        cache[dev] = n;
-    }
-    return cache[dev];
-}
-
 template <typename T>
 int launch_attn(const mmt_attn_params& p, hipStream_t st) {
-    if (p.impl != 0 && p.impl != 2 && p.impl != 4 && (p.impl < 8 || p.impl > 12) && (p.impl < 16 || p.impl > 25))
+    if (p.impl != 0 && p.impl != 2 && p.impl != 4 && (p.impl < 8 || p.impl > 12) && (p.impl < 16 || p.impl > 19))
         return MMT_EBADARG;
     if (p.lse && (sizeof(T) != 2 || p.impl == 9 || (p.impl > 9 && p.impl < 16))) return MMT_EBADARG;
     if (!p.qkv || !p.out || p.H <= 0 || p.C != p.H * D || p.S <= 0 || p.ntok <= p.n_t || p.n_t <= 0) return MMT_EBADARG;
@@ -1854,32 +1353,6 @@ int launch_attn(const mmt_attn_params& p, hipStream_t st) {
         // small grids (batch-1 tracking): the latency kernel (64 queries x KG key groups)
         const int nfa = qblocks(FQ);
         const dim3 fgrid(nfa, p.H, p.S);
-        // whole-sequence kernel: n_t % 64 == 0, n_t <= 128, <= 13 search blocks of 32, all queries
-        const int lk_s = p.asym ? p.ntok + p.n_t : p.ntok;
-        const bool ws_ok = p.n_t % KB == 0 && p.n_t <= 128 && p.ntok - p.n_t <= 13 * 32 && p.q_part != 1 &&
-                           lk_s > (WS_NSLOT - 1) * KB;
-        if (p.impl >= 20 && ws_ok) {  // 20 / 21 / 22: a barrier every 1 / 3 / 9 key tiles (9: whole
-                                      // stream resident, else 3)
-            const int nkt_s = (lk_s + KB - 1) / KB;
-            const dim3 g2(p.H, p.S);
-            if (p.impl >= 24 && p.H * p.S <= 21 * attn_cu_count()) {  // persistent: 24 / 25 = a barrier
-                // every 3 / 6 tiles (<= WS_NSLOT - 1 - n_t/64); at most 21 pairs per workgroup
-                const dim3 gp(min(p.H * p.S, attn_cu_count()));
-                if (p.impl == 24 || p.n_t / KB > 2) hipLaunchKernelGGL((mam_attention_ws_kernel<3, 8, true>), gp, dim3(512), 0, st, p);
-                else hipLaunchKernelGGL((mam_attention_ws_kernel<6, 8, true>), gp, dim3(512), 0, st, p);
-            } else if (p.impl == 20) hipLaunchKernelGGL((mam_attention_ws_kernel<1, 8, false>), g2, dim3(512), 0, st, p);
-            else if (p.impl == 23) {
-                if (nkt_s > WS_NSLOT) hipLaunchKernelGGL((mam_attention_ws_kernel<3, 16, false>), g2, dim3(1024), 0, st, p);
-                else hipLaunchKernelGGL((mam_attention_ws_kernel<WS_NSLOT, 16, false>), g2, dim3(1024), 0, st, p);
-            } else if (p.impl == 21 || nkt_s > WS_NSLOT)
-                hipLaunchKernelGGL((mam_attention_ws_kernel<3, 8, false>), g2, dim3(512), 0, st, p);
-            else hipLaunchKernelGGL((mam_attention_ws_kernel<WS_NSLOT, 8, false>), g2, dim3(512), 0, st, p);
-            return launch_status();
-        }
-        if (p.impl >= 20) {  // shape outside the whole-sequence kernel's block plan: impl 17
-            hipLaunchKernelGGL((mam_attention_lz_kernel<3, 3, true>), fgrid, dim3(256), 0, st, p);
-            return launch_status();
-        }
         if (p.impl >= 16) {  // range-checked exponent kernel (A/B): 16 = VALU row sums, ring 3, 3 WG/CU;
                              // 17 = MFMA row sums; 18 = ring 2; 19 = 2 WG/CU
             if (p.impl == 16) hipLaunchKernelGGL((mam_attention_lz_kernel<3, 3, false>), fgrid, dim3(256), 0, st, p);

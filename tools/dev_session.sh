@@ -2,7 +2,7 @@
 # Development GPU session: the whole -m gpu suite, then MAM attention A/B timings.
 # Usage: tools/dev_session.sh TAG [IMPLS] [BATCHES]
 set -u
-TAG=${1:-dev}; IMPLS=${2:-17,22,24,25}; BATCHES=${3:-1,8,32}
+TAG=${1:-dev}; IMPLS=${2:-8,17}; BATCHES=${3:-1,8,32}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"; cd "$ROOT"
