@@ -47,7 +47,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 METRIC = "tracker FPS (template+search fwd) MixViT-B RGB-T @320px, 1/2/4/8 MI355X"
-PEAK = {"bf16": 2500.0, "f32": 157.3}  # dense MFMA TFLOP/s, MI355X_MICROARCH.md
+PEAK = {"bf16": 2500.0, "fp16": 2500.0, "f32": 157.3}  # dense MFMA TFLOP/s, MI355X_MICROARCH.md
 # model geometry: ViT-B 128/320 (configs 2-4) and ViT-L 192/384 (config 5; fusion width = HIDDEN_DIM, defect D1)
 GEO_B = {"hidden": 768, "depth": 12, "search": 320, "template": 128}
 GEO_L = {"hidden": 1024, "depth": 24, "search": 384, "template": 192}
@@ -332,7 +332,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=1, help="frames (sequences) per GPU per step")
     ap.add_argument("--variant", default="rgbt", choices=list(VARIANT_NAMES))
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--gemm-impl", type=int, default=0, help="mmt_gemm_params.impl for every GEMM (A/B)")
@@ -378,7 +378,7 @@ def main():
     from mmt_amd import synthetic
     from mmt_amd.runtime import MixFormerRGBTRuntime
 
-    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    dtype = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(args.dtype, torch.float32)
     geo = GEO_L if args.vitl else GEO_B
     keys = state_dict_keys(args.variant, **geo)
     sd = {k: torch.from_numpy(v) for k, v in synthetic.synth_state_dict(keys).items()}

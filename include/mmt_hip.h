@@ -55,6 +55,9 @@ extern "C" {
 #define MMT_F32 0
 #define MMT_BF16 1
 #define MMT_F64 2
+#define MMT_F16 3 /* fp16 operands, fp32 accumulation (the path of BASELINE config 5); taken by the
+                     kernels of the forward plan (GEMM, MAM attention default kernels, norms,
+                     patch staging, bimodal MSDA, head); the others return MMT_EBADARG */
 #define MMT_EBADARG (-10000)
 #define MMT_MAX_GROUPS 2
 

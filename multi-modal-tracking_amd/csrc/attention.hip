@@ -28,9 +28,9 @@ constexpr int D = 64, KB = 64;
 // contiguous run of ids (query block fastest) keeps those re-reads in one L2.  Speed only; applied
 // to grids larger than the chip (batched inference: B = 8 / 32 throughput kernel 33 -> 29 / 90 ->
 // 84 us), not to the single-wave batch-1 grid.
-MMT_DEV void attn_block_ids(int& bx, int& by, int& bz) {
+MMT_DEV void attn_block_ids(int& bx, int& by, int& bz, bool always = false) {
     const int nbx = gridDim.x, nby = gridDim.y, nwg = nbx * nby * gridDim.z;
-    if (nwg <= 256) {
+    if (nwg <= 256 && !always) {
         bx = blockIdx.x;
         by = blockIdx.y;
         bz = blockIdx.z;
@@ -354,7 +354,7 @@ MMT_DEV void attn_wait_dyn(int n) {
 // state, and the states are merged through LDS at the end.  At batch 1 the grid is ~216 WGs, one
 // per CU: splitting the keys puts 4*KG waves on the CU to hide the per-tile dependency chain
 // (LDS read -> MFMA -> max -> exp -> MFMA) that one wave per SIMD exposed in full.
-template <int KG>
+template <typename T, int KG, bool XCDMAP = false>
 __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(KG, KG))) void mam_attention_glds_kernel(
     const mmt_attn_params p) {
     constexpr int NWV = 4 * KG, PPW = 16 / NWV;  // waves; K/V pieces per wave per tile
@@ -369,7 +369,7 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(KG, KG
     const int64_t pitch = p.tok_pitch > 0 ? p.tok_pitch : ntok;  // rows between sequences
     const int nqb_t = (n_t + 63) / 64;
     int bx, h, s;
-    attn_block_ids(bx, h, s);
+    attn_block_ids(bx, h, s, XCDMAP);  // XCDMAP: a (sequence, head)'s query blocks share an XCD's L2
     const int qb = bx + (p.q_part == 2 ? nqb_t : 0);
     const bool tmpl = qb < nqb_t;
     const int q0 = tmpl ? qb * 64 : n_t + (qb - nqb_t) * 64;
@@ -377,7 +377,7 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(KG, KG
     const int Lk = tmpl ? n_t : (p.asym ? ntok + n_t : ntok);
     const bool cross = p.asym && !tmpl;
     const int64_t rs = 3 * (int64_t)C;
-    const bf16_t* qkv = (const bf16_t*)p.qkv;
+    const T* qkv = (const T*)p.qkv;
     const int sV = s % p.Bm, sI = sV + p.Bm;
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -385,7 +385,7 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(KG, KG
     const int l16 = lane & 15, lg = lane >> 4;
     const int prow = lane >> 3, pcol = lane & 7;  // this lane's row / position in a 1-KiB piece
 
-    auto key_row = [&](int kk) -> const bf16_t* {
+    auto key_row = [&](int kk) -> const T* {
         int seq = s, row = kk;
         if (cross) {
             if (kk < n_t) seq = sV;
@@ -401,7 +401,7 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(KG, KG
 #pragma unroll
         for (int i = 0; i < PPW; ++i) {
             const int piece = w * PPW + i, isv = piece >> 3, pk = piece & 7, r = pk * 8 + prow;
-            const bf16_t* src = key_row(min(t * KB + r, Lk - 1)) + (isv ? 2 * C : C);
+            const T* src = key_row(min(t * KB + r, Lk - 1)) + (isv ? 2 * C : C);
             const int sw = isv ? (pcol ^ (prow & 6)) : (pcol ^ prow);
             attn_glds16(src + sw * 8, slot + isv * KB * 128 + pk * 1024);
         }
@@ -415,7 +415,7 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(KG, KG
 #pragma unroll
         for (int i = 0; i < (NWV >= 8 ? 1 : 8 / NWV); ++i) {
             const int piece = NWV >= 8 ? w : w * (8 / NWV) + i, r = piece * 8 + prow;
-            const bf16_t* src = qkv + ((int64_t)s * pitch + min(q0 + r, qend - 1)) * rs + h * D;
+            const T* src = qkv + ((int64_t)s * pitch + min(q0 + r, qend - 1)) * rs + h * D;
             attn_glds16(src + ((pcol ^ prow) * 8), qimg + piece * 1024);
         }
     }
@@ -473,8 +473,7 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(KG, KG
             sacc[kt16] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int t = 0; t < 2; ++t)
-                sacc[kt16] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kf[kt16][t]),
-                                                                     __builtin_bit_cast(bf16x8, qf[t]), sacc[kt16], 0, 0, 0);
+                sacc[kt16] = mfma16x16x32<T>(kf[kt16][t], qf[t], sacc[kt16]);
         }
         if (kt * KB + KB > Lk) {  // mask the tail of the key range (clamped rows)
 #pragma unroll
@@ -510,15 +509,13 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(KG, KG
         attn_lds_wait();
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
-            const bf16x8 pf = __builtin_bit_cast(
-                bf16x8, u32x4{pack_bf16x2(sacc[2 * kk][0], sacc[2 * kk][1]), pack_bf16x2(sacc[2 * kk][2], sacc[2 * kk][3]),
-                              pack_bf16x2(sacc[2 * kk + 1][0], sacc[2 * kk + 1][1]),
-                              pack_bf16x2(sacc[2 * kk + 1][2], sacc[2 * kk + 1][3])});
+            const u32x4 pf = u32x4{pack2<T>(sacc[2 * kk][0], sacc[2 * kk][1]), pack2<T>(sacc[2 * kk][2], sacc[2 * kk][3]),
+                                   pack2<T>(sacc[2 * kk + 1][0], sacc[2 * kk + 1][1]),
+                                   pack2<T>(sacc[2 * kk + 1][2], sacc[2 * kk + 1][3])};
 #pragma unroll
             for (int dt = 0; dt < 4; ++dt) {
                 const uint2 ua = vt[kk][dt][0], ub = vt[kk][dt][1];
-                const bf16x8 vf = __builtin_bit_cast(bf16x8, make_uint4(ua.x, ua.y, ub.x, ub.y));
-                o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[dt], 0, 0, 0);
+                o[dt] = mfma16x16x32<T>(u32x4{ua.x, ua.y, ub.x, ub.y}, pf, o[dt]);
             }
         }
     }
@@ -561,11 +558,11 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(KG, KG
     const float inv = 1.f / lanegroup_sum(l_run);
     const int q = q0 + 16 * qw + l16;
     if (q < qend) {
-        bf16_t* op = (bf16_t*)p.out + ((int64_t)s * pitch + q) * C + h * D;
+        T* op = (T*)p.out + ((int64_t)s * pitch + q) * C + h * D;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt)
             *(uint2*)(op + dt * 16 + 4 * lg) =
-                make_uint2(pack_bf16x2(o[dt][0] * inv, o[dt][1] * inv), pack_bf16x2(o[dt][2] * inv, o[dt][3] * inv));
+                make_uint2(pack2<T>(o[dt][0] * inv, o[dt][1] * inv), pack2<T>(o[dt][2] * inv, o[dt][3] * inv));
     }
 #if MMT_STAMP_BUILD
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -600,7 +597,7 @@ constexpr int FQ = 128, FTILE = 2 * KB * 128;
 #endif
 constexpr float FA_THR = 8.f;
 
-template <int FNS, int OCC>  // ring depth, workgroups per CU
+template <typename T, int FNS, int OCC>  // storage type, ring depth, workgroups per CU
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void mam_attention_fa_kernel(
     const mmt_attn_params p) {
     __shared__ __attribute__((aligned(1024))) char lds[FNS * FTILE + FQ * 128];
@@ -618,7 +615,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     const int Lk = tmpl ? n_t : (p.asym ? ntok + n_t : ntok);
     const bool cross = p.asym && !tmpl;
     const int64_t rs = 3 * (int64_t)C;
-    const bf16_t* qkv = (const bf16_t*)p.qkv;
+    const T* qkv = (const T*)p.qkv;
     const int sV = s % p.Bm, sI = sV + p.Bm;
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -630,7 +627,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     // pk*8 + prow of the tile, this lane's swizzled 16-B chunk.
     const int isv = w >> 1;
     const int64_t col = (isv ? 2 * C : C) + h * D + (isv ? (pcol ^ (prow & 6)) : (pcol ^ prow)) * 8;
-    auto key_row = [&](int kk) -> const bf16_t* {
+    auto key_row = [&](int kk) -> const T* {
         int seq = s, row = kk;
         if (cross) {
             if (kk < n_t) seq = sV;
@@ -644,7 +641,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     auto issue_tile = [&](int t) {
         char* slot = lds + (t % FNS) * FTILE + isv * KB * 128;
         if (aligned && t * KB + KB <= Lk) {
-            const bf16_t* base = key_row(t * KB);  // wave-uniform
+            const T* base = key_row(t * KB);  // wave-uniform
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int pk = (w & 1) * 4 + i;
@@ -662,7 +659,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int piece = w * 4 + i, r = piece * 8 + prow;
-        const bf16_t* src = qkv + ((int64_t)s * pitch + min(q0 + r, qend - 1)) * rs + h * D;
+        const T* src = qkv + ((int64_t)s * pitch + min(q0 + r, qend - 1)) * rs + h * D;
         attn_glds16(src + ((pcol ^ prow) * 8), qimg + piece * 1024);
     }
     for (int t = 0; t < FNS - 1 && t < nkt; ++t) issue_tile(t);
@@ -678,7 +675,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) o[dt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4{0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u});
+    const u32x4 ones = u32x4{one2<T>(), one2<T>(), one2<T>(), one2<T>()};
     u32x4 qf[2][2];
 
     for (int kt = 0; kt < nkt; ++kt) {
@@ -696,8 +693,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
                         u32x4 v = qf[qt][u];
 #pragma unroll
                         for (int e = 0; e < 4; ++e)
-                            v[e] = pack_bf16x2(__uint_as_float(v[e] << 16) * cexp,
-                                               __uint_as_float(v[e] & 0xffff0000u) * cexp);
+                            v[e] = pack2<T>(unpack2<T>(v[e])[0] * cexp, unpack2<T>(v[e])[1] * cexp);
                         qf[qt][u] = v;
                     }
                 }
@@ -731,9 +727,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
                 sacc[kt16][qt] = f32x4{-mr[qt], -mr[qt], -mr[qt], -mr[qt]};
 #pragma unroll
                 for (int u = 0; u < 2; ++u)
-                    sacc[kt16][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kf[kt16][u]),
-                                                                             __builtin_bit_cast(bf16x8, qf[qt][u]),
-                                                                             sacc[kt16][qt], 0, 0, 0);
+                    sacc[kt16][qt] = mfma16x16x32<T>(kf[kt16][u], qf[qt][u], sacc[kt16][qt]);
             }
         if (kt * KB + KB > Lk) {
 #pragma unroll
@@ -774,23 +768,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
         attn_lds_wait();
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
-            bf16x8 pf[2];
+            u32x4 pf[2];
 #pragma unroll
             for (int qt = 0; qt < 2; ++qt)
-                pf[qt] = __builtin_bit_cast(
-                    bf16x8, u32x4{pack_bf16x2(sacc[2 * kk][qt][0], sacc[2 * kk][qt][1]),
-                                  pack_bf16x2(sacc[2 * kk][qt][2], sacc[2 * kk][qt][3]),
-                                  pack_bf16x2(sacc[2 * kk + 1][qt][0], sacc[2 * kk + 1][qt][1]),
-                                  pack_bf16x2(sacc[2 * kk + 1][qt][2], sacc[2 * kk + 1][qt][3])});
+                pf[qt] = u32x4{pack2<T>(sacc[2 * kk][qt][0], sacc[2 * kk][qt][1]),
+                               pack2<T>(sacc[2 * kk][qt][2], sacc[2 * kk][qt][3]),
+                               pack2<T>(sacc[2 * kk + 1][qt][0], sacc[2 * kk + 1][qt][1]),
+                               pack2<T>(sacc[2 * kk + 1][qt][2], sacc[2 * kk + 1][qt][3])};
 #pragma unroll
             for (int dt = 0; dt < 4; ++dt) {
                 const uint2 ua = vt[kk][dt][0], ub = vt[kk][dt][1];
-                const bf16x8 vf = __builtin_bit_cast(bf16x8, make_uint4(ua.x, ua.y, ub.x, ub.y));
+                const u32x4 vf = u32x4{ua.x, ua.y, ub.x, ub.y};
 #pragma unroll
-                for (int qt = 0; qt < 2; ++qt) o[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qt], o[dt][qt], 0, 0, 0);
+                for (int qt = 0; qt < 2; ++qt) o[dt][qt] = mfma16x16x32<T>(vf, pf[qt], o[dt][qt]);
             }
 #pragma unroll
-            for (int qt = 0; qt < 2; ++qt) lsum[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[qt], lsum[qt], 0, 0, 0);
+            for (int qt = 0; qt < 2; ++qt) lsum[qt] = mfma16x16x32<T>(ones, pf[qt], lsum[qt]);
         }
     }
 
@@ -803,11 +796,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
         if (q < qend && p.lse && lg == 0)  // training: log2-sum-exp2 of the pre-scaled scores
             p.lse[((int64_t)s * p.H + h) * ntok + q] = mr[qt] + __builtin_amdgcn_logf(lsum[qt][0]);
         if (q < qend) {
-            bf16_t* op = (bf16_t*)p.out + ((int64_t)s * pitch + q) * C + h * D;
+            T* op = (T*)p.out + ((int64_t)s * pitch + q) * C + h * D;
 #pragma unroll
             for (int dt = 0; dt < 4; ++dt)
-                *(uint2*)(op + dt * 16 + 4 * lg) = make_uint2(pack_bf16x2(o[dt][qt][0] * inv, o[dt][qt][1] * inv),
-                                                              pack_bf16x2(o[dt][qt][2] * inv, o[dt][qt][3] * inv));
+                *(uint2*)(op + dt * 16 + 4 * lg) = make_uint2(pack2<T>(o[dt][qt][0] * inv, o[dt][qt][1] * inv),
+                                                              pack2<T>(o[dt][qt][2] * inv, o[dt][qt][3] * inv));
         }
     }
 }
@@ -1333,9 +1326,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 
 template <typename T>
 int launch_attn(const mmt_attn_params& p, hipStream_t st) {
-    if (p.impl != 0 && p.impl != 2 && p.impl != 4 && (p.impl < 8 || p.impl > 12) && (p.impl < 16 || p.impl > 19))
+    if (p.impl != 0 && p.impl != 2 && p.impl != 4 && p.impl != 6 && (p.impl < 8 || p.impl > 12) && (p.impl < 16 || p.impl > 19))
         return MMT_EBADARG;
     if (p.lse && (sizeof(T) != 2 || p.impl == 9 || (p.impl > 9 && p.impl < 16))) return MMT_EBADARG;
+    // fp16: the kernels with a running maximum (latency kernel, throughput kernel); the range-checked
+    // exponent and 32x32 variants are bf16 A/B kernels, and the training forward (lse) is bf16
+    if (__is_same(T, f16_t) && (p.lse || p.impl >= 10)) return MMT_EBADARG;
     if (!p.qkv || !p.out || p.H <= 0 || p.C != p.H * D || p.S <= 0 || p.ntok <= p.n_t || p.n_t <= 0) return MMT_EBADARG;
     if (p.tok_pitch != 0 && (p.tok_pitch < p.ntok || p.lse)) return MMT_EBADARG;
     if (p.asym && (p.Bm <= 0 || p.S != 2 * p.Bm)) return MMT_EBADARG;
@@ -1353,7 +1349,8 @@ int launch_attn(const mmt_attn_params& p, hipStream_t st) {
         // small grids (batch-1 tracking): the latency kernel (64 queries x KG key groups)
         const int nfa = qblocks(FQ);
         const dim3 fgrid(nfa, p.H, p.S);
-        if (p.impl >= 16) {  // range-checked exponent kernel (A/B): 16 = VALU row sums, ring 3, 3 WG/CU;
+        if (!__is_same(T, bf16_t)) {  // fp16: no A/B variants (rejected above)
+        } else if (p.impl >= 16) {  // range-checked exponent kernel (A/B): 16 = VALU row sums, ring 3, 3 WG/CU;
                              // 17 = MFMA row sums; 18 = ring 2; 19 = 2 WG/CU
             if (p.impl == 16) hipLaunchKernelGGL((mam_attention_lz_kernel<3, 3, false>), fgrid, dim3(256), 0, st, p);
             else if (p.impl == 17) hipLaunchKernelGGL((mam_attention_lz_kernel<3, 3, true>), fgrid, dim3(256), 0, st, p);
@@ -1362,22 +1359,26 @@ int launch_attn(const mmt_attn_params& p, hipStream_t st) {
             return launch_status();
         }
         if (p.impl == 8 || p.lse || (p.impl == 0 && (int64_t)nfa * p.H * p.S >= MMT_ATTN_FA_MIN_WG)) {
-            hipLaunchKernelGGL((mam_attention_fa_kernel<2, 3>), fgrid, dim3(256), 0, st, p);
+            hipLaunchKernelGGL((mam_attention_fa_kernel<T, 2, 3>), fgrid, dim3(256), 0, st, p);
             return launch_status();
         }
         if (p.impl == 9) {  // ring-depth / occupancy variant (A/B): 3-deep ring, 2 workgroups per CU
-            hipLaunchKernelGGL((mam_attention_fa_kernel<3, 2>), fgrid, dim3(256), 0, st, p);
+            hipLaunchKernelGGL((mam_attention_fa_kernel<T, 3, 2>), fgrid, dim3(256), 0, st, p);
             return launch_status();
         }
-        if (p.impl >= 10) {  // 32x32x16 throughput kernel (A/B): 10 = ring 2 / 2 WG per CU, 11 = 3 / 2, 12 = 2 / 3
+        if (p.impl >= 10 && __is_same(T, bf16_t)) {  // 32x32x16 throughput kernel (A/B): 10 = ring 2 / 2 WG per CU, 11 = 3 / 2, 12 = 2 / 3
             if (p.impl == 10) hipLaunchKernelGGL((mam_attention_fa32_kernel<2, 2>), fgrid, dim3(256), 0, st, p);
             else if (p.impl == 11) hipLaunchKernelGGL((mam_attention_fa32_kernel<3, 2>), fgrid, dim3(256), 0, st, p);
             else hipLaunchKernelGGL((mam_attention_fa32_kernel<2, 3>), fgrid, dim3(256), 0, st, p);
             return launch_status();
         }
+        if (p.impl == 6) {  // A/B: latency kernel (KG 4) with the XCD-grouped block map at any grid size
+            hipLaunchKernelGGL((mam_attention_glds_kernel<T, 4, true>), grid, dim3(1024), 0, st, p);
+            return launch_status();
+        }
         const int kg = p.impl > 0 ? p.impl : 4;
-        if (kg == 2) hipLaunchKernelGGL(mam_attention_glds_kernel<2>, grid, dim3(512), 0, st, p);
-        else hipLaunchKernelGGL(mam_attention_glds_kernel<4>, grid, dim3(1024), 0, st, p);
+        if (kg == 2) hipLaunchKernelGGL((mam_attention_glds_kernel<T, 2>), grid, dim3(512), 0, st, p);
+        else hipLaunchKernelGGL((mam_attention_glds_kernel<T, 4>), grid, dim3(1024), 0, st, p);
     } else {  // fp32 (parity path); small grids: 4 waves x 16 queries to occupy more SIMDs
         if ((int64_t)nqb * p.H * p.S < 1024) hipLaunchKernelGGL((mam_attention_kernel<T, 1>), grid, dim3(256), 0, st, p);
         else hipLaunchKernelGGL((mam_attention_kernel<T, 2>), grid, dim3(128), 0, st, p);
@@ -1390,6 +1391,7 @@ int launch_attn(const mmt_attn_params& p, hipStream_t st) {
 extern "C" int mmt_mam_attention(const mmt_attn_params* p, int dtype, void* stream) {
     if (!p) return MMT_EBADARG;
     if (dtype == MMT_BF16) return launch_attn<bf16_t>(*p, (hipStream_t)stream);
+    if (dtype == MMT_F16) return launch_attn<f16_t>(*p, (hipStream_t)stream);
     if (dtype == MMT_F32) return launch_attn<float>(*p, (hipStream_t)stream);
     return MMT_EBADARG;
 }

@@ -31,6 +31,38 @@ MMT_DEV uint32_t pack_bf16x2(float lo, float hi) {
     return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{lo, hi}, bf16x2));
 }
 
+// fp16 storage (MMT_F16; BASELINE config 5): the same 2-byte layouts and MFMA shapes as bf16
+// (v_mfma_f32_*_f16 issue at the bf16 rate), 11-bit significand, range +-65504.  Kernels that
+// take either 16-bit type are templated on the storage type T (bf16_t or f16_t) and reach the
+// type through the helpers below.
+typedef _Float16 f16_t;
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+template <> MMT_DEV float to_f<f16_t>(f16_t v) { return (float)v; }
+template <> MMT_DEV f16_t from_f<f16_t>(float v) { return (f16_t)v; }
+MMT_DEV uint32_t pack_f16x2(float lo, float hi) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{lo, hi}, f16x2));
+}
+template <typename T> MMT_DEV uint32_t pack2(float lo, float hi);
+template <> MMT_DEV uint32_t pack2<bf16_t>(float lo, float hi) { return pack_bf16x2(lo, hi); }
+template <> MMT_DEV uint32_t pack2<f16_t>(float lo, float hi) { return pack_f16x2(lo, hi); }
+// the two 16-bit values of a dword (lo = bits 0-15) as floats
+template <typename T> MMT_DEV f32x2 unpack2(uint32_t u);
+template <> MMT_DEV f32x2 unpack2<bf16_t>(uint32_t u) { return f32x2{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)}; }
+template <> MMT_DEV f32x2 unpack2<f16_t>(uint32_t u) {
+    return __builtin_convertvector(__builtin_bit_cast(f16x2, u), f32x2);
+}
+// MFMA on 8 packed 16-bit values per lane (operand order as the builtins)
+template <typename T> MMT_DEV f32x4 mfma16x16x32(u32x4 a, u32x4 b, f32x4 c);
+template <> MMT_DEV f32x4 mfma16x16x32<bf16_t>(u32x4 a, u32x4 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+template <> MMT_DEV f32x4 mfma16x16x32<f16_t>(u32x4 a, u32x4 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+// 1.0 in both halves of a dword
+template <typename T> constexpr uint32_t one2() { return sizeof(T) == 2 && __is_same(T, f16_t) ? 0x3c003c00u : 0x3f803f80u; }
+
 // GELU(x) = x/2 (1 + erf(x/sqrt2)) with a branch-free erf (Abramowitz-Stegun 7.1.26, |error| <=
 // 1.5e-7): libm erff branches on |x|, which in a 64-value epilogue means 64 divergent regions.
 // t comes from v_rcp_f32 (1 ulp): an IEEE division is a 10-instruction sequence per element.

@@ -157,8 +157,7 @@ __global__ __launch_bounds__(256 * KS) void gemm_kernel(const mmt_gemm_params p)
 #pragma unroll
                 for (int nt = 0; nt < NTL; ++nt) {
                     if constexpr (sizeof(T) == 2) {
-                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                            __builtin_bit_cast(bf16x8, af[mt]), __builtin_bit_cast(bf16x8, bfr[nt]), acc[mt][nt], 0, 0, 0);
+                        acc[mt][nt] = mfma16x16x32<T>(af[mt], bfr[nt], acc[mt][nt]);
                     } else {
                         const f32x4 a4 = __builtin_bit_cast(f32x4, af[mt]);
                         const f32x4 b4 = __builtin_bit_cast(f32x4, bfr[nt]);
@@ -352,7 +351,8 @@ int launch_gemm(const mmt_gemm_params& p, hipStream_t st) {
                            p.act);
         return launch_status();
     }
-    if (sizeof(T) == 2 && mmt_gemm_glds_bf16(p, st, p.impl) == 0) return launch_status();
+    if constexpr (sizeof(T) == 2)
+        if (mmt_gemm_glds<T>(p, st, p.impl) == 0) return launch_status();
     if (p.ln_fold || p.c2_copy) return MMT_EBADARG;  // LDS-DMA kernel features only
     if (p.conv_h > 0) launch_tiles<T, true>(p, st);
     else launch_tiles<T, false>(p, st);
@@ -364,6 +364,7 @@ int launch_gemm(const mmt_gemm_params& p, hipStream_t st) {
 extern "C" int mmt_gemm(const mmt_gemm_params* p, int dtype, void* stream) {
     if (!p) return MMT_EBADARG;
     if (dtype == MMT_BF16) return launch_gemm<bf16_t>(*p, (hipStream_t)stream);
+    if (dtype == MMT_F16) return launch_gemm<f16_t>(*p, (hipStream_t)stream);
     if (dtype == MMT_F32) return launch_gemm<float>(*p, (hipStream_t)stream);
     return MMT_EBADARG;
 }

@@ -1,4 +1,4 @@
-// Large-tile bf16 GEMM for gfx950 with LDS-DMA staging (global_load_lds_dwordx4).
+// Large-tile bf16 / fp16 GEMM for gfx950 with LDS-DMA staging (global_load_lds_dwordx4).
 //
 // The batch-1 ViT GEMMs of the hot path (qkv / proj / fc1 / fc2 of mixformer.py:26-76, M = 2x528
 // rows) were bound by per-CU tile traffic and staging instructions in the register-staged 64x64
@@ -73,7 +73,7 @@ __device__ __attribute__((aligned(64))) const uint32_t g_zero_chunk[16] = {0};
 // (mmt_gemm_params.ln_fold): the row statistics of A are accumulated from the A fragments the
 // waves already hold for the MFMAs (wave column wc sums fragment rows mt = wc, wc + WGN, ...), so
 // the normalised operand never exists in memory and the LayerNorm launch disappears.
-template <int BM, int BN, int WGM, int WGN, int KS, int ST, bool CONV, bool LNF>
+template <typename T, int BM, int BN, int WGM, int WGN, int KS, int ST, bool CONV, bool LNF>
 __global__ __launch_bounds__(64 * WGM * WGN * KS)
     __attribute__((amdgpu_waves_per_eu(WGM * WGN * KS / 4, WGM * WGN * KS / 4))) void gemm_glds_kernel(
         const mmt_gemm_params p) {
@@ -110,9 +110,9 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
     const int l16 = lane & 15, lg = lane >> 4;
     const int M = p.M, N = p.N, K = p.K;
 
-    const bf16_t* A0 = (const bf16_t*)p.a[g];
-    const bf16_t* A1 = (const bf16_t*)p.a1[g];
-    const bf16_t* W = (const bf16_t*)p.w[g];
+    const T* A0 = (const T*)p.a[g];
+    const T* A1 = (const T*)p.a1[g];
+    const T* W = (const T*)p.w[g];
 
     // This lane stages row (piece*8 + prow), logical chunk pch, into byte 16*lane of the piece:
     // position (lane & 7) of row prow holds chunk (lane & 7) ^ prow  (the read-side XOR).
@@ -161,7 +161,7 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
         unsigned char* base = ring + (s % ST) * STAGE;
         if constexpr (!CONV) {
             const bool hp = ks > 0 && k >= ks;
-            const bf16_t* ab = (hp ? A1 - ks : A0) + k;
+            const T* ab = (hp ? A1 - ks : A0) + k;
 #pragma unroll
             for (int i = 0; i < PA; ++i)
                 glds16(kin ? (const void*)(ab + aoff[i]) : (const void*)g_zero_chunk, base + (wid * PA + i) * 1024);
@@ -184,7 +184,7 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
                 const int iy = ay[i] + dy, ix = ax[i] + dx;
                 const bool ok = kin && iy >= 0 && ix >= 0 && iy < ch && ix < ch;
                 const uint32_t pix = (uint32_t)aoff[i] + (uint32_t)((iy >> cup_sh) * hi + (ix >> cup_sh));
-                const bf16_t* src = A0 + (pix * (uint32_t)p.lda + (uint32_t)ci);
+                const T* src = A0 + (pix * (uint32_t)p.lda + (uint32_t)ci);
                 glds16(ok ? (const void*)src : (const void*)g_zero_chunk, base + (wid * PA + i) * 1024);
             }
         }
@@ -225,8 +225,7 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
             _Pragma("unroll") for (int t = 0; t < 2; ++t)                                                        \
             _Pragma("unroll") for (int nt = 0; nt < NT; ++nt)                                                    \
             _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) acc[nt][mt] =                                      \
-                __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, BF[t][nt]),                   \
-                                                        __builtin_bit_cast(bf16x8, AF[t][mt]), acc[nt][mt], 0, 0, 0); \
+                mfma16x16x32<T>(BF[t][nt], AF[t][mt], acc[nt][mt]);                                              \
         }                                                                                                        \
         if constexpr (LNF) { /* compile-time fragment index, scalar (wave-uniform) wave-column test; */          \
             /* packed fp32 sums (v_pk_add / v_pk_fma on the {lo, hi} bf16 pair), issued after the MFMAs */       \
@@ -235,8 +234,7 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
                     f32x2 sx_ = {0.f, 0.f}, sxx_ = {0.f, 0.f};                                                   \
                     _Pragma("unroll") for (int t = 0; t < 2; ++t)                                                \
                     _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                              \
-                        const f32x2 v_ = {__uint_as_float(AF[t][mt_][e] << 16),                                  \
-                                          __uint_as_float(AF[t][mt_][e] & 0xffff0000u)};                         \
+                        const f32x2 v_ = unpack2<T>(AF[t][mt_][e]);                                              \
                         sx_ += v_;                                                                               \
                         sxx_ = __builtin_elementwise_fma(v_, v_, sxx_);                                          \
                     }                                                                                            \
@@ -437,11 +435,10 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
                     rr = (int64_t)b * hs * hs + (int64_t)(y / p.r_p1) * hs + (x / p.r_p1);
                 }
                 if (p.r_t) {
-                    const u32x4 u = *(const u32x4*)((const bf16_t*)R + rr * p.ldr + nc);
-                    ra[i] = f32x4{__uint_as_float(u[0] << 16), __uint_as_float(u[0] & 0xffff0000u),
-                                  __uint_as_float(u[1] << 16), __uint_as_float(u[1] & 0xffff0000u)};
-                    rb[i] = f32x4{__uint_as_float(u[2] << 16), __uint_as_float(u[2] & 0xffff0000u),
-                                  __uint_as_float(u[3] << 16), __uint_as_float(u[3] & 0xffff0000u)};
+                    const u32x4 u = *(const u32x4*)((const T*)R + rr * p.ldr + nc);
+                    const f32x2 u0 = unpack2<T>(u[0]), u1 = unpack2<T>(u[1]), u2 = unpack2<T>(u[2]), u3 = unpack2<T>(u[3]);
+                    ra[i] = f32x4{u0[0], u0[1], u1[0], u1[1]};
+                    rb[i] = f32x4{u2[0], u2[1], u3[0], u3[1]};
                 } else {
                     ra[i] = *(const f32x4*)(R + rr * p.ldr + nc);
                     rb[i] = *(const f32x4*)(R + rr * p.ldr + nc + 4);
@@ -489,18 +486,18 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
                     *(f32x4*)((float*)C + e) = oa;
                     *(f32x4*)((float*)C + e + 4) = ob;
                     if (C2 && p.c2_copy) {  // compute-dtype copy of C (the next LayerNorm-folded GEMM's A)
-                        *(u32x4*)((bf16_t*)C2 + e) = u32x4{pack_bf16x2(sa[0], sa[1]), pack_bf16x2(sa[2], sa[3]),
-                                                           pack_bf16x2(sb[0], sb[1]), pack_bf16x2(sb[2], sb[3])};
+                        *(u32x4*)((T*)C2 + e) = u32x4{pack2<T>(sa[0], sa[1]), pack2<T>(sa[2], sa[3]),
+                                                      pack2<T>(sb[0], sb[1]), pack2<T>(sb[2], sb[3])};
                     } else if (C2) {
                         *(f32x4*)((float*)C2 + e) = sa;
                         *(f32x4*)((float*)C2 + e + 4) = sb;
                     }
                 } else {
-                    *(u32x4*)((bf16_t*)C + e) = u32x4{pack_bf16x2(oa[0], oa[1]), pack_bf16x2(oa[2], oa[3]),
-                                                      pack_bf16x2(ob[0], ob[1]), pack_bf16x2(ob[2], ob[3])};
+                    *(u32x4*)((T*)C + e) = u32x4{pack2<T>(oa[0], oa[1]), pack2<T>(oa[2], oa[3]),
+                                                 pack2<T>(ob[0], ob[1]), pack2<T>(ob[2], ob[3])};
                     if (C2)
-                        *(u32x4*)((bf16_t*)C2 + e) = u32x4{pack_bf16x2(sa[0], sa[1]), pack_bf16x2(sa[2], sa[3]),
-                                                           pack_bf16x2(sb[0], sb[1]), pack_bf16x2(sb[2], sb[3])};
+                        *(u32x4*)((T*)C2 + e) = u32x4{pack2<T>(sa[0], sa[1]), pack2<T>(sa[2], sa[3]),
+                                                      pack2<T>(sb[0], sb[1]), pack2<T>(sb[2], sb[3])};
                 }
             }
         }
@@ -512,16 +509,16 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
     MMT_STAMP(5, "s_memrealtime");
 }
 
-template <int BM, int BN, int WGM, int WGN, int KS, int ST>
+template <typename T, int BM, int BN, int WGM, int WGN, int KS, int ST>
 void launch(const mmt_gemm_params& p, int nsk, hipStream_t st) {
     const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
     const dim3 grid(tiles, nsk, p.groups), block(64 * WGM * WGN * KS);
     if (p.conv_h > 0)
-        hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, KS, ST, true, false>), grid, block, 0, st, p);
+        hipLaunchKernelGGL((gemm_glds_kernel<T, BM, BN, WGM, WGN, KS, ST, true, false>), grid, block, 0, st, p);
     else if (p.ln_fold)
-        hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, KS, ST, false, true>), grid, block, 0, st, p);
+        hipLaunchKernelGGL((gemm_glds_kernel<T, BM, BN, WGM, WGN, KS, ST, false, true>), grid, block, 0, st, p);
     else
-        hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, KS, ST, false, false>), grid, block, 0, st, p);
+        hipLaunchKernelGGL((gemm_glds_kernel<T, BM, BN, WGM, WGN, KS, ST, false, false>), grid, block, 0, st, p);
 }
 
 bool aligned(const void* ptr, int bytes) { return ((uintptr_t)ptr & (uintptr_t)(bytes - 1)) == 0; }
@@ -529,7 +526,8 @@ bool aligned(const void* ptr, int bytes) { return ((uintptr_t)ptr & (uintptr_t)(
 }  // namespace
 
 // Returns 1 when the shape / layout is not one this kernel takes (caller uses gemm.hip's kernel).
-int mmt_gemm_glds_bf16(const mmt_gemm_params& p, hipStream_t st, int force) {
+template <typename T>
+int mmt_gemm_glds(const mmt_gemm_params& p, hipStream_t st, int force) {
     if (force < 0) return 1;
     if (p.K % 8 || p.N % 8 || p.ldc % 8 || (p.r[0] && p.ldr % 8)) return 1;
     if (p.ln_fold && p.conv_h > 0) return 1;
@@ -598,11 +596,14 @@ int mmt_gemm_glds_bf16(const mmt_gemm_params& p, hipStream_t st, int force) {
         }
     }
     switch (cfg) {
-        case 1: launch<128, 128, 2, 4, 1, 4>(p, nsk, st); break;
-        case 2: launch<128, 64, 2, 2, 2, 3>(p, nsk, st); break;
-        case 3: launch<64, 64, 2, 2, 2, 4>(p, nsk, st); break;
-        case 4: launch<128, 128, 2, 2, 1, 4>(p, nsk, st); break;
+        case 1: launch<T, 128, 128, 2, 4, 1, 4>(p, nsk, st); break;
+        case 2: launch<T, 128, 64, 2, 2, 2, 3>(p, nsk, st); break;
+        case 3: launch<T, 64, 64, 2, 2, 2, 4>(p, nsk, st); break;
+        case 4: launch<T, 128, 128, 2, 2, 1, 4>(p, nsk, st); break;
         default: return 1;
     }
     return 0;
 }
+
+template int mmt_gemm_glds<bf16_t>(const mmt_gemm_params&, hipStream_t, int);
+template int mmt_gemm_glds<f16_t>(const mmt_gemm_params&, hipStream_t, int);

@@ -45,8 +45,9 @@ __global__ __launch_bounds__(256) void conv3x3_c1_kernel(const T* __restrict__ i
                 const uint32_t xa[4] = {xv.x, xv.y, xv.z, xv.w}, wa[4] = {wv.x, wv.y, wv.z, wv.w};
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    acc += __uint_as_float(xa[j] << 16) * __uint_as_float(wa[j] << 16);
-                    acc += __uint_as_float(xa[j] & 0xffff0000u) * __uint_as_float(wa[j] & 0xffff0000u);
+                    const f32x2 xj = unpack2<T>(xa[j]), wj = unpack2<T>(wa[j]);
+                    acc += xj[0] * wj[0];
+                    acc += xj[1] * wj[1];
                 }
             } else {
                 const f32x4 xf = __builtin_bit_cast(f32x4, xv), wf = __builtin_bit_cast(f32x4, wv);
@@ -81,8 +82,9 @@ __global__ __launch_bounds__(256) void corner_score_kernel(const T* __restrict__
             const uint32_t va[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                s += __uint_as_float(va[j] << 16) * wg[cc + 2 * j];
-                s += __uint_as_float(va[j] & 0xffff0000u) * wg[cc + 2 * j + 1];
+                const f32x2 vj = unpack2<T>(va[j]);
+                s += vj[0] * wg[cc + 2 * j];
+                s += vj[1] * wg[cc + 2 * j + 1];
             }
         } else {
             const f32x4 f = __builtin_bit_cast(f32x4, v);
@@ -441,7 +443,7 @@ __global__ __launch_bounds__(256) void spm_attention_kernel(const float* __restr
 
 extern "C" int mmt_conv3x3_c1(const void* in, const void* w, const float* bias, float* out, int G, int B, int h, int cin,
                               int64_t in_stride, int dtype, void* stream) {
-    const int epc = dtype == MMT_BF16 ? 8 : 4;
+    const int epc = dtype == MMT_BF16 || dtype == MMT_F16 ? 8 : 4;
     if (!in || !w || !bias || !out || G <= 0 || B <= 0 || h <= 0 || cin <= 0 || cin % epc || in_stride % epc)
         return MMT_EBADARG;
     const int64_t npx = (int64_t)B * h * h;
@@ -449,6 +451,9 @@ extern "C" int mmt_conv3x3_c1(const void* in, const void* w, const float* bias, 
     hipStream_t st = (hipStream_t)stream;
     if (dtype == MMT_BF16)
         hipLaunchKernelGGL(conv3x3_c1_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)in, (const bf16_t*)w, bias,
+                           out, B, h, cin, in_stride);
+    else if (dtype == MMT_F16)
+        hipLaunchKernelGGL(conv3x3_c1_kernel<f16_t>, grid, dim3(256), 0, st, (const f16_t*)in, (const f16_t*)w, bias,
                            out, B, h, cin, in_stride);
     else if (dtype == MMT_F32)
         hipLaunchKernelGGL(conv3x3_c1_kernel<float>, grid, dim3(256), 0, st, (const float*)in, (const float*)w, bias,
@@ -460,7 +465,7 @@ extern "C" int mmt_conv3x3_c1(const void* in, const void* w, const float* bias, 
 extern "C" int mmt_corner_softargmax(const void* x4, const float* w5, const float* b5, const float* a3, const float* a4,
                                      float* score_maps, float* boxes_cxcywh, float* boxes_xyxy, float* rois,
                                      float roi_scale, int B, int fh, int c4, int stride, int dtype, void* stream) {
-    const int epc = dtype == MMT_BF16 ? 8 : 4;
+    const int epc = dtype == MMT_BF16 || dtype == MMT_F16 ? 8 : 4;
     if (!x4 || !w5 || !b5 || !a3 || !a4 || !score_maps || !boxes_cxcywh || B <= 0 || fh <= 0 || fh % 4 || c4 <= 0 ||
         c4 % epc || fh * fh > SA_NT * 16)
         return MMT_EBADARG;
@@ -468,6 +473,9 @@ extern "C" int mmt_corner_softargmax(const void* x4, const float* w5, const floa
     dim3 grid((unsigned)(((int64_t)B * fh * fh + 255) / 256), 2);
     if (dtype == MMT_BF16)
         hipLaunchKernelGGL(corner_score_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)x4, w5, b5, a3, a4,
+                           score_maps, B, fh, c4);
+    else if (dtype == MMT_F16)
+        hipLaunchKernelGGL(corner_score_kernel<f16_t>, grid, dim3(256), 0, st, (const f16_t*)x4, w5, b5, a3, a4,
                            score_maps, B, fh, c4);
     else if (dtype == MMT_F32)
         hipLaunchKernelGGL(corner_score_kernel<float>, grid, dim3(256), 0, st, (const float*)x4, w5, b5, a3, a4,

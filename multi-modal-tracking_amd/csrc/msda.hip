@@ -152,7 +152,7 @@ __global__ __launch_bounds__(64 * (int)sizeof(T) / 2) void msda_bimodal_kernel(c
 #pragma unroll
                 for (int j = 0; j < EPL; ++j) {
                     if constexpr (sizeof(T) == 2)
-                        v[k][j] = (j & 1) ? __uint_as_float(w4[j >> 1] & 0xffff0000u) : __uint_as_float(w4[j >> 1] << 16);
+                        v[k][j] = unpack2<T>(w4[j >> 1])[j & 1];
                     else
                         v[k][j] = __uint_as_float(w4[j]);
                 }
@@ -164,8 +164,8 @@ __global__ __launch_bounds__(64 * (int)sizeof(T) / 2) void msda_bimodal_kernel(c
     }
     T* o = out + row * CM + m * DH + c0;
     if constexpr (sizeof(T) == 2) {
-        *(uint4*)o = uint4{pack_bf16x2(col[0], col[1]), pack_bf16x2(col[2], col[3]), pack_bf16x2(col[4], col[5]),
-                           pack_bf16x2(col[6], col[7])};
+        *(uint4*)o = uint4{pack2<T>(col[0], col[1]), pack2<T>(col[2], col[3]), pack2<T>(col[4], col[5]),
+                           pack2<T>(col[6], col[7])};
     } else {
         *(f32x4*)o = f32x4{col[0], col[1], col[2], col[3]};
     }
@@ -290,6 +290,9 @@ extern "C" int mmt_msda_bimodal(const float* offw, const void* value, void* out,
     if (dtype == MMT_BF16)  // one query per workgroup: one wave (bf16) / two (fp32)
         hipLaunchKernelGGL((msda_bimodal_kernel<bf16_t>), dim3((unsigned)rows), dim3(64), 0, st, offw,
                            (const bf16_t*)value, (bf16_t*)out, B, hw);
+    else if (dtype == MMT_F16)
+        hipLaunchKernelGGL((msda_bimodal_kernel<f16_t>), dim3((unsigned)rows), dim3(64), 0, st, offw,
+                           (const f16_t*)value, (f16_t*)out, B, hw);
     else if (dtype == MMT_F32)
         hipLaunchKernelGGL((msda_bimodal_kernel<float>), dim3((unsigned)rows), dim3(128), 0, st, offw,
                            (const float*)value, (float*)out, B, hw);

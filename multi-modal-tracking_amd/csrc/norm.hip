@@ -57,8 +57,8 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
         if (out_t) {
             if constexpr (sizeof(T) == 2) {
                 uint2 pk;
-                pk.x = (uint32_t)f2bf(y.x) | ((uint32_t)f2bf(y.y) << 16);
-                pk.y = (uint32_t)f2bf(y.z) | ((uint32_t)f2bf(y.w) << 16);
+                pk.x = pack2<T>(y.x, y.y);
+                pk.y = pack2<T>(y.z, y.w);
                 ((uint2*)(out_t + row * C))[idx] = pk;
             } else {
                 ((float4*)(out_t + row * C))[idx] = y;
@@ -131,8 +131,8 @@ __global__ __launch_bounds__(GN_THREADS) void groupnorm_kernel(const float* __re
             if (out_t) {
                 if constexpr (sizeof(T) == 2) {
                     uint2 pk;
-                    pk.x = (uint32_t)f2bf(y.x) | ((uint32_t)f2bf(y.y) << 16);
-                    pk.y = (uint32_t)f2bf(y.z) | ((uint32_t)f2bf(y.w) << 16);
+                    pk.x = pack2<T>(y.x, y.y);
+                    pk.y = pack2<T>(y.z, y.w);
                     *(uint2*)(out_t + off) = pk;
                 } else {
                     *(float4*)(out_t + off) = y;
@@ -156,8 +156,8 @@ __global__ void add_cast_kernel(const float* __restrict__ in, const float* __res
     if (out_t) {
         if constexpr (sizeof(T) == 2) {
             uint2 pk;
-            pk.x = (uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16);
-            pk.y = (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16);
+            pk.x = pack2<T>(v.x, v.y);
+            pk.y = pack2<T>(v.z, v.w);
             ((uint2*)out_t)[i] = pk;
         } else {
             ((float4*)out_t)[i] = v;
@@ -213,6 +213,8 @@ extern "C" int mmt_layernorm(const float* in, const float* add, int64_t add_rows
     const int V = C / 256;
     if (dtype == MMT_BF16) {
         if (V == 2) LN_CASE(bf16_t, 2); else if (V == 3) LN_CASE(bf16_t, 3); else LN_CASE(bf16_t, 4);
+    } else if (dtype == MMT_F16) {
+        if (V == 2) LN_CASE(f16_t, 2); else if (V == 3) LN_CASE(f16_t, 3); else LN_CASE(f16_t, 4);
     } else if (dtype == MMT_F32) {
         if (V == 2) LN_CASE(float, 2); else if (V == 3) LN_CASE(float, 3); else LN_CASE(float, 4);
     } else return MMT_EBADARG;
@@ -231,6 +233,9 @@ extern "C" int mmt_groupnorm(const float* in, float* out_f32, void* out_t, const
     if (dtype == MMT_BF16)
         hipLaunchKernelGGL((groupnorm_kernel<bf16_t>), grid, dim3(GN_THREADS), 0, st, in, out_f32, (bf16_t*)out_t, gamma0,
                            beta0, gamma1, beta1, inst_per_set, P, Ctot, groups, eps);
+    else if (dtype == MMT_F16)
+        hipLaunchKernelGGL((groupnorm_kernel<f16_t>), grid, dim3(GN_THREADS), 0, st, in, out_f32, (f16_t*)out_t, gamma0,
+                           beta0, gamma1, beta1, inst_per_set, P, Ctot, groups, eps);
     else if (dtype == MMT_F32)
         hipLaunchKernelGGL((groupnorm_kernel<float>), grid, dim3(GN_THREADS), 0, st, in, out_f32, (float*)out_t, gamma0,
                            beta0, gamma1, beta1, inst_per_set, P, Ctot, groups, eps);
@@ -246,6 +251,8 @@ extern "C" int mmt_add_cast(const float* in, const float* add, int64_t add_n, fl
     hipStream_t st = (hipStream_t)stream;
     if (dtype == MMT_BF16)
         hipLaunchKernelGGL((add_cast_kernel<bf16_t>), grid, dim3(256), 0, st, in, add, add_n, out_f32, (bf16_t*)out_t, n4);
+    else if (dtype == MMT_F16)
+        hipLaunchKernelGGL((add_cast_kernel<f16_t>), grid, dim3(256), 0, st, in, add, add_n, out_f32, (f16_t*)out_t, n4);
     else if (dtype == MMT_F32)
         hipLaunchKernelGGL((add_cast_kernel<float>), grid, dim3(256), 0, st, in, add, add_n, out_f32, (float*)out_t, n4);
     else return MMT_EBADARG;
@@ -265,6 +272,9 @@ extern "C" int mmt_patch_im2col(const float* img_t0, const float* img_t1, const 
     if (dtype == MMT_BF16)
         hipLaunchKernelGGL((patch_im2col_kernel<bf16_t>), grid, dim3(256), 0, st, img_t0, img_t1, img_o0, img_o1,
                            img_s0, img_s1, (bf16_t*)out, Bm, ht, hs, patch, total);
+    else if (dtype == MMT_F16)
+        hipLaunchKernelGGL((patch_im2col_kernel<f16_t>), grid, dim3(256), 0, st, img_t0, img_t1, img_o0, img_o1,
+                           img_s0, img_s1, (f16_t*)out, Bm, ht, hs, patch, total);
     else if (dtype == MMT_F32)
         hipLaunchKernelGGL((patch_im2col_kernel<float>), grid, dim3(256), 0, st, img_t0, img_t1, img_o0, img_o1,
                            img_s0, img_s1, (float*)out, Bm, ht, hs, patch, total);

@@ -13,7 +13,7 @@ import torch  # noqa: F401  (loads the HIP runtime the kernels must share)
 LIB_PATH = os.environ.get("MMT_HIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib",
                                                          "libmmt_hip.so")
 
-MMT_F32, MMT_BF16, MMT_F64 = 0, 1, 2
+MMT_F32, MMT_BF16, MMT_F64, MMT_F16 = 0, 1, 2, 3
 MAX_GROUPS = 2
 
 vp = ctypes.c_void_p

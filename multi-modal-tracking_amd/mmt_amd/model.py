@@ -223,7 +223,8 @@ class _HipTracker(nn.Module):
         self.head_type = head_type
         self._rt = None
         self._online_batch = None
-        self.compute_dtype = torch.bfloat16 if os.environ.get("MMT_DTYPE", "bf16") == "bf16" else torch.float32
+        self.compute_dtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "f16": torch.float16}.get(
+            os.environ.get("MMT_DTYPE", "bf16"), torch.float32)
         self.use_hip_graph = True
         self.register_load_state_dict_post_hook(lambda m, keys: m.refresh_kernels())
 

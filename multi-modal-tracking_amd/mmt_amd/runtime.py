@@ -14,7 +14,7 @@ ntok = 2*n_t + n_s tokens per sequence, C = 768 for ViT-B):
   HID  dt   [S*ntok][4C]     GELU(fc1) output
   fusion encoder: SRC fp32 / SRCT dt [2][B*n_s][512] (modality-major, i.e. the reference's
   (B, 2*n_s, 512) with the halves as the outer index), head: NHWC maps.
-`dt` is the compute dtype (bf16 or fp32).  Accumulation, softmax and norm statistics are fp32.
+`dt` is the compute dtype (bf16, fp16 or fp32).  Accumulation, softmax and norm statistics are fp32.
 
 Weight preparation (load time, torch on device): casts, Linear/conv weights to [N][K] with
 K = (ky, kx, cin) for convs, eval-mode BatchNorm folded into the conv, the six first-level head
@@ -26,7 +26,7 @@ import math
 import torch
 
 from . import _lib
-from ._lib import LIB, GemmParams, AttnParams, check, MMT_F32, MMT_BF16
+from ._lib import LIB, GemmParams, AttnParams, check, MMT_F32, MMT_BF16, MMT_F16
 
 VARIANTS = ("rgbt", "shared", "asym", "asym_online", "asym_ce")
 
@@ -79,17 +79,20 @@ class MixFormerRGBTRuntime:
         The fp32 path keeps the explicit LayerNorm kernels."""
         if variant not in VARIANTS:
             raise ValueError("unknown variant %r" % (variant,))
-        if dtype not in (torch.bfloat16, torch.float32):
-            raise ValueError("dtype must be torch.bfloat16 or torch.float32")
+        if dtype not in (torch.bfloat16, torch.float16, torch.float32):
+            raise ValueError("dtype must be torch.bfloat16, torch.float16 or torch.float32")
+        if dtype == torch.float16 and variant == "asym_ce":
+            raise NotImplementedError("candidate elimination runs in bf16 / fp32 (its selection kernels have no fp16 form)")
         self.variant = variant
         # candidate elimination (asym_ce): {block: keep ratio}, lib/config/asymmetric_shared_ce/config.py:23-24
         ce = ce if ce is not None else ((3, 6, 9), (0.7, 0.7, 0.7))
         self.ce = dict(zip(ce[0], ce[1])) if variant == "asym_ce" else {}
         self.dtype = dtype
-        self.cdt = MMT_BF16 if dtype == torch.bfloat16 else MMT_F32
-        self.fold_ln = (dtype == torch.bfloat16) if fold_ln is None else bool(fold_ln)
-        if self.fold_ln and dtype != torch.bfloat16:
-            raise ValueError("the LayerNorm fold needs the bf16 (LDS-DMA) GEMM kernels")
+        self.cdt = {torch.bfloat16: MMT_BF16, torch.float16: MMT_F16}.get(dtype, MMT_F32)
+        half = dtype in (torch.bfloat16, torch.float16)
+        self.fold_ln = half if fold_ln is None else bool(fold_ln)
+        if self.fold_ln and not half:
+            raise ValueError("the LayerNorm fold needs the 16-bit (LDS-DMA) GEMM kernels")
         self.device = torch.device(device)
         sd = {k: v.detach() for k, v in state_dict.items()}
         self.d = Dims(sd, variant)

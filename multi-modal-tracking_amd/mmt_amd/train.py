@@ -86,40 +86,23 @@ class _HipLinear(torch.autograd.Function):
 
 
 class _HipMamAttention(torch.autograd.Function):
-    """MAM softmax attention (mixformer.py:52-78) over qkv [S][ntok][3C] bf16 -> [S][ntok][C] bf16."""
+    """MAM softmax attention (mixformer.py:52-78) over qkv [S][ntok][3C] bf16 -> [S][ntok][C] bf16:
+    the registered ops mmt::mam_attention_forward (with log-sum-exp) / mmt::mam_attention_backward."""
 
     @staticmethod
     def forward(ctx, qkv, n_t, heads):
-        from ._lib import LIB, AttnParams, MMT_BF16, check
-        S, ntok, C3 = qkv.shape
-        C = C3 // 3
+        from .ops import mam_attention_forward
         qkv = qkv.contiguous()
-        out = torch.empty(S, ntok, C, device=qkv.device, dtype=torch.bfloat16)
-        lse = torch.empty(S, heads, ntok, device=qkv.device, dtype=torch.float32)
-        p = AttnParams()
-        p.qkv, p.out, p.S, p.Bm, p.ntok, p.n_t, p.C, p.H, p.asym = (qkv.data_ptr(), out.data_ptr(), S, S, ntok, n_t, C,
-                                                                 heads, 0)
-        p.scale, p.impl, p.lse = (C // heads) ** -0.5, 0, lse.data_ptr()
-        check(LIB.mmt_mam_attention(p, MMT_BF16, _stream()), "mmt_mam_attention")
+        out, lse = mam_attention_forward(qkv, n_t, heads)
         ctx.save_for_backward(qkv, out, lse)
         ctx.n_t, ctx.heads = n_t, heads
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        from ._lib import LIB, AttnBwdParams, MMT_BF16, check
+        from .ops import mam_attention_backward
         qkv, out, lse = ctx.saved_tensors
-        S, ntok, C3 = qkv.shape
-        C = C3 // 3
-        dout = dout.to(torch.bfloat16).contiguous()
-        delta = torch.empty_like(lse)
-        dqkv = torch.empty_like(qkv)
-        p = AttnBwdParams()
-        p.qkv, p.out, p.dout, p.lse, p.delta, p.dqkv = (qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(),
-                                                        delta.data_ptr(), dqkv.data_ptr())
-        p.S, p.Bm, p.ntok, p.n_t, p.C, p.H, p.asym, p.scale = S, S, ntok, ctx.n_t, C, ctx.heads, 0, (C // ctx.heads) ** -0.5
-        check(LIB.mmt_mam_attention_bwd(p, MMT_BF16, _stream()), "mmt_mam_attention_bwd")
-        return dqkv, None, None
+        return mam_attention_backward(qkv, out, dout, lse, ctx.n_t, ctx.heads), None, None
 
 
 class HipOps:

@@ -13,7 +13,13 @@ from conftest import GOLDEN
 
 pytestmark = pytest.mark.gpu
 
-DT = {"f32": torch.float32, "bf16": torch.bfloat16}
+DT = {"f32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}
+
+
+def _code(dt):
+    """mmt dtype code of a torch dtype (MMT_F32 / MMT_BF16 / MMT_F16)."""
+    L = _lib()
+    return {torch.bfloat16: L.MMT_BF16, torch.float16: L.MMT_F16}.get(dt, L.MMT_F32)
 
 
 def _lib():
@@ -48,15 +54,15 @@ def _gemm(a, w, c, M, N, K, lda, ldc, dtype, **kw):
     if kw.get("sk"):  # (splitk, slab workspace, tickets)
         n, ws, cnt = kw["sk"]
         p.splitk, p.sk_ws, p.sk_ws_floats, p.sk_cnt, p.sk_cnt_n = n, ws.data_ptr(), ws.numel(), cnt.data_ptr(), cnt.numel()
-    L.check(L.LIB.mmt_gemm(p, L.MMT_BF16 if dtype == torch.bfloat16 else L.MMT_F32,
+    L.check(L.LIB.mmt_gemm(p, _code(dtype),
                            torch.cuda.current_stream().cuda_stream), "mmt_gemm")
 
 
 def _tol(dt):
-    return 2e-2 if dt == torch.bfloat16 else 2e-5
+    return 2e-2 if dt != torch.float32 else 2e-5
 
 
-@pytest.mark.parametrize("dname", ["f32", "bf16"])
+@pytest.mark.parametrize("dname", ["f32", "bf16", "fp16"])
 @pytest.mark.parametrize("M,N,K,act", [(300, 200, 192, 0), (1056, 2304, 768, 0), (128, 128, 64, 1), (77, 192, 1024, 2),
                                        (1056, 3072, 768, 1)])  # the last: fc1 shape, packed GELU epilogue
 def test_gemm_plain(dname, M, N, K, act):
@@ -78,7 +84,7 @@ def test_gemm_plain(dname, M, N, K, act):
     assert err <= 1e-3 * ref.abs().max().item() + 1e-4, err
 
 
-@pytest.mark.parametrize("dname", ["f32", "bf16"])
+@pytest.mark.parametrize("dname", ["f32", "bf16", "fp16"])
 def test_gemm_groups_segments_ksplit(dname):
     dt = DT[dname]
     g = torch.Generator().manual_seed(1)
@@ -217,21 +223,23 @@ def test_gemm_splitk_conv():
     assert int(cnt.abs().sum()) == 0
 
 
+@pytest.mark.parametrize("dname", ["bf16", "fp16"])
 @pytest.mark.parametrize("impl", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("M,N,K", [(528, 2304, 768), (300, 136, 512)])
-def test_gemm_layernorm_fold(impl, M, N, K):
+def test_gemm_layernorm_fold(dname, impl, M, N, K):
     """Linear(LayerNorm(x)) as one GEMM (ln_fold): A = bf16 rows of x with a nonzero mean, W' =
     W * gamma, colsum / bias' precomputed as the runtime does; two groups (modalities) with their
     own gamma / beta.  Also the producer side: c2_copy writes the bf16 copy of an fp32 C + R."""
     L = _lib()
+    dt = DT[dname]
     g = torch.Generator().manual_seed(M + K)
     x = torch.randn(2, M, K, generator=g) * 2 + 0.7
     W = torch.randn(N, K, generator=g) / math.sqrt(K)
     b = torch.randn(N, generator=g)
     gam = 1 + 0.3 * torch.randn(2, K, generator=g)
     bet = 0.2 * torch.randn(2, K, generator=g)
-    xb = x.bfloat16()
-    Wp = (W[None] * gam[:, None, :]).bfloat16()                      # [2][N][K]
+    xb = x.to(dt)
+    Wp = (W[None] * gam[:, None, :]).to(dt)                      # [2][N][K]
     colsum = Wp.float().sum(-1).contiguous()                         # [2][N]
     bp = (b[None] + torch.einsum("nk,gk->gn", W, bet)).contiguous()  # [2][N]
     xd, Wd, cd, bd = xb.cuda(), Wp.cuda(), colsum.cuda(), bp.cuda()
@@ -243,7 +251,7 @@ def test_gemm_layernorm_fold(impl, M, N, K):
     p.lda, p.ldc = K, N
     p.a_seg_rows, p.a_segs_a = M, 1
     p.M, p.N, p.K, p.c_f32, p.groups, p.impl, p.ln_fold, p.ln_eps = M, N, K, 1, 2, impl, 1, 1e-6
-    L.check(L.LIB.mmt_gemm(p, L.MMT_BF16, torch.cuda.current_stream().cuda_stream), "gemm_ln")
+    L.check(L.LIB.mmt_gemm(p, _code(dt), torch.cuda.current_stream().cuda_stream), "gemm_ln")
     torch.cuda.synchronize()
     for q in range(2):
         ref = F.layer_norm(xb[q].float(), (K,), gam[q], bet[q], 1e-6) @ W.t() + b
@@ -253,16 +261,16 @@ def test_gemm_layernorm_fold(impl, M, N, K):
     R = torch.randn(M, N, generator=g)
     Rd = R.cuda()
     c1 = torch.empty(M, N, device="cuda")
-    c2 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-    _gemm([xd[0].data_ptr()], [Wd[0].data_ptr()], [c1.data_ptr()], M, N, K, K, N, torch.bfloat16,
+    c2 = torch.empty(M, N, device="cuda", dtype=dt)
+    _gemm([xd[0].data_ptr()], [Wd[0].data_ptr()], [c1.data_ptr()], M, N, K, K, N, dt,
           bias=[bd[0].data_ptr()], r=[Rd.data_ptr()], ldr=N, c_f32=1, c2=[c2.data_ptr()], impl=impl, c2_copy=1)
     torch.cuda.synchronize()
     ref = xb[0].float() @ Wp[0].float().t() + bp[0] + R
     assert (c1.cpu() - ref).abs().max().item() <= 1e-3 * ref.abs().max().item() + 1e-4
-    assert torch.equal(c2.cpu(), c1.cpu().bfloat16())
+    assert torch.equal(c2.cpu(), c1.cpu().to(dt))
 
 
-@pytest.mark.parametrize("dname,impl", [("f32", 0), ("bf16", -1), ("bf16", 1), ("bf16", 2), ("bf16", 3)])
+@pytest.mark.parametrize("dname,impl", [("f32", 0), ("bf16", -1), ("bf16", 1), ("bf16", 2), ("bf16", 3), ("fp16", 1), ("fp16", -1)])
 @pytest.mark.parametrize("h,up,cin,cout", [(20, 1, 64, 96), (40, 2, 32, 48), (10, 1, 16, 200), (20, 1, 96, 48), (80, 4, 48, 32)])
 def test_conv3x3_implicit_gemm(dname, impl, h, up, cin, cout):
     """3x3/pad-1 conv as implicit GEMM on every kernel (impl); K = 9*cin is not a multiple of the
@@ -312,10 +320,11 @@ def _attn_ref(qkv, S, Bm, ntok, n_t, C, H, asym):
     return out.permute(0, 2, 1, 3).reshape(S, ntok, C)
 
 
-ATTN_BF16_IMPLS = [2, 4, 8, 9, 10, 11, 12, 16, 17, 18, 19]
+ATTN_BF16_IMPLS = [2, 4, 6, 8, 9, 10, 11, 12, 16, 17, 18, 19]
 
 
-@pytest.mark.parametrize("dname,impl", [("f32", 0), ("bf16", 0)] + [("bf16", i) for i in ATTN_BF16_IMPLS])
+@pytest.mark.parametrize("dname,impl", [("f32", 0), ("bf16", 0)] + [("bf16", i) for i in ATTN_BF16_IMPLS]
+                         + [("fp16", i) for i in (0, 2, 4, 8, 9)])
 @pytest.mark.parametrize("asym", [0, 1])
 @pytest.mark.parametrize("Bm,ntok,n_t,H", [(1, 528, 128, 12), (2, 100, 36, 2), (1, 70, 8, 1), (1, 864, 288, 2)])
 def test_mam_attention(dname, impl, asym, Bm, ntok, n_t, H):
@@ -331,15 +340,16 @@ def test_mam_attention(dname, impl, asym, Bm, ntok, n_t, H):
     p = L.AttnParams()
     p.qkv, p.out, p.S, p.Bm, p.ntok, p.n_t, p.C, p.H, p.asym, p.scale = qd.data_ptr(), out.data_ptr(), S, Bm, ntok, n_t, C, H, asym, 0.125
     p.impl = impl
-    L.check(L.LIB.mmt_mam_attention(p, L.MMT_BF16 if dt == torch.bfloat16 else L.MMT_F32,
+    L.check(L.LIB.mmt_mam_attention(p, _code(dt),
                                     torch.cuda.current_stream().cuda_stream), "attn")
     torch.cuda.synchronize()
     ref = _attn_ref(qkv.to(dt).float(), S, Bm, ntok, n_t, C, H, asym)
     err = (out.float().cpu() - ref).abs().max().item()
-    assert err <= (1.5e-2 if dt == torch.bfloat16 else 2e-5), err
+    assert err <= (1.5e-2 if dt != torch.float32 else 2e-5), err
 
 
-@pytest.mark.parametrize("dname,impl", [("f32", 0), ("bf16", 0)] + [("bf16", i) for i in ATTN_BF16_IMPLS])
+@pytest.mark.parametrize("dname,impl", [("f32", 0), ("bf16", 0)] + [("bf16", i) for i in ATTN_BF16_IMPLS]
+                         + [("fp16", i) for i in (0, 2, 4, 8, 9)])
 def test_mam_attention_rescale_branch(dname, impl):
     """Online-softmax rescale forced: one key per query block carries a huge score in a late tile
     (bf16: and in a different key group than the first tile, so the group merge rescales)."""
@@ -354,14 +364,14 @@ def test_mam_attention_rescale_branch(dname, impl):
     p = L.AttnParams()
     p.qkv, p.out, p.S, p.Bm, p.ntok, p.n_t, p.C, p.H, p.asym, p.scale = qd.data_ptr(), out.data_ptr(), S, Bm, ntok, n_t, C, H, 0, 0.125
     p.impl = impl
-    L.check(L.LIB.mmt_mam_attention(p, L.MMT_BF16 if dt == torch.bfloat16 else L.MMT_F32,
+    L.check(L.LIB.mmt_mam_attention(p, _code(dt),
                                     torch.cuda.current_stream().cuda_stream), "attn")
     torch.cuda.synchronize()
     ref = _attn_ref(qkv.to(dt).double(), S, Bm, ntok, n_t, C, H, 0).float()
-    assert (out.float().cpu() - ref).abs().max().item() < (1.5e-2 if dt == torch.bfloat16 else 5e-5)
+    assert (out.float().cpu() - ref).abs().max().item() < (1.5e-2 if dt != torch.float32 else 5e-5)
 
 
-@pytest.mark.parametrize("impl", [0, 2, 4, 8, 9, 10, 12, 16, 17, 18, 19])
+@pytest.mark.parametrize("impl", [0, 2, 4, 6, 8, 9, 10, 12, 16, 17, 18, 19])
 @pytest.mark.parametrize("asym", [0, 1])
 def test_mam_attention_prescaled_q(impl, asym):
     """The runtime's convention (bf16): q arrives multiplied by scale * log2(e) (folded into the qkv
@@ -416,7 +426,7 @@ def test_mam_attention_extreme_scores(impl, asym):
     assert (o - ref).abs().max().item() < 2.5e-2 * max(1.0, ref.abs().max().item())
 
 
-@pytest.mark.parametrize("dname", ["f32", "bf16"])
+@pytest.mark.parametrize("dname", ["f32", "bf16", "fp16"])
 @pytest.mark.parametrize("C", [512, 768, 1024])
 def test_layernorm_groups_and_add(dname, C):
     dt = DT[dname]
@@ -433,13 +443,13 @@ def test_layernorm_groups_and_add(dname, C):
     addd = add.cuda()
     L.check(L.LIB.mmt_layernorm(xd.data_ptr(), addd.data_ptr(), rpg, of.data_ptr(), ot.data_ptr(),
                                 *[t.data_ptr() for t in gs], rows, rpg, C, 1e-5,
-                                L.MMT_BF16 if dt == torch.bfloat16 else L.MMT_F32,
+                                _code(dt),
                                 torch.cuda.current_stream().cuda_stream), "ln")
     torch.cuda.synchronize()
     xa = x + torch.cat([add, add])
     ref = torch.cat([F.layer_norm(xa[:rpg], (C,), ga, ba, 1e-5), F.layer_norm(xa[rpg:], (C,), gb, bb, 1e-5)])
     assert (of.cpu() - ref).abs().max().item() < 2e-5
-    assert (ot.float().cpu() - ref).abs().max().item() < (3e-2 if dt == torch.bfloat16 else 2e-5)
+    assert (ot.float().cpu() - ref).abs().max().item() < (3e-2 if dt != torch.float32 else 2e-5)
 
 
 def test_groupnorm():
@@ -507,7 +517,7 @@ def test_msda_channels_sweep(channels):
     assert torch.allclose(out, ref, rtol=1e-12, atol=1e-15)
 
 
-@pytest.mark.parametrize("dname", ["f32", "bf16"])
+@pytest.mark.parametrize("dname", ["f32", "bf16", "fp16"])
 def test_msda_bimodal_vs_oracle(dname):
     from oracle.msda import ms_deform_attn
     dt = DT[dname]
@@ -521,7 +531,7 @@ def test_msda_bimodal_vs_oracle(dname):
     out = torch.empty(B * nq, 512, device="cuda", dtype=dt)
     offd, vald = offw.cuda(), value.to(dt).cuda()
     L.check(L.LIB.mmt_msda_bimodal(offd.data_ptr(), vald.data_ptr(), out.data_ptr(), B, hw,
-                                   L.MMT_BF16 if dt == torch.bfloat16 else L.MMT_F32,
+                                   _code(dt),
                                    torch.cuda.current_stream().cuda_stream), "msda_bimodal")
     torch.cuda.synchronize()
     # reference formulation (ms_deform_attn_bimodal.py:97-128) on the v-half queries
@@ -533,7 +543,7 @@ def test_msda_bimodal_vs_oracle(dname):
     val = torch.cat([value[0], value[1]], 1).to(dt).float().view(B, 2 * nq, 8, 64)
     ref = ms_deform_attn(val, [(hw, hw), (hw, hw)], [0, nq], loc, aw).reshape(B * nq, 512)
     err = (out.float().cpu() - ref).abs().max().item()
-    assert err <= (2e-2 if dt == torch.bfloat16 else 2e-5) * max(1.0, ref.abs().max().item()), err
+    assert err <= (2e-2 if dt != torch.float32 else 2e-5) * max(1.0, ref.abs().max().item()), err
 
 
 def test_prroi_known_answer():
@@ -611,7 +621,7 @@ def test_spm_attention(B, Lk, H):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dname", ["f32", "bf16"])
+@pytest.mark.parametrize("dname", ["f32", "bf16", "fp16"])
 @pytest.mark.parametrize("h,cin,pad", [(20, 48, 0), (40, 48, 16), (10, 16, 0), (16, 96, 8)])
 def test_conv3x3_c1_vs_torch(dname, h, cin, pad):
     """mmt_conv3x3_c1 (adjust3 / adjust4 closing conv, head.py:115-120): Cout = 1 3x3/pad-1 conv +
@@ -626,7 +636,7 @@ def test_conv3x3_c1_vs_torch(dname, h, cin, pad):
     xd, wd, bd = x.to(dt).cuda(), w.to(dt).cuda(), b.cuda()
     out = torch.empty(G, B, h * h, device="cuda")
     L.check(L.LIB.mmt_conv3x3_c1(xd.data_ptr(), wd.data_ptr(), bd.data_ptr(), out.data_ptr(), G, B, h, cin, cin + pad,
-                                 L.MMT_BF16 if dt == torch.bfloat16 else L.MMT_F32,
+                                 _code(dt),
                                  torch.cuda.current_stream().cuda_stream), "conv3x3_c1")
     torch.cuda.synchronize()
     xr = x.to(dt).float()[..., :cin]

@@ -5,7 +5,10 @@ mixformer.py:443 hard-codes 768 so the reference cannot build this model; SURVEY
 
 The reference has no fixture at this size, so the check is against the oracle (oracle/forward.py, the
 fp32 CPU restatement pinned by the ViT-B golden vectors): boxes within 1e-3 (fp32 path) / 1e-2 (bf16
-path), the score logit within the same bound relative to its magnitude (north_star tolerances)."""
+path), the score logit within the same bound relative to its magnitude (north_star tolerances).
+BASELINE config 5 names fp16: the fp16 path (MMT_F16: fp16 operands, fp32 accumulation) is held to the
+16-bit bound 1e-2.  The two-stream ViT-L (get_mixformer_vit large_patch16, mixformer.py:297-349) is
+checked the same way without the score head."""
 import numpy as np
 import pytest
 import torch
@@ -14,6 +17,7 @@ pytestmark = pytest.mark.gpu
 
 GEO = {"hidden": 1024, "depth": 24, "search": 384, "template": 192}
 _CACHE = {}
+DT = {"f32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}
 
 
 def _setup():
@@ -32,11 +36,11 @@ def _setup():
     return _CACHE
 
 
-@pytest.mark.parametrize("dname,tol", [("f32", 1e-3), ("bf16", 1e-2)])
+@pytest.mark.parametrize("dname,tol", [("f32", 1e-3), ("bf16", 1e-2), ("fp16", 1e-2)])
 def test_vit_large_matches_oracle(dname, tol):
     from mmt_amd.runtime import MixFormerRGBTRuntime
     c = _setup()
-    rt = MixFormerRGBTRuntime(c["sd"], "asym_online", dtype=torch.float32 if dname == "f32" else torch.bfloat16)
+    rt = MixFormerRGBTRuntime(c["sd"], "asym_online", dtype=DT[dname])
     assert (rt.d.C, rt.d.depth, rt.d.ntok, rt.d.n_t) == (1024, 24, 864, 288)
     t, o, s = [[x.cuda() for x in grp] for grp in c["inputs"]]
     box, sc = rt.forward(t, o, s, run_score_head=True)
@@ -46,3 +50,28 @@ def test_vit_large_matches_oracle(dname, tol):
     print("ViT-L %s box err %.3g score err %.3g (score %.4g)" % (dname, err, serr, c["score"]))
     assert err <= tol, err
     assert serr <= tol * max(1.0, abs(c["score"])), serr
+
+
+@pytest.mark.parametrize("dname,tol", [("bf16", 1e-2), ("fp16", 1e-2)])
+def test_vit_large_two_stream_matches_oracle(dname, tol):
+    """Two-stream ViT-L 192/384 (build_mixformer_vit_rgbt with the large backbone) vs the oracle."""
+    from mmt_amd import synthetic
+    from mmt_amd.model import reference_state_dict_shapes
+    from mmt_amd.runtime import MixFormerRGBTRuntime
+    from oracle.forward import forward as oracle_forward, state_dict_to_torch
+    if "sd2" not in _CACHE:
+        keys = reference_state_dict_shapes("rgbt", **GEO)
+        sd = state_dict_to_torch(synthetic.synth_state_dict(keys))
+        t, o, s = synthetic.synth_inputs(1, GEO["template"], GEO["search"])
+        with torch.no_grad():
+            out, _ = oracle_forward(sd, "rgbt", t, o, s)
+        _CACHE.update(sd2=sd, inputs2=(t, o, s), box2=out["pred_boxes"].reshape(4).numpy())
+    c = _CACHE
+    rt = MixFormerRGBTRuntime(c["sd2"], "rgbt", dtype=DT[dname])
+    assert (rt.d.C, rt.d.depth, rt.d.ntok) == (1024, 24, 864)
+    t, o, s = [[x.cuda() for x in grp] for grp in c["inputs2"]]
+    box, _ = rt.forward(t, o, s)
+    torch.cuda.synchronize()
+    err = np.abs(box.cpu().numpy().reshape(4) - c["box2"]).max()
+    print("ViT-L two-stream %s box err %.3g" % (dname, err))
+    assert err <= tol, err
