@@ -336,6 +336,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--gemm-impl", type=int, default=0, help="mmt_gemm_params.impl for every GEMM (A/B)")
+    ap.add_argument("--attn-impl", type=int, default=0, help="mmt_attn_params.impl for every MAM attention (A/B)")
     ap.add_argument("--no-kernel-profile", action="store_true",
                     help="skip the per-kernel timing (profiler runs that map dispatches to plan entries)")
     ap.add_argument("--dump-plan", default=None, help="write the plan's launch names (JSON) to this path")
@@ -384,6 +385,7 @@ def main():
     sd = {k: torch.from_numpy(v) for k, v in synthetic.synth_state_dict(keys).items()}
     rt = MixFormerRGBTRuntime(sd, args.variant, dtype=dtype)
     rt.gemm_impl = args.gemm_impl
+    rt.attn_impl = args.attn_impl
     B = args.batch
     score = args.variant == "asym_online"
     pool = []

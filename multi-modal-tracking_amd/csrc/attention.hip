@@ -28,9 +28,9 @@ constexpr int D = 64, KB = 64;
 // contiguous run of ids (query block fastest) keeps those re-reads in one L2.  Speed only; applied
 // to grids larger than the chip (batched inference: B = 8 / 32 throughput kernel 33 -> 29 / 90 ->
 // 84 us), not to the single-wave batch-1 grid.
-MMT_DEV void attn_block_ids(int& bx, int& by, int& bz, bool always = false) {
+MMT_DEV void attn_block_ids(int& bx, int& by, int& bz) {
     const int nbx = gridDim.x, nby = gridDim.y, nwg = nbx * nby * gridDim.z;
-    if (nwg <= 256 && !always) {
+    if (nwg <= 256) {
         bx = blockIdx.x;
         by = blockIdx.y;
         bz = blockIdx.z;
@@ -354,7 +354,7 @@ MMT_DEV void attn_wait_dyn(int n) {
 // state, and the states are merged through LDS at the end.  At batch 1 the grid is ~216 WGs, one
 // per CU: splitting the keys puts 4*KG waves on the CU to hide the per-tile dependency chain
 // (LDS read -> MFMA -> max -> exp -> MFMA) that one wave per SIMD exposed in full.
-template <typename T, int KG, bool XCDMAP = false>
+template <typename T, int KG>
 __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(KG, KG))) void mam_attention_glds_kernel(
     const mmt_attn_params p) {
     constexpr int NWV = 4 * KG, PPW = 16 / NWV;  // waves; K/V pieces per wave per tile
@@ -369,7 +369,8 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(KG, KG
     const int64_t pitch = p.tok_pitch > 0 ? p.tok_pitch : ntok;  // rows between sequences
     const int nqb_t = (n_t + 63) / 64;
     int bx, h, s;
-    attn_block_ids(bx, h, s, XCDMAP);  // XCDMAP: a (sequence, head)'s query blocks share an XCD's L2
+    attn_block_ids(bx, h, s);  // (grouping a (sequence, head)'s query blocks on one XCD measured
+                               // slower at batch 1: 8.94 vs 8.47 us in the frame)
     const int qb = bx + (p.q_part == 2 ? nqb_t : 0);
     const bool tmpl = qb < nqb_t;
     const int q0 = tmpl ? qb * 64 : n_t + (qb - nqb_t) * 64;
@@ -1326,7 +1327,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 
 template <typename T>
 int launch_attn(const mmt_attn_params& p, hipStream_t st) {
-    if (p.impl != 0 && p.impl != 2 && p.impl != 4 && p.impl != 6 && (p.impl < 8 || p.impl > 12) && (p.impl < 16 || p.impl > 19))
+    if (p.impl != 0 && p.impl != 2 && p.impl != 4 && (p.impl < 8 || p.impl > 12) && (p.impl < 16 || p.impl > 19))
         return MMT_EBADARG;
     if (p.lse && (sizeof(T) != 2 || p.impl == 9 || (p.impl > 9 && p.impl < 16))) return MMT_EBADARG;
     // fp16: the kernels with a running maximum (latency kernel, throughput kernel); the range-checked
@@ -1370,10 +1371,6 @@ int launch_attn(const mmt_attn_params& p, hipStream_t st) {
             if (p.impl == 10) hipLaunchKernelGGL((mam_attention_fa32_kernel<2, 2>), fgrid, dim3(256), 0, st, p);
             else if (p.impl == 11) hipLaunchKernelGGL((mam_attention_fa32_kernel<3, 2>), fgrid, dim3(256), 0, st, p);
             else hipLaunchKernelGGL((mam_attention_fa32_kernel<2, 3>), fgrid, dim3(256), 0, st, p);
-            return launch_status();
-        }
-        if (p.impl == 6) {  // A/B: latency kernel (KG 4) with the XCD-grouped block map at any grid size
-            hipLaunchKernelGGL((mam_attention_glds_kernel<T, 4, true>), grid, dim3(1024), 0, st, p);
             return launch_status();
         }
         const int kg = p.impl > 0 ? p.impl : 4;

@@ -25,7 +25,14 @@ def _update_intervals(cfg, dataset_name):
     return cfg.DATA.MAX_SAMPLE_INTERVAL
 
 
-def make_tracker_class(builder, multimodal, online_score=False, kv_cache=True):
+# Template K/V cache default, from measurement (profiles/r02_kv_cache.json): a single-sequence tracker
+# runs batch 1, where the search-only pass is no faster than the full forward (906 vs 912 frames/s:
+# the batch-1 GEMMs are one wave of tiles with or without the 128 template rows); at batch 8 it
+# gains 12 % (1981 vs 1764).  params.kv_cache overrides it.
+KV_CACHE_DEFAULT = False
+
+
+def make_tracker_class(builder, multimodal, online_score=False, kv_cache=KV_CACHE_DEFAULT):
     class MixFormer(BaseTracker):
         def __init__(self, params, dataset_name):
             super().__init__(params)
@@ -40,7 +47,8 @@ def make_tracker_class(builder, multimodal, online_score=False, kv_cache=True):
             self.update_intervals = _update_intervals(self.cfg, dataset_name)
             self.core = RGBTTrackerCore(self.network, params.template_factor, params.template_size,
                                         params.search_factor, params.search_size, self.update_intervals,
-                                        multimodal=multimodal, online_score=online_score, kv_cache=kv_cache)
+                                        multimodal=multimodal, online_score=online_score,
+                                        kv_cache=getattr(params, "kv_cache", kv_cache))
             self.state = None
             self.frame_id = 0
 

@@ -69,6 +69,7 @@ class MixFormerRGBTRuntime:
 
     gemm_impl = 0  # mmt_gemm_params.impl of every plan GEMM (0 = library's choice; A/B knob)
     gemm_splitk = 0  # mmt_gemm_params.splitk of every plan GEMM (0 = library's choice, 1 = off)
+    attn_impl = 0  # mmt_attn_params.impl of every plan attention (0 = library's choice; A/B knob)
     SPLITK_FLOATS = 8 << 20  # fp32 split-K partial-tile workspace (32 MiB), shared by every plan GEMM
     SPLITK_TICKETS = 1 << 16
 
@@ -436,6 +437,7 @@ class MixFormerRGBTRuntime:
             ap.asym = 1 if self.variant in ("asym", "asym_online", "asym_ce") else 0
             ap.scale = 1.0 / LOG2E if self.fold_ln else (C // d.H) ** -0.5  # see q_scale
             ap.q_part = {None: 0, "t": 1, "s": 2}[part]
+            ap.impl = self.attn_impl
             plan.append((LIB.mmt_mam_attention, (ctypes_byref(ap), cdt), "mam_attention", ap))
             cpx = dict(c2=rows(XN, C), c2_copy=1) if fold else {}
             self._gemm(plan, "proj", a=rows(AO, C), w=wl("attn.proj.w"), c=rows(X, C), M=Mg, N=C, K=C, lda=C,

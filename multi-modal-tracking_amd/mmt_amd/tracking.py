@@ -81,10 +81,11 @@ class RGBTTrackerCore:
     asymmetric_shared_online tracker's score-gated online-template update."""
 
     def __init__(self, network, template_factor, template_size, search_factor, search_size, update_intervals,
-                 multimodal, online_score=False, use_graph=True, kv_cache=True):
+                 multimodal, online_score=False, use_graph=True, kv_cache=False):
         self.net = network
         # kv_cache: the template tokens' per-layer qkv are computed once per template update (a
-        # separate template pass) and each frame runs only the search tokens (runtime.cache_workspace)
+        # separate template pass) and each frame runs only the search tokens (runtime.cache_workspace);
+        # off by default: no faster at batch 1 (lib/test/tracker/_rgbt.py KV_CACHE_DEFAULT)
         self.kv_cache = bool(kv_cache)
         self._tmpl_dirty = True
         self._tmpl_graph = self._tmpl_plan = None

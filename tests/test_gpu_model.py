@@ -182,3 +182,18 @@ def test_ce_keep_rate_argument():
         b_07, _ = net(t, o, s, ce_keep_rate=0.7)
     assert (full["pred_boxes"] - ref["pred_boxes"]).abs().max().item() <= 1e-5
     assert torch.equal(b_def["pred_boxes"], b_07["pred_boxes"])
+
+
+@pytest.mark.parametrize("dname,bound", [("bf16", 5e-3), ("fp16", 1e-3)])
+@pytest.mark.parametrize("variant", ["rgbt", "shared", "asym", "asym_online"])
+def test_16bit_headroom(variant, dname, bound):
+    """Headroom under the north star's 1e-2 bound: the default (LayerNorm-folded) 16-bit plans keep the
+    boxes within 5e-3 (bf16) / 1e-3 (fp16) of the reference's golden boxes (per-stage errors:
+    tools/stage_error.py, profiles/r02_stage_error.jsonl)."""
+    rt = _runtime(variant, {"bf16": torch.bfloat16, "fp16": torch.float16}[dname])
+    t, o, s = _inputs(1)
+    box, _ = rt.forward(t, o, s, run_score_head=variant == "asym_online")
+    torch.cuda.synchronize()
+    gold = np.load(GOLDEN + "/model_%s_b1.npz" % variant)["pred_boxes"].reshape(1, 4)
+    err = np.abs(box.cpu().numpy() - gold).max()
+    assert err <= bound, err
