@@ -48,6 +48,25 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "tracker FPS (template+search fwd) MixViT-B RGB-T @320px, 1/2/4/8 MI355X"
 PEAK = {"bf16": 2500.0, "fp16": 2500.0, "f32": 157.3}  # dense MFMA TFLOP/s, MI355X_MICROARCH.md
+HBM_PEAK = 8.0  # TB/s, MI355X_MICROARCH.md (6.29 measured for a float4 copy)
+
+
+def mam_memory_roofline(obj, S, ntok, C, elem_bytes):
+    """Adds the MAM kernel's memory side to a roofline object: its algorithmic HBM bytes per launch
+    (Q, K, V read once, O written once: S * ntok * 4C elements), their rate against the
+    8 TB/s peak, and `attainable_frac` = max(FLOP / MFMA peak, bytes / HBM peak) / launch time -- at
+    d = 64 the kernel's arithmetic intensity (~215 FLOP/B at the ViT-B shapes) is below the chip's
+    ridge (2.5 PF / 8 TB/s = 312 FLOP/B), so the bytes, not the MFMAs, set its floor."""
+    if obj is None:  # (no per-kernel profile in this run)
+        return None
+    by = float(S) * ntok * 4 * C * elem_bytes
+    us = obj["avg_launch_us"]
+    t_min = max(obj["flops_per_launch"] / (obj["peak"] * 1e12), by / (HBM_PEAK * 1e12)) * 1e6
+    obj.update({"hbm_bytes_per_launch": by, "hbm_tbps": round(by / (us * 1e-6) / 1e12, 3),
+                "hbm_frac": round(by / (us * 1e-6) / 1e12 / HBM_PEAK, 4),
+                "arith_intensity": round(obj["flops_per_launch"] / by, 1),
+                "attainable_frac": round(t_min / us, 4)})
+    return obj
 # model geometry: ViT-B 128/320 (configs 2-4) and ViT-L 192/384 (config 5; fusion width = HIDDEN_DIM, defect D1)
 GEO_B = {"hidden": 768, "depth": 12, "search": 320, "template": 128}
 GEO_L = {"hidden": 1024, "depth": 24, "search": 384, "template": 192}
@@ -139,7 +158,7 @@ def roofline(rt, plan, times, dtype, traffic=None):
     return obj(dom), obj("mam_attention"), total, by
 
 
-def mam_batched(rt, B=32, per_graph=20, replays=5):
+def mam_batched(rt, B=32, per_graph=20, replays=10):
     """Roofline of the MAM attention launch at B frames (2B sequences) on random bf16 q/k/v in the
     runtime's convention (q pre-scaled), timed like kernel_profile."""
     import ctypes
@@ -157,7 +176,8 @@ def mam_batched(rt, B=32, per_graph=20, replays=5):
     with torch.cuda.graph(g):
         for _ in range(per_graph):
             check(LIB.mmt_mam_attention(ctypes.byref(p), MMT_BF16, torch.cuda.current_stream().cuda_stream), "attn")
-    g.replay()
+    for _ in range(3):  # warm-up replays (clocks, caches)
+        g.replay()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(st)
     for _ in range(replays):
@@ -168,9 +188,10 @@ def mam_batched(rt, B=32, per_graph=20, replays=5):
     lk_s = d.ntok + (d.n_t if p.asym else 0)
     fl = 4.0 * 64 * d.H * S * (d.n_t * d.n_t + d.ns * lk_s)
     ach = fl / (us * 1e-6) / 1e12
-    return {"kernel": "mam_attention", "bound": "mfma", "achieved": round(ach, 2), "peak": PEAK["bf16"],
-            "unit": "TFLOP/s", "frac": round(ach / PEAK["bf16"], 4), "traffic": None, "frames": B,
-            "flops_per_launch": fl, "avg_launch_us": round(us, 2)}
+    return mam_memory_roofline({"kernel": "mam_attention", "bound": "mfma", "achieved": round(ach, 2),
+                                "peak": PEAK["bf16"], "unit": "TFLOP/s", "frac": round(ach / PEAK["bf16"], 4),
+                                "traffic": None, "frames": B, "flops_per_launch": fl, "avg_launch_us": round(us, 2)},
+                               S, d.ntok, d.C, 2)
 
 
 def kv_cache_tracking(rt, pool, score, steps, warmup):
@@ -444,7 +465,8 @@ def main():
                        "parallelism": ("dp%d sharded sequences" % world if sharded else
                                        "replicas x%d" % world if world > 1 else "single"),
                        "hip_graph": use_graph},
-            "roofline": dom, "roofline_mam": mam,
+            "roofline": dom,
+            "roofline_mam": mam_memory_roofline(mam, 2 * B, rt.d.ntok, rt.d.C, 4 if args.dtype == "f32" else 2),
             "device_ms_per_step_sum": round(dev_ms, 4) if dev_ms else None, "launches_per_step": len(plan),
             "kernels": {k: {"us": round(a["t"] * 1e3 / a["n"], 2), "n": a["n"],
                             "tflops": round(a["flops"] / a["n"] / (a["t"] / a["n"] * 1e-3) / 1e12, 1) if a["flops"] else None}
@@ -452,6 +474,7 @@ def main():
         }
         if args.dtype == "bf16" and not args.no_kernel_profile and not args.no_mam_batched:
             out["roofline_mam_batched"] = mam_batched(rt)
+            out["roofline_mam_batched_b8"] = mam_batched(rt, B=8)
         if use_graph and not args.no_kv_cache and args.variant != "asym_ce":  # no template cache with CE
             out["tracking_kv_cache"] = kv_cache_tracking(rt, pool, score, args.steps, args.warmup)
         if world == 1 and not args.no_cpu_baseline:

@@ -100,7 +100,8 @@ typedef struct {
     /* LayerNorm folded into the GEMM (bf16 LDS-DMA kernels, GEMM mode): A holds the raw rows x
      * (K = the LayerNorm width), W = W_lin * gamma (per column k), and the epilogue's v is
      *   rstd_m * (acc - mu_m * ln_colsum[g][n]) + bias[g][n],   mu / rstd over the K values of row m
-     * with ln_colsum[n] = sum_k W[n][k] and bias = b_lin + W_lin beta, i.e. Linear(LayerNorm(x)). */
+     * with ln_colsum[n] = sum_k W[n][k] and bias = b_lin + W_lin beta, i.e. Linear(LayerNorm(x)).
+     * ln_fold 1: statistics summed from the A fragments in the K loop; 2: read from ln_stats_in. */
     int32_t ln_fold;
     float ln_eps;
     const float* ln_colsum[MMT_MAX_GROUPS];
@@ -123,6 +124,15 @@ typedef struct {
      * r_mode == 0 -- e.g. the search rows [n_t, ntok) of every sequence of a [S][ntok] stream
      * (c, c2, r offset by n_t rows; c_seg_rows = ntok - n_t, c_seg_pitch = ntok). 0: identity. */
     int64_t c_seg_rows, c_seg_pitch;
+    /* LayerNorm row statistics handed from producer to consumer (16-bit LDS-DMA kernels, GEMM mode):
+     *   ln_stats_out[g] != NULL (producer, with c2_copy): for every stored row (output row map
+     *     applied) and every 64-column group j of N, (sum, sum of squares) of the C2 values as
+     *     stored (16-bit) go to ln_stats_out[g][row][j][0..1] (fp32, N/64 pairs per row);
+     *   ln_fold == 2 (consumer): as ln_fold == 1, but mu / rstd of A row m come from
+     *     ln_stats_in[g][m][0 .. K/64) (summed in order) instead of sums over the A fragments
+     *     in the K loop; the A map must be the identity (one segment, k_split == 0). */
+    float* ln_stats_out[MMT_MAX_GROUPS];
+    const float* ln_stats_in[MMT_MAX_GROUPS];
 } mmt_gemm_params;
 
 int mmt_gemm(const mmt_gemm_params* p, int dtype, void* stream);

@@ -315,7 +315,7 @@ MMT_DEV void attn_lds_wait() {
 }
 
 #if MMT_STAMP_BUILD
-__device__ unsigned long long g_mmt_attn_stamps[16384 * 6];
+__device__ unsigned long long g_mmt_attn_stamps[16384 * 8];
 extern "C" int mmt_attn_stamps(unsigned long long* host, int n) {
     return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_mmt_attn_stamps), sizeof(unsigned long long) * n);
 }

@@ -123,6 +123,19 @@ MMT_DEV float lanegroup_sum(float v) {
     return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
+// Sum over each aligned group of 8 consecutive lanes, every lane receiving its group's sum: DPP
+// (VALU) row moves -- quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror -- instead of
+// ds_bpermute round trips.
+template <int CTRL>
+MMT_DEV float dpp_f(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+MMT_DEV float sum8_lanes(float v) {
+    v += dpp_f<0xB1>(v);
+    v += dpp_f<0x4E>(v);
+    return v + dpp_f<0x141>(v);
+}
+
 // Block-wide sum for blockDim.x == NT (multiple of 64); `red` needs NT/64 floats of LDS.
 template <int NT>
 MMT_DEV float block_sum(float v, float* red) {
@@ -173,7 +186,7 @@ MMT_DEV void lds_barrier() {
     if (threadIdx.x == 0) {                                                                        \
         unsigned long long t_;                                                                     \
         asm volatile(INSN " %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                      \
-        BUF[(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 6 + (I)] = t_;       \
+        BUF[(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 8 + (I)] = t_;       \
     }
 #else
 #define MMT_STAMP_AT(BUF, I, INSN)

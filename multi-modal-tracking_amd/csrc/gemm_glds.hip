@@ -32,7 +32,7 @@
 
 // Stamp build (MMT_STAMP_BUILD): per-phase workgroup timestamps, read with mmt_gemm_stamps().
 #if MMT_STAMP_BUILD
-__device__ unsigned long long g_mmt_stamps[16384 * 6];
+__device__ unsigned long long g_mmt_stamps[16384 * 8];
 extern "C" int mmt_gemm_stamps(unsigned long long* host, int n) {
     return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_mmt_stamps), sizeof(unsigned long long) * n);
 }
@@ -73,7 +73,7 @@ __device__ __attribute__((aligned(64))) const uint32_t g_zero_chunk[16] = {0};
 // (mmt_gemm_params.ln_fold): the row statistics of A are accumulated from the A fragments the
 // waves already hold for the MFMAs (wave column wc sums fragment rows mt = wc, wc + WGN, ...), so
 // the normalised operand never exists in memory and the LayerNorm launch disappears.
-template <typename T, int BM, int BN, int WGM, int WGN, int KS, int ST, bool CONV, bool LNF>
+template <typename T, int BM, int BN, int WGM, int WGN, int KS, int ST, bool CONV, int LNM>
 __global__ __launch_bounds__(64 * WGM * WGN * KS)
     __attribute__((amdgpu_waves_per_eu(WGM * WGN * KS / 4, WGM * WGN * KS / 4))) void gemm_glds_kernel(
         const mmt_gemm_params p) {
@@ -104,6 +104,7 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
     const int tile = rem_t / nsk, slice = rem_t - tile * nsk;
     const int tiles_m = (p.M + BM - 1) / BM;
     const int tm = tile % tiles_m, tn = tile / tiles_m;
+    constexpr bool LNF = LNM != 0;  // LayerNorm folded: 1 = row statistics from the A fragments, 2 = handed in
     const int m0 = tm * BM, n0 = tn * BN;
     const int lane = threadIdx.x & 63, kg = threadIdx.x / TPG;
     const int wid = (threadIdx.x % TPG) >> 6, wr = wid / WGN, wc = wid % WGN;
@@ -227,7 +228,7 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
             _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) acc[nt][mt] =                                      \
                 mfma16x16x32<T>(BF[t][nt], AF[t][mt], acc[nt][mt]);                                              \
         }                                                                                                        \
-        if constexpr (LNF) { /* compile-time fragment index, scalar (wave-uniform) wave-column test; */          \
+        if constexpr (LNM == 1) { /* compile-time fragment index, scalar (wave-uniform) wave-column test; */     \
             /* packed fp32 sums (v_pk_add / v_pk_fma on the {lo, hi} bf16 pair), issued after the MFMAs */       \
             _Pragma("unroll") for (int mt_ = 0; mt_ < MT; ++mt_) {                                               \
                 if (mt_ % WGN == wc_u) {                                                                         \
@@ -297,8 +298,40 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
     static_assert(FLAG_OFF + 16 <= KS * ST * STAGE, "epilogue tile fits in the stage ring");
     float* ctile = (float*)lds;
     float* rstat = ctile + BM * TP;  // LNF: [KS][BM][2] partial (sum x, sum x^2) per k-group
+    // LNM 2: the handed-in row statistics (K/64 partial (sum, sum of squares) pairs per A row), read
+    // now so that their latency overlaps the tile's LDS assembly: TPRW threads per tile row, each
+    // loading every TPRW-th pair of its row (at most 8: K <= 64 * 8 * TPRW), summed below
+    constexpr int NTH_E = TPG * KS, TPRW = NTH_E / BM;
+    static_assert(TPRW >= 1 && (TPRW & (TPRW - 1)) == 0 && TPRW <= 64, "statistics reduction geometry");
+    f32x2 stp[8];
+    const int kp = K / 64, srow = threadIdx.x / TPRW, spart = threadIdx.x % TPRW;
+    if constexpr (LNM == 2) {
+        const f32x2* st = (const f32x2*)p.ln_stats_in[g] + (int64_t)min(m0 + srow, M - 1) * kp;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int j = spart + i * TPRW;
+            stp[i] = j < kp ? st[j] : f32x2{0.f, 0.f};
+        }
+    }
     lds_barrier();  // every wave is past its last fragment read (the DMA ring is drained: vmcnt(0))
-    if constexpr (LNF) {
+    if constexpr (LNM == 2) {  // (sum, sum of squares) of the row, in pair order within each thread
+        float sx = 0.f, sxx = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            sx += stp[i][0];
+            sxx += stp[i][1];
+        }
+#pragma unroll
+        for (int o = 1; o < TPRW; o <<= 1) {  // the row's TPRW threads are consecutive lanes
+            sx += __shfl_xor(sx, o, 64);
+            sxx += __shfl_xor(sxx, o, 64);
+        }
+        if (spart == 0) {
+            rstat[srow * 2] = sx;
+            rstat[srow * 2 + 1] = sxx;
+        }
+    }
+    if constexpr (LNM == 1) {
 #pragma unroll
         for (int j = 0; j < MTW; ++j) {
             const int mt = wc + j * WGN;
@@ -330,6 +363,7 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
     }
     static_assert(KS <= 2, "k-group reduction written for up to two groups");
     lds_barrier();
+    MMT_STAMP(4, "s_memtime");
 
     // 8-column strips: one 16-B store per lane for a bf16 C (two for fp32); dwordx2 stores were
     // store-issue-bound.
@@ -405,6 +439,7 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
         }
     }
     const int n = n0 + tc, nc = min(n, N - 8);
+    float* stats_out = p.c2_copy && C2 ? p.ln_stats_out[g] : nullptr;
     f32x4 bn0 = {0.f, 0.f, 0.f, 0.f}, bn1 = bn0, cs0 = bn0, cs1 = bn0;
     if (bias) {
         bn0 = *(const f32x4*)(bias + nc);
@@ -452,8 +487,9 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
             f32x4 vb = *(const f32x4*)(ctile + r * TP + tc + 4);
             if constexpr (LNF) {  // Linear(LayerNorm(x)) = rstd * (x.W' - mu * colsum(W')) + b'
                 float sx = 0.f, sxx = 0.f;
+                constexpr int NQ = LNM == 1 ? KS : 1;  // LNM 2: one (sum, sum x^2) pair per row
 #pragma unroll
-                for (int q = 0; q < KS; ++q) {
+                for (int q = 0; q < NQ; ++q) {
                     sx += rstat[(q * BM + r) * 2];
                     sxx += rstat[(q * BM + r) * 2 + 1];
                 }
@@ -480,6 +516,20 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
             const f32x4 sa = va + ra[i], sb = vb + rb[i];  // + residual
             const bool split_c2 = C2 && !p.c2_copy;           // C = v, C2 = v + R
             const f32x4 oa = split_c2 ? va : sa, ob = split_c2 ? vb : sb;
+            if (stats_out) {  // the next LayerNorm's row statistics over this 64-column group, taken
+                              // on the 16-bit values C2 holds (what the consumer's A fragments hold)
+                float ps = 0.f, pq = 0.f;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const f32x2 u = unpack2<T>(pack2<T>(j < 2 ? sa[2 * j] : sb[2 * j - 4], j < 2 ? sa[2 * j + 1] : sb[2 * j - 3]));
+                    ps += u[0] + u[1];
+                    pq = fmaf(u[0], u[0], fmaf(u[1], u[1], pq));
+                }
+                ps = sum8_lanes(ps);  // the group's 8 threads are 8 consecutive lanes
+                pq = sum8_lanes(pq);
+                if ((tc & 63) == 0 && m < M && n < N)
+                    *(f32x2*)(stats_out + (crow(m) * (N / 64) + n / 64) * 2) = f32x2{ps, pq};
+            }
             if (m < M && n < N) {
                 const int64_t e = crow(m) * p.ldc + n;
                 if (p.c_f32) {
@@ -502,11 +552,12 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
             }
         }
     }
+    MMT_STAMP(5, "s_memtime");
 #if MMT_STAMP_BUILD
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
-    MMT_STAMP(4, "s_memtime");
-    MMT_STAMP(5, "s_memrealtime");
+    MMT_STAMP(6, "s_memtime");
+    MMT_STAMP(7, "s_memrealtime");
 }
 
 template <typename T, int BM, int BN, int WGM, int WGN, int KS, int ST>
@@ -514,11 +565,13 @@ void launch(const mmt_gemm_params& p, int nsk, hipStream_t st) {
     const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
     const dim3 grid(tiles, nsk, p.groups), block(64 * WGM * WGN * KS);
     if (p.conv_h > 0)
-        hipLaunchKernelGGL((gemm_glds_kernel<T, BM, BN, WGM, WGN, KS, ST, true, false>), grid, block, 0, st, p);
+        hipLaunchKernelGGL((gemm_glds_kernel<T, BM, BN, WGM, WGN, KS, ST, true, 0>), grid, block, 0, st, p);
+    else if (p.ln_fold == 2)
+        hipLaunchKernelGGL((gemm_glds_kernel<T, BM, BN, WGM, WGN, KS, ST, false, 2>), grid, block, 0, st, p);
     else if (p.ln_fold)
-        hipLaunchKernelGGL((gemm_glds_kernel<T, BM, BN, WGM, WGN, KS, ST, false, true>), grid, block, 0, st, p);
+        hipLaunchKernelGGL((gemm_glds_kernel<T, BM, BN, WGM, WGN, KS, ST, false, 1>), grid, block, 0, st, p);
     else
-        hipLaunchKernelGGL((gemm_glds_kernel<T, BM, BN, WGM, WGN, KS, ST, false, false>), grid, block, 0, st, p);
+        hipLaunchKernelGGL((gemm_glds_kernel<T, BM, BN, WGM, WGN, KS, ST, false, 0>), grid, block, 0, st, p);
 }
 
 bool aligned(const void* ptr, int bytes) { return ((uintptr_t)ptr & (uintptr_t)(bytes - 1)) == 0; }
@@ -531,6 +584,11 @@ int mmt_gemm_glds(const mmt_gemm_params& p, hipStream_t st, int force) {
     if (force < 0) return 1;
     if (p.K % 8 || p.N % 8 || p.ldc % 8 || (p.r[0] && p.ldr % 8)) return 1;
     if (p.ln_fold && p.conv_h > 0) return 1;
+    if (p.ln_fold == 2 && (p.a_seg_rows < p.M || p.k_split || p.K % 64 || p.K > 64 * 8 * 2)) return 1;  // identity A map
+    for (int g = 0; g < p.groups; ++g) {
+        if (p.ln_fold == 2 && (!p.ln_stats_in[g] || !aligned(p.ln_stats_in[g], 8))) return 1;
+        if (p.ln_stats_out[g] && (!p.c2_copy || !p.c2[g] || p.N % 64 || !aligned(p.ln_stats_out[g], 8))) return 1;
+    }
     if (p.conv_h > 0) {  // the kernel's conv addressing: power-of-two upsample, 32-bit element offsets
         const int cup = p.conv_up, hi = p.conv_up > 0 ? p.conv_h / p.conv_up : 0;
         if (cup <= 0 || (cup & (cup - 1)) || hi * cup != p.conv_h) return 1;

@@ -36,6 +36,7 @@ class GemmParams(ctypes.Structure):
         ("ln_fold", i32), ("ln_eps", f32), ("ln_colsum", vp * MAX_GROUPS), ("c2_copy", i32),
         ("splitk", i32), ("sk_ws", vp), ("sk_ws_floats", i64), ("sk_cnt", vp), ("sk_cnt_n", i64),
         ("c_seg_rows", i64), ("c_seg_pitch", i64),
+        ("ln_stats_out", vp * MAX_GROUPS), ("ln_stats_in", vp * MAX_GROUPS),
     ]
 
 

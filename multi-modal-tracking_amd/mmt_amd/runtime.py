@@ -277,6 +277,7 @@ class MixFormerRGBTRuntime:
             "in_s": [e(B, 3, d.hs, d.hs, t=f32) for _ in range(2)],
             "PATCH": e(R, 3 * d.patch * d.patch), "X": e(R, C, t=f32), "XN": e(R, C), "QKV": e(R, 3 * C),
             "AO": e(R, C), "HID": e(R, d.hidden), "XT": e(R, C),
+            "LNST": e(R, 2 * (C // 64), t=f32),  # LayerNorm row statistics of XN, per 64 columns
             "Y1": e(2, B * ns, dm, t=f32), "SRC": e(2, B * ns, dm, t=f32), "SRCT": e(2, B * ns, dm),
             "VAL": e(2, B * ns, dm), "OFFW": e(B * ns, 192, t=f32), "MS": e(B * ns, dm),
             "SRC2": e(B * ns, dm, t=f32), "H2": e(2 * B * ns, d.ffn), "Y2": e(B * ns, C, t=f32),
@@ -308,7 +309,7 @@ class MixFormerRGBTRuntime:
     # ------------------------------------------------------------------ plan construction
     def _gemm(self, plan, name, *, a, w, c, M, N, K, lda, ldc, bias=None, r=None, ldr=0, c2=None, a1=None,
               k_split=0, act=0, c_f32=0, seg=None, r_mode=0, r_p0=0, r_p1=1, conv=None, r_t=0, dtype=None,
-              ln_colsum=None, ln_eps=0.0, c2_copy=0, cmap=None):
+              ln_colsum=None, ln_eps=0.0, c2_copy=0, cmap=None, ln_stats_in=None, ln_stats_out=None):
         p = GemmParams()
         G = len(a)
         for g in range(G):
@@ -333,9 +334,14 @@ class MixFormerRGBTRuntime:
         p.r_t = r_t
         p.impl = self.gemm_impl
         if ln_colsum is not None:
-            p.ln_fold, p.ln_eps = 1, ln_eps
+            p.ln_fold, p.ln_eps = (2 if ln_stats_in else 1), ln_eps
             for g in range(G):
                 p.ln_colsum[g] = ln_colsum[g]
+                if ln_stats_in:
+                    p.ln_stats_in[g] = ln_stats_in[g]
+        if ln_stats_out:
+            for g in range(G):
+                p.ln_stats_out[g] = ln_stats_out[g]
         p.c2_copy = c2_copy
         if cmap is not None:
             p.c_seg_rows, p.c_seg_pitch = cmap
@@ -378,11 +384,20 @@ class MixFormerRGBTRuntime:
             return P(t, (g * B * ntok + off) * ld)
         # --- patch embed (im2col + GEMM, + bias + pos-embed) -> X  (fold: + its bf16 copy XN)
         fold = self.fold_ln
+        # the producers of XN (patch embed, proj, fc2) also write its per-64-column row statistics
+        # (LNST), which the LayerNorm-folded consumers (qkv, fc1) read instead of summing them in
+        # their K loops; not for the template-cache passes (segment-mapped rows) or with candidate
+        # elimination (the gather moves rows)
+        hand = fold and part is None and not self.ce
+        nst = 2 * (C // 64)
+        LNST = ws["LNST"]
         plan.append((LIB.mmt_patch_im2col, tuple(P(t) for t in ws["in_t"]) + tuple(P(t) for t in ws["in_o"])
                      + tuple(P(t) for t in ws["in_s"]) + (P(ws["PATCH"]), B, d.ht, d.hs, d.patch, cdt), "patch_im2col", None))
         KP = 3 * d.patch * d.patch
         gm = B * nr  # rows per modality group
         cp = dict(c2_copy=1) if fold else {}
+        if hand:
+            cp["ln_stats_out"] = [at(LNST, nst, 0), at(LNST, nst, 1)] if two else [at(LNST, nst)]
         pos_at = lambda g: P(W["bb"][g]["pos"], off * C)  # noqa: E731  (pos rows of the part)
         if two:
             if fold:
@@ -424,7 +439,7 @@ class MixFormerRGBTRuntime:
             if fold:  # LayerNorm 1 folded into qkv: A = XN = bf16 copy of the residual stream X
                 self._gemm(plan, "qkv", a=rows2(XN, C), w=fl("attn.qkv.fw"), c=rows2(QKV, 3 * C), M=gm, N=3 * C,
                            K=C, lda=C, ldc=3 * C, bias=fl("attn.qkv.fb"), ln_colsum=fl("attn.qkv.fcs"), ln_eps=1e-6,
-                           **rmap(C))
+                           ln_stats_in=rows2(LNST, nst) if hand else None, **rmap(C))
             else:  # (the fp32 LayerNorm runs over all rows; rows outside the part are not read)
                 plan.append((LIB.mmt_layernorm, (P(X), None, 0, None, P(XN), P(n1[0][0]), P(n1[0][1]), P(n1[1][0]),
                                                  P(n1[1][1]), R, B * ntok, C, 1e-6, cdt), "ln1", None))
@@ -440,6 +455,8 @@ class MixFormerRGBTRuntime:
             ap.impl = self.attn_impl
             plan.append((LIB.mmt_mam_attention, (ctypes_byref(ap), cdt), "mam_attention", ap))
             cpx = dict(c2=rows(XN, C), c2_copy=1) if fold else {}
+            if hand:
+                cpx["ln_stats_out"] = rows(LNST, nst)
             self._gemm(plan, "proj", a=rows(AO, C), w=wl("attn.proj.w"), c=rows(X, C), M=Mg, N=C, K=C, lda=C,
                        ldc=C, bias=wl("attn.proj.b"), r=rows(X, C), ldr=C, c_f32=1, **cpx, **rmap(C))
             if i in self.ce:  # candidate elimination after the attention residual, before the MLP
@@ -466,7 +483,7 @@ class MixFormerRGBTRuntime:
             if fold:
                 self._gemm(plan, "fc1", a=rows2(XN, C), w=fl("mlp.fc1.fw"), c=rows2(HID, d.hidden), M=gm, N=d.hidden,
                            K=C, lda=C, ldc=d.hidden, bias=fl("mlp.fc1.fb"), act=1, ln_colsum=fl("mlp.fc1.fcs"),
-                           ln_eps=1e-6, **rmap(C))
+                           ln_eps=1e-6, ln_stats_in=rows2(LNST, nst) if hand else None, **rmap(C))
             else:
                 plan.append((LIB.mmt_layernorm, (P(X), None, 0, None, P(XN), P(n2[0][0]), P(n2[0][1]), P(n2[1][0]),
                                                  P(n2[1][1]), R, B * ntok, C, 1e-6, cdt), "ln2", None))

@@ -270,6 +270,59 @@ def test_gemm_layernorm_fold(dname, impl, M, N, K):
     assert torch.equal(c2.cpu(), c1.cpu().to(dt))
 
 
+@pytest.mark.parametrize("dname", ["bf16", "fp16"])
+@pytest.mark.parametrize("pimpl,cimpl", [(1, 1), (2, 3), (3, 2), (0, 0)])
+def test_gemm_layernorm_stats_handoff(dname, pimpl, cimpl):
+    """ln_stats_out / ln_fold 2: a producer GEMM (C fp32 = A W^T + b + R, C2 = its 16-bit copy) also
+    writes the per-64-column row statistics of C2; the LayerNorm-folded consumer reads them instead
+    of summing its A fragments.  Equal to the in-loop statistics (ln_fold 1) up to fp32 summation
+    order, and to Linear(LayerNorm(C2)) in fp32."""
+    L = _lib()
+    dt = DT[dname]
+    g = torch.Generator().manual_seed(7)
+    M, K0, C, N = 300, 256, 768, 1152
+    x = torch.randn(M, K0, generator=g).to(dt)
+    W0 = (torch.randn(C, K0, generator=g) / math.sqrt(K0)).to(dt)
+    b0 = torch.randn(C, generator=g)
+    R = torch.randn(M, C, generator=g) * 3 + 0.5
+    W = torch.randn(N, C, generator=g) / math.sqrt(C)
+    b = torch.randn(N, generator=g)
+    gam, bet = 1 + 0.3 * torch.randn(C, generator=g), 0.2 * torch.randn(C, generator=g)
+    Wp = (W * gam[None]).to(dt)
+    colsum, bp = Wp.float().sum(-1).contiguous(), (b + W @ bet).contiguous()
+    xd, W0d, b0d, Rd, Wd, cd, bd = [t.cuda() for t in (x, W0, b0, R, Wp, colsum, bp)]
+    c1 = torch.empty(M, C, device="cuda")
+    c2 = torch.empty(M, C, device="cuda", dtype=dt)
+    stats = torch.full((M, 2 * (C // 64)), float("nan"), device="cuda")
+    p = L.GemmParams()
+    p.a[0], p.w[0], p.c[0], p.c2[0], p.bias[0], p.r[0] = (xd.data_ptr(), W0d.data_ptr(), c1.data_ptr(), c2.data_ptr(),
+                                                          b0d.data_ptr(), Rd.data_ptr())
+    p.ln_stats_out[0] = stats.data_ptr()
+    p.lda, p.ldc, p.ldr, p.a_seg_rows, p.a_segs_a = K0, C, C, M, 1
+    p.M, p.N, p.K, p.c_f32, p.groups, p.impl, p.c2_copy = M, C, K0, 1, 1, pimpl, 1
+    L.check(L.LIB.mmt_gemm(p, _code(dt), torch.cuda.current_stream().cuda_stream), "producer")
+    torch.cuda.synchronize()
+    v = c2.float().cpu().reshape(M, C // 64, 64)
+    ref_st = torch.stack([v.sum(-1), (v * v).sum(-1)], -1).reshape(M, -1)
+    assert torch.allclose(stats.cpu(), ref_st, rtol=1e-5, atol=1e-3), (stats.cpu() - ref_st).abs().max()
+    outs = []
+    for mode in (1, 2):
+        out = torch.empty(M, N, device="cuda")
+        q = L.GemmParams()
+        q.a[0], q.w[0], q.c[0], q.bias[0], q.ln_colsum[0] = c2.data_ptr(), Wd.data_ptr(), out.data_ptr(), bd.data_ptr(), cd.data_ptr()
+        if mode == 2:
+            q.ln_stats_in[0] = stats.data_ptr()
+        q.lda, q.ldc, q.a_seg_rows, q.a_segs_a = C, N, M, 1
+        q.M, q.N, q.K, q.c_f32, q.groups, q.impl, q.ln_fold, q.ln_eps = M, N, C, 1, 1, cimpl, mode, 1e-6
+        L.check(L.LIB.mmt_gemm(q, _code(dt), torch.cuda.current_stream().cuda_stream), "consumer")
+        torch.cuda.synchronize()
+        outs.append(out.cpu())
+    ref = F.layer_norm(c2.float().cpu(), (C,), gam, bet, 1e-6) @ W.t() + b
+    for o in outs:
+        assert (o - ref).abs().max().item() <= 1e-2 * ref.abs().max().item()
+    assert (outs[0] - outs[1]).abs().max().item() <= 1e-4 * ref.abs().max().item()
+
+
 @pytest.mark.parametrize("dname,impl", [("f32", 0), ("bf16", -1), ("bf16", 1), ("bf16", 2), ("bf16", 3), ("fp16", 1), ("fp16", -1)])
 @pytest.mark.parametrize("h,up,cin,cout", [(20, 1, 64, 96), (40, 2, 32, 48), (10, 1, 16, 200), (20, 1, 96, 48), (80, 4, 48, 32)])
 def test_conv3x3_implicit_gemm(dname, impl, h, up, cin, cout):

@@ -48,9 +48,9 @@ def main():
             torch.cuda.synchronize()
             nqb = (n_t + 63) // 64 + (ntok - n_t + 63) // 64
             nwg = nqb * H * S
-            buf = (ctypes.c_ulonglong * (nwg * 6))()
-            L.check(L.LIB.mmt_attn_stamps(buf, nwg * 6), "stamps")
-            st = np.frombuffer(buf, dtype=np.uint64).reshape(S, H, nqb, 6).astype(np.int64)
+            buf = (ctypes.c_ulonglong * (nwg * 8))()
+            L.check(L.LIB.mmt_attn_stamps(buf, nwg * 8), "stamps")
+            st = np.frombuffer(buf, dtype=np.uint64).reshape(S, H, nqb, 8).astype(np.int64)
             freq = float(np.median((st[..., 4] - st[..., 1]) / np.maximum(st[..., 5] - st[..., 0], 1))) * 100.0
             for kind, sl in (("tmpl", slice(0, (n_t + 63) // 64)), ("search", slice((n_t + 63) // 64, nqb))):
                 x = st[:, :, sl].reshape(-1, 6)

@@ -2,7 +2,8 @@
 """Per-phase timing of the LDS-DMA GEMM from in-kernel timestamps (stamp build of tools/build_ablate.sh).
 
 Phases per workgroup (leader thread): prologue = start -> first K-step landed (DMA latency + address
-setup); loop = the K loop; epilogue = loop end -> stores retired.  Cycle counts come from s_memtime;
+setup); loop = the K loop; epilogue = loop end -> stores retired, split into the accumulator tile's LDS
+assembly (+ barriers), the strip passes (loads, epilogue math, stores issued) and the store drain.  Cycle counts come from s_memtime;
 start / end skew across workgroups from s_memrealtime (100 MHz).
 
 usage: MMT_HIP_LIB=.../_lib/stamp/libmmt_hip.so python tools/gemm_stamps.py
@@ -21,7 +22,8 @@ import torch  # noqa: E402
 from mmt_amd import _lib as L  # noqa: E402
 
 SHAPES = [("qkv", 2, 528, 2304, 768, 0, 0), ("proj", 2, 528, 768, 768, 0, 1), ("fc1", 2, 528, 3072, 768, 1, 0),
-          ("fc2", 2, 528, 768, 3072, 0, 1), ("qkv_ln", 2, 528, 2304, 768, 0, 0), ("fc1_ln", 2, 528, 3072, 768, 1, 0)]
+          ("fc2", 2, 528, 768, 3072, 0, 1), ("qkv_ln", 2, 528, 2304, 768, 0, 0), ("fc1_ln", 2, 528, 3072, 768, 1, 0),
+          ("qkv_ln2", 2, 528, 2304, 768, 0, 0), ("fc1_ln2", 2, 528, 3072, 768, 1, 0)]
 TILES = {1: (128, 128), 2: (128, 64), 3: (64, 64), 4: (128, 128)}
 
 
@@ -41,25 +43,30 @@ def main():
             p.lda, p.ldc, p.ldr = K, N, N
             p.a_seg_rows, p.a_segs_a = M, 1
             p.M, p.N, p.K, p.act, p.c_f32, p.groups, p.impl = M, N, K, act, 1 if res else 0, G, impl
-            if name.endswith("_ln"):
-                p.ln_fold, p.ln_eps = 1, 1e-6
+            if "_ln" in name:  # _ln: statistics in the K loop; _ln2: handed in (ln_stats_in)
+                p.ln_fold, p.ln_eps = (2 if name.endswith("_ln2") else 1), 1e-6
+                stats = torch.ones(G, M, 2 * (K // 64), device="cuda")
                 for g in range(G):
                     p.ln_colsum[g] = b[g].data_ptr()
+                    p.ln_stats_in[g] = stats[g].data_ptr()
             s = torch.cuda.current_stream().cuda_stream
             for _ in range(10):
                 L.check(L.LIB.mmt_gemm(ctypes.byref(p), L.MMT_BF16, s), name)
             torch.cuda.synchronize()
             bm, bn = TILES[impl]
             nwg = ((M + bm - 1) // bm) * ((N + bn - 1) // bn) * G
-            buf = (ctypes.c_ulonglong * (nwg * 6))()
-            L.check(L.LIB.mmt_gemm_stamps(buf, nwg * 6), "stamps")
-            st = np.frombuffer(buf, dtype=np.uint64).reshape(nwg, 6).astype(np.int64)
-            rt0, c0, c1, c2, c3, rt1 = st.T
+            buf = (ctypes.c_ulonglong * (nwg * 8))()
+            L.check(L.LIB.mmt_gemm_stamps(buf, nwg * 8), "stamps")
+            st = np.frombuffer(buf, dtype=np.uint64).reshape(nwg, 8).astype(np.int64)
+            rt0, c0, c1, c2, e1, e2, c3, rt1 = st.T
             freq = np.median((c3 - c0) / np.maximum(rt1 - rt0, 1)) * 100.0  # MHz (realtime = 100 MHz)
             row = {"gemm": name, "impl": impl, "nwg": nwg, "clock_mhz": round(float(freq), 0),
                    "prologue_us": round(float(np.median(c1 - c0)) / freq, 2),
                    "loop_us": round(float(np.median(c2 - c1)) / freq, 2),
                    "epilogue_us": round(float(np.median(c3 - c2)) / freq, 2),
+                   "epi_lds_tile_us": round(float(np.median(e1 - c2)) / freq, 2),
+                   "epi_passes_us": round(float(np.median(e2 - e1)) / freq, 2),
+                   "epi_store_drain_us": round(float(np.median(c3 - e2)) / freq, 2),
                    "wg_total_us_med": round(float(np.median(c3 - c0)) / freq, 2),
                    "wg_total_us_max": round(float(np.max(c3 - c0)) / freq, 2),
                    "start_spread_us": round(float(rt0.max() - rt0.min()) / 100.0, 2),
