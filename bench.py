@@ -72,7 +72,9 @@ GEO_B = {"hidden": 768, "depth": 12, "search": 320, "template": 128}
 GEO_L = {"hidden": 1024, "depth": 24, "search": 384, "template": 192}
 VARIANT_NAMES = {"rgbt": "mixformer_vit_rgbt (two-stream)", "shared": "mixformer_vit_rgbt_shared",
                  "asym": "asymmetric_shared", "asym_online": "asymmetric_shared_online_score",
-                 "asym_ce": "asymmetric_shared_ce (candidate elimination 3/6/9 x0.7)"}
+                 "asym_ce": "asymmetric_shared_ce (candidate elimination 3/6/9 x0.7)",
+                 "rgb": "mixformer_vit (RGB-only, BASELINE config 1)"}
+GEO_RGB = {"hidden": 768, "depth": 12, "search": 288, "template": 128}  # config 1: MixViT-B 128/288
 
 
 def state_dict_keys(variant, hidden=768, depth=12, search=320, template=128, fusion_layers=2):
@@ -401,7 +403,8 @@ def main():
     from mmt_amd.runtime import MixFormerRGBTRuntime
 
     dtype = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(args.dtype, torch.float32)
-    geo = GEO_L if args.vitl else GEO_B
+    geo = GEO_L if args.vitl else (GEO_RGB if args.variant == "rgb" else GEO_B)
+    nmod = 1 if args.variant == "rgb" else 2  # modalities per frame
     keys = state_dict_keys(args.variant, **geo)
     sd = {k: torch.from_numpy(v) for k, v in synthetic.synth_state_dict(keys).items()}
     rt = MixFormerRGBTRuntime(sd, args.variant, dtype=dtype)
@@ -415,6 +418,7 @@ def main():
             t, o, s = sequence_inputs(range(lo, hi), i, geo["template"], geo["search"])
         else:
             t, o, s = synthetic.synth_inputs(B, geo["template"], geo["search"], seed=seed)
+        t, o, s = t[:nmod], o[:nmod], s[:nmod]
         pool.append(([x.cuda() for x in t], [x.cuda() for x in o], [x.cuda() for x in s]))
     use_graph = not args.no_graph
     # one hipGraph per resident input set: the patch staging reads that set in place (zero-copy)
@@ -466,7 +470,7 @@ def main():
                                        "replicas x%d" % world if world > 1 else "single"),
                        "hip_graph": use_graph},
             "roofline": dom,
-            "roofline_mam": mam_memory_roofline(mam, 2 * B, rt.d.ntok, rt.d.C, 4 if args.dtype == "f32" else 2),
+            "roofline_mam": mam_memory_roofline(mam, nmod * B, rt.d.ntok, rt.d.C, 4 if args.dtype == "f32" else 2),
             "device_ms_per_step_sum": round(dev_ms, 4) if dev_ms else None, "launches_per_step": len(plan),
             "kernels": {k: {"us": round(a["t"] * 1e3 / a["n"], 2), "n": a["n"],
                             "tflops": round(a["flops"] / a["n"] / (a["t"] / a["n"] * 1e-3) / 1e12, 1) if a["flops"] else None}

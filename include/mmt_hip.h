@@ -69,7 +69,8 @@ extern "C" {
  *                                  same with a1[g] and k - k_split       (k >= k_split)
  * A addressing (conv mode, conv_h > 0): NHWC implicit im2col of a 3x3/pad-1 (conv_k3=1) or 1x1
  *   conv producing a conv_h x conv_h map; the input map is conv_h/conv_up square, pixel stride
- *   lda (channels are contiguous, conv_cin of them), k = (ky*3+kx)*conv_cin + ci.
+ *   lda (channels are contiguous, conv_cin of them), k = (ky*3+kx)*conv_cin + ci; consecutive
+ *   input images a_stride_a pixels apart (0: packed, (conv_h/conv_up)^2).
  * Epilogue: v = act(acc + bias) with act 0 none / 1 GELU(erf) / 2 ReLU;
  *   c2 == NULL: C = v (+ R if r != NULL);  c2 != NULL: C = v, C2 = v + R (c2_copy: C = v (+ R),
  *   C2 = the same values in `dtype`).
@@ -208,7 +209,8 @@ int mmt_add_cast(const float* in, const float* add, int64_t add_n, float* out_f3
 
 /* Patch staging for the 16x16/s16 patch-embed conv: for each of S = 2*Bm sequences
  * (modality m = s / Bm, batch b = s % Bm) the row block [tmpl | online | search] of tokens, each row
- * = (c, ky, kx) flattened (3*P*P), from fp32 NCHW images img_t[m], img_o[m], img_s[m]. */
+ * = (c, ky, kx) flattened (3*P*P), from fp32 NCHW images img_t[m], img_o[m], img_s[m].  With
+ * img_t1 = img_o1 = img_s1 = NULL: one modality, S = Bm (RGB-only MixFormer). */
 int mmt_patch_im2col(const float* img_t0, const float* img_t1, const float* img_o0, const float* img_o1,
                      const float* img_s0, const float* img_s1, void* out, int Bm, int ht, int hs, int patch,
                      int dtype, void* stream);

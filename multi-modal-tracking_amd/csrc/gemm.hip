@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256 * KS) void gemm_kernel(const mmt_gemm_params p)
             const int b = m / hw, rem = m - b * hw;
             ay[i] = rem / ch;
             ax[i] = rem - ay[i] * ch;
-            aoff[i] = (int64_t)b * hi * hi;
+            aoff[i] = (int64_t)b * (p.a_stride_a > 0 ? p.a_stride_a : (int64_t)hi * hi);  // image pitch (pixels)
         }
     }
 #pragma unroll

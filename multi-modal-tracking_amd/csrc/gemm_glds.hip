@@ -142,7 +142,7 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
             const int b = m / (ch * ch), rem = m - b * ch * ch;
             ay[i] = rem / ch;
             ax[i] = rem - ay[i] * ch;
-            aoff[i] = (int64_t)b * hi * hi;
+            aoff[i] = (int64_t)b * (p.a_stride_a > 0 ? p.a_stride_a : (int64_t)hi * hi);  // image pitch (pixels)
         }
     }
 #pragma unroll
@@ -593,7 +593,8 @@ int mmt_gemm_glds(const mmt_gemm_params& p, hipStream_t st, int force) {
         const int cup = p.conv_up, hi = p.conv_up > 0 ? p.conv_h / p.conv_up : 0;
         if (cup <= 0 || (cup & (cup - 1)) || hi * cup != p.conv_h) return 1;
         const int64_t imgs = (p.M + (int64_t)p.conv_h * p.conv_h - 1) / ((int64_t)p.conv_h * p.conv_h);
-        if ((imgs * hi * hi * (int64_t)p.lda + p.K) >= ((int64_t)1 << 32) || p.K >= (1 << 24)) return 1;
+        const int64_t pitch = p.a_stride_a > 0 ? p.a_stride_a : (int64_t)hi * hi;
+        if ((imgs * pitch * (int64_t)p.lda + p.K) >= ((int64_t)1 << 32) || p.K >= (1 << 24)) return 1;
     }
     if (p.lda % 8 || p.a_stride_a % 8 || p.a_stride_b % 8 || p.k_split % 8) return 1;
     if (p.a_seg_rows > INT32_MAX || p.a_segs_a > INT32_MAX) return 1;

@@ -262,10 +262,13 @@ extern "C" int mmt_add_cast(const float* in, const float* add, int64_t add_n, fl
 extern "C" int mmt_patch_im2col(const float* img_t0, const float* img_t1, const float* img_o0, const float* img_o1,
                                 const float* img_s0, const float* img_s1, void* out, int Bm, int ht, int hs, int patch,
                                 int dtype, void* stream) {
-    if (!img_t0 || !img_t1 || !img_o0 || !img_o1 || !img_s0 || !img_s1 || !out || Bm <= 0) return MMT_EBADARG;
+    // one modality (the RGB-only MixFormer, lib/models/mixformer_vit): img_t1 = img_o1 = img_s1 = NULL
+    const int nmod = (!img_t1 && !img_o1 && !img_s1) ? 1 : 2;
+    if (!img_t0 || !img_o0 || !img_s0 || !out || Bm <= 0) return MMT_EBADARG;
+    if (nmod == 2 && (!img_t1 || !img_o1 || !img_s1)) return MMT_EBADARG;
     if (patch % 4 || ht % patch || hs % patch) return MMT_EBADARG;
     const int gt = ht / patch, gs = hs / patch;
-    const int64_t rows = (int64_t)2 * Bm * (2 * gt * gt + gs * gs);
+    const int64_t rows = (int64_t)nmod * Bm * (2 * gt * gt + gs * gs);
     const int64_t total = rows * 3 * patch;
     dim3 grid((unsigned)((total + 255) / 256));
     hipStream_t st = (hipStream_t)stream;

@@ -1,1 +1,1 @@
-"""lib.models: only the RGB-T hot-path family (mixformer_vit_rgbt) is provided."""
+"""lib.models: the RGB-T hot-path family (mixformer_vit_rgbt) and the RGB-only MixViT (mixformer_vit, config 1)."""

@@ -26,9 +26,6 @@ import os
 import torch
 import torch.nn as nn
 
-VARIANT_OF_CLASS = {}
-
-
 # ----------------------------------------------------------------------------- parameter containers
 class PatchEmbed(nn.Module):
     def __init__(self, patch_size=16, in_chans=3, embed_dim=768):
@@ -418,6 +415,68 @@ class MixFormer_RGBT_OnlineScore(_HipTracker):
         self.score_branch = score_branch
 
 
+class MixFormer(_HipTracker):
+    """RGB-only MixFormer (lib/models/mixformer_vit/mixformer.py:285-337; BASELINE config 1): one ViT
+    with the same MAM, the corner head straight on its search tokens, no fusion.  forward takes
+    single (B,3,H,W) tensors (5-D inputs squeezed, :296-301) and returns ({"pred_boxes"}, coord);
+    set_online / forward_test are the reference's template-cache API (:308-321)."""
+
+    variant = "rgb"
+
+    def __init__(self, backbone, box_head, head_type="CORNER_UP"):
+        super().__init__(head_type)
+        self.backbone = backbone
+        self.box_head = box_head
+        # 16-bit default fp16, not bf16: without the fusion between backbone and head this model's
+        # boxes move 2.7e-2 from the reference's in bf16 and 1.8e-3 in fp16 on the golden inputs, at
+        # the same speed (profiles/r02_head_dtype_ab.jsonl); MMT_DTYPE / set_compute_dtype override
+        if "MMT_DTYPE" not in os.environ:
+            self.compute_dtype = torch.float16
+
+    @staticmethod
+    def _one(x, nm):
+        if isinstance(x, (list, tuple)):
+            raise ValueError("%s: the RGB-only MixFormer takes a (B,3,H,W) tensor, not a list" % nm)
+        return x.squeeze(0) if x.dim() == 5 else x
+
+    def _device(self, x):
+        if x.device.type != "cuda":
+            raise RuntimeError("the MI355X forward needs the inputs on the HIP device (got %s); there is no CPU path"
+                               % x.device)
+        return x.device
+
+    def forward(self, template, online_template, search, run_score_head=False, gt_bboxes=None):
+        t, o, s = self._one(template, "template"), self._one(online_template, "online_template"), self._one(search, "search")
+        if self.training and torch.is_grad_enabled():
+            raise NotImplementedError("training the RGB-only MixFormer is outside the RGB-T hot path (inference only)")
+        dev = self._device(s)
+        rt = self._runtime(dev)
+        with torch.cuda.device(dev):
+            box, _ = rt.forward([t], [o], [s], use_graph=self.use_hip_graph)
+            coord = box.clone().view(box.shape[0], 1, 4)
+        return {"pred_boxes": coord}, coord
+
+    def set_online(self, template, online_template):
+        t, o = self._one(template, "template"), self._one(online_template, "online_template")
+        dev = self._device(t)
+        rt = self._runtime(dev)
+        with torch.cuda.device(dev):
+            rt.set_template([t], [o])
+        self._online_batch = t.shape[0]
+
+    def forward_test(self, search, run_score_head=True, gt_bboxes=None):
+        s = self._one(search, "search")
+        if self._online_batch != s.shape[0]:
+            raise RuntimeError("forward_test needs set_online() with the same batch size first")
+        dev = self._device(s)
+        rt = self._runtime(dev)
+        with torch.cuda.device(dev):
+            box, _ = rt.forward_search([s])
+            coord = box.clone().view(-1, 1, 4)
+        return {"pred_boxes": coord}, coord
+
+
+
 # ----------------------------------------------------------------------------- builders
 def _vit_spec(cfg):
     if cfg.MODEL.VIT_TYPE == "large_patch16":
@@ -559,9 +618,25 @@ def build_asymmetric_shared_ce(cfg, train=True):
     return model
 
 
+def build_mixformer_vit(cfg, train=True):
+    """build_mixformer_vit (lib/models/mixformer_vit/mixformer.py:341-366): RGB-only MixViT with the
+    CORNER_UP head (experiments/mixformer_vit/baseline.yaml); MODEL.RGB_PRETRAINED_PATH as there."""
+    if cfg.MODEL.HEAD_TYPE != "CORNER_UP":
+        raise NotImplementedError("HEAD_TYPE %r: only CORNER_UP is implemented on MI355X" % cfg.MODEL.HEAD_TYPE)
+    bb = _backbone(cfg, False)
+    if train:
+        _load_mae(bb, cfg, False)
+    model = MixFormer(bb, _head(cfg), cfg.MODEL.HEAD_TYPE)
+    path = getattr(cfg.MODEL, "RGB_PRETRAINED_PATH", "")
+    if train and path:
+        model.load_state_dict({k: v for k, v in _load_checkpoint(path, "net").items()
+                               if "pos_embed" not in k and "mask_token" not in k}, strict=False)
+    return model
+
+
 BUILDERS = {"rgbt": build_mixformer_vit_rgbt, "shared": build_mixformer_vit_rgbt_shared,
             "asym": build_asymmetric_shared, "asym_online": build_asymmetric_shared_online_score,
-            "asym_ce": build_asymmetric_shared_ce}
+            "asym_ce": build_asymmetric_shared_ce, "rgb": build_mixformer_vit}
 
 
 def hot_path_cfg(vit="base_patch16", search=320, template=128, fusion_layers=2, hidden=None):

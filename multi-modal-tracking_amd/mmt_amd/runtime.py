@@ -28,7 +28,7 @@ import torch
 from . import _lib
 from ._lib import LIB, GemmParams, AttnParams, check, MMT_F32, MMT_BF16, MMT_F16
 
-VARIANTS = ("rgbt", "shared", "asym", "asym_online", "asym_ce")
+VARIANTS = ("rgbt", "shared", "asym", "asym_online", "asym_ce", "rgb")  # rgb: RGB-only MixFormer (config 1)
 
 
 LOG2E = 1.4426950408889634
@@ -55,11 +55,13 @@ class Dims:
         self.n_t = 2 * self.nt1
         self.ntok = self.n_t + self.ns
         self.hidden = sd[pre + "blocks.0.mlp.fc1.weight"].shape[0]
-        self.d_model = sd["fusion_vi.adjust_v.0.weight"].shape[0]
+        self.nmod = 1 if variant == "rgb" else 2  # modalities (sequences per frame)
+        fusion = self.nmod == 2  # the RGB-only model has no fusion: the head reads the backbone
+        self.d_model = sd["fusion_vi.adjust_v.0.weight"].shape[0] if fusion else 512
         self.fusion_layers = 0
-        while ("fusion_vi.fusion_attention.encoder.layers.%d.linear1.weight" % self.fusion_layers) in sd:
+        while fusion and ("fusion_vi.fusion_attention.encoder.layers.%d.linear1.weight" % self.fusion_layers) in sd:
             self.fusion_layers += 1
-        self.ffn = sd["fusion_vi.fusion_attention.encoder.layers.0.linear1.weight"].shape[0]
+        self.ffn = sd["fusion_vi.fusion_attention.encoder.layers.0.linear1.weight"].shape[0] if fusion else 1024
         self.hc = sd["box_head.conv1_tl.0.weight"].shape[0]
         self.fh = 4 * self.gs
 
@@ -73,7 +75,7 @@ class MixFormerRGBTRuntime:
     SPLITK_FLOATS = 8 << 20  # fp32 split-K partial-tile workspace (32 MiB), shared by every plan GEMM
     SPLITK_TICKETS = 1 << 16
 
-    def __init__(self, state_dict, variant, dtype=torch.bfloat16, device="cuda", fold_ln=None, ce=None):
+    def __init__(self, state_dict, variant, dtype=torch.bfloat16, device="cuda", fold_ln=None, ce=None, head_dtype=None):
         """fold_ln (default: on for bf16): the ViT's LayerNorms are folded into the qkv / fc1 GEMMs
         (mmt_gemm_params.ln_fold) and the residual-producing GEMMs also write the bf16 copy of the
         residual stream those GEMMs read, so no LayerNorm launch or normalised tensor remains.
@@ -90,6 +92,11 @@ class MixFormerRGBTRuntime:
         self.ce = dict(zip(ce[0], ce[1])) if variant == "asym_ce" else {}
         self.dtype = dtype
         self.cdt = {torch.bfloat16: MMT_BF16, torch.float16: MMT_F16}.get(dtype, MMT_F32)
+        # storage type of the corner head's activations and weights (head_dtype; default = dtype)
+        self.hdtype = head_dtype or dtype
+        if self.hdtype not in (torch.bfloat16, torch.float16, torch.float32):
+            raise ValueError("head_dtype must be torch.bfloat16, torch.float16 or torch.float32")
+        self.hcdt = {torch.bfloat16: MMT_BF16, torch.float16: MMT_F16}.get(self.hdtype, MMT_F32)
         half = dtype in (torch.bfloat16, torch.float16)
         self.fold_ln = half if fold_ln is None else bool(fold_ln)
         if self.fold_ln and not half:
@@ -117,6 +124,9 @@ class MixFormerRGBTRuntime:
     def _F(self, x):
         return x.detach().to(self.device, torch.float32).contiguous()
 
+    def _TH(self, x):  # head storage type
+        return x.detach().to(self.device, self.hdtype).contiguous()
+
     def _fold(self, sd, name):
         """conv() block (head.py:7-20): Conv3x3 -> BatchNorm2d(eval) -> ReLU, BN folded."""
         w = sd[name + ".0.weight"].double()
@@ -132,6 +142,7 @@ class MixFormerRGBTRuntime:
         d, W = self.d, self.w
         C = d.C
         pres = ["backbone_v.", "backbone_i."] if self.variant == "rgbt" else ["backbone."]
+        single_ln = self.variant in ("rgbt", "rgb")  # norm1 / norm2 (else per-modality norm*_v / norm*_i)
         W["bb"] = []
         for pre in pres:
             bb = {"patch_w": self._T(sd[pre + "patch_embed.proj.weight"].reshape(C, -1)),
@@ -145,7 +156,7 @@ class MixFormerRGBTRuntime:
                 for nm in ("attn.qkv", "attn.proj", "mlp.fc1", "mlp.fc2"):
                     blk[nm + ".w"] = self._T(sd[b + nm + ".weight"])
                     blk[nm + ".b"] = self._F(sd[b + nm + ".bias"])
-                if self.variant == "rgbt":
+                if single_ln:
                     for nm in ("norm1", "norm2"):
                         blk[nm] = (self._F(sd[b + nm + ".weight"]), self._F(sd[b + nm + ".bias"]))
                 else:
@@ -156,7 +167,7 @@ class MixFormerRGBTRuntime:
                     # Linear(LayerNorm(x)) = rstd*(x.W' - mu*colsum(W')) + b', W' = W*gamma (per k),
                     # b' = b + W.beta; one (W', colsum, b') per norm (two-stream: this backbone's;
                     # shared: norm*_v / norm*_i -> one GEMM group per modality)
-                    norms = ["", ] if self.variant == "rgbt" else ["_v", "_i"]
+                    norms = ["", ] if single_ln else ["_v", "_i"]
                     for lin, nm in (("attn.qkv", "norm1"), ("mlp.fc1", "norm2")):
                         w64, b64 = sd[b + lin + ".weight"].double(), sd[b + lin + ".bias"].double()
                         if lin == "attn.qkv":
@@ -175,7 +186,12 @@ class MixFormerRGBTRuntime:
                         blk[lin + ".fw"], blk[lin + ".fcs"], blk[lin + ".fb"] = fw, fc, fb
                 bb["blocks"].append(blk)
             W["bb"].append(bb)
-        # fusion
+        self._prepare_fusion(sd) if d.nmod == 2 else None
+        self._prepare_head(sd)
+
+    def _prepare_fusion(self, sd):
+        d, W = self.d, self.w
+        C = d.C
         f = "fusion_vi."
         for m in ("v", "i"):
             W["adj_" + m + ".w"] = self._T(sd[f + "adjust_%s.0.weight" % m].reshape(d.d_model, C))
@@ -215,6 +231,10 @@ class MixFormerRGBTRuntime:
             dm = d.d_model
             pw = sum((pos64 + le64[l]) @ w64[:, l * dm:(l + 1) * dm].t() for l in range(2)) + b64
             e["offw.pos"] = self._F(pw.float())  # [ns][192]
+
+    def _prepare_head(self, sd):
+        d, W = self.d, self.w
+        C = d.C
         # corner head
         h = "box_head."
         ws, bs = [], []
@@ -222,21 +242,21 @@ class MixFormerRGBTRuntime:
             w_, b_ = self._fold(sd, h + nm)
             ws.append(w_)
             bs.append(b_)
-        W["h0.w"], W["h0.b"] = self._T(torch.cat(ws, 0)), self._F(torch.cat(bs, 0))
+        W["h0.w"], W["h0.b"] = self._TH(torch.cat(ws, 0)), self._F(torch.cat(bs, 0))
         for nm in ("conv2", "conv3", "conv4"):
             for br in ("tl", "br"):
                 w_, b_ = self._fold(sd, h + nm + "_" + br)
-                W[nm + "_" + br + ".w"], W[nm + "_" + br + ".b"] = self._T(w_), self._F(b_)
+                W[nm + "_" + br + ".w"], W[nm + "_" + br + ".b"] = self._TH(w_), self._F(b_)
         for br in ("tl", "br"):
             for nm, idx in (("adjust3", 0), ("adjust3", 1), ("adjust4", 0)):
                 w_, b_ = self._fold(sd, h + "%s_%s.%d" % (nm, br, idx))
-                W["%s.%d_%s.w" % (nm, idx, br)], W["%s.%d_%s.b" % (nm, idx, br)] = self._T(w_), self._F(b_)
+                W["%s.%d_%s.w" % (nm, idx, br)], W["%s.%d_%s.b" % (nm, idx, br)] = self._TH(w_), self._F(b_)
         c1 = []
         for nm in ("adjust3_tl.2", "adjust3_br.2", "adjust4_tl.1", "adjust4_br.1"):
             c1.append(self._fold(sd, h + nm))
-        W["a3c1.w"] = self._T(torch.stack([c1[0][0][0], c1[1][0][0]]))
+        W["a3c1.w"] = self._TH(torch.stack([c1[0][0][0], c1[1][0][0]]))
         W["a3c1.b"] = self._F(torch.stack([c1[0][1][0], c1[1][1][0]]))
-        W["a4c1.w"] = self._T(torch.stack([c1[2][0][0], c1[3][0][0]]))
+        W["a4c1.w"] = self._TH(torch.stack([c1[2][0][0], c1[3][0][0]]))
         W["a4c1.b"] = self._F(torch.stack([c1[2][1][0], c1[3][1][0]]))
         W["c5.w"] = self._F(torch.stack([sd[h + "conv5_tl.weight"].reshape(-1), sd[h + "conv5_br.weight"].reshape(-1)]))
         W["c5.b"] = self._F(torch.cat([sd[h + "conv5_tl.bias"], sd[h + "conv5_br.bias"]]))
@@ -266,26 +286,27 @@ class MixFormerRGBTRuntime:
         if B in self._ws:
             return self._ws[B]
         d = self.d
-        dev, dt, f32 = self.device, self.dtype, torch.float32
-        S, R, C = 2 * B, 2 * B * d.ntok, d.C
+        dev, dt, f32, ht = self.device, self.dtype, torch.float32, self.hdtype
+        S, R, C = d.nmod * B, d.nmod * B * d.ntok, d.C
         ns, dm, hc = d.ns, d.d_model, d.hc
         e = lambda *shape, t=dt: torch.empty(*shape, device=dev, dtype=t)  # noqa: E731
         ws = {
             "B": B,
-            "in_t": [e(B, 3, d.ht, d.ht, t=f32) for _ in range(2)],
-            "in_o": [e(B, 3, d.ht, d.ht, t=f32) for _ in range(2)],
-            "in_s": [e(B, 3, d.hs, d.hs, t=f32) for _ in range(2)],
+            "in_t": [e(B, 3, d.ht, d.ht, t=f32) for _ in range(d.nmod)],
+            "in_o": [e(B, 3, d.ht, d.ht, t=f32) for _ in range(d.nmod)],
+            "in_s": [e(B, 3, d.hs, d.hs, t=f32) for _ in range(d.nmod)],
             "PATCH": e(R, 3 * d.patch * d.patch), "X": e(R, C, t=f32), "XN": e(R, C), "QKV": e(R, 3 * C),
             "AO": e(R, C), "HID": e(R, d.hidden), "XT": e(R, C),
             "LNST": e(R, 2 * (C // 64), t=f32),  # LayerNorm row statistics of XN, per 64 columns
             "Y1": e(2, B * ns, dm, t=f32), "SRC": e(2, B * ns, dm, t=f32), "SRCT": e(2, B * ns, dm),
             "VAL": e(2, B * ns, dm), "OFFW": e(B * ns, 192, t=f32), "MS": e(B * ns, dm),
             "SRC2": e(B * ns, dm, t=f32), "H2": e(2 * B * ns, d.ffn), "Y2": e(B * ns, C, t=f32),
-            "FUS": e(B * ns, C, t=f32), "FUST": e(B * ns, C),
-            "H0": e(B * ns, 2 * hc + hc + hc // 2), "X2": e(2, B * ns, hc // 2), "S1": e(2, B * ns, hc // 2),
-            "X3": e(2, B * 4 * ns, hc // 4), "S2": e(2, B * 4 * ns, hc // 4), "X4": e(2, B * 16 * ns, hc // 8),
-            "A3a": e(2, B * ns, hc // 4), "A3b": e(2, B * ns, hc // 8), "A3": e(2, B, ns, t=f32),
-            "A4a": e(2, B * 4 * ns, hc // 8), "A4": e(2, B, 4 * ns, t=f32),
+            "FUS": e(B * ns, C, t=f32), "FUST": e(B * ns, C, t=ht),
+            "H0": e(B * ns, 2 * hc + hc + hc // 2, t=ht), "X2": e(2, B * ns, hc // 2, t=ht),
+            "S1": e(2, B * ns, hc // 2, t=ht), "X3": e(2, B * 4 * ns, hc // 4, t=ht), "S2": e(2, B * 4 * ns, hc // 4, t=ht),
+            "X4": e(2, B * 16 * ns, hc // 8, t=ht), "A3a": e(2, B * ns, hc // 4, t=ht), "A3b": e(2, B * ns, hc // 8, t=ht),
+            "A3": e(2, B, ns, t=f32), "A4a": e(2, B * 4 * ns, hc // 8, t=ht), "A4": e(2, B, 4 * ns, t=f32),
+            "XH": e(R, C, t=ht) if d.nmod == 1 else None,  # RGB-only: the head's input in the head type
             "BOX": e(B, 4, t=f32), "XYXY": e(B, 4, t=f32), "ROIS": e(B, 5, t=f32),
             "MAPS": e(2, B, d.fh * d.fh, t=f32),
         }
@@ -367,9 +388,10 @@ class MixFormerRGBTRuntime:
         [S*ntok][3C] buffer per layer (None: the one QKV buffer, reused by every layer)."""
         d, W, B = self.d, self.w, ws["B"]
         C, ntok = d.C, d.ntok
-        S = 2 * B
+        S = d.nmod * B
         R = S * ntok
         two = self.variant == "rgbt"
+        nm_ = d.nmod  # modality groups of the per-modality LayerNorm GEMMs (1 for the RGB-only model)
         P = _ptr
         X, XN, AO, HID = ws["X"], ws["XN"], ws["AO"], ws["HID"]
         cdt = self.cdt
@@ -391,8 +413,8 @@ class MixFormerRGBTRuntime:
         hand = fold and part is None and not self.ce
         nst = 2 * (C // 64)
         LNST = ws["LNST"]
-        plan.append((LIB.mmt_patch_im2col, tuple(P(t) for t in ws["in_t"]) + tuple(P(t) for t in ws["in_o"])
-                     + tuple(P(t) for t in ws["in_s"]) + (P(ws["PATCH"]), B, d.ht, d.hs, d.patch, cdt), "patch_im2col", None))
+        plan.append((LIB.mmt_patch_im2col, self._image_args(ws["in_t"], ws["in_o"], ws["in_s"])
+                     + (P(ws["PATCH"]), B, d.ht, d.hs, d.patch, cdt), "patch_im2col", None))
         KP = 3 * d.patch * d.patch
         gm = B * nr  # rows per modality group
         cp = dict(c2_copy=1) if fold else {}
@@ -429,13 +451,13 @@ class MixFormerRGBTRuntime:
                 Mg = gm
             else:
                 blk = W["bb"][0]["blocks"][i]
-                n1 = [blk["norm1_v"], blk["norm1_i"]]
-                n2 = [blk["norm2_v"], blk["norm2_i"]]
+                n1 = [blk["norm1"]] * 2 if nm_ == 1 else [blk["norm1_v"], blk["norm1_i"]]
+                n2 = [blk["norm2"]] * 2 if nm_ == 1 else [blk["norm2_v"], blk["norm2_i"]]
                 wl = lambda nm: [P(blk[nm])]  # noqa: E731
-                fl = lambda nm: [P(blk[nm][m]) for m in range(2)]  # noqa: E731
+                fl = lambda nm: [P(blk[nm][m]) for m in range(nm_)]  # noqa: E731
                 rows = lambda t, k: [at(t, k)]  # noqa: E731
                 Mg = S * nr
-            rows2 = lambda t, k: [at(t, k, 0), at(t, k, 1)]  # noqa: E731  (one group per modality)
+            rows2 = lambda t, k: [at(t, k, g) for g in range(nm_)]  # noqa: E731  (one group per modality)
             if fold:  # LayerNorm 1 folded into qkv: A = XN = bf16 copy of the residual stream X
                 self._gemm(plan, "qkv", a=rows2(XN, C), w=fl("attn.qkv.fw"), c=rows2(QKV, 3 * C), M=gm, N=3 * C,
                            K=C, lda=C, ldc=3 * C, bias=fl("attn.qkv.fb"), ln_colsum=fl("attn.qkv.fcs"), ln_eps=1e-6,
@@ -494,6 +516,13 @@ class MixFormerRGBTRuntime:
                        **rmap(d.hidden))
         return (X, stage)
 
+    def _image_args(self, t, o, s):
+        """mmt_patch_im2col's six image pointers (t0, t1, o0, o1, s0, s1); the RGB-only model passes
+        NULL for the second modality."""
+        if self.d.nmod == 1:
+            return (_ptr(t[0]), None, _ptr(o[0]), None, _ptr(s[0]), None)
+        return tuple(_ptr(x) for x in list(t) + list(o) + list(s))
+
     def _plan_tail(self, plan, ws, score, xf=None, spm_kv1=True):
         """Fusion, corner head (and score head) on the backbone output's search rows.  xf = (the fp32
         stream holding the backbone output, elimination stages run) from _plan_backbone."""
@@ -516,7 +545,15 @@ class MixFormerRGBTRuntime:
             XT = XN  # the last fc2 already wrote the bf16 copy of the backbone output
         else:
             XT = ws["XT"]
-            plan.append((LIB.mmt_add_cast, (P(X), None, 0, None, P(XT), R * C, cdt), "cast_x", None))
+            plan.append((LIB.mmt_add_cast, (P(X), None, 0, None, P(XT), d.nmod * B * ntok * C, cdt), "cast_x", None))
+        if d.nmod == 1:  # RGB-only: the corner head reads the backbone's search tokens (an NHWC gs x gs
+            # image every ntok rows: the conv's image pitch), mixformer_vit/mixformer.py:304-305
+            if self.hdtype != self.dtype or not fold:  # the head's own storage type, from the fp32 stream
+                XT = ws["XH"]
+                plan.append((LIB.mmt_add_cast, (P(X), None, 0, None, P(XT), B * ntok * C, self.hcdt), "cast_head_in",
+                             None))
+            self._plan_head(plan, ws, score, P(XT, d.n_t * C), C, (max(B * ns, 1), 1, ntok, 0))
+            return plan
         # --- fusion: adjust_v / adjust_i (1x1 conv on the search tokens) + GroupNorm
         Y1, SRC, SRCT, VAL = ws["Y1"], ws["SRC"], ws["SRCT"], ws["VAL"]
         Mf = B * ns
@@ -549,40 +586,51 @@ class MixFormerRGBTRuntime:
         self._gemm(plan, "fusion_adjust_cat", a=[P(SRCT)], a1=[P(SRCT, Mf * dm)], k_split=dm, w=[P(W["adj_cat.w"])],
                    c=[P(ws["Y2"])], M=Mf, N=C, K=2 * dm, lda=dm, ldc=C, bias=[P(W["adj_cat.b"])], c_f32=1)
         plan.append((LIB.mmt_groupnorm, (P(ws["Y2"]), P(ws["FUS"]), P(ws["FUST"]), P(W["adj_cat.gn"][0]),
-                                         P(W["adj_cat.gn"][1]), None, None, B, B, ns, C, 32, 1e-5, cdt),
+                                         P(W["adj_cat.gn"][1]), None, None, B, B, ns, C, 32, 1e-5, self.hcdt),
                      "fusion_gn_cat", None))
+        self._plan_head(plan, ws, score, P(ws["FUST"]), C, None, spm_kv1)
+        return plan
+
+    def _plan_head(self, plan, ws, score, a_ptr, lda, seg, spm_kv1=True):
+        """Corner head (head.py:147-212) on the NHWC map at a_ptr (pixel stride lda; seg = the conv
+        input's image pitch for the RGB-only model), then the score head."""
+        d, W, B = self.d, self.w, ws["B"]
+        C, ns = d.C, d.ns
+        P = _ptr
+        cdt = self.hcdt  # the head's storage type (head_dtype)
+        hg = lambda *a, **k: self._gemm(*a, dtype=cdt, **k)  # noqa: E731
         # --- corner head (NHWC implicit-GEMM convs, BN folded, upsampling folded into addressing)
         hc, gs = d.hc, d.gs
         H0 = ws["H0"]
         n0 = 2 * hc + hc + hc // 2
-        self._gemm(plan, "head_conv1_adj12", a=[P(ws["FUST"])], w=[P(W["h0.w"])], c=[P(H0)], M=B * ns, N=n0, K=9 * C,
-                   lda=C, ldc=n0, bias=[P(W["h0.b"])], act=2, conv=(gs, 1, C, 1))
+        hg(plan, "head_conv1_adj12", a=[a_ptr], w=[P(W["h0.w"])], c=[P(H0)], M=B * ns, N=n0, K=9 * C,
+                   lda=lda, ldc=n0, bias=[P(W["h0.b"])], act=2, conv=(gs, 1, C, 1), seg=seg)
         h2, h4, h8 = hc // 2, hc // 4, hc // 8
         X2, S1, X3, S2, X4 = ws["X2"], ws["S1"], ws["X3"], ws["S2"], ws["X4"]
         br = ("tl", "br")
-        self._gemm(plan, "head_conv2", a=[P(H0, g * hc) for g in range(2)], w=[P(W["conv2_%s.w" % b]) for b in br],
+        hg(plan, "head_conv2", a=[P(H0, g * hc) for g in range(2)], w=[P(W["conv2_%s.w" % b]) for b in br],
                    c=[P(X2, g * B * ns * h2) for g in range(2)], c2=[P(S1, g * B * ns * h2) for g in range(2)],
                    r=[P(H0, 2 * hc + g * h2) for g in range(2)], ldr=n0, r_t=1, M=B * ns, N=h2, K=9 * hc, lda=n0,
                    ldc=h2, bias=[P(W["conv2_%s.b" % b]) for b in br], act=2, conv=(gs, 1, hc, 1))
-        self._gemm(plan, "head_conv3", a=[P(S1, g * B * ns * h2) for g in range(2)], w=[P(W["conv3_%s.w" % b]) for b in br],
+        hg(plan, "head_conv3", a=[P(S1, g * B * ns * h2) for g in range(2)], w=[P(W["conv3_%s.w" % b]) for b in br],
                    c=[P(X3, g * B * 4 * ns * h4) for g in range(2)], c2=[P(S2, g * B * 4 * ns * h4) for g in range(2)],
                    r=[P(H0, 2 * hc + hc + g * h4) for g in range(2)], ldr=n0, r_t=1, r_mode=2, r_p0=2 * gs, r_p1=2,
                    M=B * 4 * ns, N=h4, K=9 * h2, lda=h2, ldc=h4, bias=[P(W["conv3_%s.b" % b]) for b in br], act=2,
                    conv=(2 * gs, 2, h2, 1))
-        self._gemm(plan, "head_conv4", a=[P(S2, g * B * 4 * ns * h4) for g in range(2)], w=[P(W["conv4_%s.w" % b]) for b in br],
+        hg(plan, "head_conv4", a=[P(S2, g * B * 4 * ns * h4) for g in range(2)], w=[P(W["conv4_%s.w" % b]) for b in br],
                    c=[P(X4, g * B * 16 * ns * h8) for g in range(2)], M=B * 16 * ns, N=h8, K=9 * h4, lda=h4, ldc=h8,
                    bias=[P(W["conv4_%s.b" % b]) for b in br], act=2, conv=(4 * gs, 2, h4, 1))
-        self._gemm(plan, "head_adjust3_0", a=[P(X2, g * B * ns * h2) for g in range(2)],
+        hg(plan, "head_adjust3_0", a=[P(X2, g * B * ns * h2) for g in range(2)],
                    w=[P(W["adjust3.0_%s.w" % b]) for b in br], c=[P(ws["A3a"], g * B * ns * h4) for g in range(2)],
                    M=B * ns, N=h4, K=9 * h2, lda=h2, ldc=h4, bias=[P(W["adjust3.0_%s.b" % b]) for b in br], act=2,
                    conv=(gs, 1, h2, 1))
-        self._gemm(plan, "head_adjust3_1", a=[P(ws["A3a"], g * B * ns * h4) for g in range(2)],
+        hg(plan, "head_adjust3_1", a=[P(ws["A3a"], g * B * ns * h4) for g in range(2)],
                    w=[P(W["adjust3.1_%s.w" % b]) for b in br], c=[P(ws["A3b"], g * B * ns * h8) for g in range(2)],
                    M=B * ns, N=h8, K=9 * h4, lda=h4, ldc=h8, bias=[P(W["adjust3.1_%s.b" % b]) for b in br], act=2,
                    conv=(gs, 1, h4, 1))
         plan.append((LIB.mmt_conv3x3_c1, (P(ws["A3b"]), P(W["a3c1.w"]), P(W["a3c1.b"]), P(ws["A3"]), 2, B, gs, h8, h8,
                                           cdt), "head_adjust3_2", None))
-        self._gemm(plan, "head_adjust4_0", a=[P(X3, g * B * 4 * ns * h4) for g in range(2)],
+        hg(plan, "head_adjust4_0", a=[P(X3, g * B * 4 * ns * h4) for g in range(2)],
                    w=[P(W["adjust4.0_%s.w" % b]) for b in br], c=[P(ws["A4a"], g * B * 4 * ns * h8) for g in range(2)],
                    M=B * 4 * ns, N=h8, K=9 * h4, lda=h4, ldc=h8, bias=[P(W["adjust4.0_%s.b" % b]) for b in br], act=2,
                    conv=(2 * gs, 1, h4, 1))
@@ -593,7 +641,6 @@ class MixFormerRGBTRuntime:
                                                  float(gs), B, d.fh, h8, 4, cdt), "corner_softargmax", None))
         if score:
             self._plan_spm(plan, ws, spm_kv1)
-        return plan
 
     def _plan_spm_kv1(self, plan, ws):
         """K/V of the score decoder's second memory: the first template's tokens of both modalities
@@ -698,7 +745,7 @@ class MixFormerRGBTRuntime:
         ws = self.workspace(B)
         if "plan_t" not in ws:
             d = self.d
-            ws["QKVL"] = [torch.empty(2 * B * d.ntok, 3 * d.C, device=self.device, dtype=self.dtype)
+            ws["QKVL"] = [torch.empty(d.nmod * B * d.ntok, 3 * d.C, device=self.device, dtype=self.dtype)
                           for _ in range(d.depth)]
             ws["plan_t"] = []
             self._plan_backbone(ws["plan_t"], ws, "t", ws["QKVL"])
@@ -756,7 +803,8 @@ class MixFormerRGBTRuntime:
         for src, dst in zip(srcs, ws["in_t"] + ws["in_o"] + ws["in_s"]):
             if src.shape != dst.shape or src.dtype != torch.float32 or not src.is_contiguous() or src.device != dst.device:
                 raise ValueError("zero-copy inputs must be contiguous fp32 %s tensors on %s" % (tuple(dst.shape), dst.device))
-        new_args = tuple(_ptr(x) for x in srcs) + args[6:]
+        n = self.d.nmod
+        new_args = self._image_args(srcs[:n], srcs[n:2 * n], srcs[2 * n:]) + args[6:]
         return [(fn, new_args, name, srcs)] + base[1:]
 
     def capture_plan(self, plan):

@@ -5,6 +5,8 @@ Functional restatement, driven by a state_dict with the reference's key names, o
   shared       MixFormer_RGBT.forward           mixformer_shared.py:400-424 (modalities batch-stacked)
   asym         MixFormer_RGBT.forward           asymmetric_shared.py:349-368 (cross-modal MAM)
   asym_online  MixFormer_RGBT_OnlineScore.fwd   asymmetric_shared_online.py:351-413 (+ SPM)
+  rgb          MixFormer.forward (RGB only)     lib/models/mixformer_vit/mixformer.py:294-305, :323-337
+               (one VisionTransformer, :234-270, then the corner head on its search tokens)
 with the pieces they share:
   PatchEmbed / pos-embed / token concat          mixformer.py:29-34, :237-248
   MAM attention (template->template, search->all) mixformer.py:52-78; asymmetric_shared.py:55-104
@@ -27,7 +29,7 @@ import torch.nn.functional as F
 from .msda import ms_deform_attn
 from .prroi import prroi_pool2d
 
-VARIANTS = ("rgbt", "shared", "asym", "asym_online", "asym_ce")
+VARIANTS = ("rgbt", "shared", "asym", "asym_online", "asym_ce", "rgb")
 CE_LOC, CE_KEEP = (3, 6, 9), (0.7, 0.7, 0.7)  # lib/config/asymmetric_shared_ce/config.py:23-24
 
 
@@ -433,6 +435,19 @@ def forward(sd, variant, template, online_template, search, run_score_head=False
     with return_aux also a dict of intermediates."""
     assert variant in VARIANTS, variant
     aux = {}
+    if variant == "rgb":  # template / online_template / search: (B,3,H,W) tensors or [rgb] lists
+        one = lambda x: x[0] if isinstance(x, (list, tuple)) else x  # noqa: E731
+        _, _, sx = backbone_two_stream(sd, "backbone.", one(template), one(online_template), one(search))
+        aux["search"] = sx
+        tl, br = corner_score_maps(sd, "box_head.", sx)  # forward_box_head, mixformer.py:323-337
+        aux["score_map_tl"], aux["score_map_br"] = tl, br
+        img_sz = tl.shape[-1] * 4
+        xtl, ytl = soft_argmax(tl)
+        xbr, ybr = soft_argmax(br)
+        xyxy = torch.stack((xtl, ytl, xbr, ybr), dim=1) / img_sz
+        coord = xyxy_to_cxcywh(xyxy).view(sx.shape[0], 1, 4)
+        out = {"pred_boxes": coord}
+        return (out, coord, aux) if return_aux else (out, coord)
     if variant == "rgbt":
         tv, ov, sv = backbone_two_stream(sd, "backbone_v.", template[0], online_template[0], search[0])
         ti, oi, si = backbone_two_stream(sd, "backbone_i.", template[1], online_template[1], search[1])

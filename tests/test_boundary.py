@@ -9,11 +9,12 @@ import torch
 from conftest import GOLDEN
 
 
-@pytest.mark.parametrize("variant", ["rgbt", "shared", "asym", "asym_online", "asym_ce"])
+@pytest.mark.parametrize("variant", ["rgbt", "shared", "asym", "asym_online", "asym_ce", "rgb"])
 def test_state_dict_keys_match_reference(variant):
+    """rgb: the RGB-only MixFormer of BASELINE config 1 (lib/models/mixformer_vit, 128/288)."""
     from mmt_amd.model import reference_state_dict_shapes
     ref = json.load(open(GOLDEN + "/state_dict_%s.json" % variant))
-    ours = reference_state_dict_shapes(variant)
+    ours = reference_state_dict_shapes(variant, search=288 if variant == "rgb" else 320)
     assert [k for k, _ in ours] == [k for k, _ in ref]
     assert dict(ours) == {k: s for k, s in ref}
 
@@ -34,6 +35,8 @@ def test_lib_package_shim_exports_builders():
     from lib.models.mixformer_vit_rgbt.asymmetric_shared import build_asymmetric_shared  # noqa: F401
     from lib.models.mixformer_vit_rgbt.asymmetric_shared_online import build_asymmetric_shared_online_score  # noqa: F401
     from lib.models.mixformer_vit_rgbt.asymmetric_shared_ce import build_asymmetric_shared_ce
+    from lib.models.mixformer_vit import build_mixformer_vit  # noqa: F401
+    from lib.models.mixformer_vit.mixformer import MixFormer  # noqa: F401
 
 
 def test_ce_builder_reads_reference_config():

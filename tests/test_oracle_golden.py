@@ -55,6 +55,25 @@ def test_oracle_forward_matches_reference(weights, variant, B):
         assert np.abs(out["pred_scores"].numpy() - g["pred_scores"]).max() < 1e-5
 
 
+@pytest.mark.parametrize("B", [1, 2])
+def test_oracle_rgb_only_matches_reference(B):
+    """BASELINE config 1: the RGB-only MixFormer (lib/models/mixformer_vit, 128/288) through the
+    oracle vs the reference's own outputs (tests/golden/make_golden_rgb.py)."""
+    from mmt_amd import synthetic
+    from oracle import forward as of
+    keys = json.load(open(GOLDEN + "/state_dict_rgb.json"))
+    sd = of.state_dict_to_torch(synthetic.synth_state_dict(keys))
+    g = np.load(GOLDEN + "/model_rgb_b%d.npz" % B)
+    t, o, s = synthetic.synth_inputs(B, 128, 288)
+    out, coord, aux = of.forward(sd, "rgb", t[0], o[0], s[0], return_aux=True)
+    assert np.abs(out["pred_boxes"].numpy() - g["pred_boxes"]).max() < 1e-5
+    assert np.abs(coord.numpy() - g["coord"]).max() < 1e-5
+    for nm in ("score_map_tl", "score_map_br"):
+        assert np.abs(aux[nm].numpy() - g[nm]).max() < 1e-4 * max(1.0, np.abs(g[nm]).max())
+    sub, sums = _sub(aux["search"])
+    assert np.abs(sub - g["search_sub"]).max() < 1e-4 * max(1.0, np.abs(g["search_sub"]).max())
+
+
 def test_oracle_boxes_depend_on_input(weights):
     """Guard against vacuous box parity (SURVEY defect D8): different frames -> different boxes."""
     from mmt_amd import synthetic
