@@ -1359,6 +1359,13 @@ int launch_attn(const mmt_attn_params& p, hipStream_t st) {
             else hipLaunchKernelGGL((mam_attention_lz_kernel<3, 2, false>), fgrid, dim3(256), 0, st, p);
             return launch_status();
         }
+        // large grids, bf16 inference: the range-checked exponent kernel (impl 17; B = 8 / 32: 27-28 /
+        // 77-84 us against 30-34 / 84-93 for impl 8, profiles/r02_attn_ab.jsonl); the training forward
+        // (lse) and fp16 keep the running-maximum throughput kernel
+        if (p.impl == 0 && !p.lse && __is_same(T, bf16_t) && (int64_t)nfa * p.H * p.S >= MMT_ATTN_FA_MIN_WG) {
+            hipLaunchKernelGGL((mam_attention_lz_kernel<3, 3, true>), fgrid, dim3(256), 0, st, p);
+            return launch_status();
+        }
         if (p.impl == 8 || p.lse || (p.impl == 0 && (int64_t)nfa * p.H * p.S >= MMT_ATTN_FA_MIN_WG)) {
             hipLaunchKernelGGL((mam_attention_fa_kernel<T, 2, 3>), fgrid, dim3(256), 0, st, p);
             return launch_status();
