@@ -354,14 +354,17 @@ MMT_DEV void attn_wait_dyn(int n) {
 // state, and the states are merged through LDS at the end.  At batch 1 the grid is ~216 WGs, one
 // per CU: splitting the keys puts 4*KG waves on the CU to hide the per-tile dependency chain
 // (LDS read -> MFMA -> max -> exp -> MFMA) that one wave per SIMD exposed in full.
-template <typename T, int KG>
+// NS = ring slots (tiles held).  (KG 3 with 9 slots, the whole 528-key stream issued in the prologue
+// and three full rounds, measured no faster: 9.64 vs 9.49 us at B = 1 -- the per-CU fill of the
+// 136 KiB of K / V, not the DMA rounds, bounds this kernel.)
+template <typename T, int KG, int NS = ANS>
 __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(KG, KG))) void mam_attention_glds_kernel(
     const mmt_attn_params p) {
-    constexpr int NWV = 4 * KG, PPW = 16 / NWV;  // waves; K/V pieces per wave per tile
-    constexpr int R = ANS / KG;                    // rounds (KG tiles each) held by the ring
-    static_assert(R >= 2 && PPW >= 1, "ring geometry");
-    __shared__ __attribute__((aligned(1024))) char lds[ANS * ATILE + 64 * 128];
-    char* qimg = lds + ANS * ATILE;
+    constexpr int NWV = 4 * KG;  // waves; a tile's 16 K/V pieces go to waves piece % NWV
+    constexpr int R = NS / KG;   // rounds (KG tiles each) held by the ring
+    static_assert(R >= 2 && NWV <= 16 && NWV >= 8 && R * KG == NS, "ring geometry");
+    __shared__ __attribute__((aligned(1024))) char lds[NS * ATILE + 64 * 128];
+    char* qimg = lds + NS * ATILE;
     MMT_ASTAMP(0, "s_memrealtime");
     MMT_ASTAMP(1, "s_memtime");
 
@@ -381,8 +384,9 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(KG, KG
     const T* qkv = (const T*)p.qkv;
     const int sV = s % p.Bm, sI = sV + p.Bm;
 
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int kg = w >> 2, qw = w & 3;  // key group, 16-query sub-block
+    const int ppw = (15 - w) / NWV + 1;  // this wave's K/V pieces per tile (16 over NWV waves)
     const int l16 = lane & 15, lg = lane >> 4;
     const int prow = lane >> 3, pcol = lane & 7;  // this lane's row / position in a 1-KiB piece
 
@@ -396,12 +400,13 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(KG, KG
         return qkv + ((int64_t)seq * pitch + row) * rs + h * D;
     };
     const int nkt = (Lk + KB - 1) / KB, nr = (nkt + KG - 1) / KG;
-    // Tile t into slot t % ANS: its 16 pieces (8 K, 8 V) are dealt over the waves, PPW each.
+    // Tile t into slot t % NS: its 16 pieces (8 K, 8 V) are dealt over the waves (piece w + i*NWV).
     auto issue_tile = [&](int t) {
-        char* slot = lds + (t % ANS) * ATILE;
+        char* slot = lds + (t % NS) * ATILE;
 #pragma unroll
-        for (int i = 0; i < PPW; ++i) {
-            const int piece = w * PPW + i, isv = piece >> 3, pk = piece & 7, r = pk * 8 + prow;
+        for (int i = 0; i < (16 + NWV - 1) / NWV; ++i) {
+            const int piece = w + i * NWV, isv = piece >> 3, pk = piece & 7, r = pk * 8 + prow;
+            if (piece >= 16) break;  // wave-uniform
             const T* src = key_row(min(t * KB + r, Lk - 1)) + (isv ? 2 * C : C);
             const int sw = isv ? (pcol ^ (prow & 6)) : (pcol ^ prow);
             attn_glds16(src + sw * 8, slot + isv * KB * 128 + pk * 1024);
@@ -420,7 +425,9 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(KG, KG
             attn_glds16(src + ((pcol ^ prow) * 8), qimg + piece * 1024);
         }
     }
-    for (int r = 0; r < R - 1 && r < nr; ++r) issue_round(r);
+    // the whole stream when it fits the ring (no slot reuse), else R - 1 rounds ahead of the consumer
+    const int pro = nr <= R ? nr : R - 1;
+    for (int r = 0; r < pro; ++r) issue_round(r);
 
     const float cexp = p.scale * 1.4426950408889634f;
     float m_run = -1e30f, l_run = 0.f;
@@ -434,10 +441,10 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(KG, KG
         // this wave's DMA of round r (and of Q, issued first) has landed once at most the pieces
         // of the rounds issued after it are outstanding
         int after = 0;
-        for (int r2 = r + 1; r2 <= min(nr - 1, r + R - 2); ++r2) after += PPW * tiles_in(r2);
+        for (int r2 = r + 1; r2 <= (nr <= R ? nr - 1 : min(nr - 1, r + R - 2)); ++r2) after += ppw * tiles_in(r2);
         attn_wait_dyn(after);
         lds_barrier();  // every wave's pieces of round r landed; every wave is done with round r-1
-        if (r + R - 1 < nr) issue_round(r + R - 1);  // refills the slots of round r-1
+        if (nr > R && r + R - 1 < nr) issue_round(r + R - 1);  // refills the slots of round r-1
         if (r == 0) {
             MMT_ASTAMP(2, "s_memtime");
 #pragma unroll
@@ -446,7 +453,7 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(KG, KG
         }
         const int kt = r * KG + kg;
         if (kt >= nkt) continue;  // wave-uniform: this group has no tile in the last round
-        const char* kimg = lds + (kt % ANS) * ATILE;
+        const char* kimg = lds + (kt % NS) * ATILE;
         const char* vimg = kimg + KB * 128;
         // V^T fragments for the PV product, issued first so they land behind the QK^T work:
         // vt[kk][dt] = keys 32kk + 4lg + qr (+16), d = dt*16 + 4pc..+3
