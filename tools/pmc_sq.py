@@ -35,13 +35,15 @@ def main():
         for nm, d in zip(names, seq):
             for c, v in by_disp[d].items():
                 acc[nm][c].append(v)
+    # valu_inst = SQ_INSTS_VALU (wave-instructions; SQ_ACTIVE_INST_VALU counts quad-cycles and is only
+    # the fallback for round-1 captures)
     print("%-22s %8s %10s %10s %10s %9s" % ("entry", "waves", "mfma_inst", "valu_inst", "lds_confl", "mfma_busy"))
     for nm in dict.fromkeys(names):
         a = {c: sum(v) / len(v) for c, v in acc[nm].items()}
         busy = a.get("SQ_BUSY_CYCLES", 0.0)
         mb = a.get("SQ_INSTS_MFMA", 0.0) * 16 / (busy * 4 * 8) if busy else 0.0
         print("%-22s %8.0f %10.0f %10.0f %10.0f %8.1f%%" % (nm, a.get("SQ_WAVES", 0), a.get("SQ_INSTS_MFMA", 0),
-                                                         a.get("SQ_ACTIVE_INST_VALU", 0),
+                                                         a.get("SQ_INSTS_VALU", a.get("SQ_ACTIVE_INST_VALU", 0)),
                                                          a.get("SQ_LDS_BANK_CONFLICT", 0), 100 * mb))
 
 
