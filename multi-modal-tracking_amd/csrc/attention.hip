@@ -1332,9 +1332,431 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     }
 }
 
+// ---- impl 20: persistent whole-pair kernel (bf16 inference, batched grids) ------------------------
+// The throughput kernels above give each (sequence, head) pair 4-5 query-block workgroups, and each
+// of them streams the pair's whole K / V through its own LDS: 38 tiles of 16 KiB per pair, which
+// at batch 32 is ~530 MB of L2 -> LDS fill (~60 GB/s per CU) and bounds them at ~40 us.  Here one
+// workgroup of 16 waves owns a whole pair, so K / V pass through LDS once (9 tiles), and the
+// workgroup is persistent over pairs (pair blockIdx.x + k * gridDim.x) so that the next pair's
+// template, Q and first key tiles stream in behind the current pair's last steps.
+//   waves 0 .. nsb-1: one 32-query search block each (wave nsb-1 may be half full);
+//   waves nsb .. 15 : the template blocks (n_t / 32 of them, dealt round-robin), each over the
+//                     pair's ntt template tiles, which stay resident in their own LDS slots (the
+//                     template keys are the first keys every query sees);
+//   K / V of the rest of the key stream (asym: the other modality's template; then the search
+//   tokens) flows through a PW_NR-slot ring, one tile per step, one 1-KiB LDS-DMA piece per wave.
+// Math per 32-key block is the range-checked exponent kernel's (impl 17: P = exp2(S) with a final
+// range check and an exact fallback, row sums on the matrix pipe).  No stores are in flight while a
+// wave waits on its counted DMA pieces: template outputs are parked (bf16) in LDS and written out
+// with the search outputs at the end of the pair, and the next pair starts with vmcnt(0).
+// LDS: template K / V 32 KiB + template Q 16 KiB + parked outputs 16 KiB + ring 6 x 16 KiB = 160 KiB.
+// Shape limits (host-checked): n_t % 64 == 0, n_t <= 128, search blocks <= 15, template steps <
+// steps per pair (ViT-B 128 / 320: 13 search waves, 3 template waves, 9 steps; asym 11).
+constexpr int PW_NW = 16, PW_NR = 6;
+constexpr int PW_TKV = 2 * FTILE, PW_TQ = 128 * 128, PW_PARK = 4 * 32 * 128;
+constexpr int PW_LDS = PW_TKV + PW_TQ + PW_PARK + PW_NR * FTILE;
+
+template <int NT, int NTOK, int NH, bool ASYM>  // shape-specialised: every count below is a constant
+__global__ __launch_bounds__(1024) void mam_attention_pw_kernel(const mmt_attn_params p) {
+    __shared__ __attribute__((aligned(1024))) char lds[PW_LDS];
+    char* const tkv = lds;
+    char* const tq = lds + PW_TKV;
+    char* const park = tq + PW_TQ;
+    char* const ring = park + PW_PARK;
+
+    constexpr int n_t = NT, ntok = NTOK, H = NH, C = NH * D;
+    const int64_t pitch = p.tok_pitch > 0 ? p.tok_pitch : ntok;
+    constexpr int64_t rs = 3 * C;
+    const bf16_t* qkv = (const bf16_t*)p.qkv;
+    constexpr int nsr = ntok - n_t;                 // search tokens (queries, and keys)
+    constexpr int nsb = (nsr + 31) / 32;            // search waves
+    constexpr int ntw = PW_NW - nsb;                // template waves
+    constexpr int ntb = n_t / 32, ntt = n_t / KB;   // template blocks / tiles
+    constexpr int nrs = (nsr + KB - 1) / KB;        // search key tiles
+    constexpr int nro = ASYM ? ntt : 0;             // other modality's template tiles (asym)
+    constexpr int nring = nro + nrs, nsteps = ntt + nring;
+    constexpr int tsteps = ((ntb + ntw - 1) / ntw) * ntt;  // template waves' steps
+    constexpr int tail = nsr - (nrs - 1) * KB;      // valid keys of the last ring tile
+    static_assert(n_t % KB == 0 && ntt <= 2 && ntw > 0 && tsteps < nsteps, "pw shape");
+    const int npairs = H * p.S, G = gridDim.x;
+    const int npk = (npairs - (int)blockIdx.x + G - 1) / G;
+    const int gtot = npk * nring;
+
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar registers
+    // the lane id, made opaque to the compiler at every step (pw_opaque): every lane-derived offset
+    // is then recomputed inside the step (a few VALU) instead of being hoisted out of the loops and
+    // spilled -- 1024-thread workgroups leave 128 VGPRs, and each scratch reload drains vmcnt(0),
+    // i.e. the whole DMA ring
+    int ln = threadIdx.x & 63;
+    auto pw_opaque = [&]() { asm volatile("" : "+v"(ln)); };
+    const bool srch = w < nsb;
+    const int tw = w - nsb;
+
+    auto pair_sh = [&](int k, int& s, int& h) {
+        const int pr = (int)blockIdx.x + k * G;
+        h = pr % H;
+        s = pr / H;
+    };
+    // ---- DMA: ring tile g (pair g / nring) -> slot g % PW_NR, wave w = piece w (K: 0-7, V: 8-15).
+    // The issue pointer's pair (is_k -> is_s, is_h) and tile within the pair (is_r) advance
+    // incrementally (no divisions per tile).
+    const int isv = w >> 3, pk = w & 7;
+    int is_k = 0, is_r = 0, is_s, is_h;
+    pair_sh(0, is_s, is_h);
+    auto issue_ring = [&](int g) {
+        const int prow = ln >> 3, pcol = ln & 7;
+        const int64_t colo = (isv ? 2 * C : C) + (isv ? (pcol ^ attn_vswz(prow)) : (pcol ^ prow)) * 8;
+        const int r = is_r, s = is_s, h = is_h;
+        if (++is_r == nring) {
+            is_r = 0;
+            pair_sh(++is_k, is_s, is_h);
+        }
+        int seq = s, tok;
+        const int row = pk * 8 + prow;
+        if (r < nro) {
+            seq = s < p.Bm ? s + p.Bm : s - p.Bm;
+            tok = r * KB + row;
+        } else {
+            tok = min(n_t + (r - nro) * KB + row, ntok - 1);
+        }
+        attn_glds16(qkv + ((int64_t)seq * pitch + tok) * rs + h * D + colo,
+                    ring + (g % PW_NR) * FTILE + isv * KB * 128 + pk * 1024);
+    };
+    // template K / V (own template, ntt tiles) and template Q of pair k
+    auto issue_tmpl = [&](int k) {
+        const int prow = ln >> 3, pcol = ln & 7;
+        int s, h;
+        pair_sh(k, s, h);
+        const bf16_t* base = qkv + (int64_t)s * pitch * rs + h * D;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int piece = w + PW_NW * i;
+            if (piece < 16 * ntt) {
+                const int tt = piece >> 4, iv = (piece >> 3) & 1, pp = piece & 7;
+                const int64_t c = (iv ? 2 * C : C) + (iv ? (pcol ^ attn_vswz(prow)) : (pcol ^ prow)) * 8;
+                attn_glds16(base + (int64_t)(tt * KB + pp * 8 + prow) * rs + c, tkv + tt * FTILE + iv * KB * 128 + pp * 1024);
+            }
+        }
+        if (w < n_t / 8) attn_glds16(base + (int64_t)(w * 8 + prow) * rs + (pcol ^ prow) * 8, tq + w * 1024);
+    };
+
+    const float cexp = p.scale * 1.4426950408889634f;
+    const bool prescale = fabsf(cexp - 1.f) > 1e-6f;
+    u32x4 qf[4];  // B operand of S^T = K Q^T: query l32, d = 16ks + 8hf .. +7
+    auto scale_q = [&]() {
+        if (prescale) {
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) {
+                u32x4 v = qf[ks];
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    v[e] = pack_bf16x2(__uint_as_float(v[e] << 16) * cexp, __uint_as_float(v[e] & 0xffff0000u) * cexp);
+                qf[ks] = v;
+            }
+        }
+    };
+    // search waves: this wave's 32 query rows of pair k, straight to registers.  Inline asm: a
+    // compiler-visible load still pending on the pair loop's back edge makes hipcc put vmcnt(0)
+    // (the whole DMA ring) in front of every tile's first Q use; the wait below (q_wait, at the
+    // pair's first step) redefines qf, so nothing reads it before the loads land.
+    auto load_q = [&](int k) {
+        int s, h;
+        pair_sh(k, s, h);
+        const int q = min(n_t + 32 * w + (ln & 31), ntok - 1);
+        const bf16_t* src = qkv + ((int64_t)s * pitch + q) * rs + h * D + 8 * (ln >> 5);
+        asm volatile("global_load_dwordx4 %0, %4, off\n\t"
+                     "global_load_dwordx4 %1, %4, off offset:32\n\t"
+                     "global_load_dwordx4 %2, %4, off offset:64\n\t"
+                     "global_load_dwordx4 %3, %4, off offset:96"
+                     : "=&v"(qf[0]), "=&v"(qf[1]), "=&v"(qf[2]), "=&v"(qf[3])
+                     : "v"(src)
+                     : "memory");
+    };
+    auto q_wait = [&]() {  // vmcnt(0): Q, template and every earlier piece (no stores in flight after it)
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3])::"memory");
+    };
+
+    f32x16 o[2];
+    f32x4 lacc;
+    auto zero_acc = [&]() {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { o[0][r] = 0.f; o[1][r] = 0.f; }
+        lacc = f32x4{0.f, 0.f, 0.f, 0.f};
+    };
+    // one 32-key block kb of a tile (impl 17's block): NJ 16-key steps, MASK = zero P from key nv on
+    auto block = [&](const char* kimg, int kb, int nv, auto NJc, auto MASKc) {
+        constexpr int NJ = decltype(NJc)::value;
+        constexpr bool MASK = decltype(MASKc)::value;
+        const int l32 = ln & 31, hf = ln >> 5, kpos = (l32 & 7) * 16;
+        const int li = ln & 15, qr = li >> 2, pc = li & 3, dsub = (ln >> 4) & 1;
+        const float one_or_zero = ((li >> 2) & 1) == dsub ? 1.f : 0.f;
+        const uint32_t sel_w = pack_bf16x2(one_or_zero, one_or_zero);
+        const bf16x8 sel = __builtin_bit_cast(bf16x8, u32x4{sel_w, sel_w, sel_w, sel_w});
+        const char* vimg = kimg + KB * 128;
+        const char* krow = kimg + (32 * kb + l32) * 128;
+        f32x16 sacc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {  // K fragments two at a time (registers)
+            u32x4 kf[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) kf[i] = *(const u32x4*)(krow + ((((4 * kh + 2 * i + hf) * 16) ^ kpos)));
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+                sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kf[i]),
+                                                               __builtin_bit_cast(bf16x8, qf[2 * kh + i]), sacc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 8 * NJ; ++r) {
+            float e = MMT_ATTN_ABLATE == 3 ? sacc[r] : __builtin_amdgcn_exp2f(sacc[r]);
+            if constexpr (MASK) {
+                if (32 * kb + 8 * (r >> 2) + 4 * hf + (r & 3) >= nv) e = 0.f;
+            }
+            sacc[r] = e;
+        }
+        // V^T fragments after the exponentials (not live across them: register budget); the
+        // other waves of the SIMD cover the read latency
+        uint2 vt[NJ][2][2];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int row = 32 * kb + 16 * j + 4 * hf + qr;
+#pragma unroll
+            for (int db = 0; db < 2; ++db) {
+                const char* b1 = vimg + row * 128 + (((4 * db + 2 * dsub + (pc >> 1)) ^ attn_vswz(row)) * 16) + (pc & 1) * 8;
+                vt[j][db][0] = attn_tr16<0>(b1);
+                vt[j][db][1] = attn_tr16<8 * 128>(b1);
+            }
+        }
+        attn_lds_wait();
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int rb = 8 * j;
+            const bf16x8 pf = __builtin_bit_cast(
+                bf16x8, u32x4{pack_bf16x2(sacc[rb], sacc[rb + 1]), pack_bf16x2(sacc[rb + 2], sacc[rb + 3]),
+                              pack_bf16x2(sacc[rb + 4], sacc[rb + 5]), pack_bf16x2(sacc[rb + 6], sacc[rb + 7])});
+#pragma unroll
+            for (int db = 0; db < 2; ++db) {
+                const uint2 ua = vt[j][db][0], ub = vt[j][db][1];
+                const bf16x8 vf = __builtin_bit_cast(bf16x8, make_uint4(ua.x, ua.y, ub.x, ub.y));
+                o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[db], 0, 0, 0);
+            }
+            lacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pf, lacc, 0, 0, 0);
+        }
+    };
+    // the two 32-key blocks of a tile are fenced from each other: overlapping them doubles the
+    // working set past the 128 registers
+    auto full_tile = [&](const char* kimg) {
+        __builtin_amdgcn_sched_barrier(0);
+        block(kimg, 0, KB, attn_ic<2>{}, attn_ic<0>{});
+        __builtin_amdgcn_sched_barrier(0);
+        block(kimg, 1, KB, attn_ic<2>{}, attn_ic<0>{});
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto tail_tile = [&](const char* kimg, int nv) {  // one masked instantiation (last step only)
+        for (int kb = 0; kb < 2; ++kb)
+            if (32 * kb < nv) block(kimg, kb, nv, attn_ic<2>{}, attn_ic<1>{});
+    };
+
+    // exact two-pass fp32 softmax for query qc of (s, h) over Lk keys (cross: the asym search key
+    // order [template_V | template_I | search_s]); lane half hf owns d = 32hf .. 32hf+31.  Rare.
+    auto fallback = [&](int s, int h, int qc, int Lk, bool cross, float* acc) {
+        const int hf = ln >> 5;
+        const int sV = s % max(p.Bm, 1), sI = sV + p.Bm;
+        auto key_row = [&](int kk) -> const bf16_t* {
+            int seq = s, row = kk;
+            if (cross) {
+                if (kk < n_t) seq = sV;
+                else if (kk < 2 * n_t) { seq = sI; row = kk - n_t; }
+                else row = kk - n_t;
+            }
+            return qkv + ((int64_t)seq * pitch + row) * rs + h * D + 32 * hf;
+        };
+        float qv[32];
+        const bf16_t* qp = qkv + ((int64_t)s * pitch + qc) * rs + h * D + 32 * hf;
+#pragma unroll
+        for (int i = 0; i < 32; ++i) qv[i] = bf2f(qp[i]) * cexp;
+        auto score = [&](int kk) {
+            const bf16_t* kp = key_row(kk) + C;
+            float d0 = 0.f;
+#pragma unroll
+            for (int i = 0; i < 32; ++i) d0 += qv[i] * bf2f(kp[i]);
+            return d0 + __shfl_xor(d0, 32, 64);
+        };
+        float m = -INFINITY;
+        for (int kk = 0; kk < Lk; ++kk) m = fmaxf(m, score(kk));
+        float lf = 0.f;
+#pragma unroll
+        for (int i = 0; i < 32; ++i) acc[i] = 0.f;
+        for (int kk = 0; kk < Lk; ++kk) {
+            const float e = __builtin_amdgcn_exp2f(score(kk) - m);
+            lf += e;
+            const bf16_t* vp = key_row(kk) + 2 * C;
+#pragma unroll
+            for (int i = 0; i < 32; ++i) acc[i] += e * bf2f(vp[i]);
+        }
+        const float inv = 1.f / lf;
+#pragma unroll
+        for (int i = 0; i < 32; ++i) acc[i] *= inv;
+    };
+    // finished block: normalised bf16 rows (lane: query l32, d = 32db + 8g + 4hf .. +3) into dst
+    // (row pitch dpitch elements), or the fallback's rows (lane: d = 32hf .. +31)
+    typedef __attribute__((address_space(3))) uint64_t lds_u64;
+    typedef __attribute__((address_space(3))) u32x4 lds_u4;
+    auto finish = [&](auto TOc, bf16_t* dst, int64_t dpitch, bool valid, int s, int h, int qc, int Lk, bool cross) {
+        constexpr bool TO_LDS = decltype(TOc)::value != 0;  // parked template rows: ds_write, not flat
+        const float l = lacc[0];
+        float chk = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) chk += o[0][r] * 0.f + o[1][r] * 0.f;
+        const bool ok = (l >= LZ_LO && l <= LZ_HI && chk == 0.f) || MMT_ATTN_ABLATE != 0;
+        const int l32 = ln & 31, hf = ln >> 5;
+        bf16_t* op = dst + (int64_t)l32 * dpitch;
+        if (__builtin_expect(__all(ok), 1)) {
+            const float inv = 1.f / l;
+            if (valid) {
+#pragma unroll
+                for (int db = 0; db < 2; ++db)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g)
+                    {
+                        const uint2 v = make_uint2(pack_bf16x2(o[db][4 * g] * inv, o[db][4 * g + 1] * inv),
+                                                   pack_bf16x2(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv));
+                        if constexpr (TO_LDS) *(lds_u64*)(op + 32 * db + 8 * g + 4 * hf) = ((uint64_t)v.y << 32) | v.x;
+                        else *(uint2*)(op + 32 * db + 8 * g + 4 * hf) = v;
+                    }
+            }
+            return;
+        }
+        float acc[32];
+        fallback(s, h, qc, Lk, cross, acc);
+        if (valid) {
+#pragma unroll
+            for (int i = 0; i < 32; i += 8)
+            {
+                const u32x4 v = u32x4{pack_bf16x2(acc[i], acc[i + 1]), pack_bf16x2(acc[i + 2], acc[i + 3]),
+                                      pack_bf16x2(acc[i + 4], acc[i + 5]), pack_bf16x2(acc[i + 6], acc[i + 7])};
+                if constexpr (TO_LDS) *(lds_u4*)(op + 32 * hf + i) = v;
+                else *(u32x4*)(op + 32 * hf + i) = v;
+            }
+        }
+    };
+
+    // ---- prologue: pair 0's template and Q, the first PW_NR - 1 ring tiles
+    // stamps (measurement builds, search wave 0): 0 entry; pair 0: 1 / 2 / 3 / 4 = after the barrier of
+    // steps 0 / 1 / 4 / nsteps - 1, 5 = its last tile computed, 6 = its rows stored; 7 = last pair done
+    MMT_ASTAMP(0, "s_memtime");
+    issue_tmpl(0);
+    int gi = 0, gc = 0;  // ring tiles issued / consumed (uniform)
+    for (; gi < PW_NR - 1 && gi < gtot; ++gi) issue_ring(gi);
+    if (srch) load_q(0);
+
+    // step u of pair k, common to both roles (every wave executes the same barrier sequence): wait
+    // for this wave's pieces of the step's tile, barrier, refill the slot the previous step freed
+    auto step_sync = [&](int k, int u) {
+        pw_opaque();
+        if (u >= ntt) attn_wait_dyn(gi - 1 - gc);
+        lds_barrier();
+        if ((u == 0 && k > 0) || u > ntt) {
+            if (MMT_ATTN_ABLATE != 1 && gi < gtot) issue_ring(gi);
+            gi = min(gi + 1, gtot);
+        }
+        if (u == tsteps && k + 1 < npk) issue_tmpl(k + 1);
+    };
+    auto tmpl_wait = [&]() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
+
+    if (srch) {  // ---- search waves: one 32-query block per pair, all nsteps tiles
+#pragma unroll 1
+        for (int k = 0; k < npk; ++k) {
+            int s, h;
+            pair_sh(k, s, h);
+            zero_acc();
+            q_wait();  // Q, template and every earlier piece (no stores in flight after it)
+            constexpr int nfull = tail < KB ? nsteps - 1 : nsteps;  // the partial last tile after the loop
+#pragma unroll 1
+            for (int u = 0; u < nfull; ++u) {
+                step_sync(k, u);
+                if (k == 0) {
+                    if (u == 0) { MMT_ASTAMP(1, "s_memtime"); }
+                    else if (u == 1) { MMT_ASTAMP(2, "s_memtime"); }
+                    else if (u == 4) { MMT_ASTAMP(3, "s_memtime"); }
+                }
+                if (u == 0) scale_q();
+                if (MMT_ATTN_ABLATE != 2) full_tile(u < ntt ? tkv + u * FTILE : ring + (gc % PW_NR) * FTILE);
+                if (u >= ntt) ++gc;
+            }
+            if constexpr (nfull < nsteps) {
+                step_sync(k, nsteps - 1);
+                if (k == 0) { MMT_ASTAMP(4, "s_memtime"); }
+                if (MMT_ATTN_ABLATE != 2) tail_tile(ring + (gc % PW_NR) * FTILE, tail);
+                ++gc;
+            }
+            if (k == 0) { MMT_ASTAMP(5, "s_memtime"); }
+            if (k + 1 < npk) load_q(k + 1);  // the next pair's Q behind this pair's output stores
+            const int l32 = ln & 31, q = n_t + 32 * w + l32;
+            finish(attn_ic<0>{}, (bf16_t*)p.out + ((int64_t)s * pitch + n_t + 32 * w) * C + h * D, C, q < ntok, s, h,
+                          min(q, ntok - 1), ASYM ? ntok + n_t : ntok, ASYM);
+            if (k == 0) { MMT_ASTAMP(6, "s_memtime"); }
+            if (k == npk - 1) { MMT_ASTAMP(7, "s_memtime"); }
+        }
+    } else {  // ---- template waves: template blocks tw, tw + ntw, .. over the resident template tiles
+#pragma unroll 1
+        for (int k = 0; k < npk; ++k) {
+            int s, h;
+            pair_sh(k, s, h);
+            tmpl_wait();
+#pragma unroll 1
+            for (int u = 0; u < nsteps; ++u) {
+                step_sync(k, u);
+                if (u < tsteps) {
+                    const int bi = u / ntt, tu = u - bi * ntt, blk = tw + ntw * bi;
+                    if (blk < ntb) {
+                        if (tu == 0) {
+                            const int row = 32 * blk + (ln & 31), hf = ln >> 5;
+#pragma unroll
+                            for (int ks = 0; ks < 4; ++ks) qf[ks] = *(const u32x4*)(tq + row * 128 + (((2 * ks + hf) ^ (row & 7)) * 16));
+                            scale_q();
+                            zero_acc();
+                        }
+                        if (MMT_ATTN_ABLATE != 2) full_tile(tkv + tu * FTILE);
+                        if (tu == ntt - 1)  // rows parked in LDS until the pair's end
+                            finish(attn_ic<1>{}, (bf16_t*)(park + blk * 32 * 128), 64, true, s, h, 32 * blk + (ln & 31), n_t, false);
+                    }
+                }
+                if (u >= ntt) ++gc;
+            }
+            // parked rows to the output (the pair's only template stores)
+            bf16_t* out = (bf16_t*)p.out + (int64_t)s * pitch * C + h * D;
+            const int l32 = ln & 31, hf = ln >> 5;
+            for (int blk = tw; blk < ntb; blk += ntw) {
+                const char* pr = park + blk * 32 * 128 + l32 * 128;
+                bf16_t* op = out + (int64_t)(32 * blk + l32) * C;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) *(u32x4*)(op + 32 * hf + 8 * i) = *(const u32x4*)(pr + 64 * hf + 16 * i);
+            }
+        }
+    }
+}
+
+static int attn_cu_count() {
+    static int n = 0;
+    if (n <= 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+    }
+    return n;
+}
+
+// impl 20 applies to: bf16, no lse, all queries, the instantiated shapes (ViT-B 128 / 320: n_t 128,
+// 528 tokens, 12 heads; joint or asym key streams)
+static bool pw_shape_ok(const mmt_attn_params& p) {
+    return !p.lse && p.q_part == 0 && p.n_t == 128 && p.ntok == 528 && p.H == 12 && p.C == 12 * D;
+}
+
 template <typename T>
 int launch_attn(const mmt_attn_params& p, hipStream_t st) {
-    if (p.impl != 0 && p.impl != 2 && p.impl != 4 && (p.impl < 8 || p.impl > 12) && (p.impl < 16 || p.impl > 19))
+    if (p.impl != 0 && p.impl != 2 && p.impl != 4 && (p.impl < 8 || p.impl > 12) && (p.impl < 16 || p.impl > 20))
         return MMT_EBADARG;
     if (p.lse && (sizeof(T) != 2 || p.impl == 9 || (p.impl > 9 && p.impl < 16))) return MMT_EBADARG;
     // fp16: the kernels with a running maximum (latency kernel, throughput kernel); the range-checked
@@ -1358,6 +1780,13 @@ int launch_attn(const mmt_attn_params& p, hipStream_t st) {
         const int nfa = qblocks(FQ);
         const dim3 fgrid(nfa, p.H, p.S);
         if (!__is_same(T, bf16_t)) {  // fp16: no A/B variants (rejected above)
+        } else if (p.impl == 20) {  // persistent whole-pair kernel: one workgroup per CU, pairs strided
+            if (!pw_shape_ok(p)) return MMT_EBADARG;
+            const int npairs = p.H * p.S;
+            const dim3 g(min(npairs, attn_cu_count()));
+            if (p.asym) hipLaunchKernelGGL((mam_attention_pw_kernel<128, 528, 12, true>), g, dim3(1024), 0, st, p);
+            else hipLaunchKernelGGL((mam_attention_pw_kernel<128, 528, 12, false>), g, dim3(1024), 0, st, p);
+            return launch_status();
         } else if (p.impl >= 16) {  // range-checked exponent kernel (A/B): 16 = VALU row sums, ring 3, 3 WG/CU;
                              // 17 = MFMA row sums; 18 = ring 2; 19 = 2 WG/CU
             if (p.impl == 16) hipLaunchKernelGGL((mam_attention_lz_kernel<3, 3, false>), fgrid, dim3(256), 0, st, p);

@@ -62,3 +62,24 @@ def test_bad_arguments_rejected_without_gpu_work():
     a = _lib.AttnParams()
     a.C, a.H = 100, 2
     assert _lib.LIB.mmt_mam_attention(ctypes.byref(a), _lib.MMT_BF16, None) == -10000
+
+
+def test_persistent_pair_attention_shape_gate():
+    """impl 20 (persistent whole-pair MAM kernel) is instantiated for the ViT-B 128/320 shape only; any
+    other shape, the training forward (lse), fp16 or a query part is rejected on the host."""
+    from mmt_amd import _lib
+    fake = 1 << 20  # 16-B aligned, never dereferenced: every case fails validation before a launch
+
+    def attn(dt=_lib.MMT_BF16, **kw):
+        a = _lib.AttnParams()
+        a.qkv, a.out, a.S, a.Bm, a.ntok, a.n_t, a.H, a.C, a.scale, a.impl = fake, fake, 2, 1, 528, 128, 12, 768, 0.125, 20
+        for k, v in kw.items():
+            setattr(a, k, v)
+        return _lib.LIB.mmt_mam_attention(ctypes.byref(a), dt, None)
+
+    assert attn(ntok=864, n_t=288, H=16, C=1024) == -10000  # ViT-L shape
+    assert attn(H=4, C=256) == -10000
+    assert attn(q_part=2) == -10000
+    assert attn(lse=fake) == -10000
+    assert attn(dt=_lib.MMT_F16) == -10000
+    assert attn(impl=21) == -10000
