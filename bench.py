@@ -162,7 +162,7 @@ def roofline(rt, plan, times, dtype, traffic=None):
 
 def mam_batched(rt, B=32, per_graph=20, replays=10):
     """Roofline of the MAM attention launch at B frames (2B sequences) on random bf16 q/k/v in the
-    runtime's convention (q pre-scaled), timed like kernel_profile."""
+    runtime's convention (q pre-scaled), timed like kernel_profile (median of 5 timed segments)."""
     import ctypes
     from mmt_amd._lib import LIB, AttnParams, MMT_BF16, check
     d = rt.d
@@ -180,13 +180,16 @@ def mam_batched(rt, B=32, per_graph=20, replays=10):
             check(LIB.mmt_mam_attention(ctypes.byref(p), MMT_BF16, torch.cuda.current_stream().cuda_stream), "attn")
     for _ in range(3):  # warm-up replays (clocks, caches)
         g.replay()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(st)
-    for _ in range(replays):
-        g.replay()
-    e1.record(st)
-    torch.cuda.synchronize()
-    us = e0.elapsed_time(e1) * 1e3 / (replays * per_graph)
+    segs = []  # median of 5 timed segments: the box's clock state moves single segments by several %
+    for _ in range(5):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(replays):
+            g.replay()
+        e1.record(st)
+        torch.cuda.synchronize()
+        segs.append(e0.elapsed_time(e1) * 1e3 / (replays * per_graph))
+    us = sorted(segs)[len(segs) // 2]
     lk_s = d.ntok + (d.n_t if p.asym else 0)
     fl = 4.0 * 64 * d.H * S * (d.n_t * d.n_t + d.ns * lk_s)
     ach = fl / (us * 1e-6) / 1e12

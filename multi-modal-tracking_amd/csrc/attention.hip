@@ -1078,7 +1078,14 @@ struct attn_ic {
     static constexpr int value = N;
 };
 
-template <int FNS, int OCC, bool SUM_MFMA>
+// PIPE: the two 32-key blocks of a full tile software-pipelined inside the wave (impl 21, the
+// large-grid default): both blocks' scores are computed before either block's exponentials, so
+// block 1's QK^T MFMAs run beside block 0's v_exp / packs and block 0's PV MFMAs beside block 1's,
+// and one wave's dependency chain (scores -> exp -> PV) stops idling the matrix pipe on its own
+// VALU.  B = 32: 78.9 vs 83.8 us, asym 88.5 vs 93.2; B = 8: 27.2 vs 29.8 (same run, bit-identical
+// output).  Measured and dropped: sched_group_barrier interleave hints (79.3), the block-1 PV moved
+// past the next tile's barrier (79.6), 2 workgroups per CU (85.3).
+template <int FNS, int OCC, bool SUM_MFMA, bool PIPE = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void mam_attention_lz_kernel(
     const mmt_attn_params p) {
     __shared__ __attribute__((aligned(1024))) char lds[FNS * FTILE];
@@ -1247,13 +1254,77 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
         lds_barrier();
         if (MMT_ATTN_ABLATE != 1 && FNS - 1 < nkt) issue_tile(FNS - 1);
     }
+    // a full tile, both blocks software-pipelined (PIPE; row sums on the matrix pipe)
+    auto tile_pipe = [&](const char* kimg) {
+        const char* vimg = kimg + KB * 128;
+        auto vfrags = [&](int kb, uint2 (&vt)[2][2][2]) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int row = 32 * kb + 16 * j + 4 * hf + qr;
+#pragma unroll
+                for (int db = 0; db < 2; ++db) {
+                    const char* b1 = vimg + row * 128 + (((4 * db + 2 * dsub + (pc >> 1)) ^ attn_vswz(row)) * 16) + (pc & 1) * 8;
+                    vt[j][db][0] = attn_tr16<0>(b1);
+                    vt[j][db][1] = attn_tr16<8 * 128>(b1);
+                }
+            }
+        };
+        auto pv = [&](const uint2 (&vt)[2][2][2], const f32x16& s) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int rb = 8 * j;
+                const bf16x8 pf = __builtin_bit_cast(
+                    bf16x8, u32x4{pack_bf16x2(s[rb], s[rb + 1]), pack_bf16x2(s[rb + 2], s[rb + 3]),
+                                  pack_bf16x2(s[rb + 4], s[rb + 5]), pack_bf16x2(s[rb + 6], s[rb + 7])});
+#pragma unroll
+                for (int db = 0; db < 2; ++db) {
+                    const uint2 ua = vt[j][db][0], ub = vt[j][db][1];
+                    o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, make_uint4(ua.x, ua.y, ub.x, ub.y)),
+                                                                    pf, o[db], 0, 0, 0);
+                }
+                lacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pf, lacc, 0, 0, 0);
+            }
+        };
+        f32x16 s0, s1;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { s0[r] = 0.f; s1[r] = 0.f; }
+        u32x4 k0[4], k1[4];
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) k0[ks] = *(const u32x4*)(kimg + l32 * 128 + ((((2 * ks + hf) * 16) ^ kpos)));
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) k1[ks] = *(const u32x4*)(kimg + (32 + l32) * 128 + ((((2 * ks + hf) * 16) ^ kpos)));
+        uint2 v0[2][2][2], v1[2][2][2];
+        vfrags(0, v0);
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+            s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, k0[ks]), __builtin_bit_cast(bf16x8, qf[ks]), s0, 0, 0, 0);
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+            s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, k1[ks]), __builtin_bit_cast(bf16x8, qf[ks]), s1, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s0[r] = MMT_ATTN_ABLATE == 3 ? s0[r] : __builtin_amdgcn_exp2f(s0[r]);
+        vfrags(1, v1);
+        // block 0's V^T reads (the 8 oldest of the 16 asm reads) landed; the wait redefines them
+        asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(v0[0][0][0]), "+v"(v0[0][0][1]), "+v"(v0[0][1][0]), "+v"(v0[0][1][1]),
+                     "+v"(v0[1][0][0]), "+v"(v0[1][0][1]), "+v"(v0[1][1][0]), "+v"(v0[1][1][1]));
+        pv(v0, s0);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s1[r] = MMT_ATTN_ABLATE == 3 ? s1[r] : __builtin_amdgcn_exp2f(s1[r]);
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v1[0][0][0]), "+v"(v1[0][0][1]), "+v"(v1[0][1][0]), "+v"(v1[0][1][1]),
+                     "+v"(v1[1][0][0]), "+v"(v1[1][0][1]), "+v"(v1[1][1][0]), "+v"(v1[1][1][1]));
+        pv(v1, s1);
+    };
     const int nfull = Lk / KB;  // full 64-key tiles; Lk % KB keys remain for a tail tile
     const bool compute = active && MMT_ATTN_ABLATE != 2;
     for (int kt = 0; kt < nfull; ++kt) {
         if (compute) {
             const char* kimg = lds + (kt % FNS) * FTILE;
-            block(kimg, 0, KB, attn_ic<2>{}, attn_ic<0>{});
-            block(kimg, 1, KB, attn_ic<2>{}, attn_ic<0>{});
+            if constexpr (PIPE && SUM_MFMA) {
+                tile_pipe(kimg);
+            } else {
+                block(kimg, 0, KB, attn_ic<2>{}, attn_ic<0>{});
+                block(kimg, 1, KB, attn_ic<2>{}, attn_ic<0>{});
+            }
         }
         if (kt + 1 < nkt) next_tile(kt + 1);
     }
@@ -1756,7 +1827,7 @@ static bool pw_shape_ok(const mmt_attn_params& p) {
 
 template <typename T>
 int launch_attn(const mmt_attn_params& p, hipStream_t st) {
-    if (p.impl != 0 && p.impl != 2 && p.impl != 4 && (p.impl < 8 || p.impl > 12) && (p.impl < 16 || p.impl > 20))
+    if (p.impl != 0 && p.impl != 2 && p.impl != 4 && (p.impl < 8 || p.impl > 12) && (p.impl < 16 || p.impl > 21))
         return MMT_EBADARG;
     if (p.lse && (sizeof(T) != 2 || p.impl == 9 || (p.impl > 9 && p.impl < 16))) return MMT_EBADARG;
     // fp16: the kernels with a running maximum (latency kernel, throughput kernel); the range-checked
@@ -1788,18 +1859,21 @@ int launch_attn(const mmt_attn_params& p, hipStream_t st) {
             else hipLaunchKernelGGL((mam_attention_pw_kernel<128, 528, 12, false>), g, dim3(1024), 0, st, p);
             return launch_status();
         } else if (p.impl >= 16) {  // range-checked exponent kernel (A/B): 16 = VALU row sums, ring 3, 3 WG/CU;
-                             // 17 = MFMA row sums; 18 = ring 2; 19 = 2 WG/CU
+                             // 17 = MFMA row sums; 18 = ring 2; 19 = 2 WG/CU; 21 / 22 = 17 with the
+                             // two blocks of a tile software-pipelined
             if (p.impl == 16) hipLaunchKernelGGL((mam_attention_lz_kernel<3, 3, false>), fgrid, dim3(256), 0, st, p);
             else if (p.impl == 17) hipLaunchKernelGGL((mam_attention_lz_kernel<3, 3, true>), fgrid, dim3(256), 0, st, p);
             else if (p.impl == 18) hipLaunchKernelGGL((mam_attention_lz_kernel<2, 3, false>), fgrid, dim3(256), 0, st, p);
+            else if (p.impl == 21) hipLaunchKernelGGL((mam_attention_lz_kernel<3, 3, true, true>), fgrid, dim3(256), 0, st, p);
             else hipLaunchKernelGGL((mam_attention_lz_kernel<3, 2, false>), fgrid, dim3(256), 0, st, p);
             return launch_status();
         }
-        // large grids, bf16 inference: the range-checked exponent kernel (impl 17; B = 8 / 32: 27-28 /
-        // 77-84 us against 30-34 / 84-93 for impl 8, profiles/r02_attn_ab.jsonl); the training forward
-        // (lse) and fp16 keep the running-maximum throughput kernel
+        // large grids, bf16 inference: the range-checked exponent kernel with its two blocks per tile
+        // software-pipelined (impl 21; B = 8 / 32: 27.2 / 78.9 us against 29.8 / 83.8 for impl 17 and
+        // 30-34 / 84-93 for impl 8, profiles/r02_attn_ab.jsonl, r02_pipe_ab.jsonl); the training
+        // forward (lse) and fp16 keep the running-maximum throughput kernel
         if (p.impl == 0 && !p.lse && __is_same(T, bf16_t) && (int64_t)nfa * p.H * p.S >= MMT_ATTN_FA_MIN_WG) {
-            hipLaunchKernelGGL((mam_attention_lz_kernel<3, 3, true>), fgrid, dim3(256), 0, st, p);
+            hipLaunchKernelGGL((mam_attention_lz_kernel<3, 3, true, true>), fgrid, dim3(256), 0, st, p);
             return launch_status();
         }
         if (p.impl == 8 || p.lse || (p.impl == 0 && (int64_t)nfa * p.H * p.S >= MMT_ATTN_FA_MIN_WG)) {

@@ -82,4 +82,4 @@ def test_persistent_pair_attention_shape_gate():
     assert attn(q_part=2) == -10000
     assert attn(lse=fake) == -10000
     assert attn(dt=_lib.MMT_F16) == -10000
-    assert attn(impl=21) == -10000
+    assert attn(impl=99) == -10000

@@ -373,7 +373,7 @@ def _attn_ref(qkv, S, Bm, ntok, n_t, C, H, asym):
     return out.permute(0, 2, 1, 3).reshape(S, ntok, C)
 
 
-ATTN_BF16_IMPLS = [2, 4, 8, 9, 10, 11, 12, 16, 17, 18, 19]
+ATTN_BF16_IMPLS = [2, 4, 8, 9, 10, 11, 12, 16, 17, 18, 19, 21]
 
 
 @pytest.mark.parametrize("dname,impl", [("f32", 0), ("bf16", 0)] + [("bf16", i) for i in ATTN_BF16_IMPLS]
@@ -424,7 +424,7 @@ def test_mam_attention_rescale_branch(dname, impl):
     assert (out.float().cpu() - ref).abs().max().item() < (1.5e-2 if dt != torch.float32 else 5e-5)
 
 
-@pytest.mark.parametrize("impl", [0, 2, 4, 8, 9, 10, 12, 16, 17, 18, 19])
+@pytest.mark.parametrize("impl", [0, 2, 4, 8, 9, 10, 12, 16, 17, 18, 19, 21])
 @pytest.mark.parametrize("asym", [0, 1])
 def test_mam_attention_prescaled_q(impl, asym):
     """The runtime's convention (bf16): q arrives multiplied by scale * log2(e) (folded into the qkv
@@ -451,7 +451,7 @@ def test_mam_attention_prescaled_q(impl, asym):
     assert err <= 1.5e-2, err
 
 
-@pytest.mark.parametrize("impl", [0, 4, 8, 16, 17])
+@pytest.mark.parametrize("impl", [0, 4, 8, 16, 17, 21])
 @pytest.mark.parametrize("asym", [0, 1])
 def test_mam_attention_extreme_scores(impl, asym):
     """Scores far outside the fp32 exponent range of exp2 without a reference point: a key that
