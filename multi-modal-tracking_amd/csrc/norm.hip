@@ -22,6 +22,16 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
     if (row >= rows) return;
     const float4* x4 = (const float4*)(in + row * C);
     const float4* a4 = add ? (const float4*)(add + (row % add_rows) * C) : nullptr;
+    // gamma / beta issued with the row (not after the two reductions: one memory round trip fewer)
+    const bool second = g1 && (row / rpg) >= 1;
+    const float4* gg = (const float4*)(second ? g1 : g0);
+    const float4* bb = (const float4*)(second ? b1 : b0);
+    float4 ga[V], be[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        ga[i] = gg[lane + 64 * i];
+        be[i] = bb[lane + 64 * i];
+    }
     float4 v[V];
     float s = 0.f;
 #pragma unroll
@@ -41,18 +51,14 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
         q += dx * dx + dy * dy + dz * dz + dw * dw;
     }
     const float rstd = rsqrtf(wave_sum(q) * (1.f / C) + eps);
-    const bool second = g1 && (row / rpg) >= 1;
-    const float4* gg = (const float4*)(second ? g1 : g0);
-    const float4* bb = (const float4*)(second ? b1 : b0);
 #pragma unroll
     for (int i = 0; i < V; ++i) {
         const int idx = lane + 64 * i;
-        const float4 ga = gg[idx], be = bb[idx];
         float4 y;
-        y.x = (v[i].x - mean) * rstd * ga.x + be.x;
-        y.y = (v[i].y - mean) * rstd * ga.y + be.y;
-        y.z = (v[i].z - mean) * rstd * ga.z + be.z;
-        y.w = (v[i].w - mean) * rstd * ga.w + be.w;
+        y.x = (v[i].x - mean) * rstd * ga[i].x + be[i].x;
+        y.y = (v[i].y - mean) * rstd * ga[i].y + be[i].y;
+        y.z = (v[i].z - mean) * rstd * ga[i].z + be[i].z;
+        y.w = (v[i].w - mean) * rstd * ga[i].w + be[i].w;
         if (out_f32) ((float4*)(out_f32 + row * C))[idx] = y;
         if (out_t) {
             if constexpr (sizeof(T) == 2) {
@@ -78,9 +84,17 @@ __global__ __launch_bounds__(GN_THREADS) void groupnorm_kernel(const float* __re
                                                                const float* b1, int inst_per_set, int P, int Ctot,
                                                                int groups, float eps) {
     __shared__ float red[GN_THREADS / 64];
+    __shared__ float gbs[2 * GN_THREADS];  // this group's gamma, beta (cg <= 512), read behind the reductions
     const int inst = blockIdx.y, grp = blockIdx.x;
     const int cg = Ctot / groups, q = cg / 4, items = P * q;
     const int64_t base = (int64_t)inst * P * Ctot + grp * cg;
+    {  // issued before the input loads; block_sum's barriers publish them
+        const bool second = g1 && inst >= inst_per_set;
+        if ((int)threadIdx.x < cg) {
+            gbs[threadIdx.x] = (second ? g1 : g0)[grp * cg + threadIdx.x];
+            gbs[GN_THREADS + threadIdx.x] = (second ? b1 : b0)[grp * cg + threadIdx.x];
+        }
+    }
     // item -> (pixel, 4-channel chunk) without a runtime-divisor division per item: the float
     // quotient is exact (items < 2^24; (it + 0.5) / q sits >= 0.5 / q from an integer)
     const float inv_q = 1.f / (float)q;
@@ -113,9 +127,8 @@ __global__ __launch_bounds__(GN_THREADS) void groupnorm_kernel(const float* __re
         }
     }
     const float rstd = rsqrtf(block_sum<GN_THREADS>(sq, red) / n + eps);
-    const bool second = g1 && inst >= inst_per_set;
-    const float* gg = (second ? g1 : g0) + grp * cg;
-    const float* bb = (second ? b1 : b0) + grp * cg;
+    const float* gg = gbs;
+    const float* bb = gbs + GN_THREADS;
 #pragma unroll
     for (int i = 0; i < GN_VMAX; ++i) {
         const int it = threadIdx.x + GN_THREADS * i;
@@ -226,7 +239,8 @@ extern "C" int mmt_groupnorm(const float* in, float* out_f32, void* out_t, const
                              const float* gamma1, const float* beta1, int n_inst, int inst_per_set, int P, int Ctot,
                              int groups, float eps, int dtype, void* stream) {
     if (!in || !gamma0 || !beta0 || n_inst <= 0 || P <= 0 || groups <= 0 || Ctot % groups) return MMT_EBADARG;
-    if ((Ctot / groups) % 4 || (int64_t)P * (Ctot / groups / 4) > (int64_t)GN_THREADS * GN_VMAX) return MMT_EBADARG;
+    if ((Ctot / groups) % 4 || Ctot / groups > GN_THREADS || (int64_t)P * (Ctot / groups / 4) > (int64_t)GN_THREADS * GN_VMAX)
+        return MMT_EBADARG;
     if (inst_per_set <= 0) inst_per_set = n_inst;
     dim3 grid(groups, n_inst);
     hipStream_t st = (hipStream_t)stream;
