@@ -480,6 +480,36 @@ def test_mam_attention_extreme_scores(impl, asym):
 
 
 @pytest.mark.parametrize("asym", [0, 1])
+def test_mam_attention_pipelined_is_default_and_bitwise(asym):
+    """impl 21 (impl 17 with the two blocks of each tile software-pipelined) computes the same
+    MFMAs and exponentials in the same accumulation order, so its output is bit-identical to impl
+    17's; and it is what impl 0 launches on a large bf16 grid (B = 8: 480 workgroups)."""
+    L = _lib()
+    Bm, ntok, n_t, H = 8, 528, 128, 12
+    S, C = 2 * Bm, 64 * H
+    g = torch.Generator().manual_seed(123 + asym)
+    qkv = torch.randn(S, ntok, 3 * C, generator=g) * 0.5
+    qkv[..., :C] *= 0.125 * 1.4426950408889634  # the runtime's pre-scaled q
+    qd = qkv.bfloat16().cuda()
+    outs = {}
+    for impl in (17, 21, 0):
+        out = torch.empty(S, ntok, C, device="cuda", dtype=torch.bfloat16)
+        p = L.AttnParams()
+        p.qkv, p.out, p.S, p.Bm, p.ntok, p.n_t, p.C, p.H, p.asym = qd.data_ptr(), out.data_ptr(), S, Bm, ntok, n_t, C, H, asym
+        p.scale, p.impl = 1.0 / 1.4426950408889634, impl
+        L.check(L.LIB.mmt_mam_attention(p, L.MMT_BF16, torch.cuda.current_stream().cuda_stream), "attn")
+        torch.cuda.synchronize()
+        outs[impl] = out
+    assert torch.equal(outs[17], outs[21])
+    assert torch.equal(outs[21], outs[0])
+    qr = qkv.bfloat16().float()
+    qr[..., :C] /= 0.125 * 1.4426950408889634
+    ref = _attn_ref(qr[:4], 4, 2, ntok, n_t, C, H, 0) if not asym else None
+    if ref is not None:  # a spot check of the first 4 sequences against the fp32 reference
+        assert (outs[21][:4].float().cpu() - ref).abs().max().item() <= 1.5e-2
+
+
+@pytest.mark.parametrize("asym", [0, 1])
 @pytest.mark.parametrize("Bm,pitch,case", [(1, 0, "plain"), (5, 0, "prescaled"), (32, 0, "prescaled"), (3, 560, "plain"),
                                            (2, 0, "extreme")])
 def test_mam_attention_persistent_pair(asym, Bm, pitch, case):
