@@ -41,6 +41,11 @@ extern "C" int mmt_gemm_stamps(unsigned long long* host, int n) {
 
 namespace {
 
+template <int N>
+struct gemm_ic {
+    static constexpr int value = N;
+};
+
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void glb_void;
 
@@ -206,31 +211,31 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
         for (int j = 0; j < MT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     // Fragments of one K-step: [t][*] = the two 32-deep halves of the 64-deep step.
-#define MMT_READ(BUF, AF, BF)                                                                                    \
+#define MMT_READ(BUF, AF, BF, MTV)                                                                               \
     {                                                                                                            \
         const unsigned char* b_ = (BUF);                                                                         \
         _Pragma("unroll") for (int t = 0; t < 2; ++t) {                                                          \
             const int sw_ = (4 * t + lg) ^ (lane & 7);                                                           \
-            _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) AF[t][mt] =                                        \
+            _Pragma("unroll") for (int mt = 0; mt < MTV; ++mt) AF[t][mt] =                                       \
                 *(const u32x4*)(b_ + ((wr * WM + mt * 16 + l16) * 8 + sw_) * 16);                                \
             _Pragma("unroll") for (int nt = 0; nt < NT; ++nt) BF[t][nt] =                                        \
                 *(const u32x4*)(b_ + BM * 128 + ((wc * WN + nt * 16 + l16) * 8 + sw_) * 16);                     \
         }                                                                                                        \
         __builtin_amdgcn_sched_barrier(0); /* all reads issue before the MFMAs that hide them */                 \
     }
-#define MMT_MMA(AF, BF)                                                                                          \
+#define MMT_MMA(AF, BF, MTV)                                                                                     \
     {                                                                                                            \
         if (MMT_GEMM_ABLATE == 2) {                                                                              \
             acc[0][0] += __builtin_bit_cast(f32x4, AF[0][0]) + __builtin_bit_cast(f32x4, BF[1][NT - 1]);         \
         } else {                                                                                                 \
             _Pragma("unroll") for (int t = 0; t < 2; ++t)                                                        \
             _Pragma("unroll") for (int nt = 0; nt < NT; ++nt)                                                    \
-            _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) acc[nt][mt] =                                      \
+            _Pragma("unroll") for (int mt = 0; mt < MTV; ++mt) acc[nt][mt] =                                     \
                 mfma16x16x32<T>(BF[t][nt], AF[t][mt], acc[nt][mt]);                                              \
         }                                                                                                        \
         if constexpr (LNM == 1) { /* compile-time fragment index, scalar (wave-uniform) wave-column test; */     \
             /* packed fp32 sums (v_pk_add / v_pk_fma on the {lo, hi} bf16 pair), issued after the MFMAs */       \
-            _Pragma("unroll") for (int mt_ = 0; mt_ < MT; ++mt_) {                                               \
+            _Pragma("unroll") for (int mt_ = 0; mt_ < MTV; ++mt_) {                                              \
                 if (mt_ % WGN == wc_u) {                                                                         \
                     f32x2 sx_ = {0.f, 0.f}, sxx_ = {0.f, 0.f};                                                   \
                     _Pragma("unroll") for (int t = 0; t < 2; ++t)                                                \
@@ -257,33 +262,44 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
         lds_barrier();
         if (MMT_GEMM_ABLATE != 1 && j + ST - 1 < ns) issue(j + ST - 1);
     };
-    u32x4 fa0[2][MT], fb0[2][NT], fa1[2][MT], fb1[2][NT];
     for (int j = 0; j < ST - 1 && j < ns; ++j) issue(j);
     if (MMT_GEMM_ABLATE == 1) wait_vm<0>();
     sync_for(0);
     MMT_STAMP(2, "s_memtime");
-    MMT_READ(ring, fa0, fb0);
-    // Every k-group has a real K-step at j < ns-1; only the last can be empty (KS = 2 with an odd
-    // step count).  Keeping that test out of the loop keeps the accumulators in place (a
-    // conditional MFMA block inside the loop made hipcc shuttle them through VGPRs every step).
-    int s = 0;
-    for (; s + 2 < ns; s += 2) {
-        sync_for(s + 1);
-        MMT_READ(ring + ((s + 1) % ST) * STAGE, fa1, fb1);
-        MMT_MMA(fa0, fb0);
-        sync_for(s + 2);
-        MMT_READ(ring + ((s + 2) % ST) * STAGE, fa0, fb0);
-        MMT_MMA(fa1, fb1);
-    }
-    const bool last_ok = KS == 1 || (ns - 1) * KS + kg < nk;
-    if (s + 1 < ns) {
-        sync_for(s + 1);
-        MMT_READ(ring + ((s + 1) % ST) * STAGE, fa1, fb1);
-        MMT_MMA(fa0, fb0);
-        if (last_ok) MMT_MMA(fa1, fb1);
-    } else if (last_ok) {
-        MMT_MMA(fa0, fb0);
-    }
+    // MTV = this wave's 16-row fragments that hold rows < M.  The K loop is instantiated per MTV
+    // (all, 1, none: the row tails of the 528-row groups, M % 16 == 0) and chosen once, outside
+    // the loop, so the fragment reads and MFMAs of padding rows are never issued; the DMA and
+    // barriers are the same in every copy.
+    auto kloop = [&](auto MTVc) {
+        constexpr int MTV = decltype(MTVc)::value;
+        u32x4 fa0[2][MT], fb0[2][NT], fa1[2][MT], fb1[2][NT];
+        MMT_READ(ring, fa0, fb0, MTV);
+        // Every k-group has a real K-step at j < ns-1; only the last can be empty (KS = 2 with an odd
+        // step count).  Keeping that test out of the loop keeps the accumulators in place (a
+        // conditional MFMA block inside the loop made hipcc shuttle them through VGPRs every step).
+        int s = 0;
+        for (; s + 2 < ns; s += 2) {
+            sync_for(s + 1);
+            MMT_READ(ring + ((s + 1) % ST) * STAGE, fa1, fb1, MTV);
+            MMT_MMA(fa0, fb0, MTV);
+            sync_for(s + 2);
+            MMT_READ(ring + ((s + 2) % ST) * STAGE, fa0, fb0, MTV);
+            MMT_MMA(fa1, fb1, MTV);
+        }
+        const bool last_ok = KS == 1 || (ns - 1) * KS + kg < nk;
+        if (s + 1 < ns) {
+            sync_for(s + 1);
+            MMT_READ(ring + ((s + 1) % ST) * STAGE, fa1, fb1, MTV);
+            MMT_MMA(fa0, fb0, MTV);
+            if (last_ok) MMT_MMA(fa1, fb1, MTV);
+        } else if (last_ok) {
+            MMT_MMA(fa0, fb0, MTV);
+        }
+    };
+    const int mtv = __builtin_amdgcn_readfirstlane(min(max((M - m0 - wr * WM + 15) / 16, 0), MT));
+    if (mtv == 0) kloop(gemm_ic<0>{});
+    else if (mtv == 1 && MT > 1) kloop(gemm_ic<1>{});
+    else kloop(gemm_ic<MT>{});  // whole fragments (other partial counts: padding computed, not stored)
 #undef MMT_READ
 #undef MMT_MMA
     MMT_STAMP(3, "s_memtime");
