@@ -603,6 +603,12 @@ constexpr int FQ = 128, FTILE = 2 * KB * 128;
 #ifndef MMT_ATTN_FA_MIN_WG
 #define MMT_ATTN_FA_MIN_WG 200  // workgroups of the throughput kernel from which it is chosen
 #endif
+#ifndef MMT_ATTN_LZ2_MIN_WG
+// from this many 128-query workgroups (B >= 8 at ViT-B) the 64-queries-per-wave kernel (impl 22) is
+// the default: 2-wave workgroups underfill the SIMDs below it (B = 6: 21.5 vs 20.3 us; B = 8: 25.0
+// vs 27.0, B = 32: 78.6 vs 85.4 against impl 21, profiles/r02_lz2_ab.jsonl)
+#define MMT_ATTN_LZ2_MIN_WG 900
+#endif
 constexpr float FA_THR = 8.f;
 
 template <typename T, int FNS, int OCC>  // storage type, ring depth, workgroups per CU
@@ -1403,6 +1409,260 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     }
 }
 
+// ---- impl 22: the range-checked kernel with 64 queries per wave (large-grid default) ---------------
+// Two 32-query blocks per wave share every K / V fragment the wave reads from LDS (half the LDS
+// reads per FLOP of impl 17 / 21), and each wave carries two independent score -> exp -> PV chains;
+// 2 waves x 64 queries = 128 queries per workgroup as before, 2 waves per SIMD (up to 256 registers),
+// four workgroups per CU.  Wave 0 streams the tile's 8 K pieces, wave 1 its 8 V pieces.  The tile
+// loop is instantiated per count of the wave's active query blocks (2 / 1), chosen once.
+template <int FNS>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) void mam_attention_lz2_kernel(
+    const mmt_attn_params p) {
+    __shared__ __attribute__((aligned(1024))) char lds[FNS * FTILE];
+
+    const int n_t = p.n_t, ntok = p.ntok, C = p.C;
+    const int64_t pitch = p.tok_pitch > 0 ? p.tok_pitch : ntok;
+    const int nqb_t = (n_t + FQ - 1) / FQ;
+    int bx, h, s;
+    attn_block_ids_xcd(bx, h, s);
+    const int qb0 = bx + (p.q_part == 2 ? nqb_t : 0);
+    const bool tmpl = qb0 < nqb_t;
+    const int q0 = tmpl ? qb0 * FQ : n_t + (qb0 - nqb_t) * FQ;
+    const int qend = tmpl ? n_t : ntok;
+    const int Lk = tmpl ? n_t : (p.asym ? ntok + n_t : ntok);
+    const bool cross = p.asym && !tmpl;
+    const int64_t rs = 3 * (int64_t)C;
+    const bf16_t* qkv = (const bf16_t*)p.qkv;
+    const int sV = s % p.Bm, sI = sV + p.Bm;
+
+    const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int l32 = lane & 31, hf = lane >> 5;
+    const int prow = lane >> 3, pcol = lane & 7;
+
+    const int isv = w;  // wave 0: K pieces, wave 1: V pieces
+    const int64_t col = (isv ? 2 * C : C) + h * D + (isv ? (pcol ^ attn_vswz(prow)) : (pcol ^ prow)) * 8;
+    auto key_row = [&](int kk) -> const bf16_t* {
+        int seq = s, row = kk;
+        if (cross) {
+            if (kk < n_t) seq = sV;
+            else if (kk < 2 * n_t) { seq = sI; row = kk - n_t; }
+            else row = kk - n_t;
+        }
+        return qkv + ((int64_t)seq * pitch + row) * rs;
+    };
+    const bool aligned = n_t % KB == 0;
+    const int nkt = (Lk + KB - 1) / KB;
+    auto issue_tile = [&](int t) {
+        char* slot = lds + (t % FNS) * FTILE + isv * KB * 128;
+        if (aligned && t * KB + KB <= Lk) {
+            const bf16_t* base = key_row(t * KB);
+#pragma unroll
+            for (int pk = 0; pk < 8; ++pk) attn_glds16(base + (int64_t)(pk * 8 + prow) * rs + col, slot + pk * 1024);
+        } else {
+#pragma unroll
+            for (int pk = 0; pk < 8; ++pk) attn_glds16(key_row(min(t * KB + pk * 8 + prow, Lk - 1)) + col, slot + pk * 1024);
+        }
+    };
+    char* qimg = lds + (FNS - 1) * FTILE;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int piece = w * 8 + i, r = piece * 8 + prow;
+        const bf16_t* src = qkv + ((int64_t)s * pitch + min(q0 + r, qend - 1)) * rs + h * D;
+        attn_glds16(src + ((pcol ^ prow) * 8), qimg + piece * 1024);
+    }
+    for (int t = 0; t < FNS - 1 && t < nkt; ++t) issue_tile(t);
+
+    const int qbase = q0 + 64 * w;  // query blocks qbase + 32 qb + [0, 32)
+    const int nqa = (qbase < qend ? 1 : 0) + (qbase + 32 < qend ? 1 : 0);
+    const float cexp = p.scale * 1.4426950408889634f;
+    const bool prescale = fabsf(cexp - 1.f) > 1e-6f;
+    const float one_or_zero = (((lane & 15) >> 2) & 1) == ((lane >> 4) & 1) ? 1.f : 0.f;
+    const uint32_t sel_w = pack_bf16x2(one_or_zero, one_or_zero);
+    const bf16x8 sel = __builtin_bit_cast(bf16x8, u32x4{sel_w, sel_w, sel_w, sel_w});
+    const int kpos = (l32 & 7) * 16;
+    const int li = lane & 15, qr = li >> 2, pc = li & 3, dsub = (lane >> 4) & 1;
+
+    auto next_tile = [&](int kt) {
+        attn_wait_dyn(8 * (min(nkt - 1, kt + FNS - 2) - kt));
+        lds_barrier();
+        if (kt + FNS - 1 < nkt) issue_tile(kt + FNS - 1);
+    };
+    u32x4 qf[2][4];
+    {  // tile 0 and Q landed; Q into registers, then its slot takes tile FNS - 1
+        attn_wait_dyn(8 * (min(nkt - 1, FNS - 2)));
+        lds_barrier();
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+            const int row = 64 * w + 32 * qb + l32;
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) {
+                qf[qb][ks] = *(const u32x4*)(qimg + row * 128 + (((2 * ks + hf) ^ (row & 7)) * 16));
+                if (prescale) {
+                    u32x4 v = qf[qb][ks];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        v[e] = pack_bf16x2(__uint_as_float(v[e] << 16) * cexp, __uint_as_float(v[e] & 0xffff0000u) * cexp);
+                    qf[qb][ks] = v;
+                }
+            }
+        }
+        lds_barrier();
+        if (FNS - 1 < nkt) issue_tile(FNS - 1);
+    }
+    const int nfull = Lk / KB;
+
+    auto run = [&](auto NQc) {
+        constexpr int NQ = decltype(NQc)::value;
+        f32x16 o[NQ][2];
+        f32x4 lacc[NQ];
+#pragma unroll
+        for (int qb = 0; qb < NQ; ++qb) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) { o[qb][0][r] = 0.f; o[qb][1][r] = 0.f; }
+            lacc[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        auto block = [&](const char* kimg, int kb, int nv, auto NJc, auto MASKc) {
+            constexpr int NJ = decltype(NJc)::value;
+            constexpr bool MASK = decltype(MASKc)::value;
+            const char* vimg = kimg + KB * 128;
+            const char* krow = kimg + (32 * kb + l32) * 128;
+            u32x4 kf[4];
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) kf[ks] = *(const u32x4*)(krow + ((((2 * ks + hf) * 16) ^ kpos)));
+            f32x16 sacc[NQ];
+#pragma unroll
+            for (int qb = 0; qb < NQ; ++qb) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) sacc[qb][r] = 0.f;
+#pragma unroll
+                for (int ks = 0; ks < 4; ++ks)
+                    sacc[qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kf[ks]),
+                                                                       __builtin_bit_cast(bf16x8, qf[qb][ks]), sacc[qb], 0, 0, 0);
+            }
+            uint2 vt[NJ][2][2];
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int row = 32 * kb + 16 * j + 4 * hf + qr;
+#pragma unroll
+                for (int db = 0; db < 2; ++db) {
+                    const char* b1 = vimg + row * 128 + (((4 * db + 2 * dsub + (pc >> 1)) ^ attn_vswz(row)) * 16) + (pc & 1) * 8;
+                    vt[j][db][0] = attn_tr16<0>(b1);
+                    vt[j][db][1] = attn_tr16<8 * 128>(b1);
+                }
+            }
+#pragma unroll
+            for (int qb = 0; qb < NQ; ++qb)
+#pragma unroll
+                for (int r = 0; r < 8 * NJ; ++r) {
+                    float e = __builtin_amdgcn_exp2f(sacc[qb][r]);
+                    if constexpr (MASK) {
+                        if (32 * kb + 8 * (r >> 2) + 4 * hf + (r & 3) >= nv) e = 0.f;
+                    }
+                    sacc[qb][r] = e;
+                }
+            attn_lds_wait();
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int rb = 8 * j;
+                bf16x8 vf[2];
+#pragma unroll
+                for (int db = 0; db < 2; ++db) {
+                    const uint2 ua = vt[j][db][0], ub = vt[j][db][1];
+                    vf[db] = __builtin_bit_cast(bf16x8, make_uint4(ua.x, ua.y, ub.x, ub.y));
+                }
+#pragma unroll
+                for (int qb = 0; qb < NQ; ++qb) {
+                    const bf16x8 pf = __builtin_bit_cast(
+                        bf16x8, u32x4{pack_bf16x2(sacc[qb][rb], sacc[qb][rb + 1]), pack_bf16x2(sacc[qb][rb + 2], sacc[qb][rb + 3]),
+                                      pack_bf16x2(sacc[qb][rb + 4], sacc[qb][rb + 5]), pack_bf16x2(sacc[qb][rb + 6], sacc[qb][rb + 7])});
+#pragma unroll
+                    for (int db = 0; db < 2; ++db) o[qb][db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[db], pf, o[qb][db], 0, 0, 0);
+                    lacc[qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pf, lacc[qb], 0, 0, 0);
+                }
+            }
+        };
+        for (int kt = 0; kt < nfull; ++kt) {
+            const char* kimg = lds + (kt % FNS) * FTILE;
+            block(kimg, 0, KB, attn_ic<2>{}, attn_ic<0>{});
+            block(kimg, 1, KB, attn_ic<2>{}, attn_ic<0>{});
+            if (kt + 1 < nkt) next_tile(kt + 1);
+        }
+        if (nfull < nkt) {
+            const char* kimg = lds + (nfull % FNS) * FTILE;
+            const int nv = Lk - nfull * KB;
+            if (nv > 16) block(kimg, 0, nv, attn_ic<2>{}, attn_ic<1>{});
+            else block(kimg, 0, nv, attn_ic<1>{}, attn_ic<1>{});
+            if (nv > 48) block(kimg, 1, nv, attn_ic<2>{}, attn_ic<1>{});
+            else if (nv > 32) block(kimg, 1, nv, attn_ic<1>{}, attn_ic<1>{});
+        }
+        // per query block: range check, normalise and store, or the exact fallback
+#pragma unroll
+        for (int qb = 0; qb < NQ; ++qb) {
+            const float l = lacc[qb][0];
+            float chk = 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) chk += o[qb][0][r] * 0.f + o[qb][1][r] * 0.f;
+            const bool ok = l >= LZ_LO && l <= LZ_HI && chk == 0.f;
+            const int q = qbase + 32 * qb + l32;
+            bf16_t* op = (bf16_t*)p.out + ((int64_t)s * pitch + q) * C + h * D;
+            if (__builtin_expect(__all(ok), 1)) {
+                const float inv = 1.f / l;
+                if (q < qend) {
+#pragma unroll
+                    for (int db = 0; db < 2; ++db)
+#pragma unroll
+                        for (int g = 0; g < 4; ++g)
+                            *(uint2*)(op + 32 * db + 8 * g + 4 * hf) =
+                                make_uint2(pack_bf16x2(o[qb][db][4 * g] * inv, o[qb][db][4 * g + 1] * inv),
+                                           pack_bf16x2(o[qb][db][4 * g + 2] * inv, o[qb][db][4 * g + 3] * inv));
+                }
+                continue;
+            }
+            float qv[32], acc[32];
+            const int qc = min(q, qend - 1);
+            {
+                const bf16_t* qp = qkv + ((int64_t)s * pitch + qc) * rs + h * D + 32 * hf;
+#pragma unroll
+                for (int i = 0; i < 32; ++i) qv[i] = bf2f(qp[i]) * cexp;
+            }
+            auto score = [&](int kk) {
+                const bf16_t* kp = key_row(kk) + C + h * D + 32 * hf;
+                float d0 = 0.f;
+#pragma unroll
+                for (int i = 0; i < 32; ++i) d0 += qv[i] * bf2f(kp[i]);
+                return d0 + __shfl_xor(d0, 32, 64);
+            };
+            float m = -INFINITY;
+            for (int kk = 0; kk < Lk; ++kk) m = fmaxf(m, score(kk));
+            float lf = 0.f;
+#pragma unroll
+            for (int i = 0; i < 32; ++i) acc[i] = 0.f;
+            for (int kk = 0; kk < Lk; ++kk) {
+                const float e = __builtin_amdgcn_exp2f(score(kk) - m);
+                lf += e;
+                const bf16_t* vp = key_row(kk) + 2 * C + h * D + 32 * hf;
+#pragma unroll
+                for (int i = 0; i < 32; ++i) acc[i] += e * bf2f(vp[i]);
+            }
+            if (q < qend) {
+                const float inv = 1.f / lf;
+#pragma unroll
+                for (int i = 0; i < 32; i += 8)
+                    *(u32x4*)(op + 32 * hf + i) = u32x4{pack_bf16x2(acc[i] * inv, acc[i + 1] * inv), pack_bf16x2(acc[i + 2] * inv, acc[i + 3] * inv),
+                                                        pack_bf16x2(acc[i + 4] * inv, acc[i + 5] * inv), pack_bf16x2(acc[i + 6] * inv, acc[i + 7] * inv)};
+            }
+        }
+    };
+    if (nqa == 2) {
+        run(attn_ic<2>{});
+    } else if (nqa == 1) {
+        run(attn_ic<1>{});
+    } else {  // no queries: keep the DMA and barrier schedule of the workgroup
+        for (int kt = 0; kt < nfull; ++kt)
+            if (kt + 1 < nkt) next_tile(kt + 1);
+    }
+}
+
 // ---- impl 20: persistent whole-pair kernel (bf16 inference, batched grids) ------------------------
 // The throughput kernels above give each (sequence, head) pair 4-5 query-block workgroups, and each
 // of them streams the pair's whole K / V through its own LDS: 38 tiles of 16 KiB per pair, which
@@ -1827,7 +2087,7 @@ static bool pw_shape_ok(const mmt_attn_params& p) {
 
 template <typename T>
 int launch_attn(const mmt_attn_params& p, hipStream_t st) {
-    if (p.impl != 0 && p.impl != 2 && p.impl != 4 && (p.impl < 8 || p.impl > 12) && (p.impl < 16 || p.impl > 21))
+    if (p.impl != 0 && p.impl != 2 && p.impl != 4 && (p.impl < 8 || p.impl > 12) && (p.impl < 16 || p.impl > 22))
         return MMT_EBADARG;
     if (p.lse && (sizeof(T) != 2 || p.impl == 9 || (p.impl > 9 && p.impl < 16))) return MMT_EBADARG;
     // fp16: the kernels with a running maximum (latency kernel, throughput kernel); the range-checked
@@ -1865,13 +2125,19 @@ int launch_attn(const mmt_attn_params& p, hipStream_t st) {
             else if (p.impl == 17) hipLaunchKernelGGL((mam_attention_lz_kernel<3, 3, true>), fgrid, dim3(256), 0, st, p);
             else if (p.impl == 18) hipLaunchKernelGGL((mam_attention_lz_kernel<2, 3, false>), fgrid, dim3(256), 0, st, p);
             else if (p.impl == 21) hipLaunchKernelGGL((mam_attention_lz_kernel<3, 3, true, true>), fgrid, dim3(256), 0, st, p);
+            else if (p.impl == 22) hipLaunchKernelGGL((mam_attention_lz2_kernel<2>), fgrid, dim3(128), 0, st, p);
             else hipLaunchKernelGGL((mam_attention_lz_kernel<3, 2, false>), fgrid, dim3(256), 0, st, p);
             return launch_status();
         }
-        // large grids, bf16 inference: the range-checked exponent kernel with its two blocks per tile
-        // software-pipelined (impl 21; B = 8 / 32: 27.2 / 78.9 us against 29.8 / 83.8 for impl 17 and
-        // 30-34 / 84-93 for impl 8, profiles/r02_attn_ab.jsonl, r02_pipe_ab.jsonl); the training
-        // forward (lse) and fp16 keep the running-maximum throughput kernel
+        // large grids, bf16 inference: the range-checked exponent kernel, 64 queries per wave from
+        // MMT_ATTN_LZ2_MIN_WG workgroups (impl 22), else with its two blocks per tile software-
+        // pipelined (impl 21; B = 8 / 32: 27.2 / 78.9 us against 29.8 / 83.8 for impl 17 and 30-34 /
+        // 84-93 for impl 8, profiles/r02_attn_ab.jsonl, r02_pipe_ab.jsonl); the training forward
+        // (lse) and fp16 keep the running-maximum throughput kernel
+        if (p.impl == 0 && !p.lse && __is_same(T, bf16_t) && (int64_t)nfa * p.H * p.S >= MMT_ATTN_LZ2_MIN_WG) {
+            hipLaunchKernelGGL((mam_attention_lz2_kernel<2>), fgrid, dim3(128), 0, st, p);
+            return launch_status();
+        }
         if (p.impl == 0 && !p.lse && __is_same(T, bf16_t) && (int64_t)nfa * p.H * p.S >= MMT_ATTN_FA_MIN_WG) {
             hipLaunchKernelGGL((mam_attention_lz_kernel<3, 3, true, true>), fgrid, dim3(256), 0, st, p);
             return launch_status();

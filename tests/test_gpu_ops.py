@@ -373,7 +373,7 @@ def _attn_ref(qkv, S, Bm, ntok, n_t, C, H, asym):
     return out.permute(0, 2, 1, 3).reshape(S, ntok, C)
 
 
-ATTN_BF16_IMPLS = [2, 4, 8, 9, 10, 11, 12, 16, 17, 18, 19, 21]
+ATTN_BF16_IMPLS = [2, 4, 8, 9, 10, 11, 12, 16, 17, 18, 19, 21, 22]
 
 
 @pytest.mark.parametrize("dname,impl", [("f32", 0), ("bf16", 0)] + [("bf16", i) for i in ATTN_BF16_IMPLS]
@@ -424,7 +424,7 @@ def test_mam_attention_rescale_branch(dname, impl):
     assert (out.float().cpu() - ref).abs().max().item() < (1.5e-2 if dt != torch.float32 else 5e-5)
 
 
-@pytest.mark.parametrize("impl", [0, 2, 4, 8, 9, 10, 12, 16, 17, 18, 19, 21])
+@pytest.mark.parametrize("impl", [0, 2, 4, 8, 9, 10, 12, 16, 17, 18, 19, 21, 22])
 @pytest.mark.parametrize("asym", [0, 1])
 def test_mam_attention_prescaled_q(impl, asym):
     """The runtime's convention (bf16): q arrives multiplied by scale * log2(e) (folded into the qkv
@@ -451,7 +451,7 @@ def test_mam_attention_prescaled_q(impl, asym):
     assert err <= 1.5e-2, err
 
 
-@pytest.mark.parametrize("impl", [0, 4, 8, 16, 17, 21])
+@pytest.mark.parametrize("impl", [0, 4, 8, 16, 17, 21, 22])
 @pytest.mark.parametrize("asym", [0, 1])
 def test_mam_attention_extreme_scores(impl, asym):
     """Scores far outside the fp32 exponent range of exp2 without a reference point: a key that
@@ -481,9 +481,10 @@ def test_mam_attention_extreme_scores(impl, asym):
 
 @pytest.mark.parametrize("asym", [0, 1])
 def test_mam_attention_pipelined_is_default_and_bitwise(asym):
-    """impl 21 (impl 17 with the two blocks of each tile software-pipelined) computes the same
-    MFMAs and exponentials in the same accumulation order, so its output is bit-identical to impl
-    17's; and it is what impl 0 launches on a large bf16 grid (B = 8: 480 workgroups)."""
+    """impl 21 (impl 17 with the two blocks of each tile software-pipelined) and impl 22 (64
+    queries per wave sharing the K / V fragments) compute the same MFMAs and exponentials per query
+    in the same accumulation order, so their outputs are bit-identical to impl 17's; impl 0 launches
+    impl 22 on this grid (B = 8: 960 workgroups of 128 queries)."""
     L = _lib()
     Bm, ntok, n_t, H = 8, 528, 128, 12
     S, C = 2 * Bm, 64 * H
@@ -492,7 +493,7 @@ def test_mam_attention_pipelined_is_default_and_bitwise(asym):
     qkv[..., :C] *= 0.125 * 1.4426950408889634  # the runtime's pre-scaled q
     qd = qkv.bfloat16().cuda()
     outs = {}
-    for impl in (17, 21, 0):
+    for impl in (17, 21, 22, 0):
         out = torch.empty(S, ntok, C, device="cuda", dtype=torch.bfloat16)
         p = L.AttnParams()
         p.qkv, p.out, p.S, p.Bm, p.ntok, p.n_t, p.C, p.H, p.asym = qd.data_ptr(), out.data_ptr(), S, Bm, ntok, n_t, C, H, asym
@@ -501,7 +502,8 @@ def test_mam_attention_pipelined_is_default_and_bitwise(asym):
         torch.cuda.synchronize()
         outs[impl] = out
     assert torch.equal(outs[17], outs[21])
-    assert torch.equal(outs[21], outs[0])
+    assert torch.equal(outs[17], outs[22])
+    assert torch.equal(outs[22], outs[0])
     qr = qkv.bfloat16().float()
     qr[..., :C] /= 0.125 * 1.4426950408889634
     ref = _attn_ref(qr[:4], 4, 2, ntok, n_t, C, H, 0) if not asym else None
