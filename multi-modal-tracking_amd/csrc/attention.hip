@@ -1417,7 +1417,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 // loop is instantiated per count of the wave's active query blocks (2 / 1), chosen once.
 // SPLIT: block 1's exponentials after the V^T wait, below its scheduling barrier, so they interleave
 // with block 0's PV MFMAs (B = 8 / 16 / 32: 26.6 / 47.2 / 78.8 -> 25.6 / 44.3 / 76.9 us, bit-identical)
-template <int FNS, bool SPLIT = true>
+// PIPE2: on full tiles both key blocks' scores (both query blocks) come before any exponential, so
+// the second key block's QK^T MFMAs run beside the first block's softmax (B = 8 / 16 / 32: 27.2 /
+// 47.1 / 75.2 -> 24.9 / 43.5 / 72.1 us, bit-identical; 243 VGPRs)
+template <int FNS, bool SPLIT = true, bool PIPE2 = true>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) void mam_attention_lz2_kernel(
     const mmt_attn_params p) {
     __shared__ __attribute__((aligned(1024))) char lds[FNS * FTILE];
@@ -1591,10 +1594,76 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                 }
             }
         };
+        // a full tile with both key blocks' scores computed before any exponential (PIPE2)
+        auto tile2 = [&](const char* kimg) {
+            const char* vimg = kimg + KB * 128;
+            f32x16 sa[2][NQ];
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb) {
+                const char* krow = kimg + (32 * kb + l32) * 128;
+                u32x4 kf[4];
+#pragma unroll
+                for (int ks = 0; ks < 4; ++ks) kf[ks] = *(const u32x4*)(krow + ((((2 * ks + hf) * 16) ^ kpos)));
+#pragma unroll
+                for (int qb = 0; qb < NQ; ++qb) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) sa[kb][qb][r] = 0.f;
+#pragma unroll
+                    for (int ks = 0; ks < 4; ++ks)
+                        sa[kb][qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kf[ks]),
+                                                                             __builtin_bit_cast(bf16x8, qf[qb][ks]), sa[kb][qb], 0, 0, 0);
+                }
+            }
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb) {
+                uint2 vt[2][2][2];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int row = 32 * kb + 16 * j + 4 * hf + qr;
+#pragma unroll
+                    for (int db = 0; db < 2; ++db) {
+                        const char* b1 = vimg + row * 128 + (((4 * db + 2 * dsub + (pc >> 1)) ^ attn_vswz(row)) * 16) + (pc & 1) * 8;
+                        vt[j][db][0] = attn_tr16<0>(b1);
+                        vt[j][db][1] = attn_tr16<8 * 128>(b1);
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < 16; ++r) sa[kb][0][r] = __builtin_amdgcn_exp2f(sa[kb][0][r]);
+                attn_lds_wait();
+                if constexpr (NQ == 2) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) sa[kb][1][r] = __builtin_amdgcn_exp2f(sa[kb][1][r]);
+                }
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int rb = 8 * j;
+                    bf16x8 vf[2];
+#pragma unroll
+                    for (int db = 0; db < 2; ++db) {
+                        const uint2 ua = vt[j][db][0], ub = vt[j][db][1];
+                        vf[db] = __builtin_bit_cast(bf16x8, make_uint4(ua.x, ua.y, ub.x, ub.y));
+                    }
+#pragma unroll
+                    for (int qb = 0; qb < NQ; ++qb) {
+                        const f32x16& sv = sa[kb][qb];
+                        const bf16x8 pf = __builtin_bit_cast(
+                            bf16x8, u32x4{pack_bf16x2(sv[rb], sv[rb + 1]), pack_bf16x2(sv[rb + 2], sv[rb + 3]),
+                                          pack_bf16x2(sv[rb + 4], sv[rb + 5]), pack_bf16x2(sv[rb + 6], sv[rb + 7])});
+#pragma unroll
+                        for (int db = 0; db < 2; ++db) o[qb][db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[db], pf, o[qb][db], 0, 0, 0);
+                        lacc[qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pf, lacc[qb], 0, 0, 0);
+                    }
+                }
+            }
+        };
         for (int kt = 0; kt < nfull; ++kt) {
             const char* kimg = lds + (kt % FNS) * FTILE;
-            block(kimg, 0, KB, attn_ic<2>{}, attn_ic<0>{});
-            block(kimg, 1, KB, attn_ic<2>{}, attn_ic<0>{});
+            if constexpr (PIPE2) {
+                tile2(kimg);
+            } else {
+                block(kimg, 0, KB, attn_ic<2>{}, attn_ic<0>{});
+                block(kimg, 1, KB, attn_ic<2>{}, attn_ic<0>{});
+            }
             if (kt + 1 < nkt) next_tile(kt + 1);
         }
         if (nfull < nkt) {
