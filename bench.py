@@ -463,9 +463,10 @@ def main():
             "higher_is_better": True, "scaling": "strong" if sharded else "weak", "vs_baseline": None,
             "dtype": args.dtype,
             "data": "synthetic N(0,1) frames (seeded), seed-hash random-init weights (mmt-synth-v1)",
-            "config": {"workload": "%s %s %dpx template x2 + %dpx search, RGB+TIR, %s%s"
+            "config": {"workload": "%s %s %dpx template x2 + %dpx search, %s, %s%s"
                                    % (VARIANT_NAMES[args.variant], "ViT-L" if args.vitl else "ViT-B", geo["template"],
-                                      geo["search"], load, ", score head on" if score else ""),
+                                      geo["search"], "RGB" if args.variant == "rgb" else "RGB+TIR", load,
+                                      ", score head on" if score else ""),
                        "variant": args.variant, "batch_per_gpu": B, "total_sequences": args.total_seqs or None,
                        "template": geo["template"], "search": geo["search"], "hidden": geo["hidden"],
                        "depth": geo["depth"],
