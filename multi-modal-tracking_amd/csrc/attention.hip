@@ -1490,7 +1490,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     auto next_tile = [&](int kt) {
         attn_wait_dyn(8 * (min(nkt - 1, kt + FNS - 2) - kt));
         lds_barrier();
-        if (kt + FNS - 1 < nkt) issue_tile(kt + FNS - 1);
+        if (MMT_ATTN_ABLATE != 1 && kt + FNS - 1 < nkt) issue_tile(kt + FNS - 1);
     };
     u32x4 qf[2][4];
     {  // tile 0 and Q landed; Q into registers, then its slot takes tile FNS - 1
@@ -1558,7 +1558,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             auto expo = [&](int qb) {
 #pragma unroll
                 for (int r = 0; r < 8 * NJ; ++r) {
-                    float e = __builtin_amdgcn_exp2f(sacc[qb][r]);
+                    float e = MMT_ATTN_ABLATE == 3 ? sacc[qb][r] : __builtin_amdgcn_exp2f(sacc[qb][r]);
                     if constexpr (MASK) {
                         if (32 * kb + 8 * (r >> 2) + 4 * hf + (r & 3) >= nv) e = 0.f;
                     }
@@ -1628,11 +1628,11 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                     }
                 }
 #pragma unroll
-                for (int r = 0; r < 16; ++r) sa[kb][0][r] = __builtin_amdgcn_exp2f(sa[kb][0][r]);
+                for (int r = 0; r < 16; ++r) sa[kb][0][r] = MMT_ATTN_ABLATE == 3 ? sa[kb][0][r] : __builtin_amdgcn_exp2f(sa[kb][0][r]);
                 attn_lds_wait();
                 if constexpr (NQ == 2) {
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) sa[kb][1][r] = __builtin_amdgcn_exp2f(sa[kb][1][r]);
+                    for (int r = 0; r < 16; ++r) sa[kb][1][r] = MMT_ATTN_ABLATE == 3 ? sa[kb][1][r] : __builtin_amdgcn_exp2f(sa[kb][1][r]);
                 }
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
@@ -1732,7 +1732,10 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             }
         }
     };
-    if (nqa == 2) {
+    if (MMT_ATTN_ABLATE == 2) {  // measurement build: the DMA / barrier skeleton alone
+        for (int kt = 0; kt < nfull; ++kt)
+            if (kt + 1 < nkt) next_tile(kt + 1);
+    } else if (nqa == 2) {
         run(attn_ic<2>{});
     } else if (nqa == 1) {
         run(attn_ic<1>{});
