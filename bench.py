@@ -32,6 +32,7 @@ Extra fields:
                  on a bounded sample, rank 0 at N=1 only
 """
 import argparse
+import ctypes
 import json
 import os
 import socket
@@ -91,6 +92,8 @@ def plan_flops(rt, entry):
         return 0.0
     if hasattr(keep, "K"):
         return 2.0 * keep.M * keep.N * keep.K * keep.groups
+    if isinstance(keep, ctypes.Array):  # mmt_gemm_multi: independent problems in one launch
+        return sum(2.0 * q.M * q.N * q.K * q.groups for q in keep)
     d = rt.d
     ntok = keep.ntok  # < d.ntok after a candidate-elimination stage
     lk_s = ntok + (d.n_t if keep.asym else 0)

@@ -138,6 +138,17 @@ typedef struct {
 
 int mmt_gemm(const mmt_gemm_params* p, int dtype, void* stream);
 
+/* n (1..4) independent GEMMs / convolutions ps[0..n-1] (each as mmt_gemm; none may write what
+ * another reads) in ONE launch when the 16-bit LDS-DMA kernel takes them all in one tile shape
+ * (all GEMM or all conv mode, no folded LayerNorm, equal impl; split-K is not used), else one
+ * launch each.  The tile shape is chosen for the union, so results equal mmt_gemm's up to the fp32
+ * summation order of the tile shape (bit-identical for an equal forced impl).  The frame plan uses
+ * it for the corner head's parallel conv chains (lib/models/mixformer_cvt/head.py:159-197: conv3
+ * beside adjust3[0]; conv4 beside adjust4[0] and adjust3[1]) and the encoder's value / offset
+ * Linears (ops/modules/ms_deform_attn_bimodal.py:103-110), which are independent and a few
+ * workgroups each. */
+int mmt_gemm_multi(const mmt_gemm_params* ps, int n, int dtype, void* stream);
+
 /* ---------------------------------------------------------------- MAM attention
  * qkv: [S][ntok][3*C] (dtype) as produced by the fused qkv Linear (reshape(B,N,3,H,d) order);
  * out: [S][ntok][C].  Queries [0,n_t) attend keys [0,n_t) of their own sequence; queries

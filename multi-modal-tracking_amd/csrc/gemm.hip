@@ -320,8 +320,9 @@ __global__ __launch_bounds__(256) void gemv_f32_kernel(const float* __restrict__
     }
 }
 
+// Argument checks shared by mmt_gemm and mmt_gemm_multi: 0 or MMT_EBADARG.
 template <typename T>
-int launch_gemm(const mmt_gemm_params& p, hipStream_t st) {
+int check_gemm(const mmt_gemm_params& p) {
     const int EPC = 16 / (int)sizeof(T);
     if (p.M <= 0 || p.N <= 0 || p.K <= 0 || p.groups < 1 || p.groups > MMT_MAX_GROUPS) return MMT_EBADARG;
     if (p.impl < -1 || p.impl > 4) return MMT_EBADARG;
@@ -343,6 +344,12 @@ int launch_gemm(const mmt_gemm_params& p, hipStream_t st) {
         if (p.k_split > 0 && p.conv_h == 0 && (!p.a1[g] || ((uintptr_t)p.a1[g] & 15))) return MMT_EBADARG;
         if (p.c2[g] && !p.r[g]) return MMT_EBADARG;
     }
+    return 0;
+}
+
+template <typename T>
+int launch_gemm(const mmt_gemm_params& p, hipStream_t st) {
+    if (const int e = check_gemm<T>(p)) return e;
     if (sizeof(T) == 4 && p.M <= GEMV_MAXM && p.groups == 1 && p.conv_h == 0 && !p.r[0] && !p.c2[0] && p.c_f32 &&
         p.k_split == 0 && !p.ln_fold && p.splitk == 0 && p.c_seg_rows == 0 && p.a_seg_rows >= p.M && p.K % 4 == 0 &&
         p.lda % 4 == 0 && p.impl <= 0) {
@@ -359,7 +366,29 @@ int launch_gemm(const mmt_gemm_params& p, hipStream_t st) {
     return launch_status();
 }
 
+// Independent problems in one launch when the LDS-DMA kernel takes them all in one configuration,
+// else one launch each (same results up to the fp32 summation order of the chosen tile shapes).
+template <typename T>
+int launch_gemm_multi(const mmt_gemm_params* ps, int n, hipStream_t st) {
+    if (n < 1 || n > 4) return MMT_EBADARG;
+    for (int i = 0; i < n; ++i)
+        if (const int e = check_gemm<T>(ps[i])) return e;
+    if constexpr (sizeof(T) == 2)
+        if (mmt_gemm_glds_multi<T>(ps, n, st) == 0) return launch_status();
+    for (int i = 0; i < n; ++i)
+        if (const int e = launch_gemm<T>(ps[i], st)) return e;
+    return 0;
+}
+
 }  // namespace
+
+extern "C" int mmt_gemm_multi(const mmt_gemm_params* ps, int n, int dtype, void* stream) {
+    if (!ps) return MMT_EBADARG;
+    if (dtype == MMT_BF16) return launch_gemm_multi<bf16_t>(ps, n, (hipStream_t)stream);
+    if (dtype == MMT_F16) return launch_gemm_multi<f16_t>(ps, n, (hipStream_t)stream);
+    if (dtype == MMT_F32) return launch_gemm_multi<float>(ps, n, (hipStream_t)stream);
+    return MMT_EBADARG;
+}
 
 extern "C" int mmt_gemm(const mmt_gemm_params* p, int dtype, void* stream) {
     if (!p) return MMT_EBADARG;

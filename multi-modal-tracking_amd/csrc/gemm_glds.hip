@@ -79,9 +79,8 @@ __device__ __attribute__((aligned(64))) const uint32_t g_zero_chunk[16] = {0};
 // waves already hold for the MFMAs (wave column wc sums fragment rows mt = wc, wc + WGN, ...), so
 // the normalised operand never exists in memory and the LayerNorm launch disappears.
 template <typename T, int BM, int BN, int WGM, int WGN, int KS, int ST, bool CONV, int LNM>
-__global__ __launch_bounds__(64 * WGM * WGN * KS)
-    __attribute__((amdgpu_waves_per_eu(WGM * WGN * KS / 4, WGM * WGN * KS / 4))) void gemm_glds_kernel(
-        const mmt_gemm_params p) {
+MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int tile, const int slice, const int nsk,
+                            const int ntiles) {
     constexpr int NW = WGM * WGN, TPG = 64 * NW;  // waves / threads per k-group
     constexpr int KT = 64;                        // bf16 elements of K per step: 128-B rows
     constexpr int STAGE = (BM + BN) * 128;        // bytes of one stage image (A rows, then W rows)
@@ -95,18 +94,6 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
     MMT_STAMP(0, "s_memrealtime");
     MMT_STAMP(1, "s_memtime");
 
-    // XCD-aware bijective remap (see gemm.hip): each XCD gets a contiguous run of (group, tile,
-    // K-slice) ids, slice fastest then tm, so a run's W column slices and A rows stay in that XCD's
-    // L2 and a tile's split-K partials are mostly written and summed on one XCD (speed only: the
-    // hand-off below is correct for any placement).
-    const int nsk = gridDim.y;  // split-K slices per tile
-    const int nwg = gridDim.x * gridDim.y * gridDim.z;
-    const int orig = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-    const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-    const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-    const int per_g = gridDim.x * nsk;
-    const int g = lin / per_g, rem_t = lin - g * per_g;
-    const int tile = rem_t / nsk, slice = rem_t - tile * nsk;
     const int tiles_m = (p.M + BM - 1) / BM;
     const int tm = tile % tiles_m, tn = tile / tiles_m;
     constexpr bool LNF = LNM != 0;  // LayerNorm folded: 1 = row statistics from the A fragments, 2 = handed in
@@ -399,7 +386,7 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
     // either), summing the nsk partials in SLICE order (its own from LDS): the result does not
     // depend on which slice arrives last.  It alone runs the epilogue.
     if (nsk > 1) {
-        const int64_t tix = (int64_t)g * gridDim.x + tile;
+        const int64_t tix = (int64_t)g * ntiles + tile;
         constexpr int SLAB = BM * BN * 4;  // bytes of one partial tile
         const __amdgpu_buffer_rsrc_t slabs = __builtin_amdgcn_make_buffer_rsrc(
             p.sk_ws + tix * nsk * (BM * BN), (short)0, nsk * SLAB, 0x00020000);
@@ -576,6 +563,54 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
     MMT_STAMP(7, "s_memrealtime");
 }
 
+// XCD-aware bijective remap of the launch's workgroup ids (see gemm.hip): each XCD gets a contiguous
+// run of the linear ids, so a run's W column slices and A rows stay in that XCD's L2 and a tile's
+// split-K partials are mostly written and summed on one XCD (speed only: the hand-off is correct
+// for any placement).
+MMT_DEV int gemm_xcd_lin() {
+    const int nwg = gridDim.x * gridDim.y * gridDim.z;
+    const int orig = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+}
+
+// One GEMM: grid (tiles, split-K slices, groups); linear ids (group, tile, slice), slice fastest.
+template <typename T, int BM, int BN, int WGM, int WGN, int KS, int ST, bool CONV, int LNM>
+__global__ __launch_bounds__(64 * WGM * WGN * KS)
+    __attribute__((amdgpu_waves_per_eu(WGM * WGN * KS / 4, WGM * WGN * KS / 4))) void gemm_glds_kernel(
+        const mmt_gemm_params p) {
+    const int nsk = gridDim.y;  // split-K slices per tile
+    const int lin = gemm_xcd_lin();
+    const int per_g = gridDim.x * nsk;
+    const int g = lin / per_g, rem_t = lin - g * per_g;
+    const int tile = rem_t / nsk, slice = rem_t - tile * nsk;
+    gemm_glds_tile<T, BM, BN, WGM, WGN, KS, ST, CONV, LNM>(p, g, tile, slice, nsk, gridDim.x);
+}
+
+// Several independent GEMMs of one kernel configuration in one launch (mmt_gemm_multi): problem i
+// owns the remapped linear ids [wg0[i], wg0[i + 1]), (group, tile) with the tile fastest, no split-K.
+// The head's parallel conv chains and the fusion encoder's value / offset Linears are each a
+// handful of workgroups, so side by side they share one launch's latency instead of paying it twice.
+constexpr int GEMM_MULTI = 4;
+struct gemm_multi_args {
+    mmt_gemm_params p[GEMM_MULTI];
+    int32_t wg0[GEMM_MULTI + 1];
+    int32_t tiles[GEMM_MULTI];
+    int32_t n;
+};
+
+template <typename T, int BM, int BN, int WGM, int WGN, int KS, int ST, bool CONV>
+__global__ __launch_bounds__(64 * WGM * WGN * KS)
+    __attribute__((amdgpu_waves_per_eu(WGM * WGN * KS / 4, WGM * WGN * KS / 4))) void gemm_glds_multi_kernel(
+        const gemm_multi_args a) {
+    const int lin = gemm_xcd_lin();
+    int i = 0;
+    while (i + 1 < a.n && lin >= a.wg0[i + 1]) ++i;  // wave-uniform (scalar)
+    const int loc = lin - a.wg0[i], nt = a.tiles[i];
+    const int g = loc / nt;
+    gemm_glds_tile<T, BM, BN, WGM, WGN, KS, ST, CONV, 0>(a.p[i], g, loc - g * nt, 0, 1, nt);
+}
+
 template <typename T, int BM, int BN, int WGM, int WGN, int KS, int ST>
 void launch(const mmt_gemm_params& p, int nsk, hipStream_t st) {
     const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
@@ -592,56 +627,65 @@ void launch(const mmt_gemm_params& p, int nsk, hipStream_t st) {
 
 bool aligned(const void* ptr, int bytes) { return ((uintptr_t)ptr & (uintptr_t)(bytes - 1)) == 0; }
 
+// Whether the shape / layout is one the LDS-DMA kernel takes.
+bool glds_takes(const mmt_gemm_params& p) {
+    if (p.K % 8 || p.N % 8 || p.ldc % 8 || (p.r[0] && p.ldr % 8)) return false;
+    if (p.ln_fold && p.conv_h > 0) return false;
+    if (p.ln_fold == 2 && (p.a_seg_rows < p.M || p.k_split || p.K % 64 || p.K > 64 * 8 * 2)) return false;  // identity A map
+    for (int g = 0; g < p.groups; ++g) {
+        if (p.ln_fold == 2 && (!p.ln_stats_in[g] || !aligned(p.ln_stats_in[g], 8))) return false;
+        if (p.ln_stats_out[g] && (!p.c2_copy || !p.c2[g] || p.N % 64 || !aligned(p.ln_stats_out[g], 8))) return false;
+    }
+    if (p.conv_h > 0) {  // the kernel's conv addressing: power-of-two upsample, 32-bit element offsets
+        const int cup = p.conv_up, hi = p.conv_up > 0 ? p.conv_h / p.conv_up : 0;
+        if (cup <= 0 || (cup & (cup - 1)) || hi * cup != p.conv_h) return false;
+        const int64_t imgs = (p.M + (int64_t)p.conv_h * p.conv_h - 1) / ((int64_t)p.conv_h * p.conv_h);
+        const int64_t pitch = p.a_stride_a > 0 ? p.a_stride_a : (int64_t)hi * hi;
+        if ((imgs * pitch * (int64_t)p.lda + p.K) >= ((int64_t)1 << 32) || p.K >= (1 << 24)) return false;
+    }
+    if (p.lda % 8 || p.a_stride_a % 8 || p.a_stride_b % 8 || p.k_split % 8) return false;
+    if (p.a_seg_rows > INT32_MAX || p.a_segs_a > INT32_MAX) return false;
+    for (int g = 0; g < p.groups; ++g) {
+        if (!aligned(p.c[g], 16) || (p.c2[g] && !aligned(p.c2[g], 16))) return false;
+        if (p.bias[g] && !aligned(p.bias[g], 16)) return false;
+        if (p.r[g] && !aligned(p.r[g], 16)) return false;
+        if (p.ln_fold && (!p.ln_colsum[g] || !aligned(p.ln_colsum[g], 16))) return false;
+    }
+    return true;
+}
+
+// Cost model fitted to in-kernel stamps at batch 1 (tools/gemm_stamps.py): one workgroup per
+// CU (>= 128 KiB of LDS each), so time ~ rounds of 256 workgroups x (fixed prologue +
+// epilogue + K-steps per workgroup x time per step).  Per-step times are per-CU LDS-fill
+// bound: 128x128 (32 KiB/step) ~0.52 us, 128x64 with 2 k-groups ~0.52 us per pair of
+// steps, 64x64 with 2 k-groups ~0.33 us per pair.  A K split into n slices adds the partial
+// tile round trip of the last-arriving slice (~0.8 us + 0.5 us per 64 KiB slab it reads).
+struct Cand { int cfg, bm, bn, ks; float fixed_us, step_us; };
+constexpr Cand kCands[4] = {{1, 128, 128, 1, 6.0f, 0.52f}, {2, 128, 64, 2, 5.0f, 0.52f}, {3, 64, 64, 2, 3.2f, 0.33f},
+                            {4, 128, 128, 1, 6.0f, 0.60f}};
+int64_t tiles_of(const mmt_gemm_params& p, int bm, int bn) {
+    return (int64_t)((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn);
+}
+
 }  // namespace
 
 // Returns 1 when the shape / layout is not one this kernel takes (caller uses gemm.hip's kernel).
 template <typename T>
 int mmt_gemm_glds(const mmt_gemm_params& p, hipStream_t st, int force) {
-    if (force < 0) return 1;
-    if (p.K % 8 || p.N % 8 || p.ldc % 8 || (p.r[0] && p.ldr % 8)) return 1;
-    if (p.ln_fold && p.conv_h > 0) return 1;
-    if (p.ln_fold == 2 && (p.a_seg_rows < p.M || p.k_split || p.K % 64 || p.K > 64 * 8 * 2)) return 1;  // identity A map
-    for (int g = 0; g < p.groups; ++g) {
-        if (p.ln_fold == 2 && (!p.ln_stats_in[g] || !aligned(p.ln_stats_in[g], 8))) return 1;
-        if (p.ln_stats_out[g] && (!p.c2_copy || !p.c2[g] || p.N % 64 || !aligned(p.ln_stats_out[g], 8))) return 1;
-    }
-    if (p.conv_h > 0) {  // the kernel's conv addressing: power-of-two upsample, 32-bit element offsets
-        const int cup = p.conv_up, hi = p.conv_up > 0 ? p.conv_h / p.conv_up : 0;
-        if (cup <= 0 || (cup & (cup - 1)) || hi * cup != p.conv_h) return 1;
-        const int64_t imgs = (p.M + (int64_t)p.conv_h * p.conv_h - 1) / ((int64_t)p.conv_h * p.conv_h);
-        const int64_t pitch = p.a_stride_a > 0 ? p.a_stride_a : (int64_t)hi * hi;
-        if ((imgs * pitch * (int64_t)p.lda + p.K) >= ((int64_t)1 << 32) || p.K >= (1 << 24)) return 1;
-    }
-    if (p.lda % 8 || p.a_stride_a % 8 || p.a_stride_b % 8 || p.k_split % 8) return 1;
-    if (p.a_seg_rows > INT32_MAX || p.a_segs_a > INT32_MAX) return 1;
-    for (int g = 0; g < p.groups; ++g) {
-        if (!aligned(p.c[g], 16) || (p.c2[g] && !aligned(p.c2[g], 16))) return 1;
-        if (p.bias[g] && !aligned(p.bias[g], 16)) return 1;
-        if (p.r[g] && !aligned(p.r[g], 16)) return 1;
-        if (p.ln_fold && (!p.ln_colsum[g] || !aligned(p.ln_colsum[g], 16))) return 1;
-    }
-    auto tiles_of = [&](int bm, int bn) { return (int64_t)((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn); };
+    if (force < 0 || !glds_takes(p)) return 1;
     const int nk = (p.K + 63) / 64;
-    struct Cand { int cfg, bm, bn, ks; float fixed_us, step_us; };
-    // Cost model fitted to in-kernel stamps at batch 1 (tools/gemm_stamps.py): one workgroup per
-    // CU (>= 128 KiB of LDS each), so time ~ rounds of 256 workgroups x (fixed prologue +
-    // epilogue + K-steps per workgroup x time per step).  Per-step times are per-CU LDS-fill
-    // bound: 128x128 (32 KiB/step) ~0.52 us, 128x64 with 2 k-groups ~0.52 us per pair of
-    // steps, 64x64 with 2 k-groups ~0.33 us per pair.  A K split into n slices adds the partial
-    // tile round trip of the last-arriving slice (~0.8 us + 0.5 us per 64 KiB slab it reads).
-    const Cand cands[4] = {{1, 128, 128, 1, 6.0f, 0.52f}, {2, 128, 64, 2, 5.0f, 0.52f}, {3, 64, 64, 2, 3.2f, 0.33f},
-                           {4, 128, 128, 1, 6.0f, 0.60f}};
+    const Cand* cands = kCands;
     // largest split the workspace allows for a candidate (each slice keeps >= ks K-steps)
     auto max_split = [&](const Cand& c) -> int {
         if (p.ln_fold || !p.sk_ws || !p.sk_cnt) return 1;
-        const int64_t t = tiles_of(c.bm, c.bn) * p.groups;
+        const int64_t t = tiles_of(p, c.bm, c.bn) * p.groups;
         if (t > p.sk_cnt_n) return 1;
         int n = 8;
         while (n > 1 && ((int64_t)n * c.ks > nk || t * n * c.bm * c.bn > p.sk_ws_floats)) --n;
         return n;
     };
     auto cost = [&](const Cand& c, int n) {
-        const int64_t wg = tiles_of(c.bm, c.bn) * p.groups * n;
+        const int64_t wg = tiles_of(p, c.bm, c.bn) * p.groups * n;
         const int steps = (nk + n - 1) / n;
         const float red = n > 1 ? 0.8f + 0.5f * (float)(n - 1) * (float)(c.bm * c.bn) / 16384.f : 0.f;
         return (float)((wg + 255) / 256) * (c.fixed_us + (float)((steps + c.ks - 1) / c.ks) * c.step_us) + red;
@@ -680,5 +724,66 @@ int mmt_gemm_glds(const mmt_gemm_params& p, hipStream_t st, int force) {
     return 0;
 }
 
+namespace {
+template <typename T, int BM, int BN, int WGM, int WGN, int KS, int ST>
+void launch_multi(const mmt_gemm_params* ps, int n, bool conv, hipStream_t st) {
+    gemm_multi_args a{};
+    a.n = n;
+    a.wg0[0] = 0;
+    for (int i = 0; i < n; ++i) {
+        a.p[i] = ps[i];
+        a.tiles[i] = (int32_t)tiles_of(ps[i], BM, BN);
+        a.wg0[i + 1] = a.wg0[i] + a.tiles[i] * ps[i].groups;
+    }
+    const dim3 grid(a.wg0[n]), block(64 * WGM * WGN * KS);
+    if (conv) hipLaunchKernelGGL((gemm_glds_multi_kernel<T, BM, BN, WGM, WGN, KS, ST, true>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((gemm_glds_multi_kernel<T, BM, BN, WGM, WGN, KS, ST, false>), grid, block, 0, st, a);
+}
+}  // namespace
+
+// n independent GEMMs in one launch; returns 1 when some problem is not one the LDS-DMA kernel
+// takes in this mode (all GEMM or all conv, no folded LayerNorm, no split-K, one forced impl).  The
+// configuration is chosen once for the union: rounds of 256 workgroups over all problems times the
+// slowest problem's per-workgroup time (the cost model above).
+template <typename T>
+int mmt_gemm_glds_multi(const mmt_gemm_params* ps, int n, hipStream_t st) {
+    if (n < 1 || n > GEMM_MULTI) return 1;
+    const bool conv = ps[0].conv_h > 0;
+    const int force = ps[0].impl;
+    for (int i = 0; i < n; ++i) {
+        const mmt_gemm_params& p = ps[i];
+        if (!glds_takes(p) || (p.conv_h > 0) != conv || p.ln_fold || p.impl != force || force < 0 || force > 4) return 1;
+    }
+    int cfg = force;
+    if (cfg == 0) {
+        float best = 1e30f;
+        for (int ci = 0; ci < 3; ++ci) {
+            const Cand& c = kCands[ci];
+            int64_t wg = 0;
+            float slowest = 0.f;
+            for (int i = 0; i < n; ++i) {
+                wg += tiles_of(ps[i], c.bm, c.bn) * ps[i].groups;
+                const int steps = (ps[i].K + 63) / 64;
+                slowest = std::max(slowest, c.fixed_us + (float)((steps + c.ks - 1) / c.ks) * c.step_us);
+            }
+            const float t = (float)((wg + 255) / 256) * slowest;
+            if (t < best) best = t, cfg = c.cfg;
+        }
+    }
+    int64_t wg_total = 0;
+    for (int i = 0; i < n; ++i) wg_total += tiles_of(ps[i], kCands[cfg - 1].bm, kCands[cfg - 1].bn) * ps[i].groups;
+    if (wg_total > INT32_MAX) return 1;
+    switch (cfg) {
+        case 1: launch_multi<T, 128, 128, 2, 4, 1, 4>(ps, n, conv, st); break;
+        case 2: launch_multi<T, 128, 64, 2, 2, 2, 3>(ps, n, conv, st); break;
+        case 3: launch_multi<T, 64, 64, 2, 2, 2, 4>(ps, n, conv, st); break;
+        case 4: launch_multi<T, 128, 128, 2, 2, 1, 4>(ps, n, conv, st); break;
+        default: return 1;
+    }
+    return 0;
+}
+
 template int mmt_gemm_glds<bf16_t>(const mmt_gemm_params&, hipStream_t, int);
 template int mmt_gemm_glds<f16_t>(const mmt_gemm_params&, hipStream_t, int);
+template int mmt_gemm_glds_multi<bf16_t>(const mmt_gemm_params*, int, hipStream_t);
+template int mmt_gemm_glds_multi<f16_t>(const mmt_gemm_params*, int, hipStream_t);

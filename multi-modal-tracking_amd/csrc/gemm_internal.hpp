@@ -7,3 +7,8 @@
 // layout is not one it takes (the caller then runs gemm.hip's kernel).
 template <typename T>
 int mmt_gemm_glds(const mmt_gemm_params& p, hipStream_t st, int force);
+
+// n (1..4) independent problems of one LDS-DMA configuration in one launch (mmt_gemm_multi).
+// Returns 0 when launched, 1 when some problem does not qualify (the caller launches them one by one).
+template <typename T>
+int mmt_gemm_glds_multi(const mmt_gemm_params* ps, int n, hipStream_t st);

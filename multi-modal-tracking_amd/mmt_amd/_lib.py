@@ -64,6 +64,7 @@ class CropParams(ctypes.Structure):
 
 _PROTOS = {
     "mmt_gemm": [ctypes.POINTER(GemmParams), i32, vp],
+    "mmt_gemm_multi": [ctypes.POINTER(GemmParams), i32, i32, vp],
     "mmt_mam_attention": [ctypes.POINTER(AttnParams), i32, vp],
     "mmt_mam_attention_bwd": [ctypes.POINTER(AttnBwdParams), i32, vp],
     "mmt_transpose_bf16": [vp, vp, i32, i32, i64, i64, i32, i64, i64, vp],

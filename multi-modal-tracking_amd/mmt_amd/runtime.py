@@ -330,7 +330,8 @@ class MixFormerRGBTRuntime:
     # ------------------------------------------------------------------ plan construction
     def _gemm(self, plan, name, *, a, w, c, M, N, K, lda, ldc, bias=None, r=None, ldr=0, c2=None, a1=None,
               k_split=0, act=0, c_f32=0, seg=None, r_mode=0, r_p0=0, r_p1=1, conv=None, r_t=0, dtype=None,
-              ln_colsum=None, ln_eps=0.0, c2_copy=0, cmap=None, ln_stats_in=None, ln_stats_out=None):
+              ln_colsum=None, ln_eps=0.0, c2_copy=0, cmap=None, ln_stats_in=None, ln_stats_out=None, defer=None):
+        """Append one mmt_gemm launch to plan; defer=list: collect (params, dtype) for _gemm_multi instead."""
         p = GemmParams()
         G = len(a)
         for g in range(G):
@@ -369,7 +370,18 @@ class MixFormerRGBTRuntime:
         p.splitk = self.gemm_splitk
         p.sk_ws, p.sk_ws_floats = self._sk_ws.data_ptr(), self._sk_ws.numel()
         p.sk_cnt, p.sk_cnt_n = self._sk_cnt.data_ptr(), self._sk_cnt.numel()
+        if defer is not None:
+            defer.append((p, self.cdt if dtype is None else dtype))
+            return
         plan.append((LIB.mmt_gemm, (ctypes_byref(p), self.cdt if dtype is None else dtype), name, p))
+
+    def _gemm_multi(self, plan, name, items):
+        """One mmt_gemm_multi launch of independent problems collected by _gemm(..., defer=items)."""
+        dts = {dt for _, dt in items}
+        if len(dts) != 1:
+            raise ValueError("%s: one dtype per multi-GEMM launch" % name)
+        arr = (GemmParams * len(items))(*[q for q, _ in items])
+        plan.append((LIB.mmt_gemm_multi, (arr, len(items), dts.pop()), name, arr))
 
     def _build_plan(self, ws, score):
         plan = []
@@ -564,12 +576,15 @@ class MixFormerRGBTRuntime:
                                          P(W["adj_i.gn"][0]), P(W["adj_i.gn"][1]), 2 * B, B, ns, dm, 32, 1e-5, cdt),
                      "fusion_gn", None))
         for e in W["enc"]:
+            # value and the offsets / logits of the query src + pos (src . W^T + the folded per-cell pos
+            # term) both read SRCT only: one launch
+            vo = []
             self._gemm(plan, "enc_value", a=[P(SRCT)], w=[P(e["value.w"])], c=[P(VAL)], M=2 * Mf, N=dm, K=dm, lda=dm,
-                       ldc=dm, bias=[P(e["value.b"])])
-            # offsets / logits of the query src + pos: src . W^T + the folded per-cell pos term
+                       ldc=dm, bias=[P(e["value.b"])], defer=vo)
             self._gemm(plan, "enc_offw", a=[P(SRCT)], a1=[P(SRCT, Mf * dm)], k_split=dm, w=[P(e["offw.w"])],
                        c=[P(ws["OFFW"])], M=Mf, N=192, K=2 * dm, lda=dm, ldc=192, r=[P(e["offw.pos"])], ldr=192,
-                       r_mode=1, r_p0=ns, c_f32=1)
+                       r_mode=1, r_p0=ns, c_f32=1, defer=vo)
+            self._gemm_multi(plan, "enc_value_offw", vo)
             plan.append((LIB.mmt_msda_bimodal, (P(ws["OFFW"]), P(VAL), P(ws["MS"]), B, d.gs, cdt), "msda_bimodal", None))
             self._gemm(plan, "enc_outproj", a=[P(ws["MS"])], w=[P(e["out.w"])], c=[P(ws["SRC2"])], M=Mf, N=dm, K=dm,
                        lda=dm, ldc=dm, bias=[P(e["out.b"])], c_f32=1)
@@ -612,28 +627,33 @@ class MixFormerRGBTRuntime:
                    c=[P(X2, g * B * ns * h2) for g in range(2)], c2=[P(S1, g * B * ns * h2) for g in range(2)],
                    r=[P(H0, 2 * hc + g * h2) for g in range(2)], ldr=n0, r_t=1, M=B * ns, N=h2, K=9 * hc, lda=n0,
                    ldc=h2, bias=[P(W["conv2_%s.b" % b]) for b in br], act=2, conv=(gs, 1, hc, 1))
+        # the two pyramid branches are independent of the conv chain past their inputs
+        # (head.py:159-197): conv3 beside adjust3[0], conv4 beside adjust4[0] and adjust3[1]
+        l3, l4 = [], []
         hg(plan, "head_conv3", a=[P(S1, g * B * ns * h2) for g in range(2)], w=[P(W["conv3_%s.w" % b]) for b in br],
                    c=[P(X3, g * B * 4 * ns * h4) for g in range(2)], c2=[P(S2, g * B * 4 * ns * h4) for g in range(2)],
                    r=[P(H0, 2 * hc + hc + g * h4) for g in range(2)], ldr=n0, r_t=1, r_mode=2, r_p0=2 * gs, r_p1=2,
                    M=B * 4 * ns, N=h4, K=9 * h2, lda=h2, ldc=h4, bias=[P(W["conv3_%s.b" % b]) for b in br], act=2,
-                   conv=(2 * gs, 2, h2, 1))
-        hg(plan, "head_conv4", a=[P(S2, g * B * 4 * ns * h4) for g in range(2)], w=[P(W["conv4_%s.w" % b]) for b in br],
-                   c=[P(X4, g * B * 16 * ns * h8) for g in range(2)], M=B * 16 * ns, N=h8, K=9 * h4, lda=h4, ldc=h8,
-                   bias=[P(W["conv4_%s.b" % b]) for b in br], act=2, conv=(4 * gs, 2, h4, 1))
+                   conv=(2 * gs, 2, h2, 1), defer=l3)
         hg(plan, "head_adjust3_0", a=[P(X2, g * B * ns * h2) for g in range(2)],
                    w=[P(W["adjust3.0_%s.w" % b]) for b in br], c=[P(ws["A3a"], g * B * ns * h4) for g in range(2)],
                    M=B * ns, N=h4, K=9 * h2, lda=h2, ldc=h4, bias=[P(W["adjust3.0_%s.b" % b]) for b in br], act=2,
-                   conv=(gs, 1, h2, 1))
-        hg(plan, "head_adjust3_1", a=[P(ws["A3a"], g * B * ns * h4) for g in range(2)],
-                   w=[P(W["adjust3.1_%s.w" % b]) for b in br], c=[P(ws["A3b"], g * B * ns * h8) for g in range(2)],
-                   M=B * ns, N=h8, K=9 * h4, lda=h4, ldc=h8, bias=[P(W["adjust3.1_%s.b" % b]) for b in br], act=2,
-                   conv=(gs, 1, h4, 1))
-        plan.append((LIB.mmt_conv3x3_c1, (P(ws["A3b"]), P(W["a3c1.w"]), P(W["a3c1.b"]), P(ws["A3"]), 2, B, gs, h8, h8,
-                                          cdt), "head_adjust3_2", None))
+                   conv=(gs, 1, h2, 1), defer=l3)
+        self._gemm_multi(plan, "head_conv3_adjust3_0", l3)
+        hg(plan, "head_conv4", a=[P(S2, g * B * 4 * ns * h4) for g in range(2)], w=[P(W["conv4_%s.w" % b]) for b in br],
+                   c=[P(X4, g * B * 16 * ns * h8) for g in range(2)], M=B * 16 * ns, N=h8, K=9 * h4, lda=h4, ldc=h8,
+                   bias=[P(W["conv4_%s.b" % b]) for b in br], act=2, conv=(4 * gs, 2, h4, 1), defer=l4)
         hg(plan, "head_adjust4_0", a=[P(X3, g * B * 4 * ns * h4) for g in range(2)],
                    w=[P(W["adjust4.0_%s.w" % b]) for b in br], c=[P(ws["A4a"], g * B * 4 * ns * h8) for g in range(2)],
                    M=B * 4 * ns, N=h8, K=9 * h4, lda=h4, ldc=h8, bias=[P(W["adjust4.0_%s.b" % b]) for b in br], act=2,
-                   conv=(2 * gs, 1, h4, 1))
+                   conv=(2 * gs, 1, h4, 1), defer=l4)
+        hg(plan, "head_adjust3_1", a=[P(ws["A3a"], g * B * ns * h4) for g in range(2)],
+                   w=[P(W["adjust3.1_%s.w" % b]) for b in br], c=[P(ws["A3b"], g * B * ns * h8) for g in range(2)],
+                   M=B * ns, N=h8, K=9 * h4, lda=h4, ldc=h8, bias=[P(W["adjust3.1_%s.b" % b]) for b in br], act=2,
+                   conv=(gs, 1, h4, 1), defer=l4)
+        self._gemm_multi(plan, "head_conv4_adjust4_0_adjust3_1", l4)
+        plan.append((LIB.mmt_conv3x3_c1, (P(ws["A3b"]), P(W["a3c1.w"]), P(W["a3c1.b"]), P(ws["A3"]), 2, B, gs, h8, h8,
+                                          cdt), "head_adjust3_2", None))
         plan.append((LIB.mmt_conv3x3_c1, (P(ws["A4a"]), P(W["a4c1.w"]), P(W["a4c1.b"]), P(ws["A4"]), 2, B, 2 * gs, h8,
                                           h8, cdt), "head_adjust4_1", None))
         plan.append((LIB.mmt_corner_softargmax, (P(X4), P(W["c5.w"]), P(W["c5.b"]), P(ws["A3"]), P(ws["A4"]),

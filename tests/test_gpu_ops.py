@@ -29,6 +29,13 @@ def _lib():
 
 def _gemm(a, w, c, M, N, K, lda, ldc, dtype, **kw):
     L = _lib()
+    p = _gemm_params(a, w, c, M, N, K, lda, ldc, **kw)
+    L.check(L.LIB.mmt_gemm(p, _code(dtype),
+                           torch.cuda.current_stream().cuda_stream), "mmt_gemm")
+
+
+def _gemm_params(a, w, c, M, N, K, lda, ldc, **kw):
+    L = _lib()
     p = L.GemmParams()
     G = len(a)
     for g in range(G):
@@ -54,8 +61,7 @@ def _gemm(a, w, c, M, N, K, lda, ldc, dtype, **kw):
     if kw.get("sk"):  # (splitk, slab workspace, tickets)
         n, ws, cnt = kw["sk"]
         p.splitk, p.sk_ws, p.sk_ws_floats, p.sk_cnt, p.sk_cnt_n = n, ws.data_ptr(), ws.numel(), cnt.data_ptr(), cnt.numel()
-    L.check(L.LIB.mmt_gemm(p, _code(dtype),
-                           torch.cuda.current_stream().cuda_stream), "mmt_gemm")
+    return p
 
 
 def _tol(dt):
@@ -354,6 +360,93 @@ def test_conv3x3_implicit_gemm(dname, impl, h, up, cin, cout):
     tol = _tol(dt) * ref2.abs().max().item() + 1e-5
     assert (o - ref).abs().max().item() <= tol
     assert (o2 - ref2).abs().max().item() <= tol
+
+
+def _multi_problems(dt, mode):
+    """Independent problems for mmt_gemm_multi: mode "conv" = the corner head's conv4 / adjust4[0] /
+    adjust3[1] shapes at batch 1 (2 groups each, upsampled input and residual on one), "gemm" = the
+    fusion encoder's value Linear (bf16 out, bias) beside its offset / logit Linear (K split over two
+    operands, fp32 out, row-mapped residual)."""
+    g = torch.Generator().manual_seed(11 if mode == "conv" else 12)
+    keep, probs = [], []
+
+    def T(*shape, scale=1.0, dtype=None):
+        t = (torch.randn(*shape, generator=g) * scale).to(dtype or dt).cuda()
+        keep.append(t)
+        return t
+    if mode == "conv":
+        for h, up, cin, cout, res in ((80, 2, 96, 48, False), (40, 1, 96, 48, True), (20, 1, 96, 48, False)):
+            hi = h // up
+            xs = [T(hi * hi, cin) for _ in range(2)]
+            ws = [T(cout, 9 * cin, scale=1 / math.sqrt(9 * cin)) for _ in range(2)]
+            bs = [T(cout, dtype=torch.float32) for _ in range(2)]
+            outs = [torch.zeros(h * h, cout, device="cuda", dtype=dt) for _ in range(2)]
+            keep += outs
+            kw = dict(bias=[b.data_ptr() for b in bs], act=2, conv=(h, up, cin, 1))
+            if res:
+                rs = [T(h * h, cout, dtype=torch.float32) for _ in range(2)]
+                o2 = [torch.zeros_like(outs[0]) for _ in range(2)]
+                keep += o2
+                kw.update(r=[r.data_ptr() for r in rs], c2=[o.data_ptr() for o in o2], ldr=cout)
+                outs += o2
+            probs.append(((h * h, cout, 9 * cin, cin, cout), [x.data_ptr() for x in xs], [w.data_ptr() for w in ws],
+                          [o.data_ptr() for o in outs[:2]], kw, outs))
+    else:
+        Mf, dm = 400, 512
+        src = T(2 * Mf, dm)
+        wv, bv = T(dm, dm, scale=dm ** -0.5), T(dm, dtype=torch.float32)
+        val = torch.zeros(2 * Mf, dm, device="cuda", dtype=dt)
+        wo, pos = T(192, 2 * dm, scale=(2 * dm) ** -0.5), T(400, 192, dtype=torch.float32)
+        offw = torch.zeros(Mf, 192, device="cuda")
+        keep += [val, offw]
+        probs.append(((2 * Mf, dm, dm, dm, dm), [src.data_ptr()], [wv.data_ptr()], [val.data_ptr()],
+                      dict(bias=[bv.data_ptr()]), [val]))
+        probs.append(((Mf, 192, 2 * dm, dm, 192), [src.data_ptr()], [wo.data_ptr()], [offw.data_ptr()],
+                      dict(a1=[src.data_ptr() + Mf * dm * src.element_size()], k_split=dm, r=[pos.data_ptr()], ldr=192,
+                           r_mode=1, r_p0=400, c_f32=1), [offw]))
+    return probs, keep
+
+
+@pytest.mark.parametrize("dname", ["bf16", "fp16", "f32"])
+@pytest.mark.parametrize("mode", ["conv", "gemm"])
+def test_gemm_multi_matches_single_launches(dname, mode):
+    """mmt_gemm_multi (several independent problems in one launch, the head's conv chains and the
+    encoder's value / offset Linears) writes exactly what one mmt_gemm per problem writes for the
+    same forced tile shape (impl 1-4; 16-bit: one multi-problem launch, fp32: the per-problem
+    fallback), and the auto choice agrees within the tile shapes' fp32 summation order."""
+    L = _lib()
+    dt = DT[dname]
+    probs, keep = _multi_problems(dt, mode)
+    st = torch.cuda.current_stream().cuda_stream
+
+    def run(impl, multi):
+        for *_, outs in probs:
+            for o in outs:
+                o.zero_()
+        ps = [_gemm_params(a, w, c, *shape, impl=impl, **kw) for shape, a, w, c, kw, _ in probs]
+        if multi:
+            arr = (L.GemmParams * len(ps))(*ps)
+            L.check(L.LIB.mmt_gemm_multi(arr, len(ps), _code(dt), st), "mmt_gemm_multi")
+        else:
+            for p in ps:
+                L.check(L.LIB.mmt_gemm(p, _code(dt), st), "mmt_gemm")
+        torch.cuda.synchronize()
+        return [o.float().cpu().clone() for *_, outs in probs for o in outs]
+    for impl in ((1, 2, 3, 4) if dt != torch.float32 else (0,)):
+        single, multi = run(impl, False), run(impl, True)
+        for a, b in zip(single, multi):
+            assert torch.equal(a, b), impl
+    ref, multi = run(0, False), run(0, True)
+    for a, b in zip(ref, multi):
+        assert (a - b).abs().max().item() <= _tol(dt) * max(1.0, a.abs().max().item())
+
+
+def test_gemm_multi_rejects_bad_counts():
+    L = _lib()
+    arr = (L.GemmParams * 5)()
+    st = torch.cuda.current_stream().cuda_stream
+    for n in (0, 5):
+        assert L.LIB.mmt_gemm_multi(arr, n, L.MMT_BF16, st) == -10000  # MMT_EBADARG
 
 
 def _attn_ref(qkv, S, Bm, ntok, n_t, C, H, asym):
