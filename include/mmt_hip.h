@@ -284,6 +284,11 @@ int mmt_msda_bimodal(const float* offw, const void* value, void* out, int B, int
  * in_stride) -> out fp32 [G][B][h*h]. */
 int mmt_conv3x3_c1(const void* in, const void* w, const float* bias, float* out, int G, int B, int h,
                    int cin, int64_t in_stride, int dtype, void* stream);
+/* mmt_conv3x3_c1 of two independent convolutions (same G, B, cin; own input, weights, size and
+ * pixel stride) in one launch: the corner head's adjust3[2] and adjust4[1] (head.py:115-120). */
+int mmt_conv3x3_c1_pair(const void* in0, const void* w0, const float* bias0, float* out0, int h0, int64_t in_stride0,
+                        const void* in1, const void* w1, const float* bias1, float* out1, int h1, int64_t in_stride1,
+                        int G, int B, int cin, int dtype, void* stream);
 
 /* score(p) = x4[g][b][p] . w5[g] + b5[g] + a3[g][b][up4(p)] + a4[g][b][up2(p)] on an fh x fh map
  * (g = 0 top-left, 1 bottom-right), softmax over the map, expectation of stride*col / stride*row,

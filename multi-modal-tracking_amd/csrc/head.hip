@@ -13,14 +13,14 @@
 namespace {
 
 // 8 lanes per output pixel, each summing a strided slice of the 9*cin/EPC 16-byte chunks.
+// (the body of one 32-pixel block bx; the pair kernel runs two convolutions' blocks in one grid)
 template <typename T>
-__global__ __launch_bounds__(256) void conv3x3_c1_kernel(const T* __restrict__ in, const T* __restrict__ w,
-                                                         const float* __restrict__ bias, float* __restrict__ out, int B,
-                                                         int h, int cin, int64_t in_stride) {
+MMT_DEV void conv3x3_c1_block(const T* __restrict__ in, const T* __restrict__ w, const float* __restrict__ bias,
+                              float* __restrict__ out, int B, int h, int cin, int64_t in_stride, int bx) {
     constexpr int EPC = 16 / (int)sizeof(T);
     const int g = blockIdx.y;
     const int64_t npx = (int64_t)B * h * h;
-    const int64_t idx = (int64_t)blockIdx.x * 32 + (threadIdx.x >> 3);
+    const int64_t idx = (int64_t)bx * 32 + (threadIdx.x >> 3);
     const int sl = threadIdx.x & 7;
     const int nch = cin / EPC;
     float acc = 0.f;
@@ -59,6 +59,26 @@ __global__ __launch_bounds__(256) void conv3x3_c1_kernel(const T* __restrict__ i
     acc += __shfl_xor(acc, 2, 64);
     acc += __shfl_xor(acc, 4, 64);
     if (idx < npx && sl == 0) out[(int64_t)g * npx + idx] = fmaxf(acc + bias[g], 0.f);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void conv3x3_c1_kernel(const T* __restrict__ in, const T* __restrict__ w,
+                                                         const float* __restrict__ bias, float* __restrict__ out, int B,
+                                                         int h, int cin, int64_t in_stride) {
+    conv3x3_c1_block<T>(in, w, bias, out, B, h, cin, in_stride, blockIdx.x);
+}
+
+// Two independent Cout=1 convolutions (adjust3[2] and adjust4[1], head.py:115-120) in one launch:
+// blocks [0, nb0) take the first, the rest the second.
+template <typename T>
+__global__ __launch_bounds__(256) void conv3x3_c1_pair_kernel(const T* __restrict__ in0, const T* __restrict__ w0,
+                                                              const float* __restrict__ b0, float* __restrict__ out0,
+                                                              int h0, int64_t st0, const T* __restrict__ in1,
+                                                              const T* __restrict__ w1, const float* __restrict__ b1,
+                                                              float* __restrict__ out1, int h1, int64_t st1, int B,
+                                                              int cin, int nb0) {
+    if ((int)blockIdx.x < nb0) conv3x3_c1_block<T>(in0, w0, b0, out0, B, h0, cin, st0, blockIdx.x);
+    else conv3x3_c1_block<T>(in1, w1, b1, out1, B, h1, cin, st1, blockIdx.x - nb0);
 }
 
 // score(p) for both corners: conv5 (1x1, c4 -> 1) + up4(adjust3) + up2(adjust4); one thread per pixel.
@@ -459,6 +479,28 @@ extern "C" int mmt_conv3x3_c1(const void* in, const void* w, const float* bias, 
         hipLaunchKernelGGL(conv3x3_c1_kernel<float>, grid, dim3(256), 0, st, (const float*)in, (const float*)w, bias,
                            out, B, h, cin, in_stride);
     else return MMT_EBADARG;
+    return launch_status();
+}
+
+extern "C" int mmt_conv3x3_c1_pair(const void* in0, const void* w0, const float* b0, float* out0, int h0,
+                                   int64_t in_stride0, const void* in1, const void* w1, const float* b1, float* out1,
+                                   int h1, int64_t in_stride1, int G, int B, int cin, int dtype, void* stream) {
+    const int epc = dtype == MMT_BF16 || dtype == MMT_F16 ? 8 : 4;
+    if (!in0 || !w0 || !b0 || !out0 || !in1 || !w1 || !b1 || !out1 || G <= 0 || B <= 0 || h0 <= 0 || h1 <= 0 ||
+        cin <= 0 || cin % epc || in_stride0 % epc || in_stride1 % epc)
+        return MMT_EBADARG;
+    const int64_t nb0 = ((int64_t)B * h0 * h0 + 31) / 32, nb1 = ((int64_t)B * h1 * h1 + 31) / 32;
+    if (nb0 + nb1 > INT32_MAX) return MMT_EBADARG;
+    const dim3 grid((unsigned)(nb0 + nb1), G);
+    hipStream_t st = (hipStream_t)stream;
+#define MMT_C1_PAIR(T)                                                                                          \
+    hipLaunchKernelGGL(conv3x3_c1_pair_kernel<T>, grid, dim3(256), 0, st, (const T*)in0, (const T*)w0, b0, out0, h0, \
+                       in_stride0, (const T*)in1, (const T*)w1, b1, out1, h1, in_stride1, B, cin, (int)nb0)
+    if (dtype == MMT_BF16) MMT_C1_PAIR(bf16_t);
+    else if (dtype == MMT_F16) MMT_C1_PAIR(f16_t);
+    else if (dtype == MMT_F32) MMT_C1_PAIR(float);
+    else return MMT_EBADARG;
+#undef MMT_C1_PAIR
     return launch_status();
 }
 

@@ -76,6 +76,7 @@ _PROTOS = {
     "mmt_ms_deform_attn_backward": [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp],
     "mmt_msda_bimodal": [vp, vp, vp, i32, i32, i32, vp],
     "mmt_conv3x3_c1": [vp, vp, vp, vp, i32, i32, i32, i32, i64, i32, vp],
+    "mmt_conv3x3_c1_pair": [vp, vp, vp, vp, i32, i64, vp, vp, vp, vp, i32, i64, i32, i32, i32, i32, vp],
     "mmt_corner_softargmax": [vp, vp, vp, vp, vp, vp, vp, vp, vp, f32, i32, i32, i32, i32, i32, vp],
     "mmt_prroi_pool_forward": [vp, vp, vp, i32, i32, i32, i32, i64, i64, i64, i64, i32, i32, f32, i64, i64, i64, vp],
     "mmt_prroi_pool_backward": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, f32, vp],

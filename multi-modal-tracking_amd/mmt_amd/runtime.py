@@ -652,10 +652,9 @@ class MixFormerRGBTRuntime:
                    M=B * ns, N=h8, K=9 * h4, lda=h4, ldc=h8, bias=[P(W["adjust3.1_%s.b" % b]) for b in br], act=2,
                    conv=(gs, 1, h4, 1), defer=l4)
         self._gemm_multi(plan, "head_conv4_adjust4_0_adjust3_1", l4)
-        plan.append((LIB.mmt_conv3x3_c1, (P(ws["A3b"]), P(W["a3c1.w"]), P(W["a3c1.b"]), P(ws["A3"]), 2, B, gs, h8, h8,
-                                          cdt), "head_adjust3_2", None))
-        plan.append((LIB.mmt_conv3x3_c1, (P(ws["A4a"]), P(W["a4c1.w"]), P(W["a4c1.b"]), P(ws["A4"]), 2, B, 2 * gs, h8,
-                                          h8, cdt), "head_adjust4_1", None))
+        plan.append((LIB.mmt_conv3x3_c1_pair, (P(ws["A3b"]), P(W["a3c1.w"]), P(W["a3c1.b"]), P(ws["A3"]), gs, h8,
+                                               P(ws["A4a"]), P(W["a4c1.w"]), P(W["a4c1.b"]), P(ws["A4"]), 2 * gs, h8,
+                                               2, B, h8, cdt), "head_adjust3_2_adjust4_1", None))
         plan.append((LIB.mmt_corner_softargmax, (P(X4), P(W["c5.w"]), P(W["c5.b"]), P(ws["A3"]), P(ws["A4"]),
                                                  P(ws["MAPS"]), P(ws["BOX"]), P(ws["XYXY"]), P(ws["ROIS"]) if score else None,
                                                  float(gs), B, d.fh, h8, 4, cdt), "corner_softargmax", None))

@@ -851,6 +851,32 @@ def test_spm_attention(B, Lk, H):
     assert err.max().item() <= 1e-5
 
 
+@pytest.mark.parametrize("dname", ["f32", "bf16", "fp16"])
+def test_conv3x3_c1_pair_matches_single(dname):
+    """mmt_conv3x3_c1_pair (adjust3[2] beside adjust4[1] in one launch) writes exactly what two
+    mmt_conv3x3_c1 launches write (20x20 and 40x40 maps, 48 channels, padded pixel stride)."""
+    L = _lib()
+    dt = DT[dname]
+    G, B, cin = 2, 2, 48
+    g = torch.Generator().manual_seed(3)
+    st = torch.cuda.current_stream().cuda_stream
+    ins, ws, bs, outs, refs = [], [], [], [], []
+    for h, pad in ((20, 0), (40, 8)):
+        ins.append(torch.randn(G, B, h, h, cin + pad, generator=g).to(dt).cuda())
+        ws.append((torch.randn(G, 9, cin, generator=g) / math.sqrt(9 * cin)).to(dt).cuda())
+        bs.append((torch.randn(G, generator=g) * 0.1).cuda())
+        outs.append(torch.full((G, B, h * h), float("nan"), device="cuda"))
+        refs.append(torch.full((G, B, h * h), float("nan"), device="cuda"))
+        L.check(L.LIB.mmt_conv3x3_c1(ins[-1].data_ptr(), ws[-1].data_ptr(), bs[-1].data_ptr(), refs[-1].data_ptr(), G, B,
+                                     h, cin, cin + pad, _code(dt), st), "conv3x3_c1")
+    L.check(L.LIB.mmt_conv3x3_c1_pair(ins[0].data_ptr(), ws[0].data_ptr(), bs[0].data_ptr(), outs[0].data_ptr(), 20, cin,
+                                      ins[1].data_ptr(), ws[1].data_ptr(), bs[1].data_ptr(), outs[1].data_ptr(), 40,
+                                      cin + 8, G, B, cin, _code(dt), st), "conv3x3_c1_pair")
+    torch.cuda.synchronize()
+    for o, r in zip(outs, refs):
+        assert torch.equal(o.cpu(), r.cpu())
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("dname", ["f32", "bf16", "fp16"])
 @pytest.mark.parametrize("h,cin,pad", [(20, 48, 0), (40, 48, 16), (10, 16, 0), (16, 96, 8)])
