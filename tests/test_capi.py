@@ -62,6 +62,19 @@ def test_bad_arguments_rejected_without_gpu_work():
     a = _lib.AttnParams()
     a.C, a.H = 100, 2
     assert _lib.LIB.mmt_mam_attention(ctypes.byref(a), _lib.MMT_BF16, None) == -10000
+    # multi-problem GEMM: problem count out of 1..4, or any problem failing mmt_gemm's checks
+    arr = (_lib.GemmParams * 5)()
+    for q in arr:
+        q.M, q.N, q.K, q.groups = 16, 16, 16, 1
+    assert _lib.LIB.mmt_gemm_multi(arr, 0, _lib.MMT_BF16, None) == -10000
+    assert _lib.LIB.mmt_gemm_multi(arr, 5, _lib.MMT_BF16, None) == -10000
+    assert _lib.LIB.mmt_gemm_multi(arr, 2, _lib.MMT_BF16, None) == -10000  # null operands
+    # paired Cout=1 conv: null operands / channel count not a multiple of the 16-B vector
+    fake = 1 << 20
+    assert _lib.LIB.mmt_conv3x3_c1_pair(None, fake, fake, fake, 20, 48, fake, fake, fake, fake, 40, 48, 2, 1, 48,
+                                        _lib.MMT_BF16, None) == -10000
+    assert _lib.LIB.mmt_conv3x3_c1_pair(fake, fake, fake, fake, 20, 44, fake, fake, fake, fake, 40, 44, 2, 1, 44,
+                                        _lib.MMT_BF16, None) == -10000
 
 
 def test_persistent_pair_attention_shape_gate():
