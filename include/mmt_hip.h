@@ -24,6 +24,8 @@
  *   mmt_gemm                    the eager nn.Linear / 1x1-conv / 3x3-conv (+BN+ReLU) / patch-embed
  *       calls of mixformer.py:26-76, :137-138, fusion_utils.py:252-278, deformable_encoder*.py,
  *       head.py:7-20,159-198, score_decoder.py (implicit GEMM, fused epilogues)
+ *   mmt_gemm_multi              several independent mmt_gemm problems in one launch (the head's
+ *       parallel conv chains head.py:159-197, the encoder's value / offset Linears)
  *   mmt_mam_attention           Attention.forward MAM softmax(QK^T)V, mixformer.py:52-78 /
  *       asymmetric_shared.py:55-104
  *   mmt_mam_attention_bwd       its autograd (training step, train_script_mixformer*.py)
@@ -34,7 +36,8 @@
  *       sampling locations, MSDA gather), ms_deform_attn_bimodal.py:97-128
  *   mmt_corner_softargmax       conv5 + pyramid adds + soft_argmax + box_xyxy_to_cxcywh,
  *       head.py:191-212, mixformer.py:419-432
- *   mmt_conv3x3_c1              the 1-channel conv-BN-ReLU of adjust3/adjust4, head.py:115-120
+ *   mmt_conv3x3_c1 / mmt_conv3x3_c1_pair  the 1-channel conv-BN-ReLU of adjust3/adjust4,
+ *       head.py:115-120 (the pair form runs adjust3[2] and adjust4[1] in one launch)
  *   mmt_spm_attention           ScoreDecoder single-query attention, score_decoder.py:55-61
  *   mmt_ce_t2s_attention / mmt_ce_select / mmt_ce_gather / mmt_ce_recover  candidate elimination
  *       of asymmetric_shared_ce.py:22-102, :198-202, :426-447 (attn_t2s mean, sorted top-k, recover)
