@@ -6,6 +6,7 @@ back-to-back launches of the entry in one hipGraph, timed with HIP events (as be
 usage: python tools/plan_entry_ab.py --names head_conv1_adj12,head_conv2 --cfgs 0:0,1:4,2:3,3:1
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -52,14 +53,18 @@ def main():
     torch.cuda.synchronize()
     for nm in args.names.split(","):
         e = next(e for e in plan if e[2] == nm)
-        fn, fargs, _, p = e
-        row = {"name": nm, "M": p.M, "N": p.N, "K": p.K, "groups": p.groups, "conv": int(p.conv_h > 0)}
-        impl0, sk0 = p.impl, p.splitk
+        fn, fargs, _, keep = e
+        ps = list(keep) if isinstance(keep, ctypes.Array) else [keep]  # mmt_gemm_multi: every problem
+        row = {"name": nm, "problems": [{"M": p.M, "N": p.N, "K": p.K, "groups": p.groups, "conv": int(p.conv_h > 0)}
+                                        for p in ps]}
+        saved = [(p.impl, p.splitk) for p in ps]
         for cfg in args.cfgs.split(","):
             impl, sk = (int(v) for v in cfg.split(":"))
-            p.impl, p.splitk = impl, sk
+            for p in ps:
+                p.impl, p.splitk = impl, sk
             row[cfg] = round(time_entry(fn, fargs), 2)
-        p.impl, p.splitk = impl0, sk0
+        for p, (i0, s0) in zip(ps, saved):
+            p.impl, p.splitk = i0, s0
         print(json.dumps(row), flush=True)
 
 
