@@ -1,5 +1,6 @@
 #!/bin/bash
-# MAM attention block-order A/B: parity of impls 23 / 24 (longest-first block order) and times vs impl 22
+# MAM attention block-order A/B (impls 23 / 24, longest-first orders; measured in profiles/r02_attn_order_ab.jsonl and
+# since removed from the library): parity of the given impls and their times vs impl 22
 set -u
 TAG=${1:-lpt}; IMPLS=${2:-22,23,24,0}; BATCHES=${3:-8,16,32}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=$ROOT/gpurun_out/$TAG; mkdir -p "$OUT"; cd "$ROOT"
