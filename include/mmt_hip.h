@@ -258,6 +258,10 @@ int mmt_ms_deform_attn_backward(const void* value, const int64_t* spatial_shapes
  *     column sums of the template->search
  *     softmax (qkv [S][tok_pitch][3C], q/k in place; scale in natural-log units, i.e. 1/log2(e)
  *     when q carries scale*log2(e) already);
+ *   mmt_ce_t2s_attention_masked: the same with ce_template_mask (candidate_elimination :81-89,
+ *     lib/utils/ce_utils.py:14-38 generate_mask_cond): template_mask[Bm][2*n_t] bytes in the query
+ *     order [q_mt_V ; q_mt_I] (nonzero = the query's softmax row enters the sums; NULL = all);
+ *     mean_scale of mmt_ce_select is then 1 / (H * masked queries per frame);
  *   mmt_ce_select: sums the partials (into each frame's first partial row, so `partial` is
  *     overwritten) and ranks each modality's n_s tokens by the sum (desc, ties by index)
  *     and keeps `keep`: order[S][ns_full] (slot -> current row - n_t), gidx_out = original search
@@ -269,6 +273,8 @@ int mmt_ms_deform_attn_backward(const void* value, const int64_t* spatial_shapes
  *     final gidx) at their original positions, zeros where pruned (dtype MMT_BF16 / MMT_F32). */
 int mmt_ce_t2s_attention(const void* qkv, float* partial, int Bm, int tok_pitch, int n_t, int n_s, int C, int H,
                          float scale, int dtype, void* stream);
+int mmt_ce_t2s_attention_masked(const void* qkv, float* partial, const unsigned char* template_mask, int Bm,
+                                int tok_pitch, int n_t, int n_s, int C, int H, float scale, int dtype, void* stream);
 int mmt_ce_select(float* partial, int nparts, int Bm, int n_s, int keep, int ns_full, const int* gidx_in,
                   int* gidx_out, int* order, float* attn_mean, float mean_scale, void* stream);
 int mmt_ce_gather(const float* x, float* xc, void* xn, const int* order, int S, int tok_pitch, int n_t, int keep,

@@ -2171,7 +2171,9 @@ template <typename T>
 int launch_attn(const mmt_attn_params& p, hipStream_t st) {
     if (p.impl != 0 && p.impl != 2 && p.impl != 4 && (p.impl < 8 || p.impl > 12) && (p.impl < 16 || p.impl > 22))
         return MMT_EBADARG;
-    if (p.lse && (sizeof(T) != 2 || p.impl == 9 || (p.impl > 9 && p.impl < 16))) return MMT_EBADARG;
+    // lse (training forward) is written by impls 0 / 4 / 8 / 16-19 / 21 only: impl 22 never writes it
+    if (p.lse && (sizeof(T) != 2 || p.impl == 9 || (p.impl > 9 && p.impl < 16) || p.impl == 20 || p.impl == 22))
+        return MMT_EBADARG;
     // fp16: the kernels with a running maximum (latency kernel, throughput kernel); the range-checked
     // exponent and 32x32 variants are bf16 A/B kernels, and the training forward (lse) is bf16
     if (__is_same(T, f16_t) && (p.lse || p.impl >= 10)) return MMT_EBADARG;

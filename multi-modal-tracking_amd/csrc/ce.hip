@@ -3,8 +3,10 @@
 // Reference: lib/models/mixformer_vit_rgbt/asymmetric_shared_ce.py
 //   Asym_Attention.forward(return_attention=True) :198-202  attn_t2s = softmax over the 2k search keys
 //       [k_s_V | k_s_I] of the 2 n_t template queries [q_mt_V ; q_mt_I] (per head)
-//   candidate_elimination :52-102 (ce_template_mask None, as the tracker calls it): mean over the
-//       template queries and heads, split into the RGB / TIR halves, and per modality
+//   candidate_elimination :52-102: mean over the template queries (all of them when ce_template_mask is
+//       None, as the tracker calls it; else the masked ones, :81-89, e.g. generate_mask_cond's CTR_POINT
+//       mask, lib/utils/ce_utils.py:14-38, which the training actor passes) and heads, split into the
+//       RGB / TIR halves, and per modality
 //   get_token_from_attn :22-46: sort descending, keep the first ceil(keep_ratio * k) search tokens in
 //       that order after the template tokens, global_index gathered alongside
 //   VisionTransformer._recover_search :426-447: after the last block, the surviving tokens go back to
@@ -17,7 +19,9 @@
 //   mmt_ce_t2s_attention  partial column sums of attn_t2s: one workgroup per (16 template queries
 //                         (bf16, MFMA scores) or 8 (fp32, VALU), head, frame), scores from the qkv rows
 //                         in place, softmax per query row in LDS, the rows summed per key ->
-//                         partial[b][h][qblock][2k]
+//                         partial[b][h][qblock][2k]; with a template mask ([b][2 n_t] bytes, query
+//                         order [q_mt_V ; q_mt_I]) a row enters the sum times its 0 / 1 mask value, and
+//                         a workgroup whose queries are all masked out writes zeros without scoring
 //   mmt_ce_select         the partial sums added in a fixed order (deterministic) into each
 //                         frame's first partial row, then one workgroup per (modality, frame): the
 //                         rank of every token by (attention desc, index asc) -> the kept tokens in
@@ -64,8 +68,9 @@ template <> struct CeRow<float> {
 // against the queries read as 16-B LDS broadcasts; each wave then normalises 2 query rows with
 // 16-B LDS accesses, and the column sums over the 8 rows are written as this block's partial row.
 template <typename T>
-__global__ __launch_bounds__(256) void ce_t2s_kernel(const T* __restrict__ qkv, float* __restrict__ part, int Bm,
-                                                     int pitch, int n_t, int k, int C, float scale) {
+__global__ __launch_bounds__(256) void ce_t2s_kernel(const T* __restrict__ qkv, float* __restrict__ part,
+                                                     const unsigned char* __restrict__ tmask, int Bm, int pitch,
+                                                     int n_t, int k, int C, float scale) {
     extern __shared__ __attribute__((aligned(16))) float sm[];  // q [CE_QB][64] then scores [CE_QB][nkp]
     float* qs = sm;
     float* sc = sm + CE_QB * 64;
@@ -73,6 +78,18 @@ __global__ __launch_bounds__(256) void ce_t2s_kernel(const T* __restrict__ qkv, 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int nk = 2 * k, nkp = (nk + 3) & ~3;
     const int64_t rs = 3 * (int64_t)C;
+    float* dst = part + (((int64_t)b * H + h) * nqb + qb) * nk;
+    float mq[CE_QB];  // template-mask weight of each query row (1 without a mask)
+    bool any = false;
+#pragma unroll
+    for (int qi = 0; qi < CE_QB; ++qi) {
+        mq[qi] = tmask ? (tmask[(int64_t)b * 2 * n_t + qb * CE_QB + qi] ? 1.f : 0.f) : 1.f;
+        any |= mq[qi] != 0.f;
+    }
+    if (!any) {  // block-uniform: no query of this block counts
+        for (int key = tid; key < nk; key += 256) dst[key] = 0.f;
+        return;
+    }
     for (int e = tid; e < CE_QB * 64; e += 256) {  // [q_mt_V ; q_mt_I]: query gq < n_t from frame b's RGB rows
         const int gq = qb * CE_QB + (e >> 6);
         const int seq = gq < n_t ? b : b + Bm, row = gq < n_t ? gq : gq - n_t;
@@ -130,11 +147,10 @@ __global__ __launch_bounds__(256) void ce_t2s_kernel(const T* __restrict__ qkv, 
         }
     }
     __syncthreads();
-    float* dst = part + (((int64_t)b * H + h) * nqb + qb) * nk;
     for (int key = tid; key < nk; key += 256) {
         float s2 = 0.f;
 #pragma unroll
-        for (int qi = 0; qi < CE_QB; ++qi) s2 += sc[qi * nkp + key];
+        for (int qi = 0; qi < CE_QB; ++qi) s2 += sc[qi * nkp + key] * mq[qi];
         dst[key] = s2;
     }
 }
@@ -156,13 +172,22 @@ MMT_DEV float ce_row16_sum(float v) {
 }
 constexpr int CE_QBM = 16, CE_MAXI = 18;  // key blocks per wave: 2k <= 4 * 18 * 16 = 1152 (ViT-L 384 px)
 __global__ __launch_bounds__(256) void ce_t2s_mfma_kernel(const bf16_t* __restrict__ qkv, float* __restrict__ part,
-                                                          int Bm, int pitch, int n_t, int k, int C, float scale) {
+                                                          const unsigned char* __restrict__ tmask, int Bm, int pitch,
+                                                          int n_t, int k, int C, float scale) {
     __shared__ float red[2][4][16];
     const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z, nqb = gridDim.x, H = gridDim.y;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l16 = lane & 15, lg = lane >> 4;
     const int nk = 2 * k, nkb = (nk + 15) / 16;
     const int64_t rs = 3 * (int64_t)C;
     const int gq = qb * CE_QBM + l16;  // query of [q_mt_V ; q_mt_I]
+    float* dst = part + (((int64_t)b * H + h) * nqb + qb) * nk;
+    // template-mask weight of this lane's query (1 without a mask); every wave holds the same 16
+    // queries, so a block with none of them counted is skipped by all four waves alike
+    const float mq = tmask ? (tmask[(int64_t)b * 2 * n_t + gq] ? 1.f : 0.f) : 1.f;
+    if (__all(mq == 0.f)) {
+        for (int key = tid; key < nk; key += 256) dst[key] = 0.f;
+        return;
+    }
     const int qseq = gq < n_t ? b : b + Bm, qrow = gq < n_t ? gq : gq - n_t;
     const bf16_t* qp = qkv + ((int64_t)qseq * pitch + qrow) * rs + h * 64 + 8 * lg;
     const u32x4 q0 = *(const u32x4*)qp, q1 = *(const u32x4*)(qp + 32);
@@ -216,14 +241,13 @@ __global__ __launch_bounds__(256) void ce_t2s_mfma_kernel(const bf16_t* __restri
     if (lg == 0) red[1][w][l16] = se;
     __syncthreads();
     const float inv = 1.f / ((red[1][0][l16] + red[1][1][l16]) + (red[1][2][l16] + red[1][3][l16]));
-    float* dst = part + (((int64_t)b * H + h) * nqb + qb) * nk;
 #pragma unroll
     for (int i = 0; i < CE_MAXI; ++i) {
         const int kb = w + 4 * i;
         if (kb < nkb) {
             float v[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = ce_row16_sum(sc[i][r] * inv);  // sum over the 16 queries
+            for (int r = 0; r < 4; ++r) v[r] = ce_row16_sum(sc[i][r] * inv * mq);  // sum over the 16 queries
             if (l16 == 15) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
@@ -343,8 +367,9 @@ __global__ __launch_bounds__(256) void ce_recover_kernel(const float* __restrict
 
 }  // namespace
 
-extern "C" int mmt_ce_t2s_attention(const void* qkv, float* partial, int Bm, int tok_pitch, int n_t, int n_s, int C,
-                                    int H, float scale, int dtype, void* stream) {
+extern "C" int mmt_ce_t2s_attention_masked(const void* qkv, float* partial, const unsigned char* template_mask, int Bm,
+                                           int tok_pitch, int n_t, int n_s, int C, int H, float scale, int dtype,
+                                           void* stream) {
     if (!qkv || !partial || Bm <= 0 || n_t <= 0 || n_s <= 0 || C != 64 * H || H <= 0 || (2 * n_t) % CE_QBM ||
         tok_pitch < n_t + n_s || n_s > CE_MAXK)
         return MMT_EBADARG;
@@ -352,14 +377,19 @@ extern "C" int mmt_ce_t2s_attention(const void* qkv, float* partial, int Bm, int
     if (dtype == MMT_BF16) {
         if (2 * n_s > 4 * CE_MAXI * 16) return MMT_EBADARG;
         hipLaunchKernelGGL(ce_t2s_mfma_kernel, dim3((unsigned)(2 * n_t / CE_QBM), (unsigned)H, (unsigned)Bm), dim3(256),
-                           0, st, (const bf16_t*)qkv, partial, Bm, tok_pitch, n_t,
-                           n_s, C, scale);
+                           0, st, (const bf16_t*)qkv, partial, template_mask, Bm, tok_pitch, n_t, n_s, C, scale);
     } else if (dtype == MMT_F32) {
         const size_t shm = sizeof(float) * (CE_QB * 64 + CE_QB * (size_t)((2 * n_s + 3) & ~3));
         hipLaunchKernelGGL(ce_t2s_kernel<float>, dim3((unsigned)(2 * n_t / CE_QB), (unsigned)H, (unsigned)Bm),
-                           dim3(256), shm, st, (const float*)qkv, partial, Bm, tok_pitch, n_t, n_s, C, scale);
+                           dim3(256), shm, st, (const float*)qkv, partial, template_mask, Bm, tok_pitch, n_t, n_s, C,
+                           scale);
     } else return MMT_EBADARG;
     return launch_status();
+}
+
+extern "C" int mmt_ce_t2s_attention(const void* qkv, float* partial, int Bm, int tok_pitch, int n_t, int n_s, int C,
+                                    int H, float scale, int dtype, void* stream) {
+    return mmt_ce_t2s_attention_masked(qkv, partial, nullptr, Bm, tok_pitch, n_t, n_s, C, H, scale, dtype, stream);
 }
 
 extern "C" int mmt_ce_select(float* partial, int nparts, int Bm, int n_s, int keep, int ns_full, const int* gidx_in,

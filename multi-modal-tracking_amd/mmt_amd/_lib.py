@@ -83,6 +83,7 @@ _PROTOS = {
     "mmt_prroi_pool_coor_backward": [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, f32, vp],
     "mmt_spm_attention": [vp, i64, vp, vp, i32, i32, i32, i32, f32, vp],
     "mmt_ce_t2s_attention": [vp, vp, i32, i32, i32, i32, i32, i32, f32, i32, vp],
+    "mmt_ce_t2s_attention_masked": [vp, vp, vp, i32, i32, i32, i32, i32, i32, f32, i32, vp],
     "mmt_ce_select": [vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, f32, vp],
     "mmt_ce_gather": [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp],
     "mmt_ce_recover": [vp, vp, i32, vp, i32, i32, i32, i32, i32, i32, vp],

@@ -265,14 +265,14 @@ class _HipTracker(nn.Module):
         if dev.type != "cuda":
             raise RuntimeError("the MI355X forward needs the inputs on the HIP device (got %s); there is no CPU path" % dev)
         rt = self._runtime(dev)
+        # gt_bboxes is accepted and ignored, as in the reference: asymmetric_shared_online.py:374 calls
+        # forward_head(search, template, run_score_head) without it, so the score head always pools the
+        # predicted box (pooling given boxes is the runtime's separate score_on_boxes API)
         score = bool(run_score_head) and self.variant == "asym_online"
-        on_gt = score and gt_bboxes is not None
         with torch.cuda.device(dev):
-            box, sc = rt.forward(template, online_template, search, run_score_head=score and not on_gt,
-                                 use_graph=self.use_hip_graph)
+            box, sc = rt.forward(template, online_template, search, run_score_head=score,
+                                 use_graph=self.use_hip_graph, ce_template_mask=getattr(self, "_mask", None))
             B = box.shape[0]
-            if on_gt:  # the ROI is the given box, not the prediction (asymmetric_shared_online.py:405-410)
-                sc = rt.score_on_boxes(B, gt_bboxes.to(device=dev, dtype=torch.float32))
             coord = box.clone().view(B, 1, 4)
             out = {"pred_boxes": coord}
             if score:
@@ -373,30 +373,51 @@ class MixFormer_RGBT_CE(MixFormer_RGBT_Shared):
             keep = self.ce_keep_ratio if self._keep_override is None else (self._keep_override,) * len(self.ce_loc)
             with torch.cuda.device(device):
                 self._rt = MixFormerRGBTRuntime(self.state_dict(), self.variant, dtype=self.compute_dtype,
-                                                device=device, ce=(self.ce_loc, keep))
+                                                device=device, ce=(self.ce_loc, keep), ce_mask_count=self._mask_count)
         return self._rt
 
     _keep_override = None
+    _mask_count = None  # template queries per frame the CE mean averages (None: all of them)
+    _mask = None
 
     def forward(self, template, online_template, search, run_score_head=False, gt_bboxes=None, ce_template_mask=None,
                 ce_keep_rate=None, return_features=False):
         """asymmetric_shared_ce.py:557-587 signature.  ce_keep_rate (the actor's keep-rate schedule,
         actors/mixformer_rgbt.py:70-89) replaces every CE layer's keep ratio; >= 1 disables the
-        elimination (asymmetric_shared_ce.py:249-252).  ce_template_mask (generate_mask_cond) must be
-        None or select every template token: the CE kernels average the attention of all template
-        queries."""
-        if ce_template_mask is not None and not bool(torch.as_tensor(ce_template_mask).all()):
-            raise NotImplementedError("ce_template_mask restricted to part of the template (CE_TEMPLATE_RANGE other "
-                                      "than ALL) is not supported by the candidate-elimination kernels")
+        elimination (asymmetric_shared_ce.py:249-252).  ce_template_mask: None (the tracker) or the
+        (B, 2 n_t) bool mask of generate_mask_cond (lib/utils/ce_utils.py:14-38; CTR_POINT selects
+        the centre token of each of the four 8x8 templates) that the training actor passes
+        (actors/mixformer_rgbt.py:67-90): the elimination then averages the template->search attention
+        over the masked template queries only (candidate_elimination :81-89).  As in the reference
+        (attn[mask].view(bs, hn, -1, ...)) every frame must select the same number of queries."""
         if self.training and torch.is_grad_enabled():
             raise NotImplementedError("training forward of asymmetric_shared_ce (candidate elimination with autograd) "
                                       "is not built; its inference forward runs under eval() / no_grad()")
+        count = None
+        if ce_template_mask is not None:
+            m = torch.as_tensor(ce_template_mask).to(torch.bool)
+            B, n_q = search[0].shape[0], 2 * self.backbone.pos_embed_t.shape[1] * 2
+            if tuple(m.shape) != (B, n_q):
+                raise ValueError("ce_template_mask shape %s, expected (%d, %d) (template queries [q_mt_V ; q_mt_I])"
+                                 % (tuple(m.shape), B, n_q))
+            counts = m.sum(1).cpu()
+            if not bool((counts == counts[0]).all()) or int(counts[0]) == 0:
+                raise ValueError("ce_template_mask must select the same nonzero number of template queries in every "
+                                 "frame (the reference views attn[mask] as (bs, heads, -1, L))")
+            count = None if int(counts[0]) == n_q else int(counts[0])  # all selected == no mask
+            if count is not None:
+                ce_template_mask = m
         rate = None if ce_keep_rate is None else float(ce_keep_rate)
-        if rate != self._keep_override:
+        if rate != self._keep_override or count != self._mask_count:
             self._keep_override = rate
+            self._mask_count = count
             self.refresh_kernels()
-        return super().forward(template, online_template, search, run_score_head=run_score_head, gt_bboxes=gt_bboxes,
-                               return_features=return_features)
+        self._mask = ce_template_mask if count is not None else None
+        try:
+            return super().forward(template, online_template, search, run_score_head=run_score_head,
+                                   gt_bboxes=gt_bboxes, return_features=return_features)
+        finally:
+            self._mask = None
 
     def set_online(self, template, online_template):
         raise NotImplementedError("the template K/V cache is not defined for candidate elimination")

@@ -75,7 +75,8 @@ class MixFormerRGBTRuntime:
     SPLITK_FLOATS = 8 << 20  # fp32 split-K partial-tile workspace (32 MiB), shared by every plan GEMM
     SPLITK_TICKETS = 1 << 16
 
-    def __init__(self, state_dict, variant, dtype=torch.bfloat16, device="cuda", fold_ln=None, ce=None, head_dtype=None):
+    def __init__(self, state_dict, variant, dtype=torch.bfloat16, device="cuda", fold_ln=None, ce=None, head_dtype=None,
+                 ce_mask_count=None):
         """fold_ln (default: on for bf16): the ViT's LayerNorms are folded into the qkv / fc1 GEMMs
         (mmt_gemm_params.ln_fold) and the residual-producing GEMMs also write the bf16 copy of the
         residual stream those GEMMs read, so no LayerNorm launch or normalised tensor remains.
@@ -90,6 +91,10 @@ class MixFormerRGBTRuntime:
         # candidate elimination (asym_ce): {block: keep ratio}, lib/config/asymmetric_shared_ce/config.py:23-24
         ce = ce if ce is not None else ((3, 6, 9), (0.7, 0.7, 0.7))
         self.ce = dict(zip(ce[0], ce[1])) if variant == "asym_ce" else {}
+        # ce_template_mask (candidate_elimination :81-89): None = every template query counts (the
+        # tracker); else the number of masked template queries per frame, and forward() takes the
+        # [B][2 n_t] mask itself (ce_template_mask), copied into the workspace before the plan runs
+        self.ce_mask_count = None if not self.ce or ce_mask_count is None else int(ce_mask_count)
         self.dtype = dtype
         self.cdt = {torch.bfloat16: MMT_BF16, torch.float16: MMT_F16}.get(dtype, MMT_F32)
         # storage type of the corner head's activations and weights (head_dtype; default = dtype)
@@ -318,7 +323,8 @@ class MixFormerRGBTRuntime:
             nparts = d.H * (2 * d.n_t // 8)  # (bf16 uses 16-query blocks: half of it)
             ws.update({"XC": e(R, C, t=f32), "CEP": e(B * nparts * 2 * ns, t=f32),
                        "CEG": [e(S, ns, t=torch.int32) for _ in self.ce], "CEO": e(S, ns, t=torch.int32),
-                       "CEM": [e(B, 2 * ns, t=f32) for _ in self.ce]})
+                       "CEM": [e(B, 2 * ns, t=f32) for _ in self.ce],
+                       "CEMASK": torch.ones(B, 2 * d.n_t, device=dev, dtype=torch.uint8)})
         ws["plan"] = self._build_plan(ws, False)
         if self.variant == "asym_online":
             ws["plan_score"] = self._build_plan(ws, True)
@@ -421,8 +427,9 @@ class MixFormerRGBTRuntime:
         # the producers of XN (patch embed, proj, fc2) also write its per-64-column row statistics
         # (LNST), which the LayerNorm-folded consumers (qkv, fc1) read instead of summing them in
         # their K loops; not for the template-cache passes (segment-mapped rows) or with candidate
-        # elimination (the gather moves rows)
-        hand = fold and part is None and not self.ce
+        # elimination (the gather moves rows).  The LDS-DMA GEMM takes the hand-off for K = C <= 1024 and
+        # producer widths N = C % 64 == 0 only (gemm_glds.hip glds_takes); wider models keep ln_fold 1
+        hand = fold and part is None and not self.ce and C % 64 == 0 and C <= 1024
         nst = 2 * (C // 64)
         LNST = ws["LNST"]
         plan.append((LIB.mmt_patch_im2col, self._image_args(ws["in_t"], ws["in_o"], ws["in_s"])
@@ -498,12 +505,15 @@ class MixFormerRGBTRuntime:
                 keep = math.ceil(self.ce[i] * k)
                 if keep < k:
                     nparts = d.H * (2 * d.n_t // (16 if cdt == MMT_BF16 else 8))  # mmt_ce_t2s_attention blocks
-                    plan.append((LIB.mmt_ce_t2s_attention, (P(QKV), P(ws["CEP"]), B, ntok, d.n_t, k, C, d.H, ap.scale,
-                                                            cdt), "ce_t2s", None))
+                    masked = self.ce_mask_count is not None
+                    plan.append((LIB.mmt_ce_t2s_attention_masked,
+                                 (P(QKV), P(ws["CEP"]), P(ws["CEMASK"]) if masked else None, B, ntok, d.n_t, k, C, d.H,
+                                  ap.scale, cdt), "ce_t2s", None))
+                    nq = self.ce_mask_count if masked else 2 * d.n_t  # template queries averaged
                     plan.append((LIB.mmt_ce_select, (P(ws["CEP"]), nparts, B, k, keep, d.ns,
                                                      P(ws["CEG"][stage - 1]) if stage else None, P(ws["CEG"][stage]),
                                                      P(ws["CEO"]), P(ws["CEM"][stage]),
-                                                     1.0 / (d.H * 2 * d.n_t)), "ce_select", None))
+                                                     1.0 / (d.H * nq)), "ce_select", None))
                     Xn = ws["XC"] if X is ws["X"] else ws["X"]
                     plan.append((LIB.mmt_ce_gather, (P(X), P(Xn), P(XN) if fold else None, P(ws["CEO"]), S, ntok,
                                                      d.n_t, keep, d.ns, C, cdt), "ce_gather", None))
@@ -724,13 +734,22 @@ class MixFormerRGBTRuntime:
                 raise ValueError("input shape %s, expected %s" % (tuple(src.shape), tuple(dst.shape)))
             dst.copy_(src, non_blocking=True)
 
-    def forward(self, template, online_template, search, run_score_head=False, use_graph=False):
+    def forward(self, template, online_template, search, run_score_head=False, use_graph=False, ce_template_mask=None):
         """template / online_template / search: [rgb, tir] lists of (B,3,H,W) fp32 device tensors.
+        ce_template_mask: (B, 2 n_t) bool template-query mask of the candidate elimination (a runtime
+        built with ce_mask_count; each row must select that many queries).
         Returns (boxes_cxcywh (B,4) fp32, scores (B,) fp32 or None) — views of the workspace."""
         B = template[0].shape[0]
         ws = self.workspace(B)
         score = bool(run_score_head) and self.variant == "asym_online"
         self.load_inputs(ws, template, online_template, search)
+        if (ce_template_mask is None) != (self.ce_mask_count is None):
+            raise ValueError("ce_template_mask must be given exactly when the runtime was built with ce_mask_count")
+        if ce_template_mask is not None:
+            m = ws["CEMASK"]
+            if tuple(ce_template_mask.shape) != tuple(m.shape):
+                raise ValueError("ce_template_mask shape %s, expected %s" % (tuple(ce_template_mask.shape), tuple(m.shape)))
+            m.copy_(ce_template_mask.to(device=m.device, dtype=torch.uint8), non_blocking=True)
         if use_graph:
             g = self._graphs.get((B, score))
             if g is None:
@@ -741,9 +760,10 @@ class MixFormerRGBTRuntime:
         return ws["BOX"], (ws["SC"].view(-1) if score else None)
 
     def score_on_boxes(self, B, boxes_xyxy):
-        """The score head on given boxes (asymmetric_shared_online.py:405-410: gt_bboxes, xyxy
-        normalised to the search crop, instead of the predicted box) after forward() of batch B:
-        ROIs = [b, box * feature size] into the workspace, then the ScoreDecoder plan."""
+        """The score decoder (score_decoder.py:32-66) on caller boxes (xyxy normalised to the search
+        crop) after forward() of batch B: ROIs = [b, box * feature size] into the workspace, then the
+        ScoreDecoder plan.  Not a reference entry point: the reference's forward drops gt_bboxes
+        (asymmetric_shared_online.py:374) and always scores the predicted box, as model.forward does."""
         ws = self.workspace(B)
         gs = float(self.d.gs)
         rois = ws["ROIS"]

@@ -335,7 +335,8 @@ def module_forward(net, template, online_template, search, ops, run_score_head=F
     MixFormerRGBTActor calls, actors/mixformer_rgbt.py:82-98, possibly wrapped in DDP + SyncBN,
     train_script_mixformer.py:105-110): MixFormer_RGBT.forward (mixformer.py:366-395),
     mixformer_shared.py:400-424, asymmetric_shared.py:349-368 and asymmetric_shared_online.py:351-413
-    (score head on gt_bboxes when given, else on the predicted boxes).  Returns
+    (score head on the predicted boxes: gt_bboxes is accepted and ignored, as the reference's forward
+    drops it at asymmetric_shared_online.py:374).  Returns
     ({"pred_boxes": (B,1,4)[, "pred_scores": (B,)]}, (B,1,4))."""
     variant = net.variant
     dpr = getattr(net, "drop_path_rate", DROP_PATH_RATE)
@@ -363,11 +364,10 @@ def module_forward(net, template, online_template, search, ops, run_score_head=F
         C = tok.shape[-1]
         t_v, t_i = tok[:B].transpose(1, 2).reshape(B, C, g, g), tok[B:].transpose(1, 2).reshape(B, C, g, g)
         templ = torch.cat([t_v, t_i], 2)
-        if gt_bboxes is None:  # box_cxcywh_to_xyxy(outputs_coord.clone())
-            xc, yc, w, h = coord.clone().view(-1, 4).unbind(-1)
-            gt_bboxes = torch.stack([xc - 0.5 * w, yc - 0.5 * h, xc + 0.5 * w, yc + 0.5 * h], -1)
-        out["pred_scores"] = score_decoder_forward(net.score_branch, fused.float(), templ.float(),
-                                                   gt_bboxes.view(-1, 4).float())
+        # box_cxcywh_to_xyxy(outputs_coord.clone()) (asymmetric_shared_online.py:408-409)
+        xc, yc, w, h = coord.clone().view(-1, 4).unbind(-1)
+        rois = torch.stack([xc - 0.5 * w, yc - 0.5 * h, xc + 0.5 * w, yc + 0.5 * h], -1)
+        out["pred_scores"] = score_decoder_forward(net.score_branch, fused.float(), templ.float(), rois.float())
     return out, coord
 
 

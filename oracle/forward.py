@@ -168,13 +168,19 @@ def backbone_asym(sd, pre, t, o, s):
     return _split_out(torch.cat([x_v, x_i], 0), B2, C, gt, gs)
 
 
-def ce_attn_mean(q_v, q_i, k_v, k_i, n_t, scale):
+def ce_attn_mean(q_v, q_i, k_v, k_i, n_t, scale, mask=None):
     """attn_t2s of Asym_Attention.forward(return_attention=True) (asymmetric_shared_ce.py:198-202),
-    averaged over template queries and heads (candidate_elimination :83-89, mask None):
-    softmax over [k_s_V | k_s_I] of [q_mt_V; q_mt_I], -> (B, 2 * lens_s) [RGB | TIR]."""
+    averaged over template queries and heads (candidate_elimination :81-92): softmax over
+    [k_s_V | k_s_I] of [q_mt_V; q_mt_I], -> (B, 2 * lens_s) [RGB | TIR].  mask (B, 2 n_t) bool
+    (ce_template_mask, e.g. ce_utils.py:14-38 CTR_POINT): only the masked queries' rows are averaged,
+    attn[mask].view(bs, hn, -1, L) as :81-86."""
     q = torch.cat([q_v[:, :, :n_t], q_i[:, :, :n_t]], 2)
     k = torch.cat([k_v[:, :, n_t:], k_i[:, :, n_t:]], 2)
     a = ((q @ k.transpose(-2, -1)) * scale).softmax(dim=-1)
+    if mask is not None:
+        bs, hn, _, L = a.shape
+        m = mask.to(torch.bool).unsqueeze(1).unsqueeze(-1).expand(-1, hn, -1, L)
+        a = a[m].view(bs, hn, -1, L)
     return a.mean(dim=2).mean(dim=1)
 
 
@@ -198,10 +204,11 @@ def ce_select(attn_mean, x, n_t, keep_ratio, gidx, forced=None):
     return torch.cat([x[:, :n_t], xs], 1), gidx.gather(1, order)
 
 
-def backbone_asym_ce(sd, pre, t, o, s, stages=None, forced=None):
+def backbone_asym_ce(sd, pre, t, o, s, stages=None, forced=None, mask=None):
     """asymmetric_shared_ce.py:228-282 (CE_Block_Shared), :372-424 (VisionTransformer.forward with
     _recover_search).  The elimination runs after a CE block's attention residual, before its MLP;
-    pruned search positions come back as zero tokens.  `stages` (a list) receives the kept indices."""
+    pruned search positions come back as zero tokens.  `stages` (a list) receives the kept indices;
+    mask = ce_template_mask (see ce_attn_mean)."""
     C, H, depth, gt, gs = _vit_dims(sd, pre)
     x = _tokens(sd, pre, t, o, s)
     B2 = x.shape[0]
@@ -223,7 +230,7 @@ def backbone_asym_ce(sd, pre, t, o, s, stages=None, forced=None):
         if i in CE_LOC:
             qkv = F.linear(torch.cat([xn_v, xn_i], 0), sd[b + "attn.qkv.weight"], sd[b + "attn.qkv.bias"])
             q, k, _ = _heads(qkv, B2, n, H).unbind(0)
-            am = ce_attn_mean(q[:Bh], q[Bh:], k[:Bh], k[Bh:], n_t, scale)
+            am = ce_attn_mean(q[:Bh], q[Bh:], k[:Bh], k[Bh:], n_t, scale, mask)
             ls = n - n_t
             st = CE_LOC.index(i)
             fv, fi = forced[st] if forced is not None else (None, None)
@@ -429,7 +436,7 @@ def score_decoder(sd, pre, search, template, box_xyxy, num_heads=12):
 # ----------------------------------------------------------------------------- models
 @torch.no_grad()
 def forward(sd, variant, template, online_template, search, run_score_head=False, return_aux=False, ce_forced=None,
-            gt_bboxes=None):
+            ce_template_mask=None):
     """Reference-equivalent forward.  template / online_template / search are [rgb, tir] lists
     of (B,3,H,W) fp32 CPU tensors.  Returns (out_dict, outputs_coord) like the reference;
     with return_aux also a dict of intermediates."""
@@ -454,7 +461,8 @@ def forward(sd, variant, template, online_template, search, run_score_head=False
         t_all = torch.cat([tv, ti], 0)
     else:
         fn = {"shared": backbone_shared, "asym_ce": backbone_asym_ce}.get(variant, backbone_asym)
-        kw = {"stages": aux.setdefault("ce_stages", []), "forced": ce_forced} if variant == "asym_ce" else {}
+        kw = ({"stages": aux.setdefault("ce_stages", []), "forced": ce_forced, "mask": ce_template_mask}
+              if variant == "asym_ce" else {})
         t_all, _, s_all = fn(sd, "backbone.", torch.cat(template, 0), torch.cat(online_template, 0), torch.cat(search, 0),
                              **kw)
         Bh = s_all.shape[0] // 2
@@ -474,8 +482,10 @@ def forward(sd, variant, template, online_template, search, run_score_head=False
     if variant == "asym_online" and run_score_head:
         Bh = t_all.shape[0] // 2
         templ = torch.cat([t_all[:Bh], t_all[Bh:]], dim=2)
-        # forward_head, asymmetric_shared_online.py:405-410: the ROI is gt_bboxes when given
-        gt = cxcywh_to_xyxy(coord.clone().view(-1, 4)) if gt_bboxes is None else gt_bboxes.view(-1, 4).float()
+        aux["score_template"] = templ
+        # forward_head, asymmetric_shared_online.py:405-410, called without gt_bboxes (:374): the ROI is
+        # always the predicted box
+        gt = cxcywh_to_xyxy(coord.clone().view(-1, 4))
         out["pred_scores"] = score_decoder(sd, "score_branch.", fused, templ, gt,
                                            num_heads=fused.shape[1] // 64).view(-1)
     if return_aux:

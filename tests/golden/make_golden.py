@@ -274,6 +274,16 @@ def msda_fixture():
 
 def main():
     install_stubs()
+    if len(sys.argv) > 2 and sys.argv[1] == "--cases":
+        # extra (variant, batch) fixtures only, e.g. --cases shared:8,asym:8 (BASELINE config 3's
+        # per-rank batch; the default run below leaves them untouched)
+        for case in sys.argv[2].split(","):
+            variant, B = case.split(":")
+            t0 = time.time()
+            res, _, _ = run_model(variant, int(B), timing=False)
+            np.savez_compressed(os.path.join(OUT, "model_%s_b%d.npz" % (variant, int(B))), **res)
+            print(variant, B, "boxes", res["pred_boxes"].reshape(-1, 4).tolist(), "%.1fs" % (time.time() - t0), flush=True)
+        return
     meta = {"reference": "LZ-QWQ/Multi-modal-Tracking @ /root/reference (read-only)", "torch": torch.__version__,
             "weights": "mmt-synth-v1 (mmt_amd/synthetic.py), HEAD_GAIN=%g" % synthetic.HEAD_GAIN,
             "inputs": "synth_inputs(B, 128, 320, seed=1)", "cpu_fps_ref": {}}

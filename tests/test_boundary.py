@@ -103,15 +103,23 @@ def test_synthetic_weights_are_deterministic():
         synthetic.uniform("backbone.blocks.0.attn.qkv.weight", (5,))[0])) == 0.0
 
 
-def test_ce_partial_template_mask_raises():
-    """A CE template mask restricted to part of the template (CE_TEMPLATE_RANGE CTR_POINT) is refused
-    explicitly rather than ignored (the kernels average every template query's attention)."""
+def test_ce_template_mask_validation():
+    """ce_template_mask (generate_mask_cond, lib/utils/ce_utils.py:14-38) is validated on the host before
+    any device work: wrong shape or unequal per-frame counts raise ValueError (the reference views
+    attn[mask] as (bs, heads, -1, L)); a valid CTR_POINT mask reaches the device check (no CPU path)."""
     import pytest
     import torch
     from mmt_amd import model as M
     net = M.build_asymmetric_shared_ce(M.hot_path_cfg(), train=False).eval()
-    mask = torch.zeros(1, 256, dtype=torch.bool)
-    mask[:, 27] = True
-    x = [torch.zeros(1, 3, 128, 128)] * 2
-    with pytest.raises(NotImplementedError):
-        net(x, x, [torch.zeros(1, 3, 320, 320)] * 2, ce_template_mask=mask, ce_keep_rate=0.7)
+    x = [torch.zeros(2, 3, 128, 128)] * 2
+    s = [torch.zeros(2, 3, 320, 320)] * 2
+    mask = torch.zeros(2, 256, dtype=torch.bool)
+    mask[:, [27, 91, 155, 219]] = True  # CTR_POINT: centre token of each 8x8 template
+    with pytest.raises(ValueError):
+        net(x, x, s, ce_template_mask=mask[:, :128])
+    bad = mask.clone()
+    bad[1, 0] = True
+    with pytest.raises(ValueError):
+        net(x, x, s, ce_template_mask=bad)
+    with pytest.raises(RuntimeError):
+        net(x, x, s, ce_template_mask=mask, ce_keep_rate=0.7)

@@ -96,3 +96,5 @@ def test_persistent_pair_attention_shape_gate():
     assert attn(lse=fake) == -10000
     assert attn(dt=_lib.MMT_F16) == -10000
     assert attn(impl=99) == -10000
+    # impl 22 never writes the log-sum-exp the training backward consumes: lse with impl 22 is rejected
+    assert attn(impl=22, lse=fake) == -10000

@@ -24,14 +24,15 @@ pytestmark = pytest.mark.gpu
 _RT = {}
 
 
-def _runtime(dtype):
-    if dtype not in _RT:
+def _runtime(dtype, mask_count=None):
+    key = (dtype, mask_count)
+    if key not in _RT:
         from mmt_amd import synthetic
         from mmt_amd.runtime import MixFormerRGBTRuntime
         keys = json.load(open(GOLDEN + "/state_dict_asym_ce.json"))
         sd = {k: torch.from_numpy(v) for k, v in synthetic.synth_state_dict(keys).items()}
-        _RT[dtype] = MixFormerRGBTRuntime(sd, "asym_ce", dtype=dtype)
-    return _RT[dtype]
+        _RT[key] = MixFormerRGBTRuntime(sd, "asym_ce", dtype=dtype, ce_mask_count=mask_count)
+    return _RT[key]
 
 
 def _inputs(B):
@@ -40,14 +41,19 @@ def _inputs(B):
     return [x.cuda() for x in t], [x.cuda() for x in o], [x.cuda() for x in s]
 
 
+@pytest.mark.parametrize("masked", [False, True])
 @pytest.mark.parametrize("dname,tol", [("f32", 1e-3), ("bf16", 1e-2)])
 @pytest.mark.parametrize("B", [1, 2])
-def test_ce_model_matches_reference(B, dname, tol):
-    rt = _runtime(torch.float32 if dname == "f32" else torch.bfloat16)
+def test_ce_model_matches_reference(B, dname, tol, masked):
+    """masked: ce_template_mask = the training actor's CTR_POINT mask (generate_mask_cond,
+    lib/utils/ce_utils.py:14-38, taken from the reference-made fixture): the elimination averages
+    the attention of the 4 masked template queries per frame only."""
+    gold = np.load(GOLDEN + "/model_asym_ce_%sb%d.npz" % ("mask_" if masked else "", B))
+    mask = torch.from_numpy(gold["ce_template_mask"]) if masked else None
+    rt = _runtime(torch.float32 if dname == "f32" else torch.bfloat16, 4 if masked else None)
     inputs = _inputs(B)
-    box, _ = rt.forward(*inputs)
+    box, _ = rt.forward(*inputs, ce_template_mask=None if mask is None else mask.cuda())
     torch.cuda.synchronize()
-    gold = np.load(GOLDEN + "/model_asym_ce_b%d.npz" % B)
     err = np.abs(box.cpu().numpy() - gold["pred_boxes"].reshape(B, 4)).max()
     ws = rt.workspace(B)
     same, overlap, forced = [], [], []
@@ -66,7 +72,8 @@ def test_ce_model_matches_reference(B, dname, tol):
         from mmt_amd import synthetic
         from oracle.forward import forward as oracle_forward, state_dict_to_torch
         sd = state_dict_to_torch(synthetic.synth_state_dict(json.load(open(GOLDEN + "/state_dict_asym_ce.json"))))
-        out, _ = oracle_forward(sd, "asym_ce", *[[x.cpu() for x in grp] for grp in inputs], ce_forced=forced)
+        out, _ = oracle_forward(sd, "asym_ce", *[[x.cpu() for x in grp] for grp in inputs], ce_forced=forced,
+                                ce_template_mask=mask)
         rerr = np.abs(box.cpu().numpy() - out["pred_boxes"].reshape(B, 4).numpy()).max()
         print("bf16 box err vs the oracle replaying the bf16 selections %.3g" % rerr)
         assert rerr <= tol, rerr
@@ -86,6 +93,31 @@ def test_ce_model_matches_reference(B, dname, tol):
             am = ws["CEM"][k].view(-1)[:B * n].view(B, n).cpu().numpy()
             aerr = np.abs(am - ref).max() / np.abs(ref).max()
             assert aerr <= 1e-5, (k, aerr)
+
+
+def test_ce_module_accepts_actor_mask():
+    """The module API as the actor calls it (actors/mixformer_rgbt.py:82-90): net(t, o, s,
+    ce_template_mask=CTR_POINT mask, ce_keep_rate=...) in eval / no_grad equals the runtime's masked
+    forward, an all-True mask equals no mask, and a mask with unequal per-frame counts is refused."""
+    from mmt_amd import model as M
+    from mmt_amd import synthetic
+    net = M.build_asymmetric_shared_ce(M.hot_path_cfg(), train=False)
+    keys = [(k, list(v.shape)) for k, v in net.state_dict().items()]
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic.synth_state_dict(keys).items()}, strict=True)
+    net = net.cuda().eval().set_compute_dtype(torch.float32)
+    gold = np.load(GOLDEN + "/model_asym_ce_mask_b2.npz")
+    mask = torch.from_numpy(gold["ce_template_mask"]).cuda()
+    t, o, s = _inputs(2)
+    with torch.no_grad():
+        out, _ = net(t, o, s, ce_template_mask=mask, ce_keep_rate=0.7)
+        assert np.abs(out["pred_boxes"].cpu().numpy() - gold["pred_boxes"]).max() <= 1e-3
+        full, _ = net(t, o, s, ce_template_mask=torch.ones(2, 256, dtype=torch.bool, device="cuda"))
+        plain, _ = net(t, o, s)
+        assert torch.equal(full["pred_boxes"], plain["pred_boxes"])
+        bad = mask.clone()
+        bad[0, 0] = True
+        with pytest.raises(ValueError):
+            net(t, o, s, ce_template_mask=bad)
 
 
 def test_ce_select_matches_torch_sort():

@@ -9,7 +9,8 @@ import torch
 
 from conftest import GOLDEN
 
-CASES = [("rgbt", 1), ("shared", 1), ("asym", 1), ("asym_online", 1), ("shared", 2)]
+# B = 8: BASELINE config 3's per-rank batch (64 sequences over 8 GPUs)
+CASES = [("rgbt", 1), ("shared", 1), ("asym", 1), ("asym_online", 1), ("shared", 2), ("shared", 8), ("asym", 8)]
 
 
 def _sub(x, n=4096):
@@ -155,18 +156,24 @@ def test_oracle_prroi_empty_and_outside():
     assert 0 < out[2, 0, 1, 1] <= 1.0   # partially outside -> partial mass
 
 
+@pytest.mark.parametrize("masked", [False, True])
 @pytest.mark.parametrize("B", [1, 2])
-def test_oracle_candidate_elimination_matches_reference(B):
+def test_oracle_candidate_elimination_matches_reference(B, masked):
     """asymmetric_shared_ce: boxes, maps and features, plus every elimination
     stage's mean template->search attention and kept token indices (reference order), vs the
-    reference's own forward (tests/golden/make_golden_ce.py)."""
+    reference's own forward (tests/golden/make_golden_ce.py); masked: with the training actor's
+    CTR_POINT ce_template_mask (lib/utils/ce_utils.py:14-38, the reference's own mask in the fixture)."""
     from mmt_amd import synthetic
     from oracle import forward as of
     torch.set_num_threads(8)
-    g = np.load(GOLDEN + "/model_asym_ce_b%d.npz" % B)
+    g = np.load(GOLDEN + "/model_asym_ce_%sb%d.npz" % ("mask_" if masked else "", B))
     sd = of.state_dict_to_torch(synthetic.synth_state_dict(json.load(open(GOLDEN + "/state_dict_asym_ce.json"))))
     t, o, s = synthetic.synth_inputs(B)
-    out, coord, aux = of.forward(sd, "asym_ce", t, o, s, return_aux=True)
+    mask = torch.from_numpy(g["ce_template_mask"]) if masked else None
+    if masked:  # CTR_POINT: the centre token (3, 3) of each of the four 8x8 templates
+        assert mask.shape == (B, 256) and mask.sum().item() == 4 * B
+        assert all(bool(mask[:, 64 * j + 27].all()) for j in range(4))
+    out, coord, aux = of.forward(sd, "asym_ce", t, o, s, return_aux=True, ce_template_mask=mask)
     assert np.abs(out["pred_boxes"].numpy() - g["pred_boxes"]).max() < 1e-5
     for nm in ("score_map_tl", "score_map_br"):
         assert np.abs(aux[nm].numpy() - g[nm]).max() < 1e-4 * max(1.0, np.abs(g[nm]).max())

@@ -53,7 +53,7 @@ def main():
             st = np.frombuffer(buf, dtype=np.uint64).reshape(S, H, nqb, 8).astype(np.int64)
             freq = float(np.median((st[..., 4] - st[..., 1]) / np.maximum(st[..., 5] - st[..., 0], 1))) * 100.0
             for kind, sl in (("tmpl", slice(0, (n_t + 63) // 64)), ("search", slice((n_t + 63) // 64, nqb))):
-                x = st[:, :, sl].reshape(-1, 6)
+                x = st[:, :, sl].reshape(-1, 8)
                 row[kind] = {"prologue_us": round(float(np.median(x[:, 2] - x[:, 1])) / freq, 2),
                              "loop_us": round(float(np.median(x[:, 3] - x[:, 2])) / freq, 2),
                              "epilogue_us": round(float(np.median(x[:, 4] - x[:, 3])) / freq, 2),
