@@ -19,17 +19,21 @@ Multi-GPU (one process per GPU, no data-path collective):
   equal --gpus.
 
 Extra fields:
-  kernels        device time per launch of every plan entry (graph-replayed back-to-back launches
-                 timed with HIP events on the launch stream, after the timed region)
+  kernels        device time per launch of every plan entry inside the frame (inframe_profile: frames
+                 enqueued behind a spin kernel with HIP events around every launch, after the timed
+                 region)
   roofline       the kernel with the largest share of device time: algorithmic FLOPs per launch /
-                 that average launch time; `traffic` = HBM bytes per launch from the PMC pass in
+                 that average in-frame launch time (the warm back-to-back figure of kernel_profile
+                 beside it as warm_avg_launch_us); `traffic` = HBM bytes per launch from the PMC pass in
                  profiles/pmc_traffic.json (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction) when it
                  was measured for this workload, else null
   roofline_mam   the same for the MAM attention kernel
   roofline_mam_batched  the MAM attention kernel alone at the batched-inference size (SURVEY §8(e)
                  C3: 32 frames per GPU, the grid where the throughput kernel runs), same definition
   cpu_baseline   the oracle's fp32 CPU forward (oracle/forward.py, a restatement of the reference)
-                 on a bounded sample, rank 0 at N=1 only
+                 on a bounded sample, rank 0 at N=1 only, on every physical core available to the
+                 process (lscpu sockets x cores, capped by the affinity mask and cgroup quota);
+                 cpu_baseline_b8 the same at B = 8
 """
 import argparse
 import ctypes
@@ -128,6 +132,34 @@ def kernel_profile(rt, plan, per_graph=20, replays=5):
     return [per_name[e[2]] for e in plan]  # ms per launch
 
 
+def inframe_profile(rt, plan, frames=20):
+    """Device time of every launch of the frame as it runs inside the frame (the cache state the
+    previous launch leaves, no repeated copies): the host holds the stream with a spin kernel
+    (torch.cuda._sleep) while it enqueues `frames` frames of the plan with a HIP timing event before
+    each launch, so the launches then run back to back with no host gaps and the events bracket each
+    one.  Returns ms per launch (median over the frames) in plan order, and the median frame span."""
+    s = torch.cuda.current_stream()
+    st = s.cuda_stream
+    n = len(plan)
+    per = [[] for _ in range(n)]
+    spans = []
+    for _ in range(frames):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(n + 1)]
+        torch.cuda._sleep(20_000_000)  # ~10 ms of spin: the whole frame is enqueued before it starts
+        for i, (fn, args, name, _keep) in enumerate(plan):
+            ev[i].record(s)
+            rc = fn(*args, st)
+            if rc != 0:
+                raise RuntimeError("%s failed (%d)" % (name, rc))
+        ev[n].record(s)
+        torch.cuda.synchronize()
+        for i in range(n):
+            per[i].append(ev[i].elapsed_time(ev[i + 1]))
+        spans.append(ev[0].elapsed_time(ev[n]))
+    med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
+    return [med(v) for v in per], med(spans)
+
+
 def load_traffic(variant, B, dtype):
     """HBM bytes per launch by plan-entry name, from the committed PMC pass (tools/pmc_traffic.py)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -138,15 +170,18 @@ def load_traffic(variant, B, dtype):
         return {}
 
 
-def roofline(rt, plan, times, dtype, traffic=None):
+def roofline(rt, plan, times, dtype, traffic=None, warm_times=None):
+    """times: in-frame ms per launch (inframe_profile); warm_times: the warm back-to-back copies of
+    kernel_profile, reported beside it as `warm_avg_launch_us` / `warm_frac`."""
     traffic = traffic or {}
     by = {}
-    for e, t in zip(plan, times):
+    for i, (e, t) in enumerate(zip(plan, times)):
         nm = e[2]
-        a = by.setdefault(nm, {"t": 0.0, "n": 0, "flops": 0.0})
+        a = by.setdefault(nm, {"t": 0.0, "n": 0, "flops": 0.0, "tw": 0.0})
         a["t"] += t
         a["n"] += 1
         a["flops"] += plan_flops(rt, e)
+        a["tw"] += warm_times[i] if warm_times else 0.0
     total = sum(a["t"] for a in by.values())
     dom = max(by, key=lambda k: by[k]["t"])
 
@@ -155,10 +190,16 @@ def roofline(rt, plan, times, dtype, traffic=None):
         avg_ms = a["t"] / a["n"]
         ach = (a["flops"] / a["n"]) / (avg_ms * 1e-3) / 1e12
         tb = traffic.get(nm, {}).get("traffic_bytes")
-        return {"kernel": nm, "bound": "mfma", "achieved": round(ach, 2), "peak": PEAK[dtype], "unit": "TFLOP/s",
-                "frac": round(ach / PEAK[dtype], 4), "traffic": tb, "traffic_unit": "bytes/launch (HBM, PMC)",
-                "flops_per_launch": a["flops"] / a["n"], "avg_launch_us": round(avg_ms * 1e3, 2),
-                "launches_per_step": a["n"], "share_of_device_time": round(a["t"] / total, 4)}
+        o = {"kernel": nm, "bound": "mfma", "achieved": round(ach, 2), "peak": PEAK[dtype], "unit": "TFLOP/s",
+             "frac": round(ach / PEAK[dtype], 4), "traffic": tb, "traffic_unit": "bytes/launch (HBM, PMC)",
+             "flops_per_launch": a["flops"] / a["n"], "avg_launch_us": round(avg_ms * 1e3, 2),
+             "timing": "in-frame (HIP events around each launch of enqueued frames, median of 20)",
+             "launches_per_step": a["n"], "share_of_device_time": round(a["t"] / total, 4)}
+        if warm_times:
+            w_ms = a["tw"] / a["n"]
+            o["warm_avg_launch_us"] = round(w_ms * 1e3, 2)
+            o["warm_frac"] = round((a["flops"] / a["n"]) / (w_ms * 1e-3) / 1e12 / PEAK[dtype], 4)
+        return o
 
     return obj(dom), obj("mam_attention"), total, by
 
@@ -249,14 +290,50 @@ def host_cpu():
     return info
 
 
+def cgroup_cpus():
+    """CPUs the process's cgroup may use (cpu.max quota / period; None = no quota)."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                return max(1, int(int(q) / int(per)))
+        except (OSError, ValueError):
+            pass
+    try:  # cgroup v1
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            return max(1, q // per)
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def baseline_threads(info):
+    """All physical cores available to this process (BASELINE.md:53): lscpu sockets x cores per
+    socket, capped by the CPUs of the process's affinity mask and by its cgroup CPU quota (the
+    OMP_NUM_THREADS default of the job environment is deliberately not used)."""
+    try:
+        phys = int(info["sockets"]) * int(info["cores_per_socket"])
+    except (KeyError, ValueError):
+        phys = os.cpu_count() or 1
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = cgroup_cpus()
+    n = min(phys, aff, quota or aff)
+    return n, {"physical_cores": phys, "affinity_cpus": aff, "cgroup_cpus": quota}
+
+
 def cpu_baseline(variant, B, budget_s=12.0, geo=None):
     """Oracle (fp32 CPU restatement of the reference forward; within +-15 % of the reference's own
     CPU time on the same threads, tools/cpu_baseline_check.py -> profiles/cpu_baseline_check.json):
-    3 warm-up forwards, then the median of >= 10 timed forwards or as many as fit the budget."""
+    3 warm-up forwards, then the median of >= 10 timed forwards or as many as fit the budget, on
+    every physical core available to the process (baseline_threads)."""
     geo = geo or GEO_B
     from mmt_amd import synthetic
     from oracle.forward import forward as oracle_forward, state_dict_to_torch
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
+    info = host_cpu()
+    threads, avail = baseline_threads(info)
+    info.update(avail)
     torch.set_num_threads(threads)
     sd = state_dict_to_torch(synthetic.synth_state_dict(state_dict_keys(variant, **geo)))
     t, o, s = synthetic.synth_inputs(B, geo["template"], geo["search"])
@@ -271,9 +348,48 @@ def cpu_baseline(variant, B, budget_s=12.0, geo=None):
             break
     med = sorted(times)[len(times) // 2]
     return {"value": round(B / med, 3), "unit": "frames/s", "cores": threads, "kind": "port",
-            "host": host_cpu(),
+            "host": info,
             "sample": "median of %d fp32 CPU forwards of B=%d after 3 warm-up (%s, %d/%d), %.1f s, oracle/forward.py"
                       % (len(times), B, variant, geo["template"], geo["search"], sum(times))}
+
+
+TRAIN_FLOP_PER_SAMPLE = 3 * 218.59e9  # forward + backward ~ 3 x the 218.59 GFLOP forward
+
+
+def train_bench(world, rank, B, steps, warmup, device="cuda", ops=None, search=320, template=128):
+    """BASELINE config 4: DDP training step of the two-stream MixViT-B RGB-T,
+    B LaSOT-shaped synthetic pairs per GPU: forward with autograd on the HIP ops, CIoU + L1 box
+    loss, backward with the RCCL gradient all-reduce (DistributedDataParallel, bucketed, overlapped
+    with the backward; SyncBatchNorm in the head when world > 1), clip, AdamW
+    (mmt_amd.train.TrainStep; reference train_script_mixformer.py:105-140,
+    actors/mixformer_rgbt.py:33-168).  Returns the result object (samples/s over all ranks by the
+    max-over-ranks time, ms per step, an MFMA roofline of the whole step).  device / ops / image sizes:
+    the CPU harness test runs it over gloo with stand-in ops at small images (the product: HipOps)."""
+    from mmt_amd.model import build_mixformer_vit_rgbt, hot_path_cfg
+    from mmt_amd.train import HipOps, TrainStep, synthetic_batch
+    torch.manual_seed(0)  # identical initial replicas (DDP also broadcasts rank 0's weights)
+    net = build_mixformer_vit_rgbt(hot_path_cfg(search=search, template=template), train=False).to(device).train()
+    step_fn = TrainStep(net, ops or HipOps, ddp=world > 1)
+    g = torch.Generator().manual_seed(100 + rank)  # each rank its own shard of the clip batch
+    batches = [synthetic_batch(B, device, g, template, search) for _ in range(2)]
+    sync = torch.cuda.synchronize if device != "cpu" else (lambda: None)
+    last = {}
+
+    def step(i):
+        last["stats"] = step_fn(*batches[i % 2])
+
+    for i in range(warmup):
+        step(i)
+    elapsed = timed_steps(step, steps, world, sync, device)
+    sps = world * B * steps / elapsed
+    ach = sps / world * TRAIN_FLOP_PER_SAMPLE / 1e12  # per GPU
+    return {"value": round(sps, 2), "unit": "samples/s", "ms_per_step": round(elapsed / steps * 1e3, 3),
+            "batch_per_gpu": B, "steps": steps, "warmup": warmup,
+            "parallelism": "ddp%d (RCCL gradient all-reduce)" % world if world > 1 else "single",
+            "roofline": {"kernel": "train_step (whole step)", "bound": "mfma", "achieved": round(ach, 2),
+                         "peak": PEAK["bf16"], "unit": "TFLOP/s", "frac": round(ach / PEAK["bf16"], 4),
+                         "flops_per_sample": TRAIN_FLOP_PER_SAMPLE, "traffic": None},
+            "last_loss": round(float(last["stats"]["loss"]), 5)}
 
 
 def timed_steps(step, steps, world, sync, device):
@@ -377,7 +493,19 @@ def main():
                     help="batched multi-sequence inference (config 3): shard this many sequences over the ranks")
     ap.add_argument("--dry-run", action="store_true",
                     help="harness check without a GPU: resolve ranks and shards over gloo, print them, exit")
+    ap.add_argument("--train", action="store_true",
+                    help="BASELINE config 4: DDP training step (RCCL gradient all-reduce), --batch pairs per GPU "
+                         "(default 16), --steps / --warmup default 20 / 5")
+    ap.add_argument("--no-train-line", action="store_true",
+                    help="skip the short DDP training measurement (train_step) appended to the inference line")
     args = ap.parse_args()
+    if args.train:
+        if args.batch == 1:
+            args.batch = 16  # yaml TRAIN.BATCH_SIZE
+        if args.steps == 200:
+            args.steps = 20
+        if args.warmup == 20:
+            args.warmup = 5
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:  # self-launch: one worker process per GPU
         sys.exit(launch_workers(args.gpus, sys.argv[1:]))
@@ -407,6 +535,24 @@ def main():
 
     from mmt_amd import synthetic
     from mmt_amd.runtime import MixFormerRGBTRuntime
+
+    if args.train:
+        res = train_bench(world, rank, args.batch, args.steps, args.warmup)
+        if rank == 0:
+            out = {"metric": "train samples/s (two-stream MixViT-B RGB-T DDP step, BASELINE config 4)",
+                   "value": res["value"], "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+                   "warmup": args.warmup, "ms_per_step": res["ms_per_step"], "higher_is_better": True,
+                   "scaling": "weak", "vs_baseline": None,
+                   "dtype": "bf16 (backbone GEMM / attention operands), fp32 master weights and accumulation",
+                   "data": "synthetic LaSOT-shaped pairs (N(0,1) images, random boxes), random-init weights",
+                   "config": {"workload": "mixformer_vit_rgbt ViT-B 128/320 DDP train step, %d pairs/GPU" % args.batch,
+                              "batch_per_gpu": args.batch, "parallelism": res["parallelism"]},
+                   "roofline": res["roofline"], "cpu_baseline": None, "last_loss": res["last_loss"]}
+            print(json.dumps(out), flush=True)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
 
     dtype = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(args.dtype, torch.float32)
     geo = GEO_L if args.vitl else (GEO_RGB if args.variant == "rgb" else GEO_B)
@@ -450,8 +596,9 @@ def main():
         dom = mam = by = None
         dev_ms = None
     else:
-        times = kernel_profile(rt, plan)
-        dom, mam, dev_ms, by = roofline(rt, plan, times, args.dtype, load_traffic(args.variant, B, args.dtype))
+        times, span_ms = inframe_profile(rt, plan)
+        warm = kernel_profile(rt, plan)
+        dom, mam, dev_ms, by = roofline(rt, plan, times, args.dtype, load_traffic(args.variant, B, args.dtype), warm)
 
     if rank == 0:
         frames = world * B * args.steps
@@ -478,7 +625,8 @@ def main():
                        "hip_graph": use_graph},
             "roofline": dom,
             "roofline_mam": mam_memory_roofline(mam, nmod * B, rt.d.ntok, rt.d.C, 4 if args.dtype == "f32" else 2),
-            "device_ms_per_step_sum": round(dev_ms, 4) if dev_ms else None, "launches_per_step": len(plan),
+            "device_ms_per_step_sum": round(dev_ms, 4) if dev_ms else None,
+            "inframe_span_ms": round(span_ms, 4) if dev_ms else None, "launches_per_step": len(plan),
             "kernels": {k: {"us": round(a["t"] * 1e3 / a["n"], 2), "n": a["n"],
                             "tflops": round(a["flops"] / a["n"] / (a["t"] / a["n"] * 1e-3) / 1e12, 1) if a["flops"] else None}
                         for k, a in sorted(by.items(), key=lambda kv: -kv[1]["t"])} if by else None,
@@ -488,8 +636,23 @@ def main():
             out["roofline_mam_batched_b8"] = mam_batched(rt, B=8)
         if use_graph and not args.no_kv_cache and args.variant != "asym_ce":  # no template cache with CE
             out["tracking_kv_cache"] = kv_cache_tracking(rt, pool, score, args.steps, args.warmup)
+    if not args.no_train_line and args.variant == "rgbt" and not args.vitl and not sharded:
+        # config 4's DDP step beside the replicas: the one data-path collective (RCCL gradient
+        # all-reduce) is timed at every N of a scaling run; a failure is reported, not raised
+        del graphs, plans, pool
+        torch.cuda.empty_cache()
+        try:
+            train_res = train_bench(world, rank, 16, 5, 2)
+        except Exception as e:  # noqa: BLE001
+            train_res = {"error": "%s: %s" % (type(e).__name__, e)}
+    else:
+        train_res = None
+    if rank == 0:
+        out["train_step"] = train_res
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.variant, B, budget_s=20.0 if args.vitl else 12.0, geo=geo)
+            if B == 1 and not args.vitl:  # BASELINE.md:58: B = 1 and B = 8
+                out["cpu_baseline_b8"] = cpu_baseline(args.variant, 8, budget_s=12.0, geo=geo)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

@@ -102,3 +102,34 @@ def test_sharded_slices_equal_single_process():
     full, _ = forward(_sd(), "shared", t, o, s)
     assert sharded.shape == full["pred_boxes"].shape == (total, 1, 4)
     assert torch.allclose(sharded, full["pred_boxes"], atol=1e-5, rtol=0), (sharded - full["pred_boxes"]).abs().max()
+
+
+def _train_worker(rank, world, port, out):
+    import json as _json
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_train import TorchOps, SEARCH, TEMPLATE
+    import bench
+    torch.set_num_threads(2)
+    res = bench.train_bench(world, rank, 2, 2, 1, device="cpu", ops=TorchOps, search=SEARCH, template=TEMPLATE)
+    with open(os.path.join(out, "r%d.json" % rank), "w") as f:
+        _json.dump(res, f)
+    dist.destroy_process_group()
+
+
+def test_train_harness_gloo_two_ranks(tmp_path):
+    """bench.py --train's harness (config 4) over a world-size-2 gloo group with the
+    fp32 stand-in ops at small images: DDP step (the gradient all-reduce is the data-path collective),
+    the contract's barrier + max-over-ranks timing (both ranks report the same rate), samples/s over
+    all ranks, and the step's MFMA roofline field."""
+    import json as _json
+    import torch.multiprocessing as mp
+    port = 29500 + (os.getpid() % 500)
+    mp.spawn(_train_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    r0 = _json.load(open(tmp_path / "r0.json"))
+    r1 = _json.load(open(tmp_path / "r1.json"))
+    assert r0["value"] == r1["value"] > 0 and r0["ms_per_step"] == r1["ms_per_step"]
+    assert r0["parallelism"].startswith("ddp2")
+    assert r0["roofline"]["bound"] == "mfma" and 0 < r0["roofline"]["frac"]
+    assert abs(r0["value"] - 2 * 2 * 2 / (r0["ms_per_step"] * 2e-3)) <= 1e-2 * r0["value"]
