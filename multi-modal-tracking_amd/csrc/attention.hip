@@ -1745,6 +1745,344 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
 }
 
+// ---- impl 23: block-pipelined range-checked kernel with a hand-placed issue order ---------------------
+// The same math per 32-key block as impl 17 / 22 (P = exp2(S) with no reference point, row sums on the
+// matrix pipe, epilogue range check with the exact fallback), re-timed so that one wave carries two
+// independent instruction streams at every point of its loop:
+//   slot b, phase 1:  QK^T MFMAs of block b+1 (8)       beside the 32 v_exp_f32 of block b's scores
+//                     and the V^T fragment reads of block b
+//   slot b, phase 2:  PV + row-sum MFMAs of block b (12)  beside the 16 v_cvt_pk of block b and the K
+//                     fragment reads of block b+2
+// i.e. a two-stage software pipeline over 32-key blocks (scores of one block in flight while the
+// previous block is exponentiated and multiplied into O), with sched_group_barrier placing about two
+// exponentials / one pack per MFMA gap (the guide's "<= 24 cycles of issue per 32x32x16 gap").  64
+// queries per wave (two 32-query blocks share every K / V fragment), NW waves per workgroup sharing one
+// K / V stream (NW = 4: 256 queries, half the L2 -> LDS fill of 128-query workgroups), 2 waves per SIMD.
+// K / V tiles: a 4-slot LDS-DMA ring, one barrier per 64-key tile placed inside the slot that first
+// reads the tile; tile t + 2 is issued there into the slot of tile t - 2, which every wave has finished
+// reading (the fragment reads run one block ahead of the math).  Loop: global memory sees only the
+// LDS-DMA pieces, so the counted vmcnt waits never include a store (stores start in the epilogue).
+template <int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2))) void mam_attention_hs_kernel(
+    const mmt_attn_params p) {
+    constexpr int R = 4;          // K / V tile slots
+    constexpr int QWG = 64 * NW;  // queries per workgroup
+    constexpr int NP = 16 / NW;   // 1-KiB DMA pieces per wave per tile (8 K + 8 V pieces)
+    static_assert(QWG * 128 <= 2 * FTILE, "the Q image fits the last two ring slots");
+    __shared__ __attribute__((aligned(1024))) char lds[R * FTILE];
+
+    const int n_t = p.n_t, ntok = p.ntok, C = p.C;
+    const int64_t pitch = p.tok_pitch > 0 ? p.tok_pitch : ntok;
+    const int nqb_t = (n_t + QWG - 1) / QWG;
+    int bx, h, s;
+    attn_block_ids_xcd(bx, h, s);
+    const int qbk = bx + (p.q_part == 2 ? nqb_t : 0);
+    const bool tmpl = qbk < nqb_t;
+    const int q0 = tmpl ? qbk * QWG : n_t + (qbk - nqb_t) * QWG;
+    const int qend = tmpl ? n_t : ntok;
+    const int Lk = tmpl ? n_t : (p.asym ? ntok + n_t : ntok);
+    const bool cross = p.asym && !tmpl;
+    const int64_t rs = 3 * (int64_t)C;
+    const bf16_t* qkv = (const bf16_t*)p.qkv;
+    const int sV = s % p.Bm, sI = sV + p.Bm;
+
+    const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int l32 = lane & 31, hf = lane >> 5;
+    const int prow = lane >> 3, pcol = lane & 7;
+
+    auto key_row = [&](int kk) -> const bf16_t* {
+        int seq = s, row = kk;
+        if (cross) {
+            if (kk < n_t) seq = sV;
+            else if (kk < 2 * n_t) { seq = sI; row = kk - n_t; }
+            else row = kk - n_t;
+        }
+        return qkv + ((int64_t)seq * pitch + row) * rs;
+    };
+    const bool aligned = n_t % KB == 0;
+    const int nkt = (Lk + KB - 1) / KB;
+    // wave w DMAs pieces w*NP .. w*NP+NP-1 of a tile: pieces 0-7 = K rows 8i..8i+7, 8-15 = V rows
+    const int isv = (w * NP) >> 3;  // wave-uniform: a wave's pieces are all K or all V
+    const int64_t col = (isv ? 2 * C : C) + h * D + (isv ? (pcol ^ attn_vswz(prow)) : (pcol ^ prow)) * 8;
+    auto issue_tile = [&](int t) {
+        char* slot = lds + (t % R) * FTILE + isv * KB * 128;
+        if (aligned && t * KB + KB <= Lk) {
+            const bf16_t* base = key_row(t * KB);  // wave-uniform
+#pragma unroll
+            for (int i = 0; i < NP; ++i) {
+                const int r8 = (w * NP + i) & 7;
+                attn_glds16(base + (int64_t)(r8 * 8 + prow) * rs + col, slot + r8 * 1024);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < NP; ++i) {
+                const int r8 = (w * NP + i) & 7;
+                attn_glds16(key_row(min(t * KB + r8 * 8 + prow, Lk - 1)) + col, slot + r8 * 1024);
+            }
+        }
+    };
+    // Q image (QWG rows x 128 B, rows past the block's end re-read the last query) in the last two
+    // slots, read into registers before those slots take tiles 2 and 3
+    char* qimg = lds + (R - 2) * FTILE;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int r = 64 * w + 8 * i + prow;
+        const bf16_t* src = qkv + ((int64_t)s * pitch + min(q0 + r, qend - 1)) * rs + h * D;
+        attn_glds16(src + ((pcol ^ prow) * 8), qimg + (8 * w + i) * 1024);
+    }
+    for (int t = 0; t < 2 && t < nkt; ++t) issue_tile(t);
+
+    const int qbase = q0 + 64 * w;  // query blocks qbase + 32 qb + [0, 32)
+    const bool active = qbase < qend;
+    const float cexp = p.scale * 1.4426950408889634f;
+    const bool prescale = fabsf(cexp - 1.f) > 1e-6f;
+    const float one_or_zero = (((lane & 15) >> 2) & 1) == ((lane >> 4) & 1) ? 1.f : 0.f;
+    const uint32_t sel_w = pack_bf16x2(one_or_zero, one_or_zero);
+    const bf16x8 sel = __builtin_bit_cast(bf16x8, u32x4{sel_w, sel_w, sel_w, sel_w});
+    const int kpos = (l32 & 7) * 16;
+    const int li = lane & 15, qr = li >> 2, pc = li & 3, dsub = (lane >> 4) & 1;
+
+    u32x4 qf[2][4];
+    attn_wait_vm<0>();
+    lds_barrier();
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+        const int row = 64 * w + 32 * qb + l32;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            qf[qb][ks] = *(const u32x4*)(qimg + row * 128 + (((2 * ks + hf) ^ (row & 7)) * 16));
+            if (prescale) {
+                u32x4 v = qf[qb][ks];
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    v[e] = pack_bf16x2(__uint_as_float(v[e] << 16) * cexp, __uint_as_float(v[e] & 0xffff0000u) * cexp);
+                qf[qb][ks] = v;
+            }
+        }
+    }
+    lds_barrier();
+    for (int t = 2; t < R && t < nkt; ++t) issue_tile(t);
+
+    const int nb = (Lk + 31) / 32;       // 32-key blocks; the last holds Lk - 32 (nb - 1) keys
+    const int nvl = Lk - 32 * (nb - 1);  // valid keys of the last block
+    // LDS fragment reads (inline asm: invisible to hipcc's wait-count tracking, so that it does not
+    // drain the LDS-DMA ring before them; the waits below are explicit)
+    auto kread = [&](int b, u32x4 (&kf)[4]) {
+        const char* krow = lds + ((b >> 1) % R) * FTILE + (32 * (b & 1) + l32) * 128;
+        const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)krow;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            const uint32_t ak = a + ((((2 * ks + hf) * 16) ^ kpos));
+            asm volatile("ds_read_b128 %0, %1" : "=v"(kf[ks]) : "v"(ak));
+        }
+    };
+    auto vread = [&](int b, uint2 (&vt)[2][2][2]) {
+        const char* vimg = lds + ((b >> 1) % R) * FTILE + KB * 128;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int row = 32 * (b & 1) + 16 * j + 4 * hf + qr;
+#pragma unroll
+            for (int db = 0; db < 2; ++db) {
+                const char* b1 = vimg + row * 128 + (((4 * db + 2 * dsub + (pc >> 1)) ^ attn_vswz(row)) * 16) + (pc & 1) * 8;
+                vt[j][db][0] = attn_tr16<0>(b1);
+                vt[j][db][1] = attn_tr16<8 * 128>(b1);
+            }
+        }
+    };
+    // tile sync point X_t, in step (2t - 1, 0) before the first reads of tile t (K of block 2t): its
+    // pieces landed (own: counted vmcnt; every wave's: the barrier), and every wave is past step
+    // (2t - 2, 1), i.e. past the last reads of tile t - 2 (V^T of block 2t - 3, step (2t - 3, 0)), whose
+    // slot then takes tile t + 2
+    auto sync_tile = [&](int t) {
+        if (t < 2 || t >= nkt) return;  // tiles 0 / 1 landed in the prologue
+        attn_wait_dyn(t + 1 < nkt ? NP : 0);
+        lds_barrier();
+        if (t + 2 < nkt) issue_tile(t + 2);
+    };
+
+    f32x16 o[2][2];
+    f32x4 lacc[2];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { o[qb][0][r] = 0.f; o[qb][1][r] = 0.f; }
+        lacc[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    // Pipeline unit u = (32-key block b, query block qb), in the order (0,0), (0,1), (1,0), ...; step u
+    // issues the MFMAs of PV(u - 1) (4 + 2 row-sum) and QK^T(u + 1) (4) beside the 16 exponentials
+    // and 8 packs of unit u: 288 matrix-pipe cycles against ~240 issue cycles, with two score and two
+    // P buffers live (S(u), S(u + 1); P(u - 1), P(u)).  K fragments change every second step (read
+    // after the QK^T MFMAs of step (b, 0) that last use K(b)), V^T fragments likewise (read after
+    // the PV MFMAs of step (b, 0) that last use V(b - 1)).
+    f32x16 sc[2];    // raw scores / exponentials of the two query blocks
+    u32x4 pf[2][2];  // packed P of the two query blocks, [qb][16-key half]
+    u32x4 kf[4];
+    uint2 vt[2][2][2];
+    auto qk = [&](int qb) {  // scores of query block qb against the block whose K fragments are in kf
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+            sc[qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kf[ks]),
+                                                             __builtin_bit_cast(bf16x8, qf[qb][ks]),
+                                                             ks ? sc[qb] : f32x16{}, 0, 0, 0);
+    };
+    auto pv = [&](int qb) {  // O += V^T P^T and the row sums, query block qb, block in vt / pf[qb]
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const bf16x8 pb = __builtin_bit_cast(bf16x8, pf[qb][j]);
+#pragma unroll
+            for (int db = 0; db < 2; ++db) {
+                const uint2 ua = vt[j][db][0], ub = vt[j][db][1];
+                o[qb][db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                    __builtin_bit_cast(bf16x8, make_uint4(ua.x, ua.y, ub.x, ub.y)), pb, o[qb][db], 0, 0, 0);
+            }
+            lacc[qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pb, lacc[qb], 0, 0, 0);
+        }
+    };
+    auto softmax = [&](int qb, bool mask) {  // P = exp2(S) (keys past Lk: 0), packed to bf16
+        if (mask) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float e = __builtin_amdgcn_exp2f(sc[qb][r]);
+                sc[qb][r] = 8 * (r >> 2) + 4 * hf + (r & 3) < nvl ? e : 0.f;
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sc[qb][r] = __builtin_amdgcn_exp2f(sc[qb][r]);
+        }
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+            const int rb = 8 * jj;
+            pf[qb][jj] = u32x4{pack_bf16x2(sc[qb][rb], sc[qb][rb + 1]), pack_bf16x2(sc[qb][rb + 2], sc[qb][rb + 3]),
+                               pack_bf16x2(sc[qb][rb + 4], sc[qb][rb + 5]), pack_bf16x2(sc[qb][rb + 6], sc[qb][rb + 7])};
+        }
+    };
+    // the issue pattern of one step: MFMAs each followed by 2 exponentials and 1 pack / select, the
+    // last ones bare (the ~24 issue cycles per 32x32x16 gap of MI355X_MICROARCH.md)
+    auto interleave = [&](int nmfma) {
+        for (int i = 0; i < nmfma; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+            if (i < 8) {
+                __builtin_amdgcn_sched_group_barrier(0x400, 2, 0);  // 2 transcendental (v_exp)
+                __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);  // 1 VALU (pack / select)
+            }
+        }
+    };
+    // step (b, 0): PV(b - 1, 1), QK^T(b, 1), softmax(b, 0); reads V(b), K(b + 1)
+    auto step0 = [&](int b, auto FIRSTc, auto MASKc) {
+        constexpr bool FIRST = decltype(FIRSTc)::value, MASK = decltype(MASKc)::value;
+        attn_lds_wait();  // K(b) / V(b - 1) fragments (the sched barrier keeps their consumers below)
+        if constexpr (!FIRST) pv(1);
+        vread(b, vt);  // the previous V^T fragments are consumed by the MFMAs above
+        qk(1);
+        softmax(0, MASK);
+        interleave(FIRST ? 4 : 10);
+        __builtin_amdgcn_sched_barrier(0);
+        if (b + 1 < nb) {
+            if (b & 1) sync_tile((b + 1) / 2);  // first reads of tile (b + 1) / 2
+            kread(b + 1, kf);
+        }
+    };
+    // step (b, 1): PV(b, 0), QK^T(b + 1, 0), softmax(b, 1)
+    auto step1 = [&](auto LASTc, auto MASKc) {
+        constexpr bool LAST = decltype(LASTc)::value, MASK = decltype(MASKc)::value;
+        attn_lds_wait();  // V(b), K(b + 1)
+        pv(0);
+        if constexpr (!LAST) qk(0);
+        softmax(1, MASK);
+        interleave(LAST ? 6 : 10);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    using I0 = attn_ic<0>;
+    using I1 = attn_ic<1>;
+
+    if (active) {
+        kread(0, kf);
+        attn_lds_wait();
+        qk(0);
+        const bool mask = nvl < 32;  // the last block holds keys past Lk
+        if (nb == 1) {
+            step0(0, I1{}, I1{});
+            step1(I1{}, I1{});
+        } else {
+            step0(0, I1{}, I0{});
+            step1(I0{}, I0{});
+            for (int b = 1; b < nb - 1; ++b) {
+                step0(b, I0{}, I0{});
+                step1(I0{}, I0{});
+            }
+            if (mask) {
+                step0(nb - 1, I0{}, I1{});
+                step1(I1{}, I1{});
+            } else {
+                step0(nb - 1, I0{}, I0{});
+                step1(I1{}, I0{});
+            }
+        }
+        pv(1);  // the last unit's PV
+    } else {  // no queries: keep the DMA and barrier schedule of the workgroup
+        for (int b = 1; b < nb; b += 2) sync_tile((b + 1) / 2);
+        return;
+    }
+
+    // per query block: range check, normalise and store, or the exact fallback (as impl 22)
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+        const float l = lacc[qb][0];
+        float chk = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) chk += o[qb][0][r] * 0.f + o[qb][1][r] * 0.f;
+        const bool ok = l >= LZ_LO && l <= LZ_HI && chk == 0.f;
+        const int q = qbase + 32 * qb + l32;
+        bf16_t* op = (bf16_t*)p.out + ((int64_t)s * pitch + q) * C + h * D;
+        if (__builtin_expect(__all(ok), 1)) {
+            const float inv = 1.f / l;
+            if (q < qend) {
+#pragma unroll
+                for (int db = 0; db < 2; ++db)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g)
+                        *(uint2*)(op + 32 * db + 8 * g + 4 * hf) =
+                            make_uint2(pack_bf16x2(o[qb][db][4 * g] * inv, o[qb][db][4 * g + 1] * inv),
+                                       pack_bf16x2(o[qb][db][4 * g + 2] * inv, o[qb][db][4 * g + 3] * inv));
+            }
+            continue;
+        }
+        float qv[32], acc[32];
+        const int qc = min(q, qend - 1);
+        {
+            const bf16_t* qp = qkv + ((int64_t)s * pitch + qc) * rs + h * D + 32 * hf;
+#pragma unroll
+            for (int i = 0; i < 32; ++i) qv[i] = bf2f(qp[i]) * cexp;
+        }
+        auto score = [&](int kk) {
+            const bf16_t* kp = key_row(kk) + C + h * D + 32 * hf;
+            float d0 = 0.f;
+#pragma unroll
+            for (int i = 0; i < 32; ++i) d0 += qv[i] * bf2f(kp[i]);
+            return d0 + __shfl_xor(d0, 32, 64);
+        };
+        float m = -INFINITY;
+        for (int kk = 0; kk < Lk; ++kk) m = fmaxf(m, score(kk));
+        float lf = 0.f;
+#pragma unroll
+        for (int i = 0; i < 32; ++i) acc[i] = 0.f;
+        for (int kk = 0; kk < Lk; ++kk) {
+            const float e = __builtin_amdgcn_exp2f(score(kk) - m);
+            lf += e;
+            const bf16_t* vp = key_row(kk) + 2 * C + h * D + 32 * hf;
+#pragma unroll
+            for (int i = 0; i < 32; ++i) acc[i] += e * bf2f(vp[i]);
+        }
+        if (q < qend) {
+            const float inv = 1.f / lf;
+#pragma unroll
+            for (int i = 0; i < 32; i += 8)
+                *(u32x4*)(op + 32 * hf + i) = u32x4{pack_bf16x2(acc[i] * inv, acc[i + 1] * inv), pack_bf16x2(acc[i + 2] * inv, acc[i + 3] * inv),
+                                                    pack_bf16x2(acc[i + 4] * inv, acc[i + 5] * inv), pack_bf16x2(acc[i + 6] * inv, acc[i + 7] * inv)};
+        }
+    }
+}
+
 // ---- impl 20: persistent whole-pair kernel (bf16 inference, batched grids) ------------------------
 // The throughput kernels above give each (sequence, head) pair 4-5 query-block workgroups, and each
 // of them streams the pair's whole K / V through its own LDS: 38 tiles of 16 KiB per pair, which
@@ -2169,10 +2507,10 @@ static bool pw_shape_ok(const mmt_attn_params& p) {
 
 template <typename T>
 int launch_attn(const mmt_attn_params& p, hipStream_t st) {
-    if (p.impl != 0 && p.impl != 2 && p.impl != 4 && (p.impl < 8 || p.impl > 12) && (p.impl < 16 || p.impl > 22))
+    if (p.impl != 0 && p.impl != 2 && p.impl != 4 && (p.impl < 8 || p.impl > 12) && (p.impl < 16 || p.impl > 24))
         return MMT_EBADARG;
-    // lse (training forward) is written by impls 0 / 4 / 8 / 16-19 / 21 only: impl 22 never writes it
-    if (p.lse && (sizeof(T) != 2 || p.impl == 9 || (p.impl > 9 && p.impl < 16) || p.impl == 20 || p.impl == 22))
+    // lse (training forward) is written by impls 0 / 4 / 8 / 16-19 / 21 only: impls 22-24 never write it
+    if (p.lse && (sizeof(T) != 2 || p.impl == 9 || (p.impl > 9 && p.impl < 16) || p.impl == 20 || p.impl >= 22))
         return MMT_EBADARG;
     // fp16: the kernels with a running maximum (latency kernel, throughput kernel); the range-checked
     // exponent and 32x32 variants are bf16 A/B kernels, and the training forward (lse) is bf16
@@ -2210,6 +2548,13 @@ int launch_attn(const mmt_attn_params& p, hipStream_t st) {
             else if (p.impl == 18) hipLaunchKernelGGL((mam_attention_lz_kernel<2, 3, false>), fgrid, dim3(256), 0, st, p);
             else if (p.impl == 21) hipLaunchKernelGGL((mam_attention_lz_kernel<3, 3, true, true>), fgrid, dim3(256), 0, st, p);
             else if (p.impl == 22) hipLaunchKernelGGL((mam_attention_lz2_kernel<2>), fgrid, dim3(128), 0, st, p);
+            else if (p.impl == 23 || p.impl == 24) {  // block-pipelined kernel: 24 = 2 waves (128 queries) per WG
+                const int nw = p.impl == 23 ? 4 : 2, qwg = 64 * nw;
+                const int nt = (p.n_t + qwg - 1) / qwg, ns = (p.ntok - p.n_t + qwg - 1) / qwg;
+                const dim3 hgrid(p.q_part == 1 ? nt : p.q_part == 2 ? ns : nt + ns, p.H, p.S);
+                if (nw == 4) hipLaunchKernelGGL((mam_attention_hs_kernel<4>), hgrid, dim3(256), 0, st, p);
+                else hipLaunchKernelGGL((mam_attention_hs_kernel<2>), hgrid, dim3(128), 0, st, p);
+            }
             else hipLaunchKernelGGL((mam_attention_lz_kernel<3, 2, false>), fgrid, dim3(256), 0, st, p);
             return launch_status();
         }

@@ -87,6 +87,14 @@ class MixFormerRGBTRuntime:
             raise ValueError("dtype must be torch.bfloat16, torch.float16 or torch.float32")
         if dtype == torch.float16 and variant == "asym_ce":
             raise NotImplementedError("candidate elimination runs in bf16 / fp32 (its selection kernels have no fp16 form)")
+        if dtype == torch.bfloat16 and variant == "rgb":
+            # the RGB-only MixFormer has no fusion (GroupNorm) between backbone and corner head: its score
+            # maps carry the backbone's scale (logit std ~8.6 on the golden inputs, ~4 effective soft-argmax
+            # positions, against ~2 / hundreds for the RGB-T models), so the bf16 backbone's ~0.5 % token
+            # error alone moves its boxes 1.8e-2 (head in fp32) to 2.7e-2 (bf16 head) -- past the north
+            # star's 1e-2 (profiles/r03_rgb_dtype.jsonl).  fp16 (1.8e-3, same speed) is its 16-bit type.
+            raise ValueError("the RGB-only MixFormer (config 1) runs in fp16 or fp32, not bf16: without the fusion "
+                             "stage its boxes leave the 1e-2 bound in bf16 (use torch.float16, the same speed)")
         self.variant = variant
         # candidate elimination (asym_ce): {block: keep ratio}, lib/config/asymmetric_shared_ce/config.py:23-24
         ce = ce if ce is not None else ((3, 6, 9), (0.7, 0.7, 0.7))

@@ -60,15 +60,16 @@ def _gemm(a, w, M, N, K, bias=None, out_f32=False):
 
 
 class _HipLinear(torch.autograd.Function):
-    """y = x W^T + b (nn.Linear) with bf16 operands; x [M][K] bf16, W [N][K] fp32 master, b [N]."""
+    """y = x W^T + b (nn.Linear) with bf16 operands; x [M][K] bf16, W [N][K] fp32 master, b [N]; y bf16,
+    or fp32 straight from the GEMM's accumulators (out_f32: the residual-stream adds, no cast pass)."""
 
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, out_f32=False):
         M, K = x.shape
         N = w.shape[0]
         x = x.contiguous()
         wb = w.detach().to(torch.bfloat16).contiguous()
-        y = _gemm(x, wb, M, N, K, bias=b.detach().float().contiguous())
+        y = _gemm(x, wb, M, N, K, bias=b.detach().float().contiguous(), out_f32=out_f32)
         ctx.save_for_backward(x, wb)
         return y
 
@@ -82,7 +83,7 @@ class _HipLinear(torch.autograd.Function):
         Mp = (M + 7) // 8 * 8  # contraction over tokens, zero-padded to the GEMM's K granule
         dw = _gemm(_transpose(dy, M, N, Mp), _transpose(x, M, K, Mp), N, K, Mp, out_f32=True)
         db = dy.float().sum(0)
-        return dx, dw, db
+        return dx, dw, db, None
 
 
 class _HipMamAttention(torch.autograd.Function):
@@ -111,8 +112,8 @@ class HipOps:
     dtype = torch.bfloat16  # activation dtype of the GEMM / attention operands
 
     @staticmethod
-    def linear(x, weight, bias):
-        return _HipLinear.apply(x, weight, bias)
+    def linear(x, weight, bias, out_f32=False):
+        return _HipLinear.apply(x, weight, bias, out_f32)
 
     @staticmethod
     def mam_attention(qkv, n_t, heads):
@@ -165,6 +166,14 @@ def _drop_path(x, p, training):
     return x * keep / (1.0 - p)
 
 
+def _patches(x, p=16):
+    """(B, C, H, W) -> (B, (H/p)(W/p), C p p): F.unfold(x, p, stride=p).transpose(1, 2) for non-overlapping
+    patches (channel-major, then kernel row, kernel column; patches row-major), as one copy (aten's
+    unfold launches one im2col kernel per sample)."""
+    B, C, H, W = x.shape
+    return x.view(B, C, H // p, p, W // p, p).permute(0, 2, 4, 1, 3, 5).reshape(B, (H // p) * (W // p), C * p * p)
+
+
 def backbone_forward(bb, t, o, s, ops, drop_path_rate=DROP_PATH_RATE):
     """VisionTransformer.forward (mixformer.py:231-259) for one modality: returns the search
     features (B, C, gs, gs) fp32.  Tokens [template | online | search], pre-LN blocks; in training
@@ -174,23 +183,24 @@ def backbone_forward(bb, t, o, s, ops, drop_path_rate=DROP_PATH_RATE):
     H = C // 64
     gt, gs = bb.grid_size_t, bb.grid_size_s
     ntok, n_t = 2 * gt * gt + gs * gs, 2 * gt * gt
-    patches = torch.cat([F.unfold(x, 16, stride=16).transpose(1, 2) for x in (t, o, s)], 1)  # (B, ntok, 3*256)
+    patches = torch.cat([_patches(x) for x in (t, o, s)], 1)  # (B, ntok, 3*256)
     w = bb.patch_embed.proj.weight
-    x = ops.linear(patches.reshape(B * ntok, -1).to(ops.dtype), w.reshape(w.shape[0], -1), bb.patch_embed.proj.bias)
+    x = ops.linear(patches.reshape(B * ntok, -1).to(ops.dtype), w.reshape(w.shape[0], -1), bb.patch_embed.proj.bias,
+                   out_f32=True)
     pos = torch.cat([bb.pos_embed_t, bb.pos_embed_t, bb.pos_embed_s], 1)
-    x = x.float().view(B, ntok, C) + pos
+    x = x.view(B, ntok, C) + pos
     depth = len(bb.blocks)
     for li, blk in enumerate(bb.blocks):
         dp = drop_path_rate * li / max(depth - 1, 1)
         xn = F.layer_norm(x, (C,), blk.norm1.weight, blk.norm1.bias, 1e-6).to(ops.dtype)
         qkv = ops.linear(xn.view(B * ntok, C), blk.attn.qkv.weight, blk.attn.qkv.bias).view(B, ntok, 3 * C)
         a = ops.mam_attention(qkv, n_t, H).view(B * ntok, C)
-        x = x + _drop_path(ops.linear(a, blk.attn.proj.weight, blk.attn.proj.bias).float().view(B, ntok, C), dp,
+        x = x + _drop_path(ops.linear(a, blk.attn.proj.weight, blk.attn.proj.bias, out_f32=True).view(B, ntok, C), dp,
                            bb.training)
         xn = F.layer_norm(x, (C,), blk.norm2.weight, blk.norm2.bias, 1e-6).to(ops.dtype)
         h = ops.linear(xn.view(B * ntok, C), blk.mlp.fc1.weight, blk.mlp.fc1.bias)
         h = F.gelu(h.float()).to(ops.dtype)
-        x = x + _drop_path(ops.linear(h, blk.mlp.fc2.weight, blk.mlp.fc2.bias).float().view(B, ntok, C), dp,
+        x = x + _drop_path(ops.linear(h, blk.mlp.fc2.weight, blk.mlp.fc2.bias, out_f32=True).view(B, ntok, C), dp,
                            bb.training)
     xs = x[:, n_t:]
     return xs.transpose(1, 2).reshape(B, C, gs, gs)
@@ -207,11 +217,12 @@ def backbone_forward_stacked(bb, t, o, s, ops, asym=False, drop_path_rate=DROP_P
     H = C // 64
     gt, gs = bb.grid_size_t, bb.grid_size_s
     ntok, n_t = 2 * gt * gt + gs * gs, 2 * gt * gt
-    patches = torch.cat([F.unfold(x, 16, stride=16).transpose(1, 2) for x in (t, o, s)], 1)
+    patches = torch.cat([_patches(x) for x in (t, o, s)], 1)
     w = bb.patch_embed.proj.weight
-    x = ops.linear(patches.reshape(B2 * ntok, -1).to(ops.dtype), w.reshape(w.shape[0], -1), bb.patch_embed.proj.bias)
+    x = ops.linear(patches.reshape(B2 * ntok, -1).to(ops.dtype), w.reshape(w.shape[0], -1), bb.patch_embed.proj.bias,
+                   out_f32=True)
     pos = torch.cat([bb.pos_embed_t, bb.pos_embed_t, bb.pos_embed_s], 1)
-    x = x.float().view(B2, ntok, C) + pos
+    x = x.view(B2, ntok, C) + pos
     depth = len(bb.blocks)
 
     def ln2(x, a, b):  # norm*_v on the RGB half, norm*_i on the TIR half
@@ -223,12 +234,12 @@ def backbone_forward_stacked(bb, t, o, s, ops, asym=False, drop_path_rate=DROP_P
         xn = ln2(x, blk.norm1_v, blk.norm1_i)
         qkv = ops.linear(xn.view(B2 * ntok, C), blk.attn.qkv.weight, blk.attn.qkv.bias).view(B2, ntok, 3 * C)
         a = ops.mam_attention_asym(qkv, Bh, n_t, H) if asym else ops.mam_attention(qkv, n_t, H)
-        x = x + _drop_path(ops.linear(a.reshape(B2 * ntok, C), blk.attn.proj.weight, blk.attn.proj.bias).float()
+        x = x + _drop_path(ops.linear(a.reshape(B2 * ntok, C), blk.attn.proj.weight, blk.attn.proj.bias, out_f32=True)
                            .view(B2, ntok, C), dp, bb.training)
         xn = ln2(x, blk.norm2_v, blk.norm2_i)
         h = ops.linear(xn.view(B2 * ntok, C), blk.mlp.fc1.weight, blk.mlp.fc1.bias)
         h = F.gelu(h.float()).to(ops.dtype)
-        x = x + _drop_path(ops.linear(h, blk.mlp.fc2.weight, blk.mlp.fc2.bias).float().view(B2, ntok, C), dp,
+        x = x + _drop_path(ops.linear(h, blk.mlp.fc2.weight, blk.mlp.fc2.bias, out_f32=True).view(B2, ntok, C), dp,
                            bb.training)
     return x[:, n_t:].transpose(1, 2).reshape(B2, C, gs, gs), x[:, :gt * gt]
 
@@ -447,7 +458,10 @@ class TrainStep:
         self.net = net
         self.ops = ops
         self.grad_clip, self.iou_weight, self.l1_weight = grad_clip, iou_weight, l1_weight
-        self.opt = torch.optim.AdamW(param_groups(net, lr), lr=lr, weight_decay=weight_decay)
+        # one fused multi-tensor kernel per parameter group on the device (the foreach form is ~4x the
+        # bytes-bound time of the 190 M-parameter update)
+        fused = next(net.parameters()).is_cuda
+        self.opt = torch.optim.AdamW(param_groups(net, lr), lr=lr, weight_decay=weight_decay, fused=fused or None)
         if ddp and next(net.parameters()).is_cuda:  # train_script_mixformer.py:105
             net = self.net = torch.nn.SyncBatchNorm.convert_sync_batchnorm(net)
         if ddp:

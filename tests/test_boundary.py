@@ -123,3 +123,19 @@ def test_ce_template_mask_validation():
         net(x, x, s, ce_template_mask=bad)
     with pytest.raises(RuntimeError):
         net(x, x, s, ce_template_mask=mask, ce_keep_rate=0.7)
+
+
+def test_rgb_only_refuses_bf16():
+    """The RGB-only MixFormer (config 1) has no fusion between backbone and corner head, so the bf16
+    backbone's token error moves its boxes past the north star's 1e-2 (1.8e-2 with the head in fp32,
+    profiles/r03_rgb_dtype.jsonl): bf16 is refused on the host with an explicit error; the module's
+    16-bit default is fp16."""
+    from mmt_amd import model as M
+    from mmt_amd import synthetic
+    from mmt_amd.runtime import MixFormerRGBTRuntime
+    keys = json.load(open(GOLDEN + "/state_dict_rgb.json"))
+    sd = {k: torch.from_numpy(v) for k, v in synthetic.synth_state_dict(keys).items()}
+    with pytest.raises(ValueError, match="bf16"):
+        MixFormerRGBTRuntime(sd, "rgb", dtype=torch.bfloat16, device="cpu")
+    net = M.build_mixformer_vit(M.hot_path_cfg(search=288), train=False)
+    assert net.compute_dtype == torch.float16

@@ -129,8 +129,9 @@ class _TorchBf16Ops:
     dtype = torch.bfloat16
 
     @staticmethod
-    def linear(x, weight, bias):
-        return torch.nn.functional.linear(x.bfloat16(), weight.bfloat16(), bias.bfloat16())
+    def linear(x, weight, bias, out_f32=False):
+        y = torch.nn.functional.linear(x.bfloat16(), weight.bfloat16(), bias.bfloat16())
+        return y.float() if out_f32 else y
 
     @staticmethod
     def mam_attention(qkv, n_t, heads):

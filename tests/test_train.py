@@ -23,8 +23,9 @@ class TorchOps:
     dtype = torch.float32
 
     @staticmethod
-    def linear(x, weight, bias):
-        return F.linear(x, weight, bias)
+    def linear(x, weight, bias, out_f32=False):
+        y = F.linear(x, weight, bias)
+        return y.float() if out_f32 else y
 
     @staticmethod
     def mam_attention(qkv, n_t, heads):
