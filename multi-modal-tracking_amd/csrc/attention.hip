@@ -6,16 +6,22 @@
 // The qkv Linear output is consumed in place ([seq][token][3][head][64], no permute) and the
 // result is written as [seq][token][head*64], i.e. exactly the proj GEMM's A operand.
 //
-// One workgroup = 64 queries of one (sequence, head): 2 waves x 32 queries (two 16-query MFMA
-// tiles sharing every K/V fragment read) for large grids, or 4 waves x 16 queries when the grid
-// is small (batch-1 tracking) so that more SIMDs get a wave.  Keys stream through a double-buffered
-// LDS ring in 64-key tiles (register-staged: the next tile's global loads are in flight during
-// the current tile's matrix work).  Scores are computed transposed (S^T = K Q^T) so that each
-// lane owns one query column: the online-softmax max/sum/rescale need only two cross-lane
-// shuffles, and the exponentiated scores are already laid out as the B operand of O^T = V^T P^T
-// (no LDS round trip for P).  V^T fragments come from ds_read_b64_tr_b16 on a 160-byte-row V
-// image (bank-conflict-free).  bf16: v_mfma_f32_16x16x32_bf16; fp32: v_mfma_f32_16x16x4_f32.
-// Softmax statistics are fp32 (exp2 with the scale folded in).
+// Kernels (mmt_attn_params.impl; 0 = the library's choice, launch_attn at the end of this file):
+//   fp32 (parity path)  mam_attention_kernel: register-staged K/V ring, v_mfma_f32_16x16x4_f32
+//   impl 4   bf16/fp16 latency kernel (batch-1 tracking): 64 queries x 4 key groups per workgroup,
+//            online softmax with a running maximum, key groups merged through LDS
+//   impl 8   bf16/fp16 throughput kernel with a running maximum (training forward with log-sum-exp,
+//            fp16 batched)
+//   impl 17 / 21 / 22  bf16 range-checked exponent kernels (no reference point, exact fallback):
+//            32 (17 / 21) or 64 (22, the batched default) queries per wave; 21 = 17 with the two key
+//            blocks of a tile software-pipelined
+//   impl 23  (A/B build only, MMT_ATTN_AB) the 64-queries-per-wave kernel as a two-stage pipeline
+//            over (key block, query block) units with a sched_group_barrier issue pattern and
+//            256-query workgroups: bit-identical to 22, measured 6-10 % slower
+// Scores are computed transposed (S^T = K Q^T) so that each lane owns one query column: the softmax
+// statistics need no cross-lane reduction and the exponentiated scores are already laid out as the B
+// operand of O^T = V^T P^T (no LDS round trip for P).  V^T fragments come from ds_read_b64_tr_b16 on
+// a swizzled V image.  Softmax statistics are fp32 (exp2 with the scale folded in).
 #include "common.hpp"
 
 namespace {
@@ -820,225 +826,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 }
 
 
-// ---------------------------------------------------------------------------------------------
-// Throughput kernel on 32x32x16 MFMAs (impl 10-12): same workgroup geometry, DMA ring and softmax
-// tricks as mam_attention_fa_kernel, but each wave's 32 queries are ONE MFMA column block:
-//   S^T[32 keys][32 queries] = K Q^T: 4 v_mfma_f32_32x32x16_bf16 per 32-key block, C = the running
-//     -m broadcast (a persistent 16-register block, rewritten only when the maximum is rebased);
-//   lane l owns query l%32 and 16 keys of the block (rows 8*(r/4) + 4*(l/32) + r%4), so the row
-//     maximum is 32 v_max per 64-key tile + one permlane32 swap (no permlane16 stage), and the row
-//     sum is kept per half-wave and combined once at the end;
-//   O^T[64 d][32 queries] += V^T P^T: 2 d-blocks x 4 16-key steps; the 8 keys a lane contributes to
-//     a step are {4h..4h+3, 8+4h..8+4h+3}, so the V^T operand is two ds_read_b64_tr_b16 (rows base +
-//     qr and base + 8 + qr) and P needs no permlane.
-// Half the MFMA instructions of the 16x16x32 kernel for the same FLOPs (each 32x32x16 holds the
-// SIMD's VALU issue 8 of its 32 cycles instead of 8 of 16), which leaves the VALU for the softmax.
-// Measured SLOWER than impl 8 as compiled (B = 32: 100.5 vs 84.0 us): hipcc copies the -m block
-// into each accumulator (8 v_mov_b64 per block) and drains lgkmcnt(0) right after the first K
-// reads; kept as an A/B variant (parity-tested) for a hand-scheduled version.
 // V image swizzle: chunk c of row r at c ^ (r & 6) ^ ((r & 2) << 1): the 4 rows x 4 chunks a
 // half-wave reads per tr instruction then cover all 64 banks once.
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 MMT_DEV int attn_vswz(int row) { return (row & 6) ^ ((row & 2) << 1); }
 
-template <int FNS, int OCC>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void mam_attention_fa32_kernel(
-    const mmt_attn_params p) {
-    __shared__ __attribute__((aligned(1024))) char lds[FNS * FTILE + FQ * 128];
-    char* qimg = lds + FNS * FTILE;
-
-    const int n_t = p.n_t, ntok = p.ntok, C = p.C;
-    const int64_t pitch = p.tok_pitch > 0 ? p.tok_pitch : ntok;  // rows between sequences
-    const int nqb_t = (n_t + FQ - 1) / FQ;
-    int bx, h, s;
-    attn_block_ids(bx, h, s);
-    const int qb = bx + (p.q_part == 2 ? nqb_t : 0);
-    const bool tmpl = qb < nqb_t;
-    const int q0 = tmpl ? qb * FQ : n_t + (qb - nqb_t) * FQ;
-    const int qend = tmpl ? n_t : ntok;
-    const int Lk = tmpl ? n_t : (p.asym ? ntok + n_t : ntok);
-    const bool cross = p.asym && !tmpl;
-    const int64_t rs = 3 * (int64_t)C;
-    const bf16_t* qkv = (const bf16_t*)p.qkv;
-    const int sV = s % p.Bm, sI = sV + p.Bm;
-
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int l32 = lane & 31, hf = lane >> 5;
-    const int prow = lane >> 3, pcol = lane & 7;
-
-    // ---- K / V DMA (waves 0-1: K, 2-3: V), 4 pieces of 8 rows per wave per tile
-    const int isv = w >> 1;
-    const int64_t col = (isv ? 2 * C : C) + h * D + (isv ? (pcol ^ attn_vswz(prow)) : (pcol ^ prow)) * 8;
-    auto key_row = [&](int kk) -> const bf16_t* {
-        int seq = s, row = kk;
-        if (cross) {
-            if (kk < n_t) seq = sV;
-            else if (kk < 2 * n_t) { seq = sI; row = kk - n_t; }
-            else row = kk - n_t;
-        }
-        return qkv + ((int64_t)seq * pitch + row) * rs;
-    };
-    const bool aligned = n_t % KB == 0;
-    const int nkt = (Lk + KB - 1) / KB;
-    auto issue_tile = [&](int t) {
-        char* slot = lds + (t % FNS) * FTILE + isv * KB * 128;
-        if (aligned && t * KB + KB <= Lk) {
-            const bf16_t* base = key_row(t * KB);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int pk = (w & 1) * 4 + i;
-                attn_glds16(base + (int64_t)(pk * 8 + prow) * rs + col, slot + pk * 1024);
-            }
-        } else {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int pk = (w & 1) * 4 + i;
-                attn_glds16(key_row(min(t * KB + pk * 8 + prow, Lk - 1)) + col, slot + pk * 1024);
-            }
-        }
-    };
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int piece = w * 4 + i, r = piece * 8 + prow;
-        const bf16_t* src = qkv + ((int64_t)s * pitch + min(q0 + r, qend - 1)) * rs + h * D;
-        attn_glds16(src + ((pcol ^ prow) * 8), qimg + piece * 1024);
-    }
-    for (int t = 0; t < FNS - 1 && t < nkt; ++t) issue_tile(t);
-
-    const bool active = q0 + 32 * w < qend;
-    const float cexp = p.scale * 1.4426950408889634f;
-    const bool prescale = fabsf(cexp - 1.f) > 1e-6f;
-    float mr = 0.f, lsum = 0.f;
-    f32x16 o[2], negm;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { o[0][r] = 0.f; o[1][r] = 0.f; negm[r] = 0.f; }
-    u32x4 qf[4];
-    // this lane's K fragment rows (32kb + l32) and V^T read offsets (rows 4*hf + qr (+8), chunk 4db + 2*dsub + pc/2)
-    const int kpos = ((l32 & 7) * 16);
-    const int li = lane & 15, qr = li >> 2, pc = li & 3, dsub = (lane >> 4) & 1;
-
-    for (int kt = 0; kt < nkt; ++kt) {
-        attn_wait_dyn(4 * (min(nkt - 1, kt + FNS - 2) - kt));
-        lds_barrier();
-        if (kt + FNS - 1 < nkt) issue_tile(kt + FNS - 1);
-        if (kt == 0) {
-            const int row = 32 * w + l32;
-#pragma unroll
-            for (int ks = 0; ks < 4; ++ks) {
-                qf[ks] = *(const u32x4*)(qimg + row * 128 + (((2 * ks + hf) ^ (row & 7)) * 16));
-                if (prescale) {
-                    u32x4 v = qf[ks];
-#pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        v[e] = pack_bf16x2(__uint_as_float(v[e] << 16) * cexp, __uint_as_float(v[e] & 0xffff0000u) * cexp);
-                    qf[ks] = v;
-                }
-            }
-        }
-        if (!active) continue;
-        const char* kimg = lds + (kt % FNS) * FTILE;
-        const char* vimg = kimg + KB * 128;
-        f32x16 sacc[2];
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
-            const char* krow = kimg + (32 * kb + l32) * 128;
-            u32x4 kf[4];
-#pragma unroll
-            for (int ks = 0; ks < 4; ++ks) kf[ks] = *(const u32x4*)(krow + ((((2 * ks + hf) * 16) ^ kpos)));
-            sacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kf[0]),
-                                                               __builtin_bit_cast(bf16x8, qf[0]), negm, 0, 0, 0);
-#pragma unroll
-            for (int ks = 1; ks < 4; ++ks)
-                sacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kf[ks]),
-                                                                   __builtin_bit_cast(bf16x8, qf[ks]), sacc[kb], 0, 0, 0);
-        }
-        // V^T fragments, issued behind the QK^T MFMAs
-        uint2 vt[4][2][2];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int row = 16 * j + 4 * hf + qr;
-#pragma unroll
-            for (int db = 0; db < 2; ++db) {
-                const char* b1 = vimg + row * 128 + (((4 * db + 2 * dsub + (pc >> 1)) ^ attn_vswz(row)) * 16) + (pc & 1) * 8;
-                vt[j][db][0] = attn_tr16<0>(b1);
-                vt[j][db][1] = attn_tr16<8 * 128>(b1);
-            }
-        }
-        if (kt * KB + KB > Lk) {
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    if (kt * KB + 32 * kb + 8 * (r >> 2) + 4 * hf + (r & 3) >= Lk) sacc[kb][r] = -1e30f;
-        }
-        float mx = fmaxf(sacc[0][0], sacc[0][1]);
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int r = (kb == 0 ? 2 : 0); r < 16; r += 2) mx = __builtin_fmaxf(mx, __builtin_fmaxf(sacc[kb][r], sacc[kb][r + 1]));
-        {
-            auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-            mx = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
-        }
-        if (kt == 0 || __any(mx > FA_THR)) {
-            const float d = kt == 0 ? mx : fmaxf(mx, 0.f);
-            mr += d;
-            const float alpha = __builtin_amdgcn_exp2f(-d);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                sacc[0][r] -= d;
-                sacc[1][r] -= d;
-                o[0][r] *= alpha;
-                o[1][r] *= alpha;
-                negm[r] = -mr;
-            }
-            lsum *= alpha;
-        }
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                sacc[kb][r] = __builtin_amdgcn_exp2f(sacc[kb][r]);
-                lsum += sacc[kb][r];
-            }
-        attn_lds_wait();
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int kb = j >> 1, rb = 8 * (j & 1);
-            const bf16x8 pf = __builtin_bit_cast(
-                bf16x8, u32x4{pack_bf16x2(sacc[kb][rb], sacc[kb][rb + 1]), pack_bf16x2(sacc[kb][rb + 2], sacc[kb][rb + 3]),
-                              pack_bf16x2(sacc[kb][rb + 4], sacc[kb][rb + 5]), pack_bf16x2(sacc[kb][rb + 6], sacc[kb][rb + 7])});
-#pragma unroll
-            for (int db = 0; db < 2; ++db) {
-                const uint2 ua = vt[j][db][0], ub = vt[j][db][1];
-                const bf16x8 vf = __builtin_bit_cast(bf16x8, make_uint4(ua.x, ua.y, ub.x, ub.y));
-                o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[db], 0, 0, 0);
-            }
-        }
-    }
-
-    if (!active) return;
-    {
-        auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(lsum), __float_as_uint(lsum), false, false);
-        lsum = __uint_as_float(a[0]) + __uint_as_float(a[1]);
-    }
-    const float inv = 1.f / lsum;
-    const int q = q0 + 32 * w + l32;
-    if (q < qend) {
-        if (p.lse && hf == 0) p.lse[((int64_t)s * p.H + h) * ntok + q] = mr + __builtin_amdgcn_logf(lsum);
-        bf16_t* op = (bf16_t*)p.out + ((int64_t)s * pitch + q) * C + h * D;
-#pragma unroll
-        for (int db = 0; db < 2; ++db)
-#pragma unroll
-            for (int g = 0; g < 4; ++g)
-                *(uint2*)(op + 32 * db + 8 * g + 4 * hf) =
-                    make_uint2(pack_bf16x2(o[db][4 * g] * inv, o[db][4 * g + 1] * inv),
-                               pack_bf16x2(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv));
-    }
-}
-
 // ---------------------------------------------------------------------------------------------
-// Range-checked exponent kernel (impl 16-19; the default for large grids).  At d = 64 a score
+// Range-checked exponent kernel (impl 17 / 21; 22 below is its 64-queries-per-wave form).  At d = 64 a score
 // carries only 256 MFMA FLOPs, so the softmax's per-score VALU work decides the rate.  This
 // kernel removes all of it except the exponential and the bf16 pack:
 //   - no running maximum.  softmax(s) = exp2(s) / sum exp2(s) for any common reference point,
@@ -1051,7 +845,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 //   - the row sums come out of the matrix pipe: one v_mfma_f32_16x16x32_bf16 per 16 keys against
 //     a constant 0/1 selector operand (A[m][k] = 1 iff bit 2 of m == bit 3 of k) sums the same
 //     bf16 P fragment that multiplies V, and lands lane l's sum for its own query l%32 in every
-//     element of its accumulator (no cross-lane step).  impl 16/18/19 sum with VALU adds instead;
+//     element of its accumulator (no cross-lane step) (SUM_MFMA = false: VALU adds, A/B only);
 //   - 32x32x16 MFMAs throughout (an MFMA holds the SIMD's vector issue for 8 of its 32 cycles,
 //     against 8 of 16 for the 16x16x32 form), so at most 1/4 of the issue slots go to the matrix
 //     instructions and the rest stay free for v_exp / v_cvt_pk of the co-resident waves.
@@ -1745,6 +1539,10 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
 }
 
+#ifndef MMT_ATTN_AB
+#define MMT_ATTN_AB 0  // A/B build only (tools/build_ablate.sh ab): impl 23
+#endif
+#if MMT_ATTN_AB
 // ---- impl 23: block-pipelined range-checked kernel with a hand-placed issue order ---------------------
 // The same math per 32-key block as impl 17 / 22 (P = exp2(S) with no reference point, row sums on the
 // matrix pipe, epilogue range check with the exact fallback), re-timed so that one wave carries two
@@ -1938,23 +1736,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
             lacc[qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pb, lacc[qb], 0, 0, 0);
         }
     };
-    auto softmax = [&](int qb, bool mask) {  // P = exp2(S) (keys past Lk: 0), packed to bf16
-        if (mask) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float e = __builtin_amdgcn_exp2f(sc[qb][r]);
-                sc[qb][r] = 8 * (r >> 2) + 4 * hf + (r & 3) < nvl ? e : 0.f;
-            }
-        } else {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) sc[qb][r] = __builtin_amdgcn_exp2f(sc[qb][r]);
+    // P = exp2(S) (keys past Lk: 0) of accumulator elements [r0, r1) of query block qb, packed to bf16
+    // (r0, r1 multiples of 2: whole packed pairs)
+    auto softmax = [&](int qb, bool mask, int r0, int r1) {
+        for (int r = r0; r < r1; ++r) {
+            const float e = __builtin_amdgcn_exp2f(sc[qb][r]);
+            sc[qb][r] = !mask || 8 * (r >> 2) + 4 * hf + (r & 3) < nvl ? e : 0.f;
         }
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj) {
-            const int rb = 8 * jj;
-            pf[qb][jj] = u32x4{pack_bf16x2(sc[qb][rb], sc[qb][rb + 1]), pack_bf16x2(sc[qb][rb + 2], sc[qb][rb + 3]),
-                               pack_bf16x2(sc[qb][rb + 4], sc[qb][rb + 5]), pack_bf16x2(sc[qb][rb + 6], sc[qb][rb + 7])};
-        }
+        for (int r = r0; r < r1; r += 2) pf[qb][r >> 3][(r & 7) >> 1] = pack_bf16x2(sc[qb][r], sc[qb][r + 1]);
     };
     // the issue pattern of one step: MFMAs each followed by 2 exponentials and 1 pack / select, the
     // last ones bare (the ~24 issue cycles per 32x32x16 gap of MI355X_MICROARCH.md)
@@ -1967,29 +1756,46 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
             }
         }
     };
-    // step (b, 0): PV(b - 1, 1), QK^T(b, 1), softmax(b, 0); reads V(b), K(b + 1)
+    // an empty asm that takes query block qb's packed P: its exponentials and packs are computed inside
+    // the step's scheduling region (hipcc otherwise sinks them into the next basic block, out of reach
+    // of the region's sched_group_barrier pattern)
+    auto pin = [&](int qb) { asm volatile("" : "+v"(pf[qb][0]), "+v"(pf[qb][1])); };
+    // step (b, 0): PV(b - 1, 1), QK^T(b, 1), softmax(b, 0); reads V(b)
     auto step0 = [&](int b, auto FIRSTc, auto MASKc) {
         constexpr bool FIRST = decltype(FIRSTc)::value, MASK = decltype(MASKc)::value;
-        attn_lds_wait();  // K(b) / V(b - 1) fragments (the sched barrier keeps their consumers below)
+        attn_lds_wait();  // V(b - 1) fragments (the sched barrier keeps their consumers below)
         if constexpr (!FIRST) pv(1);
         vread(b, vt);  // the previous V^T fragments are consumed by the MFMAs above
         qk(1);
-        softmax(0, MASK);
+        softmax(0, MASK, 0, 16);
         interleave(FIRST ? 4 : 10);
+        pin(0);
         __builtin_amdgcn_sched_barrier(0);
-        if (b + 1 < nb) {
+    };
+    // step (b, 1): PV(b, 0), QK^T(b + 1, 0), softmax(b, 1); reads K(b + 1) at its start (after the
+    // sync point of a new tile), waited for just before the QK^T MFMAs that need them (the six PV /
+    // row-sum MFMAs cover the read latency)
+    auto step1 = [&](int b, auto LASTc, auto MASKc) {
+        constexpr bool LAST = decltype(LASTc)::value, MASK = decltype(MASKc)::value;
+        if constexpr (!LAST) {
             if (b & 1) sync_tile((b + 1) / 2);  // first reads of tile (b + 1) / 2
             kread(b + 1, kf);
         }
-    };
-    // step (b, 1): PV(b, 0), QK^T(b + 1, 0), softmax(b, 1)
-    auto step1 = [&](auto LASTc, auto MASKc) {
-        constexpr bool LAST = decltype(LASTc)::value, MASK = decltype(MASKc)::value;
-        attn_lds_wait();  // V(b), K(b + 1)
+        // V(b) (read in step (b, 0)): every LDS read but the four K reads just issued (LDS reads
+        // return in order)
+        if constexpr (!LAST) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
         pv(0);
+        softmax(1, MASK, 0, 12);
+        interleave(6);
+        pin(1);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (!LAST) attn_lds_wait();  // K(b + 1)
         if constexpr (!LAST) qk(0);
-        softmax(1, MASK);
-        interleave(LAST ? 6 : 10);
+        softmax(1, MASK, 12, 16);
+        if constexpr (!LAST) interleave(4);
+        pin(1);
         __builtin_amdgcn_sched_barrier(0);
     };
     using I0 = attn_ic<0>;
@@ -2002,20 +1808,20 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
         const bool mask = nvl < 32;  // the last block holds keys past Lk
         if (nb == 1) {
             step0(0, I1{}, I1{});
-            step1(I1{}, I1{});
+            step1(0, I1{}, I1{});
         } else {
             step0(0, I1{}, I0{});
-            step1(I0{}, I0{});
+            step1(0, I0{}, I0{});
             for (int b = 1; b < nb - 1; ++b) {
                 step0(b, I0{}, I0{});
-                step1(I0{}, I0{});
+                step1(b, I0{}, I0{});
             }
             if (mask) {
                 step0(nb - 1, I0{}, I1{});
-                step1(I1{}, I1{});
+                step1(nb - 1, I1{}, I1{});
             } else {
                 step0(nb - 1, I0{}, I0{});
-                step1(I1{}, I0{});
+                step1(nb - 1, I1{}, I0{});
             }
         }
         pv(1);  // the last unit's PV
@@ -2082,439 +1888,21 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
         }
     }
 }
-
-// ---- impl 20: persistent whole-pair kernel (bf16 inference, batched grids) ------------------------
-// The throughput kernels above give each (sequence, head) pair 4-5 query-block workgroups, and each
-// of them streams the pair's whole K / V through its own LDS: 38 tiles of 16 KiB per pair, which
-// at batch 32 is ~530 MB of L2 -> LDS fill (~60 GB/s per CU) and bounds them at ~40 us.  Here one
-// workgroup of 16 waves owns a whole pair, so K / V pass through LDS once (9 tiles), and the
-// workgroup is persistent over pairs (pair blockIdx.x + k * gridDim.x) so that the next pair's
-// template, Q and first key tiles stream in behind the current pair's last steps.
-//   waves 0 .. nsb-1: one 32-query search block each (wave nsb-1 may be half full);
-//   waves nsb .. 15 : the template blocks (n_t / 32 of them, dealt round-robin), each over the
-//                     pair's ntt template tiles, which stay resident in their own LDS slots (the
-//                     template keys are the first keys every query sees);
-//   K / V of the rest of the key stream (asym: the other modality's template; then the search
-//   tokens) flows through a PW_NR-slot ring, one tile per step, one 1-KiB LDS-DMA piece per wave.
-// Math per 32-key block is the range-checked exponent kernel's (impl 17: P = exp2(S) with a final
-// range check and an exact fallback, row sums on the matrix pipe).  No stores are in flight while a
-// wave waits on its counted DMA pieces: template outputs are parked (bf16) in LDS and written out
-// with the search outputs at the end of the pair, and the next pair starts with vmcnt(0).
-// LDS: template K / V 32 KiB + template Q 16 KiB + parked outputs 16 KiB + ring 6 x 16 KiB = 160 KiB.
-// Shape limits (host-checked): n_t % 64 == 0, n_t <= 128, search blocks <= 15, template steps <
-// steps per pair (ViT-B 128 / 320: 13 search waves, 3 template waves, 9 steps; asym 11).
-constexpr int PW_NW = 16, PW_NR = 6;
-constexpr int PW_TKV = 2 * FTILE, PW_TQ = 128 * 128, PW_PARK = 4 * 32 * 128;
-constexpr int PW_LDS = PW_TKV + PW_TQ + PW_PARK + PW_NR * FTILE;
-
-template <int NT, int NTOK, int NH, bool ASYM>  // shape-specialised: every count below is a constant
-__global__ __launch_bounds__(1024) void mam_attention_pw_kernel(const mmt_attn_params p) {
-    __shared__ __attribute__((aligned(1024))) char lds[PW_LDS];
-    char* const tkv = lds;
-    char* const tq = lds + PW_TKV;
-    char* const park = tq + PW_TQ;
-    char* const ring = park + PW_PARK;
-
-    constexpr int n_t = NT, ntok = NTOK, H = NH, C = NH * D;
-    const int64_t pitch = p.tok_pitch > 0 ? p.tok_pitch : ntok;
-    constexpr int64_t rs = 3 * C;
-    const bf16_t* qkv = (const bf16_t*)p.qkv;
-    constexpr int nsr = ntok - n_t;                 // search tokens (queries, and keys)
-    constexpr int nsb = (nsr + 31) / 32;            // search waves
-    constexpr int ntw = PW_NW - nsb;                // template waves
-    constexpr int ntb = n_t / 32, ntt = n_t / KB;   // template blocks / tiles
-    constexpr int nrs = (nsr + KB - 1) / KB;        // search key tiles
-    constexpr int nro = ASYM ? ntt : 0;             // other modality's template tiles (asym)
-    constexpr int nring = nro + nrs, nsteps = ntt + nring;
-    constexpr int tsteps = ((ntb + ntw - 1) / ntw) * ntt;  // template waves' steps
-    constexpr int tail = nsr - (nrs - 1) * KB;      // valid keys of the last ring tile
-    static_assert(n_t % KB == 0 && ntt <= 2 && ntw > 0 && tsteps < nsteps, "pw shape");
-    const int npairs = H * p.S, G = gridDim.x;
-    const int npk = (npairs - (int)blockIdx.x + G - 1) / G;
-    const int gtot = npk * nring;
-
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar registers
-    // the lane id, made opaque to the compiler at every step (pw_opaque): every lane-derived offset
-    // is then recomputed inside the step (a few VALU) instead of being hoisted out of the loops and
-    // spilled -- 1024-thread workgroups leave 128 VGPRs, and each scratch reload drains vmcnt(0),
-    // i.e. the whole DMA ring
-    int ln = threadIdx.x & 63;
-    auto pw_opaque = [&]() { asm volatile("" : "+v"(ln)); };
-    const bool srch = w < nsb;
-    const int tw = w - nsb;
-
-    auto pair_sh = [&](int k, int& s, int& h) {
-        const int pr = (int)blockIdx.x + k * G;
-        h = pr % H;
-        s = pr / H;
-    };
-    // ---- DMA: ring tile g (pair g / nring) -> slot g % PW_NR, wave w = piece w (K: 0-7, V: 8-15).
-    // The issue pointer's pair (is_k -> is_s, is_h) and tile within the pair (is_r) advance
-    // incrementally (no divisions per tile).
-    const int isv = w >> 3, pk = w & 7;
-    int is_k = 0, is_r = 0, is_s, is_h;
-    pair_sh(0, is_s, is_h);
-    auto issue_ring = [&](int g) {
-        const int prow = ln >> 3, pcol = ln & 7;
-        const int64_t colo = (isv ? 2 * C : C) + (isv ? (pcol ^ attn_vswz(prow)) : (pcol ^ prow)) * 8;
-        const int r = is_r, s = is_s, h = is_h;
-        if (++is_r == nring) {
-            is_r = 0;
-            pair_sh(++is_k, is_s, is_h);
-        }
-        int seq = s, tok;
-        const int row = pk * 8 + prow;
-        if (r < nro) {
-            seq = s < p.Bm ? s + p.Bm : s - p.Bm;
-            tok = r * KB + row;
-        } else {
-            tok = min(n_t + (r - nro) * KB + row, ntok - 1);
-        }
-        attn_glds16(qkv + ((int64_t)seq * pitch + tok) * rs + h * D + colo,
-                    ring + (g % PW_NR) * FTILE + isv * KB * 128 + pk * 1024);
-    };
-    // template K / V (own template, ntt tiles) and template Q of pair k
-    auto issue_tmpl = [&](int k) {
-        const int prow = ln >> 3, pcol = ln & 7;
-        int s, h;
-        pair_sh(k, s, h);
-        const bf16_t* base = qkv + (int64_t)s * pitch * rs + h * D;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int piece = w + PW_NW * i;
-            if (piece < 16 * ntt) {
-                const int tt = piece >> 4, iv = (piece >> 3) & 1, pp = piece & 7;
-                const int64_t c = (iv ? 2 * C : C) + (iv ? (pcol ^ attn_vswz(prow)) : (pcol ^ prow)) * 8;
-                attn_glds16(base + (int64_t)(tt * KB + pp * 8 + prow) * rs + c, tkv + tt * FTILE + iv * KB * 128 + pp * 1024);
-            }
-        }
-        if (w < n_t / 8) attn_glds16(base + (int64_t)(w * 8 + prow) * rs + (pcol ^ prow) * 8, tq + w * 1024);
-    };
-
-    const float cexp = p.scale * 1.4426950408889634f;
-    const bool prescale = fabsf(cexp - 1.f) > 1e-6f;
-    u32x4 qf[4];  // B operand of S^T = K Q^T: query l32, d = 16ks + 8hf .. +7
-    auto scale_q = [&]() {
-        if (prescale) {
-#pragma unroll
-            for (int ks = 0; ks < 4; ++ks) {
-                u32x4 v = qf[ks];
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    v[e] = pack_bf16x2(__uint_as_float(v[e] << 16) * cexp, __uint_as_float(v[e] & 0xffff0000u) * cexp);
-                qf[ks] = v;
-            }
-        }
-    };
-    // search waves: this wave's 32 query rows of pair k, straight to registers.  Inline asm: a
-    // compiler-visible load still pending on the pair loop's back edge makes hipcc put vmcnt(0)
-    // (the whole DMA ring) in front of every tile's first Q use; the wait below (q_wait, at the
-    // pair's first step) redefines qf, so nothing reads it before the loads land.
-    auto load_q = [&](int k) {
-        int s, h;
-        pair_sh(k, s, h);
-        const int q = min(n_t + 32 * w + (ln & 31), ntok - 1);
-        const bf16_t* src = qkv + ((int64_t)s * pitch + q) * rs + h * D + 8 * (ln >> 5);
-        asm volatile("global_load_dwordx4 %0, %4, off\n\t"
-                     "global_load_dwordx4 %1, %4, off offset:32\n\t"
-                     "global_load_dwordx4 %2, %4, off offset:64\n\t"
-                     "global_load_dwordx4 %3, %4, off offset:96"
-                     : "=&v"(qf[0]), "=&v"(qf[1]), "=&v"(qf[2]), "=&v"(qf[3])
-                     : "v"(src)
-                     : "memory");
-    };
-    auto q_wait = [&]() {  // vmcnt(0): Q, template and every earlier piece (no stores in flight after it)
-        asm volatile("s_waitcnt vmcnt(0)" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3])::"memory");
-    };
-
-    f32x16 o[2];
-    f32x4 lacc;
-    auto zero_acc = [&]() {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) { o[0][r] = 0.f; o[1][r] = 0.f; }
-        lacc = f32x4{0.f, 0.f, 0.f, 0.f};
-    };
-    // one 32-key block kb of a tile (impl 17's block): NJ 16-key steps, MASK = zero P from key nv on
-    auto block = [&](const char* kimg, int kb, int nv, auto NJc, auto MASKc) {
-        constexpr int NJ = decltype(NJc)::value;
-        constexpr bool MASK = decltype(MASKc)::value;
-        const int l32 = ln & 31, hf = ln >> 5, kpos = (l32 & 7) * 16;
-        const int li = ln & 15, qr = li >> 2, pc = li & 3, dsub = (ln >> 4) & 1;
-        const float one_or_zero = ((li >> 2) & 1) == dsub ? 1.f : 0.f;
-        const uint32_t sel_w = pack_bf16x2(one_or_zero, one_or_zero);
-        const bf16x8 sel = __builtin_bit_cast(bf16x8, u32x4{sel_w, sel_w, sel_w, sel_w});
-        const char* vimg = kimg + KB * 128;
-        const char* krow = kimg + (32 * kb + l32) * 128;
-        f32x16 sacc;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
-#pragma unroll
-        for (int kh = 0; kh < 2; ++kh) {  // K fragments two at a time (registers)
-            u32x4 kf[2];
-#pragma unroll
-            for (int i = 0; i < 2; ++i) kf[i] = *(const u32x4*)(krow + ((((4 * kh + 2 * i + hf) * 16) ^ kpos)));
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-                sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kf[i]),
-                                                               __builtin_bit_cast(bf16x8, qf[2 * kh + i]), sacc, 0, 0, 0);
-        }
-#pragma unroll
-        for (int r = 0; r < 8 * NJ; ++r) {
-            float e = MMT_ATTN_ABLATE == 3 ? sacc[r] : __builtin_amdgcn_exp2f(sacc[r]);
-            if constexpr (MASK) {
-                if (32 * kb + 8 * (r >> 2) + 4 * hf + (r & 3) >= nv) e = 0.f;
-            }
-            sacc[r] = e;
-        }
-        // V^T fragments after the exponentials (not live across them: register budget); the
-        // other waves of the SIMD cover the read latency
-        uint2 vt[NJ][2][2];
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const int row = 32 * kb + 16 * j + 4 * hf + qr;
-#pragma unroll
-            for (int db = 0; db < 2; ++db) {
-                const char* b1 = vimg + row * 128 + (((4 * db + 2 * dsub + (pc >> 1)) ^ attn_vswz(row)) * 16) + (pc & 1) * 8;
-                vt[j][db][0] = attn_tr16<0>(b1);
-                vt[j][db][1] = attn_tr16<8 * 128>(b1);
-            }
-        }
-        attn_lds_wait();
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const int rb = 8 * j;
-            const bf16x8 pf = __builtin_bit_cast(
-                bf16x8, u32x4{pack_bf16x2(sacc[rb], sacc[rb + 1]), pack_bf16x2(sacc[rb + 2], sacc[rb + 3]),
-                              pack_bf16x2(sacc[rb + 4], sacc[rb + 5]), pack_bf16x2(sacc[rb + 6], sacc[rb + 7])});
-#pragma unroll
-            for (int db = 0; db < 2; ++db) {
-                const uint2 ua = vt[j][db][0], ub = vt[j][db][1];
-                const bf16x8 vf = __builtin_bit_cast(bf16x8, make_uint4(ua.x, ua.y, ub.x, ub.y));
-                o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[db], 0, 0, 0);
-            }
-            lacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pf, lacc, 0, 0, 0);
-        }
-    };
-    // the two 32-key blocks of a tile are fenced from each other: overlapping them doubles the
-    // working set past the 128 registers
-    auto full_tile = [&](const char* kimg) {
-        __builtin_amdgcn_sched_barrier(0);
-        block(kimg, 0, KB, attn_ic<2>{}, attn_ic<0>{});
-        __builtin_amdgcn_sched_barrier(0);
-        block(kimg, 1, KB, attn_ic<2>{}, attn_ic<0>{});
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    auto tail_tile = [&](const char* kimg, int nv) {  // one masked instantiation (last step only)
-        for (int kb = 0; kb < 2; ++kb)
-            if (32 * kb < nv) block(kimg, kb, nv, attn_ic<2>{}, attn_ic<1>{});
-    };
-
-    // exact two-pass fp32 softmax for query qc of (s, h) over Lk keys (cross: the asym search key
-    // order [template_V | template_I | search_s]); lane half hf owns d = 32hf .. 32hf+31.  Rare.
-    auto fallback = [&](int s, int h, int qc, int Lk, bool cross, float* acc) {
-        const int hf = ln >> 5;
-        const int sV = s % max(p.Bm, 1), sI = sV + p.Bm;
-        auto key_row = [&](int kk) -> const bf16_t* {
-            int seq = s, row = kk;
-            if (cross) {
-                if (kk < n_t) seq = sV;
-                else if (kk < 2 * n_t) { seq = sI; row = kk - n_t; }
-                else row = kk - n_t;
-            }
-            return qkv + ((int64_t)seq * pitch + row) * rs + h * D + 32 * hf;
-        };
-        float qv[32];
-        const bf16_t* qp = qkv + ((int64_t)s * pitch + qc) * rs + h * D + 32 * hf;
-#pragma unroll
-        for (int i = 0; i < 32; ++i) qv[i] = bf2f(qp[i]) * cexp;
-        auto score = [&](int kk) {
-            const bf16_t* kp = key_row(kk) + C;
-            float d0 = 0.f;
-#pragma unroll
-            for (int i = 0; i < 32; ++i) d0 += qv[i] * bf2f(kp[i]);
-            return d0 + __shfl_xor(d0, 32, 64);
-        };
-        float m = -INFINITY;
-        for (int kk = 0; kk < Lk; ++kk) m = fmaxf(m, score(kk));
-        float lf = 0.f;
-#pragma unroll
-        for (int i = 0; i < 32; ++i) acc[i] = 0.f;
-        for (int kk = 0; kk < Lk; ++kk) {
-            const float e = __builtin_amdgcn_exp2f(score(kk) - m);
-            lf += e;
-            const bf16_t* vp = key_row(kk) + 2 * C;
-#pragma unroll
-            for (int i = 0; i < 32; ++i) acc[i] += e * bf2f(vp[i]);
-        }
-        const float inv = 1.f / lf;
-#pragma unroll
-        for (int i = 0; i < 32; ++i) acc[i] *= inv;
-    };
-    // finished block: normalised bf16 rows (lane: query l32, d = 32db + 8g + 4hf .. +3) into dst
-    // (row pitch dpitch elements), or the fallback's rows (lane: d = 32hf .. +31)
-    typedef __attribute__((address_space(3))) uint64_t lds_u64;
-    typedef __attribute__((address_space(3))) u32x4 lds_u4;
-    auto finish = [&](auto TOc, bf16_t* dst, int64_t dpitch, bool valid, int s, int h, int qc, int Lk, bool cross) {
-        constexpr bool TO_LDS = decltype(TOc)::value != 0;  // parked template rows: ds_write, not flat
-        const float l = lacc[0];
-        float chk = 0.f;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) chk += o[0][r] * 0.f + o[1][r] * 0.f;
-        const bool ok = (l >= LZ_LO && l <= LZ_HI && chk == 0.f) || MMT_ATTN_ABLATE != 0;
-        const int l32 = ln & 31, hf = ln >> 5;
-        bf16_t* op = dst + (int64_t)l32 * dpitch;
-        if (__builtin_expect(__all(ok), 1)) {
-            const float inv = 1.f / l;
-            if (valid) {
-#pragma unroll
-                for (int db = 0; db < 2; ++db)
-#pragma unroll
-                    for (int g = 0; g < 4; ++g)
-                    {
-                        const uint2 v = make_uint2(pack_bf16x2(o[db][4 * g] * inv, o[db][4 * g + 1] * inv),
-                                                   pack_bf16x2(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv));
-                        if constexpr (TO_LDS) *(lds_u64*)(op + 32 * db + 8 * g + 4 * hf) = ((uint64_t)v.y << 32) | v.x;
-                        else *(uint2*)(op + 32 * db + 8 * g + 4 * hf) = v;
-                    }
-            }
-            return;
-        }
-        float acc[32];
-        fallback(s, h, qc, Lk, cross, acc);
-        if (valid) {
-#pragma unroll
-            for (int i = 0; i < 32; i += 8)
-            {
-                const u32x4 v = u32x4{pack_bf16x2(acc[i], acc[i + 1]), pack_bf16x2(acc[i + 2], acc[i + 3]),
-                                      pack_bf16x2(acc[i + 4], acc[i + 5]), pack_bf16x2(acc[i + 6], acc[i + 7])};
-                if constexpr (TO_LDS) *(lds_u4*)(op + 32 * hf + i) = v;
-                else *(u32x4*)(op + 32 * hf + i) = v;
-            }
-        }
-    };
-
-    // ---- prologue: pair 0's template and Q, the first PW_NR - 1 ring tiles
-    // stamps (measurement builds, search wave 0): 0 entry; pair 0: 1 / 2 / 3 / 4 = after the barrier of
-    // steps 0 / 1 / 4 / nsteps - 1, 5 = its last tile computed, 6 = its rows stored; 7 = last pair done
-    MMT_ASTAMP(0, "s_memtime");
-    issue_tmpl(0);
-    int gi = 0, gc = 0;  // ring tiles issued / consumed (uniform)
-    for (; gi < PW_NR - 1 && gi < gtot; ++gi) issue_ring(gi);
-    if (srch) load_q(0);
-
-    // step u of pair k, common to both roles (every wave executes the same barrier sequence): wait
-    // for this wave's pieces of the step's tile, barrier, refill the slot the previous step freed
-    auto step_sync = [&](int k, int u) {
-        pw_opaque();
-        if (u >= ntt) attn_wait_dyn(gi - 1 - gc);
-        lds_barrier();
-        if ((u == 0 && k > 0) || u > ntt) {
-            if (MMT_ATTN_ABLATE != 1 && gi < gtot) issue_ring(gi);
-            gi = min(gi + 1, gtot);
-        }
-        if (u == tsteps && k + 1 < npk) issue_tmpl(k + 1);
-    };
-    auto tmpl_wait = [&]() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
-
-    if (srch) {  // ---- search waves: one 32-query block per pair, all nsteps tiles
-#pragma unroll 1
-        for (int k = 0; k < npk; ++k) {
-            int s, h;
-            pair_sh(k, s, h);
-            zero_acc();
-            q_wait();  // Q, template and every earlier piece (no stores in flight after it)
-            constexpr int nfull = tail < KB ? nsteps - 1 : nsteps;  // the partial last tile after the loop
-#pragma unroll 1
-            for (int u = 0; u < nfull; ++u) {
-                step_sync(k, u);
-                if (k == 0) {
-                    if (u == 0) { MMT_ASTAMP(1, "s_memtime"); }
-                    else if (u == 1) { MMT_ASTAMP(2, "s_memtime"); }
-                    else if (u == 4) { MMT_ASTAMP(3, "s_memtime"); }
-                }
-                if (u == 0) scale_q();
-                if (MMT_ATTN_ABLATE != 2) full_tile(u < ntt ? tkv + u * FTILE : ring + (gc % PW_NR) * FTILE);
-                if (u >= ntt) ++gc;
-            }
-            if constexpr (nfull < nsteps) {
-                step_sync(k, nsteps - 1);
-                if (k == 0) { MMT_ASTAMP(4, "s_memtime"); }
-                if (MMT_ATTN_ABLATE != 2) tail_tile(ring + (gc % PW_NR) * FTILE, tail);
-                ++gc;
-            }
-            if (k == 0) { MMT_ASTAMP(5, "s_memtime"); }
-            if (k + 1 < npk) load_q(k + 1);  // the next pair's Q behind this pair's output stores
-            const int l32 = ln & 31, q = n_t + 32 * w + l32;
-            finish(attn_ic<0>{}, (bf16_t*)p.out + ((int64_t)s * pitch + n_t + 32 * w) * C + h * D, C, q < ntok, s, h,
-                          min(q, ntok - 1), ASYM ? ntok + n_t : ntok, ASYM);
-            if (k == 0) { MMT_ASTAMP(6, "s_memtime"); }
-            if (k == npk - 1) { MMT_ASTAMP(7, "s_memtime"); }
-        }
-    } else {  // ---- template waves: template blocks tw, tw + ntw, .. over the resident template tiles
-#pragma unroll 1
-        for (int k = 0; k < npk; ++k) {
-            int s, h;
-            pair_sh(k, s, h);
-            tmpl_wait();
-#pragma unroll 1
-            for (int u = 0; u < nsteps; ++u) {
-                step_sync(k, u);
-                if (u < tsteps) {
-                    const int bi = u / ntt, tu = u - bi * ntt, blk = tw + ntw * bi;
-                    if (blk < ntb) {
-                        if (tu == 0) {
-                            const int row = 32 * blk + (ln & 31), hf = ln >> 5;
-#pragma unroll
-                            for (int ks = 0; ks < 4; ++ks) qf[ks] = *(const u32x4*)(tq + row * 128 + (((2 * ks + hf) ^ (row & 7)) * 16));
-                            scale_q();
-                            zero_acc();
-                        }
-                        if (MMT_ATTN_ABLATE != 2) full_tile(tkv + tu * FTILE);
-                        if (tu == ntt - 1)  // rows parked in LDS until the pair's end
-                            finish(attn_ic<1>{}, (bf16_t*)(park + blk * 32 * 128), 64, true, s, h, 32 * blk + (ln & 31), n_t, false);
-                    }
-                }
-                if (u >= ntt) ++gc;
-            }
-            // parked rows to the output (the pair's only template stores)
-            bf16_t* out = (bf16_t*)p.out + (int64_t)s * pitch * C + h * D;
-            const int l32 = ln & 31, hf = ln >> 5;
-            for (int blk = tw; blk < ntb; blk += ntw) {
-                const char* pr = park + blk * 32 * 128 + l32 * 128;
-                bf16_t* op = out + (int64_t)(32 * blk + l32) * C;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) *(u32x4*)(op + 32 * hf + 8 * i) = *(const u32x4*)(pr + 64 * hf + 16 * i);
-            }
-        }
-    }
-}
-
-static int attn_cu_count() {
-    static int n = 0;
-    if (n <= 0) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-            n = 256;
-    }
-    return n;
-}
-
-// impl 20 applies to: bf16, no lse, all queries, the instantiated shapes (ViT-B 128 / 320: n_t 128,
-// 528 tokens, 12 heads; joint or asym key streams)
-static bool pw_shape_ok(const mmt_attn_params& p) {
-    return !p.lse && p.q_part == 0 && p.n_t == 128 && p.ntok == 528 && p.H == 12 && p.C == 12 * D;
-}
+#endif  // MMT_ATTN_AB
 
 template <typename T>
 int launch_attn(const mmt_attn_params& p, hipStream_t st) {
-    if (p.impl != 0 && p.impl != 2 && p.impl != 4 && (p.impl < 8 || p.impl > 12) && (p.impl < 16 || p.impl > 24))
+    // impl: 0 = the library's choice by dtype and grid size; forced (A/B and tests): 4 = latency kernel,
+    // 8 = running-maximum throughput kernel, 17 / 21 / 22 = range-checked exponent kernels (22 = 64
+    // queries per wave); A/B build: 23 = the block-pipelined form of 22 with 256-query workgroups
+    if (p.impl != 0 && p.impl != 4 && p.impl != 8 && p.impl != 17 && p.impl != 21 && p.impl != 22 &&
+        !(MMT_ATTN_AB && p.impl == 23))
         return MMT_EBADARG;
-    // lse (training forward) is written by impls 0 / 4 / 8 / 16-19 / 21 only: impls 22-24 never write it
-    if (p.lse && (sizeof(T) != 2 || p.impl == 9 || (p.impl > 9 && p.impl < 16) || p.impl == 20 || p.impl >= 22))
-        return MMT_EBADARG;
+    // lse (training forward) is written by impls 0 / 4 / 8 / 17 / 21 only: impls 22 / 23 never write it
+    if (p.lse && (sizeof(T) != 2 || p.impl >= 22)) return MMT_EBADARG;
     // fp16: the kernels with a running maximum (latency kernel, throughput kernel); the range-checked
-    // exponent and 32x32 variants are bf16 A/B kernels, and the training forward (lse) is bf16
-    if (__is_same(T, f16_t) && (p.lse || p.impl >= 10)) return MMT_EBADARG;
+    // exponent kernels are bf16, and the training forward (lse) is bf16
+    if (__is_same(T, f16_t) && (p.lse || p.impl >= 17)) return MMT_EBADARG;
     if (!p.qkv || !p.out || p.H <= 0 || p.C != p.H * D || p.S <= 0 || p.ntok <= p.n_t || p.n_t <= 0) return MMT_EBADARG;
     if (p.tok_pitch != 0 && (p.tok_pitch < p.ntok || p.lse)) return MMT_EBADARG;
     if (p.asym && (p.Bm <= 0 || p.S != 2 * p.Bm)) return MMT_EBADARG;
@@ -2528,65 +1916,34 @@ int launch_attn(const mmt_attn_params& p, hipStream_t st) {
     const int nqb = qblocks(64);
     dim3 grid(nqb, p.H, p.S);
     if constexpr (sizeof(T) == 2) {
-        // large grids: the throughput kernel (128 queries per workgroup, 2 workgroups per CU);
-        // small grids (batch-1 tracking): the latency kernel (64 queries x KG key groups)
         const int nfa = qblocks(FQ);
         const dim3 fgrid(nfa, p.H, p.S);
-        if (!__is_same(T, bf16_t)) {  // fp16: no A/B variants (rejected above)
-        } else if (p.impl == 20) {  // persistent whole-pair kernel: one workgroup per CU, pairs strided
-            if (!pw_shape_ok(p)) return MMT_EBADARG;
-            const int npairs = p.H * p.S;
-            const dim3 g(min(npairs, attn_cu_count()));
-            if (p.asym) hipLaunchKernelGGL((mam_attention_pw_kernel<128, 528, 12, true>), g, dim3(1024), 0, st, p);
-            else hipLaunchKernelGGL((mam_attention_pw_kernel<128, 528, 12, false>), g, dim3(1024), 0, st, p);
-            return launch_status();
-        } else if (p.impl >= 16) {  // range-checked exponent kernel (A/B): 16 = VALU row sums, ring 3, 3 WG/CU;
-                             // 17 = MFMA row sums; 18 = ring 2; 19 = 2 WG/CU; 21 / 22 = 17 with the
-                             // two blocks of a tile software-pipelined
-            if (p.impl == 16) hipLaunchKernelGGL((mam_attention_lz_kernel<3, 3, false>), fgrid, dim3(256), 0, st, p);
-            else if (p.impl == 17) hipLaunchKernelGGL((mam_attention_lz_kernel<3, 3, true>), fgrid, dim3(256), 0, st, p);
-            else if (p.impl == 18) hipLaunchKernelGGL((mam_attention_lz_kernel<2, 3, false>), fgrid, dim3(256), 0, st, p);
-            else if (p.impl == 21) hipLaunchKernelGGL((mam_attention_lz_kernel<3, 3, true, true>), fgrid, dim3(256), 0, st, p);
-            else if (p.impl == 22) hipLaunchKernelGGL((mam_attention_lz2_kernel<2>), fgrid, dim3(128), 0, st, p);
-            else if (p.impl == 23 || p.impl == 24) {  // block-pipelined kernel: 24 = 2 waves (128 queries) per WG
-                const int nw = p.impl == 23 ? 4 : 2, qwg = 64 * nw;
-                const int nt = (p.n_t + qwg - 1) / qwg, ns = (p.ntok - p.n_t + qwg - 1) / qwg;
-                const dim3 hgrid(p.q_part == 1 ? nt : p.q_part == 2 ? ns : nt + ns, p.H, p.S);
-                if (nw == 4) hipLaunchKernelGGL((mam_attention_hs_kernel<4>), hgrid, dim3(256), 0, st, p);
-                else hipLaunchKernelGGL((mam_attention_hs_kernel<2>), hgrid, dim3(128), 0, st, p);
-            }
-            else hipLaunchKernelGGL((mam_attention_lz_kernel<3, 2, false>), fgrid, dim3(256), 0, st, p);
-            return launch_status();
+        const bool bf = __is_same(T, bf16_t);
+        int impl = p.impl;
+        if (impl == 0) {
+            // large grids, bf16 inference: the range-checked exponent kernel, 64 queries per wave from
+            // MMT_ATTN_LZ2_MIN_WG workgroups (impl 22), else with its two blocks per tile software-
+            // pipelined (impl 21; B = 8 / 32: 27.2 / 78.9 us against 29.8 / 83.8 for impl 17 and 30-34 /
+            // 84-93 for impl 8, profiles/r02_attn_ab.jsonl, r02_pipe_ab.jsonl); the training forward
+            // (lse) and fp16 keep the running-maximum throughput kernel; small grids (batch-1 tracking):
+            // the latency kernel (64 queries x 4 key groups)
+            const int64_t wg = (int64_t)nfa * p.H * p.S;
+            if (bf && !p.lse && wg >= MMT_ATTN_LZ2_MIN_WG) impl = 22;
+            else if (bf && !p.lse && wg >= MMT_ATTN_FA_MIN_WG) impl = 21;
+            else if (p.lse || wg >= MMT_ATTN_FA_MIN_WG) impl = 8;
+            else impl = 4;
         }
-        // large grids, bf16 inference: the range-checked exponent kernel, 64 queries per wave from
-        // MMT_ATTN_LZ2_MIN_WG workgroups (impl 22), else with its two blocks per tile software-
-        // pipelined (impl 21; B = 8 / 32: 27.2 / 78.9 us against 29.8 / 83.8 for impl 17 and 30-34 /
-        // 84-93 for impl 8, profiles/r02_attn_ab.jsonl, r02_pipe_ab.jsonl); the training forward
-        // (lse) and fp16 keep the running-maximum throughput kernel
-        if (p.impl == 0 && !p.lse && __is_same(T, bf16_t) && (int64_t)nfa * p.H * p.S >= MMT_ATTN_LZ2_MIN_WG) {
-            hipLaunchKernelGGL((mam_attention_lz2_kernel<2>), fgrid, dim3(128), 0, st, p);
-            return launch_status();
+        if (impl == 17) hipLaunchKernelGGL((mam_attention_lz_kernel<3, 3, true>), fgrid, dim3(256), 0, st, p);
+        else if (impl == 21) hipLaunchKernelGGL((mam_attention_lz_kernel<3, 3, true, true>), fgrid, dim3(256), 0, st, p);
+        else if (impl == 22) hipLaunchKernelGGL((mam_attention_lz2_kernel<2>), fgrid, dim3(128), 0, st, p);
+#if MMT_ATTN_AB
+        else if (impl == 23) {  // block-pipelined kernel, 4 waves (256 queries) per workgroup
+            const int nt = (p.n_t + 255) / 256, ns = (p.ntok - p.n_t + 255) / 256;
+            const dim3 hgrid(p.q_part == 1 ? nt : p.q_part == 2 ? ns : nt + ns, p.H, p.S);
+            hipLaunchKernelGGL((mam_attention_hs_kernel<4>), hgrid, dim3(256), 0, st, p);
         }
-        if (p.impl == 0 && !p.lse && __is_same(T, bf16_t) && (int64_t)nfa * p.H * p.S >= MMT_ATTN_FA_MIN_WG) {
-            hipLaunchKernelGGL((mam_attention_lz_kernel<3, 3, true, true>), fgrid, dim3(256), 0, st, p);
-            return launch_status();
-        }
-        if (p.impl == 8 || p.lse || (p.impl == 0 && (int64_t)nfa * p.H * p.S >= MMT_ATTN_FA_MIN_WG)) {
-            hipLaunchKernelGGL((mam_attention_fa_kernel<T, 2, 3>), fgrid, dim3(256), 0, st, p);
-            return launch_status();
-        }
-        if (p.impl == 9) {  // ring-depth / occupancy variant (A/B): 3-deep ring, 2 workgroups per CU
-            hipLaunchKernelGGL((mam_attention_fa_kernel<T, 3, 2>), fgrid, dim3(256), 0, st, p);
-            return launch_status();
-        }
-        if (p.impl >= 10 && __is_same(T, bf16_t)) {  // 32x32x16 throughput kernel (A/B): 10 = ring 2 / 2 WG per CU, 11 = 3 / 2, 12 = 2 / 3
-            if (p.impl == 10) hipLaunchKernelGGL((mam_attention_fa32_kernel<2, 2>), fgrid, dim3(256), 0, st, p);
-            else if (p.impl == 11) hipLaunchKernelGGL((mam_attention_fa32_kernel<3, 2>), fgrid, dim3(256), 0, st, p);
-            else hipLaunchKernelGGL((mam_attention_fa32_kernel<2, 3>), fgrid, dim3(256), 0, st, p);
-            return launch_status();
-        }
-        const int kg = p.impl > 0 ? p.impl : 4;
-        if (kg == 2) hipLaunchKernelGGL((mam_attention_glds_kernel<T, 2>), grid, dim3(512), 0, st, p);
+#endif
+        else if (impl == 8 || p.lse) hipLaunchKernelGGL((mam_attention_fa_kernel<T, 2, 3>), fgrid, dim3(256), 0, st, p);
         else hipLaunchKernelGGL((mam_attention_glds_kernel<T, 4>), grid, dim3(1024), 0, st, p);
     } else {  // fp32 (parity path); small grids: 4 waves x 16 queries to occupy more SIMDs
         if ((int64_t)nqb * p.H * p.S < 1024) hipLaunchKernelGGL((mam_attention_kernel<T, 1>), grid, dim3(256), 0, st, p);

@@ -82,7 +82,7 @@ class _HipLinear(torch.autograd.Function):
         dx = _gemm(dy, _transpose(wb, N, K), M, K, N) if ctx.needs_input_grad[0] else None
         Mp = (M + 7) // 8 * 8  # contraction over tokens, zero-padded to the GEMM's K granule
         dw = _gemm(_transpose(dy, M, N, Mp), _transpose(x, M, K, Mp), N, K, Mp, out_f32=True)
-        db = dy.float().sum(0)
+        db = dy.sum(0, dtype=torch.float32)  # one reduction over the bf16 gradient (no fp32 copy)
         return dx, dw, db, None
 
 
@@ -199,7 +199,7 @@ def backbone_forward(bb, t, o, s, ops, drop_path_rate=DROP_PATH_RATE):
                            bb.training)
         xn = F.layer_norm(x, (C,), blk.norm2.weight, blk.norm2.bias, 1e-6).to(ops.dtype)
         h = ops.linear(xn.view(B * ntok, C), blk.mlp.fc1.weight, blk.mlp.fc1.bias)
-        h = F.gelu(h.float()).to(ops.dtype)
+        h = F.gelu(h) if h.dtype == ops.dtype else F.gelu(h.float()).to(ops.dtype)  # bf16 in/out, fp32 math
         x = x + _drop_path(ops.linear(h, blk.mlp.fc2.weight, blk.mlp.fc2.bias, out_f32=True).view(B, ntok, C), dp,
                            bb.training)
     xs = x[:, n_t:]
@@ -238,7 +238,7 @@ def backbone_forward_stacked(bb, t, o, s, ops, asym=False, drop_path_rate=DROP_P
                            .view(B2, ntok, C), dp, bb.training)
         xn = ln2(x, blk.norm2_v, blk.norm2_i)
         h = ops.linear(xn.view(B2 * ntok, C), blk.mlp.fc1.weight, blk.mlp.fc1.bias)
-        h = F.gelu(h.float()).to(ops.dtype)
+        h = F.gelu(h) if h.dtype == ops.dtype else F.gelu(h.float()).to(ops.dtype)  # bf16 in/out, fp32 math
         x = x + _drop_path(ops.linear(h, blk.mlp.fc2.weight, blk.mlp.fc2.bias, out_f32=True).view(B2, ntok, C), dp,
                            bb.training)
     return x[:, n_t:].transpose(1, 2).reshape(B2, C, gs, gs), x[:, :gt * gt]

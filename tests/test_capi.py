@@ -77,24 +77,25 @@ def test_bad_arguments_rejected_without_gpu_work():
                                         _lib.MMT_BF16, None) == -10000
 
 
-def test_persistent_pair_attention_shape_gate():
-    """impl 20 (persistent whole-pair MAM kernel) is instantiated for the ViT-B 128/320 shape only; any
-    other shape, the training forward (lse), fp16 or a query part is rejected on the host."""
+def test_attention_impl_and_lse_gate():
+    """mmt_mam_attention takes impl 0 (library choice), 4, 8, 17, 21, 22 only (the round-2 A/B-only
+    kernels 2, 9-12, 16, 18-20 are no longer in the library; 23 is in the A/B build only); impls 22 / 23
+    never write the log-sum-exp
+    the training backward consumes, so lse with them is rejected; fp16 takes the running-maximum kernels
+    only.  Every case fails validation on the host, before a launch."""
     from mmt_amd import _lib
-    fake = 1 << 20  # 16-B aligned, never dereferenced: every case fails validation before a launch
+    fake = 1 << 20  # 16-B aligned, never dereferenced
 
     def attn(dt=_lib.MMT_BF16, **kw):
         a = _lib.AttnParams()
-        a.qkv, a.out, a.S, a.Bm, a.ntok, a.n_t, a.H, a.C, a.scale, a.impl = fake, fake, 2, 1, 528, 128, 12, 768, 0.125, 20
+        a.qkv, a.out, a.S, a.Bm, a.ntok, a.n_t, a.H, a.C, a.scale = fake, fake, 2, 1, 528, 128, 12, 768, 0.125
         for k, v in kw.items():
             setattr(a, k, v)
         return _lib.LIB.mmt_mam_attention(ctypes.byref(a), dt, None)
 
-    assert attn(ntok=864, n_t=288, H=16, C=1024) == -10000  # ViT-L shape
-    assert attn(H=4, C=256) == -10000
-    assert attn(q_part=2) == -10000
-    assert attn(lse=fake) == -10000
-    assert attn(dt=_lib.MMT_F16) == -10000
-    assert attn(impl=99) == -10000
-    # impl 22 never writes the log-sum-exp the training backward consumes: lse with impl 22 is rejected
+    for impl in (2, 9, 10, 11, 12, 16, 18, 19, 20, 23, 24, 99):
+        assert attn(impl=impl) == -10000, impl
     assert attn(impl=22, lse=fake) == -10000
+    assert attn(impl=23, lse=fake) == -10000
+    assert attn(dt=_lib.MMT_F16, impl=17) == -10000
+    assert attn(dt=_lib.MMT_F16, lse=fake) == -10000

@@ -466,11 +466,11 @@ def _attn_ref(qkv, S, Bm, ntok, n_t, C, H, asym):
     return out.permute(0, 2, 1, 3).reshape(S, ntok, C)
 
 
-ATTN_BF16_IMPLS = [2, 4, 8, 9, 10, 11, 12, 16, 17, 18, 19, 21, 22, 23, 24]
+ATTN_BF16_IMPLS = [4, 8, 17, 21, 22]
 
 
 @pytest.mark.parametrize("dname,impl", [("f32", 0), ("bf16", 0)] + [("bf16", i) for i in ATTN_BF16_IMPLS]
-                         + [("fp16", i) for i in (0, 2, 4, 8, 9)])
+                         + [("fp16", i) for i in (0, 4, 8)])
 @pytest.mark.parametrize("asym", [0, 1])
 @pytest.mark.parametrize("Bm,ntok,n_t,H", [(1, 528, 128, 12), (2, 100, 36, 2), (1, 70, 8, 1), (1, 864, 288, 2)])
 def test_mam_attention(dname, impl, asym, Bm, ntok, n_t, H):
@@ -495,7 +495,7 @@ def test_mam_attention(dname, impl, asym, Bm, ntok, n_t, H):
 
 
 @pytest.mark.parametrize("dname,impl", [("f32", 0), ("bf16", 0)] + [("bf16", i) for i in ATTN_BF16_IMPLS]
-                         + [("fp16", i) for i in (0, 2, 4, 8, 9)])
+                         + [("fp16", i) for i in (0, 4, 8)])
 def test_mam_attention_rescale_branch(dname, impl):
     """Online-softmax rescale forced: one key per query block carries a huge score in a late tile
     (bf16: and in a different key group than the first tile, so the group merge rescales)."""
@@ -517,7 +517,7 @@ def test_mam_attention_rescale_branch(dname, impl):
     assert (out.float().cpu() - ref).abs().max().item() < (1.5e-2 if dt != torch.float32 else 5e-5)
 
 
-@pytest.mark.parametrize("impl", [0, 2, 4, 8, 9, 10, 12, 16, 17, 18, 19, 21, 22, 23, 24])
+@pytest.mark.parametrize("impl", [0, 4, 8, 17, 21, 22])
 @pytest.mark.parametrize("asym", [0, 1])
 def test_mam_attention_prescaled_q(impl, asym):
     """The runtime's convention (bf16): q arrives multiplied by scale * log2(e) (folded into the qkv
@@ -544,7 +544,7 @@ def test_mam_attention_prescaled_q(impl, asym):
     assert err <= 1.5e-2, err
 
 
-@pytest.mark.parametrize("impl", [0, 4, 8, 16, 17, 21, 22, 23, 24])
+@pytest.mark.parametrize("impl", [0, 4, 8, 17, 21, 22])
 @pytest.mark.parametrize("asym", [0, 1])
 def test_mam_attention_extreme_scores(impl, asym):
     """Scores far outside the fp32 exponent range of exp2 without a reference point: a key that
@@ -586,7 +586,7 @@ def test_mam_attention_pipelined_is_default_and_bitwise(asym):
     qkv[..., :C] *= 0.125 * 1.4426950408889634  # the runtime's pre-scaled q
     qd = qkv.bfloat16().cuda()
     outs = {}
-    for impl in (17, 21, 22, 23, 24, 0):
+    for impl in (17, 21, 22, 0):
         out = torch.empty(S, ntok, C, device="cuda", dtype=torch.bfloat16)
         p = L.AttnParams()
         p.qkv, p.out, p.S, p.Bm, p.ntok, p.n_t, p.C, p.H, p.asym = qd.data_ptr(), out.data_ptr(), S, Bm, ntok, n_t, C, H, asym
@@ -597,9 +597,6 @@ def test_mam_attention_pipelined_is_default_and_bitwise(asym):
     assert torch.equal(outs[17], outs[21])
     assert torch.equal(outs[17], outs[22])
     assert torch.equal(outs[22], outs[0])
-    # impl 23 / 24 (block-pipelined, 256 / 128 queries per workgroup): the same MFMAs and exponentials per
-    # query in the same accumulation order (the masked keys of the last block add exact zeros)
-    assert torch.equal(outs[22], outs[23]) and torch.equal(outs[22], outs[24])
     qr = qkv.bfloat16().float()
     qr[..., :C] /= 0.125 * 1.4426950408889634
     # every sequence (joint and cross-modal asymmetric key streams) against the fp32 reference at
@@ -607,59 +604,6 @@ def test_mam_attention_pipelined_is_default_and_bitwise(asym):
     ref = _attn_ref(qr, S, Bm, ntok, n_t, C, H, asym)
     err = (outs[0].float().cpu() - ref).abs().max().item()
     assert err <= 1.5e-2, err
-
-
-@pytest.mark.parametrize("asym", [0, 1])
-@pytest.mark.parametrize("Bm,pitch,case", [(1, 0, "plain"), (5, 0, "prescaled"), (32, 0, "prescaled"), (3, 560, "plain"),
-                                           (2, 0, "extreme")])
-def test_mam_attention_persistent_pair(asym, Bm, pitch, case):
-    """impl 20, the persistent whole-pair kernel (ViT-B 128/320 shape: 528 tokens, 128 template, 12
-    heads): grids of 24 / 120 / 768 / 72 / 48 (sequence, head) pairs -- 768 puts three pairs on each
-    workgroup of a 256-CU chip, i.e. the template / Q / key-ring hand-off between pairs; a token pitch
-    above ntok (rows past ntok must stay untouched); q pre-multiplied by scale * log2(e) as the runtime
-    passes it; and scores outside the fp32 range of the unreferenced exponent (fallback path, a search
-    and a template query)."""
-    L = _lib()
-    ntok, n_t, H = 528, 128, 12
-    S, C = 2 * Bm, 64 * H
-    P = pitch or ntok
-    g = torch.Generator().manual_seed(31 + Bm + asym)
-    qkv = torch.randn(S, P, 3 * C, generator=g) * (0.5 if case == "extreme" else 1.0)
-    if case == "extreme":
-        qkv[:, 500, C:2 * C] = qkv[:, 300, :C] * 60
-        qkv[:, 310, :C] *= 40
-        qkv[:, 40, :C] *= 40
-    qs = qkv.clone()
-    c = 0.125 * 1.4426950408889634
-    if case == "prescaled":
-        qs[..., :C] *= c
-    qd = qs.bfloat16().cuda()
-    out = torch.full((S, P, C), float("nan"), device="cuda", dtype=torch.bfloat16)
-    p = L.AttnParams()
-    p.qkv, p.out, p.S, p.Bm, p.ntok, p.n_t, p.C, p.H, p.asym = qd.data_ptr(), out.data_ptr(), S, Bm, ntok, n_t, C, H, asym
-    p.scale = 1.0 / 1.4426950408889634 if case == "prescaled" else 0.125
-    p.tok_pitch, p.impl = pitch, 20
-    L.check(L.LIB.mmt_mam_attention(p, L.MMT_BF16, torch.cuda.current_stream().cuda_stream), "attn")
-    torch.cuda.synchronize()
-    qr = qs[:, :ntok].bfloat16().double()
-    if case == "prescaled":
-        qr[..., :C] /= c
-    ref = _attn_ref(qr, S, Bm, ntok, n_t, C, H, asym).float()
-    o = out[:, :ntok].float().cpu()
-    assert torch.isfinite(o).all()
-    err = (o - ref).abs().max().item()
-    if case == "extreme":  # the bound of test_mam_attention_extreme_scores, and no worse than impl 17
-        out17 = torch.full_like(out, float("nan"))
-        p.out, p.impl = out17.data_ptr(), 17
-        L.check(L.LIB.mmt_mam_attention(p, L.MMT_BF16, torch.cuda.current_stream().cuda_stream), "attn")
-        torch.cuda.synchronize()
-        err17 = (out17[:, :ntok].float().cpu() - ref).abs().max().item()
-        assert err <= 2.5e-2 * max(1.0, ref.abs().max().item()), (err, err17)
-        assert err <= 1.25 * err17 + 4e-3, (err, err17)
-    else:
-        assert err <= 1.5e-2, err
-    if pitch:
-        assert torch.isnan(out[:, ntok:].float()).all()
 
 
 @pytest.mark.parametrize("dname", ["f32", "bf16", "fp16"])

@@ -6,6 +6,7 @@
 #            softmax work / without exponentials / without exponentials and bf16 packing
 #            (MMT_ATTN_ABLATE=1/2/3/4)
 #   stamp:   per-phase workgroup timestamps in the GEMM / attention kernels (MMT_STAMP_BUILD=1)
+#   ab:      the product plus the A/B-only attention kernel impl 23 (MMT_ATTN_AB=1)
 # Use with MMT_HIP_LIB=multi-modal-tracking_amd/mmt_amd/_lib/<variant>/libmmt_hip.so.
 set -e
 ONLY=${1:-}
@@ -22,3 +23,4 @@ build aab1 -DMMT_ATTN_ABLATE=1
 build aab2 -DMMT_ATTN_ABLATE=2
 build aab3 -DMMT_ATTN_ABLATE=3
 build aab4 -DMMT_ATTN_ABLATE=4
+build ab -DMMT_ATTN_AB=1
