@@ -33,13 +33,16 @@ def _stream():
     return torch.cuda.current_stream().cuda_stream
 
 
-def _transpose(x, rows, cols, ld_out=None):
+def _transpose(x, rows, cols, ld_out=None, ones_row=False):
     """[rows][cols] bf16 -> [cols][ld_out] (mmt_transpose_bf16); columns rows..ld_out-1 are zero
-    (the GEMM's K must be a multiple of 8)."""
+    (the GEMM's K must be a multiple of 8).  ones_row: 8 more rows, the first all ones over the
+    `rows` columns (so a GEMM against it also yields the row sums of its other operand), the rest zero."""
     from ._lib import LIB, check
     ld_out = ld_out or rows
-    alloc = torch.empty if ld_out == rows else torch.zeros
-    out = alloc(cols, ld_out, device=x.device, dtype=torch.bfloat16)
+    alloc = torch.empty if ld_out == rows and not ones_row else torch.zeros
+    out = alloc(cols + (8 if ones_row else 0), ld_out, device=x.device, dtype=torch.bfloat16)
+    if ones_row:
+        out[cols, :rows] = 1.0
     check(LIB.mmt_transpose_bf16(x.data_ptr(), out.data_ptr(), rows, cols, cols, ld_out, 1, 0, 0, _stream()),
           "mmt_transpose_bf16")
     return out
@@ -81,9 +84,10 @@ class _HipLinear(torch.autograd.Function):
         dy = dy.to(torch.bfloat16).contiguous()
         dx = _gemm(dy, _transpose(wb, N, K), M, K, N) if ctx.needs_input_grad[0] else None
         Mp = (M + 7) // 8 * 8  # contraction over tokens, zero-padded to the GEMM's K granule
-        dw = _gemm(_transpose(dy, M, N, Mp), _transpose(x, M, K, Mp), N, K, Mp, out_f32=True)
-        db = dy.sum(0, dtype=torch.float32)  # one reduction over the bf16 gradient (no fp32 copy)
-        return dx, dw, db, None
+        # dW and the bias gradient from one GEMM: x^T carries an extra row of ones, so output column
+        # K of dy^T [x | 1] is sum_m dy[m][n] (the same bf16 dy, fp32 accumulation; no reduce kernel)
+        dwb = _gemm(_transpose(dy, M, N, Mp), _transpose(x, M, K, Mp, ones_row=True), N, K + 8, Mp, out_f32=True)
+        return dx, dwb[:, :K].contiguous(), dwb[:, K].contiguous(), None
 
 
 class _HipMamAttention(torch.autograd.Function):
@@ -158,12 +162,14 @@ def asym_attention_from_mam(mam, qkv, Bh, n_t, heads):
 DROP_PATH_RATE = 0.1  # get_mixformer_vit drop_path_rate (mixformer.py:311, :324); timm linear per-block schedule
 
 
-def _drop_path(x, p, training):
-    """timm DropPath: per-sample stochastic depth, survivors scaled by 1/(1-p)."""
+def _residual(x, y, p, training):
+    """x + DropPath(y) (timm DropPath in mixformer.py:136-139: per-sample stochastic depth, survivors
+    scaled by 1/(1-p)) as one fused multiply-add per element (torch.addcmul with the per-sample keep /
+    (1 - p) scale) instead of three elementwise passes."""
     if not training or p <= 0.0:
-        return x
-    keep = x.new_empty((x.shape[0],) + (1,) * (x.dim() - 1)).bernoulli_(1.0 - p)
-    return x * keep / (1.0 - p)
+        return x + y
+    keep = y.new_empty((y.shape[0],) + (1,) * (y.dim() - 1)).bernoulli_(1.0 - p)
+    return torch.addcmul(x, y, keep.div_(1.0 - p))
 
 
 def _patches(x, p=16):
@@ -195,13 +201,13 @@ def backbone_forward(bb, t, o, s, ops, drop_path_rate=DROP_PATH_RATE):
         xn = F.layer_norm(x, (C,), blk.norm1.weight, blk.norm1.bias, 1e-6).to(ops.dtype)
         qkv = ops.linear(xn.view(B * ntok, C), blk.attn.qkv.weight, blk.attn.qkv.bias).view(B, ntok, 3 * C)
         a = ops.mam_attention(qkv, n_t, H).view(B * ntok, C)
-        x = x + _drop_path(ops.linear(a, blk.attn.proj.weight, blk.attn.proj.bias, out_f32=True).view(B, ntok, C), dp,
-                           bb.training)
+        x = _residual(x, ops.linear(a, blk.attn.proj.weight, blk.attn.proj.bias, out_f32=True).view(B, ntok, C), dp,
+                      bb.training)
         xn = F.layer_norm(x, (C,), blk.norm2.weight, blk.norm2.bias, 1e-6).to(ops.dtype)
         h = ops.linear(xn.view(B * ntok, C), blk.mlp.fc1.weight, blk.mlp.fc1.bias)
         h = F.gelu(h) if h.dtype == ops.dtype else F.gelu(h.float()).to(ops.dtype)  # bf16 in/out, fp32 math
-        x = x + _drop_path(ops.linear(h, blk.mlp.fc2.weight, blk.mlp.fc2.bias, out_f32=True).view(B, ntok, C), dp,
-                           bb.training)
+        x = _residual(x, ops.linear(h, blk.mlp.fc2.weight, blk.mlp.fc2.bias, out_f32=True).view(B, ntok, C), dp,
+                      bb.training)
     xs = x[:, n_t:]
     return xs.transpose(1, 2).reshape(B, C, gs, gs)
 
@@ -234,13 +240,13 @@ def backbone_forward_stacked(bb, t, o, s, ops, asym=False, drop_path_rate=DROP_P
         xn = ln2(x, blk.norm1_v, blk.norm1_i)
         qkv = ops.linear(xn.view(B2 * ntok, C), blk.attn.qkv.weight, blk.attn.qkv.bias).view(B2, ntok, 3 * C)
         a = ops.mam_attention_asym(qkv, Bh, n_t, H) if asym else ops.mam_attention(qkv, n_t, H)
-        x = x + _drop_path(ops.linear(a.reshape(B2 * ntok, C), blk.attn.proj.weight, blk.attn.proj.bias, out_f32=True)
-                           .view(B2, ntok, C), dp, bb.training)
+        x = _residual(x, ops.linear(a.reshape(B2 * ntok, C), blk.attn.proj.weight, blk.attn.proj.bias, out_f32=True)
+                      .view(B2, ntok, C), dp, bb.training)
         xn = ln2(x, blk.norm2_v, blk.norm2_i)
         h = ops.linear(xn.view(B2 * ntok, C), blk.mlp.fc1.weight, blk.mlp.fc1.bias)
         h = F.gelu(h) if h.dtype == ops.dtype else F.gelu(h.float()).to(ops.dtype)  # bf16 in/out, fp32 math
-        x = x + _drop_path(ops.linear(h, blk.mlp.fc2.weight, blk.mlp.fc2.bias, out_f32=True).view(B2, ntok, C), dp,
-                           bb.training)
+        x = _residual(x, ops.linear(h, blk.mlp.fc2.weight, blk.mlp.fc2.bias, out_f32=True).view(B2, ntok, C), dp,
+                      bb.training)
     return x[:, n_t:].transpose(1, 2).reshape(B2, C, gs, gs), x[:, :gt * gt]
 
 
