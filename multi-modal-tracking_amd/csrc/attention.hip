@@ -22,7 +22,23 @@
 // statistics need no cross-lane reduction and the exponentiated scores are already laid out as the B
 // operand of O^T = V^T P^T (no LDS round trip for P).  V^T fragments come from ds_read_b64_tr_b16 on
 // a swizzled V image.  Softmax statistics are fp32 (exp2 with the scale folded in).
+//
+// Counted-wait rule (the round-2 impl 20-25 illegal-address fault): on gfx9-class
+// hardware vmcnt counts vector-memory STORES as well as loads, so no kernel below issues a global
+// store between an LDS-DMA issue and the counted s_waitcnt vmcnt(n) that covers it (outputs are
+// written after the key loop's last counted wait).  Every DMA'd key tile index is in [0, nkt);
+// building with -DMMT_ATTN_CHECK=1 turns that into a device assert (MMT_ATTN_ASSERT).
 #include "common.hpp"
+
+#ifndef MMT_ATTN_CHECK
+#define MMT_ATTN_CHECK 0
+#endif
+#if MMT_ATTN_CHECK
+#include <cassert>
+#define MMT_ATTN_ASSERT(c) assert(c)
+#else
+#define MMT_ATTN_ASSERT(c) ((void)0)
+#endif
 
 namespace {
 
@@ -408,6 +424,7 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(KG, KG
     const int nkt = (Lk + KB - 1) / KB, nr = (nkt + KG - 1) / KG;
     // Tile t into slot t % NS: its 16 pieces (8 K, 8 V) are dealt over the waves (piece w + i*NWV).
     auto issue_tile = [&](int t) {
+        MMT_ATTN_ASSERT(t >= 0 && t < nkt);
         char* slot = lds + (t % NS) * ATILE;
 #pragma unroll
         for (int i = 0; i < (16 + NWV - 1) / NWV; ++i) {
@@ -659,6 +676,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     const bool aligned = n_t % KB == 0;  // every tile lies in one key segment
     const int nkt = (Lk + KB - 1) / KB;
     auto issue_tile = [&](int t) {
+        MMT_ATTN_ASSERT(t >= 0 && t < nkt);
         char* slot = lds + (t % FNS) * FTILE + isv * KB * 128;
         if (aligned && t * KB + KB <= Lk) {
             const T* base = key_row(t * KB);  // wave-uniform
@@ -924,6 +942,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     const bool aligned = n_t % KB == 0;  // every full tile lies in one key segment
     const int nkt = (Lk + KB - 1) / KB;
     auto issue_tile = [&](int t) {
+        MMT_ATTN_ASSERT(t >= 0 && t < nkt);
         char* slot = lds + (t % FNS) * FTILE + isv * KB * 128;
         if (aligned && t * KB + KB <= Lk) {
             const bf16_t* base = key_row(t * KB);  // wave-uniform
@@ -1252,6 +1271,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const bool aligned = n_t % KB == 0;
     const int nkt = (Lk + KB - 1) / KB;
     auto issue_tile = [&](int t) {
+        MMT_ATTN_ASSERT(t >= 0 && t < nkt);
         char* slot = lds + (t % FNS) * FTILE + isv * KB * 128;
         if (aligned && t * KB + KB <= Lk) {
             const bf16_t* base = key_row(t * KB);
@@ -1603,6 +1623,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const int isv = (w * NP) >> 3;  // wave-uniform: a wave's pieces are all K or all V
     const int64_t col = (isv ? 2 * C : C) + h * D + (isv ? (pcol ^ attn_vswz(prow)) : (pcol ^ prow)) * 8;
     auto issue_tile = [&](int t) {
+        MMT_ATTN_ASSERT(t >= 0 && t < nkt);
         char* slot = lds + (t % R) * FTILE + isv * KB * 128;
         if (aligned && t * KB + KB <= Lk) {
             const bf16_t* base = key_row(t * KB);  // wave-uniform
