@@ -95,7 +95,22 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
     MMT_STAMP(1, "s_memtime");
 
     const int tiles_m = (p.M + BM - 1) / BM;
-    const int tm = tile % tiles_m, tn = tile / tiles_m;
+    // Tile order.  Grids of one or two rounds (batch 1): row tiles fastest, so the workgroups of one
+    // XCD share its W column slice.  Larger grids: row groups of GM tiles, column tiles next, so
+    // the ~32 workgroups an XCD holds at a time cover GM row panels x every column tile and each A
+    // panel / W slice is fetched into that XCD's L2 once and re-read from it (instead of the A
+    // panels streaming in again from the Infinity Cache for every column tile).
+    constexpr int GM = 8;
+    int tm, tn;
+    if (gridDim.x * gridDim.y * gridDim.z > 512 && tiles_m > GM) {
+        const int tiles_n = ntiles / tiles_m, grp = tile / (GM * tiles_n), first = grp * GM;
+        const int gsz = min(tiles_m - first, GM), r = tile - grp * GM * tiles_n;
+        tm = first + r % gsz;
+        tn = r / gsz;
+    } else {
+        tm = tile % tiles_m;
+        tn = tile / tiles_m;
+    }
     constexpr bool LNF = LNM != 0;  // LayerNorm folded: 1 = row statistics from the A fragments, 2 = handed in
     const int m0 = tm * BM, n0 = tn * BN;
     const int lane = threadIdx.x & 63, kg = threadIdx.x / TPG;
@@ -660,9 +675,11 @@ bool glds_takes(const mmt_gemm_params& p) {
 // bound: 128x128 (32 KiB/step) ~0.52 us, 128x64 with 2 k-groups ~0.52 us per pair of
 // steps, 64x64 with 2 k-groups ~0.33 us per pair.  A K split into n slices adds the partial
 // tile round trip of the last-arriving slice (~0.8 us + 0.5 us per 64 KiB slab it reads).
+// Large-M tiles (impl 5 / 6: 256x128 / 128x256, 8 waves with 64x64 wave tiles, 3-slot ring of
+// 48 KiB stages): 1.5x the MFMA work per byte of LDS fill of 128x128, for grids of many rounds.
 struct Cand { int cfg, bm, bn, ks; float fixed_us, step_us; };
-constexpr Cand kCands[4] = {{1, 128, 128, 1, 6.0f, 0.52f}, {2, 128, 64, 2, 5.0f, 0.52f}, {3, 64, 64, 2, 3.2f, 0.33f},
-                            {4, 128, 128, 1, 6.0f, 0.60f}};
+constexpr Cand kCands[6] = {{1, 128, 128, 1, 6.0f, 0.52f}, {2, 128, 64, 2, 5.0f, 0.52f}, {3, 64, 64, 2, 3.2f, 0.33f},
+                            {4, 128, 128, 1, 6.0f, 0.60f}, {5, 256, 128, 1, 7.0f, 0.70f}, {6, 128, 256, 1, 7.0f, 0.70f}};
 int64_t tiles_of(const mmt_gemm_params& p, int bm, int bn) {
     return (int64_t)((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn);
 }
@@ -693,7 +710,11 @@ int mmt_gemm_glds(const mmt_gemm_params& p, hipStream_t st, int force) {
     int cfg = force, nsk = 1;
     if (cfg == 0) {
         float best = 1e30f;
-        for (int ci = 0; ci < 3; ++ci) {
+        // 128x256 (impl 6) only for grids of more than two rounds of 128x128 tiles (large M): at
+        // batch 1 - 4 its tile quantisation loses (gemm_ab.py: qkv / fc2 at M = 2112 0.70-0.96x)
+        const bool big = tiles_of(p, 128, 128) * p.groups > 512;
+        for (int ci = 0; ci < (big ? 6 : 3); ++ci) {
+            if (ci == 3 || ci == 4) continue;  // impl 4 / 5: A/B only
             const Cand& c = cands[ci];
             const int nmax = p.splitk >= 1 ? std::min(p.splitk, max_split(c)) : max_split(c);
             for (int n = (p.splitk >= 2 ? nmax : 1); n <= nmax; ++n) {
@@ -702,7 +723,7 @@ int mmt_gemm_glds(const mmt_gemm_params& p, hipStream_t st, int force) {
                 if (t < best) best = t, cfg = c.cfg, nsk = n;
             }
         }
-    } else if (cfg >= 1 && cfg <= 4) {
+    } else if (cfg >= 1 && cfg <= 6) {
         const Cand& c = cands[cfg - 1];
         if (p.splitk >= 2) {
             nsk = std::min(p.splitk, max_split(c));
@@ -719,6 +740,8 @@ int mmt_gemm_glds(const mmt_gemm_params& p, hipStream_t st, int force) {
         case 2: launch<T, 128, 64, 2, 2, 2, 3>(p, nsk, st); break;
         case 3: launch<T, 64, 64, 2, 2, 2, 4>(p, nsk, st); break;
         case 4: launch<T, 128, 128, 2, 2, 1, 4>(p, nsk, st); break;
+        case 5: launch<T, 256, 128, 4, 2, 1, 3>(p, nsk, st); break;
+        case 6: launch<T, 128, 256, 2, 4, 1, 3>(p, nsk, st); break;
         default: return 1;
     }
     return 0;

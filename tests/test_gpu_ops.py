@@ -115,11 +115,13 @@ def test_gemm_groups_segments_ksplit(dname):
         assert err <= _tol(dt) * ref.abs().max().item(), (grp, err)
 
 
-@pytest.mark.parametrize("impl", [-1, 1, 2, 3, 4])
-@pytest.mark.parametrize("M,N,K", [(528, 768, 768), (77, 200, 64), (300, 136, 192), (1056, 256, 3072), (300, 136, 200)])
+@pytest.mark.parametrize("impl", [-1, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("M,N,K", [(528, 768, 768), (77, 200, 64), (300, 136, 192), (1056, 256, 3072), (300, 136, 200),
+                                   (4224, 1160, 256)])
 def test_gemm_bf16_tile_paths(impl, M, N, K):
     """Every bf16 GEMM kernel (impl: register-staged / LDS-DMA 128x128, 128x64 K-split, 64x64
-    K-split) on ragged M/N, odd K-step counts (the K-split's empty last step) and each epilogue:
+    K-split, 256x128 / 128x256) on ragged M/N, odd K-step counts (the K-split's empty last step), a
+    grid of more than 512 workgroups (the grouped tile order of large grids), and each epilogue:
     GELU + fp32 residual into an fp32 C; bf16 C + C2 = C + bf16 residual (r_t) with a modulo row
     map; two groups with segmented rows and a split K source."""
     g = torch.Generator().manual_seed(M * 7 + N + K)
@@ -171,7 +173,7 @@ def test_gemm_bf16_tile_paths(impl, M, N, K):
             assert e3 <= 1e-3 * r3.abs().max().item() + 1e-4, (grp, e3)
 
 
-@pytest.mark.parametrize("impl", [1, 2, 3, 4])
+@pytest.mark.parametrize("impl", [1, 2, 3, 4, 6])
 @pytest.mark.parametrize("splitk", [2, 3, 5])
 @pytest.mark.parametrize("M,N,K", [(528, 768, 3072), (77, 200, 1024), (400, 192, 640)])
 def test_gemm_splitk(impl, splitk, M, N, K):
@@ -230,7 +232,7 @@ def test_gemm_splitk_conv():
 
 
 @pytest.mark.parametrize("dname", ["bf16", "fp16"])
-@pytest.mark.parametrize("impl", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("impl", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("M,N,K", [(528, 2304, 768), (300, 136, 512)])
 def test_gemm_layernorm_fold(dname, impl, M, N, K):
     """Linear(LayerNorm(x)) as one GEMM (ln_fold): A = bf16 rows of x with a nonzero mean, W' =
@@ -277,7 +279,7 @@ def test_gemm_layernorm_fold(dname, impl, M, N, K):
 
 
 @pytest.mark.parametrize("dname", ["bf16", "fp16"])
-@pytest.mark.parametrize("pimpl,cimpl", [(1, 1), (2, 3), (3, 2), (0, 0)])
+@pytest.mark.parametrize("pimpl,cimpl", [(1, 1), (2, 3), (3, 2), (0, 0), (6, 5), (5, 6)])
 def test_gemm_layernorm_stats_handoff(dname, pimpl, cimpl):
     """ln_stats_out / ln_fold 2: a producer GEMM (C fp32 = A W^T + b + R, C2 = its 16-bit copy) also
     writes the per-64-column row statistics of C2; the LayerNorm-folded consumer reads them instead
@@ -329,7 +331,8 @@ def test_gemm_layernorm_stats_handoff(dname, pimpl, cimpl):
     assert (outs[0] - outs[1]).abs().max().item() <= 1e-4 * ref.abs().max().item()
 
 
-@pytest.mark.parametrize("dname,impl", [("f32", 0), ("bf16", -1), ("bf16", 1), ("bf16", 2), ("bf16", 3), ("fp16", 1), ("fp16", -1)])
+@pytest.mark.parametrize("dname,impl", [("f32", 0), ("bf16", -1), ("bf16", 1), ("bf16", 2), ("bf16", 3), ("bf16", 5), ("bf16", 6),
+                                        ("fp16", 1), ("fp16", -1)])
 @pytest.mark.parametrize("h,up,cin,cout", [(20, 1, 64, 96), (40, 2, 32, 48), (10, 1, 16, 200), (20, 1, 96, 48), (80, 4, 48, 32)])
 def test_conv3x3_implicit_gemm(dname, impl, h, up, cin, cout):
     """3x3/pad-1 conv as implicit GEMM on every kernel (impl); K = 9*cin is not a multiple of the

@@ -20,7 +20,14 @@ from mmt_amd import _lib as L  # noqa: E402
 SHAPES = [("qkv_ln", 2, 528, 2304, 768, 0, 0), ("fc1_ln", 2, 528, 3072, 768, 1, 0), ("qkv", 2, 528, 2304, 768, 0, 0), ("proj", 2, 528, 768, 768, 0, 1), ("fc1", 2, 528, 3072, 768, 1, 0),
           ("fc2", 2, 528, 768, 3072, 0, 1), ("qkv_B4", 2, 2112, 2304, 768, 0, 0), ("fc2_B4", 2, 2112, 768, 3072, 0, 1),
           ("head1_like", 1, 400, 1344, 6912, 2, 0), ("enc_lin2_like", 1, 800, 512, 2048, 0, 1),
-          ("conv2_like", 2, 400, 192, 3456, 2, 0)]
+          ("conv2_like", 2, 400, 192, 3456, 2, 0),
+          # large M: config-4 training step (16 pairs, two-stream: 8448 rows per backbone) and its
+          # backward dX / dW shapes (dW: K = rows), config-3 batched inference (B = 8: 4224 rows)
+          ("qkv_T16", 2, 8448, 2304, 768, 0, 0), ("fc1_T16", 2, 8448, 3072, 768, 1, 0),
+          ("fc2_T16", 2, 8448, 768, 3072, 0, 1), ("proj_T16", 2, 8448, 768, 768, 0, 1),
+          ("dW_fc1_T16", 2, 3072, 768, 8448, 0, 0), ("dW_fc2_T16", 2, 768, 3072, 8448, 0, 0),
+          ("dX_fc2_T16", 2, 8448, 3072, 768, 0, 0), ("fc1_B8", 2, 4224, 3072, 768, 1, 0),
+          ("fc2_B8", 2, 4224, 768, 3072, 0, 1)]
 
 
 SK_WS = None
