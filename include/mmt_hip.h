@@ -30,6 +30,7 @@
  *       asymmetric_shared.py:55-104
  *   mmt_mam_attention_bwd       its autograd (training step, train_script_mixformer*.py)
  *   mmt_transpose_bf16          operand transposes of the Linear backward (nn.Linear autograd)
+ *   mmt_adamw_step              gradient clipping + AdamW over every parameter (torch.optim.AdamW)
  *   mmt_layernorm / mmt_groupnorm  nn.LayerNorm / nn.GroupNorm on the hot path
  *   mmt_patch_im2col            PatchEmbed conv input staging, mixformer.py:29-34
  *   mmt_msda_bimodal            MSDeformAttn_Bimodal.forward middle part (offset/weight softmax,
@@ -372,6 +373,41 @@ int mmt_track_update(const float* pred_cxcywh, const double* crop, double* state
  * backward's dX = dY W and dW = dY^T X GEMMs (both contract over a non-contiguous dimension). */
 int mmt_transpose_bf16(const void* in, void* out, int rows, int cols, int64_t ld_in, int64_t ld_out, int batch,
                        int64_t stride_in, int64_t stride_out, void* stream);
+
+/* AdamW update with global-norm gradient clipping (torch.nn.utils.clip_grad_norm_
+ * + torch.optim.AdamW's fused form over the reference's parameter groups, train_script_mixformer.py:
+ * 105-140, base_functions.py:362-400).  Device tables: one entry per fp32 parameter tensor (p, its
+ * gradient g, the moments m / v, an optional bf16 shadow written with the updated p, the element
+ * count n and its parameter group) and a list of chunks of mmt_adamw_chunk_elems() elements (the
+ * entry and the chunk's first element), one workgroup each.
+ *   mmt_adamw_step: with max_norm > 0, partial[i] = sum of g^2 over chunk i (nchunks floats of
+ *     workspace); then the device state (32 B, zeroed before the first step) is advanced:
+ *     state[0] = total L2 norm (partials summed in chunk order), state[1] = c = min(1, max_norm /
+ *     (norm + 1e-6)) (1 without clipping), t = ++step (int32 at state[4]), state[2] = 1 - b1^t,
+ *     state[3] = sqrt(1 - b2^t); then per element, g' = c g, group lr / wd (HOST arrays of ngroups
+ *     values, copied into the launch):  p *= 1 - lr wd; m = b1 m + (1-b1) g'; v = b2 v + (1-b2) g'^2;
+ *     p -= lr / (1 - b1^t) * m / (sqrt(v) / sqrt(1 - b2^t) + eps); zero_grad: g = 0 afterwards.
+ *     No host-side state: a captured hipGraph of the step replays correct steps. */
+#define MMT_ADAMW_MAX_GROUPS 8
+typedef struct mmt_adamw_tensor {
+    float* p;
+    float* g;
+    float* m;
+    float* v;
+    uint16_t* shadow; /* bf16 copy of p after the update, or NULL */
+    int64_t n;
+    int32_t group;
+    int32_t pad_;
+} mmt_adamw_tensor;
+typedef struct mmt_adamw_chunk {
+    int32_t tensor;
+    int32_t pad_;
+    int64_t offset;
+} mmt_adamw_chunk;
+int mmt_adamw_chunk_elems(void);
+int mmt_adamw_step(const mmt_adamw_tensor* tensors, const mmt_adamw_chunk* chunks, int nchunks, float* partial,
+                   float* state, const float* lr, const float* weight_decay, int ngroups, double beta1, double beta2,
+                   double eps, float max_norm, int zero_grad, void* stream);
 
 /* Library version string (for diagnostics). */
 const char* mmt_version(void);

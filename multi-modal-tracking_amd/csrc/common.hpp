@@ -194,3 +194,26 @@ MMT_DEV void lds_barrier() {
 
 static inline int hip_status(hipError_t e) { return e == hipSuccess ? 0 : -(int)e; }
 static inline int launch_status() { return hip_status(hipGetLastError()); }
+
+// Zero a device buffer with a kernel instead of hipMemsetAsync: a memset captured into a hipGraph
+// was not re-applied on replay for the MSDA gradient buffer (ROCm 7.2; replay 0 exact, later replays
+// accumulated onto the previous replay's sums: tools/graph_replay_debug.py), a kernel is.
+static __global__ __launch_bounds__(256) void mmt_zero_fill_kernel(uint32_t* __restrict__ p, int64_t n, int vec) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (vec) {
+        const int64_t n4 = n / 4;
+        if (i < n4) ((uint4*)p)[i] = uint4{0u, 0u, 0u, 0u};
+        if (i < n - 4 * n4) p[4 * n4 + i] = 0u;  // the < 4 tail words, block 0
+    } else if (i < n) {
+        p[i] = 0u;
+    }
+}
+// bytes: a multiple of 4
+static inline int zero_fill_async(void* p, size_t bytes, hipStream_t st) {
+    const int64_t n = (int64_t)(bytes / 4);
+    if (n <= 0) return 0;
+    const int vec = (((uintptr_t)p) & 15) == 0;
+    const int64_t items = vec ? (n / 4 > 4 ? n / 4 : 4) : n;
+    hipLaunchKernelGGL(mmt_zero_fill_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, st, (uint32_t*)p, n, vec);
+    return launch_status();
+}

@@ -548,8 +548,7 @@ extern "C" int mmt_prroi_pool_backward(const float* rois, const float* grad_out,
     if (!rois || !grad_out || !grad_features || B <= 0 || R < 0 || C <= 0 || H <= 0 || W <= 0 || ph <= 0 || pw <= 0)
         return MMT_EBADARG;
     hipStream_t st = (hipStream_t)stream;
-    const hipError_t e = hipMemsetAsync(grad_features, 0, sizeof(float) * (size_t)B * C * H * W, st);
-    if (e != hipSuccess) return -(int)e;
+    if (const int e = zero_fill_async(grad_features, sizeof(float) * (size_t)B * C * H * W, st)) return e;
     if (R == 0) return 0;
     const int64_t total = (int64_t)R * C * ph * pw;
     hipLaunchKernelGGL(prroi_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, rois, grad_out,

@@ -246,8 +246,7 @@ extern "C" int mmt_ms_deform_attn_backward(const void* value, const int64_t* spa
     if (!esz) return MMT_EBADARG;
     hipStream_t st = (hipStream_t)stream;
     // grad_value accumulates by atomics; grad_loc / grad_attn are fully written by the kernel
-    const hipError_t e = hipMemsetAsync(grad_value, 0, (size_t)N * S * M * D * esz, st);
-    if (e != hipSuccess) return -(int)e;
+    if (const int e = zero_fill_async(grad_value, (size_t)N * S * M * D * esz, st)) return e;
     const int64_t nsamp = (int64_t)N * Lq * M;
     dim3 grid((unsigned)((nsamp + 3) / 4));
 #define MSDA_BWD_CASE(T)                                                                                          \

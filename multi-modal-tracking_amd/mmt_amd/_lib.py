@@ -89,6 +89,8 @@ _PROTOS = {
     "mmt_ce_recover": [vp, vp, i32, vp, i32, i32, i32, i32, i32, i32, vp],
     "mmt_sample_target": [ctypes.POINTER(CropParams), i32, vp],
     "mmt_track_update": [vp, vp, vp, i32, i32, i32, i32, f64, vp],
+    "mmt_adamw_chunk_elems": [],
+    "mmt_adamw_step": [vp, vp, i32, vp, vp, vp, vp, i32, f64, f64, f64, f32, i32, vp],
 }
 
 

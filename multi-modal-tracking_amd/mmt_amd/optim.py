@@ -1,0 +1,113 @@
+"""AdamW with global-norm gradient clipping on libmmt_hip.so (mmt_adamw_grad_norm / mmt_adamw_step).
+
+Drop-in for the training step's `torch.nn.utils.clip_grad_norm_(params, max_norm)` followed by
+`torch.optim.AdamW(param_groups, lr, weight_decay)` (train_script_mixformer.py:105-140,
+ltr_trainer.py TRAIN.GRAD_CLIP_NORM, base_functions.py:362-400 parameter groups): three launches
+over every parameter instead of PyTorch's per-group multi-tensor kernels, the norm, the clip and the
+update.  The update pass also
+  * zeroes the gradients in place (they stay allocated, so the device tables stay valid: zero_grad
+    is then a no-op), and
+  * writes a bf16 shadow of the weights registered with `shadow=` (the backbone Linears): the next
+    forward's GEMMs read it instead of casting each weight (mmt_amd.train._HipLinear), valid while
+    the parameter's version counter is the one recorded with it.
+Parameters without a gradient at a step are left untouched (as torch.optim does).
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+TENSOR_DTYPE = np.dtype([("p", "<u8"), ("g", "<u8"), ("m", "<u8"), ("v", "<u8"), ("shadow", "<u8"), ("n", "<i8"),
+                         ("group", "<i4"), ("pad_", "<i4")])  # mmt_adamw_tensor
+CHUNK_DTYPE = np.dtype([("tensor", "<i4"), ("pad_", "<i4"), ("offset", "<i8")])  # mmt_adamw_chunk
+MAX_GROUPS = 8
+
+
+class HipAdamW:
+    def __init__(self, param_groups, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, shadow=()):
+        from ._lib import LIB
+        self.lib = LIB
+        self.groups = []
+        for g in param_groups:
+            g = dict(g)
+            g["params"] = [p for p in g["params"] if p.requires_grad]
+            g.setdefault("lr", lr)
+            g.setdefault("weight_decay", weight_decay)
+            self.groups.append(g)
+        if len(self.groups) > MAX_GROUPS:
+            raise ValueError("at most %d parameter groups" % MAX_GROUPS)
+        self.betas, self.eps = betas, eps
+        self.step_count = 0
+        self.state = {}
+        self.chunk = int(LIB.mmt_adamw_chunk_elems())
+        shadow_ids = {id(p) for p in shadow}
+        self._shadow = {}
+        for g in self.groups:
+            for p in g["params"]:
+                if not (p.is_cuda and p.dtype == torch.float32 and p.is_contiguous()):
+                    raise ValueError("HipAdamW takes contiguous fp32 device parameters")
+                self.state[p] = (torch.zeros_like(p), torch.zeros_like(p))
+                if id(p) in shadow_ids:
+                    sh = p.detach().to(torch.bfloat16)
+                    self._shadow[p] = sh
+                    p._mmt_bf16 = (sh, p._version)
+        self._key = None
+        self.last_norm = None
+
+    def zero_grad(self, set_to_none=False):
+        """The update pass zeroes the gradients it consumed; only gradients of parameters that were
+        not stepped (none at the first step) are cleared here."""
+        for g in self.groups:
+            for p in g["params"]:
+                if p.grad is not None and self._key is None:
+                    p.grad.zero_()
+
+    def _tables(self, params):
+        key = tuple((p.data_ptr(), p.grad.data_ptr()) for _, p in params)
+        if key == self._key:
+            return
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("HipAdamW: the parameter / gradient set changed during hipGraph capture "
+                               "(run one eager step first)")
+        t = np.zeros(len(params), TENSOR_DTYPE)
+        chunks = []
+        for i, (gi, p) in enumerate(params):
+            if not (p.grad.dtype == torch.float32 and p.grad.is_contiguous() and p.grad.shape == p.shape):
+                raise ValueError("HipAdamW needs contiguous fp32 gradients of the parameter's shape")
+            m, v = self.state[p]
+            sh = self._shadow.get(p)
+            t[i] = (p.data_ptr(), p.grad.data_ptr(), m.data_ptr(), v.data_ptr(), sh.data_ptr() if sh is not None else 0,
+                    p.numel(), gi, 0)
+            chunks += [(i, 0, o) for o in range(0, p.numel(), self.chunk)]
+        dev = params[0][1].device
+        self._tens = torch.from_numpy(t.view(np.uint8).copy()).to(dev)
+        self._chunks = torch.from_numpy(np.array(chunks, CHUNK_DTYPE).view(np.uint8).copy()).to(dev)
+        self._nchunks = len(chunks)
+        self._partial = torch.empty(self._nchunks, device=dev)
+        if not hasattr(self, "_state"):
+            self._state = torch.zeros(8, device=dev)  # norm, clip factor, bias corrections, step (int32)
+        self._key = key
+
+    @torch.no_grad()
+    def step(self, max_norm=0.0):
+        """clip_grad_norm_(max_norm) (skipped when max_norm <= 0) + one AdamW step: three launches with
+        no host synchronisation and no host-side step state (capturable in a hipGraph once the
+        tables exist, i.e. after the first eager step).  The total gradient norm before clipping is
+        `last_norm` (a device scalar)."""
+        from ._lib import check
+        params = [(gi, p) for gi, g in enumerate(self.groups) for p in g["params"] if p.grad is not None]
+        if not params:
+            return
+        self._tables(params)
+        self.step_count += 1
+        n = len(self.groups)
+        lr = (ctypes.c_float * n)(*[float(g["lr"]) for g in self.groups])
+        wd = (ctypes.c_float * n)(*[float(g["weight_decay"]) for g in self.groups])
+        check(self.lib.mmt_adamw_step(self._tens.data_ptr(), self._chunks.data_ptr(), self._nchunks,
+                                      self._partial.data_ptr(), self._state.data_ptr(),
+                                      ctypes.cast(lr, ctypes.c_void_p), ctypes.cast(wd, ctypes.c_void_p), n,
+                                      float(self.betas[0]), float(self.betas[1]), float(self.eps), float(max_norm), 1,
+                                      torch.cuda.current_stream().cuda_stream), "mmt_adamw_step")
+        self.last_norm = self._state[0]
+        for p in self._shadow:
+            p._mmt_bf16 = (self._shadow[p], p._version)

@@ -13,11 +13,14 @@ What runs where.  The ViT backbones (≈ 85 % of the step's FLOPs) run on libmmt
 autograd Functions: every Linear (patch embed as a GEMM on the unfolded patches, qkv, proj, fc1,
 fc2) forward and backward on the LDS-DMA bf16 GEMM (dX = dY W and dW = dY^T X after bf16
 transposes, fp32 accumulation, fp32 master weights), and the MAM attention forward (throughput
-kernel, log-sum-exp kept) and backward (mmt_mam_attention_bwd).  LayerNorm / GELU / residual adds,
-the fusion encoder's deformable sampling runs on mmt_ms_deform_attn_forward / _backward
-(mmt_amd.functional.MSDeformAttnFunction, the reference's MSDeformAttnFunction), and the rest of the
-fusion and the corner head run as PyTorch-ROCm ops on the same module tree (`nn.Conv2d`,
-`nn.GroupNorm`, `SyncBatchNorm` under DDP), in bf16 autocast like the reference's AMP path.  The backbone ops are injected (`ops`), so the data-parallel plumbing can be exercised on CPU
+kernel, log-sum-exp kept) and backward (mmt_mam_attention_bwd).  The fusion encoder's Linears
+(value / offset / weight / output projections, FFN) take the same GEMM op, and its deformable
+sampling runs on mmt_ms_deform_attn_forward / _backward (mmt_amd.functional.MSDeformAttnFunction,
+the reference's MSDeformAttnFunction).  Clipping + AdamW is mmt_adamw_step (mmt_amd.optim.HipAdamW,
+three launches over every parameter, writing the bf16 copies of the backbone weights the GEMMs
+read).  LayerNorm / GELU / residual adds and the corner head run as PyTorch-ROCm ops on the same
+module tree (`nn.Conv2d`, `nn.GroupNorm`, `SyncBatchNorm` under DDP), in bf16 autocast like the
+reference's AMP path.  The backbone ops are injected (`ops`), so the data-parallel plumbing can be exercised on CPU
 with stand-in ops in tests; the product's ops are `HipOps` and have no CPU path.
 """
 import math
@@ -29,6 +32,19 @@ LOG2E = 1.4426950408889634
 
 
 # ----------------------------------------------------------------------------- HIP backbone ops
+_CONSTS = {}
+
+
+def _const(key, device, make):
+    """Small constant tensors built on the host once per device and reused (no host-to-device copy
+    inside a step, so the step can be captured in a hipGraph)."""
+    k = key + (str(device),)
+    if k not in _CONSTS:
+        v = make()
+        _CONSTS[k] = tuple(t.to(device) for t in v) if isinstance(v, tuple) else v.to(device)
+    return _CONSTS[k]
+
+
 def _stream():
     return torch.cuda.current_stream().cuda_stream
 
@@ -71,7 +87,8 @@ class _HipLinear(torch.autograd.Function):
         M, K = x.shape
         N = w.shape[0]
         x = x.contiguous()
-        wb = w.detach().to(torch.bfloat16).contiguous()
+        sh = getattr(w, "_mmt_bf16", None)  # bf16 shadow written by HipAdamW's update (same values)
+        wb = sh[0] if sh is not None and sh[1] == w._version else w.detach().to(torch.bfloat16).contiguous()
         y = _gemm(x, wb, M, N, K, bias=b.detach().float().contiguous(), out_f32=out_f32)
         ctx.save_for_backward(x, wb)
         return y
@@ -133,8 +150,9 @@ class HipOps:
         fp32 as the reference op; L levels of hw x hw."""
         from .functional import MSDeformAttnFunction
         L = loc.shape[3]
-        shapes = torch.tensor([[hw, hw]] * L, dtype=torch.long, device=value.device)
-        starts = torch.arange(L, dtype=torch.long, device=value.device) * (hw * hw)
+        shapes, starts = _const(("msda_levels", hw, L), value.device,
+                                lambda: (torch.tensor([[hw, hw]] * L, dtype=torch.long),
+                                         torch.arange(L, dtype=torch.long) * (hw * hw)))
         return MSDeformAttnFunction.apply(value, shapes, starts, loc, aw, 64)
 
 
@@ -287,21 +305,27 @@ def fusion_forward(fu, s_v, s_i, ops):
     lpos = torch.cat([pos + fa.level_embed[0].view(1, 1, -1), pos + fa.level_embed[1].view(1, 1, -1)], 1)
     ref = _ref_points(h, w, b, 2, s_v.device)
     nl = 2 * h * w
+
+    def lin(mod, x):  # the encoder's nn.Linear layers on the backbone's GEMM op (bf16 operands, as autocast)
+        y = ops.linear(x.reshape(-1, x.shape[-1]).to(ops.dtype).contiguous(), mod.weight, mod.bias)
+        return y.view(*x.shape[:-1], -1)
+
     for layer in fa.encoder.layers:
         sa = layer.self_attn
         query = src + lpos
         q_bi = torch.cat(torch.chunk(query, 2, 1), dim=2)
-        value = sa.value_proj(src).view(b, nl, sa.n_heads, d // sa.n_heads)
-        off = sa.sampling_offsets(q_bi).view(b, nl // 2, sa.n_heads, sa.n_levels, sa.n_points, 2)
+        value = lin(sa.value_proj, src).view(b, nl, sa.n_heads, d // sa.n_heads)
+        off = lin(sa.sampling_offsets, q_bi).view(b, nl // 2, sa.n_heads, sa.n_levels, sa.n_points, 2)
         off = torch.cat([off, off], 1)
-        aw = sa.attention_weights(q_bi).view(b, nl // 2, sa.n_heads, sa.n_levels * sa.n_points)
+        aw = lin(sa.attention_weights, q_bi).view(b, nl // 2, sa.n_heads, sa.n_levels * sa.n_points)
         aw = F.softmax(torch.cat([aw, aw], 1).float(), -1).view(b, nl, sa.n_heads, sa.n_levels, sa.n_points)
-        loc = ref[:, :, None, :, None, :] + off.float() / torch.tensor([w, h], device=src.device, dtype=torch.float32)
-        src2 = sa.output_proj(ops.ms_deform_attn(value.float().contiguous(), h, loc.contiguous(), aw.contiguous()))
+        wh = _const(("loc_norm", w, h), src.device, lambda: torch.tensor([w, h], dtype=torch.float32))
+        loc = ref[:, :, None, :, None, :] + off.float() / wh
+        src2 = lin(sa.output_proj, ops.ms_deform_attn(value.float().contiguous(), h, loc.contiguous(), aw.contiguous()))
         src = src + layer.dropout1(src2)
         s1, s2 = torch.chunk(src, 2, 1)
         src = torch.cat([layer.norm1_v(s1), layer.norm1_i(s2)], 1)
-        src = src + layer.dropout3(layer.linear2(layer.dropout2(F.relu(layer.linear1(src)))))
+        src = src + layer.dropout3(lin(layer.linear2, layer.dropout2(F.relu(lin(layer.linear1, src)))))
         s1, s2 = torch.chunk(src, 2, 1)
         src = torch.cat([layer.norm2_v(s1), layer.norm2_i(s2)], 1)
     o_v, o_i = torch.chunk(src, 2, 1)
@@ -464,10 +488,18 @@ class TrainStep:
         self.net = net
         self.ops = ops
         self.grad_clip, self.iou_weight, self.l1_weight = grad_clip, iou_weight, l1_weight
-        # one fused multi-tensor kernel per parameter group on the device (the foreach form is ~4x the
-        # bytes-bound time of the 190 M-parameter update)
-        fused = next(net.parameters()).is_cuda
-        self.opt = torch.optim.AdamW(param_groups(net, lr), lr=lr, weight_decay=weight_decay, fused=fused or None)
+        # on the device: clip + AdamW as three launches over every parameter (mmt_amd.optim.HipAdamW,
+        # which also keeps the bf16 copies of the backbone Linear weights the GEMMs read); on the
+        # host (stand-in ops in tests): torch.optim.AdamW + clip_grad_norm_
+        groups = param_groups(net, lr)
+        if next(net.parameters()).is_cuda:
+            from .optim import HipAdamW
+            shadow = [m.weight for n, m in net.named_modules()
+                      if isinstance(m, torch.nn.Linear) and "backbone" in n and m.weight.requires_grad]
+            self.opt = HipAdamW(groups, lr=lr, weight_decay=weight_decay, shadow=shadow)
+        else:
+            self.opt = torch.optim.AdamW(groups, lr=lr, weight_decay=weight_decay)
+        self.hip_opt = next(net.parameters()).is_cuda
         if ddp and next(net.parameters()).is_cuda:  # train_script_mixformer.py:105
             net = self.net = torch.nn.SyncBatchNorm.convert_sync_batchnorm(net)
         if ddp:
@@ -477,7 +509,7 @@ class TrainStep:
 
     def backward(self, t, o, s, gt_xywh):
         """Forward, loss and backward; under DDP the gradient all-reduce runs inside backward()."""
-        self.opt.zero_grad(set_to_none=True)
+        self.opt.zero_grad(set_to_none=not self.hip_opt)  # (HipAdamW zeroes them in its update)
         pred = self.model(t, o, s)
         loss, stats = box_loss(pred, gt_xywh, self.iou_weight, self.l1_weight)
         loss.backward()
@@ -486,6 +518,9 @@ class TrainStep:
 
     def apply(self):
         """Gradient clipping (TRAIN.GRAD_CLIP_NORM) and the AdamW update."""
+        if self.hip_opt:
+            self.opt.step(self.grad_clip)
+            return
         if self.grad_clip > 0:
             torch.nn.utils.clip_grad_norm_(self.net.parameters(), self.grad_clip)
         self.opt.step()

@@ -99,3 +99,28 @@ def test_attention_impl_and_lse_gate():
     assert attn(impl=23, lse=fake) == -10000
     assert attn(dt=_lib.MMT_F16, impl=17) == -10000
     assert attn(dt=_lib.MMT_F16, lse=fake) == -10000
+
+
+def test_adamw_table_layouts_match_header(tmp_path):
+    """mmt_amd.optim's numpy mirrors of mmt_adamw_tensor / mmt_adamw_chunk have the C sizes and field
+    offsets (checked by gcc), and mmt_adamw_chunk_elems answers without a GPU."""
+    import subprocess
+    import numpy as np
+    from mmt_amd import _lib
+    from mmt_amd.optim import TENSOR_DTYPE, CHUNK_DTYPE
+    src = ['#include <stdio.h>', '#include <stddef.h>', '#include "%s"' % HEADER, "int main(void){",
+           'printf("%zu %zu\\n", sizeof(mmt_adamw_tensor), sizeof(mmt_adamw_chunk));']
+    src += ['printf("%%zu\\n", offsetof(mmt_adamw_tensor, %s));' % f for f in TENSOR_DTYPE.names]
+    src += ['printf("%%zu\\n", offsetof(mmt_adamw_chunk, %s));' % f for f in CHUNK_DTYPE.names]
+    src += ["return 0;}"]
+    c = tmp_path / "adamw.c"
+    c.write_text("\n".join(src))
+    exe = tmp_path / "adamw"
+    subprocess.check_call(["gcc", str(c), "-o", str(exe)])
+    out = [int(x) for x in subprocess.check_output([str(exe)]).decode().split()]
+    assert out[0] == TENSOR_DTYPE.itemsize and out[1] == CHUNK_DTYPE.itemsize
+    offs = [TENSOR_DTYPE.fields[f][1] for f in TENSOR_DTYPE.names] + [CHUNK_DTYPE.fields[f][1] for f in CHUNK_DTYPE.names]
+    assert out[2:] == offs
+    assert _lib.LIB.mmt_adamw_chunk_elems() == 1 << 16
+    assert _lib.LIB.mmt_adamw_step(None, None, 0, None, None, None, None, 1, 0.9, 0.999, 1e-8, 0.1, 0, None) == -10000
+    _ = np
