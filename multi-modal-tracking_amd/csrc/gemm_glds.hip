@@ -96,13 +96,15 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
 
     const int tiles_m = (p.M + BM - 1) / BM;
     // Tile order.  Grids of one or two rounds (batch 1): row tiles fastest, so the workgroups of one
-    // XCD share its W column slice.  Larger grids: row groups of GM tiles, column tiles next, so
+    // XCD share its W column slice.  Larger grids (impl 5 / 6): row groups of GM tiles, column tiles next, so
     // the ~32 workgroups an XCD holds at a time cover GM row panels x every column tile and each A
     // panel / W slice is fetched into that XCD's L2 once and re-read from it (instead of the A
     // panels streaming in again from the Infinity Cache for every column tile).
+    // (compiled into the large-M tiles only: in the batch-1 tile shapes the extra prologue code cost
+    // ~1 % of the frame, interleaved bench A/B 953.5 vs 944.5 frames/s)
     constexpr int GM = 8;
     int tm, tn;
-    if (gridDim.x * gridDim.y * gridDim.z > 512 && tiles_m > GM) {
+    if (BM * BN >= 256 * 128 && gridDim.x * gridDim.y * gridDim.z > 512 && tiles_m > GM) {
         const int tiles_n = ntiles / tiles_m, grp = tile / (GM * tiles_n), first = grp * GM;
         const int gsz = min(tiles_m - first, GM), r = tile - grp * GM * tiles_n;
         tm = first + r % gsz;
