@@ -712,9 +712,10 @@ int mmt_gemm_glds(const mmt_gemm_params& p, hipStream_t st, int force) {
     int cfg = force, nsk = 1;
     if (cfg == 0) {
         float best = 1e30f;
-        // 128x256 (impl 6) only for grids of more than two rounds of 128x128 tiles (large M): at
-        // batch 1 - 4 its tile quantisation loses (gemm_ab.py: qkv / fc2 at M = 2112 0.70-0.96x)
-        const bool big = tiles_of(p, 128, 128) * p.groups > 512;
+        // 128x256 (impl 6) only for grids of more than one round of 128x128 tiles: the batch-1 grids
+        // (<= 240 tiles) keep their shapes; the large-M ones gain (gemm_ab.py: training dW 481-554 ->
+        // 635-640 TFLOP/s, batch-8 fc2 571 -> 680; profiles/r03_gemm_large_vs_hipblaslt.jsonl)
+        const bool big = tiles_of(p, 128, 128) * p.groups > 256;
         for (int ci = 0; ci < (big ? 6 : 3); ++ci) {
             if (ci == 3 || ci == 4) continue;  // impl 4 / 5: A/B only
             const Cand& c = cands[ci];
