@@ -325,7 +325,7 @@ template <typename T>
 int check_gemm(const mmt_gemm_params& p) {
     const int EPC = 16 / (int)sizeof(T);
     if (p.M <= 0 || p.N <= 0 || p.K <= 0 || p.groups < 1 || p.groups > MMT_MAX_GROUPS) return MMT_EBADARG;
-    if (p.impl < -1 || p.impl > 6) return MMT_EBADARG;
+    if (p.impl < -1 || p.impl > 7) return MMT_EBADARG;
     if (p.K % EPC || p.lda % EPC) return MMT_EBADARG;
     if (p.conv_h > 0) {
         if (p.conv_cin % EPC || p.conv_up < 1 || p.conv_h % p.conv_up) return MMT_EBADARG;

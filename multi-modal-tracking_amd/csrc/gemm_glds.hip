@@ -89,6 +89,8 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
     constexpr int L = PA + PB;  // DMA instructions per wave per stage
     constexpr int WM = BM / WGM, WN = BN / WGN, MT = WM / 16, NT = WN / 16;
     static_assert(KS * ST * STAGE <= 160 * 1024, "LDS budget");
+    constexpr bool SB = BM * BN >= 256 * 256;  // single-buffered fragments (the 256x256 tile, impl 7)
+    static_assert(!SB || (KS == 1 && LNM == 0 && !CONV), "impl 7: plain GEMM only");
     static_assert(KS == 1 || BM * BN * 4 <= KS * ST * STAGE, "k-group reduction buffer");
     __shared__ __attribute__((aligned(1024))) unsigned char lds[KS * ST * STAGE];
     MMT_STAMP(0, "s_memrealtime");
@@ -114,7 +116,7 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
         tn = tile / tiles_m;
     }
     constexpr bool LNF = LNM != 0;  // LayerNorm folded: 1 = row statistics from the A fragments, 2 = handed in
-    const int m0 = tm * BM, n0 = tn * BN;
+    const int m0_tile = tm * BM, n0 = tn * BN;
     const int lane = threadIdx.x & 63, kg = threadIdx.x / TPG;
     const int wid = (threadIdx.x % TPG) >> 6, wr = wid / WGN, wc = wid % WGN;
     const int l16 = lane & 15, lg = lane >> 4;
@@ -135,7 +137,7 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
         const bool plain = segr >= M;  // one segment (wave-uniform): no divisions ahead of the first DMA
 #pragma unroll
         for (int i = 0; i < PA; ++i) {
-            const int m = min(m0 + (wid * PA + i) * 8 + prow, M - 1);
+            const int m = min(m0_tile + (wid * PA + i) * 8 + prow, M - 1);
             if (plain) {
                 aoff[i] = (int64_t)m * p.lda;
             } else {
@@ -147,7 +149,7 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
     } else {
 #pragma unroll
         for (int i = 0; i < PA; ++i) {
-            const int m = min(m0 + (wid * PA + i) * 8 + prow, M - 1);
+            const int m = min(m0_tile + (wid * PA + i) * 8 + prow, M - 1);
             const int b = m / (ch * ch), rem = m - b * ch * ch;
             ay[i] = rem / ch;
             ax[i] = rem - ay[i] * ch;
@@ -276,6 +278,28 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
     // barriers are the same in every copy.
     auto kloop = [&](auto MTVc) {
         constexpr int MTV = decltype(MTVc)::value;
+        if constexpr (SB) {
+            // 256x256 tile (2 waves per SIMD, 128 accumulator registers each): one fragment set, read
+            // and multiplied per 32-deep half; the SIMD's other wave covers the read latency
+            u32x4 ha[1][MT], hb[1][NT];
+            for (int s = 0; s < ns; ++s) {
+                if (s > 0) sync_for(s);
+                const unsigned char* b_ = ring + (s % ST) * STAGE;
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    const int sw_ = (4 * t + lg) ^ (lane & 7);
+#pragma unroll
+                    for (int mt = 0; mt < MTV; ++mt) ha[0][mt] = *(const u32x4*)(b_ + ((wr * WM + mt * 16 + l16) * 8 + sw_) * 16);
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt) hb[0][nt] = *(const u32x4*)(b_ + BM * 128 + ((wc * WN + nt * 16 + l16) * 8 + sw_) * 16);
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                        for (int mt = 0; mt < MTV; ++mt) acc[nt][mt] = mfma16x16x32<T>(hb[0][nt], ha[0][mt], acc[nt][mt]);
+                }
+            }
+            return;
+        }
         u32x4 fa0[2][MT], fb0[2][NT], fa1[2][MT], fb1[2][NT];
         MMT_READ(ring, fa0, fb0, MTV);
         // Every k-group has a real K-step at j < ns-1; only the last can be empty (KS = 2 with an odd
@@ -300,7 +324,7 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
             MMT_MMA(fa0, fb0, MTV);
         }
     };
-    const int mtv = __builtin_amdgcn_readfirstlane(min(max((M - m0 - wr * WM + 15) / 16, 0), MT));
+    const int mtv = __builtin_amdgcn_readfirstlane(min(max((M - m0_tile - wr * WM + 15) / 16, 0), MT));
     if (mtv == 0) kloop(gemm_ic<0>{});
     else if (mtv == 1 && MT > 1) kloop(gemm_ic<1>{});
     else kloop(gemm_ic<MT>{});  // whole fragments (other partial counts: padding computed, not stored)
@@ -314,8 +338,12 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
     // every thread owns 8 consecutive columns of RPP-row strips: bias / residual loads and C / C2
     // stores are whole 256-512-B row segments per wave-instruction.
     constexpr int TP = BN + 4;  // tile row pitch (floats); +4 keeps the fragment writes 2-way
-    constexpr int FLAG_OFF = BM * TP * 4 + KS * BM * 8;  // split-K "this workgroup sums" word
-    static_assert(FLAG_OFF + 16 <= KS * ST * STAGE, "epilogue tile fits in the stage ring");
+    // EPASS: a tile whose fp32 image does not fit the stage ring (256x256) is assembled and written
+    // out in WGM passes of one wave row (WM rows) each
+    constexpr int EPASS = BM * TP * 4 + KS * BM * 8 + 16 <= KS * ST * STAGE ? 1 : WGM, EB = BM / EPASS;
+    static_assert(EPASS == 1 || (EB == WM && KS == 1 && LNM == 0), "multi-pass epilogue: plain GEMM tiles");
+    static_assert(EB * TP * 4 <= KS * ST * STAGE, "epilogue pass fits in the stage ring");
+    constexpr int FLAG_OFF = EB * TP * 4 + KS * BM * 8;  // split-K "this workgroup sums" word
     float* ctile = (float*)lds;
     float* rstat = ctile + BM * TP;  // LNF: [KS][BM][2] partial (sum x, sum x^2) per k-group
     // LNM 2: the handed-in row statistics (K/64 partial (sum, sum of squares) pairs per A row), read
@@ -326,7 +354,7 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
     f32x2 stp[8];
     const int kp = K / 64, srow = threadIdx.x / TPRW, spart = threadIdx.x % TPRW;
     if constexpr (LNM == 2) {
-        const f32x2* st = (const f32x2*)p.ln_stats_in[g] + (int64_t)min(m0 + srow, M - 1) * kp;
+        const f32x2* st = (const f32x2*)p.ln_stats_in[g] + (int64_t)min(m0_tile + srow, M - 1) * kp;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int j = spart + i * TPRW;
@@ -362,12 +390,13 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
             }
         }
     }
-    if (KS == 1 || kg == 1) {
+    if ((KS == 1 || kg == 1) && (EPASS == 1 || wr == 0)) {
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt)
-                *(f32x4*)(ctile + (wr * WM + mt * 16 + l16) * TP + wc * WN + nt * 16 + lg * 4) = acc[nt][mt];
+                *(f32x4*)(ctile + ((EPASS == 1 ? wr * WM : 0) + mt * 16 + l16) * TP + wc * WN + nt * 16 + lg * 4) =
+                    acc[nt][mt];
     }
     if constexpr (KS == 2) {
         lds_barrier();
@@ -387,8 +416,8 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
 
     // 8-column strips: one 16-B store per lane for a bf16 C (two for fp32); dwordx2 stores were
     // store-issue-bound.
-    constexpr int NTHR = TPG * KS, TPR = BN / 8, RPP = NTHR / TPR, NPASS = BM / RPP;
-    static_assert(NTHR % TPR == 0 && BM % RPP == 0, "strip geometry");
+    constexpr int NTHR = TPG * KS, TPR = BN / 8, RPP = NTHR / TPR, NPASS = EB / RPP;
+    static_assert(NTHR % TPR == 0 && EB % RPP == 0, "strip geometry");
     const float* bias = p.bias[g];
     const float* R = p.r[g];
     char* C = (char*)p.c[g];
@@ -474,6 +503,19 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
     const int64_t csr = p.c_seg_rows > 0 ? p.c_seg_rows : INT64_MAX, csp = p.c_seg_pitch;
     auto crow = [&](int m) -> int64_t { return csr == INT64_MAX ? (int64_t)m : (m / csr) * csp + m % csr; };
     constexpr int PG = NPASS < 4 ? NPASS : 4;  // passes whose residual loads are in flight together
+    for (int ep = 0; ep < EPASS; ++ep) {
+    if (ep > 0) {  // the next wave row's accumulators into the (re-used) tile image
+        lds_barrier();
+        if (wr == ep) {
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+                    *(f32x4*)(ctile + (mt * 16 + l16) * TP + wc * WN + nt * 16 + lg * 4) = acc[nt][mt];
+        }
+        lds_barrier();
+    }
+    const int m0 = m0_tile + ep * EB;  // first tile row of this pass
 #pragma unroll
     for (int p0 = 0; p0 < NPASS; p0 += PG) {
         f32x4 ra[PG], rb[PG];
@@ -572,6 +614,7 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
             }
         }
     }
+    }  // epilogue passes
     MMT_STAMP(5, "s_memtime");
 #if MMT_STAMP_BUILD
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -680,8 +723,9 @@ bool glds_takes(const mmt_gemm_params& p) {
 // Large-M tiles (impl 5 / 6: 256x128 / 128x256, 8 waves with 64x64 wave tiles, 3-slot ring of
 // 48 KiB stages): 1.5x the MFMA work per byte of LDS fill of 128x128, for grids of many rounds.
 struct Cand { int cfg, bm, bn, ks; float fixed_us, step_us; };
-constexpr Cand kCands[6] = {{1, 128, 128, 1, 6.0f, 0.52f}, {2, 128, 64, 2, 5.0f, 0.52f}, {3, 64, 64, 2, 3.2f, 0.33f},
-                            {4, 128, 128, 1, 6.0f, 0.60f}, {5, 256, 128, 1, 7.0f, 0.70f}, {6, 128, 256, 1, 7.0f, 0.70f}};
+constexpr Cand kCands[7] = {{1, 128, 128, 1, 6.0f, 0.52f}, {2, 128, 64, 2, 5.0f, 0.52f}, {3, 64, 64, 2, 3.2f, 0.33f},
+                            {4, 128, 128, 1, 6.0f, 0.60f}, {5, 256, 128, 1, 7.0f, 0.70f}, {6, 128, 256, 1, 7.0f, 0.70f},
+                            {7, 256, 256, 1, 9.0f, 1.33f}};
 int64_t tiles_of(const mmt_gemm_params& p, int bm, int bn) {
     return (int64_t)((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn);
 }
@@ -716,8 +760,16 @@ int mmt_gemm_glds(const mmt_gemm_params& p, hipStream_t st, int force) {
         // (<= 240 tiles) keep their shapes; the large-M ones gain (gemm_ab.py: training dW 481-554 ->
         // 635-640 TFLOP/s, batch-8 fc2 571 -> 680; profiles/r03_gemm_large_vs_hipblaslt.jsonl)
         const bool big = tiles_of(p, 128, 128) * p.groups > 256;
-        for (int ci = 0; ci < (big ? 6 : 3); ++ci) {
+        // 256x256 (impl 7): plain GEMMs only (no folded LayerNorm, no conv, no split-K), and not under a
+        // GELU epilogue, whose four-pass form measured slower (fc1 at 16 pairs: 515 vs 565 TFLOP/s)
+        const bool big7 = big && !p.ln_fold && p.conv_h == 0 && p.act != 1;
+        for (int ci = 0; ci < (big7 ? 7 : big ? 6 : 3); ++ci) {
             if (ci == 3 || ci == 4) continue;  // impl 4 / 5: A/B only
+            if (ci == 6) {  // impl 7: no split-K
+                const float t = cost(cands[ci], 1);
+                if (t < best) best = t, cfg = 7, nsk = 1;
+                continue;
+            }
             const Cand& c = cands[ci];
             const int nmax = p.splitk >= 1 ? std::min(p.splitk, max_split(c)) : max_split(c);
             for (int n = (p.splitk >= 2 ? nmax : 1); n <= nmax; ++n) {
@@ -726,7 +778,7 @@ int mmt_gemm_glds(const mmt_gemm_params& p, hipStream_t st, int force) {
                 if (t < best) best = t, cfg = c.cfg, nsk = n;
             }
         }
-    } else if (cfg >= 1 && cfg <= 6) {
+    } else if (cfg >= 1 && cfg <= 7) {
         const Cand& c = cands[cfg - 1];
         if (p.splitk >= 2) {
             nsk = std::min(p.splitk, max_split(c));
@@ -745,6 +797,11 @@ int mmt_gemm_glds(const mmt_gemm_params& p, hipStream_t st, int force) {
         case 4: launch<T, 128, 128, 2, 2, 1, 4>(p, nsk, st); break;
         case 5: launch<T, 256, 128, 4, 2, 1, 3>(p, nsk, st); break;
         case 6: launch<T, 128, 256, 2, 4, 1, 3>(p, nsk, st); break;
+        case 7:
+            if (p.ln_fold || p.conv_h > 0 || nsk > 1) return 1;
+            hipLaunchKernelGGL((gemm_glds_kernel<T, 256, 256, 4, 2, 1, 2, false, 0>),
+                               dim3((unsigned)tiles_of(p, 256, 256), 1, p.groups), dim3(512), 0, st, p);
+            break;
         default: return 1;
     }
     return 0;

@@ -115,12 +115,12 @@ def test_gemm_groups_segments_ksplit(dname):
         assert err <= _tol(dt) * ref.abs().max().item(), (grp, err)
 
 
-@pytest.mark.parametrize("impl", [-1, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("impl", [-1, 1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("M,N,K", [(528, 768, 768), (77, 200, 64), (300, 136, 192), (1056, 256, 3072), (300, 136, 200),
                                    (4224, 1160, 256)])
 def test_gemm_bf16_tile_paths(impl, M, N, K):
     """Every bf16 GEMM kernel (impl: register-staged / LDS-DMA 128x128, 128x64 K-split, 64x64
-    K-split, 256x128 / 128x256) on ragged M/N, odd K-step counts (the K-split's empty last step), a
+    K-split, 256x128 / 128x256, 256x256 with its four-pass epilogue) on ragged M/N, odd K-step counts (the K-split's empty last step), a
     grid of more than 512 workgroups (the grouped tile order of large grids), and each epilogue:
     GELU + fp32 residual into an fp32 C; bf16 C + C2 = C + bf16 residual (r_t) with a modulo row
     map; two groups with segmented rows and a split K source."""
