@@ -16,7 +16,7 @@ timeout -k 10 400 python -u bench.py "$@" > "$OUT/bench.log" 2>&1
 rc=$?; echo "bench rc=$rc"; grep -o '"value": [0-9.]*\|"roofline_mam[_a-z0-9]*": {"kernel": "mam_attention", "bound": "mfma", "achieved": [0-9.]*, "peak": [0-9.]*, "unit": "TFLOP/s", "frac": [0-9.]*' "$OUT/bench.log"; [ $rc -ne 0 ] && exit $rc
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o trace --output-format csv -- \
-    python3 "$ROOT/bench.py" --no-cpu-baseline --no-kernel-profile --no-mam-batched --no-kv-cache --steps 100 --warmup 10 --dump-plan "$OUT/plan_names.json" "$@" > "$OUT/bench_prof.log" 2>&1
+    python3 "$ROOT/bench.py" --no-cpu-baseline --no-kernel-profile --no-mam-batched --no-kv-cache --no-fp16-line --no-train-line --steps 100 --warmup 10 --dump-plan "$OUT/plan_names.json" "$@" > "$OUT/bench_prof.log" 2>&1
 rc=$?; echo "rocprof rc=$rc"
 python3 "$ROOT/tools/trace_breakdown.py" "$OUT/prof/trace_kernel_trace.csv" "$OUT/plan_names.json" > "$OUT/breakdown.txt" 2>&1
 head -8 "$OUT/breakdown.txt"
