@@ -55,9 +55,11 @@ def _transpose(x, rows, cols, ld_out=None, ones_row=False):
     `rows` columns (so a GEMM against it also yields the row sums of its other operand), the rest zero."""
     from ._lib import LIB, check
     ld_out = ld_out or rows
-    alloc = torch.empty if ld_out == rows and not ones_row else torch.zeros
-    out = alloc(cols + (8 if ones_row else 0), ld_out, device=x.device, dtype=torch.bfloat16)
+    out = torch.empty(cols + (8 if ones_row else 0), ld_out, device=x.device, dtype=torch.bfloat16)
+    if ld_out > rows:  # only the padding columns and the extra rows need values of their own
+        out[:, rows:].zero_()
     if ones_row:
+        out[cols:].zero_()
         out[cols, :rows] = 1.0
     check(LIB.mmt_transpose_bf16(x.data_ptr(), out.data_ptr(), rows, cols, cols, ld_out, 1, 0, 0, _stream()),
           "mmt_transpose_bf16")
@@ -104,7 +106,9 @@ class _HipLinear(torch.autograd.Function):
         # dW and the bias gradient from one GEMM: x^T carries an extra row of ones, so output column
         # K of dy^T [x | 1] is sum_m dy[m][n] (the same bf16 dy, fp32 accumulation; no reduce kernel)
         dwb = _gemm(_transpose(dy, M, N, Mp), _transpose(x, M, K, Mp, ones_row=True), N, K + 8, Mp, out_f32=True)
-        return dx, dwb[:, :K].contiguous(), dwb[:, K].contiguous(), None
+        # strided views: autograd accumulates them into the persistent .grad buffers with one add
+        # (HipAdamW keeps the gradients allocated), so a contiguous copy first would be a wasted pass
+        return dx, dwb[:, :K], dwb[:, K], None
 
 
 class _HipMamAttention(torch.autograd.Function):
