@@ -1021,7 +1021,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
         // P = exp2(S) (the scores are in log2 units; no reference point, see above)
 #pragma unroll
         for (int r = 0; r < 8 * NJ; ++r) {
-            float e = MMT_ATTN_ABLATE == 3 ? sacc[r] : __builtin_amdgcn_exp2f(sacc[r]);
+            float e = (MMT_ATTN_ABLATE == 3 || MMT_ATTN_ABLATE == 6) ? sacc[r] : __builtin_amdgcn_exp2f(sacc[r]);
             if constexpr (MASK) {
                 if (32 * kb + 8 * (r >> 2) + 4 * hf + (r & 3) >= nv) e = 0.f;
             }
@@ -1121,14 +1121,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
         for (int ks = 0; ks < 4; ++ks)
             s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, k1[ks]), __builtin_bit_cast(bf16x8, qf[ks]), s1, 0, 0, 0);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) s0[r] = MMT_ATTN_ABLATE == 3 ? s0[r] : __builtin_amdgcn_exp2f(s0[r]);
+        for (int r = 0; r < 16; ++r) s0[r] = (MMT_ATTN_ABLATE == 3 || MMT_ATTN_ABLATE == 6) ? s0[r] : __builtin_amdgcn_exp2f(s0[r]);
         vfrags(1, v1);
         // block 0's V^T reads (the 8 oldest of the 16 asm reads) landed; the wait redefines them
         asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(v0[0][0][0]), "+v"(v0[0][0][1]), "+v"(v0[0][1][0]), "+v"(v0[0][1][1]),
                      "+v"(v0[1][0][0]), "+v"(v0[1][0][1]), "+v"(v0[1][1][0]), "+v"(v0[1][1][1]));
         pv(v0, s0);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) s1[r] = MMT_ATTN_ABLATE == 3 ? s1[r] : __builtin_amdgcn_exp2f(s1[r]);
+        for (int r = 0; r < 16; ++r) s1[r] = (MMT_ATTN_ABLATE == 3 || MMT_ATTN_ABLATE == 6) ? s1[r] : __builtin_amdgcn_exp2f(s1[r]);
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v1[0][0][0]), "+v"(v1[0][0][1]), "+v"(v1[0][1][0]), "+v"(v1[0][1][1]),
                      "+v"(v1[1][0][0]), "+v"(v1[1][0][1]), "+v"(v1[1][1][0]), "+v"(v1[1][1][1]));
         pv(v1, s1);
@@ -1233,16 +1233,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 // PIPE2: on full tiles both key blocks' scores (both query blocks) come before any exponential, so
 // the second key block's QK^T MFMAs run beside the first block's softmax (B = 8 / 16 / 32: 27.2 /
 // 47.1 / 75.2 -> 24.9 / 43.5 / 72.1 us, bit-identical; 243 VGPRs)
+// One work item of impl 22 (query block bx of 128 queries, head h, sequence s); lds = FNS tile slots.
+// Every LDS-DMA it issues has landed when it returns (the last tile's wait is vmcnt(0)); its output
+// stores may still be in flight.  (A persistent form that looped over these items in a longest-first
+// static order measured no faster: profiles/r03_attn_persistent_ab.jsonl.)
 template <int FNS, bool SPLIT = true, bool PIPE2 = true>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) void mam_attention_lz2_kernel(
-    const mmt_attn_params p) {
-    __shared__ __attribute__((aligned(1024))) char lds[FNS * FTILE];
-
+MMT_DEV void mam_lz2_item(const mmt_attn_params& p, char* lds, const int bx, const int h, const int s) {
     const int n_t = p.n_t, ntok = p.ntok, C = p.C;
     const int64_t pitch = p.tok_pitch > 0 ? p.tok_pitch : ntok;
     const int nqb_t = (n_t + FQ - 1) / FQ;
-    int bx, h, s;
-    attn_block_ids_xcd(bx, h, s);
     const int qb0 = bx + (p.q_part == 2 ? nqb_t : 0);
     const bool tmpl = qb0 < nqb_t;
     const int q0 = tmpl ? qb0 * FQ : n_t + (qb0 - nqb_t) * FQ;
@@ -1302,6 +1301,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const int li = lane & 15, qr = li >> 2, pc = li & 3, dsub = (lane >> 4) & 1;
 
     auto next_tile = [&](int kt) {
+        if (MMT_ATTN_ABLATE == 5 || MMT_ATTN_ABLATE == 6) return;  // measurement builds: free-running waves (no waits / barriers / refills; 6: no exponentials either)
         attn_wait_dyn(8 * (min(nkt - 1, kt + FNS - 2) - kt));
         lds_barrier();
         if (MMT_ATTN_ABLATE != 1 && kt + FNS - 1 < nkt) issue_tile(kt + FNS - 1);
@@ -1372,7 +1372,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             auto expo = [&](int qb) {
 #pragma unroll
                 for (int r = 0; r < 8 * NJ; ++r) {
-                    float e = MMT_ATTN_ABLATE == 3 ? sacc[qb][r] : __builtin_amdgcn_exp2f(sacc[qb][r]);
+                    float e = (MMT_ATTN_ABLATE == 3 || MMT_ATTN_ABLATE == 6) ? sacc[qb][r] : __builtin_amdgcn_exp2f(sacc[qb][r]);
                     if constexpr (MASK) {
                         if (32 * kb + 8 * (r >> 2) + 4 * hf + (r & 3) >= nv) e = 0.f;
                     }
@@ -1442,11 +1442,11 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                     }
                 }
 #pragma unroll
-                for (int r = 0; r < 16; ++r) sa[kb][0][r] = MMT_ATTN_ABLATE == 3 ? sa[kb][0][r] : __builtin_amdgcn_exp2f(sa[kb][0][r]);
+                for (int r = 0; r < 16; ++r) sa[kb][0][r] = (MMT_ATTN_ABLATE == 3 || MMT_ATTN_ABLATE == 6) ? sa[kb][0][r] : __builtin_amdgcn_exp2f(sa[kb][0][r]);
                 attn_lds_wait();
                 if constexpr (NQ == 2) {
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) sa[kb][1][r] = MMT_ATTN_ABLATE == 3 ? sa[kb][1][r] : __builtin_amdgcn_exp2f(sa[kb][1][r]);
+                    for (int r = 0; r < 16; ++r) sa[kb][1][r] = (MMT_ATTN_ABLATE == 3 || MMT_ATTN_ABLATE == 6) ? sa[kb][1][r] : __builtin_amdgcn_exp2f(sa[kb][1][r]);
                 }
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
@@ -1495,7 +1495,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             float chk = 0.f;
 #pragma unroll
             for (int r = 0; r < 16; ++r) chk += o[qb][0][r] * 0.f + o[qb][1][r] * 0.f;
-            const bool ok = l >= LZ_LO && l <= LZ_HI && chk == 0.f;
+            const bool ok = (l >= LZ_LO && l <= LZ_HI && chk == 0.f) || MMT_ATTN_ABLATE != 0;
             const int q = qbase + 32 * qb + l32;
             bf16_t* op = (bf16_t*)p.out + ((int64_t)s * pitch + q) * C + h * D;
             if (__builtin_expect(__all(ok), 1)) {
@@ -1557,6 +1557,15 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int kt = 0; kt < nfull; ++kt)
             if (kt + 1 < nkt) next_tile(kt + 1);
     }
+}
+
+template <int FNS>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) void mam_attention_lz2_kernel(
+    const mmt_attn_params p) {
+    __shared__ __attribute__((aligned(1024))) char lds[FNS * FTILE];
+    int bx, h, s;
+    attn_block_ids_xcd(bx, h, s);
+    mam_lz2_item<FNS>(p, lds, bx, h, s);
 }
 
 #ifndef MMT_ATTN_AB

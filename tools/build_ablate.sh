@@ -4,7 +4,7 @@
 #   ablate2: LDS-DMA GEMM K loop without MFMA work          (MMT_GEMM_ABLATE=2)
 #   aab1/2/3: range-checked MAM attention without K/V DMA after the prologue / without matrix and
 #            softmax work / without exponentials / without exponentials and bf16 packing
-#            (MMT_ATTN_ABLATE=1/2/3/4)
+#            (MMT_ATTN_ABLATE=1/2/3/4); aab5: impl 22 free-running (no per-tile wait / barrier / refill); aab6: aab5 without exponentials
 #   stamp:   per-phase workgroup timestamps in the GEMM / attention kernels (MMT_STAMP_BUILD=1)
 #   ab:      the product plus the A/B-only attention kernel impl 23 (MMT_ATTN_AB=1)
 # Use with MMT_HIP_LIB=multi-modal-tracking_amd/mmt_amd/_lib/<variant>/libmmt_hip.so.
@@ -23,4 +23,6 @@ build aab1 -DMMT_ATTN_ABLATE=1
 build aab2 -DMMT_ATTN_ABLATE=2
 build aab3 -DMMT_ATTN_ABLATE=3
 build aab4 -DMMT_ATTN_ABLATE=4
+build aab5 -DMMT_ATTN_ABLATE=5
+build aab6 -DMMT_ATTN_ABLATE=6
 build ab -DMMT_ATTN_AB=1
