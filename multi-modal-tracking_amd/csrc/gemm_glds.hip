@@ -361,6 +361,40 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
             stp[i] = j < kp ? st[j] : f32x2{0.f, 0.f};
         }
     }
+    // Residual rows of a single-pass, unsplit epilogue, loaded before the tile assembly: their L2 /
+    // Infinity Cache latency then overlaps the fragment writes and barriers below instead of being
+    // exposed once per group of four strip passes (proj / fc2 / encoder Linears: fp32 residual stream).
+    constexpr int TPR0 = BN / 8, RPP0 = TPG * KS / TPR0, NPASS0 = EB / RPP0;
+    constexpr bool RPRE = EPASS == 1 && NPASS0 <= 8 && BM * BN <= 128 * 128;  // batch-1 tiles (large ones spill)
+    const int tc0 = (threadIdx.x % TPR0) * 8, tr0 = threadIdx.x / TPR0, nc0 = min(n0 + tc0, N - 8);
+    auto rload = [&](int m, int nc, f32x4& ra, f32x4& rb) {  // residual row of output row m, columns nc..nc+7
+        const float* R = p.r[g];
+        const int64_t csr = p.c_seg_rows > 0 ? p.c_seg_rows : INT64_MAX, csp = p.c_seg_pitch;
+        int64_t rr = csr == INT64_MAX ? (int64_t)m : (m / csr) * csp + m % csr;
+        if (p.r_mode == 1) rr = m % p.r_p0;
+        else if (p.r_mode == 2) {
+            const int hw = p.r_p0 * p.r_p0, b = m / hw, rem = m - b * hw;
+            const int y = rem / p.r_p0, x = rem - y * p.r_p0, hs = p.r_p0 / p.r_p1;
+            rr = (int64_t)b * hs * hs + (int64_t)(y / p.r_p1) * hs + (x / p.r_p1);
+        }
+        if (p.r_t) {
+            const u32x4 u = *(const u32x4*)((const T*)R + rr * p.ldr + nc);
+            const f32x2 u0 = unpack2<T>(u[0]), u1 = unpack2<T>(u[1]), u2 = unpack2<T>(u[2]), u3 = unpack2<T>(u[3]);
+            ra = f32x4{u0[0], u0[1], u1[0], u1[1]};
+            rb = f32x4{u2[0], u2[1], u3[0], u3[1]};
+        } else {
+            ra = *(const f32x4*)(R + rr * p.ldr + nc);
+            rb = *(const f32x4*)(R + rr * p.ldr + nc + 4);
+        }
+    };
+    f32x4 rpa[RPRE ? NPASS0 : 1], rpb[RPRE ? NPASS0 : 1];
+    const bool rpre = RPRE && p.r[g] != nullptr && nsk == 1;  // wave-uniform
+    if constexpr (RPRE) {
+        if (rpre) {
+#pragma unroll
+            for (int i = 0; i < NPASS0; ++i) rload(min(m0_tile + tr0 + i * RPP0, M - 1), nc0, rpa[i], rpb[i]);
+        }
+    }
     lds_barrier();  // every wave is past its last fragment read (the DMA ring is drained: vmcnt(0))
     if constexpr (LNM == 2) {  // (sum, sum of squares) of the row, in pair order within each thread
         float sx = 0.f, sxx = 0.f;
@@ -522,25 +556,14 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
 #pragma unroll
         for (int i = 0; i < PG; ++i) {
             ra[i] = rb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (R) {  // wave-uniform; loads unconditional from a clamped row
-                const int m = min(m0 + tr + (p0 + i) * RPP, M - 1);
-                int64_t rr = crow(m);
-                if (p.r_mode == 1) rr = m % p.r_p0;
-                else if (p.r_mode == 2) {
-                    const int hw = p.r_p0 * p.r_p0, b = m / hw, rem = m - b * hw;
-                    const int y = rem / p.r_p0, x = rem - y * p.r_p0, hs = p.r_p0 / p.r_p1;
-                    rr = (int64_t)b * hs * hs + (int64_t)(y / p.r_p1) * hs + (x / p.r_p1);
-                }
-                if (p.r_t) {
-                    const u32x4 u = *(const u32x4*)((const T*)R + rr * p.ldr + nc);
-                    const f32x2 u0 = unpack2<T>(u[0]), u1 = unpack2<T>(u[1]), u2 = unpack2<T>(u[2]), u3 = unpack2<T>(u[3]);
-                    ra[i] = f32x4{u0[0], u0[1], u1[0], u1[1]};
-                    rb[i] = f32x4{u2[0], u2[1], u3[0], u3[1]};
-                } else {
-                    ra[i] = *(const f32x4*)(R + rr * p.ldr + nc);
-                    rb[i] = *(const f32x4*)(R + rr * p.ldr + nc + 4);
+            if constexpr (RPRE) {
+                if (rpre) {
+                    ra[i] = rpa[p0 + i];
+                    rb[i] = rpb[p0 + i];
+                    continue;
                 }
             }
+            if (R) rload(min(m0 + tr + (p0 + i) * RPP, M - 1), nc, ra[i], rb[i]);  // wave-uniform test; clamped row
         }
 #pragma unroll
         for (int i = 0; i < PG; ++i) {
