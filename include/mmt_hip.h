@@ -216,6 +216,19 @@ int mmt_layernorm(const float* in, const float* add, int64_t add_rows, float* ou
                   const float* gamma0, const float* beta0, const float* gamma1, const float* beta1,
                   int64_t rows, int64_t rows_per_group, int C, float eps, int dtype, void* stream);
 
+/* LayerNorm backward (training step; forward = mmt_layernorm without `add`): x [rows][C] fp32 = the
+ * LayerNorm input, dy [rows][C] in dy_dtype (bf16 / fp16 / fp32) = the output gradient, gamma per row
+ * group as the forward (gamma1 NULL: one group).  dx [rows][C] fp32 = rstd * (g - mean(g) - xhat *
+ * mean(g * xhat)), g = dy * gamma (statistics recomputed from x, eps as the forward).  dgb = fp32
+ * [groups][2][C]: (dgamma, dbeta) of each group = column sums of dy * xhat and dy over its rows, summed
+ * in a fixed order (bitwise reproducible), added to dgb if dgb_accumulate.  ws: fp32 workspace of
+ * >= ceil(rows / 32) * 4 * C floats.  Replaces aten's layer_norm backward in the training step
+ * (timm Block norm1 / norm2, mixformer.py:129-138; the per-modality norm*_v / norm*_i of the shared
+ * backbone, mixformer_shared.py:143-159). */
+int mmt_layernorm_bwd(const float* x, const void* dy, int dy_dtype, const float* gamma0, const float* gamma1,
+                      float* dx, float* dgb, int dgb_accumulate, float* ws, int64_t ws_floats, int64_t rows,
+                      int64_t rows_per_group, int C, float eps, void* stream);
+
 /* GroupNorm over [n_inst][P][Ctot] fp32 (channels-last, P positions, Ctot channels in `groups`
  * equal groups), per-instance affine set chosen by inst / inst_per_set (2 sets max).  Outputs
  * fp32 and/or dtype copies with the same layout. */

@@ -3,6 +3,7 @@
 //                    per-modality norm1_v/_i, norm2_v/_i, mixformer_shared.py:149-157) and of the
 //                    fusion encoder (eps 1e-5, deformable_encoder_lnspecific.py:153-155 with the
 //                    src + output_proj residual fused in via a broadcast row map)
+//   mmt_layernorm_bwd  its backward for the training step (dx, per-group dgamma / dbeta)
 //   mmt_groupnorm    nn.GroupNorm(32) after the fusion 1x1 convs (fusion_utils.py:252-268)
 //   mmt_add_cast     src + pos -> bf16 query staging (ms_deform_attn_bimodal.py:93-95)
 //   mmt_patch_im2col PatchEmbed input staging for the patch GEMM (mixformer.py:29-34, :237-247)
@@ -155,6 +156,124 @@ __global__ __launch_bounds__(GN_THREADS) void groupnorm_kernel(const float* __re
     }
 }
 
+// LayerNorm backward (training step): one wave per row, LNB_RPW rows per 256-thread workgroup.
+// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * gamma, xhat = (x - mean) * rstd with the
+// row statistics recomputed from x (two-pass, as the forward).  The affine gradients are per-lane
+// column partial sums over the workgroup's rows (one set per row group), reduced across the 4 waves
+// in LDS and stored per workgroup; layernorm_bwd_reduce_kernel then sums the workgroups' partials in
+// workgroup order (deterministic, no atomics) into dgb.
+constexpr int LNB_RPW = 32;
+
+template <typename TD, int V>
+__global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restrict__ x, const TD* __restrict__ dy,
+                                                            const float* g0, const float* g1, float* __restrict__ dx,
+                                                            float* __restrict__ part, int64_t rows, int64_t rpg,
+                                                            float eps) {
+    constexpr int C = 256 * V;
+    __shared__ float4 red[4][4][V][64];  // [wave][group x (dgamma, dbeta)][V][lane]
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    float4 pg[2][V], pb[2][V];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < V; ++i) pg[h][i] = pb[h][i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int r = w; r < LNB_RPW; r += 4) {
+        const int64_t row = (int64_t)blockIdx.x * LNB_RPW + r;
+        if (row >= rows) break;
+        const int h = (g1 && row >= rpg) ? 1 : 0;  // wave-uniform
+        const float4* gam = (const float4*)(h ? g1 : g0);
+        float4 v[V], d[V], ga[V];
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            const int idx = lane + 64 * i;
+            v[i] = ((const float4*)(x + row * C))[idx];
+            ga[i] = gam[idx];
+            if constexpr (sizeof(TD) == 2) {
+                const uint2 u = ((const uint2*)(dy + row * C))[idx];
+                const f32x2 a = unpack2<TD>(u.x), b = unpack2<TD>(u.y);
+                d[i] = make_float4(a[0], a[1], b[0], b[1]);
+            } else {
+                d[i] = ((const float4*)(dy + row * C))[idx];
+            }
+            s += v[i].x + v[i].y + v[i].z + v[i].w;
+        }
+        const float mean = wave_sum(s) * (1.f / C);
+        float q = 0.f;
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            v[i].x -= mean; v[i].y -= mean; v[i].z -= mean; v[i].w -= mean;
+            q += v[i].x * v[i].x + v[i].y * v[i].y + v[i].z * v[i].z + v[i].w * v[i].w;
+        }
+        const float rstd = rsqrtf(wave_sum(q) * (1.f / C) + eps);
+        float sg = 0.f, sgx = 0.f;
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            v[i].x *= rstd; v[i].y *= rstd; v[i].z *= rstd; v[i].w *= rstd;  // xhat
+            const float4 g = make_float4(d[i].x * ga[i].x, d[i].y * ga[i].y, d[i].z * ga[i].z, d[i].w * ga[i].w);
+            sg += g.x + g.y + g.z + g.w;
+            sgx += g.x * v[i].x + g.y * v[i].y + g.z * v[i].z + g.w * v[i].w;
+            float4& acg = pg[h][i];
+            float4& acb = pb[h][i];
+            acg.x += d[i].x * v[i].x; acg.y += d[i].y * v[i].y; acg.z += d[i].z * v[i].z; acg.w += d[i].w * v[i].w;
+            acb.x += d[i].x; acb.y += d[i].y; acb.z += d[i].z; acb.w += d[i].w;
+            d[i] = g;
+        }
+        const float mg = wave_sum(sg) * (1.f / C), mgx = wave_sum(sgx) * (1.f / C);
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            float4 o;
+            o.x = rstd * (d[i].x - mg - v[i].x * mgx);
+            o.y = rstd * (d[i].y - mg - v[i].y * mgx);
+            o.z = rstd * (d[i].z - mg - v[i].z * mgx);
+            o.w = rstd * (d[i].w - mg - v[i].w * mgx);
+            ((float4*)(dx + row * C))[lane + 64 * i] = o;
+        }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            red[w][2 * h][i][lane] = pg[h][i];
+            red[w][2 * h + 1][i][lane] = pb[h][i];
+        }
+    __syncthreads();
+    // thread t sums the 4 waves for (set j = t / 64, every V column chunk of lane t % 64), in wave order
+    const int j = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        float4 a = red[0][j][i][lane];
+#pragma unroll
+        for (int ww = 1; ww < 4; ++ww) {
+            const float4 b = red[ww][j][i][lane];
+            a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+        }
+        ((float4*)(part + ((int64_t)blockIdx.x * 4 + j) * C))[lane + 64 * i] = a;
+    }
+}
+
+// dgb[j][c] += sum over workgroups b (in order) of part[b][j][c]; j = group * 2 + (0 gamma, 1 beta).
+// One thread per (j, c); the partials are loaded 16 at a time (independent loads in flight) and added
+// in workgroup order, so the sum is the same on every launch.
+__global__ __launch_bounds__(64) void layernorm_bwd_reduce_kernel(const float* __restrict__ part, float* dgb, int nwg,
+                                                                  int C, int sets, int accumulate) {
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= sets * C) return;
+    const float* col = part + i;
+    const int64_t st = (int64_t)4 * C;
+    float s = 0.f;
+    int b = 0;
+    for (; b + 16 <= nwg; b += 16) {
+        float v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = col[(b + u) * st];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) s += v[u];
+    }
+    for (; b < nwg; ++b) s += col[b * st];
+    dgb[i] = accumulate ? dgb[i] + s : s;
+}
+
 template <typename T>
 __global__ void add_cast_kernel(const float* __restrict__ in, const float* __restrict__ add, int64_t add_n,
                                 float* out_f32, T* out_t, int64_t n4) {
@@ -223,15 +342,45 @@ extern "C" int mmt_layernorm(const float* in, const float* add, int64_t add_rows
 #define LN_CASE(T, V)                                                                                              \
     hipLaunchKernelGGL((layernorm_kernel<T, V>), grid, dim3(256), 0, st, in, add, add_rows, out_f32, (T*)out_t,  \
                        gamma0, beta0, gamma1, beta1, rows, rows_per_group, eps)
-    const int V = C / 256;
+    const int V = C / 256;  // 1..4 (the checks above): one instantiation each
     if (dtype == MMT_BF16) {
-        if (V == 2) LN_CASE(bf16_t, 2); else if (V == 3) LN_CASE(bf16_t, 3); else LN_CASE(bf16_t, 4);
+        if (V == 1) LN_CASE(bf16_t, 1); else if (V == 2) LN_CASE(bf16_t, 2); else if (V == 3) LN_CASE(bf16_t, 3); else LN_CASE(bf16_t, 4);
     } else if (dtype == MMT_F16) {
-        if (V == 2) LN_CASE(f16_t, 2); else if (V == 3) LN_CASE(f16_t, 3); else LN_CASE(f16_t, 4);
+        if (V == 1) LN_CASE(f16_t, 1); else if (V == 2) LN_CASE(f16_t, 2); else if (V == 3) LN_CASE(f16_t, 3); else LN_CASE(f16_t, 4);
     } else if (dtype == MMT_F32) {
-        if (V == 2) LN_CASE(float, 2); else if (V == 3) LN_CASE(float, 3); else LN_CASE(float, 4);
+        if (V == 1) LN_CASE(float, 1); else if (V == 2) LN_CASE(float, 2); else if (V == 3) LN_CASE(float, 3); else LN_CASE(float, 4);
     } else return MMT_EBADARG;
 #undef LN_CASE
+    return launch_status();
+}
+
+extern "C" int mmt_layernorm_bwd(const float* x, const void* dy, int dy_dtype, const float* gamma0,
+                                 const float* gamma1, float* dx, float* dgb, int dgb_accumulate, float* ws,
+                                 int64_t ws_floats, int64_t rows, int64_t rows_per_group, int C, float eps,
+                                 void* stream) {
+    if (!x || !dy || !gamma0 || !dx || !dgb || !ws || rows <= 0 || (C % 256) || C < 256 || C > 1024) return MMT_EBADARG;
+    if (gamma1 && rows_per_group <= 0) return MMT_EBADARG;
+    if (!gamma1) rows_per_group = rows;
+    if (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)gamma0 | (uintptr_t)gamma1 | (uintptr_t)dx | (uintptr_t)ws) & 15)
+        return MMT_EBADARG;
+    const int64_t nwg = (rows + LNB_RPW - 1) / LNB_RPW;
+    if (nwg > INT32_MAX || ws_floats < nwg * 4 * C) return MMT_EBADARG;
+    hipStream_t st = (hipStream_t)stream;
+    const int V = C / 256;
+#define LNB_CASE(TD, VV)                                                                                           \
+    hipLaunchKernelGGL((layernorm_bwd_kernel<TD, VV>), dim3((unsigned)nwg), dim3(256), 0, st, x, (const TD*)dy,    \
+                       gamma0, gamma1, dx, ws, rows, rows_per_group, eps)
+#define LNB_V(TD)                                                                                                  \
+    if (V == 1) LNB_CASE(TD, 1); else if (V == 2) LNB_CASE(TD, 2); else if (V == 3) LNB_CASE(TD, 3); else LNB_CASE(TD, 4)
+    if (dy_dtype == MMT_BF16) { LNB_V(bf16_t); }
+    else if (dy_dtype == MMT_F16) { LNB_V(f16_t); }
+    else if (dy_dtype == MMT_F32) { LNB_V(float); }
+    else return MMT_EBADARG;
+#undef LNB_V
+#undef LNB_CASE
+    const int sets = gamma1 ? 4 : 2;
+    hipLaunchKernelGGL(layernorm_bwd_reduce_kernel, dim3((unsigned)((sets * C + 63) / 64)), dim3(64), 0, st, ws, dgb,
+                       (int)nwg, C, sets, dgb_accumulate);
     return launch_status();
 }
 

@@ -18,7 +18,8 @@ kernel, log-sum-exp kept) and backward (mmt_mam_attention_bwd).  The fusion enco
 sampling runs on mmt_ms_deform_attn_forward / _backward (mmt_amd.functional.MSDeformAttnFunction,
 the reference's MSDeformAttnFunction).  Clipping + AdamW is mmt_adamw_step (mmt_amd.optim.HipAdamW,
 three launches over every parameter, writing the bf16 copies of the backbone weights the GEMMs
-read).  LayerNorm / GELU / residual adds and the corner head run as PyTorch-ROCm ops on the same
+read).  The backbone LayerNorms run on mmt_layernorm / mmt_layernorm_bwd (_HipLayerNorm).  GELU / residual
+adds, the encoder's LayerNorms and the corner head run as PyTorch-ROCm ops on the same
 module tree (`nn.Conv2d`, `nn.GroupNorm`, `SyncBatchNorm` under DDP), in bf16 autocast like the
 reference's AMP path.  The backbone ops are injected (`ops`), so the data-parallel plumbing can be exercised on CPU
 with stand-in ops in tests; the product's ops are `HipOps` and have no CPU path.
@@ -131,10 +132,72 @@ class _HipMamAttention(torch.autograd.Function):
         return mam_attention_backward(qkv, out, dout, lse, ctx.n_t, ctx.heads), None, None
 
 
+class _HipLayerNorm(torch.autograd.Function):
+    """nn.LayerNorm over the last dim of the fp32 residual stream -> bf16 (the next Linear's operand),
+    rows [0, rows0) with (w0, b0) and the rest with (w1, b1) (the shared backbone's per-modality
+    norm*_v / norm*_i) or all rows with (w0, b0): forward mmt_layernorm, backward mmt_layernorm_bwd
+    (dx, dgamma / dbeta from the saved fp32 input; statistics recomputed)."""
+
+    @staticmethod
+    def forward(ctx, x, w0, b0, w1, b1, rows0, eps):
+        from ._lib import LIB, MMT_BF16, check
+        C = x.shape[-1]
+        x2 = x.reshape(-1, C).contiguous()
+        rows = x2.shape[0]
+        two = w1 is not None  # (LayerNorm parameters are contiguous fp32 leaves)
+        out = torch.empty(rows, C, device=x.device, dtype=torch.bfloat16)
+        check(LIB.mmt_layernorm(x2.data_ptr(), None, 0, None, out.data_ptr(), w0.data_ptr(), b0.data_ptr(),
+                                w1.data_ptr() if two else None, b1.data_ptr() if two else None, rows,
+                                rows0 if two else rows, C, eps, MMT_BF16, _stream()), "mmt_layernorm")
+        ctx.save_for_backward(x2, w0, w1 if two else w0)
+        ctx.two, ctx.rows0, ctx.eps, ctx.shape = two, rows0, eps, x.shape
+        return out.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        from ._lib import LIB, MMT_BF16, MMT_F32, check
+        x2, g0, g1 = ctx.saved_tensors
+        rows, C = x2.shape
+        dy = dy.reshape(rows, C).contiguous()
+        code = {torch.bfloat16: MMT_BF16, torch.float32: MMT_F32}[dy.dtype]
+        sets = 4 if ctx.two else 2
+        nws = (rows + 31) // 32 * 4 * C
+        buf = torch.empty(rows * C + sets * C + nws, device=x2.device, dtype=torch.float32)  # one allocation
+        dx, dgb, ws = buf[:rows * C].view(rows, C), buf[rows * C:(rows + sets) * C].view(sets, C), buf[(rows + sets) * C:]
+        check(LIB.mmt_layernorm_bwd(x2.data_ptr(), dy.data_ptr(), code, g0.data_ptr(),
+                                    g1.data_ptr() if ctx.two else None, dx.data_ptr(), dgb.data_ptr(), 0,
+                                    ws.data_ptr(), ws.numel(), rows, ctx.rows0 if ctx.two else rows, C, ctx.eps,
+                                    _stream()), "mmt_layernorm_bwd")
+        if ctx.two:
+            return dx.view(ctx.shape), dgb[0], dgb[1], dgb[2], dgb[3], None, None
+        return dx.view(ctx.shape), dgb[0], dgb[1], None, None, None, None
+
+
+def _layer_norm(ops, x, a, b=None, eps=1e-6):
+    """LayerNorm of the fp32 stream x to ops.dtype: norm module a on every row, or a on the first half of
+    the rows and b on the second (per-modality norms of the shared backbone).  ops.layer_norm when the
+    ops provide one (HipOps: the HIP kernels), else aten's (stand-in ops of the CPU tests)."""
+    ln = getattr(ops, "layer_norm", None)
+    if ln is not None:
+        return ln(x, a.weight, a.bias, eps, b.weight if b is not None else None, b.bias if b is not None else None)
+    C = x.shape[-1]
+    if b is None:
+        return F.layer_norm(x, (C,), a.weight, a.bias, eps).to(ops.dtype)
+    h = x.shape[0] // 2
+    return torch.cat([F.layer_norm(x[:h], (C,), a.weight, a.bias, eps),
+                      F.layer_norm(x[h:], (C,), b.weight, b.bias, eps)], 0).to(ops.dtype)
+
+
 class HipOps:
     """The backbone's matrix work on libmmt_hip.so (bf16 in, bf16 out)."""
 
     dtype = torch.bfloat16  # activation dtype of the GEMM / attention operands
+
+    @staticmethod
+    def layer_norm(x, w0, b0, eps, w1=None, b1=None):
+        """x [2h or n, ..., C] fp32 -> bf16; (w1, b1) given: rows of the second half of dim 0 take them."""
+        rows0 = x.numel() // x.shape[-1] // 2 if w1 is not None else 0
+        return _HipLayerNorm.apply(x, w0, b0, w1, b1, rows0, eps)
 
     @staticmethod
     def linear(x, weight, bias, out_f32=False):
@@ -220,12 +283,12 @@ def backbone_forward(bb, t, o, s, ops, drop_path_rate=DROP_PATH_RATE):
     depth = len(bb.blocks)
     for li, blk in enumerate(bb.blocks):
         dp = drop_path_rate * li / max(depth - 1, 1)
-        xn = F.layer_norm(x, (C,), blk.norm1.weight, blk.norm1.bias, 1e-6).to(ops.dtype)
+        xn = _layer_norm(ops, x, blk.norm1)
         qkv = ops.linear(xn.view(B * ntok, C), blk.attn.qkv.weight, blk.attn.qkv.bias).view(B, ntok, 3 * C)
         a = ops.mam_attention(qkv, n_t, H).view(B * ntok, C)
         x = _residual(x, ops.linear(a, blk.attn.proj.weight, blk.attn.proj.bias, out_f32=True).view(B, ntok, C), dp,
                       bb.training)
-        xn = F.layer_norm(x, (C,), blk.norm2.weight, blk.norm2.bias, 1e-6).to(ops.dtype)
+        xn = _layer_norm(ops, x, blk.norm2)
         h = ops.linear(xn.view(B * ntok, C), blk.mlp.fc1.weight, blk.mlp.fc1.bias)
         h = F.gelu(h) if h.dtype == ops.dtype else F.gelu(h.float()).to(ops.dtype)  # bf16 in/out, fp32 math
         x = _residual(x, ops.linear(h, blk.mlp.fc2.weight, blk.mlp.fc2.bias, out_f32=True).view(B, ntok, C), dp,
@@ -254,8 +317,7 @@ def backbone_forward_stacked(bb, t, o, s, ops, asym=False, drop_path_rate=DROP_P
     depth = len(bb.blocks)
 
     def ln2(x, a, b):  # norm*_v on the RGB half, norm*_i on the TIR half
-        return torch.cat([F.layer_norm(x[:Bh], (C,), a.weight, a.bias, 1e-6),
-                          F.layer_norm(x[Bh:], (C,), b.weight, b.bias, 1e-6)], 0).to(ops.dtype)
+        return _layer_norm(ops, x, a, b)
 
     for li, blk in enumerate(bb.blocks):
         dp = drop_path_rate * li / max(depth - 1, 1)

@@ -610,7 +610,7 @@ def test_mam_attention_pipelined_is_default_and_bitwise(asym):
 
 
 @pytest.mark.parametrize("dname", ["f32", "bf16", "fp16"])
-@pytest.mark.parametrize("C", [512, 768, 1024])
+@pytest.mark.parametrize("C", [256, 512, 768, 1024])
 def test_layernorm_groups_and_add(dname, C):
     dt = DT[dname]
     L = _lib()

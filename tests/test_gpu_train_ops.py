@@ -357,3 +357,81 @@ def test_hip_adamw_matches_torch(max_norm):
         sh, ver = hip[1]._mmt_bf16
         assert ver == hip[1]._version and torch.equal(sh, hip[1].detach().to(torch.bfloat16))
 
+
+
+@pytest.mark.parametrize("C,rows,two,dyt", [(768, 1056, False, "bf16"), (768, 1000, True, "bf16"), (512, 77, True, "f32"),
+                                            (1024, 300, False, "f32"), (256, 33, True, "bf16")])
+def test_layernorm_backward_matches_autograd(C, rows, two, dyt):
+    """mmt_layernorm_bwd (the training step's backbone LayerNorms) against torch fp32 autograd of
+    F.layer_norm on the same input and output gradient: dx, and dgamma / dbeta of each row group
+    (rows [0, rows0) -> norm 0, the rest -> norm 1), including a ragged last workgroup; bitwise
+    repeatable (fixed-order partial sums) and accumulating into dgb on request."""
+    L = _lib()
+    g = torch.Generator().manual_seed(C + rows)
+    x = torch.randn(rows, C, generator=g) * 3 + 0.5
+    gam = torch.randn(2, C, generator=g)
+    dt = {"bf16": torch.bfloat16, "f32": torch.float32}[dyt]
+    dy = torch.randn(rows, C, generator=g).to(dt)
+    rows0 = rows // 2 if two else rows
+    xd, gd, dyd = x.cuda(), gam.cuda(), dy.cuda()
+    outs = []
+    for rep in range(2):
+        dx = torch.empty(rows, C, device="cuda")
+        dgb = torch.full((4 if two else 2, C), 1.0 if rep else 0.0, device="cuda")
+        ws = torch.empty((rows + 31) // 32 * 4 * C, device="cuda")
+        L.check(L.LIB.mmt_layernorm_bwd(xd.data_ptr(), dyd.data_ptr(), {"bf16": L.MMT_BF16, "f32": L.MMT_F32}[dyt],
+                                        gd[0].data_ptr(), gd[1].data_ptr() if two else None, dx.data_ptr(),
+                                        dgb.data_ptr(), rep, ws.data_ptr(), ws.numel(), rows, rows0, C, 1e-6,
+                                        torch.cuda.current_stream().cuda_stream), "ln bwd")
+        torch.cuda.synchronize()
+        outs.append((dx.cpu(), dgb.cpu() - (1.0 if rep else 0.0)))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert (outs[0][1] - outs[1][1]).abs().max().item() <= 1e-6 * max(1.0, outs[0][1].abs().max().item())
+    dx, dgb = outs[0]
+    xr = x.clone().requires_grad_(True)
+    ws_, bs_ = [], []
+    parts = [(0, rows0, 0), (rows0, rows, 1)] if two else [(0, rows, 0)]
+    ys = []
+    for a, b, h in parts:
+        w = gam[h].clone().requires_grad_(True)
+        bb = torch.zeros(C, requires_grad=True)
+        ws_.append(w), bs_.append(bb)
+        ys.append(torch.nn.functional.layer_norm(xr[a:b], (C,), w, bb, 1e-6))
+    torch.cat(ys).backward(dy.float())
+    assert (dx - xr.grad).abs().max().item() <= 2e-4 * max(1.0, xr.grad.abs().max().item())
+    for i, (w, bb) in enumerate(zip(ws_, bs_)):
+        assert (dgb[2 * i] - w.grad).abs().max().item() <= 2e-4 * max(1.0, w.grad.abs().max().item())
+        assert (dgb[2 * i + 1] - bb.grad).abs().max().item() <= 2e-4 * max(1.0, bb.grad.abs().max().item())
+
+
+@pytest.mark.parametrize("two", [False, True])
+def test_hip_layernorm_autograd(two):
+    """HipOps.layer_norm (mmt_layernorm -> bf16, mmt_layernorm_bwd) as the training forward calls it
+    (fp32 residual stream in, the next Linear's bf16 operand out) against aten's layer_norm + cast."""
+    from mmt_amd.train import HipOps
+    g = torch.Generator().manual_seed(3 + two)
+    B, ntok, C = 4, 100, 768
+    x = (torch.randn(B, ntok, C, generator=g) * 2).cuda()
+    n = [torch.nn.LayerNorm(C, eps=1e-6).cuda() for _ in range(2)]
+    for m in n:
+        with torch.no_grad():
+            m.weight.copy_(torch.randn(C, generator=g).cuda())
+            m.bias.copy_(torch.randn(C, generator=g).cuda())
+    dy = torch.randn(B, ntok, C, generator=g).cuda().bfloat16()
+    xa = x.clone().requires_grad_(True)
+    ya = HipOps.layer_norm(xa, n[0].weight, n[0].bias, 1e-6, n[1].weight if two else None, n[1].bias if two else None)
+    assert ya.dtype == torch.bfloat16 and ya.shape == x.shape
+    ya.backward(dy)
+    ga = [xa.grad] + [p.grad.clone() for m in (n if two else n[:1]) for p in (m.weight, m.bias)]
+    for m in n:
+        m.weight.grad = m.bias.grad = None
+    xb = x.clone().requires_grad_(True)
+    if two:
+        yb = torch.cat([n[0](xb[:B // 2]), n[1](xb[B // 2:])]).bfloat16()
+    else:
+        yb = n[0](xb).bfloat16()
+    assert (ya.float() - yb.float()).abs().max().item() <= 3e-2
+    yb.backward(dy)
+    gb = [xb.grad] + [p.grad for m in (n if two else n[:1]) for p in (m.weight, m.bias)]
+    for a, b in zip(ga, gb):
+        assert (a - b).abs().max().item() <= 1e-3 * max(1.0, b.abs().max().item())
