@@ -75,9 +75,11 @@ extern "C" {
  *   conv producing a conv_h x conv_h map; the input map is conv_h/conv_up square, pixel stride
  *   lda (channels are contiguous, conv_cin of them), k = (ky*3+kx)*conv_cin + ci; consecutive
  *   input images a_stride_a pixels apart (0: packed, (conv_h/conv_up)^2).
- * Epilogue: v = act(acc + bias) with act 0 none / 1 GELU(erf) / 2 ReLU;
- *   c2 == NULL: C = v (+ R if r != NULL);  c2 != NULL: C = v, C2 = v + R (c2_copy: C = v (+ R),
- *   C2 = the same values in `dtype`).
+ * Epilogue: v = act(acc + bias) with act 0 none / 1 GELU(erf) / 2 ReLU / 5 GELU backward:
+ *   v = (acc + bias) * GELU'(R) (R then not added; 16-bit LDS-DMA kernels);
+ *   c2 == NULL: C = v (+ R if r != NULL);  c2 != NULL: C = v, C2 = v + R (c2_copy 1: C = v (+ R),
+ *   C2 = the same values in `dtype`; c2_copy 2: C = v (+ R), C2 = acc + bias, the pre-activation, in
+ *   `dtype`, no R needed -- the training step's fc1 keeps it for the GELU backward).
  *   R row index: r_mode 0 -> m, 1 -> m % r_p0, 2 -> conv map m=(b,y,x) of an r_p0 x r_p0 map read
  *   at (y / r_p1, x / r_p1) of an (r_p0/r_p1)^2 map.  R is fp32 (or dtype if r_t); C/C2 are fp32
  *   if c_f32 else dtype.

@@ -96,6 +96,26 @@ MMT_DEV f32x2 gelu_erf2(f32x2 x) {
     return __builtin_elementwise_fma(h, s, h);
 }
 
+// d GELU(x) / dx = Phi(x) + x phi(x) for two values, with gelu_erf2's erf approximation:
+// Phi(x) = 0.5 (1 + sign(x) erf(|x| / sqrt 2)), phi(x) = exp(-x^2 / 2) / sqrt(2 pi) (the same exponential)
+MMT_DEV f32x2 gelu_erf_grad2(f32x2 x) {
+    const f32x2 z = x * 0.70710678118654752440f;
+    const f32x2 a = __builtin_elementwise_abs(z);
+    const f32x2 d = __builtin_elementwise_fma(a, f32x2(0.3275911f), f32x2(1.0f));
+    const f32x2 t = {__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+    f32x2 y = __builtin_elementwise_fma(t, f32x2(1.061405429f), f32x2(-1.453152027f));
+    y = __builtin_elementwise_fma(y, t, f32x2(1.421413741f));
+    y = __builtin_elementwise_fma(y, t, f32x2(-0.284496736f));
+    y = __builtin_elementwise_fma(y, t, f32x2(0.254829592f));
+    y = y * t;
+    const f32x2 q = a * (a * -1.44269504088896340736f);
+    const f32x2 e = {__builtin_amdgcn_exp2f(q[0]), __builtin_amdgcn_exp2f(q[1])};  // exp(-x^2 / 2)
+    const f32x2 r = __builtin_elementwise_fma(-y, e, f32x2(1.0f));                  // erf(|z|)
+    const f32x2 s = {copysignf(r[0], x[0]), copysignf(r[1], x[1])};
+    const f32x2 phi = __builtin_elementwise_fma(s, f32x2(0.5f), f32x2(0.5f));        // Phi(x)
+    return __builtin_elementwise_fma(x * 0.39894228040143267794f, e, phi);
+}
+
 MMT_DEV float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -326,6 +326,7 @@ int check_gemm(const mmt_gemm_params& p) {
     const int EPC = 16 / (int)sizeof(T);
     if (p.M <= 0 || p.N <= 0 || p.K <= 0 || p.groups < 1 || p.groups > MMT_MAX_GROUPS) return MMT_EBADARG;
     if (p.impl < -1 || p.impl > 7) return MMT_EBADARG;
+    if (p.act < 0 || (p.act > 2 && p.act != 5) || p.c2_copy < 0 || p.c2_copy > 2) return MMT_EBADARG;
     if (p.K % EPC || p.lda % EPC) return MMT_EBADARG;
     if (p.conv_h > 0) {
         if (p.conv_cin % EPC || p.conv_up < 1 || p.conv_h % p.conv_up) return MMT_EBADARG;
@@ -342,7 +343,8 @@ int check_gemm(const mmt_gemm_params& p) {
         if (!p.a[g] || !p.w[g] || !p.c[g]) return MMT_EBADARG;
         if (((uintptr_t)p.a[g] | (uintptr_t)p.w[g]) & 15) return MMT_EBADARG;
         if (p.k_split > 0 && p.conv_h == 0 && (!p.a1[g] || ((uintptr_t)p.a1[g] & 15))) return MMT_EBADARG;
-        if (p.c2[g] && !p.r[g]) return MMT_EBADARG;
+        if (p.c2[g] && !p.r[g] && p.c2_copy != 2) return MMT_EBADARG;
+        if ((p.act == 5 && !p.r[g]) || (p.c2_copy == 2 && !p.c2[g])) return MMT_EBADARG;
     }
     return 0;
 }
@@ -360,7 +362,7 @@ int launch_gemm(const mmt_gemm_params& p, hipStream_t st) {
     }
     if constexpr (sizeof(T) == 2)
         if (mmt_gemm_glds<T>(p, st, p.impl) == 0) return launch_status();
-    if (p.ln_fold || p.c2_copy) return MMT_EBADARG;  // LDS-DMA kernel features only
+    if (p.ln_fold || p.c2_copy || p.act == 5) return MMT_EBADARG;  // LDS-DMA kernel features only
     if (p.conv_h > 0) launch_tiles<T, true>(p, st);
     else launch_tiles<T, false>(p, st);
     return launch_status();

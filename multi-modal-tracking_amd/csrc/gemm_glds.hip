@@ -585,6 +585,14 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
             }
             va += bn0;
             vb += bn1;
+            const f32x4 prea = va, preb = vb;  // pre-activation (c2_copy 2)
+            if (p.act == 5) {  // GELU backward: (acc + bias) * GELU'(R), R not added
+                const f32x2 g0 = gelu_erf_grad2(ra[i].xy), g1 = gelu_erf_grad2(ra[i].zw);
+                const f32x2 g2 = gelu_erf_grad2(rb[i].xy), g3 = gelu_erf_grad2(rb[i].zw);
+                va = f32x4{va[0] * g0[0], va[1] * g0[1], va[2] * g1[0], va[3] * g1[1]};
+                vb = f32x4{vb[0] * g2[0], vb[1] * g2[1], vb[2] * g3[0], vb[3] * g3[1]};
+                ra[i] = rb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
             if (p.act == 1) {
                 va.xy = gelu_erf2(va.xy);
                 va.zw = gelu_erf2(va.zw);
@@ -620,7 +628,10 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
                 if (p.c_f32) {
                     *(f32x4*)((float*)C + e) = oa;
                     *(f32x4*)((float*)C + e + 4) = ob;
-                    if (C2 && p.c2_copy) {  // compute-dtype copy of C (the next LayerNorm-folded GEMM's A)
+                    if (C2 && p.c2_copy == 2) {  // the pre-activation in the compute dtype
+                        *(u32x4*)((T*)C2 + e) = u32x4{pack2<T>(prea[0], prea[1]), pack2<T>(prea[2], prea[3]),
+                                                      pack2<T>(preb[0], preb[1]), pack2<T>(preb[2], preb[3])};
+                    } else if (C2 && p.c2_copy) {  // compute-dtype copy of C (the next LayerNorm-folded GEMM's A)
                         *(u32x4*)((T*)C2 + e) = u32x4{pack2<T>(sa[0], sa[1]), pack2<T>(sa[2], sa[3]),
                                                       pack2<T>(sb[0], sb[1]), pack2<T>(sb[2], sb[3])};
                     } else if (C2) {
@@ -630,7 +641,10 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
                 } else {
                     *(u32x4*)((T*)C + e) = u32x4{pack2<T>(oa[0], oa[1]), pack2<T>(oa[2], oa[3]),
                                                  pack2<T>(ob[0], ob[1]), pack2<T>(ob[2], ob[3])};
-                    if (C2)
+                    if (C2 && p.c2_copy == 2)
+                        *(u32x4*)((T*)C2 + e) = u32x4{pack2<T>(prea[0], prea[1]), pack2<T>(prea[2], prea[3]),
+                                                      pack2<T>(preb[0], preb[1]), pack2<T>(preb[2], preb[3])};
+                    else if (C2)
                         *(u32x4*)((T*)C2 + e) = u32x4{pack2<T>(sa[0], sa[1]), pack2<T>(sa[2], sa[3]),
                                                       pack2<T>(sb[0], sb[1]), pack2<T>(sb[2], sb[3])};
                 }

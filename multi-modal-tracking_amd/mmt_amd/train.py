@@ -18,8 +18,9 @@ kernel, log-sum-exp kept) and backward (mmt_mam_attention_bwd).  The fusion enco
 sampling runs on mmt_ms_deform_attn_forward / _backward (mmt_amd.functional.MSDeformAttnFunction,
 the reference's MSDeformAttnFunction).  Clipping + AdamW is mmt_adamw_step (mmt_amd.optim.HipAdamW,
 three launches over every parameter, writing the bf16 copies of the backbone weights the GEMMs
-read).  The backbone LayerNorms run on mmt_layernorm / mmt_layernorm_bwd (_HipLayerNorm).  GELU / residual
-adds, the encoder's LayerNorms and the corner head run as PyTorch-ROCm ops on the same
+read).  The backbone LayerNorms run on mmt_layernorm / mmt_layernorm_bwd (_HipLayerNorm), and each
+block's MLP is one autograd Function whose GELU and GELU backward live in GEMM epilogues (_HipMlp).  The
+residual adds, the encoder's LayerNorms and the corner head run as PyTorch-ROCm ops on the same
 module tree (`nn.Conv2d`, `nn.GroupNorm`, `SyncBatchNorm` under DDP), in bf16 autocast like the
 reference's AMP path.  The backbone ops are injected (`ops`), so the data-parallel plumbing can be exercised on CPU
 with stand-in ops in tests; the product's ops are `HipOps` and have no CPU path.
@@ -67,8 +68,10 @@ def _transpose(x, rows, cols, ld_out=None, ones_row=False):
     return out
 
 
-def _gemm(a, w, M, N, K, bias=None, out_f32=False):
-    """C[M][N] = A[M][K] W[N][K]^T (+ bias), bf16 operands, fp32 accumulation (mmt_gemm)."""
+def _gemm(a, w, M, N, K, bias=None, out_f32=False, act=0, r=None, c2=None, c2_copy=0):
+    """C[M][N] = A[M][K] W[N][K]^T (+ bias), bf16 operands, fp32 accumulation (mmt_gemm); act / r (bf16,
+    [M][N]) / c2 / c2_copy as mmt_gemm_params (act 1 GELU, 5 GELU backward against r; c2_copy 2: c2 = the
+    pre-activation)."""
     from ._lib import LIB, GemmParams, MMT_BF16, check
     c = torch.empty(M, N, device=a.device, dtype=torch.float32 if out_f32 else torch.bfloat16)
     p = GemmParams()
@@ -77,8 +80,27 @@ def _gemm(a, w, M, N, K, bias=None, out_f32=False):
     p.lda, p.ldc = K, N
     p.a_seg_rows, p.a_segs_a = M, 1
     p.M, p.N, p.K, p.groups, p.c_f32 = M, N, K, 1, 1 if out_f32 else 0
+    p.act = act
+    if r is not None:
+        p.r[0], p.ldr, p.r_t = r.data_ptr(), N, 1
+    if c2 is not None:
+        p.c2[0], p.c2_copy = c2.data_ptr(), c2_copy
     check(LIB.mmt_gemm(p, MMT_BF16, _stream()), "mmt_gemm")
     return c
+
+
+def _bf16_weight(w):
+    """The bf16 copy of an fp32 master weight HipAdamW's update wrote (same values), else a fresh cast."""
+    sh = getattr(w, "_mmt_bf16", None)
+    return sh[0] if sh is not None and sh[1] == w._version else w.detach().to(torch.bfloat16).contiguous()
+
+
+def _weight_grads(dy, x, M, N, K):
+    """dW [N][K] and db [N] of y = x W^T + b from one GEMM: dy^T [x | 1] (a row of ones appended to the
+    transposed activations gives the bias gradient as output column K; fp32 accumulation)."""
+    Mp = (M + 7) // 8 * 8  # contraction over tokens, zero-padded to the GEMM's K granule
+    dwb = _gemm(_transpose(dy, M, N, Mp), _transpose(x, M, K, Mp, ones_row=True), N, K + 8, Mp, out_f32=True)
+    return dwb[:, :K], dwb[:, K]
 
 
 class _HipLinear(torch.autograd.Function):
@@ -90,8 +112,7 @@ class _HipLinear(torch.autograd.Function):
         M, K = x.shape
         N = w.shape[0]
         x = x.contiguous()
-        sh = getattr(w, "_mmt_bf16", None)  # bf16 shadow written by HipAdamW's update (same values)
-        wb = sh[0] if sh is not None and sh[1] == w._version else w.detach().to(torch.bfloat16).contiguous()
+        wb = _bf16_weight(w)  # bf16 shadow written by HipAdamW's update (same values)
         y = _gemm(x, wb, M, N, K, bias=b.detach().float().contiguous(), out_f32=out_f32)
         ctx.save_for_backward(x, wb)
         return y
@@ -110,6 +131,37 @@ class _HipLinear(torch.autograd.Function):
         # strided views: autograd accumulates them into the persistent .grad buffers with one add
         # (HipAdamW keeps the gradients allocated), so a contiguous copy first would be a wasted pass
         return dx, dwb[:, :K], dwb[:, K], None
+
+
+class _HipMlp(torch.autograd.Function):
+    """timm Mlp of the ViT blocks (mixformer.py:136-139): y = fc2(GELU(fc1(x))) with x [M][C] bf16, y [M][C]
+    fp32 (the residual branch).  fc1 runs with the GELU epilogue and also stores its pre-activation (bf16,
+    c2_copy 2); the backward's dX GEMM of fc2 multiplies by GELU'(pre-activation) in its epilogue (act 5),
+    so neither the activation nor its gradient is a separate pass."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2):
+        M, C = x.shape
+        F4 = w1.shape[0]
+        x = x.contiguous()
+        wb1, wb2 = _bf16_weight(w1), _bf16_weight(w2)
+        hp = torch.empty(M, F4, device=x.device, dtype=torch.bfloat16)
+        h = _gemm(x, wb1, M, F4, C, bias=b1.detach(), act=1, c2=hp, c2_copy=2)
+        y = _gemm(h, wb2, M, C, F4, bias=b2.detach(), out_f32=True)
+        ctx.save_for_backward(x, wb1, wb2, h, hp)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wb1, wb2, h, hp = ctx.saved_tensors
+        M, C = x.shape
+        F4 = wb1.shape[0]
+        dy = dy.to(torch.bfloat16).contiguous()
+        dhp = _gemm(dy, _transpose(wb2, C, F4), M, F4, C, act=5, r=hp)  # d(pre-activation), bf16
+        dw2, db2 = _weight_grads(dy, h, M, C, F4)
+        dx = _gemm(dhp, _transpose(wb1, F4, C), M, C, F4) if ctx.needs_input_grad[0] else None
+        dw1, db1 = _weight_grads(dhp, x, M, F4, C)
+        return dx, dw1, db1, dw2, db2
 
 
 class _HipMamAttention(torch.autograd.Function):
@@ -173,6 +225,17 @@ class _HipLayerNorm(torch.autograd.Function):
         return dx.view(ctx.shape), dgb[0], dgb[1], None, None, None, None
 
 
+def _mlp(ops, x, mlp):
+    """timm Mlp (fc1 -> GELU -> fc2) of a block on x [M][C] in ops.dtype -> fp32: ops.mlp when the ops
+    provide one (HipOps: fused GELU epilogues), else two ops.linear calls around aten's GELU."""
+    fn = getattr(ops, "mlp", None)
+    if fn is not None:
+        return fn(x, mlp.fc1.weight, mlp.fc1.bias, mlp.fc2.weight, mlp.fc2.bias)
+    h = ops.linear(x, mlp.fc1.weight, mlp.fc1.bias)
+    h = F.gelu(h) if h.dtype == ops.dtype else F.gelu(h.float()).to(ops.dtype)  # bf16 in/out, fp32 math
+    return ops.linear(h, mlp.fc2.weight, mlp.fc2.bias, out_f32=True)
+
+
 def _layer_norm(ops, x, a, b=None, eps=1e-6):
     """LayerNorm of the fp32 stream x to ops.dtype: norm module a on every row, or a on the first half of
     the rows and b on the second (per-modality norms of the shared backbone).  ops.layer_norm when the
@@ -202,6 +265,11 @@ class HipOps:
     @staticmethod
     def linear(x, weight, bias, out_f32=False):
         return _HipLinear.apply(x, weight, bias, out_f32)
+
+    @staticmethod
+    def mlp(x, w1, b1, w2, b2):
+        """fc2(GELU(fc1(x))), x [M][C] bf16 -> fp32 (_HipMlp)."""
+        return _HipMlp.apply(x, w1, b1, w2, b2)
 
     @staticmethod
     def mam_attention(qkv, n_t, heads):
@@ -289,10 +357,7 @@ def backbone_forward(bb, t, o, s, ops, drop_path_rate=DROP_PATH_RATE):
         x = _residual(x, ops.linear(a, blk.attn.proj.weight, blk.attn.proj.bias, out_f32=True).view(B, ntok, C), dp,
                       bb.training)
         xn = _layer_norm(ops, x, blk.norm2)
-        h = ops.linear(xn.view(B * ntok, C), blk.mlp.fc1.weight, blk.mlp.fc1.bias)
-        h = F.gelu(h) if h.dtype == ops.dtype else F.gelu(h.float()).to(ops.dtype)  # bf16 in/out, fp32 math
-        x = _residual(x, ops.linear(h, blk.mlp.fc2.weight, blk.mlp.fc2.bias, out_f32=True).view(B, ntok, C), dp,
-                      bb.training)
+        x = _residual(x, _mlp(ops, xn.view(B * ntok, C), blk.mlp).view(B, ntok, C), dp, bb.training)
     xs = x[:, n_t:]
     return xs.transpose(1, 2).reshape(B, C, gs, gs)
 
@@ -327,10 +392,7 @@ def backbone_forward_stacked(bb, t, o, s, ops, asym=False, drop_path_rate=DROP_P
         x = _residual(x, ops.linear(a.reshape(B2 * ntok, C), blk.attn.proj.weight, blk.attn.proj.bias, out_f32=True)
                       .view(B2, ntok, C), dp, bb.training)
         xn = ln2(x, blk.norm2_v, blk.norm2_i)
-        h = ops.linear(xn.view(B2 * ntok, C), blk.mlp.fc1.weight, blk.mlp.fc1.bias)
-        h = F.gelu(h) if h.dtype == ops.dtype else F.gelu(h.float()).to(ops.dtype)  # bf16 in/out, fp32 math
-        x = _residual(x, ops.linear(h, blk.mlp.fc2.weight, blk.mlp.fc2.bias, out_f32=True).view(B2, ntok, C), dp,
-                      bb.training)
+        x = _residual(x, _mlp(ops, xn.view(B2 * ntok, C), blk.mlp).view(B2, ntok, C), dp, bb.training)
     return x[:, n_t:].transpose(1, 2).reshape(B2, C, gs, gs), x[:, :gt * gt]
 
 

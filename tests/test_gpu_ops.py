@@ -173,6 +173,49 @@ def test_gemm_bf16_tile_paths(impl, M, N, K):
             assert e3 <= 1e-3 * r3.abs().max().item() + 1e-4, (grp, e3)
 
 
+@pytest.mark.parametrize("impl", [-1, 0, 1, 2, 3, 4, 5, 6, 7])
+def test_gemm_gelu_backward_and_preact_epilogues(impl):
+    """The training MLP's epilogues: act 1 with c2_copy 2 (C = GELU(acc + b), C2 = acc + b in bf16) and
+    act 5 (C = (acc + b) * GELU'(R), R bf16); 16-bit LDS-DMA kernels only (impl -1, the register-staged
+    kernel, rejects both)."""
+    L = _lib()
+    M, N, K = 528, 768, 256
+    g = torch.Generator().manual_seed(impl + 40)
+    A = torch.randn(M, K, generator=g).bfloat16()
+    W = (torch.randn(N, K, generator=g) / math.sqrt(K)).bfloat16()
+    b = torch.randn(N, generator=g)
+    R = (torch.randn(M, N, generator=g) * 2).bfloat16()
+    Ad, Wd, bd, Rd = A.cuda(), W.cuda(), b.cuda(), R.cuda()
+    pre = A.float() @ W.float().t() + b
+    c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    c2 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    p = _gemm_params([Ad.data_ptr()], [Wd.data_ptr()], [c.data_ptr()], M, N, K, K, N, bias=[bd.data_ptr()], act=1,
+                     c2=[c2.data_ptr()], c2_copy=2, impl=impl)
+    st = torch.cuda.current_stream().cuda_stream
+    rc = L.LIB.mmt_gemm(p, L.MMT_BF16, st)
+    if impl == -1:
+        assert rc == -10000
+    else:
+        L.check(rc, "gemm act1 c2_copy2")
+        torch.cuda.synchronize()
+        assert (c2.float().cpu() - pre).abs().max().item() <= 2e-2 * pre.abs().max().item()
+        gel = F.gelu(pre)
+        assert (c.float().cpu() - gel).abs().max().item() <= 2e-2 * gel.abs().max().item()
+    c5 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    p5 = _gemm_params([Ad.data_ptr()], [Wd.data_ptr()], [c5.data_ptr()], M, N, K, K, N, bias=[bd.data_ptr()], act=5,
+                      r=[Rd.data_ptr()], ldr=N, r_t=1, impl=impl)
+    rc = L.LIB.mmt_gemm(p5, L.MMT_BF16, st)
+    if impl == -1:
+        assert rc == -10000
+        return
+    L.check(rc, "gemm act5")
+    torch.cuda.synchronize()
+    r = R.float().requires_grad_(True)
+    F.gelu(r).backward(torch.ones_like(r))
+    ref = pre * r.grad
+    assert (c5.float().cpu() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
+
+
 @pytest.mark.parametrize("impl", [1, 2, 3, 4, 6])
 @pytest.mark.parametrize("splitk", [2, 3, 5])
 @pytest.mark.parametrize("M,N,K", [(528, 768, 3072), (77, 200, 1024), (400, 192, 640)])

@@ -435,3 +435,34 @@ def test_hip_layernorm_autograd(two):
     gb = [xb.grad] + [p.grad for m in (n if two else n[:1]) for p in (m.weight, m.bias)]
     for a, b in zip(ga, gb):
         assert (a - b).abs().max().item() <= 1e-3 * max(1.0, b.abs().max().item())
+
+
+def test_hip_mlp_autograd():
+    """HipOps.mlp (_HipMlp: fc1 with the GELU epilogue storing its pre-activation, fc2, and a backward
+    whose fc2 dX GEMM applies GELU' in its epilogue) against the same MLP as torch fp32 autograd on the
+    bf16-rounded operands (timm Mlp, mixformer.py:136-139): output and every gradient."""
+    from mmt_amd.train import HipOps
+    g = torch.Generator().manual_seed(17)
+    M, C, F4 = 1056, 768, 3072
+    x = torch.randn(M, C, generator=g).bfloat16()
+    w1 = torch.randn(F4, C, generator=g) / math.sqrt(C)
+    b1 = torch.randn(F4, generator=g) * 0.1
+    w2 = torch.randn(C, F4, generator=g) / math.sqrt(F4)
+    b2 = torch.randn(C, generator=g) * 0.1
+    dy = torch.randn(M, C, generator=g)
+    ps = [t.cuda().requires_grad_(True) for t in (w1, b1, w2, b2)]
+    xa = x.cuda().requires_grad_(True)
+    y = HipOps.mlp(xa, *ps)
+    assert y.dtype == torch.float32
+    y.backward(dy.cuda())
+    got = [y.detach().cpu(), xa.grad.float().cpu()] + [p.grad.cpu() for p in ps]
+    # reference: fp32 math on the bf16 operands the kernels read (x, bf16 weights, bf16 h / pre-activation)
+    xr = x.float().requires_grad_(True)
+    rs = [w1.bfloat16().float().requires_grad_(True), b1.clone().requires_grad_(True),
+          w2.bfloat16().float().requires_grad_(True), b2.clone().requires_grad_(True)]
+    yr = torch.nn.functional.linear(torch.nn.functional.gelu(torch.nn.functional.linear(xr, rs[0], rs[1])), rs[2], rs[3])
+    yr.backward(dy)
+    ref = [yr.detach(), xr.grad] + [r.grad for r in rs]
+    for name, a, b in zip(("y", "dx", "dw1", "db1", "dw2", "db2"), got, ref):
+        err = (a - b).abs().max().item() / max(1.0, b.abs().max().item())
+        assert err <= 2e-2, (name, err)

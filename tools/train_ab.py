@@ -23,6 +23,11 @@ class AtenLayerNormOps(HipOps):
     layer_norm = None
 
 
+class SplitMlpOps(HipOps):
+    """HipOps with each MLP as fc1 / aten GELU / fc2 (three autograd nodes) instead of _HipMlp."""
+    mlp = None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
@@ -30,7 +35,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=16)
     args = ap.parse_args()
-    variants = {"hip": HipOps, "aten_layernorm": AtenLayerNormOps}
+    variants = {"hip": HipOps, "split_mlp": SplitMlpOps}
     for r in range(args.rounds):
         for name, ops in variants.items():
             o = bench.train_bench(1, 0, args.batch, args.steps, args.warmup, ops=ops)
