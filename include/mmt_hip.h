@@ -388,7 +388,10 @@ int mmt_track_update(const float* pred_cxcywh, const double* crop, double* state
  * ld_out in elements, `batch` matrices stride_in / stride_out elements apart).  Feeds the Linear
  * backward's dX = dY W and dW = dY^T X GEMMs (both contract over a non-contiguous dimension). */
 int mmt_transpose_bf16(const void* in, void* out, int rows, int cols, int64_t ld_in, int64_t ld_out, int batch,
-                       int64_t stride_in, int64_t stride_out, void* stream);
+                       int64_t stride_in, int64_t stride_out, int fill, void* stream);
+/* fill: 0 writes out[c][r] for r < rows only; 1 also zeros in the padding columns [rows, ld_out); 2 (batch 1)
+ * as 1 plus 8 appended output rows, row `cols` = 1.0 over [0, rows) and the rest zero (the ones row of
+ * the dW GEMM that also yields the bias gradient) -- the whole padded operand in one launch. */
 
 /* AdamW update with global-norm gradient clipping (torch.nn.utils.clip_grad_norm_
  * + torch.optim.AdamW's fused form over the reference's parameter groups, train_script_mixformer.py:

@@ -58,12 +58,9 @@ def _transpose(x, rows, cols, ld_out=None, ones_row=False):
     from ._lib import LIB, check
     ld_out = ld_out or rows
     out = torch.empty(cols + (8 if ones_row else 0), ld_out, device=x.device, dtype=torch.bfloat16)
-    if ld_out > rows:  # only the padding columns and the extra rows need values of their own
-        out[:, rows:].zero_()
-    if ones_row:
-        out[cols:].zero_()
-        out[cols, :rows] = 1.0
-    check(LIB.mmt_transpose_bf16(x.data_ptr(), out.data_ptr(), rows, cols, cols, ld_out, 1, 0, 0, _stream()),
+    # the kernel writes the padding columns and the ones-row block itself (fill 1 / 2): one launch
+    fill = 2 if ones_row else (1 if ld_out > rows else 0)
+    check(LIB.mmt_transpose_bf16(x.data_ptr(), out.data_ptr(), rows, cols, cols, ld_out, 1, 0, 0, fill, _stream()),
           "mmt_transpose_bf16")
     return out
 

@@ -97,6 +97,19 @@ def test_transpose_bf16_bit_exact(rows, cols):
     y = _transpose(x, rows, cols)
     torch.cuda.synchronize()
     assert torch.equal(y.cpu(), x.cpu().t().contiguous())
+    # the dW GEMM's padded operand in one launch: zero padding columns up to ld_out (fill 1) and the
+    # appended ones row block (fill 2), written into poisoned memory
+    ld = (rows + 7) // 8 * 8 + 8
+    for ones in (False, True):
+        poison = torch.full(((cols + 8) * ld,), float("nan"), device="cuda").bfloat16()
+        del poison  # the allocator hands these NaN bytes to the output below: every element must be written
+        yp = _transpose(x, rows, cols, ld, ones_row=ones)
+        torch.cuda.synchronize()
+        ref = torch.zeros(cols + (8 if ones else 0), ld, dtype=torch.bfloat16)
+        ref[:cols, :rows] = x.cpu().t()
+        if ones:
+            ref[cols, :rows] = 1.0
+        assert torch.equal(yp.cpu(), ref), ones
 
 
 @pytest.mark.parametrize("M,N,K", [(1056, 2304, 768), (1056, 768, 3072), (130, 96, 768)])

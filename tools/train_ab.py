@@ -35,7 +35,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=16)
     args = ap.parse_args()
-    variants = {"hip": HipOps, "split_mlp": SplitMlpOps}
+    variants = {"hip": HipOps, "aten_layernorm": AtenLayerNormOps, "split_mlp": SplitMlpOps}
     for r in range(args.rounds):
         for name, ops in variants.items():
             o = bench.train_bench(1, 0, args.batch, args.steps, args.warmup, ops=ops)
