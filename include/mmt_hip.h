@@ -211,8 +211,9 @@ int mmt_mam_attention_bwd(const mmt_attn_bwd_params* p, int dtype, void* stream)
 
 /* ---------------------------------------------------------------- norms / elementwise
  * LayerNorm over the last dim C (C % 256 == 0) of fp32 rows; x = in[row] (+ add[row % add_rows]);
- * gamma/beta chosen per group = row / rows_per_group (up to 2 groups).  Writes out_f32 and/or
- * out_t (dtype) when non-NULL.
+ * gamma/beta chosen per group = (row / rows_per_group) % 2 (2 groups that alternate every
+ * rows_per_group rows: the modality halves of a [2][...] stream, or of each sequence's [2][h*w]
+ * token block in the fusion encoder).  Writes out_f32 and/or out_t (dtype) when non-NULL.
  */
 int mmt_layernorm(const float* in, const float* add, int64_t add_rows, float* out_f32, void* out_t,
                   const float* gamma0, const float* beta0, const float* gamma1, const float* beta1,
@@ -220,7 +221,7 @@ int mmt_layernorm(const float* in, const float* add, int64_t add_rows, float* ou
 
 /* LayerNorm backward (training step; forward = mmt_layernorm without `add`): x [rows][C] fp32 = the
  * LayerNorm input, dy [rows][C] in dy_dtype (bf16 / fp16 / fp32) = the output gradient, gamma per row
- * group as the forward (gamma1 NULL: one group).  dx [rows][C] fp32 = rstd * (g - mean(g) - xhat *
+ * group as the forward ((row / rows_per_group) % 2; gamma1 NULL: one group).  dx [rows][C] fp32 = rstd * (g - mean(g) - xhat *
  * mean(g * xhat)), g = dy * gamma (statistics recomputed from x, eps as the forward).  dgb = fp32
  * [groups][2][C]: (dgamma, dbeta) of each group = column sums of dy * xhat and dy over its rows, summed
  * in a fixed order (bitwise reproducible), added to dgb if dgb_accumulate.  ws: fp32 workspace of
@@ -237,6 +238,15 @@ int mmt_layernorm_bwd(const float* x, const void* dy, int dy_dtype, const float*
 int mmt_groupnorm(const float* in, float* out_f32, void* out_t, const float* gamma0, const float* beta0,
                   const float* gamma1, const float* beta1, int n_inst, int inst_per_set, int P, int Ctot,
                   int groups, float eps, int dtype, void* stream);
+
+/* GroupNorm backward (training step; forward = mmt_groupnorm with one affine set), channels-last fp32
+ * [n_inst][P][Ctot] x (the GroupNorm input) and dy; dx = rstd * (g - mean(g) - xhat * mean(g * xhat)) per
+ * (instance, group), g = dy * gamma[c]; dgb = fp32 [2][Ctot] (dgamma, dbeta) = sums over instances and
+ * positions of dy * xhat and dy (fixed order: bitwise reproducible), added to dgb if dgb_accumulate.
+ * ws: >= n_inst * 2 * Ctot floats.  Limits: Ctot / groups a multiple of 4 and <= 256, P * Ctot / groups
+ * <= 9600.  The fusion's adjust_v / adjust_i / adjust_cat GroupNorms (fusion_utils.py:252-279). */
+int mmt_groupnorm_bwd(const float* x, const float* dy, const float* gamma, float* dx, float* dgb, int dgb_accumulate,
+                      float* ws, int64_t ws_floats, int n_inst, int P, int Ctot, int groups, float eps, void* stream);
 
 /* out_t[i] = (dtype) in[i] (+ add[i % add_n] if add) for n elements; also writes out_f32 = in+add
  * when out_f32 != NULL. */

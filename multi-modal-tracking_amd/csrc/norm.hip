@@ -5,6 +5,7 @@
 //                    src + output_proj residual fused in via a broadcast row map)
 //   mmt_layernorm_bwd  its backward for the training step (dx, per-group dgamma / dbeta)
 //   mmt_groupnorm    nn.GroupNorm(32) after the fusion 1x1 convs (fusion_utils.py:252-268)
+//   mmt_groupnorm_bwd  its backward for the training step (dx, dgamma / dbeta; channels-last)
 //   mmt_add_cast     src + pos -> bf16 query staging (ms_deform_attn_bimodal.py:93-95)
 //   mmt_patch_im2col PatchEmbed input staging for the patch GEMM (mixformer.py:29-34, :237-247)
 #include "common.hpp"
@@ -24,7 +25,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
     const float4* x4 = (const float4*)(in + row * C);
     const float4* a4 = add ? (const float4*)(add + (row % add_rows) * C) : nullptr;
     // gamma / beta issued with the row (not after the two reductions: one memory round trip fewer)
-    const bool second = g1 && (row / rpg) >= 1;
+    const bool second = g1 && ((row / rpg) & 1);  // groups alternate every rpg rows
     const float4* gg = (const float4*)(second ? g1 : g0);
     const float4* bb = (const float4*)(second ? b1 : b0);
     float4 ga[V], be[V];
@@ -180,7 +181,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
     for (int r = w; r < LNB_RPW; r += 4) {
         const int64_t row = (int64_t)blockIdx.x * LNB_RPW + r;
         if (row >= rows) break;
-        const int h = (g1 && row >= rpg) ? 1 : 0;  // wave-uniform
+        const int h = (g1 && ((row / rpg) & 1)) ? 1 : 0;  // wave-uniform; groups alternate every rpg rows
         const float4* gam = (const float4*)(h ? g1 : g0);
         float4 v[V], d[V], ga[V];
         float s = 0.f;
@@ -271,6 +272,104 @@ __global__ __launch_bounds__(64) void layernorm_bwd_reduce_kernel(const float* _
         for (int u = 0; u < 16; ++u) s += v[u];
     }
     for (; b < nwg; ++b) s += col[b * st];
+    dgb[i] = accumulate ? dgb[i] + s : s;
+}
+
+// GroupNorm backward (training step): one 512-thread workgroup per (instance, group) as the forward, the
+// group's x and dy in registers.  dx = rstd * (g - mean(g) - xhat * mean(g * xhat)) with g = dy * gamma_c;
+// the per-channel (sum dy * xhat, sum dy) of the workgroup go through LDS as [P][cg] products and are
+// summed over P in position order by one thread per channel, into part[instance][2][Ctot]; a second
+// launch sums the instances in order (deterministic, no atomics).
+constexpr int GNB_LDS = 2 * 9600;  // floats: P * cg products of each kind (P 400 x cg 24)
+
+__global__ __launch_bounds__(GN_THREADS) void groupnorm_bwd_kernel(const float* __restrict__ in,
+                                                                   const float* __restrict__ dy, const float* gamma,
+                                                                   float* __restrict__ dx, float* __restrict__ part,
+                                                                   int P, int Ctot, int groups, float eps) {
+    __shared__ float red[GN_THREADS / 64];
+    __shared__ float prod[GNB_LDS];  // [P][cg] dy * xhat, then [P][cg] dy
+    const int inst = blockIdx.y, grp = blockIdx.x;
+    const int cg = Ctot / groups, q = cg / 4, items = P * q;
+    const int64_t base = (int64_t)inst * P * Ctot + grp * cg;
+    const float inv_q = 1.f / (float)q;
+    int pix[GN_VMAX], c4s[GN_VMAX];
+#pragma unroll
+    for (int i = 0; i < GN_VMAX; ++i) {
+        const int it = threadIdx.x + GN_THREADS * i;
+        pix[i] = (int)(((float)it + 0.5f) * inv_q);
+        c4s[i] = 4 * (it - pix[i] * q);
+    }
+    float4 v[GN_VMAX], d[GN_VMAX];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < GN_VMAX; ++i) {
+        const int it = threadIdx.x + GN_THREADS * i;
+        if (it < items) {
+            const int64_t off = base + (int64_t)pix[i] * Ctot + c4s[i];
+            v[i] = *(const float4*)(in + off);
+            d[i] = *(const float4*)(dy + off);
+            s += v[i].x + v[i].y + v[i].z + v[i].w;
+        }
+    }
+    const float n = (float)(P * cg);
+    const float mean = block_sum<GN_THREADS>(s, red) / n;
+    float sq = 0.f;
+#pragma unroll
+    for (int i = 0; i < GN_VMAX; ++i) {
+        const int it = threadIdx.x + GN_THREADS * i;
+        if (it < items) {
+            v[i].x -= mean; v[i].y -= mean; v[i].z -= mean; v[i].w -= mean;
+            sq += v[i].x * v[i].x + v[i].y * v[i].y + v[i].z * v[i].z + v[i].w * v[i].w;
+        }
+    }
+    const float rstd = rsqrtf(block_sum<GN_THREADS>(sq, red) / n + eps);
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int i = 0; i < GN_VMAX; ++i) {
+        const int it = threadIdx.x + GN_THREADS * i;
+        if (it < items) {
+            const int c = grp * cg + c4s[i];
+            const float4 ga = *(const float4*)(gamma + c);
+            v[i].x *= rstd; v[i].y *= rstd; v[i].z *= rstd; v[i].w *= rstd;  // xhat
+            float* pp = prod + pix[i] * cg + c4s[i];
+            pp[0] = d[i].x * v[i].x; pp[1] = d[i].y * v[i].y; pp[2] = d[i].z * v[i].z; pp[3] = d[i].w * v[i].w;
+            float* pb = prod + P * cg + pix[i] * cg + c4s[i];
+            pb[0] = d[i].x; pb[1] = d[i].y; pb[2] = d[i].z; pb[3] = d[i].w;
+            d[i] = make_float4(d[i].x * ga.x, d[i].y * ga.y, d[i].z * ga.z, d[i].w * ga.w);  // g
+            sg += d[i].x + d[i].y + d[i].z + d[i].w;
+            sgx += d[i].x * v[i].x + d[i].y * v[i].y + d[i].z * v[i].z + d[i].w * v[i].w;
+        }
+    }
+    const float mg = block_sum<GN_THREADS>(sg, red) / n;  // (its barriers also publish the LDS products)
+    const float mgx = block_sum<GN_THREADS>(sgx, red) / n;
+#pragma unroll
+    for (int i = 0; i < GN_VMAX; ++i) {
+        const int it = threadIdx.x + GN_THREADS * i;
+        if (it < items) {
+            float4 o;
+            o.x = rstd * (d[i].x - mg - v[i].x * mgx);
+            o.y = rstd * (d[i].y - mg - v[i].y * mgx);
+            o.z = rstd * (d[i].z - mg - v[i].z * mgx);
+            o.w = rstd * (d[i].w - mg - v[i].w * mgx);
+            *(float4*)(dx + base + (int64_t)pix[i] * Ctot + c4s[i]) = o;
+        }
+    }
+    if ((int)threadIdx.x < 2 * cg) {  // thread -> (kind, channel): sum over positions in order
+        const int kind = (int)threadIdx.x / cg, c = (int)threadIdx.x % cg;
+        const float* col = prod + kind * P * cg + c;
+        float acc = 0.f;
+        for (int pp = 0; pp < P; ++pp) acc += col[pp * cg];
+        part[((int64_t)inst * 2 + kind) * Ctot + grp * cg + c] = acc;
+    }
+}
+
+// dgb[j][c] (+)= sum over instances (in order) of part[inst][j][c]
+__global__ __launch_bounds__(256) void groupnorm_bwd_reduce_kernel(const float* __restrict__ part, float* dgb, int n_inst,
+                                                                   int Ctot, int accumulate) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= 2 * Ctot) return;
+    float s = 0.f;
+    for (int b = 0; b < n_inst; ++b) s += part[(int64_t)b * 2 * Ctot + i];
     dgb[i] = accumulate ? dgb[i] + s : s;
 }
 
@@ -403,6 +502,24 @@ extern "C" int mmt_groupnorm(const float* in, float* out_f32, void* out_t, const
         hipLaunchKernelGGL((groupnorm_kernel<float>), grid, dim3(GN_THREADS), 0, st, in, out_f32, (float*)out_t, gamma0,
                            beta0, gamma1, beta1, inst_per_set, P, Ctot, groups, eps);
     else return MMT_EBADARG;
+    return launch_status();
+}
+
+extern "C" int mmt_groupnorm_bwd(const float* x, const float* dy, const float* gamma, float* dx, float* dgb,
+                                 int dgb_accumulate, float* ws, int64_t ws_floats, int n_inst, int P, int Ctot,
+                                 int groups, float eps, void* stream) {
+    if (!x || !dy || !gamma || !dx || !dgb || !ws || n_inst <= 0 || P <= 0 || groups <= 0 || Ctot % groups)
+        return MMT_EBADARG;
+    const int cg = Ctot / groups;
+    if (cg % 4 || 2 * cg > GN_THREADS || (int64_t)P * (cg / 4) > (int64_t)GN_THREADS * GN_VMAX ||
+        2 * (int64_t)P * cg > GNB_LDS || ws_floats < (int64_t)n_inst * 2 * Ctot)
+        return MMT_EBADARG;
+    if (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)gamma | (uintptr_t)dx) & 15) return MMT_EBADARG;
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(groupnorm_bwd_kernel, dim3(groups, n_inst), dim3(GN_THREADS), 0, st, x, dy, gamma, dx, ws, P, Ctot,
+                       groups, eps);
+    hipLaunchKernelGGL(groupnorm_bwd_reduce_kernel, dim3((unsigned)((2 * Ctot + 255) / 256)), dim3(256), 0, st, ws, dgb,
+                       n_inst, Ctot, dgb_accumulate);
     return launch_status();
 }
 

@@ -19,8 +19,10 @@ sampling runs on mmt_ms_deform_attn_forward / _backward (mmt_amd.functional.MSDe
 the reference's MSDeformAttnFunction).  Clipping + AdamW is mmt_adamw_step (mmt_amd.optim.HipAdamW,
 three launches over every parameter, writing the bf16 copies of the backbone weights the GEMMs
 read).  The backbone LayerNorms run on mmt_layernorm / mmt_layernorm_bwd (_HipLayerNorm), and each
-block's MLP is one autograd Function whose GELU and GELU backward live in GEMM epilogues (_HipMlp).  The
-residual adds, the encoder's LayerNorms and the corner head run as PyTorch-ROCm ops on the same
+block's MLP is one autograd Function whose GELU and GELU backward live in GEMM epilogues (_HipMlp); the
+fusion encoder's LayerNorms take the same kernels, and the fusion's adjust_* 1x1 convs + GroupNorms run on
+token rows as the HIP GEMM + mmt_groupnorm / mmt_groupnorm_bwd.  The residual adds and the corner head run as
+PyTorch-ROCm ops on the same
 module tree (`nn.Conv2d`, `nn.GroupNorm`, `SyncBatchNorm` under DDP), in bf16 autocast like the
 reference's AMP path.  The backbone ops are injected (`ops`), so the data-parallel plumbing can be exercised on CPU
 with stand-in ops in tests; the product's ops are `HipOps` and have no CPU path.
@@ -182,20 +184,22 @@ class _HipMamAttention(torch.autograd.Function):
 
 
 class _HipLayerNorm(torch.autograd.Function):
-    """nn.LayerNorm over the last dim of the fp32 residual stream -> bf16 (the next Linear's operand),
-    rows [0, rows0) with (w0, b0) and the rest with (w1, b1) (the shared backbone's per-modality
-    norm*_v / norm*_i) or all rows with (w0, b0): forward mmt_layernorm, backward mmt_layernorm_bwd
-    (dx, dgamma / dbeta from the saved fp32 input; statistics recomputed)."""
+    """nn.LayerNorm over the last dim of the fp32 residual stream -> bf16 (the next Linear's operand; fp32
+    with out_f32), rows in alternating blocks of rows0 with (w0, b0) / (w1, b1) (the per-modality
+    norm*_v / norm*_i: the shared backbone's [rgb; tir] halves, or the fusion encoder's [v; i] token
+    halves of every sequence) or all rows with (w0, b0): forward mmt_layernorm, backward
+    mmt_layernorm_bwd (dx, dgamma / dbeta from the saved fp32 input; statistics recomputed)."""
 
     @staticmethod
-    def forward(ctx, x, w0, b0, w1, b1, rows0, eps):
+    def forward(ctx, x, w0, b0, w1, b1, rows0, eps, out_f32=False):
         from ._lib import LIB, MMT_BF16, check
         C = x.shape[-1]
         x2 = x.reshape(-1, C).contiguous()
         rows = x2.shape[0]
         two = w1 is not None  # (LayerNorm parameters are contiguous fp32 leaves)
-        out = torch.empty(rows, C, device=x.device, dtype=torch.bfloat16)
-        check(LIB.mmt_layernorm(x2.data_ptr(), None, 0, None, out.data_ptr(), w0.data_ptr(), b0.data_ptr(),
+        out = torch.empty(rows, C, device=x.device, dtype=torch.float32 if out_f32 else torch.bfloat16)
+        check(LIB.mmt_layernorm(x2.data_ptr(), None, 0, out.data_ptr() if out_f32 else None,
+                                None if out_f32 else out.data_ptr(), w0.data_ptr(), b0.data_ptr(),
                                 w1.data_ptr() if two else None, b1.data_ptr() if two else None, rows,
                                 rows0 if two else rows, C, eps, MMT_BF16, _stream()), "mmt_layernorm")
         ctx.save_for_backward(x2, w0, w1 if two else w0)
@@ -218,8 +222,48 @@ class _HipLayerNorm(torch.autograd.Function):
                                     ws.data_ptr(), ws.numel(), rows, ctx.rows0 if ctx.two else rows, C, ctx.eps,
                                     _stream()), "mmt_layernorm_bwd")
         if ctx.two:
-            return dx.view(ctx.shape), dgb[0], dgb[1], dgb[2], dgb[3], None, None
-        return dx.view(ctx.shape), dgb[0], dgb[1], None, None, None, None
+            return dx.view(ctx.shape), dgb[0], dgb[1], dgb[2], dgb[3], None, None, None
+        return dx.view(ctx.shape), dgb[0], dgb[1], None, None, None, None, None
+
+
+class _HipGroupNorm(torch.autograd.Function):
+    """nn.GroupNorm over channels-last fp32 [n][P][C] (the fusion's adjust_* GroupNorms on token rows):
+    forward mmt_groupnorm, backward mmt_groupnorm_bwd (statistics recomputed from the saved input)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, groups, eps):
+        from ._lib import LIB, MMT_F32, check
+        n, P, C = x.shape
+        x = x.contiguous()
+        out = torch.empty_like(x)
+        check(LIB.mmt_groupnorm(x.data_ptr(), out.data_ptr(), None, w.data_ptr(), b.data_ptr(), None, None, n, n, P,
+                                C, groups, eps, MMT_F32, _stream()), "mmt_groupnorm")
+        ctx.save_for_backward(x, w)
+        ctx.groups, ctx.eps = groups, eps
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        from ._lib import LIB, check
+        x, w = ctx.saved_tensors
+        n, P, C = x.shape
+        dy = dy.float().contiguous()
+        buf = torch.empty(n * P * C + 2 * C + n * 2 * C, device=x.device, dtype=torch.float32)
+        dx, dgb, ws = buf[:n * P * C].view(n, P, C), buf[n * P * C:n * P * C + 2 * C].view(2, C), buf[n * P * C + 2 * C:]
+        check(LIB.mmt_groupnorm_bwd(x.data_ptr(), dy.data_ptr(), w.data_ptr(), dx.data_ptr(), dgb.data_ptr(), 0,
+                                    ws.data_ptr(), ws.numel(), n, P, C, ctx.groups, ctx.eps, _stream()),
+              "mmt_groupnorm_bwd")
+        return dx, dgb[0], dgb[1], None, None
+
+
+def _adjust_tokens(ops, seq, tok):
+    """nn.Sequential(Conv2d 1x1, GroupNorm) of the fusion (fusion_utils.py:252-268) on token rows
+    tok [B][P][Cin] -> [B][P][Cout] fp32: the 1x1 conv as ops.linear (HIP GEMM) and ops.group_norm."""
+    conv, gn = seq[0], seq[1]
+    B, P, Cin = tok.shape
+    w = conv.weight.view(conv.weight.shape[0], Cin)
+    y = ops.linear(tok.reshape(B * P, Cin).to(ops.dtype).contiguous(), w, conv.bias, out_f32=True)
+    return ops.group_norm(y.view(B, P, -1), gn.weight, gn.bias, gn.num_groups, gn.eps)
 
 
 def _mlp(ops, x, mlp):
@@ -254,14 +298,21 @@ class HipOps:
     dtype = torch.bfloat16  # activation dtype of the GEMM / attention operands
 
     @staticmethod
-    def layer_norm(x, w0, b0, eps, w1=None, b1=None):
-        """x [2h or n, ..., C] fp32 -> bf16; (w1, b1) given: rows of the second half of dim 0 take them."""
-        rows0 = x.numel() // x.shape[-1] // 2 if w1 is not None else 0
-        return _HipLayerNorm.apply(x, w0, b0, w1, b1, rows0, eps)
+    def layer_norm(x, w0, b0, eps, w1=None, b1=None, rows0=None, out_f32=False):
+        """x [2h or n, ..., C] fp32 -> bf16 (fp32 with out_f32); (w1, b1) given: rows of the second half of
+        dim 0 take them, or alternate blocks of rows0 rows when rows0 is given."""
+        if w1 is not None and rows0 is None:
+            rows0 = x.numel() // x.shape[-1] // 2
+        return _HipLayerNorm.apply(x, w0, b0, w1, b1, rows0 or 0, eps, out_f32)
 
     @staticmethod
     def linear(x, weight, bias, out_f32=False):
         return _HipLinear.apply(x, weight, bias, out_f32)
+
+    @staticmethod
+    def group_norm(x, w, b, groups, eps):
+        """GroupNorm over channels-last x [n][P][C] fp32 (_HipGroupNorm)."""
+        return _HipGroupNorm.apply(x, w, b, groups, eps)
 
     @staticmethod
     def mlp(x, w1, b1, w2, b2):
@@ -422,11 +473,18 @@ def fusion_forward(fu, s_v, s_i, ops):
     encoder (deformable_encoder_lnspecific.py:131-160) and MSDeformAttn_Bimodal
     (ms_deform_attn_bimodal.py:83-130)."""
     b, _, h, w = s_v.shape
-    av, ai = fu.adjust_v(s_v), fu.adjust_i(s_i)
-    d = av.shape[1]
+    tokens = getattr(ops, "group_norm", None) is not None  # adjust_* on token rows (HIP GEMM + GroupNorm)
+    if tokens:
+        av = _adjust_tokens(ops, fu.adjust_v, s_v.flatten(2).transpose(1, 2))
+        ai = _adjust_tokens(ops, fu.adjust_i, s_i.flatten(2).transpose(1, 2))
+        d = av.shape[2]
+        src = torch.cat([av, ai], 1)
+    else:
+        av, ai = fu.adjust_v(s_v), fu.adjust_i(s_i)
+        d = av.shape[1]
+        src = torch.cat([av.flatten(2).transpose(1, 2), ai.flatten(2).transpose(1, 2)], 1)
     fa = fu.fusion_attention
     pos = _sine_pos(b, d, h, w, s_v.device).flatten(2).transpose(1, 2)
-    src = torch.cat([av.flatten(2).transpose(1, 2), ai.flatten(2).transpose(1, 2)], 1)
     lpos = torch.cat([pos + fa.level_embed[0].view(1, 1, -1), pos + fa.level_embed[1].view(1, 1, -1)], 1)
     ref = _ref_points(h, w, b, 2, s_v.device)
     nl = 2 * h * w
@@ -448,15 +506,27 @@ def fusion_forward(fu, s_v, s_i, ops):
         loc = ref[:, :, None, :, None, :] + off.float() / wh
         src2 = lin(sa.output_proj, ops.ms_deform_attn(value.float().contiguous(), h, loc.contiguous(), aw.contiguous()))
         src = src + layer.dropout1(src2)
-        s1, s2 = torch.chunk(src, 2, 1)
-        src = torch.cat([layer.norm1_v(s1), layer.norm1_i(s2)], 1)
+        src = _ln_halves(ops, src, layer.norm1_v, layer.norm1_i)
         src = src + layer.dropout3(lin(layer.linear2, layer.dropout2(F.relu(lin(layer.linear1, src)))))
-        s1, s2 = torch.chunk(src, 2, 1)
-        src = torch.cat([layer.norm2_v(s1), layer.norm2_i(s2)], 1)
+        src = _ln_halves(ops, src, layer.norm2_v, layer.norm2_i)
     o_v, o_i = torch.chunk(src, 2, 1)
+    if tokens:  # channel concat on token rows, then back to NCHW for the corner head's convolutions
+        y = _adjust_tokens(ops, fu.adjust_cat, torch.cat([o_v, o_i], 2))
+        return y.transpose(1, 2).reshape(b, -1, h, w)
     o_v = o_v.permute(0, 2, 1).reshape(b, -1, h, w)
     o_i = o_i.permute(0, 2, 1).reshape(b, -1, h, w)
     return fu.adjust_cat(torch.cat([o_v, o_i], 1))
+
+
+def _ln_halves(ops, src, nv, ni):
+    """The LN-specific encoder's norms (deformable_encoder_lnspecific.py:94-148): nv on the first half of
+    every sequence's tokens, ni on the second, fp32 -> fp32 (ops.layer_norm's alternating row groups; the
+    aten path chunks and concatenates)."""
+    ln = getattr(ops, "layer_norm", None)
+    if ln is not None:
+        return ln(src, nv.weight, nv.bias, nv.eps, ni.weight, ni.bias, rows0=src.shape[1] // 2, out_f32=True)
+    s1, s2 = torch.chunk(src, 2, 1)
+    return torch.cat([nv(s1), ni(s2)], 1)
 
 
 def _soft_argmax(score_map, stride):

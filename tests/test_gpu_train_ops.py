@@ -402,17 +402,17 @@ def test_layernorm_backward_matches_autograd(C, rows, two, dyt):
     assert (outs[0][1] - outs[1][1]).abs().max().item() <= 1e-6 * max(1.0, outs[0][1].abs().max().item())
     dx, dgb = outs[0]
     xr = x.clone().requires_grad_(True)
-    ws_, bs_ = [], []
-    parts = [(0, rows0, 0), (rows0, rows, 1)] if two else [(0, rows, 0)]
-    ys = []
-    for a, b, h in parts:
-        w = gam[h].clone().requires_grad_(True)
-        bb = torch.zeros(C, requires_grad=True)
-        ws_.append(w), bs_.append(bb)
-        ys.append(torch.nn.functional.layer_norm(xr[a:b], (C,), w, bb, 1e-6))
-    torch.cat(ys).backward(dy.float())
+    # row groups alternate every rows0 rows (an odd row count puts the last row back in group 0)
+    grp = (torch.arange(rows) // rows0) % 2 if two else torch.zeros(rows, dtype=torch.long)
+    ws_ = [gam[h].clone().requires_grad_(True) for h in range(2)]
+    bs_ = [torch.zeros(C, requires_grad=True) for _ in range(2)]
+    ys = [torch.nn.functional.layer_norm(xr[grp == h], (C,), ws_[h], bs_[h], 1e-6) for h in range(2)]
+    y = torch.zeros(rows, C).index_put((torch.nonzero(grp == 0).view(-1),), ys[0]) \
+        .index_put((torch.nonzero(grp == 1).view(-1),), ys[1])
+    y.backward(dy.float())
     assert (dx - xr.grad).abs().max().item() <= 2e-4 * max(1.0, xr.grad.abs().max().item())
-    for i, (w, bb) in enumerate(zip(ws_, bs_)):
+    for i in range(2 if two else 1):
+        w, bb = ws_[i], bs_[i]
         assert (dgb[2 * i] - w.grad).abs().max().item() <= 2e-4 * max(1.0, w.grad.abs().max().item())
         assert (dgb[2 * i + 1] - bb.grad).abs().max().item() <= 2e-4 * max(1.0, bb.grad.abs().max().item())
 
@@ -479,3 +479,64 @@ def test_hip_mlp_autograd():
     for name, a, b in zip(("y", "dx", "dw1", "db1", "dw2", "db2"), got, ref):
         err = (a - b).abs().max().item() / max(1.0, b.abs().max().item())
         assert err <= 2e-2, (name, err)
+
+
+def test_hip_layernorm_alternating_groups_fp32():
+    """The fusion encoder's LN-specific norms in training (deformable_encoder_lnspecific.py:94-148):
+    norm_v on the first half of every sequence's 2hw tokens and norm_i on the second, fp32 in / out
+    (HipOps.layer_norm with rows0 = hw alternating groups) against chunk + two nn.LayerNorm + cat."""
+    from mmt_amd.train import HipOps
+    g = torch.Generator().manual_seed(5)
+    b, hw, d = 3, 400, 512
+    x = (torch.randn(b, 2 * hw, d, generator=g) * 2).cuda()
+    nv, ni = torch.nn.LayerNorm(d).cuda(), torch.nn.LayerNorm(d).cuda()
+    with torch.no_grad():
+        for m in (nv, ni):
+            m.weight.copy_(torch.randn(d, generator=g).cuda())
+            m.bias.copy_(torch.randn(d, generator=g).cuda())
+    dy = torch.randn(b, 2 * hw, d, generator=g).cuda()
+    xa = x.clone().requires_grad_(True)
+    ya = HipOps.layer_norm(xa, nv.weight, nv.bias, 1e-5, ni.weight, ni.bias, rows0=hw, out_f32=True)
+    assert ya.dtype == torch.float32
+    ya.backward(dy)
+    ga = [xa.grad] + [p.grad.clone() for m in (nv, ni) for p in (m.weight, m.bias)]
+    for m in (nv, ni):
+        m.weight.grad = m.bias.grad = None
+    xb = x.clone().requires_grad_(True)
+    s1, s2 = torch.chunk(xb, 2, 1)
+    yb = torch.cat([nv(s1), ni(s2)], 1)
+    assert (ya - yb).abs().max().item() <= 1e-4 * max(1.0, yb.abs().max().item())
+    yb.backward(dy)
+    gb = [xb.grad] + [p.grad for m in (nv, ni) for p in (m.weight, m.bias)]
+    for a, r in zip(ga, gb):
+        assert (a - r).abs().max().item() <= 2e-4 * max(1.0, r.abs().max().item())
+
+
+@pytest.mark.parametrize("B,P,C,groups", [(4, 400, 512, 32), (2, 400, 768, 32), (3, 64, 256, 8)])
+def test_hip_groupnorm_autograd(B, P, C, groups):
+    """HipOps.group_norm (mmt_groupnorm / mmt_groupnorm_bwd on channels-last token rows) against
+    nn.GroupNorm on the NCHW map the reference applies it to (fusion_utils.py:252-279): output, dx,
+    dgamma, dbeta; the backward is bitwise repeatable."""
+    from mmt_amd.train import HipOps
+    g = torch.Generator().manual_seed(B * P + C)
+    x = (torch.randn(B, P, C, generator=g) * 3 + 1).cuda()
+    gn = torch.nn.GroupNorm(groups, C).cuda()
+    with torch.no_grad():
+        gn.weight.copy_(torch.randn(C, generator=g).cuda())
+        gn.bias.copy_(torch.randn(C, generator=g).cuda())
+    dy = torch.randn(B, P, C, generator=g).cuda()
+    grads = []
+    for rep in range(2):
+        xa = x.clone().requires_grad_(True)
+        ya = HipOps.group_norm(xa, gn.weight, gn.bias, groups, 1e-5)
+        ya.backward(dy)
+        grads.append([ya.detach(), xa.grad] + [p.grad.clone() for p in (gn.weight, gn.bias)])
+        gn.weight.grad = gn.bias.grad = None
+    assert all(torch.equal(a, b) for a, b in zip(grads[0], grads[1]))
+    xb = x.clone().requires_grad_(True)
+    yb = gn(xb.transpose(1, 2).reshape(B, C, P, 1)).reshape(B, C, P).transpose(1, 2)
+    yb.backward(dy)
+    ref = [yb.detach(), xb.grad, gn.weight.grad, gn.bias.grad]
+    for name, a, r in zip(("y", "dx", "dgamma", "dbeta"), grads[0], ref):
+        err = (a - r).abs().max().item() / max(1.0, r.abs().max().item())
+        assert err <= 2e-4, (name, err)

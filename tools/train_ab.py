@@ -23,6 +23,11 @@ class AtenLayerNormOps(HipOps):
     layer_norm = None
 
 
+class AtenGroupNormOps(HipOps):
+    """HipOps with the fusion's adjust_* as NCHW Conv2d (MIOpen) + nn.GroupNorm (aten), as before."""
+    group_norm = None
+
+
 class SplitMlpOps(HipOps):
     """HipOps with each MLP as fc1 / aten GELU / fc2 (three autograd nodes) instead of _HipMlp."""
     mlp = None
@@ -34,8 +39,12 @@ def main():
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--only", default="", help="comma-separated variant names")
     args = ap.parse_args()
-    variants = {"hip": HipOps, "aten_layernorm": AtenLayerNormOps, "split_mlp": SplitMlpOps}
+    variants = {"hip": HipOps, "aten_groupnorm": AtenGroupNormOps, "aten_layernorm": AtenLayerNormOps,
+                "split_mlp": SplitMlpOps}
+    if args.only:
+        variants = {k: v for k, v in variants.items() if k in args.only.split(",")}
     for r in range(args.rounds):
         for name, ops in variants.items():
             o = bench.train_bench(1, 0, args.batch, args.steps, args.warmup, ops=ops)
