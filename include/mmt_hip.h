@@ -104,7 +104,8 @@ typedef struct {
                      -1 register-staged 64/128 tiles; LDS-DMA (bf16, K % 8 == 0): 1 128x128
                      (8 waves), 2 128x64 (K split over 2 wave groups), 3 64x64 (K split 2),
                      4 128x128 (4 waves), 5 256x128 / 6 128x256 (8 waves, large M), 7 256x256
-                     (8 waves, plain GEMM mode only: no ln_fold / conv / split-K) */
+                     (8 waves, plain GEMM mode only: no ln_fold / conv / split-K), 8 128x128 at two
+                     workgroups per CU (64 KiB ring; same restrictions as 7; auto on big unsplit grids) */
     /* LayerNorm folded into the GEMM (bf16 LDS-DMA kernels, GEMM mode): A holds the raw rows x
      * (K = the LayerNorm width), W = W_lin * gamma (per column k), and the epilogue's v is
      *   rstd_m * (acc - mu_m * ln_colsum[g][n]) + bias[g][n],   mu / rstd over the K values of row m

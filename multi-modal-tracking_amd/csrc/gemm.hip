@@ -325,7 +325,7 @@ template <typename T>
 int check_gemm(const mmt_gemm_params& p) {
     const int EPC = 16 / (int)sizeof(T);
     if (p.M <= 0 || p.N <= 0 || p.K <= 0 || p.groups < 1 || p.groups > MMT_MAX_GROUPS) return MMT_EBADARG;
-    if (p.impl < -1 || p.impl > 7) return MMT_EBADARG;
+    if (p.impl < -1 || p.impl > 8) return MMT_EBADARG;
     if (p.act < 0 || (p.act > 2 && p.act != 5) || p.c2_copy < 0 || p.c2_copy > 2) return MMT_EBADARG;
     if (p.K % EPC || p.lda % EPC) return MMT_EBADARG;
     if (p.conv_h > 0) {

@@ -29,6 +29,10 @@
 #ifndef MMT_GEMM_ABLATE
 #define MMT_GEMM_ABLATE 0
 #endif
+// A/B build knob (tools/build_ablate.sh noocc2): 1 = the cost model never switches to impl 8
+#ifndef MMT_GEMM_NO_OCC2
+#define MMT_GEMM_NO_OCC2 0
+#endif
 
 // Stamp build (MMT_STAMP_BUILD): per-phase workgroup timestamps, read with mmt_gemm_stamps().
 #if MMT_STAMP_BUILD
@@ -78,7 +82,7 @@ __device__ __attribute__((aligned(64))) const uint32_t g_zero_chunk[16] = {0};
 // (mmt_gemm_params.ln_fold): the row statistics of A are accumulated from the A fragments the
 // waves already hold for the MFMAs (wave column wc sums fragment rows mt = wc, wc + WGN, ...), so
 // the normalised operand never exists in memory and the LayerNorm launch disappears.
-template <typename T, int BM, int BN, int WGM, int WGN, int KS, int ST, bool CONV, int LNM>
+template <typename T, int BM, int BN, int WGM, int WGN, int KS, int ST, bool CONV, int LNM, int OCC = 1>
 MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int tile, const int slice, const int nsk,
                             const int ntiles) {
     constexpr int NW = WGM * WGN, TPG = 64 * NW;  // waves / threads per k-group
@@ -89,7 +93,7 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
     constexpr int L = PA + PB;  // DMA instructions per wave per stage
     constexpr int WM = BM / WGM, WN = BN / WGN, MT = WM / 16, NT = WN / 16;
     static_assert(KS * ST * STAGE <= 160 * 1024, "LDS budget");
-    constexpr bool SB = BM * BN >= 256 * 256;  // single-buffered fragments (the 256x256 tile, impl 7)
+    constexpr bool SB = BM * BN >= 256 * 256 || OCC > 1;  // single-buffered fragments (impl 7's 256x256; impl 8)
     static_assert(!SB || (KS == 1 && LNM == 0 && !CONV), "impl 7: plain GEMM only");
     static_assert(KS == 1 || BM * BN * 4 <= KS * ST * STAGE, "k-group reduction buffer");
     __shared__ __attribute__((aligned(1024))) unsigned char lds[KS * ST * STAGE];
@@ -365,7 +369,8 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
     // Infinity Cache latency then overlaps the fragment writes and barriers below instead of being
     // exposed once per group of four strip passes (proj / fc2 / encoder Linears: fp32 residual stream).
     constexpr int TPR0 = BN / 8, RPP0 = TPG * KS / TPR0, NPASS0 = EB / RPP0;
-    constexpr bool RPRE = EPASS == 1 && NPASS0 <= 8 && BM * BN <= 128 * 128;  // batch-1 tiles (large ones spill)
+    constexpr bool RPRE = EPASS == 1 && NPASS0 <= 8 && BM * BN <= 128 * 128 && OCC == 1;  // batch-1 tiles (large
+                                                                                          // ones / OCC 2 spill)
     const int tc0 = (threadIdx.x % TPR0) * 8, tr0 = threadIdx.x / TPR0, nc0 = min(n0 + tc0, N - 8);
     auto rload = [&](int m, int nc, f32x4& ra, f32x4& rb) {  // residual row of output row m, columns nc..nc+7
         const float* R = p.r[g];
@@ -684,6 +689,21 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
     gemm_glds_tile<T, BM, BN, WGM, WGN, KS, ST, CONV, LNM>(p, g, tile, slice, nsk, gridDim.x);
 }
 
+// The same tile at two workgroups per CU (impl 8: 128x128, 8 waves, 2-slot ring = 64 KiB of LDS, <= 128
+// VGPRs): one workgroup's prologue / epilogue runs beside the other's K loop on the CU, which the one-
+// workgroup-per-CU tiles cannot overlap (large-M grids of short K: the training step's K = 768 GEMMs).
+template <typename T, int BM, int BN, int WGM, int WGN, int KS, int ST>
+__global__ __launch_bounds__(64 * WGM * WGN * KS)
+    __attribute__((amdgpu_waves_per_eu(WGM * WGN * KS / 2, WGM * WGN * KS / 2))) void gemm_glds_kernel_occ2(
+        const mmt_gemm_params p) {
+    const int nsk = gridDim.y;
+    const int lin = gemm_xcd_lin();
+    const int per_g = gridDim.x * nsk;
+    const int g = lin / per_g, rem_t = lin - g * per_g;
+    const int tile = rem_t / nsk, slice = rem_t - tile * nsk;
+    gemm_glds_tile<T, BM, BN, WGM, WGN, KS, ST, false, 0, 2>(p, g, tile, slice, nsk, gridDim.x);
+}
+
 // Several independent GEMMs of one kernel configuration in one launch (mmt_gemm_multi): problem i
 // owns the remapped linear ids [wg0[i], wg0[i + 1]), (group, tile) with the tile fastest, no split-K.
 // The head's parallel conv chains and the fusion encoder's value / offset Linears are each a
@@ -815,6 +835,17 @@ int mmt_gemm_glds(const mmt_gemm_params& p, hipStream_t st, int force) {
                 if (t < best) best = t, cfg = c.cfg, nsk = n;
             }
         }
+        // 128x128 at two workgroups per CU (impl 8) instead of a one-per-CU 128x128 / 256x128 / 128x256 tile
+        // on big unsplit plain grids: 1.14-1.25x impl 1 and 1.02-1.16x the model's pick on the training
+        // step's forward / dX shapes and batch-8 fc1 / fc2 (profiles/r03_gemm_occ2_ab.jsonl); the
+        // 256x256 tile (impl 7) keeps its shapes (dX of fc2: 597 vs 525 TFLOP/s)
+        // Not for the inference residual producers (C2 copy + LayerNorm statistics out: config 3 at 64
+        // sequences 2650 -> 2541 frames/s with them on impl 8, interleaved, profiles/r03_gemm_occ2_ab.jsonl)
+        if (!MMT_GEMM_NO_OCC2 && big && nsk == 1 && !p.ln_fold && p.conv_h == 0 && !p.ln_stats_out[0] &&
+            (cfg == 1 || cfg == 5 || cfg == 6))
+            cfg = 8;
+    } else if (cfg == 8) {
+        nsk = 1;  // impl 8: no split-K
     } else if (cfg >= 1 && cfg <= 7) {
         const Cand& c = cands[cfg - 1];
         if (p.splitk >= 2) {
@@ -838,6 +869,12 @@ int mmt_gemm_glds(const mmt_gemm_params& p, hipStream_t st, int force) {
             if (p.ln_fold || p.conv_h > 0 || nsk > 1) return 1;
             hipLaunchKernelGGL((gemm_glds_kernel<T, 256, 256, 4, 2, 1, 2, false, 0>),
                                dim3((unsigned)tiles_of(p, 256, 256), 1, p.groups), dim3(512), 0, st, p);
+            break;
+        case 8:  // 128x128 at two workgroups per CU: plain GEMM mode (no folded LayerNorm / conv), and no split-K:
+                 // its 64 KiB ring holds the fp32 tile image only in two passes (as impl 7)
+            if (p.ln_fold || p.conv_h > 0 || nsk > 1) return 1;
+            hipLaunchKernelGGL((gemm_glds_kernel_occ2<T, 128, 128, 2, 4, 1, 2>),
+                               dim3((unsigned)tiles_of(p, 128, 128), nsk, p.groups), dim3(512), 0, st, p);
             break;
         default: return 1;
     }

@@ -115,7 +115,7 @@ def test_gemm_groups_segments_ksplit(dname):
         assert err <= _tol(dt) * ref.abs().max().item(), (grp, err)
 
 
-@pytest.mark.parametrize("impl", [-1, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("impl", [-1, 1, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("M,N,K", [(528, 768, 768), (77, 200, 64), (300, 136, 192), (1056, 256, 3072), (300, 136, 200),
                                    (4224, 1160, 256)])
 def test_gemm_bf16_tile_paths(impl, M, N, K):
@@ -173,7 +173,7 @@ def test_gemm_bf16_tile_paths(impl, M, N, K):
             assert e3 <= 1e-3 * r3.abs().max().item() + 1e-4, (grp, e3)
 
 
-@pytest.mark.parametrize("impl", [-1, 0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("impl", [-1, 0, 1, 2, 3, 4, 5, 6, 7, 8])
 def test_gemm_gelu_backward_and_preact_epilogues(impl):
     """The training MLP's epilogues: act 1 with c2_copy 2 (C = GELU(acc + b), C2 = acc + b in bf16) and
     act 5 (C = (acc + b) * GELU'(R), R bf16); 16-bit LDS-DMA kernels only (impl -1, the register-staged

@@ -7,6 +7,7 @@
 #            (MMT_ATTN_ABLATE=1/2/3/4); aab5: impl 22 free-running (no per-tile wait / barrier / refill); aab6: aab5 without exponentials
 #   stamp:   per-phase workgroup timestamps in the GEMM / attention kernels (MMT_STAMP_BUILD=1)
 #   ab:      the product plus the A/B-only attention kernel impl 23 (MMT_ATTN_AB=1)
+#   noocc2:  the product without the cost model's switch to the two-per-CU 128x128 GEMM tile (impl 8)
 # Use with MMT_HIP_LIB=multi-modal-tracking_amd/mmt_amd/_lib/<variant>/libmmt_hip.so.
 set -e
 ONLY=${1:-}
@@ -26,3 +27,4 @@ build aab4 -DMMT_ATTN_ABLATE=4
 build aab5 -DMMT_ATTN_ABLATE=5
 build aab6 -DMMT_ATTN_ABLATE=6
 build ab -DMMT_ATTN_AB=1
+build noocc2 -DMMT_GEMM_NO_OCC2=1

@@ -27,7 +27,15 @@ SHAPES = [("qkv_ln", 2, 528, 2304, 768, 0, 0), ("fc1_ln", 2, 528, 3072, 768, 1, 
           ("fc2_T16", 2, 8448, 768, 3072, 0, 1), ("proj_T16", 2, 8448, 768, 768, 0, 1),
           ("dW_fc1_T16", 2, 3072, 768, 8448, 0, 0), ("dW_fc2_T16", 2, 768, 3072, 8448, 0, 0),
           ("dX_fc2_T16", 2, 8448, 3072, 768, 0, 0), ("fc1_B8", 2, 4224, 3072, 768, 1, 0),
-          ("fc2_B8", 2, 4224, 768, 3072, 0, 1)]
+          ("fc2_B8", 2, 4224, 768, 3072, 0, 1),
+          # the training step's GEMMs as it issues them (one backbone per call, 16 pairs: 8448 rows;
+          # dW with the bias column block: N = K_fwd + 8, contraction over the 8448 rows)
+          ("g1_qkv", 1, 8448, 2304, 768, 0, 0), ("g1_fc1", 1, 8448, 3072, 768, 1, 0),
+          ("g1_fc2", 1, 8448, 768, 3072, 0, 1), ("g1_proj", 1, 8448, 768, 768, 0, 1),
+          ("g1_dX_qkv", 1, 8448, 768, 2304, 0, 0), ("g1_dX_fc1", 1, 8448, 768, 3072, 0, 0),
+          ("g1_dX_fc2", 1, 8448, 3072, 768, 0, 0), ("g1_dX_proj", 1, 8448, 768, 768, 0, 0),
+          ("g1_dW_qkv", 1, 2304, 776, 8448, 0, 0), ("g1_dW_fc1", 1, 3072, 776, 8448, 0, 0),
+          ("g1_dW_fc2", 1, 768, 3080, 8448, 0, 0), ("g1_dW_proj", 1, 768, 776, 8448, 0, 0)]
 
 
 SK_WS = None

@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""Which aten ops the config-4 training step still launches: torch.profiler over one step (after warm-up)
+of bench.train_bench's workload, aten ops grouped by name with call counts and device time, top N.
+
+    python tools/train_ops_profile.py [--top 30]
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "multi-modal-tracking_amd"))
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--batch", type=int, default=16)
+    args = ap.parse_args()
+    from mmt_amd.model import build_mixformer_vit_rgbt, hot_path_cfg
+    from mmt_amd.train import HipOps, TrainStep, synthetic_batch
+    torch.manual_seed(0)
+    net = build_mixformer_vit_rgbt(hot_path_cfg(), train=False).cuda().train()
+    step = TrainStep(net, HipOps, ddp=False)
+    g = torch.Generator().manual_seed(100)
+    batch = synthetic_batch(args.batch, "cuda", g)
+    for _ in range(3):
+        step(*batch)
+    torch.cuda.synchronize()
+    acts = [torch.profiler.ProfilerActivity.CPU, torch.profiler.ProfilerActivity.CUDA]
+    with torch.profiler.profile(activities=acts) as prof:
+        step(*batch)
+        torch.cuda.synchronize()
+    ka = prof.key_averages()
+    rows = [e for e in ka if e.key.startswith("aten::")]
+    rows.sort(key=lambda e: -e.count)
+    print("%-44s %7s %12s %12s" % ("aten op", "calls", "self cpu us", "device us"))
+    for e in rows[:args.top]:
+        dev = getattr(e, "self_device_time_total", getattr(e, "self_cuda_time_total", 0.0))
+        print("%-44s %7d %12.0f %12.0f" % (e.key[:44], e.count, e.self_cpu_time_total, dev))
+
+
+if __name__ == "__main__":
+    main()
