@@ -416,7 +416,8 @@ def train_bench(world, rank, B, steps, warmup, device="cuda", ops=None, search=3
             "roofline": {"kernel": "train_step (whole step)", "bound": "mfma", "achieved": round(ach, 2),
                          "peak": PEAK["bf16"], "unit": "TFLOP/s", "frac": round(ach / PEAK["bf16"], 4),
                          "flops_per_sample": TRAIN_FLOP_PER_SAMPLE, "traffic": None},
-            "last_loss": round(float(last["stats"]["loss"]), 5)}
+            "last_loss": round(float(last["stats"]["loss"]), 5),
+            "opt_table_writes": getattr(step_fn.opt, "table_writes", None)}
 
 
 def timed_steps(step, steps, world, sync, device):

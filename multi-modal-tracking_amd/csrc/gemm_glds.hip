@@ -527,7 +527,11 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
         }
     }
     const int n = n0 + tc, nc = min(n, N - 8);
-    float* stats_out = p.c2_copy && C2 ? p.ln_stats_out[g] : nullptr;
+    float* stats_out = p.c2_copy && p.c2_copy != 3 && C2 ? p.ln_stats_out[g] : nullptr;
+    // c2_copy 3: the last 8 output columns go to C2 (row pitch 8), the others to C (pitch ldc >= N - 8)
+    const bool colsplit = p.c2_copy == 3 && n >= N - 8;
+    char* Cs = colsplit ? C2 : C;
+    if (p.c2_copy == 3) C2 = nullptr;
     f32x4 bn0 = {0.f, 0.f, 0.f, 0.f}, bn1 = bn0, cs0 = bn0, cs1 = bn0;
     if (bias) {
         bn0 = *(const f32x4*)(bias + nc);
@@ -629,10 +633,10 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
                     *(f32x2*)(stats_out + (crow(m) * (N / 64) + n / 64) * 2) = f32x2{ps, pq};
             }
             if (m < M && n < N) {
-                const int64_t e = crow(m) * p.ldc + n;
+                const int64_t e = crow(m) * p.ldc + n, es = colsplit ? crow(m) * 8 : e;
                 if (p.c_f32) {
-                    *(f32x4*)((float*)C + e) = oa;
-                    *(f32x4*)((float*)C + e + 4) = ob;
+                    *(f32x4*)((float*)Cs + es) = oa;
+                    *(f32x4*)((float*)Cs + es + 4) = ob;
                     if (C2 && p.c2_copy == 2) {  // the pre-activation in the compute dtype
                         *(u32x4*)((T*)C2 + e) = u32x4{pack2<T>(prea[0], prea[1]), pack2<T>(prea[2], prea[3]),
                                                       pack2<T>(preb[0], preb[1]), pack2<T>(preb[2], preb[3])};
@@ -644,7 +648,7 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
                         *(f32x4*)((float*)C2 + e + 4) = sb;
                     }
                 } else {
-                    *(u32x4*)((T*)C + e) = u32x4{pack2<T>(oa[0], oa[1]), pack2<T>(oa[2], oa[3]),
+                    *(u32x4*)((T*)Cs + es) = u32x4{pack2<T>(oa[0], oa[1]), pack2<T>(oa[2], oa[3]),
                                                  pack2<T>(ob[0], ob[1]), pack2<T>(ob[2], ob[3])};
                     if (C2 && p.c2_copy == 2)
                         *(u32x4*)((T*)C2 + e) = u32x4{pack2<T>(prea[0], prea[1]), pack2<T>(prea[2], prea[3]),

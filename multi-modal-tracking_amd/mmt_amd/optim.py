@@ -6,7 +6,9 @@ ltr_trainer.py TRAIN.GRAD_CLIP_NORM, base_functions.py:362-400 parameter groups)
 over every parameter instead of PyTorch's per-group multi-tensor kernels, the norm, the clip and the
 update.  The update pass also
   * zeroes the gradients in place (they stay allocated, so the device tables stay valid: zero_grad
-    is then a no-op), and
+    is then a no-op) -- or, with set_to_none=True, leaves them to zero_grad(set_to_none=True), which
+    drops them so that autograd hands the next step's gradients over as .grad without an accumulate
+    pass (only the small pointer table is rewritten when their addresses change), and
   * writes a bf16 shadow of the weights registered with `shadow=` (the backbone Linears): the next
     forward's GEMMs read it instead of casting each weight (mmt_amd.train._HipLinear), valid while
     the parameter's version counter is the one recorded with it.
@@ -24,9 +26,11 @@ MAX_GROUPS = 8
 
 
 class HipAdamW:
-    def __init__(self, param_groups, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, shadow=()):
+    def __init__(self, param_groups, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, shadow=(),
+                 set_to_none=False):
         from ._lib import LIB
         self.lib = LIB
+        self.set_to_none = set_to_none
         self.groups = []
         for g in param_groups:
             g = dict(g)
@@ -53,40 +57,52 @@ class HipAdamW:
                     p._mmt_bf16 = (sh, p._version)
         self._key = None
         self.last_norm = None
+        self.table_writes = 0
 
     def zero_grad(self, set_to_none=False):
-        """The update pass zeroes the gradients it consumed; only gradients of parameters that were
-        not stepped (none at the first step) are cleared here."""
+        """set_to_none: drop every gradient.  Else the update pass has zeroed the gradients it consumed
+        (unless constructed with set_to_none=True); the others are cleared here."""
         for g in self.groups:
             for p in g["params"]:
-                if p.grad is not None and self._key is None:
+                if p.grad is None:
+                    continue
+                if set_to_none:
+                    p.grad = None
+                elif self._key is None or self.set_to_none:
                     p.grad.zero_()
 
     def _tables(self, params):
-        key = tuple((p.data_ptr(), p.grad.data_ptr()) for _, p in params)
-        if key == self._key:
+        gkey = [p.grad.data_ptr() for _, p in params]
+        pkey = [p.data_ptr() for _, p in params]
+        if self._key is not None and gkey == self._key[1] and pkey == self._key[0]:
             return
         if torch.cuda.is_current_stream_capturing():
             raise RuntimeError("HipAdamW: the parameter / gradient set changed during hipGraph capture "
                                "(run one eager step first)")
-        t = np.zeros(len(params), TENSOR_DTYPE)
-        chunks = []
-        for i, (gi, p) in enumerate(params):
+        for _, p in params:
             if not (p.grad.dtype == torch.float32 and p.grad.is_contiguous() and p.grad.shape == p.shape):
                 raise ValueError("HipAdamW needs contiguous fp32 gradients of the parameter's shape")
-            m, v = self.state[p]
-            sh = self._shadow.get(p)
-            t[i] = (p.data_ptr(), p.grad.data_ptr(), m.data_ptr(), v.data_ptr(), sh.data_ptr() if sh is not None else 0,
-                    p.numel(), gi, 0)
-            chunks += [(i, 0, o) for o in range(0, p.numel(), self.chunk)]
         dev = params[0][1].device
-        self._tens = torch.from_numpy(t.view(np.uint8).copy()).to(dev)
-        self._chunks = torch.from_numpy(np.array(chunks, CHUNK_DTYPE).view(np.uint8).copy()).to(dev)
-        self._nchunks = len(chunks)
-        self._partial = torch.empty(self._nchunks, device=dev)
+        if self._key is None or pkey != self._key[0]:  # the parameter set: tensor rows and chunk list
+            t = np.zeros(len(params), TENSOR_DTYPE)
+            chunks = []
+            for i, (gi, p) in enumerate(params):
+                m, v = self.state[p]
+                sh = self._shadow.get(p)
+                t[i] = (p.data_ptr(), 0, m.data_ptr(), v.data_ptr(), sh.data_ptr() if sh is not None else 0,
+                        p.numel(), gi, 0)
+                chunks += [(i, 0, o) for o in range(0, p.numel(), self.chunk)]
+            self._tab = t
+            self._chunks = torch.from_numpy(np.array(chunks, CHUNK_DTYPE).view(np.uint8).copy()).to(dev)
+            self._nchunks = len(chunks)
+            self._partial = torch.empty(self._nchunks, device=dev)
+        self._tab["g"] = np.asarray(gkey, np.uint64)  # only the gradient addresses change between steps
+        # through pinned memory, asynchronously: a pageable copy would hold the host until the stream drains
+        self._tens = torch.from_numpy(self._tab.view(np.uint8).copy()).pin_memory().to(dev, non_blocking=True)
+        self.table_writes += 1
         if not hasattr(self, "_state"):
             self._state = torch.zeros(8, device=dev)  # norm, clip factor, bias corrections, step (int32)
-        self._key = key
+        self._key = (pkey, gkey)
 
     @torch.no_grad()
     def step(self, max_norm=0.0):
@@ -106,7 +122,8 @@ class HipAdamW:
         check(self.lib.mmt_adamw_step(self._tens.data_ptr(), self._chunks.data_ptr(), self._nchunks,
                                       self._partial.data_ptr(), self._state.data_ptr(),
                                       ctypes.cast(lr, ctypes.c_void_p), ctypes.cast(wd, ctypes.c_void_p), n,
-                                      float(self.betas[0]), float(self.betas[1]), float(self.eps), float(max_norm), 1,
+                                      float(self.betas[0]), float(self.betas[1]), float(self.eps), float(max_norm),
+                                      0 if self.set_to_none else 1,
                                       torch.cuda.current_stream().cuda_stream), "mmt_adamw_step")
         self.last_norm = self._state[0]
         for p in self._shadow:

@@ -67,16 +67,17 @@ def _transpose(x, rows, cols, ld_out=None, ones_row=False):
     return out
 
 
-def _gemm(a, w, M, N, K, bias=None, out_f32=False, act=0, r=None, c2=None, c2_copy=0):
+def _gemm(a, w, M, N, K, bias=None, out_f32=False, act=0, r=None, c2=None, c2_copy=0, c=None, ldc=None):
     """C[M][N] = A[M][K] W[N][K]^T (+ bias), bf16 operands, fp32 accumulation (mmt_gemm); act / r (bf16,
     [M][N]) / c2 / c2_copy as mmt_gemm_params (act 1 GELU, 5 GELU backward against r; c2_copy 2: c2 = the
-    pre-activation)."""
+    pre-activation; 3: the last 8 columns to c2 [M][8]); c / ldc: a preallocated output and its pitch."""
     from ._lib import LIB, GemmParams, MMT_BF16, check
-    c = torch.empty(M, N, device=a.device, dtype=torch.float32 if out_f32 else torch.bfloat16)
+    if c is None:
+        c = torch.empty(M, N, device=a.device, dtype=torch.float32 if out_f32 else torch.bfloat16)
     p = GemmParams()
     p.a[0], p.w[0], p.c[0] = a.data_ptr(), w.data_ptr(), c.data_ptr()
     p.bias[0] = bias.data_ptr() if bias is not None else None
-    p.lda, p.ldc = K, N
+    p.lda, p.ldc = K, ldc or N
     p.a_seg_rows, p.a_segs_a = M, 1
     p.M, p.N, p.K, p.groups, p.c_f32 = M, N, K, 1, 1 if out_f32 else 0
     p.act = act
@@ -96,10 +97,15 @@ def _bf16_weight(w):
 
 def _weight_grads(dy, x, M, N, K):
     """dW [N][K] and db [N] of y = x W^T + b from one GEMM: dy^T [x | 1] (a row of ones appended to the
-    transposed activations gives the bias gradient as output column K; fp32 accumulation)."""
+    transposed activations gives the bias gradient as output column K; fp32 accumulation).  The GEMM
+    writes dW contiguous and its last 8 columns (db, then zeros) to a [N][8] block behind it (c2_copy 3),
+    so autograd takes dW as the parameter's .grad as it is (no accumulate / copy pass)."""
     Mp = (M + 7) // 8 * 8  # contraction over tokens, zero-padded to the GEMM's K granule
-    dwb = _gemm(_transpose(dy, M, N, Mp), _transpose(x, M, K, Mp, ones_row=True), N, K + 8, Mp, out_f32=True)
-    return dwb[:, :K], dwb[:, K]
+    buf = torch.empty(N * (K + 8), device=dy.device, dtype=torch.float32)
+    dw, db8 = buf[:N * K].view(N, K), buf[N * K:].view(N, 8)
+    _gemm(_transpose(dy, M, N, Mp), _transpose(x, M, K, Mp, ones_row=True), N, K + 8, Mp, out_f32=True,
+          c=dw, ldc=K, c2=db8, c2_copy=3)
+    return dw, db8[:, 0]
 
 
 class _HipLinear(torch.autograd.Function):
@@ -123,13 +129,10 @@ class _HipLinear(torch.autograd.Function):
         N = wb.shape[0]
         dy = dy.to(torch.bfloat16).contiguous()
         dx = _gemm(dy, _transpose(wb, N, K), M, K, N) if ctx.needs_input_grad[0] else None
-        Mp = (M + 7) // 8 * 8  # contraction over tokens, zero-padded to the GEMM's K granule
         # dW and the bias gradient from one GEMM: x^T carries an extra row of ones, so output column
         # K of dy^T [x | 1] is sum_m dy[m][n] (the same bf16 dy, fp32 accumulation; no reduce kernel)
-        dwb = _gemm(_transpose(dy, M, N, Mp), _transpose(x, M, K, Mp, ones_row=True), N, K + 8, Mp, out_f32=True)
-        # strided views: autograd accumulates them into the persistent .grad buffers with one add
-        # (HipAdamW keeps the gradients allocated), so a contiguous copy first would be a wasted pass
-        return dx, dwb[:, :K], dwb[:, K], None
+        dw, db = _weight_grads(dy, x, M, N, K)
+        return dx, dw, db, None
 
 
 class _HipMlp(torch.autograd.Function):
@@ -691,7 +694,7 @@ class TrainStep:
             from .optim import HipAdamW
             shadow = [m.weight for n, m in net.named_modules()
                       if isinstance(m, torch.nn.Linear) and "backbone" in n and m.weight.requires_grad]
-            self.opt = HipAdamW(groups, lr=lr, weight_decay=weight_decay, shadow=shadow)
+            self.opt = HipAdamW(groups, lr=lr, weight_decay=weight_decay, shadow=shadow, set_to_none=True)
         else:
             self.opt = torch.optim.AdamW(groups, lr=lr, weight_decay=weight_decay)
         self.hip_opt = next(net.parameters()).is_cuda
@@ -704,7 +707,7 @@ class TrainStep:
 
     def backward(self, t, o, s, gt_xywh):
         """Forward, loss and backward; under DDP the gradient all-reduce runs inside backward()."""
-        self.opt.zero_grad(set_to_none=not self.hip_opt)  # (HipAdamW zeroes them in its update)
+        self.opt.zero_grad(set_to_none=True)  # autograd then hands each fresh gradient over as .grad
         pred = self.model(t, o, s)
         loss, stats = box_loss(pred, gt_xywh, self.iou_weight, self.l1_weight)
         loss.backward()

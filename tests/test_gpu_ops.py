@@ -216,6 +216,45 @@ def test_gemm_gelu_backward_and_preact_epilogues(impl):
     assert (c5.float().cpu() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
 
 
+@pytest.mark.parametrize("impl", [-1, 0, 1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("splitk", [0, 3])
+@pytest.mark.parametrize("N,K,M", [(768, 3072, 776), (3072, 768, 1024), (256, 2112, 264)])
+def test_gemm_column_split_epilogue(impl, splitk, N, K, M):
+    """c2_copy 3 (the training dW GEMM, dy^T [x | 1]): output columns [0, M - 8) go to C with pitch
+    M - 8, the last 8 columns (the bias gradient, then zeros) to C2 [rows][8]; fp32 outputs.  Every
+    16-bit LDS-DMA configuration, with and without split-K (impl -1 rejects the mode)."""
+    if splitk and impl in (5, 7, 8):
+        pytest.skip("forced impl 5 / 7 / 8 take no split-K")
+    L = _lib()
+    g = torch.Generator().manual_seed(N + K + impl)
+    A = torch.randn(N, K, generator=g).bfloat16()  # dy^T
+    X = torch.randn(M, K, generator=g)  # [x | 1]^T: rows M - 8 ones, M - 7.. zeros
+    X[M - 8] = 1.0
+    X[M - 7:] = 0.0
+    Xb = X.bfloat16()
+    Ad, Xd = A.cuda(), Xb.cuda()
+    buf = torch.full((N * M,), float("nan"), device="cuda")
+    dw, db8 = buf[:N * (M - 8)].view(N, M - 8), buf[N * (M - 8):].view(N, 8)
+    kw = {}
+    if splitk:
+        kw["sk"] = (splitk, torch.empty(8 << 20, device="cuda"), torch.zeros(1 << 16, device="cuda", dtype=torch.int32))
+    p = _gemm_params([Ad.data_ptr()], [Xd.data_ptr()], [dw.data_ptr()], N, M, K, K, M - 8, c_f32=1,
+                     c2=[db8.data_ptr()], c2_copy=3, impl=impl, **kw)
+    rc = L.LIB.mmt_gemm(p, L.MMT_BF16, torch.cuda.current_stream().cuda_stream)
+    if impl == -1:
+        assert rc == -10000
+        return
+    L.check(rc, "gemm c2_copy 3")
+    torch.cuda.synchronize()
+    ref = A.float() @ Xb.float().t()
+    got = torch.cat([dw.cpu(), db8.cpu()], 1)
+    err = (got - ref).abs().max().item()
+    assert err <= 1e-3 * ref.abs().max().item() + 1e-4, err
+    assert torch.equal(db8[:, 1:].cpu(), torch.zeros(N, 7))
+    if splitk:
+        assert int(kw["sk"][2].abs().sum()) == 0
+
+
 @pytest.mark.parametrize("impl", [1, 2, 3, 4, 6])
 @pytest.mark.parametrize("splitk", [2, 3, 5])
 @pytest.mark.parametrize("M,N,K", [(528, 768, 3072), (77, 200, 1024), (400, 192, 640)])

@@ -328,12 +328,15 @@ def test_module_forward_training_gpu_grads(variant):
 
 
 @pytest.mark.parametrize("max_norm", [0.0, 0.1, 1e6])
-def test_hip_adamw_matches_torch(max_norm):
+@pytest.mark.parametrize("set_to_none", [False, True])
+def test_hip_adamw_matches_torch(max_norm, set_to_none):
     """mmt_adamw_grad_norm / mmt_adamw_step (mmt_amd.optim.HipAdamW) against
     torch.nn.utils.clip_grad_norm_ + torch.optim.AdamW(fused=True) over three parameter groups with their own
     lr / weight decay, tensor sizes below / across the 65536-element chunk and not multiples of 4,
     five steps: parameters and moments within 1e-6 relative per step, the norm within 1e-5, the
-    gradients zeroed by the update, and the bf16 shadow equal to the bf16 cast of the new weights."""
+    gradients zeroed by the update, and the bf16 shadow equal to the bf16 cast of the new weights.
+    set_to_none (the training step's mode): fresh gradient tensors every step (new addresses: the
+    pointer table is refreshed), left untouched by the update."""
     from mmt_amd.optim import HipAdamW
     g = torch.Generator().manual_seed(3)
     shapes = [(7,), (768, 768), (3, 65537), (130001,), (12, 64)]
@@ -343,11 +346,12 @@ def test_hip_adamw_matches_torch(max_norm):
     groups = lambda ps: [{"params": ps[:2], "lr": 1e-3}, {"params": ps[2:4], "lr": 2e-4, "weight_decay": 0.05},  # noqa: E731
                          {"params": ps[4:]}]
     opt_ref = torch.optim.AdamW(groups(ref), lr=5e-4, weight_decay=1e-4, fused=True)  # the form it replaces
-    opt = HipAdamW(groups(hip), lr=5e-4, weight_decay=1e-4, shadow=[hip[1]])
+    opt = HipAdamW(groups(hip), lr=5e-4, weight_decay=1e-4, shadow=[hip[1]], set_to_none=set_to_none)
     for step in range(5):
         grads = [torch.randn(s, generator=g).cuda() * (10.0 if step == 2 else 1.0) for s in shapes]
         opt_ref.zero_grad(set_to_none=True)
-        opt.zero_grad()
+        opt.zero_grad(set_to_none=set_to_none)
+        keep = [torch.empty(1 << 16, device="cuda") for _ in range(step)]  # moves the next allocations
         for p, q, gr in zip(ref, hip, grads):
             p.grad = gr.clone()
             if q.grad is None:
@@ -361,12 +365,16 @@ def test_hip_adamw_matches_torch(max_norm):
         torch.cuda.synchronize()
         if max_norm > 0:
             assert abs(opt.last_norm.item() - n_ref.item()) <= 1e-5 * n_ref.item()
-        for p, q in zip(ref, hip):
+        del keep
+        for k, (p, q) in enumerate(zip(ref, hip)):
             assert torch.allclose(q, p, rtol=1e-6, atol=1e-7), (step, (q - p).abs().max().item())
             m_r, v_r = opt_ref.state[p]["exp_avg"], opt_ref.state[p]["exp_avg_sq"]
             m_h, v_h = opt.state[q]
             assert torch.allclose(m_h, m_r, rtol=1e-5, atol=1e-7) and torch.allclose(v_h, v_r, rtol=1e-5, atol=1e-9)
-            assert int((q.grad != 0).sum()) == 0
+            if set_to_none:
+                assert torch.equal(q.grad, grads[k])
+            else:
+                assert int((q.grad != 0).sum()) == 0
         sh, ver = hip[1]._mmt_bf16
         assert ver == hip[1]._version and torch.equal(sh, hip[1].detach().to(torch.bfloat16))
 

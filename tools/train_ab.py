@@ -6,6 +6,7 @@ variants that swap one op back to aten.  One JSON line per (round, variant).
     python tools/train_ab.py --rounds 3 --steps 8 --warmup 3
 """
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -33,6 +34,32 @@ class SplitMlpOps(HipOps):
     mlp = None
 
 
+@contextlib.contextmanager
+def accumulated_grads():
+    """The previous gradient handling: persistent .grad buffers zeroed by the AdamW update, autograd
+    adding each step's (strided [N][K+8] view) dW into them."""
+    from mmt_amd import optim, train
+    saved = train._weight_grads, optim.HipAdamW.__init__, optim.HipAdamW.zero_grad
+
+    def weight_grads(dy, x, M, N, K):
+        Mp = (M + 7) // 8 * 8
+        dwb = train._gemm(train._transpose(dy, M, N, Mp), train._transpose(x, M, K, Mp, ones_row=True), N, K + 8,
+                          Mp, out_f32=True)
+        return dwb[:, :K], dwb[:, K]
+
+    def init(self, *a, **kw):
+        kw["set_to_none"] = False
+        saved[1](self, *a, **kw)
+
+    train._weight_grads = weight_grads
+    optim.HipAdamW.__init__ = init
+    optim.HipAdamW.zero_grad = lambda self, set_to_none=False: saved[2](self, False)
+    try:
+        yield
+    finally:
+        train._weight_grads, optim.HipAdamW.__init__, optim.HipAdamW.zero_grad = saved
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
@@ -42,14 +69,16 @@ def main():
     ap.add_argument("--only", default="", help="comma-separated variant names")
     args = ap.parse_args()
     variants = {"hip": HipOps, "aten_groupnorm": AtenGroupNormOps, "aten_layernorm": AtenLayerNormOps,
-                "split_mlp": SplitMlpOps}
+                "split_mlp": SplitMlpOps, "accum_grads": (HipOps, accumulated_grads)}
     if args.only:
         variants = {k: v for k, v in variants.items() if k in args.only.split(",")}
     for r in range(args.rounds):
         for name, ops in variants.items():
-            o = bench.train_bench(1, 0, args.batch, args.steps, args.warmup, ops=ops)
+            ops, ctx = ops if isinstance(ops, tuple) else (ops, contextlib.nullcontext)
+            with ctx():
+                o = bench.train_bench(1, 0, args.batch, args.steps, args.warmup, ops=ops)
             print(json.dumps({"round": r, "variant": name, "samples_per_s": o["value"], "ms_per_step": o["ms_per_step"],
-                              "frac": o["roofline"]["frac"], "loss": o["last_loss"]}), flush=True)
+                              "frac": o["roofline"]["frac"], "loss": o["last_loss"], "table_writes": o.get("opt_table_writes")}), flush=True)
 
 
 if __name__ == "__main__":
