@@ -79,7 +79,10 @@ extern "C" {
  *   v = (acc + bias) * GELU'(R) (R then not added; 16-bit LDS-DMA kernels);
  *   c2 == NULL: C = v (+ R if r != NULL);  c2 != NULL: C = v, C2 = v + R (c2_copy 1: C = v (+ R),
  *   C2 = the same values in `dtype`; c2_copy 2: C = v (+ R), C2 = acc + bias, the pre-activation, in
- *   `dtype`, no R needed -- the training step's fc1 keeps it for the GELU backward).
+ *   `dtype`, no R needed -- the training step's fc1 keeps it for the GELU backward; c2_copy 3: a
+ *   column split, output columns [0, N-8) to C with pitch ldc >= N-8 and the last 8 columns to C2
+ *   [M][8] (pitch 8), N % 8 == 0, no R needed -- the training dW GEMM, whose last column is the
+ *   bias gradient; 16-bit LDS-DMA kernels).
  *   R row index: r_mode 0 -> m, 1 -> m % r_p0, 2 -> conv map m=(b,y,x) of an r_p0 x r_p0 map read
  *   at (y / r_p1, x / r_p1) of an (r_p0/r_p1)^2 map.  R is fp32 (or dtype if r_t); C/C2 are fp32
  *   if c_f32 else dtype.
