@@ -35,12 +35,17 @@ def main():
         step(*batch)
         torch.cuda.synchronize()
     ka = prof.key_averages()
+    dev = lambda e: getattr(e, "self_device_time_total", getattr(e, "self_cuda_time_total", 0.0))  # noqa: E731
     rows = [e for e in ka if e.key.startswith("aten::")]
     rows.sort(key=lambda e: -e.count)
     print("%-44s %7s %12s %12s" % ("aten op", "calls", "self cpu us", "device us"))
     for e in rows[:args.top]:
-        dev = getattr(e, "self_device_time_total", getattr(e, "self_cuda_time_total", 0.0))
-        print("%-44s %7d %12.0f %12.0f" % (e.key[:44], e.count, e.self_cpu_time_total, dev))
+        print("%-44s %7d %12.0f %12.0f" % (e.key[:44], e.count, e.self_cpu_time_total, dev(e)))
+    kern = [e for e in ka if not e.key.startswith("aten::") and dev(e) > 0 and e.self_cpu_time_total == 0]
+    kern.sort(key=lambda e: -dev(e))
+    print("\n%-90s %7s %12s" % ("device kernel", "calls", "device us"))
+    for e in kern[:args.top]:
+        print("%-90s %7d %12.0f" % (e.key[:90], e.count, dev(e)))
 
 
 if __name__ == "__main__":
