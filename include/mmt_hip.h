@@ -145,6 +145,17 @@ typedef struct {
      *     in the K loop; the A map must be the identity (one segment, k_split == 0). */
     float* ln_stats_out[MMT_MAX_GROUPS];
     const float* ln_stats_in[MMT_MAX_GROUPS];
+    /* MN-major operands (16-bit LDS-DMA kernels, 128x128 tiles; plain GEMM mode: no conv, no LayerNorm
+     * fold, identity A map, k_split 0), read with ds_read_b64_tr_b16 instead of a transposed copy:
+     *   w_t 1: W given as W^T [K][ldw] (row k holds the N elements of contraction index k) -- the
+     *          Linear backward's dX = dY W reads the weight [N_out][K_in] as it is;
+     *   w_t 2: as 1 with N - 8 real columns, column N - 8 all ones and N - 7 .. N - 1 zero (with
+     *          c2_copy 3: the dW GEMM's bias gradient as the last column block);
+     *   a_t 1 (needs w_t): A given as A^T [K][lda] (M % 8 == 0, lda >= M) -- dW = dY^T X reads dY and
+     *          X as they are.  K need not be a multiple of 64 (rows past K are zero). */
+    int32_t a_t;
+    int32_t w_t;
+    int64_t ldw;
 } mmt_gemm_params;
 
 int mmt_gemm(const mmt_gemm_params* p, int dtype, void* stream);

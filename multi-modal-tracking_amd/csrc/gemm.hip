@@ -336,6 +336,13 @@ int check_gemm(const mmt_gemm_params& p) {
         if (p.a_seg_rows <= 0 || p.a_segs_a <= 0) return MMT_EBADARG;
         if (p.k_split % EPC || p.a_stride_a % EPC || p.a_stride_b % EPC) return MMT_EBADARG;
     }
+    // MN-major operands (16-bit LDS-DMA kernels): W alone (w_t 1 / 2) or A and W (a_t 1), plain GEMM mode
+    if (p.a_t < 0 || p.a_t > 1 || p.w_t < 0 || p.w_t > 2 || (p.a_t && !p.w_t)) return MMT_EBADARG;
+    if (p.w_t) {
+        if (sizeof(T) != 2 || p.conv_h > 0 || p.ln_fold || p.k_split || p.a_seg_rows < p.M) return MMT_EBADARG;
+        if (p.N % 8 || p.ldw % EPC || p.ldw < (p.w_t == 2 ? p.N - 8 : p.N)) return MMT_EBADARG;
+        if (p.a_t && (p.M % 8 || p.lda < p.M)) return MMT_EBADARG;
+    }
     if (p.r_mode == 2 && (p.r_p1 < 1 || p.r_p0 % p.r_p1)) return MMT_EBADARG;
     if (p.r_mode == 1 && p.r_p0 < 1) return MMT_EBADARG;
     if (p.c_seg_rows < 0 || (p.c_seg_rows > 0 && (p.conv_h > 0 || p.c_seg_pitch < p.c_seg_rows))) return MMT_EBADARG;
@@ -346,6 +353,7 @@ int check_gemm(const mmt_gemm_params& p) {
         if (p.c2[g] && !p.r[g] && p.c2_copy < 2) return MMT_EBADARG;
         if ((p.act == 5 && !p.r[g]) || (p.c2_copy >= 2 && !p.c2[g])) return MMT_EBADARG;
         if (p.c2_copy == 3 && (p.N % 8 || p.ldc < p.N - 8)) return MMT_EBADARG;
+        if (p.w_t && (((uintptr_t)p.w[g] & 15) || (p.a_t && ((uintptr_t)p.a[g] & 15)))) return MMT_EBADARG;
     }
     return 0;
 }
@@ -363,7 +371,7 @@ int launch_gemm(const mmt_gemm_params& p, hipStream_t st) {
     }
     if constexpr (sizeof(T) == 2)
         if (mmt_gemm_glds<T>(p, st, p.impl) == 0) return launch_status();
-    if (p.ln_fold || p.c2_copy || p.act == 5) return MMT_EBADARG;  // LDS-DMA kernel features only
+    if (p.ln_fold || p.c2_copy || p.act == 5 || p.w_t) return MMT_EBADARG;  // LDS-DMA kernel features only
     if (p.conv_h > 0) launch_tiles<T, true>(p, st);
     else launch_tiles<T, false>(p, st);
     return launch_status();

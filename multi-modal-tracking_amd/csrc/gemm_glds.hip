@@ -75,6 +75,27 @@ MMT_DEV void wait_stages(int ahead) {
 // Zero source for A chunks outside the operand: conv padding taps and the K tail past K (a glds
 // lane cannot zero its LDS bytes, so it loads zeros instead).
 __device__ __attribute__((aligned(64))) const uint32_t g_zero_chunk[16] = {0};
+// Ones column of the MN-major W operand (w_t 2): the chunk of columns N-8 .. N-1 is (1, 0, ..., 0) in
+// every contraction row (bf16 / fp16 one in the low half of the first dword).
+__device__ __attribute__((aligned(64))) const uint32_t g_one_chunk_bf16[4] = {0x3F80u, 0u, 0u, 0u};
+__device__ __attribute__((aligned(64))) const uint32_t g_one_chunk_f16[4] = {0x3C00u, 0u, 0u, 0u};
+
+// ds_read_b64_tr_b16 as inline asm (the builtin makes hipcc drain vmcnt(0), i.e. the whole DMA ring,
+// before each read); the K loop orders the reads against their MFMAs itself (lds_barrier's lgkmcnt(0)
+// or an explicit wait, then a register pin).
+template <int OFF>
+MMT_DEV uint2 gemm_tr16(const unsigned char* p) {
+    uint2 r;
+    const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) unsigned char*)p;
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(a), "n"(OFF));
+    return r;
+}
+
+// MN-major operand images (mmt_gemm_params.a_t / w_t, LNM 3 / 4): the 64 contraction rows of a K-step
+// as 256-B rows of 128 M (or N) elements; 16-B chunk c of row k stored at c ^ gemm_trsw(k), which
+// makes the transposed fragment reads below conflict-free (the 8 rows a 32-lane half reads, k & 3 and
+// bit 3 distinct, land on 8 disjoint 32-B bank groups).
+MMT_DEV int gemm_trsw(int k) { return 2 * ((k & 3) | (((k >> 3) & 1) << 2)); }
 
 // WGM x WGN waves per k-group own WM x WN sub-tiles; KS k-groups split the K-steps.  CONV: A is
 // the implicit im2col of an NHWC 3x3/pad-1 (conv_k3) or 1x1 convolution, input read through the
@@ -94,7 +115,10 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
     constexpr int WM = BM / WGM, WN = BN / WGN, MT = WM / 16, NT = WN / 16;
     static_assert(KS * ST * STAGE <= 160 * 1024, "LDS budget");
     constexpr bool SB = BM * BN >= 256 * 256 || OCC > 1;  // single-buffered fragments (impl 7's 256x256; impl 8)
-    static_assert(!SB || (KS == 1 && LNM == 0 && !CONV), "impl 7: plain GEMM only");
+    static_assert(!SB || (KS == 1 && (LNM == 0 || LNM >= 3) && !CONV), "impl 7: plain GEMM only");
+    // LNM 3: W given MN-major (W^T [K][ldw], the Linear backward's dX); 4: A and W MN-major (dW)
+    constexpr bool TA = LNM == 4, TB = LNM == 3 || LNM == 4;
+    static_assert(!TB || (BM == 128 && BN == 128 && !CONV), "MN-major operands: 128x128 tiles");
     static_assert(KS == 1 || BM * BN * 4 <= KS * ST * STAGE, "k-group reduction buffer");
     __shared__ __attribute__((aligned(1024))) unsigned char lds[KS * ST * STAGE];
     MMT_STAMP(0, "s_memrealtime");
@@ -119,7 +143,7 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
         tm = tile % tiles_m;
         tn = tile / tiles_m;
     }
-    constexpr bool LNF = LNM != 0;  // LayerNorm folded: 1 = row statistics from the A fragments, 2 = handed in
+    constexpr bool LNF = LNM == 1 || LNM == 2;  // LayerNorm folded: 1 = row statistics from the A fragments, 2 = handed in
     const int m0_tile = tm * BM, n0 = tn * BN;
     const int lane = threadIdx.x & 63, kg = threadIdx.x / TPG;
     const int wid = (threadIdx.x % TPG) >> 6, wr = wid / WGN, wc = wid % WGN;
@@ -175,7 +199,16 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
         const int k = (min(s * KS + kg, nk - 1) + kb0) * KT + pch * 8;  // this lane's 8-element chunk
         const bool kin = k < K;
         unsigned char* base = ring + (s % ST) * STAGE;
-        if constexpr (!CONV) {
+        // MN-major images: lane -> row (lane >> 4) of its 4-row piece, physical chunk lane & 15
+        const int kst = (min(s * KS + kg, nk - 1) + kb0) * KT, trq = lane >> 4, trc = lane & 15;
+        if constexpr (TA) {
+#pragma unroll
+            for (int i = 0; i < PA; ++i) {
+                const int kr = (wid * PA + i) * 4 + trq, kk = kst + kr, m = m0_tile + (trc ^ gemm_trsw(kr)) * 8;
+                glds16(kk < K && m < M ? (const void*)(A0 + (int64_t)kk * p.lda + m) : (const void*)g_zero_chunk,
+                       base + (wid * PA + i) * 1024);
+            }
+        } else if constexpr (!CONV) {
             const bool hp = ks > 0 && k >= ks;
             const T* ab = (hp ? A1 - ks : A0) + k;
 #pragma unroll
@@ -204,9 +237,21 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
                 glds16(ok ? (const void*)src : (const void*)g_zero_chunk, base + (wid * PA + i) * 1024);
             }
         }
-        const int kw = kin ? k : 0;  // past K: any in-bounds W bytes (they meet zero A chunks)
+        if constexpr (TB) {
+            const void* one = __is_same(T, bf16_t) ? (const void*)g_one_chunk_bf16 : (const void*)g_one_chunk_f16;
 #pragma unroll
-        for (int i = 0; i < PB; ++i) glds16(W + boff[i] + kw, base + BM * 128 + (wid * PB + i) * 1024);
+            for (int i = 0; i < PB; ++i) {
+                const int kr = (wid * PB + i) * 4 + trq, kk = kst + kr, n = n0 + (trc ^ gemm_trsw(kr)) * 8;
+                const void* src = kk >= K || n >= N ? (const void*)g_zero_chunk
+                                  : p.w_t == 2 && n == N - 8 ? one
+                                                             : (const void*)(W + (int64_t)kk * p.ldw + n);
+                glds16(src, base + BM * 128 + (wid * PB + i) * 1024);
+            }
+        } else {
+            const int kw = kin ? k : 0;  // past K: any in-bounds W bytes (they meet zero A chunks)
+#pragma unroll
+            for (int i = 0; i < PB; ++i) glds16(W + boff[i] + kw, base + BM * 128 + (wid * PB + i) * 1024);
+        }
     };
 
     constexpr int MTW = (MT + WGN - 1) / WGN;  // LNF: fragment rows whose statistics this wave sums
@@ -220,18 +265,47 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
 #pragma unroll
         for (int j = 0; j < MT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    // MN-major image: the 16 x 32 fragment of rows c0 .. c0+15, K-half t, as two transposed 4 x 16 reads
+    // (lane l16 gets row c0 + l16, contraction 32t + 8lg + 4h .. +3 in read h)
+    const int trl = 2 * (lg & 1) * 4, trq4 = l16 >> 2, trp = l16 & 3;
+    auto tr_frag = [&](const unsigned char* img, int t, int c0) -> u32x4 {
+        const int sw = 2 * trq4 + trl;  // gemm_trsw of rows 32t + 8lg + 4h + trq4
+        const unsigned char* a = img + (32 * t + 8 * lg + trq4) * 256 + ((((c0 >> 3) + (trp >> 1)) ^ sw) * 16) + 8 * (trp & 1);
+        const uint2 lo = gemm_tr16<0>(a), hi = gemm_tr16<1024>(a);
+        return u32x4{lo.x, lo.y, hi.x, hi.y};
+    };
+    auto frag_a = [&](const unsigned char* b_, int t, int sw_, int mt) -> u32x4 {
+        if constexpr (TA) return tr_frag(b_, t, wr * WM + mt * 16);
+        else return *(const u32x4*)(b_ + ((wr * WM + mt * 16 + l16) * 8 + sw_) * 16);
+    };
+    auto frag_b = [&](const unsigned char* b_, int t, int sw_, int nt) -> u32x4 {
+        if constexpr (TB) return tr_frag(b_ + BM * 128, t, wc * WN + nt * 16);
+        else return *(const u32x4*)(b_ + BM * 128 + ((wc * WN + nt * 16 + l16) * 8 + sw_) * 16);
+    };
     // Fragments of one K-step: [t][*] = the two 32-deep halves of the 64-deep step.
 #define MMT_READ(BUF, AF, BF, MTV)                                                                               \
     {                                                                                                            \
         const unsigned char* b_ = (BUF);                                                                         \
         _Pragma("unroll") for (int t = 0; t < 2; ++t) {                                                          \
             const int sw_ = (4 * t + lg) ^ (lane & 7);                                                           \
-            _Pragma("unroll") for (int mt = 0; mt < MTV; ++mt) AF[t][mt] =                                       \
-                *(const u32x4*)(b_ + ((wr * WM + mt * 16 + l16) * 8 + sw_) * 16);                                \
-            _Pragma("unroll") for (int nt = 0; nt < NT; ++nt) BF[t][nt] =                                        \
-                *(const u32x4*)(b_ + BM * 128 + ((wc * WN + nt * 16 + l16) * 8 + sw_) * 16);                     \
+            _Pragma("unroll") for (int mt = 0; mt < MTV; ++mt) AF[t][mt] = frag_a(b_, t, sw_, mt);               \
+            _Pragma("unroll") for (int nt = 0; nt < NT; ++nt) BF[t][nt] = frag_b(b_, t, sw_, nt);                \
         }                                                                                                        \
         __builtin_amdgcn_sched_barrier(0); /* all reads issue before the MFMAs that hide them */                 \
+    }
+    // asm (transposed) reads: after the wait that completed them, the registers pass through an empty asm
+    // so that no MFMA reading them is scheduled above it (no-op for the plain reads)
+#define MMT_PIN(AF, BF, MTV)                                                                                     \
+    if constexpr (TB) {                                                                                          \
+        _Pragma("unroll") for (int t = 0; t < 2; ++t) {                                                          \
+            _Pragma("unroll") for (int mt = 0; mt < MTV; ++mt) asm volatile("" : "+v"(AF[t][mt]));               \
+            _Pragma("unroll") for (int nt = 0; nt < NT; ++nt) asm volatile("" : "+v"(BF[t][nt]));                \
+        }                                                                                                        \
+    }
+#define MMT_WAIT_PIN(AF, BF, MTV)                                                                                \
+    if constexpr (TB) {                                                                                          \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                       \
+        MMT_PIN(AF, BF, MTV)                                                                                     \
     }
 #define MMT_MMA(AF, BF, MTV)                                                                                     \
     {                                                                                                            \
@@ -293,9 +367,16 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
                 for (int t = 0; t < 2; ++t) {
                     const int sw_ = (4 * t + lg) ^ (lane & 7);
 #pragma unroll
-                    for (int mt = 0; mt < MTV; ++mt) ha[0][mt] = *(const u32x4*)(b_ + ((wr * WM + mt * 16 + l16) * 8 + sw_) * 16);
+                    for (int mt = 0; mt < MTV; ++mt) ha[0][mt] = frag_a(b_, t, sw_, mt);
 #pragma unroll
-                    for (int nt = 0; nt < NT; ++nt) hb[0][nt] = *(const u32x4*)(b_ + BM * 128 + ((wc * WN + nt * 16 + l16) * 8 + sw_) * 16);
+                    for (int nt = 0; nt < NT; ++nt) hb[0][nt] = frag_b(b_, t, sw_, nt);
+                    if constexpr (TB) {
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+                        for (int mt = 0; mt < MTV; ++mt) asm volatile("" : "+v"(ha[0][mt]));
+#pragma unroll
+                        for (int nt = 0; nt < NT; ++nt) asm volatile("" : "+v"(hb[0][nt]));
+                    }
 #pragma unroll
                     for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
@@ -311,20 +392,25 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
         // conditional MFMA block inside the loop made hipcc shuttle them through VGPRs every step).
         int s = 0;
         for (; s + 2 < ns; s += 2) {
-            sync_for(s + 1);
+            sync_for(s + 1);  // (its lds_barrier waits lgkmcnt(0): fa0 / fb0 are complete)
+            MMT_PIN(fa0, fb0, MTV);
             MMT_READ(ring + ((s + 1) % ST) * STAGE, fa1, fb1, MTV);
             MMT_MMA(fa0, fb0, MTV);
             sync_for(s + 2);
+            MMT_PIN(fa1, fb1, MTV);
             MMT_READ(ring + ((s + 2) % ST) * STAGE, fa0, fb0, MTV);
             MMT_MMA(fa1, fb1, MTV);
         }
         const bool last_ok = KS == 1 || (ns - 1) * KS + kg < nk;
         if (s + 1 < ns) {
             sync_for(s + 1);
+            MMT_PIN(fa0, fb0, MTV);
             MMT_READ(ring + ((s + 1) % ST) * STAGE, fa1, fb1, MTV);
             MMT_MMA(fa0, fb0, MTV);
+            MMT_WAIT_PIN(fa1, fb1, MTV);
             if (last_ok) MMT_MMA(fa1, fb1, MTV);
         } else if (last_ok) {
+            MMT_WAIT_PIN(fa0, fb0, MTV);
             MMT_MMA(fa0, fb0, MTV);
         }
     };
@@ -334,6 +420,8 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
     else kloop(gemm_ic<MT>{});  // whole fragments (other partial counts: padding computed, not stored)
 #undef MMT_READ
 #undef MMT_MMA
+#undef MMT_PIN
+#undef MMT_WAIT_PIN
     MMT_STAMP(3, "s_memtime");
 
     // ---- epilogue through LDS.  Fragment-shaped stores (16 rows x 32 B per wave-instruction) ran
@@ -345,7 +433,7 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
     // EPASS: a tile whose fp32 image does not fit the stage ring (256x256) is assembled and written
     // out in WGM passes of one wave row (WM rows) each
     constexpr int EPASS = BM * TP * 4 + KS * BM * 8 + 16 <= KS * ST * STAGE ? 1 : WGM, EB = BM / EPASS;
-    static_assert(EPASS == 1 || (EB == WM && KS == 1 && LNM == 0), "multi-pass epilogue: plain GEMM tiles");
+    static_assert(EPASS == 1 || (EB == WM && KS == 1 && (LNM == 0 || LNM >= 3)), "multi-pass epilogue: plain GEMM tiles");
     static_assert(EB * TP * 4 <= KS * ST * STAGE, "epilogue pass fits in the stage ring");
     constexpr int FLAG_OFF = EB * TP * 4 + KS * BM * 8;  // split-K "this workgroup sums" word
     float* ctile = (float*)lds;
@@ -708,6 +796,18 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
     gemm_glds_tile<T, BM, BN, WGM, WGN, KS, ST, false, 0, 2>(p, g, tile, slice, nsk, gridDim.x);
 }
 
+// impl 8's tile with MN-major operands (LNM 3: W; 4: A and W)
+template <typename T, int LNM>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void gemm_glds_kernel_occ2_t(
+    const mmt_gemm_params p) {
+    const int nsk = gridDim.y;
+    const int lin = gemm_xcd_lin();
+    const int per_g = gridDim.x * nsk;
+    const int g = lin / per_g, rem_t = lin - g * per_g;
+    const int tile = rem_t / nsk, slice = rem_t - tile * nsk;
+    gemm_glds_tile<T, 128, 128, 2, 4, 1, 2, false, LNM, 2>(p, g, tile, slice, nsk, gridDim.x);
+}
+
 // Several independent GEMMs of one kernel configuration in one launch (mmt_gemm_multi): problem i
 // owns the remapped linear ids [wg0[i], wg0[i + 1]), (group, tile) with the tile fastest, no split-K.
 // The head's parallel conv chains and the fusion encoder's value / offset Linears are each a
@@ -815,6 +915,32 @@ int mmt_gemm_glds(const mmt_gemm_params& p, hipStream_t st, int force) {
         return (float)((wg + 255) / 256) * (c.fixed_us + (float)((steps + c.ks - 1) / c.ks) * c.step_us) + red;
     };
     int cfg = force, nsk = 1;
+    if (p.a_t || p.w_t) {  // MN-major operands: the 128x128 tiles (impl 1, or impl 8 on big unsplit grids)
+        if (force != 0 && force != 1 && force != 8) return 1;
+        const bool big = tiles_of(p, 128, 128) * p.groups > 256;
+        const Cand& c = cands[0];
+        if (force == 1 || (force == 0 && !big)) {
+            cfg = 1;
+            const int nmax = p.splitk >= 1 ? std::min(p.splitk, max_split(c)) : max_split(c);
+            float best = 1e30f;
+            for (int n = (p.splitk >= 2 ? nmax : 1); n <= nmax; ++n) {
+                const float t = cost(c, n) * (n > 1 && p.splitk == 0 ? 1.15f : 1.f);
+                if (t < best) best = t, nsk = n;
+            }
+        } else {
+            cfg = 8;
+        }
+        const int lnm = p.a_t ? 4 : 3;
+        const dim3 grid((unsigned)tiles_of(p, 128, 128), nsk, p.groups);
+        if (cfg == 8) {
+            if (lnm == 4) hipLaunchKernelGGL((gemm_glds_kernel_occ2_t<T, 4>), grid, dim3(512), 0, st, p);
+            else hipLaunchKernelGGL((gemm_glds_kernel_occ2_t<T, 3>), grid, dim3(512), 0, st, p);
+        } else {
+            if (lnm == 4) hipLaunchKernelGGL((gemm_glds_kernel<T, 128, 128, 2, 4, 1, 4, false, 4>), grid, dim3(512), 0, st, p);
+            else hipLaunchKernelGGL((gemm_glds_kernel<T, 128, 128, 2, 4, 1, 4, false, 3>), grid, dim3(512), 0, st, p);
+        }
+        return 0;
+    }
     if (cfg == 0) {
         float best = 1e30f;
         // 128x256 (impl 6) only for grids of more than one round of 128x128 tiles: the batch-1 grids
@@ -913,7 +1039,9 @@ int mmt_gemm_glds_multi(const mmt_gemm_params* ps, int n, hipStream_t st) {
     const int force = ps[0].impl;
     for (int i = 0; i < n; ++i) {
         const mmt_gemm_params& p = ps[i];
-        if (!glds_takes(p) || (p.conv_h > 0) != conv || p.ln_fold || p.impl != force || force < 0 || force > 4) return 1;
+        if (!glds_takes(p) || (p.conv_h > 0) != conv || p.ln_fold || p.impl != force || force < 0 || force > 4 ||
+            p.a_t || p.w_t)
+            return 1;
     }
     int cfg = force;
     if (cfg == 0) {

@@ -67,17 +67,38 @@ def _transpose(x, rows, cols, ld_out=None, ones_row=False):
     return out
 
 
-def _gemm(a, w, M, N, K, bias=None, out_f32=False, act=0, r=None, c2=None, c2_copy=0, c=None, ldc=None):
+# The Linear backward reads dY, X and W as they are (MN-major GEMM operands, ds_read_b64_tr_b16) instead
+# of transposed copies; False: the transposing form (A/B knob, tools/train_ab.py)
+MN_MAJOR = True
+_SPLITK = {}  # device -> (slab workspace, arrival tickets) of the dW GEMMs' split-K (stream-ordered: one set)
+
+
+def _splitk_ws(dev):
+    ws = _SPLITK.get(dev)
+    if ws is None:
+        ws = _SPLITK[dev] = (torch.empty(16 << 20, device=dev, dtype=torch.float32),
+                             torch.zeros(1 << 16, device=dev, dtype=torch.int32))
+    return ws
+
+
+def _gemm(a, w, M, N, K, bias=None, out_f32=False, act=0, r=None, c2=None, c2_copy=0, c=None, ldc=None, a_t=0,
+          w_t=0, ldw=0, lda=None, splitk=False):
     """C[M][N] = A[M][K] W[N][K]^T (+ bias), bf16 operands, fp32 accumulation (mmt_gemm); act / r (bf16,
     [M][N]) / c2 / c2_copy as mmt_gemm_params (act 1 GELU, 5 GELU backward against r; c2_copy 2: c2 = the
-    pre-activation; 3: the last 8 columns to c2 [M][8]); c / ldc: a preallocated output and its pitch."""
+    pre-activation; 3: the last 8 columns to c2 [M][8]); c / ldc: a preallocated output and its pitch;
+    a_t / w_t / ldw / lda: MN-major operands (A^T [K][lda], W^T [K][ldw]); splitk: with a split-K
+    workspace (the cost model may split K over workgroups)."""
     from ._lib import LIB, GemmParams, MMT_BF16, check
     if c is None:
         c = torch.empty(M, N, device=a.device, dtype=torch.float32 if out_f32 else torch.bfloat16)
     p = GemmParams()
     p.a[0], p.w[0], p.c[0] = a.data_ptr(), w.data_ptr(), c.data_ptr()
     p.bias[0] = bias.data_ptr() if bias is not None else None
-    p.lda, p.ldc = K, ldc or N
+    p.lda, p.ldc = lda or K, ldc or N
+    p.a_t, p.w_t, p.ldw = a_t, w_t, ldw
+    if splitk:
+        ws, cnt = _splitk_ws(a.device)
+        p.sk_ws, p.sk_ws_floats, p.sk_cnt, p.sk_cnt_n = ws.data_ptr(), ws.numel(), cnt.data_ptr(), cnt.numel()
     p.a_seg_rows, p.a_segs_a = M, 1
     p.M, p.N, p.K, p.groups, p.c_f32 = M, N, K, 1, 1 if out_f32 else 0
     p.act = act
@@ -100,12 +121,23 @@ def _weight_grads(dy, x, M, N, K):
     transposed activations gives the bias gradient as output column K; fp32 accumulation).  The GEMM
     writes dW contiguous and its last 8 columns (db, then zeros) to a [N][8] block behind it (c2_copy 3),
     so autograd takes dW as the parameter's .grad as it is (no accumulate / copy pass)."""
-    Mp = (M + 7) // 8 * 8  # contraction over tokens, zero-padded to the GEMM's K granule
     buf = torch.empty(N * (K + 8), device=dy.device, dtype=torch.float32)
     dw, db8 = buf[:N * K].view(N, K), buf[N * K:].view(N, 8)
+    if MN_MAJOR and M % 8 == 0:  # dY [M][N] and X [M][K] read as they are (a_t, w_t 2: the ones column)
+        _gemm(dy, x, N, K + 8, M, out_f32=True, c=dw, ldc=K, c2=db8, c2_copy=3, a_t=1, w_t=2, ldw=K, lda=N,
+              splitk=True)
+        return dw, db8[:, 0]
+    Mp = (M + 7) // 8 * 8  # contraction over tokens, zero-padded to the GEMM's K granule
     _gemm(_transpose(dy, M, N, Mp), _transpose(x, M, K, Mp, ones_row=True), N, K + 8, Mp, out_f32=True,
           c=dw, ldc=K, c2=db8, c2_copy=3)
     return dw, db8[:, 0]
+
+
+def _dx(dy, wb, M, N, K, act=0, r=None):
+    """dX [M][K] = dY [M][N] W [N][K] (bf16 out; act 5: times GELU'(r))."""
+    if MN_MAJOR:  # W read MN-major as it is
+        return _gemm(dy, wb, M, K, N, act=act, r=r, w_t=1, ldw=K)
+    return _gemm(dy, _transpose(wb, N, K), M, K, N, act=act, r=r)
 
 
 class _HipLinear(torch.autograd.Function):
@@ -128,7 +160,7 @@ class _HipLinear(torch.autograd.Function):
         M, K = x.shape
         N = wb.shape[0]
         dy = dy.to(torch.bfloat16).contiguous()
-        dx = _gemm(dy, _transpose(wb, N, K), M, K, N) if ctx.needs_input_grad[0] else None
+        dx = _dx(dy, wb, M, N, K) if ctx.needs_input_grad[0] else None
         # dW and the bias gradient from one GEMM: x^T carries an extra row of ones, so output column
         # K of dy^T [x | 1] is sum_m dy[m][n] (the same bf16 dy, fp32 accumulation; no reduce kernel)
         dw, db = _weight_grads(dy, x, M, N, K)
@@ -159,9 +191,9 @@ class _HipMlp(torch.autograd.Function):
         M, C = x.shape
         F4 = wb1.shape[0]
         dy = dy.to(torch.bfloat16).contiguous()
-        dhp = _gemm(dy, _transpose(wb2, C, F4), M, F4, C, act=5, r=hp)  # d(pre-activation), bf16
+        dhp = _dx(dy, wb2, M, C, F4, act=5, r=hp)  # d(pre-activation), bf16
         dw2, db2 = _weight_grads(dy, h, M, C, F4)
-        dx = _gemm(dhp, _transpose(wb1, F4, C), M, C, F4) if ctx.needs_input_grad[0] else None
+        dx = _dx(dhp, wb1, M, F4, C) if ctx.needs_input_grad[0] else None
         dw1, db1 = _weight_grads(dhp, x, M, F4, C)
         return dx, dw1, db1, dw2, db2
 

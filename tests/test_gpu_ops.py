@@ -255,6 +255,91 @@ def test_gemm_column_split_epilogue(impl, splitk, N, K, M):
         assert int(kw["sk"][2].abs().sum()) == 0
 
 
+def _mn_major(p, a_t, w_t, ldw):
+    p.a_t, p.w_t, p.ldw = a_t, w_t, ldw
+    return p
+
+
+@pytest.mark.parametrize("impl", [0, 1, 8])
+@pytest.mark.parametrize("splitk", [0, 3])
+@pytest.mark.parametrize("M,N,K,act", [(1056, 768, 2304, 0), (200, 136, 1000, 5), (4224, 3072, 768, 5), (96, 64, 72, 0)])
+def test_gemm_mn_major_w(impl, splitk, M, N, K, act):
+    """w_t 1 (the Linear backward's dX = dY W): W given MN-major as W^T [K][ldw] and read with
+    ds_read_b64_tr_b16; plain and GELU-backward (act 5) epilogues, K tails (K % 64 != 0), row / column
+    tails, split-K; every launch repeats bitwise; impl -1 / 2 reject the mode."""
+    if splitk and impl == 8:
+        pytest.skip("impl 8 takes no split-K")
+    L = _lib()
+    g = torch.Generator().manual_seed(M + N + K + act)
+    A = torch.randn(M, K, generator=g).bfloat16()
+    Wt = (torch.randn(K, N + 8, generator=g) / math.sqrt(K)).bfloat16()  # pitch N + 8 (ldw > N)
+    b = torch.randn(N, generator=g)
+    R = (torch.randn(M, N, generator=g) * 2).bfloat16()
+    Ad, Wd, bd, Rd = A.cuda(), Wt.cuda(), b.cuda(), R.cuda()
+    kw = {"r": [Rd.data_ptr()], "ldr": N, "r_t": 1} if act == 5 else {}
+    if splitk:
+        kw["sk"] = (splitk, torch.empty(8 << 20, device="cuda"), torch.zeros(1 << 16, device="cuda", dtype=torch.int32))
+    outs = []
+    for rep in range(2):
+        c = torch.full((M, N), float("nan"), device="cuda")
+        p = _mn_major(_gemm_params([Ad.data_ptr()], [Wd.data_ptr()], [c.data_ptr()], M, N, K, K, N, bias=[bd.data_ptr()],
+                                   act=act, c_f32=1, impl=impl, **kw), 0, 1, N + 8)
+        L.check(L.LIB.mmt_gemm(p, L.MMT_BF16, torch.cuda.current_stream().cuda_stream), "gemm w_t 1")
+        torch.cuda.synchronize()
+        outs.append(c.cpu())
+    ref = A.float() @ Wt[:, :N].float() + b
+    if act == 5:
+        r = R.float().requires_grad_(True)
+        F.gelu(r).backward(torch.ones_like(r))
+        ref = ref * r.grad
+    err = (outs[0] - ref).abs().max().item()
+    assert err <= 2e-3 * ref.abs().max().item() + 1e-4, err
+    assert torch.equal(outs[0], outs[1])
+    if splitk:
+        assert int(kw["sk"][2].abs().sum()) == 0
+    for bad in (-1, 2):
+        p = _mn_major(_gemm_params([Ad.data_ptr()], [Wd.data_ptr()], [c.data_ptr()], M, N, K, K, N, c_f32=1, impl=bad),
+                      0, 1, N + 8)
+        assert L.LIB.mmt_gemm(p, L.MMT_BF16, torch.cuda.current_stream().cuda_stream) == -10000
+
+
+@pytest.mark.parametrize("impl", [0, 1, 8])
+@pytest.mark.parametrize("splitk", [0, 4])
+@pytest.mark.parametrize("M,Kx,T", [(768, 768, 8448), (2304, 768, 1000), (136, 200, 520), (3072, 768, 4224)])
+def test_gemm_mn_major_dw(impl, splitk, M, Kx, T):
+    """a_t 1 + w_t 2 + c2_copy 3: the Linear backward's dW / db = dY^T [X | 1] straight from dY [T][M] and
+    X [T][Kx] (both MN-major, no transposed copies): dW [M][Kx] contiguous, db in column 0 of C2 [M][8],
+    columns 1..7 zero; T (the contraction) not a multiple of 64; split-K; bitwise repeatable."""
+    if splitk and impl == 8:
+        pytest.skip("impl 8 takes no split-K")
+    L = _lib()
+    g = torch.Generator().manual_seed(M + Kx + T)
+    dY = torch.randn(T, M, generator=g).bfloat16()
+    X = torch.randn(T, Kx, generator=g).bfloat16()
+    dYd, Xd = dY.cuda(), X.cuda()
+    kw = {}
+    if splitk:
+        kw["sk"] = (splitk, torch.empty(16 << 20, device="cuda"), torch.zeros(1 << 16, device="cuda", dtype=torch.int32))
+    outs = []
+    for rep in range(2):
+        buf = torch.full((M * (Kx + 8),), float("nan"), device="cuda")
+        dw, db8 = buf[:M * Kx].view(M, Kx), buf[M * Kx:].view(M, 8)
+        p = _mn_major(_gemm_params([dYd.data_ptr()], [Xd.data_ptr()], [dw.data_ptr()], M, Kx + 8, T, M, Kx, c_f32=1,
+                                   c2=[db8.data_ptr()], c2_copy=3, impl=impl, **kw), 1, 2, Kx)
+        L.check(L.LIB.mmt_gemm(p, L.MMT_BF16, torch.cuda.current_stream().cuda_stream), "gemm a_t 1 w_t 2")
+        torch.cuda.synchronize()
+        outs.append(buf.cpu())
+    dw, db8 = outs[0][:M * Kx].view(M, Kx), outs[0][M * Kx:].view(M, 8)
+    ref_w = dY.float().t() @ X.float()
+    ref_b = dY.float().sum(0)
+    assert (dw - ref_w).abs().max().item() <= 2e-3 * ref_w.abs().max().item() + 1e-4
+    assert (db8[:, 0] - ref_b).abs().max().item() <= 2e-3 * ref_b.abs().max().item() + 1e-4
+    assert torch.equal(db8[:, 1:], torch.zeros(M, 7))
+    assert torch.equal(outs[0], outs[1])
+    if splitk:
+        assert int(kw["sk"][2].abs().sum()) == 0
+
+
 @pytest.mark.parametrize("impl", [1, 2, 3, 4, 6])
 @pytest.mark.parametrize("splitk", [2, 3, 5])
 @pytest.mark.parametrize("M,N,K", [(528, 768, 3072), (77, 200, 1024), (400, 192, 640)])

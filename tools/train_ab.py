@@ -60,6 +60,17 @@ def accumulated_grads():
         train._weight_grads, optim.HipAdamW.__init__, optim.HipAdamW.zero_grad = saved
 
 
+@contextlib.contextmanager
+def transposed_copies():
+    """The Linear backward through transposed operand copies (mmt_transpose_bf16) instead of MN-major reads."""
+    from mmt_amd import train
+    train.MN_MAJOR = False
+    try:
+        yield
+    finally:
+        train.MN_MAJOR = True
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
@@ -69,7 +80,8 @@ def main():
     ap.add_argument("--only", default="", help="comma-separated variant names")
     args = ap.parse_args()
     variants = {"hip": HipOps, "aten_groupnorm": AtenGroupNormOps, "aten_layernorm": AtenLayerNormOps,
-                "split_mlp": SplitMlpOps, "accum_grads": (HipOps, accumulated_grads)}
+                "split_mlp": SplitMlpOps, "accum_grads": (HipOps, accumulated_grads),
+                "transposed": (HipOps, transposed_copies)}
     if args.only:
         variants = {k: v for k, v in variants.items() if k in args.only.split(",")}
     for r in range(args.rounds):
