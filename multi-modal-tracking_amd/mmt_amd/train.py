@@ -113,7 +113,11 @@ def _gemm(a, w, M, N, K, bias=None, out_f32=False, act=0, r=None, c2=None, c2_co
 def _bf16_weight(w):
     """The bf16 copy of an fp32 master weight HipAdamW's update wrote (same values), else a fresh cast."""
     sh = getattr(w, "_mmt_bf16", None)
-    return sh[0] if sh is not None and sh[1] == w._version else w.detach().to(torch.bfloat16).contiguous()
+    if sh is None and w._base is not None:  # a reshaped conv weight (patch embed, 1x1 adjust convs)
+        sh = getattr(w._base, "_mmt_bf16", None)
+    if sh is not None and sh[1] == w._version and sh[0].numel() == w.numel():
+        return sh[0].view(w.shape)
+    return w.detach().to(torch.bfloat16).contiguous()
 
 
 def _weight_grads(dy, x, M, N, K):
@@ -724,8 +728,8 @@ class TrainStep:
         groups = param_groups(net, lr)
         if next(net.parameters()).is_cuda:
             from .optim import HipAdamW
-            shadow = [m.weight for n, m in net.named_modules()
-                      if isinstance(m, torch.nn.Linear) and "backbone" in n and m.weight.requires_grad]
+            shadow = [m.weight for m in net.modules()
+                      if isinstance(m, (torch.nn.Linear, torch.nn.Conv2d)) and m.weight.requires_grad]
             self.opt = HipAdamW(groups, lr=lr, weight_decay=weight_decay, shadow=shadow, set_to_none=True)
         else:
             self.opt = torch.optim.AdamW(groups, lr=lr, weight_decay=weight_decay)
