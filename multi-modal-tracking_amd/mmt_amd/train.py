@@ -82,7 +82,7 @@ def _splitk_ws(dev):
 
 
 def _gemm(a, w, M, N, K, bias=None, out_f32=False, act=0, r=None, c2=None, c2_copy=0, c=None, ldc=None, a_t=0,
-          w_t=0, ldw=0, lda=None, splitk=False):
+          w_t=0, ldw=0, lda=None, splitk=False, impl=0):
     """C[M][N] = A[M][K] W[N][K]^T (+ bias), bf16 operands, fp32 accumulation (mmt_gemm); act / r (bf16,
     [M][N]) / c2 / c2_copy as mmt_gemm_params (act 1 GELU, 5 GELU backward against r; c2_copy 2: c2 = the
     pre-activation; 3: the last 8 columns to c2 [M][8]); c / ldc: a preallocated output and its pitch;
@@ -95,7 +95,7 @@ def _gemm(a, w, M, N, K, bias=None, out_f32=False, act=0, r=None, c2=None, c2_co
     p.a[0], p.w[0], p.c[0] = a.data_ptr(), w.data_ptr(), c.data_ptr()
     p.bias[0] = bias.data_ptr() if bias is not None else None
     p.lda, p.ldc = lda or K, ldc or N
-    p.a_t, p.w_t, p.ldw = a_t, w_t, ldw
+    p.a_t, p.w_t, p.ldw, p.impl = a_t, w_t, ldw, impl
     if splitk:
         ws, cnt = _splitk_ws(a.device)
         p.sk_ws, p.sk_ws_floats, p.sk_cnt, p.sk_cnt_n = ws.data_ptr(), ws.numel(), cnt.data_ptr(), cnt.numel()

@@ -54,6 +54,9 @@ def main():
                     round(timed(lambda: train._weight_grads(dy, x, M, N, K), args.reps), 2))
                 outs[mode] = (train._dx(dy, w, M, N, K).float(), *train._weight_grads(dy, x, M, N, K))
         train.MN_MAJOR = True
+        for impl in (1, 8):  # the MN-major dX GEMM on each of its two tile configurations
+            res["mn_major_dx_impl%d_us" % impl] = round(
+                timed(lambda: train._gemm(dy, w, M, K, N, w_t=1, ldw=K, impl=impl), args.reps), 2)
         for i, part in enumerate(("dx", "dw", "db")):
             a, b = outs[True][i], outs[False][i]
             res["rel_diff_" + part] = float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
