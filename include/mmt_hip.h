@@ -156,6 +156,11 @@ typedef struct {
     int32_t a_t;
     int32_t w_t;
     int64_t ldw;
+    /* row_scale != NULL (16-bit LDS-DMA kernels): v *= row_scale[m / row_scale_div] before R is added
+     * (the training step's per-sample stochastic depth on a residual branch, x + keep_b / (1 - p) * f(x)) */
+    const float* row_scale;
+    int32_t row_scale_div;
+    int32_t pad_;
 } mmt_gemm_params;
 
 int mmt_gemm(const mmt_gemm_params* p, int dtype, void* stream);

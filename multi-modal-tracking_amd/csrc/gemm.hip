@@ -343,6 +343,7 @@ int check_gemm(const mmt_gemm_params& p) {
         if (p.N % 8 || p.ldw % EPC || p.ldw < (p.w_t == 2 ? p.N - 8 : p.N)) return MMT_EBADARG;
         if (p.a_t && (p.M % 8 || p.lda < p.M)) return MMT_EBADARG;
     }
+    if (p.row_scale && p.row_scale_div < 1) return MMT_EBADARG;
     if (p.r_mode == 2 && (p.r_p1 < 1 || p.r_p0 % p.r_p1)) return MMT_EBADARG;
     if (p.r_mode == 1 && p.r_p0 < 1) return MMT_EBADARG;
     if (p.c_seg_rows < 0 || (p.c_seg_rows > 0 && (p.conv_h > 0 || p.c_seg_pitch < p.c_seg_rows))) return MMT_EBADARG;
@@ -371,7 +372,7 @@ int launch_gemm(const mmt_gemm_params& p, hipStream_t st) {
     }
     if constexpr (sizeof(T) == 2)
         if (mmt_gemm_glds<T>(p, st, p.impl) == 0) return launch_status();
-    if (p.ln_fold || p.c2_copy || p.act == 5 || p.w_t) return MMT_EBADARG;  // LDS-DMA kernel features only
+    if (p.ln_fold || p.c2_copy || p.act == 5 || p.w_t || p.row_scale) return MMT_EBADARG;  // LDS-DMA kernel features only
     if (p.conv_h > 0) launch_tiles<T, true>(p, st);
     else launch_tiles<T, false>(p, st);
     return launch_status();

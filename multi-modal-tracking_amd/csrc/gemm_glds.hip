@@ -703,6 +703,11 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
                     vb[j] = fmaxf(vb[j], 0.f);
                 }
             }
+            if (p.row_scale) {  // per-sample stochastic depth of a residual branch (wave-uniform test)
+                const float sc = p.row_scale[min(m, M - 1) / p.row_scale_div];
+                va *= sc;
+                vb *= sc;
+            }
             const f32x4 sa = va + ra[i], sb = vb + rb[i];  // + residual
             const bool split_c2 = C2 && !p.c2_copy;           // C = v, C2 = v + R
             const f32x4 oa = split_c2 ? va : sa, ob = split_c2 ? vb : sb;

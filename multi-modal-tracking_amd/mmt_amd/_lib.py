@@ -37,7 +37,7 @@ class GemmParams(ctypes.Structure):
         ("splitk", i32), ("sk_ws", vp), ("sk_ws_floats", i64), ("sk_cnt", vp), ("sk_cnt_n", i64),
         ("c_seg_rows", i64), ("c_seg_pitch", i64),
         ("ln_stats_out", vp * MAX_GROUPS), ("ln_stats_in", vp * MAX_GROUPS),
-        ("a_t", i32), ("w_t", i32), ("ldw", i64),
+        ("a_t", i32), ("w_t", i32), ("ldw", i64), ("row_scale", vp), ("row_scale_div", i32), ("pad_", i32),
     ]
 
 

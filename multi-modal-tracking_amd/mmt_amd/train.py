@@ -82,7 +82,7 @@ def _splitk_ws(dev):
 
 
 def _gemm(a, w, M, N, K, bias=None, out_f32=False, act=0, r=None, c2=None, c2_copy=0, c=None, ldc=None, a_t=0,
-          w_t=0, ldw=0, lda=None, splitk=False, impl=0):
+          w_t=0, ldw=0, lda=None, splitk=False, impl=0, row_scale=None, row_scale_div=1):
     """C[M][N] = A[M][K] W[N][K]^T (+ bias), bf16 operands, fp32 accumulation (mmt_gemm); act / r (bf16,
     [M][N]) / c2 / c2_copy as mmt_gemm_params (act 1 GELU, 5 GELU backward against r; c2_copy 2: c2 = the
     pre-activation; 3: the last 8 columns to c2 [M][8]); c / ldc: a preallocated output and its pitch;
@@ -102,8 +102,10 @@ def _gemm(a, w, M, N, K, bias=None, out_f32=False, act=0, r=None, c2=None, c2_co
     p.a_seg_rows, p.a_segs_a = M, 1
     p.M, p.N, p.K, p.groups, p.c_f32 = M, N, K, 1, 1 if out_f32 else 0
     p.act = act
-    if r is not None:
-        p.r[0], p.ldr, p.r_t = r.data_ptr(), N, 1
+    if r is not None:  # bf16 (act 5's pre-activation) or the fp32 residual stream
+        p.r[0], p.ldr, p.r_t = r.data_ptr(), N, 0 if r.dtype == torch.float32 else 1
+    if row_scale is not None:
+        p.row_scale, p.row_scale_div = row_scale.data_ptr(), row_scale_div
     if c2 is not None:
         p.c2[0], p.c2_copy = c2.data_ptr(), c2_copy
     check(LIB.mmt_gemm(p, MMT_BF16, _stream()), "mmt_gemm")
@@ -200,6 +202,77 @@ class _HipMlp(torch.autograd.Function):
         dx = _dx(dhp, wb1, M, F4, C) if ctx.needs_input_grad[0] else None
         dw1, db1 = _weight_grads(dhp, x, M, F4, C)
         return dx, dw1, db1, dw2, db2
+
+
+def _scaled_bf16(dy, keep, rows_per):
+    """keep[m // rows_per] * dy in bf16, one pass (the residual branch's gradient under stochastic depth)."""
+    if keep is None:
+        return dy.to(torch.bfloat16).contiguous()
+    out = torch.empty(dy.shape, device=dy.device, dtype=torch.bfloat16)
+    torch.mul(dy.view(keep.shape[0], rows_per, -1), keep.view(-1, 1, 1), out=out.view(keep.shape[0], rows_per, -1))
+    return out
+
+
+class _HipLinearResidual(torch.autograd.Function):
+    """x + keep * (a W^T + b) in one GEMM (fp32 residual stream x [M][N] as the epilogue's R, keep [B] the
+    per-sample stochastic-depth scale over blocks of M / B rows as its row_scale, or None): the block's
+    proj + DropPath + residual add (mixformer.py:136-137) without the addcmul pass; the backward hands
+    the stream gradient through and scales + casts the branch gradient in one pass."""
+
+    @staticmethod
+    def forward(ctx, x, a, w, b, keep):
+        M, K = a.shape
+        N = w.shape[0]
+        a = a.contiguous()
+        wb = _bf16_weight(w)
+        rows = M // keep.shape[0] if keep is not None else 1
+        y = _gemm(a, wb, M, N, K, bias=b.detach(), out_f32=True, r=x.detach().reshape(M, N),
+                  row_scale=keep, row_scale_div=rows)
+        ctx.save_for_backward(a, wb, keep)
+        ctx.rows = rows
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dout):
+        a, wb, keep = ctx.saved_tensors
+        M, K = a.shape
+        N = wb.shape[0]
+        dy = _scaled_bf16(dout.reshape(M, N), keep, ctx.rows)
+        da = _dx(dy, wb, M, N, K) if ctx.needs_input_grad[1] else None
+        dw, db = _weight_grads(dy, a, M, N, K)
+        return dout, da, dw, db, None
+
+
+class _HipMlpResidual(torch.autograd.Function):
+    """x + keep * fc2(GELU(fc1(xn))) (the block's MLP branch + DropPath + residual, mixformer.py:138-139):
+    _HipMlp with the residual add and the per-sample scale in fc2's epilogue."""
+
+    @staticmethod
+    def forward(ctx, x, xn, w1, b1, w2, b2, keep):
+        M, C = xn.shape
+        F4 = w1.shape[0]
+        xn = xn.contiguous()
+        wb1, wb2 = _bf16_weight(w1), _bf16_weight(w2)
+        rows = M // keep.shape[0] if keep is not None else 1
+        hp = torch.empty(M, F4, device=xn.device, dtype=torch.bfloat16)
+        h = _gemm(xn, wb1, M, F4, C, bias=b1.detach(), act=1, c2=hp, c2_copy=2)
+        y = _gemm(h, wb2, M, C, F4, bias=b2.detach(), out_f32=True, r=x.detach().reshape(M, C), row_scale=keep,
+                  row_scale_div=rows)
+        ctx.save_for_backward(xn, wb1, wb2, h, hp, keep)
+        ctx.rows = rows
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dout):
+        xn, wb1, wb2, h, hp, keep = ctx.saved_tensors
+        M, C = xn.shape
+        F4 = wb1.shape[0]
+        dy = _scaled_bf16(dout.reshape(M, C), keep, ctx.rows)
+        dhp = _dx(dy, wb2, M, C, F4, act=5, r=hp)
+        dw2, db2 = _weight_grads(dy, h, M, C, F4)
+        dxn = _dx(dhp, wb1, M, F4, C) if ctx.needs_input_grad[1] else None
+        dw1, db1 = _weight_grads(dhp, xn, M, F4, C)
+        return dout, dxn, dw1, db1, dw2, db2, None
 
 
 class _HipMamAttention(torch.autograd.Function):
@@ -359,6 +432,16 @@ class HipOps:
         return _HipMlp.apply(x, w1, b1, w2, b2)
 
     @staticmethod
+    def linear_residual(x, a, weight, bias, keep):
+        """x + keep * Linear(a) (fp32 x, bf16 a, keep [B] per-sample scale or None) (_HipLinearResidual)."""
+        return _HipLinearResidual.apply(x, a, weight, bias, keep)
+
+    @staticmethod
+    def mlp_residual(x, xn, w1, b1, w2, b2, keep):
+        """x + keep * Mlp(xn) (_HipMlpResidual)."""
+        return _HipMlpResidual.apply(x, xn, w1, b1, w2, b2, keep)
+
+    @staticmethod
     def mam_attention(qkv, n_t, heads):
         return _HipMamAttention.apply(qkv, n_t, heads)
 
@@ -412,6 +495,30 @@ def _residual(x, y, p, training):
     return torch.addcmul(x, y, keep.div_(1.0 - p))
 
 
+def _keep(x, p, training):
+    """Per-sample DropPath scale (survivors 1 / (1 - p), others 0) for the fused residual GEMMs, or None."""
+    if not training or p <= 0.0:
+        return None
+    return torch.empty(x.shape[0], device=x.device, dtype=torch.float32).bernoulli_(1.0 - p).div_(1.0 - p)
+
+
+def _branch_residual(ops, x, a, lin, p, training):
+    """x + DropPath(lin(a)) for the block's attention projection: one fused GEMM with HipOps."""
+    fn = getattr(ops, "linear_residual", None)
+    if fn is not None:
+        return fn(x, a, lin.weight, lin.bias, _keep(x, p, training))
+    B, ntok, C = x.shape
+    return _residual(x, ops.linear(a, lin.weight, lin.bias, out_f32=True).view(B, ntok, C), p, training)
+
+
+def _mlp_residual(ops, x, xn, mlp, p, training):
+    """x + DropPath(Mlp(xn)): one fused autograd node with HipOps."""
+    fn = getattr(ops, "mlp_residual", None)
+    if fn is not None:
+        return fn(x, xn, mlp.fc1.weight, mlp.fc1.bias, mlp.fc2.weight, mlp.fc2.bias, _keep(x, p, training))
+    return _residual(x, _mlp(ops, xn, mlp).view(x.shape), p, training)
+
+
 def _patches(x, p=16):
     """(B, C, H, W) -> (B, (H/p)(W/p), C p p): F.unfold(x, p, stride=p).transpose(1, 2) for non-overlapping
     patches (channel-major, then kernel row, kernel column; patches row-major), as one copy (aten's
@@ -441,10 +548,9 @@ def backbone_forward(bb, t, o, s, ops, drop_path_rate=DROP_PATH_RATE):
         xn = _layer_norm(ops, x, blk.norm1)
         qkv = ops.linear(xn.view(B * ntok, C), blk.attn.qkv.weight, blk.attn.qkv.bias).view(B, ntok, 3 * C)
         a = ops.mam_attention(qkv, n_t, H).view(B * ntok, C)
-        x = _residual(x, ops.linear(a, blk.attn.proj.weight, blk.attn.proj.bias, out_f32=True).view(B, ntok, C), dp,
-                      bb.training)
+        x = _branch_residual(ops, x, a, blk.attn.proj, dp, bb.training)
         xn = _layer_norm(ops, x, blk.norm2)
-        x = _residual(x, _mlp(ops, xn.view(B * ntok, C), blk.mlp).view(B, ntok, C), dp, bb.training)
+        x = _mlp_residual(ops, x, xn.view(B * ntok, C), blk.mlp, dp, bb.training)
     xs = x[:, n_t:]
     return xs.transpose(1, 2).reshape(B, C, gs, gs)
 
@@ -476,10 +582,9 @@ def backbone_forward_stacked(bb, t, o, s, ops, asym=False, drop_path_rate=DROP_P
         xn = ln2(x, blk.norm1_v, blk.norm1_i)
         qkv = ops.linear(xn.view(B2 * ntok, C), blk.attn.qkv.weight, blk.attn.qkv.bias).view(B2, ntok, 3 * C)
         a = ops.mam_attention_asym(qkv, Bh, n_t, H) if asym else ops.mam_attention(qkv, n_t, H)
-        x = _residual(x, ops.linear(a.reshape(B2 * ntok, C), blk.attn.proj.weight, blk.attn.proj.bias, out_f32=True)
-                      .view(B2, ntok, C), dp, bb.training)
+        x = _branch_residual(ops, x, a.reshape(B2 * ntok, C), blk.attn.proj, dp, bb.training)
         xn = ln2(x, blk.norm2_v, blk.norm2_i)
-        x = _residual(x, _mlp(ops, xn.view(B2 * ntok, C), blk.mlp).view(B2, ntok, C), dp, bb.training)
+        x = _mlp_residual(ops, x, xn.view(B2 * ntok, C), blk.mlp, dp, bb.training)
     return x[:, n_t:].transpose(1, 2).reshape(B2, C, gs, gs), x[:, :gt * gt]
 
 

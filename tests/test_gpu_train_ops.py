@@ -489,6 +489,49 @@ def test_hip_mlp_autograd():
         assert err <= 2e-2, (name, err)
 
 
+@pytest.mark.parametrize("drop", [False, True])
+def test_hip_fused_residual_branches(drop):
+    """HipOps.linear_residual / mlp_residual (_HipLinearResidual / _HipMlpResidual: the block's proj and
+    MLP with DropPath and the residual add in the GEMM epilogue, row_scale = keep[m // ntok]) against
+    x + keep * branch(a) in torch fp32 autograd on the bf16 operands: outputs and every gradient, with
+    keep = (1 / (1 - p), 0, 1 / (1 - p), 1 / (1 - p)) (a dropped sample) or None."""
+    from mmt_amd.train import HipOps
+    g = torch.Generator().manual_seed(23)
+    B, ntok, C, F4 = 4, 264, 768, 3072
+    M = B * ntok
+    x = torch.randn(B, ntok, C, generator=g)
+    a = torch.randn(M, C, generator=g).bfloat16()
+    w = torch.randn(C, C, generator=g) / math.sqrt(C)
+    b = torch.randn(C, generator=g) * 0.1
+    w1 = torch.randn(F4, C, generator=g) / math.sqrt(C)
+    b1 = torch.randn(F4, generator=g) * 0.1
+    w2 = torch.randn(C, F4, generator=g) / math.sqrt(F4)
+    b2 = torch.randn(C, generator=g) * 0.1
+    dy = torch.randn(B, ntok, C, generator=g)
+    keep = torch.tensor([1 / 0.9, 0.0, 1 / 0.9, 1 / 0.9]) if drop else None
+    F = torch.nn.functional
+    cases = (("linear", HipOps.linear_residual, [w, b], lambda t, ps: F.linear(t, ps[0], ps[1])),
+             ("mlp", HipOps.mlp_residual, [w1, b1, w2, b2],
+              lambda t, ps: F.linear(F.gelu(F.linear(t, ps[0], ps[1])), ps[2], ps[3])))
+    for name, fn, params, branch in cases:
+        xd = x.cuda().requires_grad_(True)
+        ad = a.cuda().requires_grad_(True)
+        ps = [t.cuda().requires_grad_(True) for t in params]
+        y = fn(xd, ad, *ps, keep.cuda() if drop else None)
+        y.backward(dy.cuda())
+        got = [y.detach().cpu(), xd.grad.cpu(), ad.grad.float().cpu()] + [p.grad.cpu() for p in ps]
+        xr = x.clone().requires_grad_(True)
+        ar = a.float().requires_grad_(True)
+        rs = [(t.bfloat16().float() if t.dim() == 2 else t.clone()).requires_grad_(True) for t in params]
+        br = branch(ar, rs).view(B, ntok, C)
+        yr = xr + (br * keep.view(B, 1, 1) if drop else br)
+        yr.backward(dy)
+        ref = [yr.detach(), xr.grad, ar.grad] + [r.grad for r in rs]
+        for what, u, v in zip(("y", "dx", "da") + tuple("d%d" % i for i in range(len(ps))), got, ref):
+            err = (u - v).abs().max().item() / max(1.0, v.abs().max().item())
+            assert err <= 2e-2, (name, what, err)
+
+
 def test_hip_layernorm_alternating_groups_fp32():
     """The fusion encoder's LN-specific norms in training (deformable_encoder_lnspecific.py:94-148):
     norm_v on the first half of every sequence's 2hw tokens and norm_i on the second, fp32 in / out

@@ -29,6 +29,12 @@ class AtenGroupNormOps(HipOps):
     group_norm = None
 
 
+class UnfusedResidualOps(HipOps):
+    """HipOps with the blocks' residual branches as GEMM + addcmul (DropPath) + autograd's adds."""
+    linear_residual = None
+    mlp_residual = None
+
+
 class SplitMlpOps(HipOps):
     """HipOps with each MLP as fc1 / aten GELU / fc2 (three autograd nodes) instead of _HipMlp."""
     mlp = None
@@ -80,7 +86,7 @@ def main():
     ap.add_argument("--only", default="", help="comma-separated variant names")
     args = ap.parse_args()
     variants = {"hip": HipOps, "aten_groupnorm": AtenGroupNormOps, "aten_layernorm": AtenLayerNormOps,
-                "split_mlp": SplitMlpOps, "accum_grads": (HipOps, accumulated_grads),
+                "split_mlp": SplitMlpOps, "unfused_residual": UnfusedResidualOps, "accum_grads": (HipOps, accumulated_grads),
                 "transposed": (HipOps, transposed_copies)}
     if args.only:
         variants = {k: v for k, v in variants.items() if k in args.only.split(",")}
