@@ -156,7 +156,8 @@ typedef struct {
     int32_t a_t;
     int32_t w_t;
     int64_t ldw;
-    /* row_scale != NULL (16-bit LDS-DMA kernels): v *= row_scale[m / row_scale_div] before R is added
+    /* row_scale != NULL (16-bit LDS-DMA kernels, impl 0 / 8 on the 128x128 two-per-CU tile, no conv / LayerNorm fold /
+     * MN-major operands / split-K): v *= row_scale[m / row_scale_div] before R is added
      * (the training step's per-sample stochastic depth on a residual branch, x + keep_b / (1 - p) * f(x)) */
     const float* row_scale;
     int32_t row_scale_div;

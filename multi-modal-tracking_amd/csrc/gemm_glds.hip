@@ -103,7 +103,7 @@ MMT_DEV int gemm_trsw(int k) { return 2 * ((k & 3) | (((k >> 3) & 1) << 2)); }
 // (mmt_gemm_params.ln_fold): the row statistics of A are accumulated from the A fragments the
 // waves already hold for the MFMAs (wave column wc sums fragment rows mt = wc, wc + WGN, ...), so
 // the normalised operand never exists in memory and the LayerNorm launch disappears.
-template <typename T, int BM, int BN, int WGM, int WGN, int KS, int ST, bool CONV, int LNM, int OCC = 1>
+template <typename T, int BM, int BN, int WGM, int WGN, int KS, int ST, bool CONV, int LNM, int OCC = 1, bool RS = false>
 MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int tile, const int slice, const int nsk,
                             const int ntiles) {
     constexpr int NW = WGM * WGN, TPG = 64 * NW;  // waves / threads per k-group
@@ -703,7 +703,8 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
                     vb[j] = fmaxf(vb[j], 0.f);
                 }
             }
-            if (p.row_scale) {  // per-sample stochastic depth of a residual branch (wave-uniform test)
+            if constexpr (RS) {  // per-sample stochastic depth of a residual branch (row_scale; training only:
+                                 // a run-time test here cost the inference frame ~1 %)
                 const float sc = p.row_scale[min(m, M - 1) / p.row_scale_div];
                 va *= sc;
                 vb *= sc;
@@ -789,7 +790,7 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
 // The same tile at two workgroups per CU (impl 8: 128x128, 8 waves, 2-slot ring = 64 KiB of LDS, <= 128
 // VGPRs): one workgroup's prologue / epilogue runs beside the other's K loop on the CU, which the one-
 // workgroup-per-CU tiles cannot overlap (large-M grids of short K: the training step's K = 768 GEMMs).
-template <typename T, int BM, int BN, int WGM, int WGN, int KS, int ST>
+template <typename T, int BM, int BN, int WGM, int WGN, int KS, int ST, bool RS = false>
 __global__ __launch_bounds__(64 * WGM * WGN * KS)
     __attribute__((amdgpu_waves_per_eu(WGM * WGN * KS / 2, WGM * WGN * KS / 2))) void gemm_glds_kernel_occ2(
         const mmt_gemm_params p) {
@@ -798,7 +799,7 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
     const int per_g = gridDim.x * nsk;
     const int g = lin / per_g, rem_t = lin - g * per_g;
     const int tile = rem_t / nsk, slice = rem_t - tile * nsk;
-    gemm_glds_tile<T, BM, BN, WGM, WGN, KS, ST, false, 0, 2>(p, g, tile, slice, nsk, gridDim.x);
+    gemm_glds_tile<T, BM, BN, WGM, WGN, KS, ST, false, 0, 2, RS>(p, g, tile, slice, nsk, gridDim.x);
 }
 
 // impl 8's tile with MN-major operands (LNM 3: W; 4: A and W)
@@ -920,6 +921,12 @@ int mmt_gemm_glds(const mmt_gemm_params& p, hipStream_t st, int force) {
         return (float)((wg + 255) / 256) * (c.fixed_us + (float)((steps + c.ks - 1) / c.ks) * c.step_us) + red;
     };
     int cfg = force, nsk = 1;
+    if (p.row_scale) {  // the training step's residual branches: impl 8's tile with the row-scale epilogue
+        if ((force != 0 && force != 8) || p.ln_fold || p.conv_h > 0 || p.a_t || p.w_t) return 1;
+        hipLaunchKernelGGL((gemm_glds_kernel_occ2<T, 128, 128, 2, 4, 1, 2, true>),
+                           dim3((unsigned)tiles_of(p, 128, 128), 1, p.groups), dim3(512), 0, st, p);
+        return 0;
+    }
     if (p.a_t || p.w_t) {  // MN-major operands: the 128x128 tiles (impl 1, or impl 8 on big unsplit grids)
         if (force != 0 && force != 1 && force != 8) return 1;
         const bool big = tiles_of(p, 128, 128) * p.groups > 256;
