@@ -681,7 +681,7 @@ def main():
         del graphs, plans, pool
         torch.cuda.empty_cache()
         try:
-            train_res = train_bench(world, rank, 16, 5, 2)
+            train_res = train_bench(world, rank, 16, 10, 3)  # 10 timed steps: 5 read one-off stalls
         except Exception as e:  # noqa: BLE001
             train_res = {"error": "%s: %s" % (type(e).__name__, e)}
     else:
