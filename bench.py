@@ -414,7 +414,7 @@ def train_bench(world, rank, B, steps, warmup, device="cuda", ops=None, search=3
             "batch_per_gpu": B, "steps": steps, "warmup": warmup,
             "parallelism": "ddp%d (RCCL gradient all-reduce)" % world if world > 1 else "single",
             "roofline": {"kernel": "train_step (whole step)", "bound": "mfma", "achieved": round(ach, 2),
-                         "peak": PEAK["bf16"], "unit": "TFLOP/s", "frac": round(ach / PEAK["bf16"], 4),
+                         "peak": PEAK["bf16"], "unit": "TFLOP/s", "frac": float("%.4g" % (ach / PEAK["bf16"])),
                          "flops_per_sample": TRAIN_FLOP_PER_SAMPLE, "traffic": None},
             "last_loss": round(float(last["stats"]["loss"]), 5),
             "opt_table_writes": getattr(step_fn.opt, "table_writes", None)}

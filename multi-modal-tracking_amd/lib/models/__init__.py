@@ -1,1 +1,8 @@
-"""lib.models: the RGB-T hot-path family (mixformer_vit_rgbt) and the RGB-only MixViT (mixformer_vit, config 1)."""
+"""lib.models overlay: the RGB-T hot-path family (mixformer_vit_rgbt) and the RGB-only MixViT (mixformer_vit, config 1)."""
+from pkgutil import extend_path
+
+# Overlay, not replacement: the same package directories found later on sys.path (the reference
+# checkout's lib/, e.g. appended by tracking/test.py:10-12) join this package's search path, so the
+# modules this tree does not provide (lib.config, lib.train, lib.test.evaluation, lib.utils, ...)
+# still import from there, while the ones it does provide come from here.
+__path__ = extend_path(__path__, __name__)

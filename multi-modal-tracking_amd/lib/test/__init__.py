@@ -1,1 +1,8 @@
-"""Drop-in mirror of the reference's lib/test (tracker entry points of the RGB-T models)."""
+"""Overlay of the reference's lib/test (tracker entry points of the RGB-T models)."""
+from pkgutil import extend_path
+
+# Overlay, not replacement: the same package directories found later on sys.path (the reference
+# checkout's lib/, e.g. appended by tracking/test.py:10-12) join this package's search path, so the
+# modules this tree does not provide (lib.config, lib.train, lib.test.evaluation, lib.utils, ...)
+# still import from there, while the ones it does provide come from here.
+__path__ = extend_path(__path__, __name__)

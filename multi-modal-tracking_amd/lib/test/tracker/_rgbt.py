@@ -13,7 +13,10 @@ import torch
 
 from mmt_amd.tracking import RGBTTrackerCore
 
-from .basetracker import BaseTracker
+try:  # the reference's BaseTracker (with its visdom helpers) when its lib/ is overlaid
+    from lib.test.tracker.basetracker import BaseTracker
+except ModuleNotFoundError:  # standalone: the same interface, lib/test/tracker/basetracker.py:4-22
+    from ._basetracker import BaseTracker
 
 
 def _update_intervals(cfg, dataset_name):
