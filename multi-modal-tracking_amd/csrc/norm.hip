@@ -277,10 +277,12 @@ __global__ __launch_bounds__(64) void layernorm_bwd_reduce_kernel(const float* _
 
 // GroupNorm backward (training step): one 512-thread workgroup per (instance, group) as the forward, the
 // group's x and dy in registers.  dx = rstd * (g - mean(g) - xhat * mean(g * xhat)) with g = dy * gamma_c;
-// the per-channel (sum dy * xhat, sum dy) of the workgroup go through LDS as [P][cg] products and are
-// summed over P in position order by one thread per channel, into part[instance][2][Ctot]; a second
-// launch sums the instances in order (deterministic, no atomics).
-constexpr int GNB_LDS = 2 * 9600;  // floats: P * cg products of each kind (P 400 x cg 24)
+// the per-channel (sum dy * xhat, sum dy) of the workgroup go through LDS as [PC][cg] products, in chunks of
+// PC = GNB_LDS / (2 cg) positions, and are summed over P in position order by one thread per channel (the
+// accumulator carried across chunks), into part[instance][2][Ctot]; a second launch sums the instances in
+// order (deterministic, no atomics).  ViT-B at 320 (P 400, cg 24) is one chunk; ViT-L at 384 (P 576, cg 32)
+// two.
+constexpr int GNB_LDS = 2 * 9600;  // floats: PC * cg products of each kind (one chunk covers P 400 x cg 24)
 
 __global__ __launch_bounds__(GN_THREADS) void groupnorm_bwd_kernel(const float* __restrict__ in,
                                                                    const float* __restrict__ dy, const float* gamma,
@@ -324,6 +326,8 @@ __global__ __launch_bounds__(GN_THREADS) void groupnorm_bwd_kernel(const float* 
     }
     const float rstd = rsqrtf(block_sum<GN_THREADS>(sq, red) / n + eps);
     float sg = 0.f, sgx = 0.f;
+    const int PC = GNB_LDS / (2 * cg);  // positions per LDS chunk
+    float4 dd[GN_VMAX];                 // dy kept for the later chunks' products
 #pragma unroll
     for (int i = 0; i < GN_VMAX; ++i) {
         const int it = threadIdx.x + GN_THREADS * i;
@@ -331,10 +335,13 @@ __global__ __launch_bounds__(GN_THREADS) void groupnorm_bwd_kernel(const float* 
             const int c = grp * cg + c4s[i];
             const float4 ga = *(const float4*)(gamma + c);
             v[i].x *= rstd; v[i].y *= rstd; v[i].z *= rstd; v[i].w *= rstd;  // xhat
-            float* pp = prod + pix[i] * cg + c4s[i];
-            pp[0] = d[i].x * v[i].x; pp[1] = d[i].y * v[i].y; pp[2] = d[i].z * v[i].z; pp[3] = d[i].w * v[i].w;
-            float* pb = prod + P * cg + pix[i] * cg + c4s[i];
-            pb[0] = d[i].x; pb[1] = d[i].y; pb[2] = d[i].z; pb[3] = d[i].w;
+            if (pix[i] < PC) {  // first chunk's products now; later chunks after the dx pass
+                float* pp = prod + pix[i] * cg + c4s[i];
+                pp[0] = d[i].x * v[i].x; pp[1] = d[i].y * v[i].y; pp[2] = d[i].z * v[i].z; pp[3] = d[i].w * v[i].w;
+                float* pb = prod + PC * cg + pix[i] * cg + c4s[i];
+                pb[0] = d[i].x; pb[1] = d[i].y; pb[2] = d[i].z; pb[3] = d[i].w;
+            }
+            dd[i] = d[i];
             d[i] = make_float4(d[i].x * ga.x, d[i].y * ga.y, d[i].z * ga.z, d[i].w * ga.w);  // g
             sg += d[i].x + d[i].y + d[i].z + d[i].w;
             sgx += d[i].x * v[i].x + d[i].y * v[i].y + d[i].z * v[i].z + d[i].w * v[i].w;
@@ -354,13 +361,33 @@ __global__ __launch_bounds__(GN_THREADS) void groupnorm_bwd_kernel(const float* 
             *(float4*)(dx + base + (int64_t)pix[i] * Ctot + c4s[i]) = o;
         }
     }
-    if ((int)threadIdx.x < 2 * cg) {  // thread -> (kind, channel): sum over positions in order
-        const int kind = (int)threadIdx.x / cg, c = (int)threadIdx.x % cg;
-        const float* col = prod + kind * P * cg + c;
-        float acc = 0.f;
-        for (int pp = 0; pp < P; ++pp) acc += col[pp * cg];
-        part[((int64_t)inst * 2 + kind) * Ctot + grp * cg + c] = acc;
+    // thread -> (kind, channel): sum over positions in order, chunk by chunk
+    const int kind = (int)threadIdx.x / cg, ch = (int)threadIdx.x % cg;
+    float acc = 0.f;
+    for (int p0 = 0; p0 < P; p0 += PC) {
+        if (p0) {  // refill the LDS image with this chunk's products (the first chunk was written above)
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < GN_VMAX; ++i) {
+                const int it = threadIdx.x + GN_THREADS * i;
+                const int r = pix[i] - p0;
+                if (it < items && r >= 0 && r < PC) {
+                    float* pp = prod + r * cg + c4s[i];
+                    pp[0] = dd[i].x * v[i].x; pp[1] = dd[i].y * v[i].y; pp[2] = dd[i].z * v[i].z;
+                    pp[3] = dd[i].w * v[i].w;
+                    float* pb = prod + PC * cg + r * cg + c4s[i];
+                    pb[0] = dd[i].x; pb[1] = dd[i].y; pb[2] = dd[i].z; pb[3] = dd[i].w;
+                }
+            }
+            __syncthreads();
+        }
+        if ((int)threadIdx.x < 2 * cg) {
+            const float* col = prod + kind * PC * cg + ch;
+            const int np = min(PC, P - p0);
+            for (int pp = 0; pp < np; ++pp) acc += col[pp * cg];
+        }
     }
+    if ((int)threadIdx.x < 2 * cg) part[((int64_t)inst * 2 + kind) * Ctot + grp * cg + ch] = acc;
 }
 
 // dgb[j][c] (+)= sum over instances (in order) of part[inst][j][c]
@@ -512,7 +539,7 @@ extern "C" int mmt_groupnorm_bwd(const float* x, const float* dy, const float* g
         return MMT_EBADARG;
     const int cg = Ctot / groups;
     if (cg % 4 || 2 * cg > GN_THREADS || (int64_t)P * (cg / 4) > (int64_t)GN_THREADS * GN_VMAX ||
-        2 * (int64_t)P * cg > GNB_LDS || ws_floats < (int64_t)n_inst * 2 * Ctot)
+        ws_floats < (int64_t)n_inst * 2 * Ctot)
         return MMT_EBADARG;
     if (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)gamma | (uintptr_t)dx) & 15) return MMT_EBADARG;
     hipStream_t st = (hipStream_t)stream;

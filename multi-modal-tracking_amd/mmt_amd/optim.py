@@ -25,24 +25,31 @@ CHUNK_DTYPE = np.dtype([("tensor", "<i4"), ("pad_", "<i4"), ("offset", "<i8")]) 
 MAX_GROUPS = 8
 
 
-class HipAdamW:
+class HipAdamW(torch.optim.Optimizer):
+    """A torch.optim.Optimizer: `param_groups` are the live group dicts (the update reads each group's
+    "lr" / "weight_decay" at every step, so the reference trainer's LR schedulers attach to it), and
+    state_dict / load_state_dict carry exp_avg / exp_avg_sq and the step per parameter, as
+    torch.optim.AdamW's do.  The bias corrections come from ONE device step counter (shared by every
+    parameter, advanced once per step()); load_state_dict therefore requires one step value for all
+    parameters (a state_dict written by torch.optim.AdamW over a run where every parameter had a
+    gradient at every step has that)."""
+
     def __init__(self, param_groups, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, shadow=(),
                  set_to_none=False):
         from ._lib import LIB
         self.lib = LIB
         self.set_to_none = set_to_none
-        self.groups = []
+        groups = []
         for g in param_groups:
             g = dict(g)
             g["params"] = [p for p in g["params"] if p.requires_grad]
-            g.setdefault("lr", lr)
-            g.setdefault("weight_decay", weight_decay)
-            self.groups.append(g)
-        if len(self.groups) > MAX_GROUPS:
+            groups.append(g)
+        if len(groups) > MAX_GROUPS:
             raise ValueError("at most %d parameter groups" % MAX_GROUPS)
+        super().__init__(groups, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        self.groups = self.param_groups  # the live dicts
         self.betas, self.eps = betas, eps
         self.step_count = 0
-        self.state = {}
         self.chunk = int(LIB.mmt_adamw_chunk_elems())
         shadow_ids = {id(p) for p in shadow}
         self._shadow = {}
@@ -50,7 +57,7 @@ class HipAdamW:
             for p in g["params"]:
                 if not (p.is_cuda and p.dtype == torch.float32 and p.is_contiguous()):
                     raise ValueError("HipAdamW takes contiguous fp32 device parameters")
-                self.state[p] = (torch.zeros_like(p), torch.zeros_like(p))
+                self.state[p] = {"exp_avg": torch.zeros_like(p), "exp_avg_sq": torch.zeros_like(p)}
                 if id(p) in shadow_ids:
                     sh = p.detach().to(torch.bfloat16)
                     self._shadow[p] = sh
@@ -58,6 +65,32 @@ class HipAdamW:
         self._key = None
         self.last_norm = None
         self.table_writes = 0
+
+    def _device_state(self, dev):
+        if not hasattr(self, "_state"):
+            self._state = torch.zeros(8, device=dev)  # norm, clip factor, bias corrections, step (int32)
+        return self._state
+
+    def state_dict(self):
+        """torch.optim.AdamW's layout; every parameter's "step" is the device step counter."""
+        step = float(self._state.view(torch.int32)[4].item()) if hasattr(self, "_state") else 0.0
+        for p, st in self.state.items():
+            st["step"] = torch.tensor(step)
+        return super().state_dict()
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        steps = {float(st["step"]) for st in self.state.values() if "step" in st}
+        if len(steps) > 1:
+            raise ValueError("HipAdamW keeps one step counter for all parameters; the state_dict has %d "
+                             "different per-parameter steps" % len(steps))
+        dev = next(p for g in self.groups for p in g["params"]).device
+        for p, st in self.state.items():  # moments on the parameter's device, contiguous fp32
+            for k in ("exp_avg", "exp_avg_sq"):
+                st[k] = st[k].to(device=p.device, dtype=torch.float32).contiguous()
+        self._device_state(dev).view(torch.int32)[4] = int(steps.pop()) if steps else 0
+        self.step_count = int(self._state.view(torch.int32)[4].item())
+        self._key = None  # the moment tensors are new: rebuild the device tables at the next step
 
     def zero_grad(self, set_to_none=False):
         """set_to_none: drop every gradient.  Else the update pass has zeroed the gradients it consumed
@@ -87,7 +120,7 @@ class HipAdamW:
             t = np.zeros(len(params), TENSOR_DTYPE)
             chunks = []
             for i, (gi, p) in enumerate(params):
-                m, v = self.state[p]
+                m, v = self.state[p]["exp_avg"], self.state[p]["exp_avg_sq"]
                 sh = self._shadow.get(p)
                 t[i] = (p.data_ptr(), 0, m.data_ptr(), v.data_ptr(), sh.data_ptr() if sh is not None else 0,
                         p.numel(), gi, 0)
@@ -100,16 +133,17 @@ class HipAdamW:
         # through pinned memory, asynchronously: a pageable copy would hold the host until the stream drains
         self._tens = torch.from_numpy(self._tab.view(np.uint8).copy()).pin_memory().to(dev, non_blocking=True)
         self.table_writes += 1
-        if not hasattr(self, "_state"):
-            self._state = torch.zeros(8, device=dev)  # norm, clip factor, bias corrections, step (int32)
+        self._device_state(dev)
         self._key = (pkey, gkey)
 
     @torch.no_grad()
     def step(self, max_norm=0.0):
         """clip_grad_norm_(max_norm) (skipped when max_norm <= 0) + one AdamW step: three launches with
-        no host synchronisation and no host-side step state (capturable in a hipGraph once the
-        tables exist, i.e. after the first eager step).  The total gradient norm before clipping is
-        `last_norm` (a device scalar)."""
+        no host synchronisation and no host-side step state.  Capturable in a hipGraph after one eager
+        step only when the gradient addresses stay fixed (set_to_none=False, gradients accumulated in
+        place); with set_to_none=True each step's fresh gradients rewrite the pointer table, which a
+        capture refuses (RuntimeError).  The total gradient norm before clipping is `last_norm` (a device
+        scalar) when max_norm > 0, else None (the norm pass is skipped)."""
         from ._lib import check
         params = [(gi, p) for gi, g in enumerate(self.groups) for p in g["params"] if p.grad is not None]
         if not params:
@@ -125,6 +159,6 @@ class HipAdamW:
                                       float(self.betas[0]), float(self.betas[1]), float(self.eps), float(max_norm),
                                       0 if self.set_to_none else 1,
                                       torch.cuda.current_stream().cuda_stream), "mmt_adamw_step")
-        self.last_norm = self._state[0]
+        self.last_norm = self._state[0] if max_norm > 0 else None
         for p in self._shadow:
             p._mmt_bf16 = (self._shadow[p], p._version)

@@ -327,8 +327,11 @@ class _HipLayerNorm(torch.autograd.Function):
         code = {torch.bfloat16: MMT_BF16, torch.float32: MMT_F32}[dy.dtype]
         sets = 4 if ctx.two else 2
         nws = (rows + 31) // 32 * 4 * C
-        buf = torch.empty(rows * C + sets * C + nws, device=x2.device, dtype=torch.float32)  # one allocation
-        dx, dgb, ws = buf[:rows * C].view(rows, C), buf[rows * C:(rows + sets) * C].view(sets, C), buf[(rows + sets) * C:]
+        # dgamma / dbeta in their own small tensor: AccumulateGrad keeps them as .grad, and views into the
+        # dx / workspace buffer would hold its rows * C floats alive until the next zero_grad
+        buf = torch.empty(rows * C + nws, device=x2.device, dtype=torch.float32)
+        dx, ws = buf[:rows * C].view(rows, C), buf[rows * C:]
+        dgb = torch.empty(sets, C, device=x2.device, dtype=torch.float32)
         check(LIB.mmt_layernorm_bwd(x2.data_ptr(), dy.data_ptr(), code, g0.data_ptr(),
                                     g1.data_ptr() if ctx.two else None, dx.data_ptr(), dgb.data_ptr(), 0,
                                     ws.data_ptr(), ws.numel(), rows, ctx.rows0 if ctx.two else rows, C, ctx.eps,
@@ -360,8 +363,9 @@ class _HipGroupNorm(torch.autograd.Function):
         x, w = ctx.saved_tensors
         n, P, C = x.shape
         dy = dy.float().contiguous()
-        buf = torch.empty(n * P * C + 2 * C + n * 2 * C, device=x.device, dtype=torch.float32)
-        dx, dgb, ws = buf[:n * P * C].view(n, P, C), buf[n * P * C:n * P * C + 2 * C].view(2, C), buf[n * P * C + 2 * C:]
+        buf = torch.empty(n * P * C + n * 2 * C, device=x.device, dtype=torch.float32)
+        dx, ws = buf[:n * P * C].view(n, P, C), buf[n * P * C:]
+        dgb = torch.empty(2, C, device=x.device, dtype=torch.float32)  # separate from dx (see _HipLayerNorm)
         check(LIB.mmt_groupnorm_bwd(x.data_ptr(), dy.data_ptr(), w.data_ptr(), dx.data_ptr(), dgb.data_ptr(), 0,
                                     ws.data_ptr(), ws.numel(), n, P, C, ctx.groups, ctx.eps, _stream()),
               "mmt_groupnorm_bwd")

@@ -1021,3 +1021,58 @@ def test_conv3x3_c1_vs_torch(dname, h, cin, pad):
         ref = F.relu(F.conv2d(xr[gi].permute(0, 3, 1, 2), wr[gi].t().reshape(1, cin, 3, 3), b[gi:gi + 1], padding=1))
         got = out[gi].cpu().reshape(B, 1, h, h)
         assert (got - ref).abs().max().item() <= 1e-4 * (1 + ref.abs().max().item())
+
+
+def _fixture_sub(x, n=4096):
+    """tests/golden/make_golden.py's `sub`: every step-th element of the flattened output (float64 sums)."""
+    f = x.detach().reshape(-1).double()
+    step = max(1, f.numel() // n)
+    return f[::step][:n].float(), torch.tensor([f.sum().item(), f.abs().sum().item(), f.numel()], dtype=torch.float64)
+
+
+@pytest.mark.parametrize("dname", ["f32", "bf16"])
+@pytest.mark.parametrize("kind", ["mam", "mam_asym"])
+def test_mam_module_matches_reference_fixture(kind, dname):
+    """the whole MAM `Attention` module on the GPU -- qkv Linear (mmt_gemm, bias), the MAM
+    kernel the dtype's default picks (mmt_mam_attention), proj Linear (mmt_gemm, bias) -- against the
+    outputs the reference's OWN modules produced (tests/golden/op_attention.npz, make_golden.py
+    attention_fixture: mixformer.py:52-78 `Attention` and asymmetric_shared.py:55-104 `Attention`, B = 1,
+    528 tokens of N(0,1), seed-5 inputs, synthetic weights).  Bars: fp32 1e-4, bf16 1e-2, relative to the
+    output's largest magnitude (and the float64 sum of |y| within the same fraction)."""
+    from mmt_amd import synthetic
+    dt = DT[dname]
+    L = _lib()
+    z = np.load(GOLDEN + "/op_attention.npz")
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(1, 528, 768, generator=g)
+    xi = torch.randn(1, 528, 768, generator=g)
+    shapes = [("attn.qkv.weight", [2304, 768]), ("attn.qkv.bias", [2304]), ("attn.proj.weight", [768, 768]),
+              ("attn.proj.bias", [768])]
+    sd = {k: torch.from_numpy(v) for k, v in synthetic.synth_state_dict(shapes).items()}
+    asym = kind == "mam_asym"
+    X = torch.cat([x, xi], 0) if asym else x  # modality-major sequences: s = m * Bm + b
+    S, M = X.shape[0], X.shape[0] * 528
+    Xd = X.reshape(M, 768).to(dt).cuda()
+    Wq, bq = sd["attn.qkv.weight"].to(dt).cuda(), sd["attn.qkv.bias"].cuda()
+    Wp, bp = sd["attn.proj.weight"].to(dt).cuda(), sd["attn.proj.bias"].cuda()
+    qkv = torch.empty(M, 2304, device="cuda", dtype=dt)
+    ao = torch.empty(M, 768, device="cuda", dtype=dt)
+    y = torch.empty(M, 768, device="cuda")
+    _gemm([Xd.data_ptr()], [Wq.data_ptr()], [qkv.data_ptr()], M, 2304, 768, 768, 2304, dt, bias=[bq.data_ptr()])
+    p = L.AttnParams()
+    p.qkv, p.out, p.S, p.Bm, p.ntok, p.n_t, p.C, p.H, p.asym, p.scale = (qkv.data_ptr(), ao.data_ptr(), S, 1, 528, 128,
+                                                                       768, 12, int(asym), 0.125)
+    L.check(L.LIB.mmt_mam_attention(p, _code(dt), torch.cuda.current_stream().cuda_stream), "attn")
+    _gemm([ao.data_ptr()], [Wp.data_ptr()], [y.data_ptr()], M, 768, 768, 768, 768, dt, bias=[bp.data_ptr()], c_f32=1)
+    torch.cuda.synchronize()
+    y = y.cpu().view(S, 528, 768)
+    bar = 1e-4 if dt == torch.float32 else 1e-2
+    outs = [(y[0], "mam")] if not asym else [(y[0], "mam_asym_v"), (y[1], "mam_asym_i")]
+    for out, key in outs:
+        sub, sums = _fixture_sub(out)
+        ref = torch.from_numpy(z[key + "_sub"])
+        scale = ref.abs().max().item()
+        err = (sub - ref).abs().max().item() / scale
+        assert err <= bar, (key, dname, err)
+        assert abs(sums[1].item() - z[key + "_sum"][1]) <= bar * z[key + "_sum"][1], (key, sums, z[key + "_sum"])
+        assert int(sums[2].item()) == int(z[key + "_sum"][2])

@@ -365,11 +365,13 @@ def test_hip_adamw_matches_torch(max_norm, set_to_none):
         torch.cuda.synchronize()
         if max_norm > 0:
             assert abs(opt.last_norm.item() - n_ref.item()) <= 1e-5 * n_ref.item()
+        else:
+            assert opt.last_norm is None
         del keep
         for k, (p, q) in enumerate(zip(ref, hip)):
             assert torch.allclose(q, p, rtol=1e-6, atol=1e-7), (step, (q - p).abs().max().item())
             m_r, v_r = opt_ref.state[p]["exp_avg"], opt_ref.state[p]["exp_avg_sq"]
-            m_h, v_h = opt.state[q]
+            m_h, v_h = opt.state[q]["exp_avg"], opt.state[q]["exp_avg_sq"]
             assert torch.allclose(m_h, m_r, rtol=1e-5, atol=1e-7) and torch.allclose(v_h, v_r, rtol=1e-5, atol=1e-9)
             if set_to_none:
                 assert torch.equal(q.grad, grads[k])
@@ -377,6 +379,49 @@ def test_hip_adamw_matches_torch(max_norm, set_to_none):
                 assert int((q.grad != 0).sum()) == 0
         sh, ver = hip[1]._mmt_bf16
         assert ver == hip[1]._version and torch.equal(sh, hip[1].detach().to(torch.bfloat16))
+
+
+def test_hip_adamw_state_dict_resume_and_scheduler():
+    """HipAdamW is a torch.optim.Optimizer: a state_dict written by torch.optim.AdamW after
+    three steps loads into it (moments + the shared step, so the bias corrections continue from t = 4, not
+    t = 1), its own state_dict round-trips into torch.optim.AdamW, and an LR scheduler attached to it
+    changes the lr the next update uses; two steps after the resume both optimizers agree within 1e-6."""
+    from mmt_amd.optim import HipAdamW
+    g = torch.Generator().manual_seed(5)
+    shapes = [(300,), (64, 65)]
+    init = [torch.randn(s, generator=g) for s in shapes]
+    ref = [torch.nn.Parameter(t.clone().cuda()) for t in init]
+    opt_ref = torch.optim.AdamW([{"params": ref, "lr": 1e-3}], weight_decay=0.01)
+    sched_ref = torch.optim.lr_scheduler.StepLR(opt_ref, step_size=1, gamma=0.5)
+    grads = [[torch.randn(s, generator=g).cuda() for s in shapes] for _ in range(5)]
+    for k in range(3):
+        for p, gr in zip(ref, grads[k]):
+            p.grad = gr.clone()
+        opt_ref.step()
+        sched_ref.step()
+    hip = [torch.nn.Parameter(p.detach().clone()) for p in ref]
+    opt = HipAdamW([{"params": hip, "lr": 1e-3}], weight_decay=0.01, set_to_none=True)
+    opt.load_state_dict(opt_ref.state_dict())
+    sched = torch.optim.lr_scheduler.StepLR(opt, step_size=1, gamma=0.5)
+    sched.load_state_dict(sched_ref.state_dict())
+    assert opt.param_groups[0]["lr"] == opt_ref.param_groups[0]["lr"]
+    for k in range(3, 5):
+        for p, q, gr in zip(ref, hip, grads[k]):
+            p.grad, q.grad = gr.clone(), gr.clone()
+        opt_ref.step()
+        sched_ref.step()
+        opt.step()
+        sched.step()
+        torch.cuda.synchronize()
+        for p, q in zip(ref, hip):
+            assert torch.allclose(q, p, rtol=1e-6, atol=1e-7), (k, (q - p).abs().max().item())
+    sd = opt.state_dict()
+    assert all(float(st["step"]) == 5.0 for st in sd["state"].values())
+    back = torch.optim.AdamW([{"params": [torch.nn.Parameter(p.detach().clone()) for p in hip], "lr": 1e-3}],
+                             weight_decay=0.01)
+    back.load_state_dict(sd)
+    for a, b in zip(back.state.values(), opt_ref.state.values()):
+        assert torch.allclose(a["exp_avg"], b["exp_avg"], rtol=1e-5, atol=1e-8)
 
 
 
@@ -563,7 +608,8 @@ def test_hip_layernorm_alternating_groups_fp32():
         assert (a - r).abs().max().item() <= 2e-4 * max(1.0, r.abs().max().item())
 
 
-@pytest.mark.parametrize("B,P,C,groups", [(4, 400, 512, 32), (2, 400, 768, 32), (3, 64, 256, 8)])
+@pytest.mark.parametrize("B,P,C,groups", [(4, 400, 512, 32), (2, 400, 768, 32), (3, 64, 256, 8),
+                                          (2, 576, 1024, 32), (2, 400, 1024, 32), (1, 1000, 768, 32)])
 def test_hip_groupnorm_autograd(B, P, C, groups):
     """HipOps.group_norm (mmt_groupnorm / mmt_groupnorm_bwd on channels-last token rows) against
     nn.GroupNorm on the NCHW map the reference applies it to (fusion_utils.py:252-279): output, dx,
