@@ -28,21 +28,11 @@
 // store between an LDS-DMA issue and the counted s_waitcnt vmcnt(n) that covers it (outputs are
 // written after the key loop's last counted wait).  Every DMA'd key tile index is in [0, nkt);
 // building with -DMMT_ATTN_CHECK=1 turns that into a device assert (MMT_ATTN_ASSERT).
-#include "common.hpp"
+#include "attn_common.hpp"
 
-#ifndef MMT_ATTN_CHECK
-#define MMT_ATTN_CHECK 0
-#endif
-#if MMT_ATTN_CHECK
-#include <cassert>
-#define MMT_ATTN_ASSERT(c) assert(c)
-#else
-#define MMT_ATTN_ASSERT(c) ((void)0)
-#endif
 
 namespace {
 
-constexpr int D = 64, KB = 64;
 
 // XCD-aware bijective block remap (as gemm.hip): workgroups are dealt round-robin over the 8 XCDs,
 // so consecutive (query block, head, sequence) ids would put the query blocks of one (sequence,
@@ -312,30 +302,6 @@ __global__ __launch_bounds__(256 / QT) void mam_attention_kernel(const mmt_attn_
 // per-lane source address and again on the read: K / Q rows (read by ds_read_b128) hold chunk c at
 // c ^ (row & 7); V rows (read transposed by ds_read_b64_tr_b16: 8 rows x 2 adjacent chunks per
 // 32-lane group) hold chunk c at c ^ (row & 6).
-template <int N>
-MMT_DEV void attn_wait_vm() {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-typedef __attribute__((address_space(3))) void attn_lds_void;
-typedef __attribute__((address_space(1))) void attn_glb_void;
-MMT_DEV void attn_glds16(const void* src, char* dst) {
-    __builtin_amdgcn_global_load_lds((attn_glb_void*)src, (attn_lds_void*)dst, 16, 0, 0);
-}
-// ds_read_b64_tr_b16 as inline asm: through the builtin, hipcc cannot tell the read from the
-// in-flight LDS-DMA writes and drains vmcnt(0) before it (i.e. waits for the whole prefetch ring).
-// Inline asm is invisible to its wait-count tracking, so the caller waits with attn_lds_wait().
-template <int OFF>
-MMT_DEV uint2 attn_tr16(const char* p) {
-    uint2 r;
-    const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
-    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(a), "n"(OFF));
-    return r;
-}
-MMT_DEV void attn_lds_wait() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);  // keep the MFMAs that consume the asm reads below the wait
-}
-
 #if MMT_STAMP_BUILD
 __device__ unsigned long long g_mmt_attn_stamps[16384 * 8];
 extern "C" int mmt_attn_stamps(unsigned long long* host, int n) {
@@ -347,29 +313,6 @@ extern "C" int mmt_attn_stamps(unsigned long long* host, int n) {
 constexpr int ANS = 8;              // K/V tile slots in the ring
 constexpr int ATILE = 2 * KB * 128; // bytes of one slot: K image then V image
 
-MMT_DEV void attn_wait_dyn(int n) {
-    switch (n) {
-        case 0: attn_wait_vm<0>(); break;
-        case 1: attn_wait_vm<1>(); break;
-        case 2: attn_wait_vm<2>(); break;
-        case 3: attn_wait_vm<3>(); break;
-        case 4: attn_wait_vm<4>(); break;
-        case 5: attn_wait_vm<5>(); break;
-        case 6: attn_wait_vm<6>(); break;
-        case 7: attn_wait_vm<7>(); break;
-        case 8: attn_wait_vm<8>(); break;
-        case 9: attn_wait_vm<9>(); break;
-        case 10: attn_wait_vm<10>(); break;
-        case 11: attn_wait_vm<11>(); break;
-        case 12: attn_wait_vm<12>(); break;
-        case 13: attn_wait_vm<13>(); break;
-        case 14: attn_wait_vm<14>(); break;
-        case 15: attn_wait_vm<15>(); break;
-        case 16: attn_wait_vm<16>(); break;
-        case 17: attn_wait_vm<17>(); break;
-        default: attn_wait_vm<18>(); break;
-    }
-}
 
 // KG key groups of 4 waves: the WG's 64 queries (16 per wave) are shared, the key tiles are dealt
 // round-robin over the groups (tile t -> group t % KG), each group keeps its own online-softmax
@@ -622,7 +565,6 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(KG, KG
 // pipelined variant with one workgroup per CU measured 2.6x slower).  When the key segments are
 // 64-aligned (n_t % 64 == 0) a tile never straddles a segment and its DMA source is one
 // wave-uniform row base plus per-lane constant offsets.
-constexpr int FQ = 128, FTILE = 2 * KB * 128;
 #ifndef MMT_ATTN_FA_MIN_WG
 #define MMT_ATTN_FA_MIN_WG 200  // workgroups of the throughput kernel from which it is chosen
 #endif
@@ -844,10 +786,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 }
 
 
-// V image swizzle: chunk c of row r at c ^ (r & 6) ^ ((r & 2) << 1): the 4 rows x 4 chunks a
-// half-wave reads per tr instruction then cover all 64 banks once.
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-MMT_DEV int attn_vswz(int row) { return (row & 6) ^ ((row & 2) << 1); }
 
 // ---------------------------------------------------------------------------------------------
 // Range-checked exponent kernel (impl 17 / 21; 22 below is its 64-queries-per-wave form).  At d = 64 a score
@@ -874,27 +812,13 @@ MMT_DEV int attn_vswz(int row) { return (row & 6) ^ ((row & 2) << 1); }
 // the matching key order by ds_read_b64_tr_b16.  The last tile computes only the 16-key steps
 // that hold valid keys (528 = 8 x 64 + 16).  The block -> tile map is XCD-aware at every grid size
 // (the query blocks of one (sequence, head) share one XCD's L2 for their K / V re-reads).
-constexpr float LZ_LO = 0x1p-100f, LZ_HI = 0x1p100f;
 // MMT_ATTN_ABLATE (measurement builds only, tools/build_ablate.sh; results are wrong): 1 = no K/V
 // DMA after the prologue, 2 = no matrix / softmax work, 3 = no exponentials (P = S)
 #ifndef MMT_ATTN_ABLATE
 #define MMT_ATTN_ABLATE 0
 #endif
 
-MMT_DEV void attn_block_ids_xcd(int& bx, int& by, int& bz) {
-    const int nbx = gridDim.x, nby = gridDim.y, nwg = nbx * nby * gridDim.z;
-    const int orig = blockIdx.x + nbx * (blockIdx.y + nby * blockIdx.z);
-    const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-    const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-    bx = lin % nbx;
-    by = (lin / nbx) % nby;
-    bz = lin / (nbx * nby);
-}
 
-template <int N>
-struct attn_ic {
-    static constexpr int value = N;
-};
 
 // PIPE: the two 32-key blocks of a full tile software-pipelined inside the wave (impl 21, the
 // large-grid default): both blocks' scores are computed before either block's exponentials, so
@@ -1589,8 +1513,8 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 // reads the tile; tile t + 2 is issued there into the slot of tile t - 2, which every wave has finished
 // reading (the fragment reads run one block ahead of the math).  Loop: global memory sees only the
 // LDS-DMA pieces, so the counted vmcnt waits never include a store (stores start in the epilogue).
-template <int NW>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2))) void mam_attention_hs_kernel(
+template <int NW, int WPE = 2>  // waves per workgroup, waves per SIMD (1: the whole 512-register file)
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void mam_attention_hs_kernel(
     const mmt_attn_params p) {
     constexpr int R = 4;          // K / V tile slots
     constexpr int QWG = 64 * NW;  // queries per workgroup
@@ -1765,6 +1689,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
             }
             lacc[qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pb, lacc[qb], 0, 0, 0);
         }
+        if constexpr (WPE == 1) {  // O and the row sums live in the accumulator registers
+            asm volatile("" : "+a"(o[qb][0]), "+a"(o[qb][1]), "+a"(lacc[qb]));
+        }
     };
     // P = exp2(S) (keys past Lk: 0) of accumulator elements [r0, r1) of query block qb, packed to bf16
     // (r0, r1 multiples of 2: whole packed pairs)
@@ -1920,13 +1847,19 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
 }
 #endif  // MMT_ATTN_AB
 
+}  // namespace
+
+int mmt_attn_launch_pp(const mmt_attn_params& p, hipStream_t st);  // attention_pp.hip: impl 24
+
+namespace {
+
 template <typename T>
 int launch_attn(const mmt_attn_params& p, hipStream_t st) {
     // impl: 0 = the library's choice by dtype and grid size; forced (A/B and tests): 4 = latency kernel,
     // 8 = running-maximum throughput kernel, 17 / 21 / 22 = range-checked exponent kernels (22 = 64
     // queries per wave); A/B build: 23 = the block-pipelined form of 22 with 256-query workgroups
-    if (p.impl != 0 && p.impl != 4 && p.impl != 8 && p.impl != 17 && p.impl != 21 && p.impl != 22 &&
-        !(MMT_ATTN_AB && p.impl == 23))
+    if (p.impl != 0 && p.impl != 4 && p.impl != 8 && p.impl != 17 && p.impl != 21 && p.impl != 22 && p.impl != 24 &&
+        !(MMT_ATTN_AB && (p.impl == 23 || p.impl == 25 || p.impl == 26)))
         return MMT_EBADARG;
     // lse (training forward) is written by impls 0 / 4 / 8 / 17 / 21 only: impls 22 / 23 never write it
     if (p.lse && (sizeof(T) != 2 || p.impl >= 22)) return MMT_EBADARG;
@@ -1966,11 +1899,18 @@ int launch_attn(const mmt_attn_params& p, hipStream_t st) {
         if (impl == 17) hipLaunchKernelGGL((mam_attention_lz_kernel<3, 3, true>), fgrid, dim3(256), 0, st, p);
         else if (impl == 21) hipLaunchKernelGGL((mam_attention_lz_kernel<3, 3, true, true>), fgrid, dim3(256), 0, st, p);
         else if (impl == 22) hipLaunchKernelGGL((mam_attention_lz2_kernel<2>), fgrid, dim3(128), 0, st, p);
+        else if (impl == 24) mmt_attn_launch_pp(p, st);
 #if MMT_ATTN_AB
         else if (impl == 23) {  // block-pipelined kernel, 4 waves (256 queries) per workgroup
             const int nt = (p.n_t + 255) / 256, ns = (p.ntok - p.n_t + 255) / 256;
             const dim3 hgrid(p.q_part == 1 ? nt : p.q_part == 2 ? ns : nt + ns, p.H, p.S);
             hipLaunchKernelGGL((mam_attention_hs_kernel<4>), hgrid, dim3(256), 0, st, p);
+        } else if (impl == 26) {  // the same at one wave per SIMD (one 256-query workgroup per CU)
+            const int nt = (p.n_t + 255) / 256, ns = (p.ntok - p.n_t + 255) / 256;
+            const dim3 hgrid(p.q_part == 1 ? nt : p.q_part == 2 ? ns : nt + ns, p.H, p.S);
+            hipLaunchKernelGGL((mam_attention_hs_kernel<4, 1>), hgrid, dim3(256), 0, st, p);
+        } else if (impl == 25) {  // 2-wave (128-query) workgroups at one wave per SIMD (two per CU)
+            hipLaunchKernelGGL((mam_attention_hs_kernel<2, 1>), fgrid, dim3(128), 0, st, p);
         }
 #endif
         else if (impl == 8 || p.lse) hipLaunchKernelGGL((mam_attention_fa_kernel<T, 2, 3>), fgrid, dim3(256), 0, st, p);
