@@ -169,13 +169,23 @@ def inframe_profile(graphs, plan, frames=20):
 
 
 def load_traffic(variant, B, dtype):
-    """HBM bytes per launch by plan-entry name, from the committed PMC pass (tools/pmc_traffic.py)."""
+    """HBM bytes per launch by plan-entry name, from the committed PMC pass (tools/pmc_traffic.py),
+    and the stamp check: the counts are used only if they were taken on kernel sources with this
+    tree's digest (mmt_amd.stamp); otherwise `traffic` is null and the reason is reported."""
+    from mmt_amd.stamp import source_digest
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            return json.load(f).get("%s/B%d/%s" % (variant, B, dtype), {})
+            res = json.load(f).get("%s/B%d/%s" % (variant, B, dtype), {})
     except (OSError, ValueError):
-        return {}
+        return {}, "no PMC traffic file"
+    if not res:
+        return {}, "no PMC pass for this workload"
+    stamp = res.get("_stamp", {}).get("source_digest")
+    here = source_digest()
+    if stamp != here:
+        return {}, "PMC pass taken on sources %s, this tree is %s: not reported" % (stamp, here)
+    return res, "PMC pass on this tree's sources (%s)" % here
 
 
 def roofline(rt, plan, times, dtype, traffic=None, warm_times=None):
@@ -633,7 +643,10 @@ def main():
         timing = "in-frame (profiler dispatch timestamps of graph-replayed frames, median of 20)"
         if times is None:  # no profiler records: the warm back-to-back figure, labelled as such
             times, timing = warm, "warm back-to-back launches (no in-frame records)"
-        dom, mam, dev_ms, by = roofline(rt, plan, times, args.dtype, load_traffic(args.variant, B, args.dtype), warm)
+        traffic, traffic_note = load_traffic(args.variant, B, args.dtype)
+        dom, mam, dev_ms, by = roofline(rt, plan, times, args.dtype, traffic, warm)
+        for o in (dom, mam):
+            o["traffic_source"] = traffic_note
         for o in (dom, mam):
             o["timing"] = timing
 

@@ -54,10 +54,14 @@ def main():
         allres = json.load(open(dst))
     except (OSError, ValueError):
         allres = {}
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "multi-modal-tracking_amd"))
+    from mmt_amd.stamp import source_digest
+    # the kernel sources these counts were taken on: bench.py reports them only for the same digest
+    res["_stamp"] = {"source_digest": source_digest(), "git_head": os.environ.get("MMT_GIT_HEAD", "")}
     allres[key] = res
     with open(dst, "w") as f:
         json.dump(allres, f, indent=1, sort_keys=True)
-    for nm in sorted(res, key=lambda k: -res[k]["traffic_bytes"])[:12]:
+    for nm in sorted((k for k in res if not k.startswith("_")), key=lambda k: -res[k]["traffic_bytes"])[:12]:
         print("%-22s fetch %8.2f MB  write %8.2f MB" % (nm, res[nm]["fetch_bytes"] / 1e6, res[nm]["write_bytes"] / 1e6))
 
 
