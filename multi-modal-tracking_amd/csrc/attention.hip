@@ -1849,7 +1849,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
 
 }  // namespace
 
-int mmt_attn_launch_pp(const mmt_attn_params& p, hipStream_t st);  // attention_pp.hip: impl 24
+int mmt_attn_launch_pp(const mmt_attn_params& p, int ks, hipStream_t st);  // attention_pp.hip: impl 24 / 25
 
 namespace {
 
@@ -1859,7 +1859,7 @@ int launch_attn(const mmt_attn_params& p, hipStream_t st) {
     // 8 = running-maximum throughput kernel, 17 / 21 / 22 = range-checked exponent kernels (22 = 64
     // queries per wave); A/B build: 23 = the block-pipelined form of 22 with 256-query workgroups
     if (p.impl != 0 && p.impl != 4 && p.impl != 8 && p.impl != 17 && p.impl != 21 && p.impl != 22 && p.impl != 24 &&
-        !(MMT_ATTN_AB && (p.impl == 23 || p.impl == 25 || p.impl == 26)))
+        p.impl != 25 && !(MMT_ATTN_AB && (p.impl == 23 || p.impl == 26 || p.impl == 27)))
         return MMT_EBADARG;
     // lse (training forward) is written by impls 0 / 4 / 8 / 17 / 21 only: impls 22 / 23 never write it
     if (p.lse && (sizeof(T) != 2 || p.impl >= 22)) return MMT_EBADARG;
@@ -1899,7 +1899,7 @@ int launch_attn(const mmt_attn_params& p, hipStream_t st) {
         if (impl == 17) hipLaunchKernelGGL((mam_attention_lz_kernel<3, 3, true>), fgrid, dim3(256), 0, st, p);
         else if (impl == 21) hipLaunchKernelGGL((mam_attention_lz_kernel<3, 3, true, true>), fgrid, dim3(256), 0, st, p);
         else if (impl == 22) hipLaunchKernelGGL((mam_attention_lz2_kernel<2>), fgrid, dim3(128), 0, st, p);
-        else if (impl == 24) mmt_attn_launch_pp(p, st);
+        else if (impl == 24 || impl == 25) mmt_attn_launch_pp(p, impl == 25 ? 2 : 1, st);
 #if MMT_ATTN_AB
         else if (impl == 23) {  // block-pipelined kernel, 4 waves (256 queries) per workgroup
             const int nt = (p.n_t + 255) / 256, ns = (p.ntok - p.n_t + 255) / 256;
@@ -1909,7 +1909,7 @@ int launch_attn(const mmt_attn_params& p, hipStream_t st) {
             const int nt = (p.n_t + 255) / 256, ns = (p.ntok - p.n_t + 255) / 256;
             const dim3 hgrid(p.q_part == 1 ? nt : p.q_part == 2 ? ns : nt + ns, p.H, p.S);
             hipLaunchKernelGGL((mam_attention_hs_kernel<4, 1>), hgrid, dim3(256), 0, st, p);
-        } else if (impl == 25) {  // 2-wave (128-query) workgroups at one wave per SIMD (two per CU)
+        } else if (impl == 27) {  // 2-wave (128-query) workgroups at one wave per SIMD (two per CU)
             hipLaunchKernelGGL((mam_attention_hs_kernel<2, 1>), fgrid, dim3(128), 0, st, p);
         }
 #endif

@@ -51,9 +51,14 @@ struct PPState {
     f32x4 lacc[NQ];   // row sums (every element = this lane's query)
 };
 
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1, 1))) void mam_attention_pp_kernel(
+// KS = key halves per workgroup: 1 (impl 24: 2 waves = 128 queries over all keys, two workgroups per CU)
+// or 2 (impl 25, small grids such as batch-1 tracking: 4 waves, waves 2-3 take the second half of the
+// 32-key blocks of the same 128 queries with their own K / V ring; without a reference point the halves'
+// O and row sums simply add, through LDS at the end).
+template <int KS>
+__global__ __launch_bounds__(128 * KS) __attribute__((amdgpu_waves_per_eu(1, 1))) void mam_attention_pp_kernel(
     const mmt_attn_params p) {
-    __shared__ __attribute__((aligned(1024))) char lds[PP_R * FTILE];
+    __shared__ __attribute__((aligned(1024))) char lds_all[KS * PP_R * FTILE];
     int bx, h, s;
     attn_block_ids_xcd(bx, h, s);
 
@@ -73,9 +78,19 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int l32 = lane & 31, hf = lane >> 5;
     const int prow = lane >> 3, pcol = lane & 7;
+    const int wq = w & 1;                     // query wave: queries q0 + 64 wq + [0, 64)
+    const int half = KS == 2 ? (w >> 1) : 0;  // key half
+    char* lds = lds_all + half * PP_R * FTILE;
+    // this half's 32-key blocks [kb0, kb0 + nb) of the nb_all blocks: keys k0 .. k0 + Lh - 1
+    const int nb_all = (Lk + 31) / 32;
+    const int nb_h0 = KS == 2 ? (nb_all + 1) / 2 : nb_all;
+    const int kb0 = half ? nb_h0 : 0;
+    const int nb = half ? nb_all - nb_h0 : nb_h0;
+    const int k0 = 32 * kb0;
+    const int Lh = min(Lk, 32 * (kb0 + nb)) - k0;
 
-    // ---- K / V tiles: wave 0 DMAs the 8 K pieces of a tile, wave 1 the 8 V pieces
-    const int isv = w;
+    // ---- K / V tiles of the half: wave 0 of the pair DMAs the 8 K pieces of a tile, wave 1 the 8 V pieces
+    const int isv = wq;
     const int64_t col = (isv ? 2 * C : C) + h * D + (isv ? (pcol ^ attn_vswz(prow)) : (pcol ^ prow)) * 8;
     auto key_row = [&](int kk) -> const bf16_t* {
         int seq = s, row = kk;
@@ -86,25 +101,32 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
         return qkv + ((int64_t)seq * pitch + row) * rs;
     };
-    const bool aligned = n_t % KB == 0;
-    const int nkt = (Lk + KB - 1) / KB;
+    const bool aligned = n_t % KB == 0 && k0 % KB == 0;
+    const int nkt = nb > 0 ? (Lh + KB - 1) / KB : 0;  // tiles of this half
     auto issue_tile = [&](int t) {
         MMT_ATTN_ASSERT(t >= 0 && t < nkt);
         char* slot = lds + (t % PP_R) * FTILE + isv * KB * 128;
-        if (aligned && t * KB + KB <= Lk) {
-            const bf16_t* base = key_row(t * KB);
+        if (aligned && t * KB + KB <= Lh) {
+            const bf16_t* base = key_row(k0 + t * KB);
 #pragma unroll
             for (int pk = 0; pk < 8; ++pk) attn_glds16(base + (int64_t)(pk * 8 + prow) * rs + col, slot + pk * 1024);
         } else {
 #pragma unroll
-            for (int pk = 0; pk < 8; ++pk) attn_glds16(key_row(min(t * KB + pk * 8 + prow, Lk - 1)) + col, slot + pk * 1024);
+            for (int pk = 0; pk < 8; ++pk)
+                attn_glds16(key_row(min(k0 + t * KB + pk * 8 + prow, Lk - 1)) + col, slot + pk * 1024);
         }
+    };
+    // barriers: each half syncs once per tile after its first; the halves' counts are evened out before
+    // the merge (s_barrier is a workgroup-wide rendezvous)
+    const int nkt_max = KS == 2 ? (min(Lk, 32 * nb_h0) + KB - 1) / KB : nkt;
+    auto pad_barriers = [&]() {
+        for (int t = max(nkt, 1); t < nkt_max; ++t) lds_barrier();
     };
 
     // ---- Q fragments straight from global memory (B operand of S^T = K Q^T: query l32 of the block,
     // d = 16 ks + 8 hf .. + 7); rows past the block's end re-read the last query.  Issued before the
     // first tiles, so the counted waits below cover them.
-    const int qbase = q0 + 64 * w;  // query blocks qbase + 32 qb + [0, 32)
+    const int qbase = q0 + 64 * wq;  // query blocks qbase + 32 qb + [0, 32)
     const int nqa = (qbase < qend ? 1 : 0) + (qbase + 32 < qend ? 1 : 0);
     u32x4 qf[2][4];
 #pragma unroll
@@ -138,13 +160,17 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         lds_barrier();
         if (t + 2 < nkt) issue_tile(t + 2);
     };
-    attn_wait_dyn(8 * (min(nkt - 1, 2)));
+    attn_wait_dyn(8 * (max(0, min(nkt - 1, 2))));
     lds_barrier();
 
-    const int nb = (Lk + 31) / 32;  // 32-key blocks; the last holds nvl keys
-    const int nvl = Lk - 32 * (nb - 1);
-    if (nqa == 0) {  // no queries: keep the workgroup's DMA / barrier schedule
+    const int nvl = Lh - 32 * (nb - 1);  // keys of this half's last block
+    // the halves' merge (KS = 2): half 1 leaves O and the row sums of its query wave in LDS (its own
+    // ring, done with), half 0 adds them before its epilogue
+    float* mrg = (float*)(lds_all + PP_R * FTILE) + wq * (4 * 16 * 64 + 2 * 64);
+    if (nqa == 0 || nb == 0) {  // no queries / no keys: keep the workgroup's DMA / barrier schedule
         for (int t = 1; t < nkt; ++t) sync_tile(t);
+        pad_barriers();
+        if (KS == 2) lds_barrier();  // the merge (half 0 always has keys: it takes the longer half)
         return;
     }
 
@@ -232,7 +258,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const float e = __builtin_amdgcn_exp2f(sv[r]);
-                sv[r] = (!MASK || 32 * b + 8 * (r >> 2) + 4 * hf + (r & 3) < Lk) ? e : 0.f;
+                sv[r] = (!MASK || 32 * (kb0 + b) + 8 * (r >> 2) + 4 * hf + (r & 3) < Lk) ? e : 0.f;
             }
 #pragma unroll
             for (int j = 0; j < 2; ++j)
@@ -383,6 +409,39 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             else last(i, sA, pB, pA, attn_ic<0>{});
         }
 
+        if constexpr (KS == 2) {
+            pad_barriers();
+            if (half == 1) {
+#pragma unroll
+                for (int qb = 0; qb < NQ; ++qb) {
+#pragma unroll
+                    for (int db = 0; db < 2; ++db)
+#pragma unroll
+                        for (int r4 = 0; r4 < 4; ++r4)
+                            *(f32x4*)(mrg + (((qb * 2 + db) * 4 + r4) * 64 + lane) * 4) =
+                                f32x4{st.o[qb][db][4 * r4], st.o[qb][db][4 * r4 + 1], st.o[qb][db][4 * r4 + 2],
+                                      st.o[qb][db][4 * r4 + 3]};
+                    mrg[4 * 16 * 64 + qb * 64 + lane] = st.lacc[qb][0];
+                }
+                lds_barrier();
+                return;
+            }
+            lds_barrier();
+            if (nb_all - nb_h0 > 0) {  // half 1 had keys
+#pragma unroll
+                for (int qb = 0; qb < NQ; ++qb) {
+#pragma unroll
+                    for (int db = 0; db < 2; ++db)
+#pragma unroll
+                        for (int r4 = 0; r4 < 4; ++r4) {
+                            const f32x4 v = *(const f32x4*)(mrg + (((qb * 2 + db) * 4 + r4) * 64 + lane) * 4);
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) st.o[qb][db][4 * r4 + e] += v[e];
+                        }
+                    st.lacc[qb][0] += mrg[4 * 16 * 64 + qb * 64 + lane];
+                }
+            }
+        }
         // per query block: range check, normalise and store, or the exact fallback (impl 22's)
 #pragma unroll
         for (int qb = 0; qb < NQ; ++qb) {
@@ -447,10 +506,12 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
 }  // namespace
 
-// launched by attention.hip's dispatcher (impl 24): grid (128-query blocks, heads, sequences), 128 threads
-int mmt_attn_launch_pp(const mmt_attn_params& p, hipStream_t st) {
+// launched by attention.hip's dispatcher (impl 24: ks 1, impl 25: ks 2): grid (128-query blocks, heads,
+// sequences), 128 x ks threads
+int mmt_attn_launch_pp(const mmt_attn_params& p, int ks, hipStream_t st) {
     const int t = (p.n_t + FQ - 1) / FQ, sr = (p.ntok - p.n_t + FQ - 1) / FQ;
     const int nqb = p.q_part == 1 ? t : p.q_part == 2 ? sr : t + sr;
-    hipLaunchKernelGGL(mam_attention_pp_kernel, dim3(nqb, p.H, p.S), dim3(128), 0, st, p);
+    if (ks == 2) hipLaunchKernelGGL(mam_attention_pp_kernel<2>, dim3(nqb, p.H, p.S), dim3(256), 0, st, p);
+    else hipLaunchKernelGGL(mam_attention_pp_kernel<1>, dim3(nqb, p.H, p.S), dim3(128), 0, st, p);
     return 0;
 }

@@ -78,8 +78,8 @@ def test_bad_arguments_rejected_without_gpu_work():
 
 
 def test_attention_impl_and_lse_gate():
-    """mmt_mam_attention takes impl 0 (library choice), 4, 8, 17, 21, 22, 24 only (the round-2 A/B-only
-    kernels 2, 9-12, 16, 18-20 are no longer in the library; 23 is in the A/B build only); impls 22 - 24
+    """mmt_mam_attention takes impl 0 (library choice), 4, 8, 17, 21, 22, 24, 25 only (the round-2 A/B-only
+    kernels 2, 9-12, 16, 18-20 are no longer in the library; 23 is in the A/B build only); impls 22 - 25
     never write the log-sum-exp
     the training backward consumes, so lse with them is rejected; fp16 takes the running-maximum kernels
     only.  Every case fails validation on the host, before a launch."""
@@ -93,11 +93,12 @@ def test_attention_impl_and_lse_gate():
             setattr(a, k, v)
         return _lib.LIB.mmt_mam_attention(ctypes.byref(a), dt, None)
 
-    for impl in (2, 9, 10, 11, 12, 16, 18, 19, 20, 23, 25, 99):
+    for impl in (2, 9, 10, 11, 12, 16, 18, 19, 20, 23, 26, 27, 99):
         assert attn(impl=impl) == -10000, impl
     assert attn(impl=22, lse=fake) == -10000
     assert attn(impl=23, lse=fake) == -10000
     assert attn(impl=24, lse=fake) == -10000
+    assert attn(impl=25, lse=fake) == -10000
     assert attn(dt=_lib.MMT_F16, impl=24) == -10000
     assert attn(dt=_lib.MMT_F16, impl=17) == -10000
     assert attn(dt=_lib.MMT_F16, lse=fake) == -10000

@@ -9,7 +9,7 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_ops.py -m gpu -q -rf --time
     -k "mam or attention" > "$OUT/pytest_attn.log" 2>&1
 rc=$?; echo "pytest attn rc=$rc"; tail -5 "$OUT/pytest_attn.log"
 if [ $rc -gt 1 ]; then exit $rc; fi
-timeout -k 10 300 python -u tools/attn_ab.py --impls 22,24 --batches 1,4,8,32 > "$OUT/attn_ab.jsonl" 2>&1
+timeout -k 10 300 python -u tools/attn_ab.py --impls 4,22,24,25 --batches 1,2,4,8,32 > "$OUT/attn_ab.jsonl" 2>&1
 rc=$?; echo "attn rc=$rc"; grep -v amdgpu.ids "$OUT/attn_ab.jsonl" | tail -8
 if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 600 python -u -m pytest tests/test_gpu_train_ops.py tests/test_gpu_cache.py tests/test_gpu_ce.py -m gpu -q -rf --timeout 120 \
