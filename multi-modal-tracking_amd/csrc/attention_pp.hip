@@ -34,7 +34,13 @@
 
 namespace {
 
-constexpr int PP_R = 4;  // K / V tile slots
+// MMT_ATTN_ABLATE (measurement builds only, tools/build_ablate.sh; results are wrong): 1 = no K / V DMA
+// after the prologue, 3 = no exponentials, 5 = free-running (no per-tile wait / barrier / refill), 7 = no
+// K / V fragment reads in the steady-state loop, 8 = no s_nop before the PV MFMAs, 9 = no packs (P = S
+// bits), 10 = no PV MFMAs in the steady-state loop, 11 = no QK^T MFMAs in the steady-state loop
+#ifndef MMT_ATTN_ABLATE
+#define MMT_ATTN_ABLATE 0
+#endif
 
 // LDS fragment reads as inline asm (invisible to hipcc's wait-count tracking, which would otherwise
 // drain the LDS-DMA ring before each read); the waits are explicit (wait_k / wait_v below).
@@ -44,6 +50,16 @@ MMT_DEV u32x4 pp_b128(const char* p) {
     asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(a));
     return r;
 }
+
+#if MMT_STAMP_BUILD
+// measurement build (tools/build_ablate.sh stamp): per workgroup, wave 0: [0] realtime / [1] memtime at
+// entry, [2] loop start, [3] loop end (before the last block), [4] end, [5] realtime end, [6] blocks, [7] nqa
+__device__ unsigned long long g_mmt_attn_pp_stamps[16384 * 8];
+extern "C" int mmt_attn_pp_stamps(unsigned long long* host, int n) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_mmt_attn_pp_stamps), sizeof(unsigned long long) * n);
+}
+#endif
+#define MMT_PPSTAMP(I, INSN) MMT_STAMP_AT(g_mmt_attn_pp_stamps, I, INSN)
 
 template <int NQ>
 struct PPState {
@@ -58,7 +74,12 @@ struct PPState {
 template <int KS>
 __global__ __launch_bounds__(128 * KS) __attribute__((amdgpu_waves_per_eu(1, 1))) void mam_attention_pp_kernel(
     const mmt_attn_params p) {
+    // K / V tile slots per key half: R - 2 tiles in flight ahead of the one being read (4: two workgroups
+    // per CU; a 5-slot ring measured slower, B = 32 84.7 -> 92.0 us, profiles/r04_attn_pp_ab.jsonl)
+    constexpr int PP_R = 4;
     __shared__ __attribute__((aligned(1024))) char lds_all[KS * PP_R * FTILE];
+    MMT_PPSTAMP(0, "s_memrealtime");
+    MMT_PPSTAMP(1, "s_memtime");
     int bx, h, s;
     attn_block_ids_xcd(bx, h, s);
 
@@ -103,13 +124,30 @@ __global__ __launch_bounds__(128 * KS) __attribute__((amdgpu_waves_per_eu(1, 1))
     };
     const bool aligned = n_t % KB == 0 && k0 % KB == 0;
     const int nkt = nb > 0 ? (Lh + KB - 1) / KB : 0;  // tiles of this half
+    // Full tiles inside one key segment (all but a tail) are DMA'd by buffer_load ... lds: the lane's
+    // offset inside a piece (row prow, swizzled chunk) is a constant VGPR, the piece's row base a scalar
+    // soffset, so a tile costs no vector instructions (a flat global_load_lds needs a 64-bit address
+    // per piece: ~60 VALU per tile, a quarter of the kernel's vector issue at B = 32).
+    const __amdgpu_buffer_rsrc_t qrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)qkv, 0, (int)min((int64_t)0x7fffffff, (int64_t)p.S * pitch * rs * 2), 0x00020000);
+    const int lane_voff = (int)((prow * rs + col) * 2);
+    typedef __attribute__((address_space(3))) void lds_void_t;
     auto issue_tile = [&](int t) {
         MMT_ATTN_ASSERT(t >= 0 && t < nkt);
         char* slot = lds + (t % PP_R) * FTILE + isv * KB * 128;
         if (aligned && t * KB + KB <= Lh) {
-            const bf16_t* base = key_row(k0 + t * KB);
+            const int kk = k0 + t * KB;  // wave-uniform: the tile's first key, its (sequence, row)
+            int seq = s, row = kk;
+            if (cross) {
+                if (kk < n_t) seq = sV;
+                else if (kk < 2 * n_t) { seq = sI; row = kk - n_t; }
+                else row = kk - n_t;
+            }
+            const int soff = __builtin_amdgcn_readfirstlane((int)(((int64_t)seq * pitch + row) * rs * 2));
 #pragma unroll
-            for (int pk = 0; pk < 8; ++pk) attn_glds16(base + (int64_t)(pk * 8 + prow) * rs + col, slot + pk * 1024);
+            for (int pk = 0; pk < 8; ++pk)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(qrs, (lds_void_t*)(slot + pk * 1024), 16, lane_voff,
+                                                         soff + pk * 8 * (int)rs * 2, 0, 0);
         } else {
 #pragma unroll
             for (int pk = 0; pk < 8; ++pk)
@@ -135,8 +173,8 @@ __global__ __launch_bounds__(128 * KS) __attribute__((amdgpu_waves_per_eu(1, 1))
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) qf[qb][ks] = *(const u32x4*)(qp + (2 * ks + hf) * 8);
     }
-    // prologue DMA: tiles 0, 1, 2 (sync point t issues tile t + 2)
-    for (int t = 0; t < 3 && t < nkt; ++t) issue_tile(t);
+    // prologue DMA: tiles 0 .. R - 2 (sync point t issues tile t + R - 2)
+    for (int t = 0; t < PP_R - 1 && t < nkt; ++t) issue_tile(t);
 
     const float cexp = p.scale * 1.4426950408889634f;
     if (fabsf(cexp - 1.f) > 1e-6f) {  // natural-scale q: to log2 units
@@ -152,15 +190,16 @@ __global__ __launch_bounds__(128 * KS) __attribute__((amdgpu_waves_per_eu(1, 1))
             }
     }
 
-    // sync point of tile t (t >= 1): this wave's pieces of tile t landed (tile t + 1's may still be in
-    // flight), every wave's (the barrier), and every wave is past the V reads of tile t - 2, whose slot
-    // then takes tile t + 2.  Tile 0: the prologue wait.
+    // sync point of tile t (t >= 1): this wave's pieces of tile t landed (the R - 3 tiles after it may
+    // still be in flight), every wave's (the barrier), and every wave is past the V reads of tile t - 2,
+    // whose slot then takes tile t + R - 2.  Tile 0: the prologue wait.
     auto sync_tile = [&](int t) {
-        attn_wait_dyn(t + 1 < nkt ? 8 : 0);
+        if (MMT_ATTN_ABLATE == 5) return;
+        attn_wait_dyn(8 * (min(nkt - 1, t + PP_R - 3) - t));
         lds_barrier();
-        if (t + 2 < nkt) issue_tile(t + 2);
+        if (MMT_ATTN_ABLATE != 1 && t + PP_R - 2 < nkt) issue_tile(t + PP_R - 2);
     };
-    attn_wait_dyn(8 * (max(0, min(nkt - 1, 2))));
+    attn_wait_dyn(8 * (max(0, min(nkt - 1, PP_R - 2))));
     lds_barrier();
 
     const int nvl = Lh - 32 * (nb - 1);  // keys of this half's last block
@@ -301,21 +340,34 @@ __global__ __launch_bounds__(128 * KS) __attribute__((amdgpu_waves_per_eu(1, 1))
         auto mf_o = [&](int qb, int j, int db, const u32x4& pb) {
             const uint2 ua = vt[j][db][0], ub = vt[j][db][1];
             const u32x4 vf = u32x4{ua.x, ua.y, ub.x, ub.y};
-            asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(st.o[qb][db]) : "v"(vf), "v"(pb));
+            if (MMT_ATTN_ABLATE == 10) return;
+            if (MMT_ATTN_ABLATE == 8)
+                asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(st.o[qb][db]) : "v"(vf), "v"(pb));
+            else
+                asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(st.o[qb][db]) : "v"(vf), "v"(pb));
         };
         auto mf_l = [&](int qb, const u32x4& pb) {
             const u32x4 su = sel_u;
-            asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(st.lacc[qb]) : "v"(su), "v"(pb));
+            if (MMT_ATTN_ABLATE == 10) return;
+            if (MMT_ATTN_ABLATE == 8)
+                asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(st.lacc[qb]) : "v"(su), "v"(pb));
+            else
+                asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(st.lacc[qb]) : "v"(su), "v"(pb));
         };
         auto ex2 = [&](f32x16& sv, int r) {
+            if (MMT_ATTN_ABLATE == 3) return;
             sv[r] = __builtin_amdgcn_exp2f(sv[r]);
             sv[r + 1] = __builtin_amdgcn_exp2f(sv[r + 1]);
         };
-        auto cv = [&](const f32x16& sv, u32x4 (&dst)[2], int r) { dst[r >> 3][(r & 7) >> 1] = pack_bf16x2(sv[r], sv[r + 1]); };
+        auto cv = [&](const f32x16& sv, u32x4 (&dst)[2], int r) {
+            dst[r >> 3][(r & 7) >> 1] = MMT_ATTN_ABLATE == 9 ? __float_as_uint(sv[r]) : pack_bf16x2(sv[r], sv[r + 1]);
+        };
         auto kr = [&](int b, int ks) {
+            if (MMT_ATTN_ABLATE == 7) return;
             kf[ks] = pp_b128(kimg_of(b) + l32 * 128 + ((((2 * ks + hf) * 16) ^ kpos)));
         };
         auto vr = [&](int b, int j, int db) {
+            if (MMT_ATTN_ABLATE == 7) return;
             const char* vimg = lds + ((b >> 1) % PP_R) * FTILE + KB * 128;
             const int row = 32 * (b & 1) + 16 * j + 4 * hf + qr;
             const char* b1 = vimg + row * 128 + (((4 * db + 2 * dsub + (pc >> 1)) ^ attn_vswz(row)) * 16) + (pc & 1) * 8;
@@ -323,6 +375,7 @@ __global__ __launch_bounds__(128 * KS) __attribute__((amdgpu_waves_per_eu(1, 1))
             vt[j][db][1] = attn_tr16<8 * 128>(b1);
         };
         auto qk1 = [&](f32x16& dst, int qb, int ks) {
+            if (MMT_ATTN_ABLATE == 11) return;
             dst = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kf[ks]), __builtin_bit_cast(bf16x8, qf[qb][ks]),
                                                           ks ? dst : f32x16{}, 0, 0, 0);
         };
@@ -383,6 +436,7 @@ __global__ __launch_bounds__(128 * KS) __attribute__((amdgpu_waves_per_eu(1, 1))
         };
 
         // prologue: K(0) -> S(0)
+        MMT_PPSTAMP(2, "s_memtime");
         kread(0, kf);
         wait_k();
         qk(sA);
@@ -405,6 +459,7 @@ __global__ __launch_bounds__(128 * KS) __attribute__((amdgpu_waves_per_eu(1, 1))
                 else iter(i, sB, sA, pA, pB, attn_ic<0>{});
                 ++i;
             }
+            MMT_PPSTAMP(3, "s_memtime");
             if (i & 1) last(i, sB, pA, pB, attn_ic<0>{});
             else last(i, sA, pB, pA, attn_ic<0>{});
         }
@@ -449,7 +504,7 @@ __global__ __launch_bounds__(128 * KS) __attribute__((amdgpu_waves_per_eu(1, 1))
             float chk = 0.f;
 #pragma unroll
             for (int r = 0; r < 16; ++r) chk += st.o[qb][0][r] * 0.f + st.o[qb][1][r] * 0.f;
-            const bool ok = l >= LZ_LO && l <= LZ_HI && chk == 0.f;
+            const bool ok = (l >= LZ_LO && l <= LZ_HI && chk == 0.f) || MMT_ATTN_ABLATE != 0;
             const int q = qbase + 32 * qb + l32;
             bf16_t* op = (bf16_t*)p.out + ((int64_t)s * pitch + q) * C + h * D;
             if (__builtin_expect(__all(ok), 1)) {
@@ -502,6 +557,15 @@ __global__ __launch_bounds__(128 * KS) __attribute__((amdgpu_waves_per_eu(1, 1))
     };
     if (nqa == 2) run(attn_ic<2>{});
     else run(attn_ic<1>{});
+    MMT_PPSTAMP(4, "s_memtime");
+    MMT_PPSTAMP(5, "s_memrealtime");
+#if MMT_STAMP_BUILD
+    if (threadIdx.x == 0) {
+        const int wg = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+        g_mmt_attn_pp_stamps[wg * 8 + 6] = nb;
+        g_mmt_attn_pp_stamps[wg * 8 + 7] = nqa;
+    }
+#endif
 }
 
 }  // namespace

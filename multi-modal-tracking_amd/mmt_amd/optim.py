@@ -47,7 +47,6 @@ class HipAdamW(torch.optim.Optimizer):
         if len(groups) > MAX_GROUPS:
             raise ValueError("at most %d parameter groups" % MAX_GROUPS)
         super().__init__(groups, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
-        self.groups = self.param_groups  # the live dicts
         self.betas, self.eps = betas, eps
         self.step_count = 0
         self.chunk = int(LIB.mmt_adamw_chunk_elems())
@@ -65,6 +64,11 @@ class HipAdamW(torch.optim.Optimizer):
         self._key = None
         self.last_norm = None
         self.table_writes = 0
+
+    @property
+    def groups(self):
+        """The live group dicts (load_state_dict replaces the list; schedulers write its "lr")."""
+        return self.param_groups
 
     def _device_state(self, dev):
         if not hasattr(self, "_state"):
