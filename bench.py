@@ -393,7 +393,7 @@ def cpu_baseline(variant, B, budget_s=12.0, geo=None):
 TRAIN_FLOP_PER_SAMPLE = 3 * 218.59e9  # forward + backward ~ 3 x the 218.59 GFLOP forward
 
 
-def train_bench(world, rank, B, steps, warmup, device="cuda", ops=None, search=320, template=128):
+def train_bench(world, rank, B, steps, warmup, device="cuda", ops=None, search=320, template=128, graph=True):
     """BASELINE config 4: DDP training step of the two-stream MixViT-B RGB-T,
     B LaSOT-shaped synthetic pairs per GPU: forward with autograd on the HIP ops, CIoU + L1 box
     loss, backward with the RCCL gradient all-reduce (DistributedDataParallel, bucketed, overlapped
@@ -411,18 +411,36 @@ def train_bench(world, rank, B, steps, warmup, device="cuda", ops=None, search=3
     batches = [synthetic_batch(B, device, g, template, search) for _ in range(2)]
     sync = torch.cuda.synchronize if device != "cpu" else (lambda: None)
     last = {}
+    # single process on the device: the whole step captured as one hipGraph (TrainStep.capture; its
+    # eager warm-up steps count as this harness's warm-up), each timed step = the copy of that step's
+    # batch into the static inputs + one replay.  DDP (world > 1) stays eager.
+    graphed = graph and device != "cpu" and world == 1 and ops is None
+    capture_error = None
+    if graphed:
+        static = [[x.clone() for x in z] if isinstance(z, (list, tuple)) else z.clone() for z in batches[0]]
+        try:
+            step_fn.capture(*static, warmup=max(1, warmup))
+        except RuntimeError as e:  # reported in the line; the step then runs eagerly
+            graphed, capture_error = False, str(e)[:200]
+    if graphed:
+        def step(i):
+            last["stats"] = step_fn.replay(*batches[i % 2])
 
-    def step(i):
-        last["stats"] = step_fn(*batches[i % 2])
+        step(0)
+    else:
+        def step(i):
+            last["stats"] = step_fn(*batches[i % 2])
 
-    for i in range(warmup):
-        step(i)
+        for i in range(warmup):
+            step(i)
     elapsed = timed_steps(step, steps, world, sync, device)
     sps = world * B * steps / elapsed
     ach = sps / world * TRAIN_FLOP_PER_SAMPLE / 1e12  # per GPU
     return {"value": round(sps, 2), "unit": "samples/s", "ms_per_step": round(elapsed / steps * 1e3, 3),
             "batch_per_gpu": B, "steps": steps, "warmup": warmup,
             "parallelism": "ddp%d (RCCL gradient all-reduce)" % world if world > 1 else "single",
+            "step_issue": ("one hipGraph replay per step (whole step captured)" if graphed else
+                           "eager" + (" (capture failed: %s)" % capture_error if capture_error else "")),
             "roofline": {"kernel": "train_step (whole step)", "bound": "mfma", "achieved": round(ach, 2),
                          "peak": PEAK["bf16"], "unit": "TFLOP/s", "frac": float("%.4g" % (ach / PEAK["bf16"])),
                          "flops_per_sample": TRAIN_FLOP_PER_SAMPLE, "traffic": None},
@@ -536,6 +554,8 @@ def main():
     ap.add_argument("--train", action="store_true",
                     help="BASELINE config 4: DDP training step (RCCL gradient all-reduce), --batch pairs per GPU "
                          "(default 16), --steps / --warmup default 20 / 5")
+    ap.add_argument("--train-eager", action="store_true",
+                    help="training step without the whole-step hipGraph (Python-issued kernels; A/B)")
     ap.add_argument("--no-train-line", action="store_true",
                     help="skip the short DDP training measurement (train_step) appended to the inference line")
     args = ap.parse_args()
@@ -579,7 +599,7 @@ def main():
     from mmt_amd.runtime import MixFormerRGBTRuntime
 
     if args.train:
-        res = train_bench(world, rank, args.batch, args.steps, args.warmup)
+        res = train_bench(world, rank, args.batch, args.steps, args.warmup, graph=not args.train_eager)
         if rank == 0:
             out = {"metric": "train samples/s (two-stream MixViT-B RGB-T DDP step, BASELINE config 4)",
                    "value": res["value"], "unit": "samples/s", "n_gpus": world, "steps": args.steps,
@@ -694,7 +714,7 @@ def main():
         del graphs, plans, pool
         torch.cuda.empty_cache()
         try:
-            train_res = train_bench(world, rank, 16, 10, 3)  # 10 timed steps: 5 read one-off stalls
+            train_res = train_bench(world, rank, 16, 10, 3, graph=not args.train_eager)  # 10 timed steps: 5 read one-off stalls
         except Exception as e:  # noqa: BLE001
             train_res = {"error": "%s: %s" % (type(e).__name__, e)}
     else:

@@ -424,6 +424,12 @@ int mmt_transpose_bf16(const void* in, void* out, int rows, int cols, int64_t ld
  * as 1 plus 8 appended output rows, row `cols` = 1.0 over [0, rows) and the rest zero (the ones row of
  * the dW GEMM that also yields the bias gradient) -- the whole padded operand in one launch. */
 
+/* 3x3 / pad-1 im2col of an NHWC bf16 map [B][H][W][C] (C % 8 == 0): out[(b*H + y)*W + x][(ky*3 + kx)*C + c]
+ * = in[b][y+ky-1][x+kx-1][c], zero outside the map -- the implicit-GEMM conv's A layout, materialised for
+ * the corner head's weight gradients in the training step (dW = dY^T im2col(X), one GEMM over pixels;
+ * replaces the autograd of nn.Conv2d 3x3 in lib/models/mixformer_cvt/head.py:7-20). */
+int mmt_im2col3x3_bf16(const void* in, void* out, int B, int H, int W, int C, void* stream);
+
 /* AdamW update with global-norm gradient clipping (torch.nn.utils.clip_grad_norm_
  * + torch.optim.AdamW's fused form over the reference's parameter groups, train_script_mixformer.py:
  * 105-140, base_functions.py:362-400).  Device tables: one entry per fp32 parameter tensor (p, its

@@ -83,3 +83,36 @@ extern "C" int mmt_transpose_bf16(const void* in, void* out, int rows, int cols,
                        rows, cols, ld_in, ld_out, stride_in, stride_out, fill);
     return launch_status();
 }
+
+// 3x3 / pad-1 im2col of an NHWC bf16 map for the corner head's weight-gradient GEMMs (training step):
+// out[(b, y, x)][(ky * 3 + kx) * C + c] = in[b][y + ky - 1][x + kx - 1][c], 0 outside the map -- the A
+// operand layout of the implicit-GEMM conv (k = (ky * 3 + kx) * C + ci), materialised so that
+// dW = dY^T im2col(X) is one GEMM contracting over pixels.  One thread per 16 B (8 channels): coalesced
+// 16-B loads and stores, HBM-bound (9 x the map written, the map read ~9 x from L2).
+namespace {
+__global__ __launch_bounds__(256) void im2col3x3_kernel(const u32x4* __restrict__ in, u32x4* __restrict__ out, int H,
+                                                         int W, int c8, int64_t total) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (pixel, tap, chunk)
+    if (i >= total) return;
+    const int ch = (int)(i % c8);
+    const int64_t pt = i / c8;
+    const int tap = (int)(pt % 9);
+    const int64_t pix = pt / 9;
+    const int x = (int)(pix % W), y = (int)((pix / W) % H);
+    const int64_t b = pix / ((int64_t)W * H);
+    const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
+    u32x4 v = u32x4{0u, 0u, 0u, 0u};
+    if (yy >= 0 && yy < H && xx >= 0 && xx < W) v = in[((b * H + yy) * W + xx) * c8 + ch];
+    out[i] = v;
+}
+}  // namespace
+
+extern "C" int mmt_im2col3x3_bf16(const void* in, void* out, int B, int H, int W, int C, void* stream) {
+    if (!in || !out || B <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 8) return MMT_EBADARG;
+    if (((uintptr_t)in | (uintptr_t)out) & 15) return MMT_EBADARG;
+    const int c8 = C / 8;
+    const int64_t total = (int64_t)B * H * W * 9 * c8;
+    hipLaunchKernelGGL(im2col3x3_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const u32x4*)in, (u32x4*)out, H, W, c8, total);
+    return launch_status();
+}

@@ -69,6 +69,7 @@ _PROTOS = {
     "mmt_mam_attention": [ctypes.POINTER(AttnParams), i32, vp],
     "mmt_mam_attention_bwd": [ctypes.POINTER(AttnBwdParams), i32, vp],
     "mmt_transpose_bf16": [vp, vp, i32, i32, i64, i64, i32, i64, i64, i32, vp],
+    "mmt_im2col3x3_bf16": [vp, vp, i32, i32, i32, i32, vp],
     "mmt_layernorm": [vp, vp, i64, vp, vp, vp, vp, vp, vp, i64, i64, i32, f32, i32, vp],
     "mmt_layernorm_bwd": [vp, vp, i32, vp, vp, vp, vp, i32, vp, i64, i64, i64, i32, f32, vp],
     "mmt_groupnorm": [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, f32, i32, vp],

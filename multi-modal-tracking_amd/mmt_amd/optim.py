@@ -113,9 +113,9 @@ class HipAdamW(torch.optim.Optimizer):
         pkey = [p.data_ptr() for _, p in params]
         if self._key is not None and gkey == self._key[1] and pkey == self._key[0]:
             return
-        if torch.cuda.is_current_stream_capturing():
-            raise RuntimeError("HipAdamW: the parameter / gradient set changed during hipGraph capture "
-                               "(run one eager step first)")
+        capturing = torch.cuda.is_current_stream_capturing()
+        if capturing and (self._key is None or pkey != self._key[0]):
+            raise RuntimeError("HipAdamW: the parameter set changed during hipGraph capture (run one eager step first)")
         for _, p in params:
             if not (p.grad.dtype == torch.float32 and p.grad.is_contiguous() and p.grad.shape == p.shape):
                 raise ValueError("HipAdamW needs contiguous fp32 gradients of the parameter's shape")
@@ -134,8 +134,12 @@ class HipAdamW(torch.optim.Optimizer):
             self._nchunks = len(chunks)
             self._partial = torch.empty(self._nchunks, device=dev)
         self._tab["g"] = np.asarray(gkey, np.uint64)  # only the gradient addresses change between steps
-        # through pinned memory, asynchronously: a pageable copy would hold the host until the stream drains
-        self._tens = torch.from_numpy(self._tab.view(np.uint8).copy()).pin_memory().to(dev, non_blocking=True)
+        # through pinned memory, asynchronously: a pageable copy would hold the host until the stream drains.
+        # Under hipGraph capture (TrainStep.capture) the copy is recorded with this pinned source, which is
+        # kept alive and never rewritten: every replay reproduces the captured gradient addresses (the
+        # graph's private memory pool), so the recorded table stays valid.
+        self._tens_host = torch.from_numpy(self._tab.view(np.uint8).copy()).pin_memory()
+        self._tens = self._tens_host.to(dev, non_blocking=True)
         self.table_writes += 1
         self._device_state(dev)
         self._key = (pkey, gkey)
@@ -144,10 +148,11 @@ class HipAdamW(torch.optim.Optimizer):
     def step(self, max_norm=0.0):
         """clip_grad_norm_(max_norm) (skipped when max_norm <= 0) + one AdamW step: three launches with
         no host synchronisation and no host-side step state.  Capturable in a hipGraph after one eager
-        step only when the gradient addresses stay fixed (set_to_none=False, gradients accumulated in
-        place); with set_to_none=True each step's fresh gradients rewrite the pointer table, which a
-        capture refuses (RuntimeError).  The total gradient norm before clipping is `last_norm` (a device
-        scalar) when max_norm > 0, else None (the norm pass is skipped)."""
+        step (TrainStep.capture): the pointer table write is recorded as a copy from a pinned buffer that
+        stays valid because replays reuse the captured gradient addresses; the learning rates and weight
+        decays are baked into the capture as kernel arguments (recapture after changing them).  The total
+        gradient norm before clipping is `last_norm` (a device scalar) when max_norm > 0, else None (the
+        norm pass is skipped)."""
         from ._lib import check
         params = [(gi, p) for gi, g in enumerate(self.groups) for p in g["params"] if p.grad is not None]
         if not params:

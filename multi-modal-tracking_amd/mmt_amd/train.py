@@ -372,6 +372,74 @@ class _HipGroupNorm(torch.autograd.Function):
         return dx, dgb[0], dgb[1], None, None
 
 
+def _conv_gemm(x, wr, B, H, Cin, Cout, bias=None):
+    """NHWC 3x3 / pad-1 convolution as the implicit-GEMM conv mode of mmt_gemm: y [B*H*H][Cout] bf16 =
+    im2col(x) wr^T (+ bias), x [B][H][H][Cin] bf16 (square maps), wr [Cout][(ky*3 + kx)*Cin + ci] bf16."""
+    from ._lib import LIB, GemmParams, MMT_BF16, check
+    M = B * H * H
+    y = torch.empty(M, Cout, device=x.device, dtype=torch.bfloat16)
+    p = GemmParams()
+    p.a[0], p.w[0], p.c[0] = x.data_ptr(), wr.data_ptr(), y.data_ptr()
+    p.bias[0] = bias.data_ptr() if bias is not None else None
+    p.lda, p.ldc = Cin, Cout
+    p.a_seg_rows, p.a_segs_a = M, 1
+    p.M, p.N, p.K, p.groups = M, Cout, 9 * Cin, 1
+    p.conv_h, p.conv_up, p.conv_cin, p.conv_k3 = H, 1, Cin, 1
+    check(LIB.mmt_gemm(p, MMT_BF16, _stream()), "mmt_gemm (conv)")
+    return y
+
+
+class _HipConv3x3(torch.autograd.Function):
+    """nn.Conv2d(Cin, Cout, 3, padding=1) of the corner head's conv() blocks (lib/models/mixformer_cvt/head.py:
+    7-20) on NHWC bf16 maps, all three products on the LDS-DMA GEMM: the forward and dX as implicit-GEMM
+    convs (dX = the 3x3 conv of dY with the weights flipped and Cin / Cout swapped), dW and the bias
+    gradient as one GEMM over pixels against the im2col of X (mmt_im2col3x3_bf16; `_weight_grads`).  Replaces
+    MIOpen's igemm forward / backward-data / backward-weights kernels, whose backward did not replay
+    correctly from a captured hipGraph."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        B, H, W, Cin = x.shape
+        Cout = w.shape[0]
+        if H != W or Cin % 8 or w.shape[2:] != (3, 3):
+            raise ValueError("HIP conv3x3: square NHWC maps, input channels multiple of 8, 3x3 kernels")
+        Cp = (Cout + 7) // 8 * 8  # output channels padded to the GEMM's N granule (the 48 -> 1 adjust convs)
+        x = x.contiguous()
+        wr = torch.zeros(Cp, 9 * Cin, device=x.device, dtype=torch.bfloat16)
+        wr[:Cout] = w.detach().permute(0, 2, 3, 1).reshape(Cout, 9 * Cin)
+        bp = torch.zeros(Cp, device=x.device, dtype=torch.float32)
+        bp[:Cout] = b.detach()
+        y = _conv_gemm(x, wr, B, H, Cin, Cp, bias=bp)
+        ctx.save_for_backward(x, w)
+        y = y.view(B, H, W, Cp)
+        return y if Cp == Cout else y[..., :Cout]
+
+    @staticmethod
+    def backward(ctx, dy):
+        from ._lib import LIB, check
+        x, w = ctx.saved_tensors
+        B, H, W, Cin = x.shape
+        Cout = w.shape[0]
+        Cp = (Cout + 7) // 8 * 8
+        if Cp != Cout:
+            dyp = torch.zeros(B, H, W, Cp, device=dy.device, dtype=torch.bfloat16)
+            dyp[..., :Cout] = dy
+            dy = dyp
+        else:
+            dy = dy.to(torch.bfloat16).contiguous()
+        dx = None
+        if ctx.needs_input_grad[0]:
+            wt = torch.zeros(Cin, 9, Cp, device=x.device, dtype=torch.bfloat16)
+            wt[:, :, :Cout] = w.detach().flip(2, 3).permute(1, 2, 3, 0).reshape(Cin, 9, Cout)
+            dx = _conv_gemm(dy, wt.view(Cin, 9 * Cp), B, H, Cp, Cin).view(B, H, W, Cin)
+        M = B * H * W
+        col = torch.empty(M, 9 * Cin, device=x.device, dtype=torch.bfloat16)
+        check(LIB.mmt_im2col3x3_bf16(x.data_ptr(), col.data_ptr(), B, H, W, Cin, _stream()), "mmt_im2col3x3_bf16")
+        dw, db = _weight_grads(dy.view(M, Cp), col, M, Cp, 9 * Cin)
+        dw = dw[:Cout].view(Cout, 3, 3, Cin).permute(0, 3, 1, 2).contiguous()
+        return dx, dw, db[:Cout].contiguous()
+
+
 def _adjust_tokens(ops, seq, tok):
     """nn.Sequential(Conv2d 1x1, GroupNorm) of the fusion (fusion_utils.py:252-268) on token rows
     tok [B][P][Cin] -> [B][P][Cout] fp32: the 1x1 conv as ops.linear (HIP GEMM) and ops.group_norm."""
@@ -452,6 +520,11 @@ class HipOps:
     @staticmethod
     def mam_attention_asym(qkv, Bh, n_t, heads):
         return asym_attention_from_mam(HipOps.mam_attention, qkv, Bh, n_t, heads)
+
+    @staticmethod
+    def conv3x3(x, w, b):
+        """The corner head's 3x3 convolutions on NHWC bf16 maps (_HipConv3x3)."""
+        return _HipConv3x3.apply(x, w, b)
 
     @staticmethod
     def ms_deform_attn(value, hw, loc, aw):
@@ -687,8 +760,44 @@ def _soft_argmax(score_map, stride):
     return (coord_x * prob).sum(1), (coord_y * prob).sum(1)
 
 
-def head_forward(hd, x):
-    """Pyramid_Corner_Predictor.forward / get_score_map (head.py:147-212) -> (B, 4) xyxy in [0, 1]."""
+def head_forward_nhwc(hd, x, ops):
+    """head_forward with channels-last maps and the 3x3 convolutions on ops.conv3x3 (HIP): every conv()
+    block = conv (HIP) -> its BatchNorm / SyncBatchNorm / FrozenBatchNorm2d module -> ReLU, the modules
+    called on NCHW-shaped views of the NHWC maps (channels_last strides), so SyncBN's RCCL statistics and
+    the running-stat updates are the modules' own; nearest upsampling, the pyramid adds, the 48 -> 1
+    1x1 convs and the soft-argmax stay PyTorch ops (head.py:147-212)."""
+    nchw = lambda t: t.permute(0, 3, 1, 2)  # noqa: E731
+    nhwc = lambda t: t.permute(0, 2, 3, 1)  # noqa: E731
+
+    def block(seq, t):  # conv(): Conv2d 3x3 + BN + ReLU (head.py:7-20)
+        y = ops.conv3x3(t.contiguous(), seq[0].weight, seq[0].bias)
+        return nhwc(seq[2](seq[1](nchw(y))))
+
+    def c1(mod, t):  # Conv2d(48, 1, 1) on channels-last rows
+        return F.linear(t, mod.weight.view(mod.weight.shape[0], -1), mod.bias)
+
+    def up(t, f):
+        return nhwc(F.interpolate(nchw(t), scale_factor=f))
+
+    xh = nhwc(x).to(torch.bfloat16).contiguous()
+    coords = []
+    for br in ("tl", "br"):
+        g = lambda n: getattr(hd, n + "_" + br)  # noqa: E731
+        x1 = block(g("conv1"), xh)
+        x2 = block(g("conv2"), x1)
+        x3 = block(g("conv3"), up(block(g("adjust1"), xh), 2) + up(x2, 2))
+        x4 = block(g("conv4"), up(block(g("adjust2"), xh), 4) + up(x3, 2))
+        a3, a4 = g("adjust3"), g("adjust4")
+        sm = c1(g("conv5"), x4) + up(block(a3[2], block(a3[1], block(a3[0], x2))), 4) + up(block(a4[1], block(a4[0], x3)), 2)
+        coords += list(_soft_argmax(nchw(sm), hd.stride))
+    return torch.stack(coords, dim=1) / hd.img_sz
+
+
+def head_forward(hd, x, ops=None):
+    """Pyramid_Corner_Predictor.forward / get_score_map (head.py:147-212) -> (B, 4) xyxy in [0, 1].  With ops
+    providing conv3x3 (HipOps) the convolutions run on the HIP GEMM (head_forward_nhwc)."""
+    if getattr(ops, "conv3x3", None) is not None:
+        return head_forward_nhwc(hd, x, ops)
     up = lambda t, f: F.interpolate(t, scale_factor=f)  # noqa: E731
     coords = []
     for br in ("tl", "br"):
@@ -709,7 +818,7 @@ def forward_boxes(net, template, online_template, search, ops):
     s_i = backbone_forward(net.backbone_i, template[1], online_template[1], search[1], ops)
     with torch.autocast(s_v.device.type, dtype=torch.bfloat16, enabled=s_v.device.type == "cuda"):
         fused = fusion_forward(net.fusion_vi, s_v, s_i, ops)
-        xyxy = head_forward(net.box_head, fused)
+        xyxy = head_forward(net.box_head, fused, ops)
     x0, y0, x1, y1 = xyxy.float().unbind(-1)
     return torch.stack([(x0 + x1) / 2, (y0 + y1) / 2, (x1 - x0), (y1 - y0)], -1).view(-1, 1, 4)
 
@@ -737,7 +846,7 @@ def module_forward(net, template, online_template, search, ops, run_score_head=F
                                   "its inference forward runs under eval() / no_grad()" % variant)
     with torch.autocast(s_v.device.type, dtype=torch.bfloat16, enabled=s_v.device.type == "cuda"):
         fused = fusion_forward(net.fusion_vi, s_v, s_i, ops)
-        xyxy = head_forward(net.box_head, fused)
+        xyxy = head_forward(net.box_head, fused, ops)
     x0, y0, x1, y1 = xyxy.float().unbind(-1)
     coord = torch.stack([(x0 + x1) / 2, (y0 + y1) / 2, (x1 - x0), (y1 - y0)], -1).view(-1, 1, 4)
     out = {"pred_boxes": coord}
@@ -872,6 +981,38 @@ class TrainStep:
         stats = self.backward(t, o, s, gt_xywh)
         self.apply()
         return stats
+
+    def capture(self, t, o, s, gt_xywh, warmup=2):
+        """Record the whole step -- forward, loss, backward, clip + AdamW -- as one hipGraph on the static
+        input tensors t / o / s / gt_xywh (single process, HIP ops: every kernel of the step is then
+        libmmt_hip.so's or PyTorch's own, none of MIOpen's convolutions).  `warmup` eager steps on a side
+        stream first (they update the weights like any step).  replay() then runs one step on whatever
+        was copied into the static inputs, with no Python issue cost.  The learning rates and weight decay
+        are those at capture time."""
+        if not self.hip_opt or isinstance(self.model, torch.nn.parallel.DistributedDataParallel):
+            raise RuntimeError("TrainStep.capture: single-process HIP training step only")
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                self(t, o, s, gt_xywh)
+        torch.cuda.current_stream().wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        self.opt.zero_grad(set_to_none=True)
+        with torch.cuda.graph(self.graph):
+            self.graph_stats = self(t, o, s, gt_xywh)
+        self.static_inputs = (t, o, s, gt_xywh)
+        return self.graph_stats
+
+    def replay(self, t=None, o=None, s=None, gt_xywh=None):
+        """One captured step; given inputs are first copied into the static ones (device copies)."""
+        if t is not None:
+            st, so, ss, sg = self.static_inputs
+            for dst, src in zip(st + so + ss, t + o + s):
+                dst.copy_(src)
+            sg.copy_(gt_xywh)
+        self.graph.replay()
+        return self.graph_stats
 
 
 class _Wrapped(torch.nn.Module):

@@ -637,3 +637,78 @@ def test_hip_groupnorm_autograd(B, P, C, groups):
     for name, a, r in zip(("y", "dx", "dgamma", "dbeta"), grads[0], ref):
         err = (a - r).abs().max().item() / max(1.0, r.abs().max().item())
         assert err <= 2e-4, (name, err)
+
+
+@pytest.mark.parametrize("B,H,Cin,Cout", [(2, 20, 768, 384), (2, 40, 192, 96), (1, 80, 96, 48), (2, 40, 48, 1),
+                                          (3, 20, 48, 1)])
+def test_hip_conv3x3_autograd(B, H, Cin, Cout):
+    """HipOps.conv3x3 (_HipConv3x3: implicit-GEMM conv forward and dX, im2col + GEMM dW / db) against
+    F.conv2d autograd in fp32 on the same bf16-rounded input and weights (NHWC in, NHWC out), including
+    the corner head's 48 -> 1 convs (output channels padded to 8 inside).  Relative errors: output 1e-2,
+    dX / dW / db 2e-2 (bf16 operands, bf16 dY)."""
+    import torch.nn.functional as F
+    from mmt_amd.train import HipOps
+    g = torch.Generator().manual_seed(B * H + Cin + Cout)
+    x = torch.randn(B, H, H, Cin, generator=g).bfloat16().float()
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) / (3 * Cin ** 0.5)).bfloat16().float()
+    b = torch.randn(Cout, generator=g)
+    dy = torch.randn(B, H, H, Cout, generator=g).bfloat16().float()
+    xr, wr, br = x.clone().requires_grad_(True), w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    yr = F.conv2d(xr.permute(0, 3, 1, 2), wr, br, padding=1).permute(0, 2, 3, 1)
+    yr.backward(dy)
+    xd = x.bfloat16().cuda().requires_grad_(True)
+    wd, bd = w.cuda().requires_grad_(True), b.cuda().requires_grad_(True)
+    yd = HipOps.conv3x3(xd, wd, bd)
+    yd.backward(dy.bfloat16().cuda())
+    torch.cuda.synchronize()
+    for name, a, r, tol in (("y", yd, yr, 1e-2), ("dx", xd.grad, xr.grad, 2e-2), ("dw", wd.grad, wr.grad, 2e-2),
+                            ("db", bd.grad, br.grad, 2e-2)):
+        a = a.detach().float().cpu()
+        assert a.shape == r.shape, (name, a.shape, r.shape)
+        err = ((a - r).norm() / r.norm()).item()
+        assert err <= tol, (name, err)
+
+
+def test_train_step_graph_replay_matches_eager():
+    """TrainStep.capture / replay (the whole step -- forward on the HIP ops incl. the HIP head convs, box
+    loss, backward, clip + HipAdamW -- as one hipGraph) against the same steps run eagerly from identical
+    weights on the same batches (drop-path and dropout off, BatchNorm in train mode): losses and every
+    parameter within 2e-3 relative after four steps (two eager warm-up steps, then two replays with new
+    batches copied into the static inputs); a third replay changes the weights again (it is not a no-op)."""
+    import copy
+    import mmt_amd.model as M
+    from mmt_amd.train import HipOps, TrainStep, synthetic_batch
+    torch.manual_seed(0)
+    net = M.build_mixformer_vit_rgbt(M.hot_path_cfg(), train=False)
+    net.drop_path_rate = 0.0
+    for m in net.modules():
+        if isinstance(m, torch.nn.Dropout):
+            m.p = 0.0
+    net_b = copy.deepcopy(net)
+    net, net_b = net.cuda().train(), net_b.cuda().train()
+    g = torch.Generator().manual_seed(11)
+    batches = [synthetic_batch(2, "cuda", g) for _ in range(4)]
+    eager, graphed = TrainStep(net, HipOps), TrainStep(net_b, HipOps)
+    le = [float(eager(*b)["loss"]) for b in batches]
+    static = [[x.clone() for x in z] if isinstance(z, list) else z.clone() for z in batches[0]]
+    graphed.capture(*static, warmup=1)  # one eager warm-up step: batch 0 (its static copy)
+    lg = [None]
+    graphed.replay(*batches[1])  # the captured step on batch 1
+    torch.cuda.synchronize()
+    for b in batches[2:]:
+        lg.append(float(graphed.replay(*b)["loss"]))
+        torch.cuda.synchronize()
+    for a, b in zip(le[2:], lg[1:]):
+        assert abs(a - b) <= 2e-3 * max(1.0, abs(a)), (le, lg)
+    bad = []
+    for (n, pa), pb in zip(net.named_parameters(), net_b.parameters()):
+        if pa.requires_grad:
+            err = ((pa - pb).norm() / pa.norm().clamp_min(1e-12)).item()
+            if err > 2e-3:
+                bad.append((n, err))
+    assert not bad, bad[:5]
+    before = [p.detach().clone() for p in net_b.parameters() if p.requires_grad][:4]
+    graphed.replay(*batches[0])
+    torch.cuda.synchronize()
+    after = [p.detach() for p in net_b.parameters() if p.requires_grad][:4]
+    assert any(not torch.equal(a, b) for a, b in zip(before, after))
