@@ -761,17 +761,19 @@ def _soft_argmax(score_map, stride):
 
 
 def head_forward_nhwc(hd, x, ops):
-    """head_forward with channels-last maps and the 3x3 convolutions on ops.conv3x3 (HIP): every conv()
-    block = conv (HIP) -> its BatchNorm / SyncBatchNorm / FrozenBatchNorm2d module -> ReLU, the modules
-    called on NCHW-shaped views of the NHWC maps (channels_last strides), so SyncBN's RCCL statistics and
-    the running-stat updates are the modules' own; nearest upsampling, the pyramid adds, the 48 -> 1
-    1x1 convs and the soft-argmax stay PyTorch ops (head.py:147-212)."""
+    """head_forward with NHWC maps and the 3x3 convolutions on ops.conv3x3 (HIP): every conv() block =
+    conv (HIP) -> its BatchNorm / SyncBatchNorm / FrozenBatchNorm2d module -> ReLU, the modules called on
+    the NCHW map as the reference runs them, so SyncBN's RCCL statistics and the running-stat updates are
+    the modules' own; nearest upsampling, the pyramid adds, the 48 -> 1 1x1 convs and the soft-argmax stay
+    PyTorch ops (head.py:147-212)."""
     nchw = lambda t: t.permute(0, 3, 1, 2)  # noqa: E731
     nhwc = lambda t: t.permute(0, 2, 3, 1)  # noqa: E731
 
     def block(seq, t):  # conv(): Conv2d 3x3 + BN + ReLU (head.py:7-20)
         y = ops.conv3x3(t.contiguous(), seq[0].weight, seq[0].bias)
-        return nhwc(seq[2](seq[1](nchw(y))))
+        # the BN module on a contiguous NCHW map (BatchNorm / SyncBatchNorm as the reference runs them;
+        # MIOpen's batch norm on the channels-last view of a bf16 map crashed in train mode)
+        return nhwc(seq[2](seq[1](nchw(y).contiguous()))).contiguous()
 
     def c1(mod, t):  # Conv2d(48, 1, 1) on channels-last rows
         return F.linear(t, mod.weight.view(mod.weight.shape[0], -1), mod.bias)
