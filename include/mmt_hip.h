@@ -265,7 +265,7 @@ int mmt_groupnorm(const float* in, float* out_f32, void* out_t, const float* gam
  * (instance, group), g = dy * gamma[c]; dgb = fp32 [2][Ctot] (dgamma, dbeta) = sums over instances and
  * positions of dy * xhat and dy (fixed order: bitwise reproducible), added to dgb if dgb_accumulate.
  * ws: >= n_inst * 2 * Ctot floats.  Limits: Ctot / groups a multiple of 4 and <= 256, P * Ctot / groups
- * <= 9600.  The fusion's adjust_v / adjust_i / adjust_cat GroupNorms (fusion_utils.py:252-279). */
+ * <= 24576 (the group's x and dy in registers).  The fusion's adjust_v / adjust_i / adjust_cat GroupNorms (fusion_utils.py:252-279). */
 int mmt_groupnorm_bwd(const float* x, const float* dy, const float* gamma, float* dx, float* dgb, int dgb_accumulate,
                       float* ws, int64_t ws_floats, int n_inst, int P, int Ctot, int groups, float eps, void* stream);
 
@@ -429,6 +429,25 @@ int mmt_transpose_bf16(const void* in, void* out, int rows, int cols, int64_t ld
  * the corner head's weight gradients in the training step (dW = dY^T im2col(X), one GEMM over pixels;
  * replaces the autograd of nn.Conv2d 3x3 in lib/models/mixformer_cvt/head.py:7-20). */
 int mmt_im2col3x3_bf16(const void* in, void* out, int B, int H, int W, int C, void* stream);
+
+/* BatchNorm2d (+ ReLU) of the corner head's conv() blocks in the training step (nn.BatchNorm2d -> nn.ReLU,
+ * lib/models/mixformer_cvt/head.py:7-20) on an NHWC bf16 map x [M = B*H*W][C] (C % 8 == 0, C <= 2048,
+ * 16-B aligned) -> y bf16 [M][C] = relu?((x - mean) * invstd * gamma + beta).  training: batch mean and
+ * biased variance over the M rows (fixed-order sums: bitwise reproducible), and when running_mean /
+ * running_var are given they are updated in place as nn.BatchNorm2d does (momentum, unbiased variance);
+ * else (eval) the running statistics normalise.  save: fp32 [4][C] (mean, invstd, scale, shift), kept
+ * for the backward.  ws: >= mmt_batchnorm_ws_floats(M, C) floats (training only).  gamma / beta may be
+ * NULL (1 / 0). */
+int64_t mmt_batchnorm_ws_floats(int64_t M, int C);
+int mmt_batchnorm_relu(const void* x, void* y, int64_t M, int C, const float* gamma, const float* beta,
+                       float* running_mean, float* running_var, float momentum, float eps, int training, int relu,
+                       float* save, float* ws, int64_t ws_floats, void* stream);
+/* Its backward: dy bf16 [M][C] -> dx bf16 (through the ReLU mask recomputed from x and save), dgb fp32
+ * [2][C] = (dgamma, dbeta) (fixed order).  training: dx = gamma * invstd * (g - mean(g) - xhat *
+ * mean(g * xhat)); eval: gamma * invstd * g.  ws: >= mmt_batchnorm_ws_floats(M, C) floats. */
+int mmt_batchnorm_relu_bwd(const void* x, const void* dy, void* dx, int64_t M, int C, const float* gamma,
+                           const float* save, int training, int relu, float* dgb, float* ws, int64_t ws_floats,
+                           void* stream);
 
 /* AdamW update with global-norm gradient clipping (torch.nn.utils.clip_grad_norm_
  * + torch.optim.AdamW's fused form over the reference's parameter groups, train_script_mixformer.py:

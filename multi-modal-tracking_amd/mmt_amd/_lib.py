@@ -70,6 +70,9 @@ _PROTOS = {
     "mmt_mam_attention_bwd": [ctypes.POINTER(AttnBwdParams), i32, vp],
     "mmt_transpose_bf16": [vp, vp, i32, i32, i64, i64, i32, i64, i64, i32, vp],
     "mmt_im2col3x3_bf16": [vp, vp, i32, i32, i32, i32, vp],
+    "mmt_batchnorm_ws_floats": [i64, i32],
+    "mmt_batchnorm_relu": [vp, vp, i64, i32, vp, vp, vp, vp, f32, f32, i32, i32, vp, vp, i64, vp],
+    "mmt_batchnorm_relu_bwd": [vp, vp, vp, i64, i32, vp, vp, i32, i32, vp, vp, i64, vp],
     "mmt_layernorm": [vp, vp, i64, vp, vp, vp, vp, vp, vp, i64, i64, i32, f32, i32, vp],
     "mmt_layernorm_bwd": [vp, vp, i32, vp, vp, vp, vp, i32, vp, i64, i64, i64, i32, f32, vp],
     "mmt_groupnorm": [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, f32, i32, vp],
@@ -108,6 +111,7 @@ def _load():
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = ctypes.c_int
+    lib.mmt_batchnorm_ws_floats.restype = ctypes.c_int64
     lib.mmt_version.argtypes = []
     lib.mmt_version.restype = ctypes.c_char_p
     return lib

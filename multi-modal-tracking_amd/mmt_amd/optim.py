@@ -89,9 +89,9 @@ class HipAdamW(torch.optim.Optimizer):
             raise ValueError("HipAdamW keeps one step counter for all parameters; the state_dict has %d "
                              "different per-parameter steps" % len(steps))
         dev = next(p for g in self.groups for p in g["params"]).device
-        for p, st in self.state.items():  # moments on the parameter's device, contiguous fp32
-            for k in ("exp_avg", "exp_avg_sq"):
-                st[k] = st[k].to(device=p.device, dtype=torch.float32).contiguous()
+        for p, st in self.state.items():  # own copies of the moments on the parameter's device, contiguous fp32
+            for k in ("exp_avg", "exp_avg_sq"):  # (Optimizer.load_state_dict keeps the source's tensors when
+                st[k] = torch.empty_like(p).copy_(st[k])  # device and dtype match: updated in place here)
         self._device_state(dev).view(torch.int32)[4] = int(steps.pop()) if steps else 0
         self.step_count = int(self._state.view(torch.int32)[4].item())
         self._key = None  # the moment tensors are new: rebuild the device tables at the next step
@@ -135,11 +135,25 @@ class HipAdamW(torch.optim.Optimizer):
             self._partial = torch.empty(self._nchunks, device=dev)
         self._tab["g"] = np.asarray(gkey, np.uint64)  # only the gradient addresses change between steps
         # through pinned memory, asynchronously: a pageable copy would hold the host until the stream drains.
-        # Under hipGraph capture (TrainStep.capture) the copy is recorded with this pinned source, which is
-        # kept alive and never rewritten: every replay reproduces the captured gradient addresses (the
-        # graph's private memory pool), so the recorded table stays valid.
-        self._tens_host = torch.from_numpy(self._tab.view(np.uint8).copy()).pin_memory()
-        self._tens = self._tens_host.to(dev, non_blocking=True)
+        # Eager writes take a fresh pinned buffer (an earlier one may still be in flight) and reserve one
+        # for a capture, because no pinned memory can be allocated while a stream captures.  Under hipGraph
+        # capture (TrainStep.capture) the copy is recorded from that reserved buffer, which is then kept
+        # alive and never rewritten: every replay reproduces the captured gradient addresses (the graph's
+        # private memory pool), so the recorded table stays valid.
+        data = self._tab.view(np.uint8)
+        if capturing:
+            host = getattr(self, "_cap_host", None)
+            if host is None or host.numel() != data.size:
+                raise RuntimeError("HipAdamW: no table buffer reserved for hipGraph capture (run one eager step first)")
+            host.numpy()[:] = data
+            self._captured_hosts = getattr(self, "_captured_hosts", []) + [host]
+            self._cap_host = None
+        else:
+            host = torch.from_numpy(data.copy()).pin_memory()
+            if getattr(self, "_cap_host", None) is None or self._cap_host.numel() != data.size:
+                self._cap_host = torch.empty(data.size, dtype=torch.uint8).pin_memory()
+        self._tens_host = host
+        self._tens = host.to(dev, non_blocking=True)
         self.table_writes += 1
         self._device_state(dev)
         self._key = (pkey, gkey)

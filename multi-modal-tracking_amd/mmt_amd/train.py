@@ -389,6 +389,46 @@ def _conv_gemm(x, wr, B, H, Cin, Cout, bias=None):
     return y
 
 
+class _HipBatchNormReLU(torch.autograd.Function):
+    """nn.BatchNorm2d -> nn.ReLU of a conv() block (head.py:7-20) on an NHWC bf16 map [B][H][W][C]
+    (mmt_batchnorm_relu / _bwd): batch statistics in training (running statistics updated in place with the
+    module's momentum) or the running statistics in eval, affine + ReLU in one pass; the backward recomputes
+    the ReLU mask and x-hat from the saved input and per-channel coefficients."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, training):
+        from ._lib import LIB, check
+        C = x.shape[-1]
+        M = x.numel() // C
+        y = torch.empty_like(x)
+        save = torch.empty(4, C, device=x.device, dtype=torch.float32)
+        nws = int(LIB.mmt_batchnorm_ws_floats(M, C))
+        ws = torch.empty(nws, device=x.device, dtype=torch.float32) if training else None
+        ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+        check(LIB.mmt_batchnorm_relu(x.data_ptr(), y.data_ptr(), M, C, ptr(weight), ptr(bias), ptr(running_mean),
+                                     ptr(running_var), float(momentum), float(eps), int(training), 1, save.data_ptr(),
+                                     ptr(ws), nws if training else 0, _stream()), "mmt_batchnorm_relu")
+        ctx.save_for_backward(x, weight, save)
+        ctx.training, ctx.nws = training, nws
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from ._lib import LIB, check
+        x, weight, save = ctx.saved_tensors
+        C = x.shape[-1]
+        M = x.numel() // C
+        dy = dy.to(torch.bfloat16).contiguous()
+        dx = torch.empty_like(x)
+        dgb = torch.empty(2, C, device=x.device, dtype=torch.float32)
+        ws = torch.empty(ctx.nws, device=x.device, dtype=torch.float32)
+        check(LIB.mmt_batchnorm_relu_bwd(x.data_ptr(), dy.data_ptr(), dx.data_ptr(), M, C,
+                                         weight.data_ptr() if weight is not None else None, save.data_ptr(),
+                                         int(ctx.training), 1, dgb.data_ptr(), ws.data_ptr(), ctx.nws, _stream()),
+              "mmt_batchnorm_relu_bwd")
+        return dx, dgb[0], dgb[1], None, None, None, None, None
+
+
 class _HipConv3x3(torch.autograd.Function):
     """nn.Conv2d(Cin, Cout, 3, padding=1) of the corner head's conv() blocks (lib/models/mixformer_cvt/head.py:
     7-20) on NHWC bf16 maps, all three products on the LDS-DMA GEMM: the forward and dX as implicit-GEMM
@@ -525,6 +565,19 @@ class HipOps:
     def conv3x3(x, w, b):
         """The corner head's 3x3 convolutions on NHWC bf16 maps (_HipConv3x3)."""
         return _HipConv3x3.apply(x, w, b)
+
+    @staticmethod
+    def bn_relu(x, bn):
+        """bn (nn.BatchNorm2d) then ReLU on an NHWC bf16 map (_HipBatchNormReLU), with the module's training /
+        eval semantics: batch statistics when training or not tracking, running statistics updated (and
+        num_batches_tracked advanced) when training and tracking."""
+        training = bn.training or not bn.track_running_stats
+        update = bn.training and bn.track_running_stats
+        if update:
+            bn.num_batches_tracked.add_(1)
+        keep = update or not training
+        return _HipBatchNormReLU.apply(x.contiguous(), bn.weight, bn.bias, bn.running_mean if keep else None,
+                                       bn.running_var if keep else None, bn.momentum, bn.eps, training)
 
     @staticmethod
     def ms_deform_attn(value, hw, loc, aw):
@@ -762,18 +815,25 @@ def _soft_argmax(score_map, stride):
 
 def head_forward_nhwc(hd, x, ops):
     """head_forward with NHWC maps and the 3x3 convolutions on ops.conv3x3 (HIP): every conv() block =
-    conv (HIP) -> its BatchNorm / SyncBatchNorm / FrozenBatchNorm2d module -> ReLU, the modules called on
-    the NCHW map as the reference runs them, so SyncBN's RCCL statistics and the running-stat updates are
-    the modules' own; nearest upsampling, the pyramid adds, the 48 -> 1 1x1 convs and the soft-argmax stay
-    PyTorch ops (head.py:147-212)."""
+    conv (HIP) -> BatchNorm2d + ReLU on ops.bn_relu (HIP, the module's statistics semantics and running-stat
+    updates); SyncBatchNorm (its RCCL statistics), FrozenBatchNorm2d and the 1-channel maps call the modules
+    on the NCHW map as the reference runs them.  Nearest upsampling, the pyramid adds, the 48 -> 1 1x1 convs
+    and the soft-argmax stay PyTorch ops (head.py:147-212)."""
     nchw = lambda t: t.permute(0, 3, 1, 2)  # noqa: E731
     nhwc = lambda t: t.permute(0, 2, 3, 1)  # noqa: E731
 
+    bn_relu = getattr(ops, "bn_relu", None)
+
     def block(seq, t):  # conv(): Conv2d 3x3 + BN + ReLU (head.py:7-20)
         y = ops.conv3x3(t.contiguous(), seq[0].weight, seq[0].bias)
-        # the BN module on a contiguous NCHW map (BatchNorm / SyncBatchNorm as the reference runs them;
-        # MIOpen's batch norm on the channels-last view of a bf16 map crashed in train mode)
-        return nhwc(seq[2](seq[1](nchw(y).contiguous()))).contiguous()
+        bn = seq[1]
+        if (bn_relu is not None and type(bn) is torch.nn.BatchNorm2d and type(seq[2]) is torch.nn.ReLU and
+                bn.momentum is not None and y.shape[-1] % 8 == 0):
+            return bn_relu(y, bn)  # HIP batch norm + ReLU on the NHWC map
+        # other norms (SyncBatchNorm under DDP: its RCCL statistics; FrozenBatchNorm2d) and the 1-channel
+        # maps: the module on a contiguous NCHW map as the reference runs it (MIOpen's batch norm on the
+        # channels-last view of a bf16 map crashed in train mode)
+        return nhwc(seq[2](bn(nchw(y).contiguous()))).contiguous()
 
     def c1(mod, t):  # Conv2d(48, 1, 1) on channels-last rows
         return F.linear(t, mod.weight.view(mod.weight.shape[0], -1), mod.bias)

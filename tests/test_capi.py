@@ -11,7 +11,7 @@ HEADER = os.path.join(ROOT, "include", "mmt_hip.h")
 def declared_symbols():
     src = open(HEADER).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(mmt_\w+)\s*\(", src, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(mmt_\w+)\s*\(", src, flags=re.M)))
 
 
 def test_header_declares_expected_entry_points():

@@ -640,7 +640,9 @@ def test_hip_groupnorm_autograd(B, P, C, groups):
 
 
 @pytest.mark.parametrize("B,H,Cin,Cout", [(2, 20, 768, 384), (2, 40, 192, 96), (1, 80, 96, 48), (2, 40, 48, 1),
-                                          (3, 20, 48, 1)])
+                                          (3, 20, 48, 1), (2, 20, 384, 192), (2, 20, 768, 192), (2, 20, 768, 96),
+                                          (2, 20, 192, 96), (2, 20, 96, 48), (2, 40, 96, 48), (2, 80, 96, 48),
+                                          (2, 20, 48, 1), (16, 20, 768, 384), (16, 80, 96, 48)])
 def test_hip_conv3x3_autograd(B, H, Cin, Cout):
     """HipOps.conv3x3 (_HipConv3x3: implicit-GEMM conv forward and dX, im2col + GEMM dW / db) against
     F.conv2d autograd in fp32 on the same bf16-rounded input and weights (NHWC in, NHWC out), including
@@ -667,6 +669,82 @@ def test_hip_conv3x3_autograd(B, H, Cin, Cout):
         assert a.shape == r.shape, (name, a.shape, r.shape)
         err = ((a - r).norm() / r.norm()).item()
         assert err <= tol, (name, err)
+
+
+@pytest.mark.parametrize("B,H,C,train", [(2, 20, 384, True), (16, 80, 48, True), (3, 40, 96, True), (2, 20, 192, False),
+                                         (1, 7, 8, True)])
+def test_hip_batchnorm_relu(B, H, C, train):
+    """HipOps.bn_relu (mmt_batchnorm_relu / _bwd on NHWC bf16) against nn.BatchNorm2d -> ReLU in fp32 on the same
+    bf16-rounded map: output (1e-2 relative, bf16 storage), the running mean / variance after the update
+    (1e-5 / 1e-4), num_batches_tracked, dX (2e-2) and dgamma / dbeta (1e-3 relative L2; bf16 dY); eval mode
+    normalises with the running statistics.  Bitwise repeatable."""
+    from mmt_amd.train import HipOps
+    g = torch.Generator().manual_seed(B * H + C)
+    x = (torch.randn(B, H, H, C, generator=g) * 2.0 + 0.7).bfloat16().float()
+    dy = torch.randn(B, H, H, C, generator=g).bfloat16().float()
+    ref = torch.nn.BatchNorm2d(C)
+    with torch.no_grad():
+        ref.weight.copy_(torch.rand(C, generator=g) + 0.5)
+        ref.bias.copy_(torch.randn(C, generator=g) * 0.3)
+        ref.running_mean.copy_(torch.randn(C, generator=g) * 0.1)
+        ref.running_var.copy_(torch.rand(C, generator=g) + 0.5)
+    import copy
+    hip = copy.deepcopy(ref).cuda()
+    ref.train(train)
+    hip.train(train)
+    xr = x.clone().requires_grad_(True)
+    yr = torch.relu(ref(xr.permute(0, 3, 1, 2))).permute(0, 2, 3, 1)
+    yr.backward(dy)
+    xd = x.bfloat16().cuda().requires_grad_(True)
+    yd = HipOps.bn_relu(xd, hip)
+    yd.backward(dy.bfloat16().cuda())
+    torch.cuda.synchronize()
+    rel = lambda a, r: ((a.detach().float().cpu() - r).norm() / r.norm().clamp_min(1e-12)).item()  # noqa: E731
+    assert rel(yd, yr.detach()) <= 1e-2
+    assert rel(xd.grad, xr.grad) <= 2e-2
+    assert rel(hip.weight.grad, ref.weight.grad) <= 1e-3 and rel(hip.bias.grad, ref.bias.grad) <= 1e-3
+    assert torch.allclose(hip.running_mean.cpu(), ref.running_mean, rtol=1e-5, atol=1e-6)
+    assert torch.allclose(hip.running_var.cpu(), ref.running_var, rtol=1e-4, atol=1e-6)
+    assert int(hip.num_batches_tracked) == int(ref.num_batches_tracked)
+    y2 = HipOps.bn_relu(xd.detach(), hip.eval())
+    y3 = HipOps.bn_relu(xd.detach(), hip)
+    assert torch.equal(y2, y3)
+
+
+@pytest.mark.parametrize("bn_train", [False, True])
+def test_head_forward_nhwc_matches_aten(bn_train):
+    """The corner head on the HIP convs (head_forward_nhwc, bf16 maps under autocast, as module_forward runs it)
+    against head_forward on aten's fp32 convs (head.py:147-212) for the same module and fused map, B = 2:
+    the normalised corners within 2e-2 and the gradients of the map and of every head parameter within 5e-2
+    relative L2 (BatchNorm in eval mode, or in train mode with its batch statistics)."""
+    import copy
+    import mmt_amd.model as M
+    from mmt_amd.train import HipOps, head_forward
+    torch.manual_seed(3)
+    net = M.build_mixformer_vit_rgbt(M.hot_path_cfg(), train=False)
+    hd = net.box_head.cuda()
+    with torch.no_grad():
+        for br in ("tl", "br"):
+            getattr(hd, "conv5_" + br).weight.mul_(30.0)
+    hd.train(bn_train)
+    hd_ref = copy.deepcopy(hd)
+    x = torch.randn(2, hd.conv1_tl[0].weight.shape[1], 20, 20, device="cuda").bfloat16().float()
+    xr, xh = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    ref = head_forward(hd_ref, xr, None)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out = head_forward(hd, xh, HipOps)
+    out = out.float()
+    wgt = torch.linspace(0.5, 1.5, 8, device="cuda").view(2, 4)
+    (ref * wgt).sum().backward()
+    (out * wgt).sum().backward()
+    torch.cuda.synchronize()
+    assert (out - ref).abs().max().item() <= 2e-2, (out, ref)
+    pairs = [("x", xh.grad, xr.grad)] + [(n, p.grad, q.grad) for (n, p), (_, q) in
+                                        zip(hd.named_parameters(), hd_ref.named_parameters()) if q.grad is not None]
+    for name, a, r in pairs:
+        assert a is not None, name
+        err = ((a.float() - r).norm() / r.norm().clamp_min(1e-12)).item()
+        assert err <= 5e-2, (name, err)
 
 
 def test_train_step_graph_replay_matches_eager():
