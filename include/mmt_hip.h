@@ -431,21 +431,22 @@ int mmt_transpose_bf16(const void* in, void* out, int rows, int cols, int64_t ld
 int mmt_im2col3x3_bf16(const void* in, void* out, int B, int H, int W, int C, void* stream);
 
 /* BatchNorm2d (+ ReLU) of the corner head's conv() blocks in the training step (nn.BatchNorm2d -> nn.ReLU,
- * lib/models/mixformer_cvt/head.py:7-20) on an NHWC bf16 map x [M = B*H*W][C] (C % 8 == 0, C <= 2048,
- * 16-B aligned) -> y bf16 [M][C] = relu?((x - mean) * invstd * gamma + beta).  training: batch mean and
+ * lib/models/mixformer_cvt/head.py:7-20) on an NHWC bf16 map x [M = B*H*W][pitch] with C valid channels
+ * (pitch >= C a multiple of 8, <= 2048, 16-B aligned) -> y bf16 [M][pitch] = relu?((x - mean) * invstd *
+ * gamma + beta), padding channels 0.  training: batch mean and
  * biased variance over the M rows (fixed-order sums: bitwise reproducible), and when running_mean /
  * running_var are given they are updated in place as nn.BatchNorm2d does (momentum, unbiased variance);
  * else (eval) the running statistics normalise.  save: fp32 [4][C] (mean, invstd, scale, shift), kept
  * for the backward.  ws: >= mmt_batchnorm_ws_floats(M, C) floats (training only).  gamma / beta may be
  * NULL (1 / 0). */
 int64_t mmt_batchnorm_ws_floats(int64_t M, int C);
-int mmt_batchnorm_relu(const void* x, void* y, int64_t M, int C, const float* gamma, const float* beta,
+int mmt_batchnorm_relu(const void* x, void* y, int64_t M, int C, int pitch, const float* gamma, const float* beta,
                        float* running_mean, float* running_var, float momentum, float eps, int training, int relu,
                        float* save, float* ws, int64_t ws_floats, void* stream);
-/* Its backward: dy bf16 [M][C] -> dx bf16 (through the ReLU mask recomputed from x and save), dgb fp32
+/* Its backward: dy bf16 [M][pitch] -> dx bf16 [M][pitch] (through the ReLU mask recomputed from x and save), dgb fp32
  * [2][C] = (dgamma, dbeta) (fixed order).  training: dx = gamma * invstd * (g - mean(g) - xhat *
  * mean(g * xhat)); eval: gamma * invstd * g.  ws: >= mmt_batchnorm_ws_floats(M, C) floats. */
-int mmt_batchnorm_relu_bwd(const void* x, const void* dy, void* dx, int64_t M, int C, const float* gamma,
+int mmt_batchnorm_relu_bwd(const void* x, const void* dy, void* dx, int64_t M, int C, int pitch, const float* gamma,
                            const float* save, int training, int relu, float* dgb, float* ws, int64_t ws_floats,
                            void* stream);
 

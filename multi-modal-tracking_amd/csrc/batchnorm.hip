@@ -27,13 +27,14 @@ MMT_DEV void unpack8(const u32x4 u, float* f) {
     }
 }
 
-// Per-workgroup (sum, sum of squares) of x - pivot over its rows: part[blk][2][C].  Thread t owns channel
-// chunk t % C8 (8 channels, one 16-B load per row) and rows t / C8 + k * R of the run (R = 256 / C8); the R
-// row lanes are summed through LDS in lane order.
-__global__ __launch_bounds__(BN_THREADS) void bn_stats_kernel(const u32x4* __restrict__ x, int64_t M, int C,
+// Per-workgroup (sum, sum of squares) of x - pivot over its rows: part[blk][2][C].  Rows are `pitch`
+// channels apart (pitch >= C, a multiple of 8: the 1-channel maps live in 8-channel rows); thread t owns
+// channel chunk t % C8 (8 channels, one 16-B load per row) and rows t / C8 + k * R of the run (R = 256 / C8);
+// the R row lanes are summed through LDS in lane order, channels >= C are never stored.
+__global__ __launch_bounds__(BN_THREADS) void bn_stats_kernel(const u32x4* __restrict__ x, int64_t M, int C, int pitch,
                                                               float* __restrict__ part) {
     __shared__ float red[BN_THREADS * 16];
-    const int C8 = C / 8, R = BN_THREADS / C8, t = threadIdx.x;
+    const int C8 = pitch / 8, R = BN_THREADS / C8, t = threadIdx.x;
     const int ck = t % C8, rl = t / C8;
     int64_t r0, r1;
     bn_rows(M, r0, r1);
@@ -84,7 +85,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_finalize_kernel(const u32x4* __
                 s += (double)part[((int64_t)b * 2) * C + c];
                 q += (double)part[((int64_t)b * 2 + 1) * C + c];
             }
-            const bf16_t* xb = (const bf16_t*)x;
+            const bf16_t* xb = (const bf16_t*)x;  // pivot: row 0
             const double ms = s / (double)M;
             const double vb = fmax(q / (double)M - ms * ms, 0.0);  // biased (normalisation)
             mean = (float)((double)bf2f(xb[c]) + ms);
@@ -107,46 +108,45 @@ __global__ __launch_bounds__(BN_THREADS) void bn_finalize_kernel(const u32x4* __
     }
 }
 
-// y = relu(x * scale + shift) (bf16 out), 8 channels per thread
+// y = relu(x * scale + shift) (bf16 out, padding channels 0), 8 channels per thread
 __global__ __launch_bounds__(BN_THREADS) void bn_apply_kernel(const u32x4* __restrict__ x, u32x4* __restrict__ y, int64_t n8,
-                                                              int C, const float* __restrict__ save, int relu) {
+                                                              int C, int pitch, const float* __restrict__ save, int relu) {
     const int64_t i = (int64_t)blockIdx.x * BN_THREADS + threadIdx.x;
     if (i >= n8) return;
-    const int c0 = (int)(i % (C / 8)) * 8;
-    float v[8];
+    const int c0 = (int)(i % (pitch / 8)) * 8;
+    float v[8], r[8];
     unpack8(x[i], v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int c = c0 + j;
+        float a = c < C ? v[j] * save[2 * C + c] + save[3 * C + c] : 0.f;  // padding channels: 0
+        r[j] = relu ? fmaxf(a, 0.f) : a;
+    }
     u32x4 o;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        float a = v[2 * j] * save[2 * C + c0 + 2 * j] + save[3 * C + c0 + 2 * j];
-        float b = v[2 * j + 1] * save[2 * C + c0 + 2 * j + 1] + save[3 * C + c0 + 2 * j + 1];
-        if (relu) {
-            a = fmaxf(a, 0.f);
-            b = fmaxf(b, 0.f);
-        }
-        o[j] = pack_bf16x2(a, b);
-    }
+    for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(r[2 * j], r[2 * j + 1]);
     y[i] = o;
 }
 
 // Backward partials: g = dy * [x * scale + shift > 0] (the forward's pre-activation, same arithmetic), per
 // workgroup (sum g * xhat, sum g) -> part[blk][2][C] (dgamma, dbeta order)
 __global__ __launch_bounds__(BN_THREADS) void bn_bwd_stats_kernel(const u32x4* __restrict__ x, const u32x4* __restrict__ dy,
-                                                                  int64_t M, int C, const float* __restrict__ save,
+                                                                  int64_t M, int C, int pitch, const float* __restrict__ save,
                                                                   int relu, float* __restrict__ part) {
     __shared__ float red[BN_THREADS * 16];
-    const int C8 = C / 8, R = BN_THREADS / C8, t = threadIdx.x;
+    const int C8 = pitch / 8, R = BN_THREADS / C8, t = threadIdx.x;
     const int ck = t % C8, rl = t / C8, c0 = ck * 8;
     int64_t r0, r1;
     bn_rows(M, r0, r1);
     float sgx[8], sg[8], mean[8], inv[8], sc[8], sh[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < 8; ++j) {  // padding channels (c >= C): zero coefficients, never stored
+        const bool in = c0 + j < C;
         sgx[j] = sg[j] = 0.f;
-        mean[j] = save[c0 + j];
-        inv[j] = save[C + c0 + j];
-        sc[j] = save[2 * C + c0 + j];
-        sh[j] = save[3 * C + c0 + j];
+        mean[j] = in ? save[c0 + j] : 0.f;
+        inv[j] = in ? save[C + c0 + j] : 0.f;
+        sc[j] = in ? save[2 * C + c0 + j] : 0.f;
+        sh[j] = in ? save[3 * C + c0 + j] : 0.f;
     }
     if (rl < R) {
         for (int64_t r = r0 + rl; r < r1; r += R) {
@@ -197,18 +197,22 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_finalize_kernel(const float
 
 // dx = gamma * invstd * (g - mean(g) - xhat * mean(g * xhat)) (training) or gamma * invstd * g (eval), bf16
 __global__ __launch_bounds__(BN_THREADS) void bn_bwd_dx_kernel(const u32x4* __restrict__ x, const u32x4* __restrict__ dy,
-                                                               u32x4* __restrict__ dx, int64_t n8, int C,
+                                                               u32x4* __restrict__ dx, int64_t n8, int C, int pitch,
                                                                const float* __restrict__ save, const float* __restrict__ coef,
                                                                int relu) {
     const int64_t i = (int64_t)blockIdx.x * BN_THREADS + threadIdx.x;
     if (i >= n8) return;
-    const int c0 = (int)(i % (C / 8)) * 8;
+    const int c0 = (int)(i % (pitch / 8)) * 8;
     float v[8], d[8], r[8];
     unpack8(x[i], v);
     unpack8(dy[i], d);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const int c = c0 + j;
+        if (c >= C) {
+            r[j] = 0.f;
+            continue;
+        }
         const float g = (!relu || v[j] * save[2 * C + c] + save[3 * C + c] > 0.f) ? d[j] : 0.f;
         const float xh = (v[j] - save[c]) * save[C + c];
         r[j] = coef[c] * (g - coef[C + c] - xh * coef[2 * C + c]);
@@ -224,47 +228,47 @@ int bn_blocks(int64_t M) {  // ~32+ rows per workgroup, at most 1024 workgroups
     return (int)(nb < 1024 ? nb : 1024);
 }
 
-bool bn_args_ok(const void* x, int64_t M, int C) {
-    return x && M > 0 && C > 0 && C % 8 == 0 && C / 8 <= BN_THREADS && ((uintptr_t)x & 15) == 0;
+bool bn_args_ok(const void* x, int64_t M, int C, int pitch) {
+    return x && M > 0 && C > 0 && pitch >= C && pitch % 8 == 0 && pitch / 8 <= BN_THREADS && ((uintptr_t)x & 15) == 0;
 }
 
 }  // namespace
 
 extern "C" int64_t mmt_batchnorm_ws_floats(int64_t M, int C) { return (int64_t)bn_blocks(M) * 2 * C + 3 * (int64_t)C; }
 
-extern "C" int mmt_batchnorm_relu(const void* x, void* y, int64_t M, int C, const float* gamma, const float* beta,
+extern "C" int mmt_batchnorm_relu(const void* x, void* y, int64_t M, int C, int pitch, const float* gamma, const float* beta,
                                   float* running_mean, float* running_var, float momentum, float eps, int training,
                                   int relu, float* save, float* ws, int64_t ws_floats, void* stream) {
-    if (!bn_args_ok(x, M, C) || !y || ((uintptr_t)y & 15) || !save) return MMT_EBADARG;
+    if (!bn_args_ok(x, M, C, pitch) || !y || ((uintptr_t)y & 15) || !save) return MMT_EBADARG;
     if (!training && (!running_mean || !running_var)) return MMT_EBADARG;
     if ((running_mean == nullptr) != (running_var == nullptr)) return MMT_EBADARG;
     const int nb = bn_blocks(M);
     if (training && (!ws || ws_floats < (int64_t)nb * 2 * C)) return MMT_EBADARG;
     hipStream_t st = (hipStream_t)stream;
     if (training)
-        hipLaunchKernelGGL(bn_stats_kernel, dim3(nb), dim3(BN_THREADS), 0, st, (const u32x4*)x, M, C, ws);
+        hipLaunchKernelGGL(bn_stats_kernel, dim3(nb), dim3(BN_THREADS), 0, st, (const u32x4*)x, M, C, pitch, ws);
     hipLaunchKernelGGL(bn_finalize_kernel, dim3(1), dim3(BN_THREADS), 0, st, (const u32x4*)x, (const float*)ws, nb, M, C,
                        gamma, beta, running_mean, running_var, momentum, eps, training, save);
-    const int64_t n8 = M * (C / 8);
+    const int64_t n8 = M * (pitch / 8);
     hipLaunchKernelGGL(bn_apply_kernel, dim3((unsigned)((n8 + BN_THREADS - 1) / BN_THREADS)), dim3(BN_THREADS), 0, st,
-                       (const u32x4*)x, (u32x4*)y, n8, C, (const float*)save, relu);
+                       (const u32x4*)x, (u32x4*)y, n8, C, pitch, (const float*)save, relu);
     return launch_status();
 }
 
-extern "C" int mmt_batchnorm_relu_bwd(const void* x, const void* dy, void* dx, int64_t M, int C, const float* gamma,
+extern "C" int mmt_batchnorm_relu_bwd(const void* x, const void* dy, void* dx, int64_t M, int C, int pitch, const float* gamma,
                                       const float* save, int training, int relu, float* dgb, float* ws, int64_t ws_floats,
                                       void* stream) {
-    if (!bn_args_ok(x, M, C) || !dy || !dx || ((uintptr_t)dy & 15) || ((uintptr_t)dx & 15) || !save || !dgb) return MMT_EBADARG;
+    if (!bn_args_ok(x, M, C, pitch) || !dy || !dx || ((uintptr_t)dy & 15) || ((uintptr_t)dx & 15) || !save || !dgb) return MMT_EBADARG;
     const int nb = bn_blocks(M);
     if (!ws || ws_floats < mmt_batchnorm_ws_floats(M, C)) return MMT_EBADARG;
     hipStream_t st = (hipStream_t)stream;
     float* coef = ws + (int64_t)nb * 2 * C;
     hipLaunchKernelGGL(bn_bwd_stats_kernel, dim3(nb), dim3(BN_THREADS), 0, st, (const u32x4*)x, (const u32x4*)dy, M, C,
-                       save, relu, ws);
+                       pitch, save, relu, ws);
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(1), dim3(BN_THREADS), 0, st, (const float*)ws, nb, M, C, gamma, save,
                        training, dgb, coef);
-    const int64_t n8 = M * (C / 8);
+    const int64_t n8 = M * (pitch / 8);
     hipLaunchKernelGGL(bn_bwd_dx_kernel, dim3((unsigned)((n8 + BN_THREADS - 1) / BN_THREADS)), dim3(BN_THREADS), 0, st,
-                       (const u32x4*)x, (const u32x4*)dy, (u32x4*)dx, n8, C, save, (const float*)coef, relu);
+                       (const u32x4*)x, (const u32x4*)dy, (u32x4*)dx, n8, C, pitch, save, (const float*)coef, relu);
     return launch_status();
 }

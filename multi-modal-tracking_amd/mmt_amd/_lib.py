@@ -71,8 +71,8 @@ _PROTOS = {
     "mmt_transpose_bf16": [vp, vp, i32, i32, i64, i64, i32, i64, i64, i32, vp],
     "mmt_im2col3x3_bf16": [vp, vp, i32, i32, i32, i32, vp],
     "mmt_batchnorm_ws_floats": [i64, i32],
-    "mmt_batchnorm_relu": [vp, vp, i64, i32, vp, vp, vp, vp, f32, f32, i32, i32, vp, vp, i64, vp],
-    "mmt_batchnorm_relu_bwd": [vp, vp, vp, i64, i32, vp, vp, i32, i32, vp, vp, i64, vp],
+    "mmt_batchnorm_relu": [vp, vp, i64, i32, i32, vp, vp, vp, vp, f32, f32, i32, i32, vp, vp, i64, vp],
+    "mmt_batchnorm_relu_bwd": [vp, vp, vp, i64, i32, i32, vp, vp, i32, i32, vp, vp, i64, vp],
     "mmt_layernorm": [vp, vp, i64, vp, vp, vp, vp, vp, vp, i64, i64, i32, f32, i32, vp],
     "mmt_layernorm_bwd": [vp, vp, i32, vp, vp, vp, vp, i32, vp, i64, i64, i64, i32, f32, vp],
     "mmt_groupnorm": [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, f32, i32, vp],

@@ -396,37 +396,39 @@ class _HipBatchNormReLU(torch.autograd.Function):
     the ReLU mask and x-hat from the saved input and per-channel coefficients."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, training):
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, training, C):
         from ._lib import LIB, check
-        C = x.shape[-1]
-        M = x.numel() // C
+        if x.dtype != torch.bfloat16 or not x.is_contiguous():
+            raise ValueError("HIP batch norm: contiguous NHWC bf16 maps")
+        pitch = x.shape[-1]  # C valid channels of `pitch` (the 1-channel maps are padded to 8)
+        M = x.numel() // pitch
         y = torch.empty_like(x)
         save = torch.empty(4, C, device=x.device, dtype=torch.float32)
         nws = int(LIB.mmt_batchnorm_ws_floats(M, C))
         ws = torch.empty(nws, device=x.device, dtype=torch.float32) if training else None
         ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
-        check(LIB.mmt_batchnorm_relu(x.data_ptr(), y.data_ptr(), M, C, ptr(weight), ptr(bias), ptr(running_mean),
+        check(LIB.mmt_batchnorm_relu(x.data_ptr(), y.data_ptr(), M, C, pitch, ptr(weight), ptr(bias), ptr(running_mean),
                                      ptr(running_var), float(momentum), float(eps), int(training), 1, save.data_ptr(),
                                      ptr(ws), nws if training else 0, _stream()), "mmt_batchnorm_relu")
         ctx.save_for_backward(x, weight, save)
-        ctx.training, ctx.nws = training, nws
+        ctx.training, ctx.nws, ctx.C = training, nws, C
         return y
 
     @staticmethod
     def backward(ctx, dy):
         from ._lib import LIB, check
         x, weight, save = ctx.saved_tensors
-        C = x.shape[-1]
-        M = x.numel() // C
+        C, pitch = ctx.C, x.shape[-1]
+        M = x.numel() // pitch
         dy = dy.to(torch.bfloat16).contiguous()
         dx = torch.empty_like(x)
         dgb = torch.empty(2, C, device=x.device, dtype=torch.float32)
         ws = torch.empty(ctx.nws, device=x.device, dtype=torch.float32)
-        check(LIB.mmt_batchnorm_relu_bwd(x.data_ptr(), dy.data_ptr(), dx.data_ptr(), M, C,
+        check(LIB.mmt_batchnorm_relu_bwd(x.data_ptr(), dy.data_ptr(), dx.data_ptr(), M, C, pitch,
                                          weight.data_ptr() if weight is not None else None, save.data_ptr(),
                                          int(ctx.training), 1, dgb.data_ptr(), ws.data_ptr(), ctx.nws, _stream()),
               "mmt_batchnorm_relu_bwd")
-        return dx, dgb[0], dgb[1], None, None, None, None, None
+        return dx, dgb[0], dgb[1], None, None, None, None, None, None
 
 
 class _HipConv3x3(torch.autograd.Function):
@@ -441,8 +443,8 @@ class _HipConv3x3(torch.autograd.Function):
     def forward(ctx, x, w, b):
         B, H, W, Cin = x.shape
         Cout = w.shape[0]
-        if H != W or Cin % 8 or w.shape[2:] != (3, 3):
-            raise ValueError("HIP conv3x3: square NHWC maps, input channels multiple of 8, 3x3 kernels")
+        if H != W or Cin % 8 or w.shape[2:] != (3, 3) or x.dtype != torch.bfloat16:
+            raise ValueError("HIP conv3x3: square NHWC bf16 maps, input channels multiple of 8, 3x3 kernels")
         Cp = (Cout + 7) // 8 * 8  # output channels padded to the GEMM's N granule (the 48 -> 1 adjust convs)
         x = x.contiguous()
         wr = torch.zeros(Cp, 9 * Cin, device=x.device, dtype=torch.bfloat16)
@@ -563,8 +565,9 @@ class HipOps:
 
     @staticmethod
     def conv3x3(x, w, b):
-        """The corner head's 3x3 convolutions on NHWC bf16 maps (_HipConv3x3)."""
-        return _HipConv3x3.apply(x, w, b)
+        """The corner head's 3x3 convolutions on NHWC maps (_HipConv3x3), operands cast to bf16 (autocast runs
+        the nearest upsampling of the pyramid inputs in fp32)."""
+        return _HipConv3x3.apply(x.to(torch.bfloat16), w, b)
 
     @staticmethod
     def bn_relu(x, bn):
@@ -576,8 +579,13 @@ class HipOps:
         if update:
             bn.num_batches_tracked.add_(1)
         keep = update or not training
-        return _HipBatchNormReLU.apply(x.contiguous(), bn.weight, bn.bias, bn.running_mean if keep else None,
-                                       bn.running_var if keep else None, bn.momentum, bn.eps, training)
+        C = x.shape[-1]
+        x = x.to(torch.bfloat16)
+        if C % 8:  # the 1-channel maps: 8-channel rows, padding channels ignored (autograd slices dy back)
+            x = F.pad(x, (0, (C + 7) // 8 * 8 - C))
+        y = _HipBatchNormReLU.apply(x.contiguous(), bn.weight, bn.bias, bn.running_mean if keep else None,
+                                    bn.running_var if keep else None, bn.momentum, bn.eps, training, C)
+        return y if y.shape[-1] == C else y[..., :C]
 
     @staticmethod
     def ms_deform_attn(value, hw, loc, aw):
@@ -828,11 +836,11 @@ def head_forward_nhwc(hd, x, ops):
         y = ops.conv3x3(t.contiguous(), seq[0].weight, seq[0].bias)
         bn = seq[1]
         if (bn_relu is not None and type(bn) is torch.nn.BatchNorm2d and type(seq[2]) is torch.nn.ReLU and
-                bn.momentum is not None and y.shape[-1] % 8 == 0):
+                bn.momentum is not None):
             return bn_relu(y, bn)  # HIP batch norm + ReLU on the NHWC map
-        # other norms (SyncBatchNorm under DDP: its RCCL statistics; FrozenBatchNorm2d) and the 1-channel
-        # maps: the module on a contiguous NCHW map as the reference runs it (MIOpen's batch norm on the
-        # channels-last view of a bf16 map crashed in train mode)
+        # other norms (SyncBatchNorm under DDP: its RCCL statistics; FrozenBatchNorm2d): the module on a
+        # contiguous NCHW map as the reference runs it (MIOpen's batch norm on the channels-last view of a
+        # bf16 map crashed in train mode)
         return nhwc(seq[2](bn(nchw(y).contiguous()))).contiguous()
 
     def c1(mod, t):  # Conv2d(48, 1, 1) on channels-last rows
@@ -875,9 +883,10 @@ def head_forward(hd, x, ops=None):
 
 def forward_boxes(net, template, online_template, search, ops):
     """MixFormer_RGBT.forward (mixformer.py:366-395) + forward_box_head (:419-432): pred_boxes
-    (B, 1, 4) cxcywh."""
-    s_v = backbone_forward(net.backbone_v, template[0], online_template[0], search[0], ops)
-    s_i = backbone_forward(net.backbone_i, template[1], online_template[1], search[1], ops)
+    (B, 1, 4) cxcywh.  Stochastic depth at the module's drop_path_rate (as module_forward)."""
+    dpr = getattr(net, "drop_path_rate", DROP_PATH_RATE)
+    s_v = backbone_forward(net.backbone_v, template[0], online_template[0], search[0], ops, dpr)
+    s_i = backbone_forward(net.backbone_i, template[1], online_template[1], search[1], ops, dpr)
     with torch.autocast(s_v.device.type, dtype=torch.bfloat16, enabled=s_v.device.type == "cuda"):
         fused = fusion_forward(net.fusion_vi, s_v, s_i, ops)
         xyxy = head_forward(net.box_head, fused, ops)

@@ -421,7 +421,7 @@ def test_hip_adamw_state_dict_resume_and_scheduler():
                              weight_decay=0.01)
     back.load_state_dict(sd)
     for a, b in zip(back.state.values(), opt_ref.state.values()):
-        assert torch.allclose(a["exp_avg"], b["exp_avg"], rtol=1e-5, atol=1e-8)
+        assert torch.allclose(a["exp_avg"], b["exp_avg"], rtol=1e-5, atol=1e-6)  # fma vs torch's lerp
 
 
 
@@ -672,7 +672,7 @@ def test_hip_conv3x3_autograd(B, H, Cin, Cout):
 
 
 @pytest.mark.parametrize("B,H,C,train", [(2, 20, 384, True), (16, 80, 48, True), (3, 40, 96, True), (2, 20, 192, False),
-                                         (1, 7, 8, True)])
+                                         (1, 7, 8, True), (2, 20, 1, True), (16, 40, 1, True), (2, 40, 1, False)])
 def test_hip_batchnorm_relu(B, H, C, train):
     """HipOps.bn_relu (mmt_batchnorm_relu / _bwd on NHWC bf16) against nn.BatchNorm2d -> ReLU in fp32 on the same
     bf16-rounded map: output (1e-2 relative, bf16 storage), the running mean / variance after the update
@@ -713,10 +713,12 @@ def test_hip_batchnorm_relu(B, H, C, train):
 
 @pytest.mark.parametrize("bn_train", [False, True])
 def test_head_forward_nhwc_matches_aten(bn_train):
-    """The corner head on the HIP convs (head_forward_nhwc, bf16 maps under autocast, as module_forward runs it)
-    against head_forward on aten's fp32 convs (head.py:147-212) for the same module and fused map, B = 2:
-    the normalised corners within 2e-2 and the gradients of the map and of every head parameter within 5e-2
-    relative L2 (BatchNorm in eval mode, or in train mode with its batch statistics)."""
+    """The corner head on the HIP convs and batch norm (head_forward_nhwc, bf16 maps under autocast, as
+    module_forward runs it) against head_forward on aten's fp32 convs (head.py:147-212) for the same module and
+    fused map, B = 2, output convs x30 (peaked maps): the normalised corners and the gradients of the map and of
+    every head parameter within max(bar, 1.5 x the distance of aten's own bf16 autocast path from fp32) --
+    corners 2e-2 absolute, gradients 5e-2 relative L2 (BatchNorm in eval mode, or in train mode with its batch
+    statistics)."""
     import copy
     import mmt_amd.model as M
     from mmt_amd.train import HipOps, head_forward
@@ -727,24 +729,30 @@ def test_head_forward_nhwc_matches_aten(bn_train):
         for br in ("tl", "br"):
             getattr(hd, "conv5_" + br).weight.mul_(30.0)
     hd.train(bn_train)
-    hd_ref = copy.deepcopy(hd)
+    heads = [hd, copy.deepcopy(hd), copy.deepcopy(hd)]  # HIP, aten bf16 (autocast), aten fp32
     x = torch.randn(2, hd.conv1_tl[0].weight.shape[1], 20, 20, device="cuda").bfloat16().float()
-    xr, xh = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
-    ref = head_forward(hd_ref, xr, None)
-    with torch.autocast("cuda", dtype=torch.bfloat16):
-        out = head_forward(hd, xh, HipOps)
-    out = out.float()
+    xs = [x.clone().requires_grad_(True) for _ in heads]
     wgt = torch.linspace(0.5, 1.5, 8, device="cuda").view(2, 4)
-    (ref * wgt).sum().backward()
-    (out * wgt).sum().backward()
+    outs = []
+    for h, xi, ops in zip(heads, xs, (HipOps, None, None)):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=h is not heads[2]):
+            out = head_forward(h, xi, ops).float()
+        (out * wgt).sum().backward()
+        outs.append(out.detach())
     torch.cuda.synchronize()
-    assert (out - ref).abs().max().item() <= 2e-2, (out, ref)
-    pairs = [("x", xh.grad, xr.grad)] + [(n, p.grad, q.grad) for (n, p), (_, q) in
-                                        zip(hd.named_parameters(), hd_ref.named_parameters()) if q.grad is not None]
-    for name, a, r in pairs:
+    err = lambda a, r: (a - r).abs().max().item()  # noqa: E731
+    assert err(outs[0], outs[2]) <= max(2e-2, 1.5 * err(outs[1], outs[2])), outs
+    grads = [[xi.grad] + [p.grad for _, p in h.named_parameters()] for h, xi in zip(heads, xs)]
+    names = ["x"] + [n for n, _ in hd.named_parameters()]
+    # gradients that vanish mathematically (biases ahead of a train-mode BatchNorm or of the soft-argmax's
+    # softmax) are rounding noise in every path: measured against the median gradient norm instead of their own
+    floor = torch.tensor([r.norm().item() for r in grads[2] if r is not None]).median().item() * 5e-2
+    rel = lambda a, r: ((a.float() - r).norm() / max(r.norm().item(), floor)).item()  # noqa: E731
+    for name, a, b, r in zip(names, *grads):
+        if r is None:
+            continue
         assert a is not None, name
-        err = ((a.float() - r).norm() / r.norm().clamp_min(1e-12)).item()
-        assert err <= 5e-2, (name, err)
+        assert rel(a, r) <= max(5e-2, 1.5 * rel(b, r)), (name, rel(a, r), rel(b, r))
 
 
 def test_train_step_graph_replay_matches_eager():
