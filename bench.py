@@ -609,7 +609,8 @@ def main():
                    "data": "synthetic LaSOT-shaped pairs (N(0,1) images, random boxes), random-init weights",
                    "config": {"workload": "mixformer_vit_rgbt ViT-B 128/320 DDP train step, %d pairs/GPU" % args.batch,
                               "batch_per_gpu": args.batch, "parallelism": res["parallelism"]},
-                   "roofline": res["roofline"], "cpu_baseline": None, "last_loss": res["last_loss"]}
+                   "roofline": res["roofline"], "cpu_baseline": None, "last_loss": res["last_loss"],
+                   "step_issue": res["step_issue"]}
             print(json.dumps(out), flush=True)
         if world > 1:
             dist.barrier()

@@ -74,7 +74,9 @@ extern "C" {
  * A addressing (conv mode, conv_h > 0): NHWC implicit im2col of a 3x3/pad-1 (conv_k3=1) or 1x1
  *   conv producing a conv_h x conv_h map; the input map is conv_h/conv_up square, pixel stride
  *   lda (channels are contiguous, conv_cin of them), k = (ky*3+kx)*conv_cin + ci; consecutive
- *   input images a_stride_a pixels apart (0: packed, (conv_h/conv_up)^2).
+ *   input images a_stride_a pixels apart (0: packed, (conv_h/conv_up)^2).  conv_k3=2: the 3x3 taps
+ *   read in reverse order (input pixel (y+1-ky, x+1-kx)), i.e. the convolution with the flipped
+ *   kernel -- the data gradient of a 3x3 conv from its unflipped weights [Cin][ky][kx][Cout].
  * Epilogue: v = act(acc + bias) with act 0 none / 1 GELU(erf) / 2 ReLU / 5 GELU backward:
  *   v = (acc + bias) * GELU'(R) (R then not added; 16-bit LDS-DMA kernels);
  *   c2 == NULL: C = v (+ R if r != NULL);  c2 != NULL: C = v, C2 = v + R (c2_copy 1: C = v (+ R),

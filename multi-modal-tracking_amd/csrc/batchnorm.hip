@@ -68,44 +68,67 @@ __global__ __launch_bounds__(BN_THREADS) void bn_stats_kernel(const u32x4* __res
     }
 }
 
-// One workgroup: the batch mean / variance from the partials (workgroups in order, double), the running
-// statistics update (momentum, unbiased variance as nn.BatchNorm2d), and the per-channel coefficients
-// save[4][C] = (mean, invstd, scale = gamma * invstd, shift = beta - mean * scale).  Eval (training = 0):
-// the running statistics give mean / invstd.
+// The batch mean / variance from the partials, the running statistics update (momentum, unbiased variance
+// as nn.BatchNorm2d), and the per-channel coefficients save[4][C] = (mean, invstd, scale = gamma * invstd,
+// shift = beta - mean * scale); eval (training = 0): the running statistics give mean / invstd.  A
+// workgroup serves 32 channels: lane l of channel c sums the workgroup partials l, l + 8, ... in double,
+// then the 8 lanes are added in order (fixed order: bitwise reproducible).
+constexpr int BN_FCH = 32, BN_FLANES = BN_THREADS / BN_FCH;
+
+MMT_DEV void bn_lane_sums(const float* __restrict__ part, int nblk, int C, int c, int lane, double* red, double& a,
+                          double& b) {
+    double s = 0.0, q = 0.0;
+    if (c < C) {
+        for (int k = lane; k < nblk; k += BN_FLANES) {
+            s += (double)part[((int64_t)k * 2) * C + c];
+            q += (double)part[((int64_t)k * 2 + 1) * C + c];
+        }
+    }
+    const int t = threadIdx.x;
+    red[t] = s;
+    red[BN_THREADS + t] = q;
+    __syncthreads();
+    a = b = 0.0;
+    if (lane == 0) {
+        for (int l = 0; l < BN_FLANES; ++l) {
+            a += red[l * BN_FCH + t];
+            b += red[BN_THREADS + l * BN_FCH + t];
+        }
+    }
+}
+
 __global__ __launch_bounds__(BN_THREADS) void bn_finalize_kernel(const u32x4* __restrict__ x, const float* __restrict__ part,
                                                                  int nblk, int64_t M, int C, const float* __restrict__ gamma,
                                                                  const float* __restrict__ beta, float* running_mean,
                                                                  float* running_var, float momentum, float eps,
                                                                  int training, float* __restrict__ save) {
-    for (int c = threadIdx.x; c < C; c += BN_THREADS) {
-        float mean, var;
-        if (training) {
-            double s = 0.0, q = 0.0;
-            for (int b = 0; b < nblk; ++b) {
-                s += (double)part[((int64_t)b * 2) * C + c];
-                q += (double)part[((int64_t)b * 2 + 1) * C + c];
-            }
-            const bf16_t* xb = (const bf16_t*)x;  // pivot: row 0
-            const double ms = s / (double)M;
-            const double vb = fmax(q / (double)M - ms * ms, 0.0);  // biased (normalisation)
-            mean = (float)((double)bf2f(xb[c]) + ms);
-            var = (float)vb;
-            if (running_mean) {
-                running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
-                const double vu = M > 1 ? vb * (double)M / (double)(M - 1) : vb;  // unbiased (running)
-                running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)vu;
-            }
-        } else {
-            mean = running_mean[c];
-            var = running_var[c];
+    __shared__ double red[2 * BN_THREADS];
+    const int lane = threadIdx.x / BN_FCH, c = blockIdx.x * BN_FCH + threadIdx.x % BN_FCH;
+    double s = 0.0, q = 0.0;
+    if (training) bn_lane_sums(part, nblk, C, c, lane, red, s, q);
+    if (lane != 0 || c >= C) return;
+    float mean, var;
+    if (training) {
+        const bf16_t* xb = (const bf16_t*)x;  // pivot: row 0
+        const double ms = s / (double)M;
+        const double vb = fmax(q / (double)M - ms * ms, 0.0);  // biased (normalisation)
+        mean = (float)((double)bf2f(xb[c]) + ms);
+        var = (float)vb;
+        if (running_mean) {
+            running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
+            const double vu = M > 1 ? vb * (double)M / (double)(M - 1) : vb;  // unbiased (running)
+            running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)vu;
         }
-        const float inv = 1.f / sqrtf(var + eps);
-        const float sc = (gamma ? gamma[c] : 1.f) * inv;
-        save[c] = mean;
-        save[C + c] = inv;
-        save[2 * C + c] = sc;
-        save[3 * C + c] = (beta ? beta[c] : 0.f) - mean * sc;
+    } else {
+        mean = running_mean[c];
+        var = running_var[c];
     }
+    const float inv = 1.f / sqrtf(var + eps);
+    const float sc = (gamma ? gamma[c] : 1.f) * inv;
+    save[c] = mean;
+    save[C + c] = inv;
+    save[2 * C + c] = sc;
+    save[3 * C + c] = (beta ? beta[c] : 0.f) - mean * sc;
 }
 
 // y = relu(x * scale + shift) (bf16 out, padding channels 0), 8 channels per thread
@@ -175,24 +198,22 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_stats_kernel(const u32x4* _
     }
 }
 
-// dgb[2][C] = (dgamma, dbeta) summed over the workgroups in order (double), and the dx coefficients
+// dgb[2][C] = (dgamma, dbeta) summed over the workgroups (bn_lane_sums order), and the dx coefficients
 // coef[3][C] = (gamma * invstd, dbeta / M, dgamma / M) (training) or (gamma * invstd, 0, 0) (eval)
 __global__ __launch_bounds__(BN_THREADS) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int64_t M,
                                                                      int C, const float* __restrict__ gamma,
                                                                      const float* __restrict__ save, int training,
                                                                      float* __restrict__ dgb, float* __restrict__ coef) {
-    for (int c = threadIdx.x; c < C; c += BN_THREADS) {
-        double a = 0.0, b = 0.0;
-        for (int k = 0; k < nblk; ++k) {
-            a += (double)part[((int64_t)k * 2) * C + c];
-            b += (double)part[((int64_t)k * 2 + 1) * C + c];
-        }
-        dgb[c] = (float)a;
-        dgb[C + c] = (float)b;
-        coef[c] = (gamma ? gamma[c] : 1.f) * save[C + c];
-        coef[C + c] = training ? (float)(b / (double)M) : 0.f;
-        coef[2 * C + c] = training ? (float)(a / (double)M) : 0.f;
-    }
+    __shared__ double red[2 * BN_THREADS];
+    const int lane = threadIdx.x / BN_FCH, c = blockIdx.x * BN_FCH + threadIdx.x % BN_FCH;
+    double a, b;
+    bn_lane_sums(part, nblk, C, c, lane, red, a, b);
+    if (lane != 0 || c >= C) return;
+    dgb[c] = (float)a;
+    dgb[C + c] = (float)b;
+    coef[c] = (gamma ? gamma[c] : 1.f) * save[C + c];
+    coef[C + c] = training ? (float)(b / (double)M) : 0.f;
+    coef[2 * C + c] = training ? (float)(a / (double)M) : 0.f;
 }
 
 // dx = gamma * invstd * (g - mean(g) - xhat * mean(g * xhat)) (training) or gamma * invstd * g (eval), bf16
@@ -223,9 +244,9 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_dx_kernel(const u32x4* __re
     dx[i] = o;
 }
 
-int bn_blocks(int64_t M) {  // ~32+ rows per workgroup, at most 1024 workgroups
+int bn_blocks(int64_t M) {  // ~32+ rows per workgroup, at most 256 workgroups (one per CU)
     const int64_t nb = (M + 31) / 32;
-    return (int)(nb < 1024 ? nb : 1024);
+    return (int)(nb < 256 ? nb : 256);
 }
 
 bool bn_args_ok(const void* x, int64_t M, int C, int pitch) {
@@ -247,7 +268,7 @@ extern "C" int mmt_batchnorm_relu(const void* x, void* y, int64_t M, int C, int 
     hipStream_t st = (hipStream_t)stream;
     if (training)
         hipLaunchKernelGGL(bn_stats_kernel, dim3(nb), dim3(BN_THREADS), 0, st, (const u32x4*)x, M, C, pitch, ws);
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3(1), dim3(BN_THREADS), 0, st, (const u32x4*)x, (const float*)ws, nb, M, C,
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + BN_FCH - 1) / BN_FCH), dim3(BN_THREADS), 0, st, (const u32x4*)x, (const float*)ws, nb, M, C,
                        gamma, beta, running_mean, running_var, momentum, eps, training, save);
     const int64_t n8 = M * (pitch / 8);
     hipLaunchKernelGGL(bn_apply_kernel, dim3((unsigned)((n8 + BN_THREADS - 1) / BN_THREADS)), dim3(BN_THREADS), 0, st,
@@ -265,7 +286,7 @@ extern "C" int mmt_batchnorm_relu_bwd(const void* x, const void* dy, void* dx, i
     float* coef = ws + (int64_t)nb * 2 * C;
     hipLaunchKernelGGL(bn_bwd_stats_kernel, dim3(nb), dim3(BN_THREADS), 0, st, (const u32x4*)x, (const u32x4*)dy, M, C,
                        pitch, save, relu, ws);
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(1), dim3(BN_THREADS), 0, st, (const float*)ws, nb, M, C, gamma, save,
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + BN_FCH - 1) / BN_FCH), dim3(BN_THREADS), 0, st, (const float*)ws, nb, M, C, gamma, save,
                        training, dgb, coef);
     const int64_t n8 = M * (pitch / 8);
     hipLaunchKernelGGL(bn_bwd_dx_kernel, dim3((unsigned)((n8 + BN_THREADS - 1) / BN_THREADS)), dim3(BN_THREADS), 0, st,

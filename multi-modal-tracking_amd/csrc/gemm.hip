@@ -95,8 +95,9 @@ __global__ __launch_bounds__(256 * KS) void gemm_kernel(const mmt_gemm_params p)
         const int k_ = kin_ ? kraw_ : 0;                                                                 \
         int iyd_ = 0, ixd_ = 0, ci_ = k_;                                                                \
         if (CONV && p.conv_k3) {                                                                         \
-            const int tap_ = k_ / p.conv_cin;                                                            \
+            int tap_ = k_ / p.conv_cin;                                                                  \
             ci_ = k_ - tap_ * p.conv_cin;                                                                \
+            if (p.conv_k3 == 2) tap_ = 8 - tap_; /* flipped taps */                                      \
             iyd_ = tap_ / 3 - 1;                                                                         \
             ixd_ = tap_ % 3 - 1;                                                                         \
         }                                                                                                \
@@ -330,7 +331,7 @@ int check_gemm(const mmt_gemm_params& p) {
     if (p.K % EPC || p.lda % EPC) return MMT_EBADARG;
     if (p.conv_h > 0) {
         if (p.conv_cin % EPC || p.conv_up < 1 || p.conv_h % p.conv_up) return MMT_EBADARG;
-        if (p.K != (p.conv_k3 ? 9 : 1) * p.conv_cin) return MMT_EBADARG;
+        if (p.conv_k3 < 0 || p.conv_k3 > 2 || p.K != (p.conv_k3 ? 9 : 1) * p.conv_cin) return MMT_EBADARG;
         if (p.M % (p.conv_h * p.conv_h)) return MMT_EBADARG;
     } else {
         if (p.a_seg_rows <= 0 || p.a_segs_a <= 0) return MMT_EBADARG;

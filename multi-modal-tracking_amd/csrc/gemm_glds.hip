@@ -221,12 +221,13 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
             // from an integer), the upsample factor is a power of two (shift), and the element
             // offset fits 32 bits (both checked by the launcher).
             int dy = 0, dx = 0, ci = k;
-            if (k3) {  // k = (ky*3 + kx)*cin + ci
+            if (k3) {  // k = (ky*3 + kx)*cin + ci; k3 == 2: the taps in reverse order (the flipped kernel)
                 const uint32_t tap = (uint32_t)(((float)k + 0.5f) * inv_cin);
                 ci = k - (int)tap * cin;
-                const int ty = (int)(tap / 3u);
+                const uint32_t tf = k3 == 2 ? 8u - tap : tap;
+                const int ty = (int)(tf / 3u);
                 dy = ty - 1;
-                dx = (int)tap - ty * 3 - 1;
+                dx = (int)tf - ty * 3 - 1;
             }
 #pragma unroll
             for (int i = 0; i < PA; ++i) {

