@@ -715,9 +715,9 @@ def test_hip_batchnorm_relu(B, H, C, train):
 def test_head_forward_nhwc_matches_aten(bn_train):
     """The corner head on the HIP convs and batch norm (head_forward_nhwc, bf16 maps under autocast, as
     module_forward runs it) against head_forward on aten's fp32 convs (head.py:147-212) for the same module and
-    fused map, B = 2, output convs x30 (peaked maps): the normalised corners within max(2e-2, 1.5 x) and the
-    gradients of the map and of every head parameter within max(5e-2, 2 x) the distance of aten's own bf16
-    autocast path from fp32 --
+    fused map, B = 2, output convs x30 (peaked maps): the normalised corners within max(2e-2, 1.5 x), the
+    gradients of the map and of every head parameter within max(5e-2, 3 x) and all head parameter gradients
+    together within max(5e-2, 1.5 x) the distance of aten's own bf16 autocast path from fp32 --
     corners absolute, gradients relative L2 (BatchNorm in eval mode, or in train mode with its batch
     statistics)."""
     import copy
@@ -753,7 +753,10 @@ def test_head_forward_nhwc_matches_aten(bn_train):
         if r is None:
             continue
         assert a is not None, name
-        assert rel(a, r) <= max(5e-2, 2.0 * rel(b, r)), (name, rel(a, r), rel(b, r))
+        assert rel(a, r) <= max(5e-2, 3.0 * rel(b, r)), (name, rel(a, r), rel(b, r))
+    # all head parameters as one vector (as test_module_forward_training_gpu_grads' groups)
+    cat = [torch.cat([g.flatten().float() for g, r in zip(gs[1:], grads[2][1:]) if r is not None]) for gs in grads]
+    assert rel(cat[0], cat[2]) <= max(5e-2, 1.5 * rel(cat[1], cat[2])), (rel(cat[0], cat[2]), rel(cat[1], cat[2]))
 
 
 def test_train_step_graph_replay_matches_eager():
