@@ -766,8 +766,9 @@ def test_train_step_graph_replay_matches_eager():
     """TrainStep.capture / replay (the whole step -- forward on the HIP ops incl. the HIP head convs, box
     loss, backward, clip + HipAdamW -- as one hipGraph) against the same steps run eagerly from identical
     weights on the same batches (drop-path and dropout off, BatchNorm in train mode): losses and every
-    parameter within max(2e-3 relative, 3 x the spread between two eager runs -- the MSDA backward's atomics)
-    after four steps (two eager warm-up steps, then two replays with new
+    parameter within max(2e-3 relative, 3 x the spread between two eager runs -- the MSDA backward's atomics --,
+    one AdamW step's size: noise-level gradients such as a 1-channel map's BatchNorm bias flip their update's
+    sign) after four steps (two eager warm-up steps, then two replays with new
     batches copied into the static inputs); a third replay changes the weights again (it is not a no-op)."""
     import copy
     import mmt_amd.model as M
@@ -798,12 +799,12 @@ def test_train_step_graph_replay_matches_eager():
     for a, b in zip(le[2:], lg[1:]):
         assert abs(a - b) <= max(2e-3 * max(1.0, abs(a)), 3 * spread), (le, le2, lg)
     bad = []
+    lr = 1e-4  # TrainStep's default: one AdamW update moves an element by about lr whatever its gradient's size
     for (n, pa), pb, pc in zip(net.named_parameters(), net_b.parameters(), net_c.parameters()):
         if pa.requires_grad:
-            err = ((pa - pb).norm() / pa.norm().clamp_min(1e-12)).item()
-            pspread = ((pa - pc).norm() / pa.norm().clamp_min(1e-12)).item()
-            if err > max(2e-3, 3 * pspread):
-                bad.append((n, err, pspread))
+            err, pspread = (pa - pb).norm().item(), (pa - pc).norm().item()
+            if err > max(2e-3 * pa.norm().item(), 3 * pspread, lr * pa.numel() ** 0.5):
+                bad.append((n, err, pspread, pa.norm().item()))
     assert not bad, bad[:5]
     before = [p.detach().clone() for p in net_b.parameters() if p.requires_grad][:4]
     graphed.replay(*batches[0])
