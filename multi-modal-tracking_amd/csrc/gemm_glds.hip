@@ -24,7 +24,8 @@
 
 #include <algorithm>
 
-// MMT_GEMM_ABLATE (measurement builds only, tools/build_ablate.sh): 1 = no DMA after the prologue
+// MMT_GEMM_ABLATE (measurement builds only, tools/build_ablate.sh): 3 = no epilogue C / C2 stores,
+// 4 = no epilogue tile reads (constants instead); 1 = no DMA after the prologue
 // (MFMA + LDS reads + barriers alone), 2 = no MFMA work (DMA pipeline alone).
 #ifndef MMT_GEMM_ABLATE
 #define MMT_GEMM_ABLATE 0
@@ -103,7 +104,12 @@ MMT_DEV int gemm_trsw(int k) { return 2 * ((k & 3) | (((k >> 3) & 1) << 2)); }
 // (mmt_gemm_params.ln_fold): the row statistics of A are accumulated from the A fragments the
 // waves already hold for the MFMAs (wave column wc sums fragment rows mt = wc, wc + WGN, ...), so
 // the normalised operand never exists in memory and the LayerNorm launch disappears.
-template <typename T, int BM, int BN, int WGM, int WGN, int KS, int ST, bool CONV, int LNM, int OCC = 1, bool RS = false>
+// EPI 1: the compact epilogue of a 16-bit C with bias / LayerNorm fold / ReLU or GELU only (no residual, C2,
+// statistics, row map or row scale; the launcher checks): the general epilogue's branches for every other mode
+// made the strip passes ~44 KiB of code per kernel, fetched cold by every workgroup (per-phase stamps: qkv
+// passes 1.96 -> 0.68 us, fc1 2.90 -> 1.63 us with this form, profiles/r04_gemm_epilogue_stamps.jsonl).
+template <typename T, int BM, int BN, int WGM, int WGN, int KS, int ST, bool CONV, int LNM, int OCC = 1, bool RS = false,
+          int EPI = 0>
 MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int tile, const int slice, const int nsk,
                             const int ntiles) {
     constexpr int NW = WGM * WGN, TPG = 64 * NW;  // waves / threads per k-group
@@ -635,6 +641,45 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
     const int64_t csr = p.c_seg_rows > 0 ? p.c_seg_rows : INT64_MAX, csp = p.c_seg_pitch;
     auto crow = [&](int m) -> int64_t { return csr == INT64_MAX ? (int64_t)m : (m / csr) * csp + m % csr; };
     constexpr int PG = NPASS < 4 ? NPASS : 4;  // passes whose residual loads are in flight together
+    if constexpr (EPI == 1) {
+        static_assert(EPASS == 1 && !RS, "compact epilogue: single-pass tiles");
+#pragma unroll
+        for (int i = 0; i < NPASS; ++i) {
+            const int r = tr + i * RPP, m = m0_tile + r;
+            f32x4 va = *(const f32x4*)(ctile + r * TP + tc);
+            f32x4 vb = *(const f32x4*)(ctile + r * TP + tc + 4);
+            if constexpr (LNF) {  // as the general path
+                float sx = 0.f, sxx = 0.f;
+                constexpr int NQ = LNM == 1 ? KS : 1;
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    sx += rstat[(q * BM + r) * 2];
+                    sxx += rstat[(q * BM + r) * 2 + 1];
+                }
+                const float mu = sx * inv_k, var = fmaxf(sxx * inv_k - mu * mu, 0.f);
+                const float rstd = rsqrtf(var + p.ln_eps);
+                va = (va - mu * cs0) * rstd;
+                vb = (vb - mu * cs1) * rstd;
+            }
+            va += bn0;
+            vb += bn1;
+            if (p.act == 1) {
+                va.xy = gelu_erf2(va.xy);
+                va.zw = gelu_erf2(va.zw);
+                vb.xy = gelu_erf2(vb.xy);
+                vb.zw = gelu_erf2(vb.zw);
+            } else if (p.act == 2) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    va[j] = fmaxf(va[j], 0.f);
+                    vb[j] = fmaxf(vb[j], 0.f);
+                }
+            }
+            if (m < M && n < N)
+                *(u32x4*)((T*)C + (int64_t)m * p.ldc + n) = u32x4{pack2<T>(va[0], va[1]), pack2<T>(va[2], va[3]),
+                                                               pack2<T>(vb[0], vb[1]), pack2<T>(vb[2], vb[3])};
+        }
+    } else
     for (int ep = 0; ep < EPASS; ++ep) {
     if (ep > 0) {  // the next wave row's accumulators into the (re-used) tile image
         lds_barrier();
@@ -668,6 +713,7 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
             const int r = tr + (p0 + i) * RPP, m = m0 + r;
             f32x4 va = *(const f32x4*)(ctile + r * TP + tc);
             f32x4 vb = *(const f32x4*)(ctile + r * TP + tc + 4);
+            if (MMT_GEMM_ABLATE == 4) va = vb = f32x4{(float)r, (float)tc, 0.f, 1.f};  // measurement: no tile reads
             if constexpr (LNF) {  // Linear(LayerNorm(x)) = rstd * (x.W' - mu * colsum(W')) + b'
                 float sx = 0.f, sxx = 0.f;
                 constexpr int NQ = LNM == 1 ? KS : 1;  // LNM 2: one (sum, sum x^2) pair per row
@@ -727,7 +773,7 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
                 if ((tc & 63) == 0 && m < M && n < N)
                     *(f32x2*)(stats_out + (crow(m) * (N / 64) + n / 64) * 2) = f32x2{ps, pq};
             }
-            if (m < M && n < N) {
+            if (m < M && n < N && (MMT_GEMM_ABLATE != 3 || oa[0] == -1.2345e30f)) {  // (3: measurement, no stores)
                 const int64_t e = crow(m) * p.ldc + n, es = colsplit ? crow(m) * 8 : e;
                 if (p.c_f32) {
                     *(f32x4*)((float*)Cs + es) = oa;
@@ -776,7 +822,7 @@ MMT_DEV int gemm_xcd_lin() {
 }
 
 // One GEMM: grid (tiles, split-K slices, groups); linear ids (group, tile, slice), slice fastest.
-template <typename T, int BM, int BN, int WGM, int WGN, int KS, int ST, bool CONV, int LNM>
+template <typename T, int BM, int BN, int WGM, int WGN, int KS, int ST, bool CONV, int LNM, int EPI = 0>
 __global__ __launch_bounds__(64 * WGM * WGN * KS)
     __attribute__((amdgpu_waves_per_eu(WGM * WGN * KS / 4, WGM * WGN * KS / 4))) void gemm_glds_kernel(
         const mmt_gemm_params p) {
@@ -785,7 +831,7 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
     const int per_g = gridDim.x * nsk;
     const int g = lin / per_g, rem_t = lin - g * per_g;
     const int tile = rem_t / nsk, slice = rem_t - tile * nsk;
-    gemm_glds_tile<T, BM, BN, WGM, WGN, KS, ST, CONV, LNM>(p, g, tile, slice, nsk, gridDim.x);
+    gemm_glds_tile<T, BM, BN, WGM, WGN, KS, ST, CONV, LNM, 1, false, EPI>(p, g, tile, slice, nsk, gridDim.x);
 }
 
 // The same tile at two workgroups per CU (impl 8: 128x128, 8 waves, 2-slot ring = 64 KiB of LDS, <= 128
@@ -839,10 +885,25 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
     gemm_glds_tile<T, BM, BN, WGM, WGN, KS, ST, CONV, 0>(a.p[i], g, loc - g * nt, 0, 1, nt);
 }
 
+// Whether the compact 16-bit epilogue (EPI 1) covers the GEMM's epilogue.
+bool compact_epilogue(const mmt_gemm_params& p) {
+    if (p.c_f32 || p.c2_copy || p.c_seg_rows || p.row_scale || p.act < 0 || p.act > 2) return false;
+    for (int g = 0; g < p.groups; ++g)
+        if (p.r[g] || p.c2[g] || p.ln_stats_out[g]) return false;
+    return true;
+}
+
 template <typename T, int BM, int BN, int WGM, int WGN, int KS, int ST>
 void launch(const mmt_gemm_params& p, int nsk, hipStream_t st) {
     const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
     const dim3 grid(tiles, nsk, p.groups), block(64 * WGM * WGN * KS);
+    if (p.conv_h == 0 && p.ln_fold != 1 && compact_epilogue(p)) {  // (LayerNorm folded with handed-in statistics or none)
+        if (p.ln_fold == 2)
+            hipLaunchKernelGGL((gemm_glds_kernel<T, BM, BN, WGM, WGN, KS, ST, false, 2, 1>), grid, block, 0, st, p);
+        else
+            hipLaunchKernelGGL((gemm_glds_kernel<T, BM, BN, WGM, WGN, KS, ST, false, 0, 1>), grid, block, 0, st, p);
+        return;
+    }
     if (p.conv_h > 0)
         hipLaunchKernelGGL((gemm_glds_kernel<T, BM, BN, WGM, WGN, KS, ST, true, 0>), grid, block, 0, st, p);
     else if (p.ln_fold == 2)

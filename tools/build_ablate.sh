@@ -6,6 +6,7 @@
 #            softmax work / without exponentials / without exponentials and bf16 packing
 #            (MMT_ATTN_ABLATE=1/2/3/4); aab5: impl 22 free-running (no per-tile wait / barrier / refill); aab6: aab5 without exponentials
 #   stamp:   per-phase workgroup timestamps in the GEMM / attention kernels (MMT_STAMP_BUILD=1)
+#   stamp_e3 / stamp_e4: stamp builds of the GEMM without epilogue stores / tile reads (MMT_GEMM_ABLATE=3 / 4)
 #   ab:      the product plus the A/B-only attention kernel impl 23 (MMT_ATTN_AB=1)
 #   noocc2:  the product without the cost model's switch to the two-per-CU 128x128 GEMM tile (impl 8)
 # Use with MMT_HIP_LIB=multi-modal-tracking_amd/mmt_amd/_lib/<variant>/libmmt_hip.so.
@@ -20,6 +21,8 @@ build() {
 build ablate1 -DMMT_GEMM_ABLATE=1
 build ablate2 -DMMT_GEMM_ABLATE=2
 build stamp -DMMT_STAMP_BUILD=1
+build stamp_e3 "-DMMT_STAMP_BUILD=1 -DMMT_GEMM_ABLATE=3"
+build stamp_e4 "-DMMT_STAMP_BUILD=1 -DMMT_GEMM_ABLATE=4"
 build aab1 -DMMT_ATTN_ABLATE=1
 build aab2 -DMMT_ATTN_ABLATE=2
 build aab3 -DMMT_ATTN_ABLATE=3
