@@ -108,6 +108,8 @@ MMT_DEV int gemm_trsw(int k) { return 2 * ((k & 3) | (((k >> 3) & 1) << 2)); }
 // statistics, row map or row scale; the launcher checks): the general epilogue's branches for every other mode
 // made the strip passes ~44 KiB of code per kernel, fetched cold by every workgroup (per-phase stamps: qkv
 // passes 1.96 -> 0.68 us, fc1 2.90 -> 1.63 us with this form, profiles/r04_gemm_epilogue_stamps.jsonl).
+// EPI 2: the compact epilogue of the residual producers (fp32 C = acc + bias + R, its 16-bit copy C2, the next
+// LayerNorm's row statistics).
 template <typename T, int BM, int BN, int WGM, int WGN, int KS, int ST, bool CONV, int LNM, int OCC = 1, bool RS = false,
           int EPI = 0>
 MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int tile, const int slice, const int nsk,
@@ -679,6 +681,56 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
                 *(u32x4*)((T*)C + (int64_t)m * p.ldc + n) = u32x4{pack2<T>(va[0], va[1]), pack2<T>(va[2], va[3]),
                                                                pack2<T>(vb[0], vb[1]), pack2<T>(vb[2], vb[3])};
         }
+    } else if constexpr (EPI == 2) {  // compact residual producer: fp32 C = acc + bias + R, C2 its 16-bit copy,
+                                      // the next LayerNorm's row statistics (proj / fc2 of the ViT blocks)
+        static_assert(EPASS == 1 && !RS && !LNF, "compact residual epilogue: single-pass plain tiles");
+#pragma unroll
+        for (int p0 = 0; p0 < NPASS; p0 += PG) {
+            f32x4 ra[PG], rb[PG];
+#pragma unroll
+            for (int i = 0; i < PG; ++i) {
+                ra[i] = rb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+                if constexpr (RPRE) {
+                    if (rpre) {
+                        ra[i] = rpa[p0 + i];
+                        rb[i] = rpb[p0 + i];
+                        continue;
+                    }
+                }
+                if (R) {  // plain rows (the launcher checks r_mode / r_t / c_seg_rows)
+                    const float* rr = R + (int64_t)min(m0_tile + tr + (p0 + i) * RPP, M - 1) * p.ldr + nc;
+                    ra[i] = *(const f32x4*)rr;
+                    rb[i] = *(const f32x4*)(rr + 4);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < PG; ++i) {
+                const int r = tr + (p0 + i) * RPP, m = m0_tile + r;
+                const f32x4 sa = *(const f32x4*)(ctile + r * TP + tc) + bn0 + ra[i];
+                const f32x4 sb = *(const f32x4*)(ctile + r * TP + tc + 4) + bn1 + rb[i];
+                if (stats_out) {  // as the general path
+                    float ps = 0.f, pq = 0.f;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const f32x2 u = unpack2<T>(pack2<T>(j < 2 ? sa[2 * j] : sb[2 * j - 4], j < 2 ? sa[2 * j + 1] : sb[2 * j - 3]));
+                        ps += u[0] + u[1];
+                        pq = fmaf(u[0], u[0], fmaf(u[1], u[1], pq));
+                    }
+                    ps = sum8_lanes(ps);
+                    pq = sum8_lanes(pq);
+                    if ((tc & 63) == 0 && m < M && n < N)
+                        *(f32x2*)(stats_out + ((int64_t)m * (N / 64) + n / 64) * 2) = f32x2{ps, pq};
+                }
+                if (m < M && n < N) {
+                    const int64_t e = (int64_t)m * p.ldc + n;
+                    *(f32x4*)((float*)C + e) = sa;
+                    *(f32x4*)((float*)C + e + 4) = sb;
+                    if (C2)
+                        *(u32x4*)((T*)C2 + e) = u32x4{pack2<T>(sa[0], sa[1]), pack2<T>(sa[2], sa[3]),
+                                                      pack2<T>(sb[0], sb[1]), pack2<T>(sb[2], sb[3])};
+                }
+            }
+        }
     } else
     for (int ep = 0; ep < EPASS; ++ep) {
     if (ep > 0) {  // the next wave row's accumulators into the (re-used) tile image
@@ -893,6 +945,17 @@ bool compact_epilogue(const mmt_gemm_params& p) {
     return true;
 }
 
+// Whether the compact residual-producer epilogue (EPI 2) covers it: fp32 C = acc + bias (+ R, plain rows),
+// C2 (if any) its 16-bit copy (c2_copy 1), LayerNorm statistics out (with C2) -- no activation, row map or scale.
+bool residual_epilogue(const mmt_gemm_params& p) {
+    if (!p.c_f32 || p.act || p.c_seg_rows || p.row_scale || p.r_mode || p.r_t || p.ln_fold) return false;
+    for (int g = 0; g < p.groups; ++g) {
+        if (p.c2[g] && p.c2_copy != 1) return false;
+        if (!p.c2[g] && (p.c2_copy || p.ln_stats_out[g])) return false;
+    }
+    return true;
+}
+
 template <typename T, int BM, int BN, int WGM, int WGN, int KS, int ST>
 void launch(const mmt_gemm_params& p, int nsk, hipStream_t st) {
     const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
@@ -902,6 +965,10 @@ void launch(const mmt_gemm_params& p, int nsk, hipStream_t st) {
             hipLaunchKernelGGL((gemm_glds_kernel<T, BM, BN, WGM, WGN, KS, ST, false, 2, 1>), grid, block, 0, st, p);
         else
             hipLaunchKernelGGL((gemm_glds_kernel<T, BM, BN, WGM, WGN, KS, ST, false, 0, 1>), grid, block, 0, st, p);
+        return;
+    }
+    if (p.conv_h == 0 && residual_epilogue(p)) {
+        hipLaunchKernelGGL((gemm_glds_kernel<T, BM, BN, WGM, WGN, KS, ST, false, 0, 2>), grid, block, 0, st, p);
         return;
     }
     if (p.conv_h > 0)
