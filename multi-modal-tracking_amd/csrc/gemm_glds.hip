@@ -971,7 +971,9 @@ void launch(const mmt_gemm_params& p, int nsk, hipStream_t st) {
         hipLaunchKernelGGL((gemm_glds_kernel<T, BM, BN, WGM, WGN, KS, ST, false, 0, 2>), grid, block, 0, st, p);
         return;
     }
-    if (p.conv_h > 0)
+    if (p.conv_h > 0 && compact_epilogue(p))  // the corner head's plain conv + ReLU layers
+        hipLaunchKernelGGL((gemm_glds_kernel<T, BM, BN, WGM, WGN, KS, ST, true, 0, 1>), grid, block, 0, st, p);
+    else if (p.conv_h > 0)
         hipLaunchKernelGGL((gemm_glds_kernel<T, BM, BN, WGM, WGN, KS, ST, true, 0>), grid, block, 0, st, p);
     else if (p.ln_fold == 2)
         hipLaunchKernelGGL((gemm_glds_kernel<T, BM, BN, WGM, WGN, KS, ST, false, 2>), grid, block, 0, st, p);
