@@ -643,11 +643,24 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
     const int64_t csr = p.c_seg_rows > 0 ? p.c_seg_rows : INT64_MAX, csp = p.c_seg_pitch;
     auto crow = [&](int m) -> int64_t { return csr == INT64_MAX ? (int64_t)m : (m / csr) * csp + m % csr; };
     constexpr int PG = NPASS < 4 ? NPASS : 4;  // passes whose residual loads are in flight together
+    for (int ep = 0; ep < EPASS; ++ep) {
+    if (ep > 0) {  // the next wave row's accumulators into the (re-used) tile image
+        lds_barrier();
+        if (wr == ep) {
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+                    *(f32x4*)(ctile + (mt * 16 + l16) * TP + wc * WN + nt * 16 + lg * 4) = acc[nt][mt];
+        }
+        lds_barrier();
+    }
+    const int m0 = m0_tile + ep * EB;  // first tile row of this pass
     if constexpr (EPI == 1) {
-        static_assert(EPASS == 1 && !RS, "compact epilogue: single-pass tiles");
+        static_assert(!RS, "compact epilogue: no row scale");
 #pragma unroll
         for (int i = 0; i < NPASS; ++i) {
-            const int r = tr + i * RPP, m = m0_tile + r;
+            const int r = tr + i * RPP, m = m0 + r;
             f32x4 va = *(const f32x4*)(ctile + r * TP + tc);
             f32x4 vb = *(const f32x4*)(ctile + r * TP + tc + 4);
             if constexpr (LNF) {  // as the general path
@@ -665,6 +678,9 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
             }
             va += bn0;
             vb += bn1;
+            if (C2 && m < M && n < N)  // c2_copy 2: the pre-activation in the compute dtype (training fc1)
+                *(u32x4*)((T*)C2 + (int64_t)m * p.ldc + n) = u32x4{pack2<T>(va[0], va[1]), pack2<T>(va[2], va[3]),
+                                                                pack2<T>(vb[0], vb[1]), pack2<T>(vb[2], vb[3])};
             if (p.act == 1) {
                 va.xy = gelu_erf2(va.xy);
                 va.zw = gelu_erf2(va.zw);
@@ -683,7 +699,7 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
         }
     } else if constexpr (EPI == 2) {  // compact residual producer: fp32 C = acc + bias + R, C2 its 16-bit copy,
                                       // the next LayerNorm's row statistics (proj / fc2 of the ViT blocks)
-        static_assert(EPASS == 1 && !RS && !LNF, "compact residual epilogue: single-pass plain tiles");
+        static_assert(!LNF, "compact residual epilogue: plain tiles");
 #pragma unroll
         for (int p0 = 0; p0 < NPASS; p0 += PG) {
             f32x4 ra[PG], rb[PG];
@@ -698,16 +714,22 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
                     }
                 }
                 if (R) {  // plain rows (the launcher checks r_mode / r_t / c_seg_rows)
-                    const float* rr = R + (int64_t)min(m0_tile + tr + (p0 + i) * RPP, M - 1) * p.ldr + nc;
+                    const float* rr = R + (int64_t)min(m0 + tr + (p0 + i) * RPP, M - 1) * p.ldr + nc;
                     ra[i] = *(const f32x4*)rr;
                     rb[i] = *(const f32x4*)(rr + 4);
                 }
             }
 #pragma unroll
             for (int i = 0; i < PG; ++i) {
-                const int r = tr + (p0 + i) * RPP, m = m0_tile + r;
-                const f32x4 sa = *(const f32x4*)(ctile + r * TP + tc) + bn0 + ra[i];
-                const f32x4 sb = *(const f32x4*)(ctile + r * TP + tc + 4) + bn1 + rb[i];
+                const int r = tr + (p0 + i) * RPP, m = m0 + r;
+                f32x4 va = *(const f32x4*)(ctile + r * TP + tc) + bn0;
+                f32x4 vb = *(const f32x4*)(ctile + r * TP + tc + 4) + bn1;
+                if constexpr (RS) {  // the residual branch's per-sample stochastic-depth scale (training)
+                    const float sc = p.row_scale[min(m, M - 1) / p.row_scale_div];
+                    va *= sc;
+                    vb *= sc;
+                }
+                const f32x4 sa = va + ra[i], sb = vb + rb[i];
                 if (stats_out) {  // as the general path
                     float ps = 0.f, pq = 0.f;
 #pragma unroll
@@ -731,20 +753,7 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
                 }
             }
         }
-    } else
-    for (int ep = 0; ep < EPASS; ++ep) {
-    if (ep > 0) {  // the next wave row's accumulators into the (re-used) tile image
-        lds_barrier();
-        if (wr == ep) {
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-                for (int mt = 0; mt < MT; ++mt)
-                    *(f32x4*)(ctile + (mt * 16 + l16) * TP + wc * WN + nt * 16 + lg * 4) = acc[nt][mt];
-        }
-        lds_barrier();
-    }
-    const int m0 = m0_tile + ep * EB;  // first tile row of this pass
+    } else {
 #pragma unroll
     for (int p0 = 0; p0 < NPASS; p0 += PG) {
         f32x4 ra[PG], rb[PG];
@@ -853,6 +862,7 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
             }
         }
     }
+    }
     }  // epilogue passes
     MMT_STAMP(5, "s_memtime");
 #if MMT_STAMP_BUILD
@@ -889,7 +899,7 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
 // The same tile at two workgroups per CU (impl 8: 128x128, 8 waves, 2-slot ring = 64 KiB of LDS, <= 128
 // VGPRs): one workgroup's prologue / epilogue runs beside the other's K loop on the CU, which the one-
 // workgroup-per-CU tiles cannot overlap (large-M grids of short K: the training step's K = 768 GEMMs).
-template <typename T, int BM, int BN, int WGM, int WGN, int KS, int ST, bool RS = false>
+template <typename T, int BM, int BN, int WGM, int WGN, int KS, int ST, bool RS = false, int EPI = 0>
 __global__ __launch_bounds__(64 * WGM * WGN * KS)
     __attribute__((amdgpu_waves_per_eu(WGM * WGN * KS / 2, WGM * WGN * KS / 2))) void gemm_glds_kernel_occ2(
         const mmt_gemm_params p) {
@@ -898,11 +908,11 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
     const int per_g = gridDim.x * nsk;
     const int g = lin / per_g, rem_t = lin - g * per_g;
     const int tile = rem_t / nsk, slice = rem_t - tile * nsk;
-    gemm_glds_tile<T, BM, BN, WGM, WGN, KS, ST, false, 0, 2, RS>(p, g, tile, slice, nsk, gridDim.x);
+    gemm_glds_tile<T, BM, BN, WGM, WGN, KS, ST, false, 0, 2, RS, EPI>(p, g, tile, slice, nsk, gridDim.x);
 }
 
 // impl 8's tile with MN-major operands (LNM 3: W; 4: A and W)
-template <typename T, int LNM>
+template <typename T, int LNM, int EPI = 0>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void gemm_glds_kernel_occ2_t(
     const mmt_gemm_params p) {
     const int nsk = gridDim.y;
@@ -910,7 +920,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     const int per_g = gridDim.x * nsk;
     const int g = lin / per_g, rem_t = lin - g * per_g;
     const int tile = rem_t / nsk, slice = rem_t - tile * nsk;
-    gemm_glds_tile<T, 128, 128, 2, 4, 1, 2, false, LNM, 2>(p, g, tile, slice, nsk, gridDim.x);
+    gemm_glds_tile<T, 128, 128, 2, 4, 1, 2, false, LNM, 2, false, EPI>(p, g, tile, slice, nsk, gridDim.x);
 }
 
 // Several independent GEMMs of one kernel configuration in one launch (mmt_gemm_multi): problem i
@@ -937,18 +947,20 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
     gemm_glds_tile<T, BM, BN, WGM, WGN, KS, ST, CONV, 0>(a.p[i], g, loc - g * nt, 0, 1, nt);
 }
 
-// Whether the compact 16-bit epilogue (EPI 1) covers the GEMM's epilogue.
+// Whether the compact 16-bit epilogue (EPI 1) covers the GEMM's epilogue (bias, folded LayerNorm, ReLU / GELU,
+// the pre-activation copy of c2_copy 2).
 bool compact_epilogue(const mmt_gemm_params& p) {
-    if (p.c_f32 || p.c2_copy || p.c_seg_rows || p.row_scale || p.act < 0 || p.act > 2) return false;
-    for (int g = 0; g < p.groups; ++g)
-        if (p.r[g] || p.c2[g] || p.ln_stats_out[g]) return false;
+    if (p.c_f32 || (p.c2_copy != 0 && p.c2_copy != 2) || p.c_seg_rows || p.row_scale || p.act < 0 || p.act > 2)
+        return false;
+    for (int g = 0; g < p.groups; ++g)  // C2 only as c2_copy 2's pre-activation copy
+        if (p.r[g] || p.ln_stats_out[g] || (p.c2[g] != nullptr) != (p.c2_copy == 2)) return false;
     return true;
 }
 
 // Whether the compact residual-producer epilogue (EPI 2) covers it: fp32 C = acc + bias (+ R, plain rows),
 // C2 (if any) its 16-bit copy (c2_copy 1), LayerNorm statistics out (with C2) -- no activation, row map or scale.
-bool residual_epilogue(const mmt_gemm_params& p) {
-    if (!p.c_f32 || p.act || p.c_seg_rows || p.row_scale || p.r_mode || p.r_t || p.ln_fold) return false;
+bool residual_epilogue(const mmt_gemm_params& p, bool rs = false) {  // rs: a row-scale (RS) kernel
+    if (!p.c_f32 || p.act || p.c_seg_rows || (p.row_scale != nullptr) != rs || p.r_mode || p.r_t || p.ln_fold) return false;
     for (int g = 0; g < p.groups; ++g) {
         if (p.c2[g] && p.c2_copy != 1) return false;
         if (!p.c2[g] && (p.c2_copy || p.ln_stats_out[g])) return false;
@@ -1054,8 +1066,11 @@ int mmt_gemm_glds(const mmt_gemm_params& p, hipStream_t st, int force) {
     int cfg = force, nsk = 1;
     if (p.row_scale) {  // the training step's residual branches: impl 8's tile with the row-scale epilogue
         if ((force != 0 && force != 8) || p.ln_fold || p.conv_h > 0 || p.a_t || p.w_t) return 1;
-        hipLaunchKernelGGL((gemm_glds_kernel_occ2<T, 128, 128, 2, 4, 1, 2, true>),
-                           dim3((unsigned)tiles_of(p, 128, 128), 1, p.groups), dim3(512), 0, st, p);
+        const dim3 grid((unsigned)tiles_of(p, 128, 128), 1, p.groups);
+        if (residual_epilogue(p, true))
+            hipLaunchKernelGGL((gemm_glds_kernel_occ2<T, 128, 128, 2, 4, 1, 2, true, 2>), grid, dim3(512), 0, st, p);
+        else
+            hipLaunchKernelGGL((gemm_glds_kernel_occ2<T, 128, 128, 2, 4, 1, 2, true>), grid, dim3(512), 0, st, p);
         return 0;
     }
     if (p.a_t || p.w_t) {  // MN-major operands: the 128x128 tiles (impl 1, or impl 8 on big unsplit grids)
@@ -1077,6 +1092,7 @@ int mmt_gemm_glds(const mmt_gemm_params& p, hipStream_t st, int force) {
         const dim3 grid((unsigned)tiles_of(p, 128, 128), nsk, p.groups);
         if (cfg == 8) {
             if (lnm == 4) hipLaunchKernelGGL((gemm_glds_kernel_occ2_t<T, 4>), grid, dim3(512), 0, st, p);
+            else if (compact_epilogue(p)) hipLaunchKernelGGL((gemm_glds_kernel_occ2_t<T, 3, 1>), grid, dim3(512), 0, st, p);
             else hipLaunchKernelGGL((gemm_glds_kernel_occ2_t<T, 3>), grid, dim3(512), 0, st, p);
         } else {
             if (lnm == 4) hipLaunchKernelGGL((gemm_glds_kernel<T, 128, 128, 2, 4, 1, 4, false, 4>), grid, dim3(512), 0, st, p);
@@ -1146,8 +1162,15 @@ int mmt_gemm_glds(const mmt_gemm_params& p, hipStream_t st, int force) {
         case 8:  // 128x128 at two workgroups per CU: plain GEMM mode (no folded LayerNorm / conv), and no split-K:
                  // its 64 KiB ring holds the fp32 tile image only in two passes (as impl 7)
             if (p.ln_fold || p.conv_h > 0 || nsk > 1) return 1;
-            hipLaunchKernelGGL((gemm_glds_kernel_occ2<T, 128, 128, 2, 4, 1, 2>),
-                               dim3((unsigned)tiles_of(p, 128, 128), nsk, p.groups), dim3(512), 0, st, p);
+            {
+                const dim3 grid((unsigned)tiles_of(p, 128, 128), nsk, p.groups);
+                if (compact_epilogue(p))
+                    hipLaunchKernelGGL((gemm_glds_kernel_occ2<T, 128, 128, 2, 4, 1, 2, false, 1>), grid, dim3(512), 0, st, p);
+                else if (residual_epilogue(p))
+                    hipLaunchKernelGGL((gemm_glds_kernel_occ2<T, 128, 128, 2, 4, 1, 2, false, 2>), grid, dim3(512), 0, st, p);
+                else
+                    hipLaunchKernelGGL((gemm_glds_kernel_occ2<T, 128, 128, 2, 4, 1, 2>), grid, dim3(512), 0, st, p);
+            }
             break;
         default: return 1;
     }

@@ -24,7 +24,10 @@ from mmt_amd import _lib as L  # noqa: E402
 SHAPES = [("qkv", 2, 528, 2304, 768, 0, 0), ("proj", 2, 528, 768, 768, 0, 1), ("fc1", 2, 528, 3072, 768, 1, 0),
           ("fc2", 2, 528, 768, 3072, 0, 1), ("qkv_ln", 2, 528, 2304, 768, 0, 0), ("fc1_ln", 2, 528, 3072, 768, 1, 0),
           ("qkv_ln2", 2, 528, 2304, 768, 0, 0), ("fc1_ln2", 2, 528, 3072, 768, 1, 0)]
-TILES = {1: (128, 128), 2: (128, 64), 3: (64, 64), 4: (128, 128)}
+if os.environ.get("GEMM_STAMP_SHAPES") == "train":  # the training step's forward GEMMs (16 pairs: 8448 rows per backbone)
+    SHAPES = [("t_qkv", 1, 8448, 2304, 768, 0, 0), ("t_fc1", 1, 8448, 3072, 768, 1, 0), ("t_proj", 1, 8448, 768, 768, 0, 1),
+              ("t_fc2", 1, 8448, 768, 3072, 0, 1)]
+TILES = {1: (128, 128), 2: (128, 64), 3: (64, 64), 4: (128, 128), 8: (128, 128)}
 IMPLS = [int(x) for x in os.environ.get("GEMM_STAMP_IMPLS", "1,2,3,4").split(",")]
 SK_WS = None
 
