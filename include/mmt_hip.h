@@ -276,6 +276,12 @@ int mmt_groupnorm_bwd(const float* x, const float* dy, const float* gamma, float
 int mmt_add_cast(const float* in, const float* add, int64_t add_n, float* out_f32, void* out_t, int64_t n,
                  int dtype, void* stream);
 
+/* out[r][c] = (dtype) (in[r][c] * scale[r / rows_per]) over an fp32 [rows][cols] (cols % 8 == 0, 16-B aligned),
+ * dtype MMT_BF16 / MMT_F16: the training step's residual-branch gradient under stochastic depth (the per-sample
+ * DropPath scale, mixformer.py:136-139) cast to the GEMM operand type in one pass. */
+int mmt_scale_rows_cast(const float* in, const float* scale, int64_t rows_per, void* out, int64_t rows, int64_t cols,
+                        int dtype, void* stream);
+
 /* Patch staging for the 16x16/s16 patch-embed conv: for each of S = 2*Bm sequences
  * (modality m = s / Bm, batch b = s % Bm) the row block [tmpl | online | search] of tokens, each row
  * = (c, ky, kx) flattened (3*P*P), from fp32 NCHW images img_t[m], img_o[m], img_s[m].  With

@@ -423,6 +423,19 @@ __global__ void add_cast_kernel(const float* __restrict__ in, const float* __res
     }
 }
 
+// out[r][c] = (T)(in[r][c] * scale[r / rows_per]), 8 elements per thread (two 16-B loads, one 16-B store)
+template <typename T>
+__global__ __launch_bounds__(256) void scale_rows_cast_kernel(const float4* __restrict__ in, const float* __restrict__ scale,
+                                                              int64_t rows_per, int64_t cols8, uint4* __restrict__ out,
+                                                              int64_t n8) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n8) return;
+    const float sc = scale[(i / cols8) / rows_per];
+    const float4 a = in[2 * i], b = in[2 * i + 1];
+    out[i] = uint4{pack2<T>(a.x * sc, a.y * sc), pack2<T>(a.z * sc, a.w * sc), pack2<T>(b.x * sc, b.y * sc),
+                   pack2<T>(b.z * sc, b.w * sc)};
+}
+
 // One thread per (sequence-row token, channel, ky): 16 contiguous kx pixels -> 16 outputs.
 template <typename T>
 __global__ void patch_im2col_kernel(const float* t0, const float* t1, const float* o0, const float* o1, const float* s0,
@@ -562,6 +575,23 @@ extern "C" int mmt_add_cast(const float* in, const float* add, int64_t add_n, fl
         hipLaunchKernelGGL((add_cast_kernel<f16_t>), grid, dim3(256), 0, st, in, add, add_n, out_f32, (f16_t*)out_t, n4);
     else if (dtype == MMT_F32)
         hipLaunchKernelGGL((add_cast_kernel<float>), grid, dim3(256), 0, st, in, add, add_n, out_f32, (float*)out_t, n4);
+    else return MMT_EBADARG;
+    return launch_status();
+}
+
+extern "C" int mmt_scale_rows_cast(const float* in, const float* scale, int64_t rows_per, void* out, int64_t rows,
+                                   int64_t cols, int dtype, void* stream) {
+    if (!in || !scale || !out || rows <= 0 || cols <= 0 || cols % 8 || rows_per <= 0) return MMT_EBADARG;
+    if (((uintptr_t)in | (uintptr_t)out) & 15) return MMT_EBADARG;
+    const int64_t n8 = rows * cols / 8;
+    const dim3 grid((unsigned)((n8 + 255) / 256));
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == MMT_BF16)
+        hipLaunchKernelGGL((scale_rows_cast_kernel<bf16_t>), grid, dim3(256), 0, st, (const float4*)in, scale, rows_per,
+                           cols / 8, (uint4*)out, n8);
+    else if (dtype == MMT_F16)
+        hipLaunchKernelGGL((scale_rows_cast_kernel<f16_t>), grid, dim3(256), 0, st, (const float4*)in, scale, rows_per,
+                           cols / 8, (uint4*)out, n8);
     else return MMT_EBADARG;
     return launch_status();
 }

@@ -78,6 +78,7 @@ _PROTOS = {
     "mmt_groupnorm": [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, f32, i32, vp],
     "mmt_groupnorm_bwd": [vp, vp, vp, vp, vp, i32, vp, i64, i32, i32, i32, i32, f32, vp],
     "mmt_add_cast": [vp, vp, i64, vp, vp, i64, i32, vp],
+    "mmt_scale_rows_cast": [vp, vp, i64, vp, i64, i64, i32, vp],
     "mmt_patch_im2col": [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp],
     "mmt_ms_deform_attn_forward": [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp],
     "mmt_ms_deform_attn_backward": [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp],

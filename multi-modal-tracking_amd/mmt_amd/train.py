@@ -208,8 +208,12 @@ def _scaled_bf16(dy, keep, rows_per):
     """keep[m // rows_per] * dy in bf16, one pass (the residual branch's gradient under stochastic depth)."""
     if keep is None:
         return dy.to(torch.bfloat16).contiguous()
+    from ._lib import LIB, MMT_BF16, check
+    dy = dy.float().contiguous()
     out = torch.empty(dy.shape, device=dy.device, dtype=torch.bfloat16)
-    torch.mul(dy.view(keep.shape[0], rows_per, -1), keep.view(-1, 1, 1), out=out.view(keep.shape[0], rows_per, -1))
+    cols = dy.shape[-1]
+    check(LIB.mmt_scale_rows_cast(dy.data_ptr(), keep.float().contiguous().data_ptr(), rows_per, out.data_ptr(),
+                                  dy.numel() // cols, cols, MMT_BF16, _stream()), "mmt_scale_rows_cast")
     return out
 
 

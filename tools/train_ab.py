@@ -16,6 +16,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "multi-modal-tracking_amd"))
 
 import bench  # noqa: E402
+import torch  # noqa: E402
 from mmt_amd.train import HipOps  # noqa: E402
 
 
@@ -77,6 +78,27 @@ def transposed_copies():
         train.MN_MAJOR = True
 
 
+@contextlib.contextmanager
+def aten_scale_cast():
+    """The residual branches' DropPath-scaled gradient cast as aten's broadcasting torch.mul into bf16 instead of
+    mmt_scale_rows_cast."""
+    from mmt_amd import train
+    saved = train._scaled_bf16
+
+    def scaled(dy, keep, rows_per):
+        if keep is None:
+            return dy.to(torch.bfloat16).contiguous()
+        out = torch.empty(dy.shape, device=dy.device, dtype=torch.bfloat16)
+        torch.mul(dy.view(keep.shape[0], rows_per, -1), keep.view(-1, 1, 1), out=out.view(keep.shape[0], rows_per, -1))
+        return out
+
+    train._scaled_bf16 = scaled
+    try:
+        yield
+    finally:
+        train._scaled_bf16 = saved
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
@@ -87,7 +109,7 @@ def main():
     args = ap.parse_args()
     variants = {"hip": HipOps, "aten_groupnorm": AtenGroupNormOps, "aten_layernorm": AtenLayerNormOps,
                 "split_mlp": SplitMlpOps, "unfused_residual": UnfusedResidualOps, "accum_grads": (HipOps, accumulated_grads),
-                "transposed": (HipOps, transposed_copies)}
+                "transposed": (HipOps, transposed_copies), "aten_scale_cast": (HipOps, aten_scale_cast)}
     if args.only:
         variants = {k: v for k, v in variants.items() if k in args.only.split(",")}
     for r in range(args.rounds):
