@@ -70,6 +70,9 @@ def _transpose(x, rows, cols, ld_out=None, ones_row=False):
 # The Linear backward reads dY, X and W as they are (MN-major GEMM operands, ds_read_b64_tr_b16) instead
 # of transposed copies; False: the transposing form (A/B knob, tools/train_ab.py)
 MN_MAJOR = True
+# The two-stream backbones in lockstep with grouped GEMMs (backbone_forward_pair); False: one after the
+# other (A/B knob, tools/train_ab.py)
+PAIR = True
 _SPLITK = {}  # device -> (slab workspace, arrival tickets) of the dW GEMMs' split-K (stream-ordered: one set)
 
 
@@ -87,27 +90,44 @@ def _gemm(a, w, M, N, K, bias=None, out_f32=False, act=0, r=None, c2=None, c2_co
     [M][N]) / c2 / c2_copy as mmt_gemm_params (act 1 GELU, 5 GELU backward against r; c2_copy 2: c2 = the
     pre-activation; 3: the last 8 columns to c2 [M][8]); c / ldc: a preallocated output and its pitch;
     a_t / w_t / ldw / lda: MN-major operands (A^T [K][lda], W^T [K][ldw]); splitk: with a split-K
-    workspace (the cost model may split K over workgroups)."""
+    workspace (the cost model may split K over workgroups).
+    Grouped form (the two-stream backbones in lockstep): a and w (and bias / r / c2 / c) tuples, one entry
+    per group, one launch; without c the output is one [groups * M][N] tensor, group g on rows g M ..."""
     from ._lib import LIB, GemmParams, MMT_BF16, check
+    grouped = isinstance(a, tuple)
+    A, W = (a, w) if grouped else ((a,), (w,))
+    G = len(A)
     if c is None:
-        c = torch.empty(M, N, device=a.device, dtype=torch.float32 if out_f32 else torch.bfloat16)
+        c = torch.empty(G * M, N, device=A[0].device, dtype=torch.float32 if out_f32 else torch.bfloat16)
+        cs = c.split(M) if grouped else (c,)
+    else:
+        cs = c if grouped else (c,)
+    bs = bias if grouped else (bias,)
     p = GemmParams()
-    p.a[0], p.w[0], p.c[0] = a.data_ptr(), w.data_ptr(), c.data_ptr()
-    p.bias[0] = bias.data_ptr() if bias is not None else None
+    for g in range(G):
+        p.a[g], p.w[g], p.c[g] = A[g].data_ptr(), W[g].data_ptr(), cs[g].data_ptr()
+        p.bias[g] = bs[g].data_ptr() if bs is not None and bs[g] is not None else None
     p.lda, p.ldc = lda or K, ldc or N
     p.a_t, p.w_t, p.ldw, p.impl = a_t, w_t, ldw, impl
     if splitk:
-        ws, cnt = _splitk_ws(a.device)
+        ws, cnt = _splitk_ws(A[0].device)
         p.sk_ws, p.sk_ws_floats, p.sk_cnt, p.sk_cnt_n = ws.data_ptr(), ws.numel(), cnt.data_ptr(), cnt.numel()
     p.a_seg_rows, p.a_segs_a = M, 1
-    p.M, p.N, p.K, p.groups, p.c_f32 = M, N, K, 1, 1 if out_f32 else 0
+    p.M, p.N, p.K, p.groups, p.c_f32 = M, N, K, G, 1 if out_f32 else 0
     p.act = act
     if r is not None:  # bf16 (act 5's pre-activation) or the fp32 residual stream
-        p.r[0], p.ldr, p.r_t = r.data_ptr(), N, 0 if r.dtype == torch.float32 else 1
-    if row_scale is not None:
+        rs = r if grouped else (r,)
+        for g in range(G):
+            p.r[g] = rs[g].data_ptr()
+        p.ldr, p.r_t = N, 0 if rs[0].dtype == torch.float32 else 1
+    if row_scale is not None:  # one per-row scale vector, indexed by the row within a group
+        if G > 1:
+            raise ValueError("row_scale with grouped operands")
         p.row_scale, p.row_scale_div = row_scale.data_ptr(), row_scale_div
     if c2 is not None:
-        p.c2[0], p.c2_copy = c2.data_ptr(), c2_copy
+        for g, t in enumerate(c2 if grouped else (c2,)):
+            p.c2[g] = t.data_ptr()
+        p.c2_copy = c2_copy
     check(LIB.mmt_gemm(p, MMT_BF16, _stream()), "mmt_gemm")
     return c
 
@@ -277,6 +297,131 @@ class _HipMlpResidual(torch.autograd.Function):
         dxn = _dx(dhp, wb1, M, F4, C) if ctx.needs_input_grad[1] else None
         dw1, db1 = _weight_grads(dhp, xn, M, F4, C)
         return dout, dxn, dw1, db1, dw2, db2, None
+
+
+# -- the two-stream backbones in lockstep: the RGB rows [0, M) and the TIR rows [M, 2M) of one stacked
+# operand, each modality with its own weights, as one grouped GEMM (groups 2) per Linear and per gradient.
+# One modality's dW GEMM (768-3080 output columns, K = the 8448 tokens of 16 pairs) is a 42-168 tile grid on
+# 256 CUs; the pair fills the chip twice as well (tools/dw_split_ab.py: 250-425 TFLOP/s at one group).
+def _halves(t, M):
+    return t[:M], t[M:]
+
+
+def _weight_grads2(dy, x, M, N, K):
+    """_weight_grads of both modalities (dy [2M][N], x [2M][K]) in one launch: ((dW, db) RGB, (dW, db) TIR)."""
+    bufs = [torch.empty(N * (K + 8), device=dy.device, dtype=torch.float32) for _ in range(2)]
+    dws = tuple(b[:N * K].view(N, K) for b in bufs)
+    dbs = tuple(b[N * K:].view(N, 8) for b in bufs)
+    if not (MN_MAJOR and M % 8 == 0):
+        return [_weight_grads(u, v, M, N, K) for u, v in zip(_halves(dy, M), _halves(x, M))]
+    _gemm(_halves(dy, M), _halves(x, M), N, K + 8, M, out_f32=True, c=dws, ldc=K, c2=dbs, c2_copy=3, a_t=1,
+          w_t=2, ldw=K, lda=N, splitk=True)
+    return [(dws[0], dbs[0][:, 0]), (dws[1], dbs[1][:, 0])]
+
+
+def _dx2(dy, wbs, M, N, K, act=0, r=None):
+    """_dx of both modalities: dX [2M][K] = dY [2M][N] W_m [N][K] per half (bf16; act 5 with r [2M][N])."""
+    rr = _halves(r, M) if r is not None else None
+    if MN_MAJOR:
+        return _gemm(_halves(dy, M), wbs, M, K, N, act=act, r=rr, w_t=1, ldw=K)
+    return _gemm(_halves(dy, M), tuple(_transpose(w, N, K) for w in wbs), M, K, N, act=act, r=rr)
+
+
+class _HipLinear2(torch.autograd.Function):
+    """_HipLinear for the two modalities: x [2M][K] bf16 (RGB rows first), weights (w0, b0) / (w1, b1)."""
+
+    @staticmethod
+    def forward(ctx, x, w0, b0, w1, b1, out_f32=False):
+        M2, K = x.shape
+        M, N = M2 // 2, w0.shape[0]
+        x = x.contiguous()
+        wbs = (_bf16_weight(w0), _bf16_weight(w1))
+        y = _gemm(_halves(x, M), wbs, M, N, K, bias=(b0.detach().float(), b1.detach().float()), out_f32=out_f32)
+        ctx.save_for_backward(x, *wbs)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wb0, wb1 = ctx.saved_tensors
+        M2, K = x.shape
+        M, N = M2 // 2, wb0.shape[0]
+        dy = dy.to(torch.bfloat16).contiguous()
+        dx = _dx2(dy, (wb0, wb1), M, N, K) if ctx.needs_input_grad[0] else None
+        (dw0, db0), (dw1, db1) = _weight_grads2(dy, x, M, N, K)
+        return dx, dw0, db0, dw1, db1, None
+
+
+def _residual_gemm2(a, wbs, bs, x, keep, M, N, K, rows):
+    """x + keep * (a W_m^T + b_m) for both halves, fp32 [2M][N]: one grouped launch without stochastic depth;
+    with it one launch per modality (the row scale is one vector indexed by the row within a group)."""
+    xr = x.detach().reshape(2 * M, N)
+    if keep is None:
+        return _gemm(_halves(a, M), wbs, M, N, K, bias=bs, out_f32=True, r=_halves(xr, M))
+    y = torch.empty(2 * M, N, device=a.device, dtype=torch.float32)
+    B = keep.shape[0] // 2
+    for m, (am, ym, xm) in enumerate(zip(_halves(a, M), _halves(y, M), _halves(xr, M))):
+        _gemm(am, wbs[m], M, N, K, bias=bs[m], out_f32=True, r=xm, c=ym, row_scale=keep[m * B:(m + 1) * B],
+              row_scale_div=rows)
+    return y
+
+
+class _HipLinearResidual2(torch.autograd.Function):
+    """_HipLinearResidual for the two modalities: x [2B][ntok][N] fp32, a [2M][K], keep [2B] or None."""
+
+    @staticmethod
+    def forward(ctx, x, a, w0, b0, w1, b1, keep):
+        M2, K = a.shape
+        M, N = M2 // 2, w0.shape[0]
+        a = a.contiguous()
+        wbs = (_bf16_weight(w0), _bf16_weight(w1))
+        rows = M2 // keep.shape[0] if keep is not None else 1
+        y = _residual_gemm2(a, wbs, (b0.detach(), b1.detach()), x, keep, M, N, K, rows)
+        ctx.save_for_backward(a, *wbs, keep)
+        ctx.rows = rows
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dout):
+        a, wb0, wb1, keep = ctx.saved_tensors
+        M2, K = a.shape
+        M, N = M2 // 2, wb0.shape[0]
+        dy = _scaled_bf16(dout.reshape(M2, N), keep, ctx.rows)
+        da = _dx2(dy, (wb0, wb1), M, N, K) if ctx.needs_input_grad[1] else None
+        (dw0, db0), (dw1, db1) = _weight_grads2(dy, a, M, N, K)
+        return dout, da, dw0, db0, dw1, db1, None
+
+
+class _HipMlpResidual2(torch.autograd.Function):
+    """_HipMlpResidual for the two modalities: fc1 (GELU epilogue, pre-activation stored) as one grouped GEMM,
+    fc2 + DropPath + residual as _residual_gemm2, the backward's four GEMMs grouped."""
+
+    @staticmethod
+    def forward(ctx, x, xn, w10, b10, w20, b20, w11, b11, w21, b21, keep):
+        M2, C = xn.shape
+        M, F4 = M2 // 2, w10.shape[0]
+        xn = xn.contiguous()
+        wb1 = (_bf16_weight(w10), _bf16_weight(w11))
+        wb2 = (_bf16_weight(w20), _bf16_weight(w21))
+        rows = M2 // keep.shape[0] if keep is not None else 1
+        hp = torch.empty(M2, F4, device=xn.device, dtype=torch.bfloat16)
+        h = _gemm(_halves(xn, M), wb1, M, F4, C, bias=(b10.detach(), b11.detach()), act=1, c2=_halves(hp, M),
+                  c2_copy=2)
+        y = _residual_gemm2(h, wb2, (b20.detach(), b21.detach()), x, keep, M, C, F4, rows)
+        ctx.save_for_backward(xn, *wb1, *wb2, h, hp, keep)
+        ctx.rows = rows
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dout):
+        xn, wb10, wb11, wb20, wb21, h, hp, keep = ctx.saved_tensors
+        M2, C = xn.shape
+        M, F4 = M2 // 2, wb10.shape[0]
+        dy = _scaled_bf16(dout.reshape(M2, C), keep, ctx.rows)
+        dhp = _dx2(dy, (wb20, wb21), M, C, F4, act=5, r=hp)
+        (dw20, db20), (dw21, db21) = _weight_grads2(dy, h, M, C, F4)
+        dxn = _dx2(dhp, (wb10, wb11), M, F4, C) if ctx.needs_input_grad[1] else None
+        (dw10, db10), (dw11, db11) = _weight_grads2(dhp, xn, M, F4, C)
+        return dout, dxn, dw10, db10, dw20, db20, dw11, db11, dw21, db21, None
 
 
 class _HipMamAttention(torch.autograd.Function):
@@ -566,6 +711,21 @@ class HipOps:
         return _HipMlpResidual.apply(x, xn, w1, b1, w2, b2, keep)
 
     @staticmethod
+    def linear2(x, w0, b0, w1, b1, out_f32=False):
+        """Linear of the stacked modalities, rows [0, M) with (w0, b0) and [M, 2M) with (w1, b1) (_HipLinear2)."""
+        return _HipLinear2.apply(x, w0, b0, w1, b1, out_f32)
+
+    @staticmethod
+    def linear_residual2(x, a, w0, b0, w1, b1, keep):
+        """linear_residual of the stacked modalities (_HipLinearResidual2; keep [2B] or None)."""
+        return _HipLinearResidual2.apply(x, a, w0, b0, w1, b1, keep)
+
+    @staticmethod
+    def mlp_residual2(x, xn, p0, p1, keep):
+        """mlp_residual of the stacked modalities; p0 / p1 = (w1, b1, w2, b2) of each (_HipMlpResidual2)."""
+        return _HipMlpResidual2.apply(x, xn, *p0, *p1, keep)
+
+    @staticmethod
     def mam_attention(qkv, n_t, heads):
         return _HipMamAttention.apply(qkv, n_t, heads)
 
@@ -701,6 +861,51 @@ def backbone_forward(bb, t, o, s, ops, drop_path_rate=DROP_PATH_RATE):
         x = _mlp_residual(ops, x, xn.view(B * ntok, C), blk.mlp, dp, bb.training)
     xs = x[:, n_t:]
     return xs.transpose(1, 2).reshape(B, C, gs, gs)
+
+
+def backbone_forward_pair(bv, bi, t, o, s, ops, drop_path_rate=DROP_PATH_RATE):
+    """backbone_forward of the two-stream model's RGB (bv) and TIR (bi) backbones in lockstep, the
+    modalities stacked on the batch ([rgb; tir], t / o / s pairs of (B, 3, H, W)): the same math per
+    modality (mixformer.py:231-259, own weights, own norms, own DropPath draws), but every Linear and
+    every gradient GEMM one grouped launch for both, and one attention / LayerNorm launch over 2B
+    sequences.  Returns (s_v, s_i), each (B, C, gs, gs) fp32."""
+    B = t[0].shape[0]
+    C = bv.pos_embed_s.shape[-1]
+    H = C // 64
+    gt, gs = bv.grid_size_t, bv.grid_size_s
+    ntok, n_t = 2 * gt * gt + gs * gs, 2 * gt * gt
+    patches = torch.cat([_patches(torch.cat(x, 0)) for x in (t, o, s)], 1)  # (2B, ntok, 3*256)
+    wv, wi = bv.patch_embed.proj.weight, bi.patch_embed.proj.weight
+    x = ops.linear2(patches.reshape(2 * B * ntok, -1).to(ops.dtype), wv.reshape(wv.shape[0], -1),
+                    bv.patch_embed.proj.bias, wi.reshape(wi.shape[0], -1), bi.patch_embed.proj.bias, out_f32=True)
+    pos = torch.stack([torch.cat([bb.pos_embed_t, bb.pos_embed_t, bb.pos_embed_s], 1) for bb in (bv, bi)], 0)
+    x = (x.view(2, B, ntok, C) + pos).view(2 * B, ntok, C)
+    depth = len(bv.blocks)
+    M2 = 2 * B * ntok
+    for li, (kv, ki) in enumerate(zip(bv.blocks, bi.blocks)):
+        dp = drop_path_rate * li / max(depth - 1, 1)
+        keep = _keep(x, dp, bv.training)
+        xn = _layer_norm(ops, x, kv.norm1, ki.norm1)
+        qkv = ops.linear2(xn.view(M2, C), kv.attn.qkv.weight, kv.attn.qkv.bias, ki.attn.qkv.weight,
+                          ki.attn.qkv.bias).view(2 * B, ntok, 3 * C)
+        a = ops.mam_attention(qkv, n_t, H).view(M2, C)
+        x = ops.linear_residual2(x, a, kv.attn.proj.weight, kv.attn.proj.bias, ki.attn.proj.weight,
+                                 ki.attn.proj.bias, keep)
+        keep = _keep(x, dp, bv.training)
+        xn = _layer_norm(ops, x, kv.norm2, ki.norm2)
+        mp = [(k.mlp.fc1.weight, k.mlp.fc1.bias, k.mlp.fc2.weight, k.mlp.fc2.bias) for k in (kv, ki)]
+        x = ops.mlp_residual2(x, xn.view(M2, C), mp[0], mp[1], keep)
+    xs = x[:, n_t:].transpose(1, 2).reshape(2 * B, C, gs, gs)
+    return xs[:B], xs[B:]
+
+
+def _backbones_rgbt(net, template, online_template, search, ops, dpr):
+    """(s_v, s_i) of the two-stream model: the lockstep pair when the ops provide grouped Linears (HipOps),
+    else one backbone after the other."""
+    if PAIR and getattr(ops, "linear2", None) is not None:
+        return backbone_forward_pair(net.backbone_v, net.backbone_i, template, online_template, search, ops, dpr)
+    return (backbone_forward(net.backbone_v, template[0], online_template[0], search[0], ops, dpr),
+            backbone_forward(net.backbone_i, template[1], online_template[1], search[1], ops, dpr))
 
 
 def backbone_forward_stacked(bb, t, o, s, ops, asym=False, drop_path_rate=DROP_PATH_RATE):
@@ -895,8 +1100,7 @@ def forward_boxes(net, template, online_template, search, ops):
     """MixFormer_RGBT.forward (mixformer.py:366-395) + forward_box_head (:419-432): pred_boxes
     (B, 1, 4) cxcywh.  Stochastic depth at the module's drop_path_rate (as module_forward)."""
     dpr = getattr(net, "drop_path_rate", DROP_PATH_RATE)
-    s_v = backbone_forward(net.backbone_v, template[0], online_template[0], search[0], ops, dpr)
-    s_i = backbone_forward(net.backbone_i, template[1], online_template[1], search[1], ops, dpr)
+    s_v, s_i = _backbones_rgbt(net, template, online_template, search, ops, dpr)
     with torch.autocast(s_v.device.type, dtype=torch.bfloat16, enabled=s_v.device.type == "cuda"):
         fused = fusion_forward(net.fusion_vi, s_v, s_i, ops)
         xyxy = head_forward(net.box_head, fused, ops)
@@ -915,8 +1119,7 @@ def module_forward(net, template, online_template, search, ops, run_score_head=F
     variant = net.variant
     dpr = getattr(net, "drop_path_rate", DROP_PATH_RATE)
     if variant == "rgbt":
-        s_v = backbone_forward(net.backbone_v, template[0], online_template[0], search[0], ops, dpr)
-        s_i = backbone_forward(net.backbone_i, template[1], online_template[1], search[1], ops, dpr)
+        s_v, s_i = _backbones_rgbt(net, template, online_template, search, ops, dpr)
         tok = None
     elif variant in ("shared", "asym", "asym_online"):
         feats, tok = backbone_forward_stacked(net.backbone, torch.cat(template, 0), torch.cat(online_template, 0),

@@ -811,3 +811,56 @@ def test_train_step_graph_replay_matches_eager():
     torch.cuda.synchronize()
     after = [p.detach() for p in net_b.parameters() if p.requires_grad][:4]
     assert any(not torch.equal(a, b) for a, b in zip(before, after))
+
+
+@pytest.mark.parametrize("drop", [False, True])
+def test_hip_lockstep_pair_functions(drop):
+    """HipOps.linear2 / linear_residual2 / mlp_residual2 (the two-stream backbones in lockstep: rows [0, M)
+    with the RGB weights, [M, 2M) with the TIR weights, grouped GEMMs forward and backward, per-modality
+    launches for the DropPath row scale) against torch fp32 autograd on the bf16 operands, per half:
+    outputs and every gradient within 2e-2 of the largest magnitude, as the one-modality Functions."""
+    from mmt_amd.train import HipOps
+    g = torch.Generator().manual_seed(31)
+    B, ntok, C, F4 = 4, 264, 768, 3072
+    M = B * ntok
+    F = torch.nn.functional
+    x = torch.randn(2 * B, ntok, C, generator=g)
+    a = torch.randn(2 * M, C, generator=g).bfloat16()
+    lin = [[torch.randn(C, C, generator=g) / math.sqrt(C), torch.randn(C, generator=g) * 0.1] for _ in range(2)]
+    mlp = [[torch.randn(F4, C, generator=g) / math.sqrt(C), torch.randn(F4, generator=g) * 0.1,
+            torch.randn(C, F4, generator=g) / math.sqrt(F4), torch.randn(C, generator=g) * 0.1] for _ in range(2)]
+    dy = torch.randn(2 * B, ntok, C, generator=g)
+    keep = torch.tensor([1 / 0.9, 0.0, 1 / 0.9, 1 / 0.9, 0.0, 1 / 0.9, 1 / 0.9, 1 / 0.9]) if drop else None
+
+    def run(kind, xd, ad, ps):
+        if kind == "linear2":
+            return HipOps.linear2(ad, *ps[0], *ps[1], out_f32=True)
+        if kind == "linear_residual2":
+            return HipOps.linear_residual2(xd, ad, *ps[0], *ps[1], keep.cuda() if drop else None)
+        return HipOps.mlp_residual2(xd, ad, ps[0], ps[1], keep.cuda() if drop else None)
+
+    def ref_branch(kind, u, ps):
+        return F.linear(u, ps[0], ps[1]) if kind != "mlp_residual2" else \
+            F.linear(F.gelu(F.linear(u, ps[0], ps[1])), ps[2], ps[3])
+
+    for kind, params in (("linear2", lin), ("linear_residual2", lin), ("mlp_residual2", mlp)):
+        xd = x.cuda().requires_grad_(True)
+        ad = a.cuda().requires_grad_(True)
+        ps = [[t.cuda().requires_grad_(True) for t in pm] for pm in params]
+        y = run(kind, xd, ad, ps)
+        y.backward(dy.cuda().view(y.shape))
+        got = [y.detach().cpu().view(2 * B, ntok, C), ad.grad.float().cpu()] + [t.grad.cpu() for pm in ps for t in pm]
+        if kind != "linear2":
+            got.append(xd.grad.cpu())
+        xr = x.clone().requires_grad_(True)
+        ar = a.float().requires_grad_(True)
+        rs = [[(t.bfloat16().float() if t.dim() == 2 else t.clone()).requires_grad_(True) for t in pm] for pm in params]
+        br = torch.cat([ref_branch(kind, ar[:M], rs[0]), ref_branch(kind, ar[M:], rs[1])], 0).view(2 * B, ntok, C)
+        yr = br if kind == "linear2" else xr + (br * keep.view(-1, 1, 1) if drop else br)
+        yr.backward(dy)
+        ref = [yr.detach(), ar.grad] + [t.grad for pm in rs for t in pm]
+        if kind != "linear2":
+            ref.append(xr.grad)
+        for i, (u, v) in enumerate(zip(got, ref)):
+            err = (u - v).abs().max().item() / max(1.0, v.abs().max().item())
+            assert err <= 2e-2, (kind, i, err)

@@ -106,6 +106,49 @@ def test_forward_and_grads_match_oracle():
         assert (g - rg).abs().max().item() <= 1e-3 * rg.abs().max().item() + 1e-6, k
 
 
+class TorchPairOps(TorchOps):
+    """TorchOps with the grouped two-modality Linears of HipOps (linear2 / linear_residual2 / mlp_residual2):
+    rows [0, M) take the first weights, rows [M, 2M) the second; keep [2B] scales the branch per sequence."""
+
+    @staticmethod
+    def linear2(x, w0, b0, w1, b1, out_f32=False):
+        h = x.shape[0] // 2
+        return torch.cat([F.linear(x[:h], w0, b0), F.linear(x[h:], w1, b1)], 0)
+
+    @staticmethod
+    def linear_residual2(x, a, w0, b0, w1, b1, keep):
+        y = TorchPairOps.linear2(a, w0, b0, w1, b1).view(x.shape)
+        return x + (y if keep is None else y * keep.view(-1, 1, 1))
+
+    @staticmethod
+    def mlp_residual2(x, xn, p0, p1, keep):
+        h = xn.shape[0] // 2
+        y = torch.cat([F.linear(F.gelu(F.linear(u, p[0], p[1])), p[2], p[3]) for u, p in ((xn[:h], p0), (xn[h:], p1))],
+                      0).view(x.shape)
+        return x + (y if keep is None else y * keep.view(-1, 1, 1))
+
+
+def test_lockstep_backbone_pair_matches_sequential():
+    """backbone_forward_pair (both backbones in lockstep on the stacked batch, HipOps' grouped-GEMM form)
+    against backbone_forward run once per modality: boxes, loss and every parameter gradient (eval-mode
+    module: no stochastic depth draws, so both forms compute the same function)."""
+    from mmt_amd import train
+    torch.set_num_threads(8)
+    t, o, s, gt = _batch(2, 3)
+    out = []
+    for ops in (TorchOps, TorchPairOps):
+        net = _net(seed=1)
+        pred = train.forward_boxes(net, t, o, s, ops)
+        loss, _ = train.box_loss(pred, gt)
+        loss.backward()
+        out.append((pred.detach(), {k: p.grad for k, p in net.named_parameters() if p.requires_grad}))
+    (p0, g0), (p1, g1) = out
+    assert (p0 - p1).abs().max().item() < 1e-5
+    for k, g in g0.items():
+        assert g1[k] is not None, k
+        assert (g - g1[k]).abs().max().item() <= 1e-4 * g.abs().max().item() + 1e-7, k
+
+
 def test_param_groups_follow_reference():
     from mmt_amd.train import param_groups
     net = _net()

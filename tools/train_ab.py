@@ -34,6 +34,7 @@ class UnfusedResidualOps(HipOps):
     """HipOps with the blocks' residual branches as GEMM + addcmul (DropPath) + autograd's adds."""
     linear_residual = None
     mlp_residual = None
+    linear2 = None  # (the lockstep pair needs the fused residual Functions)
 
 
 class SplitMlpOps(HipOps):
@@ -99,6 +100,17 @@ def aten_scale_cast():
         train._scaled_bf16 = saved
 
 
+@contextlib.contextmanager
+def sequential_backbones():
+    """The two-stream backbones one after the other (one-group GEMMs) instead of backbone_forward_pair."""
+    from mmt_amd import train
+    train.PAIR = False
+    try:
+        yield
+    finally:
+        train.PAIR = True
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
@@ -109,7 +121,8 @@ def main():
     args = ap.parse_args()
     variants = {"hip": HipOps, "aten_groupnorm": AtenGroupNormOps, "aten_layernorm": AtenLayerNormOps,
                 "split_mlp": SplitMlpOps, "unfused_residual": UnfusedResidualOps, "accum_grads": (HipOps, accumulated_grads),
-                "transposed": (HipOps, transposed_copies), "aten_scale_cast": (HipOps, aten_scale_cast)}
+                "transposed": (HipOps, transposed_copies), "aten_scale_cast": (HipOps, aten_scale_cast),
+                "sequential": (HipOps, sequential_backbones)}
     if args.only:
         variants = {k: v for k, v in variants.items() if k in args.only.split(",")}
     for r in range(args.rounds):
