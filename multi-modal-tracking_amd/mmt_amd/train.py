@@ -302,7 +302,8 @@ class _HipMlpResidual(torch.autograd.Function):
 # -- the two-stream backbones in lockstep: the RGB rows [0, M) and the TIR rows [M, 2M) of one stacked
 # operand, each modality with its own weights, as one grouped GEMM (groups 2) per Linear and per gradient.
 # One modality's dW GEMM (768-3080 output columns, K = the 8448 tokens of 16 pairs) is a 42-168 tile grid on
-# 256 CUs; the pair fills the chip twice as well (tools/dw_split_ab.py: 250-425 TFLOP/s at one group).
+# 256 CUs; the pair fills the chip twice as well (tools/dw_split_ab.py: 250-425 TFLOP/s at one group, 390-595
+# at two; the step 417 -> 462 samples/s, profiles/r04_train_pair_ab.jsonl).
 def _halves(t, M):
     return t[:M], t[M:]
 
@@ -353,7 +354,8 @@ class _HipLinear2(torch.autograd.Function):
 
 def _residual_gemm2(a, wbs, bs, x, keep, M, N, K, rows):
     """x + keep * (a W_m^T + b_m) for both halves, fp32 [2M][N]: one grouped launch without stochastic depth;
-    with it one launch per modality (the row scale is one vector indexed by the row within a group)."""
+    with it one launch per modality (the row scale is one vector indexed by the row within a group; a
+    per-group index and so one launch measured no faster: 458.6 vs 462.1 samples/s on the step)."""
     xr = x.detach().reshape(2 * M, N)
     if keep is None:
         return _gemm(_halves(a, M), wbs, M, N, K, bias=bs, out_f32=True, r=_halves(xr, M))
