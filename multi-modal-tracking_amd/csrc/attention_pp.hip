@@ -32,6 +32,11 @@
 // Results are bit-identical to impl 22 (same MFMA order per accumulator, same exponentials).
 #include "attn_common.hpp"
 
+#ifndef MMT_ATTN_AB
+#define MMT_ATTN_AB 0
+#endif
+#if MMT_ATTN_AB  // A/B build only (tools/build_ablate.sh ab): not faster than impl 22 / 4 anywhere
+
 namespace {
 
 // MMT_ATTN_ABLATE (measurement builds only, tools/build_ablate.sh; results are wrong): 1 = no K / V DMA
@@ -579,3 +584,4 @@ int mmt_attn_launch_pp(const mmt_attn_params& p, int ks, hipStream_t st) {
     else hipLaunchKernelGGL(mam_attention_pp_kernel<1>, dim3(nqb, p.H, p.S), dim3(128), 0, st, p);
     return 0;
 }
+#endif  // MMT_ATTN_AB

@@ -144,7 +144,11 @@ class Attention_Fusion_Bimodal_LNSpecific(nn.Module):
 
 
 class FrozenBatchNorm2d(nn.Module):
-    """lib/models/mixformer_cvt/utils.py:21-57 (buffers only)."""
+    """lib/models/mixformer_cvt/utils.py:21-57: fixed statistics and affine (buffers); eps 1e-5 inside the
+    rsqrt as the reference's.  The inference runtime folds it into the conv; training's head on the HIP ops
+    computes it with mmt_batchnorm_relu in eval mode (train.HipOps.bn_relu)."""
+
+    eps = 1e-5
 
     def __init__(self, n):
         super().__init__()
@@ -152,6 +156,16 @@ class FrozenBatchNorm2d(nn.Module):
         self.register_buffer("bias", torch.zeros(n))
         self.register_buffer("running_mean", torch.zeros(n))
         self.register_buffer("running_var", torch.ones(n))
+
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys,
+                              error_msgs):
+        state_dict.pop(prefix + "num_batches_tracked", None)  # utils.py:37-45
+        super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys,
+                                      error_msgs)
+
+    def forward(self, x):  # utils.py:47-57
+        scale = self.weight.reshape(1, -1, 1, 1) * (self.running_var.reshape(1, -1, 1, 1) + self.eps).rsqrt()
+        return x * scale + (self.bias.reshape(1, -1, 1, 1) - self.running_mean.reshape(1, -1, 1, 1) * scale)
 
 
 def conv(cin, cout, freeze_bn=False):

@@ -89,9 +89,17 @@ class HipAdamW(torch.optim.Optimizer):
             raise ValueError("HipAdamW keeps one step counter for all parameters; the state_dict has %d "
                              "different per-parameter steps" % len(steps))
         dev = next(p for g in self.groups for p in g["params"]).device
-        for p, st in self.state.items():  # own copies of the moments on the parameter's device, contiguous fp32
-            for k in ("exp_avg", "exp_avg_sq"):  # (Optimizer.load_state_dict keeps the source's tensors when
-                st[k] = torch.empty_like(p).copy_(st[k])  # device and dtype match: updated in place here)
+        # Optimizer.load_state_dict keeps entries only for the parameters the saved state has: a
+        # torch.optim.AdamW state_dict written before its first step, or one where a parameter never had a
+        # gradient, leaves others without moments.  Those start from zero moments (what torch.optim.AdamW
+        # would do at their first gradient); they share the device step counter for the bias corrections.
+        for g in self.groups:
+            for p in g["params"]:
+                st = self.state[p]
+                for k in ("exp_avg", "exp_avg_sq"):  # own contiguous fp32 copies on the parameter's device
+                    # (Optimizer.load_state_dict keeps the source's tensors when device and dtype match:
+                    # they are updated in place here)
+                    st[k] = torch.empty_like(p).copy_(st[k]) if k in st else torch.zeros_like(p)
         self._device_state(dev).view(torch.int32)[4] = int(steps.pop()) if steps else 0
         self.step_count = int(self._state.view(torch.int32)[4].item())
         self._key = None  # the moment tensors are new: rebuild the device tables at the next step

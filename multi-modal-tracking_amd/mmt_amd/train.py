@@ -32,6 +32,8 @@ import math
 import torch
 import torch.nn.functional as F
 
+from .model import FrozenBatchNorm2d
+
 LOG2E = 1.4426950408889634
 
 
@@ -580,7 +582,10 @@ class _HipBatchNormReLU(torch.autograd.Function):
                                          weight.data_ptr() if weight is not None else None, save.data_ptr(),
                                          int(ctx.training), 1, dgb.data_ptr(), ws.data_ptr(), ctx.nws, _stream()),
               "mmt_batchnorm_relu_bwd")
-        return dx, dgb[0], dgb[1], None, None, None, None, None, None
+        # weight / bias may be None (affine=False) or buffers (FrozenBatchNorm2d): no gradient for those
+        dw = dgb[0] if ctx.needs_input_grad[1] else None
+        db = dgb[1] if ctx.needs_input_grad[2] else None
+        return dx, dw, db, None, None, None, None, None, None
 
 
 class _HipConv3x3(torch.autograd.Function):
@@ -746,6 +751,14 @@ class HipOps:
         """bn (nn.BatchNorm2d) then ReLU on an NHWC bf16 map (_HipBatchNormReLU), with the module's training /
         eval semantics: batch statistics when training or not tracking, running statistics updated (and
         num_batches_tracked advanced) when training and tracking."""
+        if isinstance(bn, FrozenBatchNorm2d):  # fixed statistics and affine (buffers): eval semantics
+            C = x.shape[-1]
+            x = x.to(torch.bfloat16)
+            if C % 8:
+                x = F.pad(x, (0, (C + 7) // 8 * 8 - C))
+            y = _HipBatchNormReLU.apply(x.contiguous(), bn.weight, bn.bias, bn.running_mean, bn.running_var, 0.0,
+                                        bn.eps, False, C)
+            return y if y.shape[-1] == C else y[..., :C]
         training = bn.training or not bn.track_running_stats
         update = bn.training and bn.track_running_stats
         if update:
@@ -1038,6 +1051,24 @@ def _soft_argmax(score_map, stride):
     return (coord_x * prob).sum(1), (coord_y * prob).sum(1)
 
 
+def _hip_bn_ok(bn):
+    """The conv() block norms the HIP batch norm computes with the module's own semantics: BatchNorm2d with a
+    momentum, SyncBatchNorm when its statistics are local (eval, or a process group of one rank: SyncBatchNorm
+    then runs F.batch_norm itself), and FrozenBatchNorm2d (fixed statistics and affine, lib/models/mixformer_cvt/
+    utils.py:21-57)."""
+    if isinstance(bn, FrozenBatchNorm2d):
+        return True
+    if type(bn) is torch.nn.SyncBatchNorm:
+        if bn.momentum is None:
+            return False
+        if not bn.training:
+            return True
+        import torch.distributed as dist
+        pg = bn.process_group
+        return not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(pg) == 1
+    return type(bn) is torch.nn.BatchNorm2d and bn.momentum is not None
+
+
 def head_forward_nhwc(hd, x, ops):
     """head_forward with NHWC maps and the 3x3 convolutions on ops.conv3x3 (HIP): every conv() block =
     conv (HIP) -> BatchNorm2d + ReLU on ops.bn_relu (HIP, the module's statistics semantics and running-stat
@@ -1052,12 +1083,11 @@ def head_forward_nhwc(hd, x, ops):
     def block(seq, t):  # conv(): Conv2d 3x3 + BN + ReLU (head.py:7-20)
         y = ops.conv3x3(t.contiguous(), seq[0].weight, seq[0].bias)
         bn = seq[1]
-        if (bn_relu is not None and type(bn) is torch.nn.BatchNorm2d and type(seq[2]) is torch.nn.ReLU and
-                bn.momentum is not None):
+        if bn_relu is not None and type(seq[2]) is torch.nn.ReLU and _hip_bn_ok(bn):
             return bn_relu(y, bn)  # HIP batch norm + ReLU on the NHWC map
-        # other norms (SyncBatchNorm under DDP: its RCCL statistics; FrozenBatchNorm2d): the module on a
-        # contiguous NCHW map as the reference runs it (MIOpen's batch norm on the channels-last view of a
-        # bf16 map crashed in train mode)
+        # SyncBatchNorm in a process group of more than one rank (its RCCL statistics) and cumulative-average
+        # BatchNorm (momentum None): the module on a contiguous NCHW map as the reference runs it (MIOpen's
+        # batch norm on the channels-last view of a bf16 map crashed in train mode: DESIGN.md §7)
         return nhwc(seq[2](bn(nchw(y).contiguous()))).contiguous()
 
     def c1(mod, t):  # Conv2d(48, 1, 1) on channels-last rows

@@ -78,9 +78,10 @@ def test_bad_arguments_rejected_without_gpu_work():
 
 
 def test_attention_impl_and_lse_gate():
-    """mmt_mam_attention takes impl 0 (library choice), 4, 8, 17, 21, 22, 24, 25 only (the round-2 A/B-only
-    kernels 2, 9-12, 16, 18-20 are no longer in the library; 23 is in the A/B build only); impls 22 - 25
-    never write the log-sum-exp
+    """mmt_mam_attention takes impl 0 (library choice), 4, 8, 17, 21, 22 only (the round-2 A/B-only
+    kernels 2, 9-12, 16, 18-20 are no longer in the library; 23-28 -- incl. round 4's one-wave-per-SIMD
+    impl 24 / 25 and round 5's ping-pong impl 28 -- are in the A/B build only); impl 22 never writes the
+    log-sum-exp
     the training backward consumes, so lse with them is rejected; fp16 takes the running-maximum kernels
     only.  Every case fails validation on the host, before a launch."""
     from mmt_amd import _lib
@@ -93,13 +94,10 @@ def test_attention_impl_and_lse_gate():
             setattr(a, k, v)
         return _lib.LIB.mmt_mam_attention(ctypes.byref(a), dt, None)
 
-    for impl in (2, 9, 10, 11, 12, 16, 18, 19, 20, 23, 26, 27, 99):
+    for impl in (2, 9, 10, 11, 12, 16, 18, 19, 20, 23, 24, 25, 26, 27, 28, 99):
         assert attn(impl=impl) == -10000, impl
     assert attn(impl=22, lse=fake) == -10000
     assert attn(impl=23, lse=fake) == -10000
-    assert attn(impl=24, lse=fake) == -10000
-    assert attn(impl=25, lse=fake) == -10000
-    assert attn(dt=_lib.MMT_F16, impl=24) == -10000
     assert attn(dt=_lib.MMT_F16, impl=17) == -10000
     assert attn(dt=_lib.MMT_F16, lse=fake) == -10000
 

@@ -426,6 +426,51 @@ def test_hip_adamw_state_dict_resume_and_scheduler():
         assert torch.allclose(a["exp_avg"], b["exp_avg"], rtol=1e-5, atol=1e-6)  # fma vs torch's lerp
 
 
+def test_hip_adamw_load_state_dict_with_missing_entries():
+    """a torch.optim.AdamW state_dict saved before its first step (no per-parameter state)
+    and one where a parameter never had a gradient both load into HipAdamW; the next steps run (zero
+    moments for the missing entries) and match torch.optim.AdamW resumed from the same state_dict."""
+    from mmt_amd.optim import HipAdamW
+    g = torch.Generator().manual_seed(11)
+    shapes = [(40,), (8, 9)]
+    init = [torch.randn(s, generator=g) for s in shapes]
+    grads = [[torch.randn(s, generator=g).cuda() for s in shapes] for _ in range(2)]
+    # (a) empty state: both continue from t = 1
+    ref = [torch.nn.Parameter(t.clone().cuda()) for t in init]
+    opt_ref = torch.optim.AdamW(ref, lr=1e-3, weight_decay=0.01)
+    hip = [torch.nn.Parameter(t.clone().cuda()) for t in init]
+    opt = HipAdamW([{"params": hip, "lr": 1e-3}], weight_decay=0.01)
+    opt.load_state_dict(opt_ref.state_dict())
+    for k in range(2):
+        for p, q, gr in zip(ref, hip, grads[k]):
+            p.grad, q.grad = gr.clone(), gr.clone()
+        opt_ref.step()
+        opt.step()
+    torch.cuda.synchronize()
+    for p, q in zip(ref, hip):
+        assert torch.allclose(q, p, rtol=1e-6, atol=1e-7)
+    # (b) the second parameter never had a gradient: its moments start at zero, the step continues
+    ref = [torch.nn.Parameter(t.clone().cuda()) for t in init]
+    opt_ref = torch.optim.AdamW(ref, lr=1e-3, weight_decay=0.01)
+    ref[0].grad = grads[0][0].clone()
+    opt_ref.step()
+    sd = opt_ref.state_dict()
+    assert len(sd["state"]) == 1
+    hip = [torch.nn.Parameter(p.detach().clone()) for p in ref]
+    opt = HipAdamW([{"params": hip, "lr": 1e-3}], weight_decay=0.01)
+    opt.load_state_dict(sd)
+    assert all(torch.equal(opt.state[p]["exp_avg"], torch.zeros_like(p)) for p in hip[1:])
+    for q, gr in zip(hip, grads[1]):
+        q.grad = gr.clone()
+    opt.step()
+    torch.cuda.synchronize()
+    assert all(torch.isfinite(q).all() for q in hip)
+    for p, gr in zip(ref, grads[1]):
+        p.grad = gr.clone()
+    opt_ref.step()
+    assert torch.allclose(hip[0], ref[0], rtol=1e-6, atol=1e-7)  # the parameter with state: same as torch
+
+
 
 @pytest.mark.parametrize("C,rows,two,dyt", [(768, 1056, False, "bf16"), (768, 1000, True, "bf16"), (512, 77, True, "f32"),
                                             (1024, 300, False, "f32"), (256, 33, True, "bf16")])
@@ -765,13 +810,58 @@ def test_head_forward_nhwc_matches_aten(bn_train):
     assert rel(cat[0], cat[2]) <= max(5e-2, 1.5 * rel(cat[1], cat[2])), (rel(cat[0], cat[2]), rel(cat[1], cat[2]))
 
 
+@pytest.mark.parametrize("norm", ["sync", "frozen"])
+def test_head_forward_nhwc_sync_and_frozen_bn(norm):
+    """the norms of the reference trainer's head -- SyncBatchNorm (train_script_mixformer.py:105
+    converts every head BatchNorm, even on one GPU) and FrozenBatchNorm2d (head.py:7-20 freeze_bn) -- take the
+    HIP batch norm (world size 1 / fixed statistics), run in train mode without error, and match the aten fp32
+    head on the same module within the bf16 bar of test_head_forward_nhwc_matches_aten; SyncBatchNorm updates
+    its running statistics like BatchNorm2d."""
+    import copy
+    import mmt_amd.model as M
+    import mmt_amd.train as T
+    from mmt_amd.train import HipOps, head_forward
+    torch.manual_seed(4)
+    hd = M.Pyramid_Corner_Predictor(inplanes=64, channel=64, feat_sz=20, stride=16, freeze_bn=norm == "frozen")
+    if norm == "sync":
+        hd = torch.nn.SyncBatchNorm.convert_sync_batchnorm(hd)
+        assert any(type(m) is torch.nn.SyncBatchNorm for m in hd.modules())
+    else:  # non-trivial fixed statistics
+        with torch.no_grad():
+            for m in hd.modules():
+                if isinstance(m, M.FrozenBatchNorm2d):
+                    m.weight.uniform_(0.5, 1.5)
+                    m.bias.uniform_(-0.2, 0.2)
+                    m.running_mean.uniform_(-0.2, 0.2)
+                    m.running_var.uniform_(0.5, 2.0)
+    hd = hd.cuda().train()
+    assert all(T._hip_bn_ok(m) for m in hd.modules() if isinstance(m, (torch.nn.SyncBatchNorm, M.FrozenBatchNorm2d)))
+    heads = [hd, copy.deepcopy(hd)]
+    x = torch.randn(2, 64, 20, 20, device="cuda").bfloat16().float()
+    xs = [x.clone().requires_grad_(True) for _ in heads]
+    outs = []
+    for h, xi, ops in zip(heads, xs, (HipOps, None)):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=ops is not None):
+            out = head_forward(h, xi, ops).float()
+        out.sum().backward()
+        outs.append(out.detach())
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[0]).all() and torch.isfinite(xs[0].grad).all()
+    assert (outs[0] - outs[1]).abs().max().item() <= 3e-2, outs
+    rel = ((xs[0].grad - xs[1].grad).norm() / xs[1].grad.norm()).item()
+    assert rel <= 1e-1, rel
+    if norm == "sync":
+        for (n, a), b in zip(heads[0].named_buffers(), heads[1].buffers()):
+            if "running" in n:
+                assert torch.allclose(a, b, rtol=2e-2, atol=2e-3), n
+
+
 def test_train_step_graph_replay_matches_eager():
     """TrainStep.capture / replay (the whole step -- forward on the HIP ops incl. the HIP head convs, box
     loss, backward, clip + HipAdamW -- as one hipGraph) against the same steps run eagerly from identical
-    weights on the same batches (drop-path and dropout off, BatchNorm in train mode): losses and every
-    parameter within max(2e-3 relative, 3 x the spread between two eager runs -- the MSDA backward's atomics --,
-    one AdamW step's size: noise-level gradients such as a 1-channel map's BatchNorm bias flip their update's
-    sign) after four steps (two eager warm-up steps, then two replays with new
+    weights on the same batches (drop-path and dropout off, BatchNorm in train mode): losses within
+    max(2e-3 relative, 3 x the spread between two eager runs) and every parameter's update direction over
+    the four steps at cosine >= 0.99 to the eager one (two eager warm-up steps, then two replays with new
     batches copied into the static inputs); a third replay changes the weights again (it is not a no-op)."""
     import copy
     import mmt_amd.model as M
@@ -787,6 +877,7 @@ def test_train_step_graph_replay_matches_eager():
     g = torch.Generator().manual_seed(11)
     batches = [synthetic_batch(2, "cuda", g) for _ in range(4)]
     net_c = copy.deepcopy(net)
+    p0 = [p.detach().clone() for p in net.parameters()]
     eager, graphed, eager2 = TrainStep(net, HipOps), TrainStep(net_b, HipOps), TrainStep(net_c, HipOps)
     le = [float(eager(*b)["loss"]) for b in batches]
     le2 = [float(eager2(*b)["loss"]) for b in batches]  # the eager step's own run-to-run spread (atomics)
@@ -801,14 +892,25 @@ def test_train_step_graph_replay_matches_eager():
     spread = max(abs(a - a2) for a, a2 in zip(le, le2))  # over the four steps
     for a, b in zip(le[2:], lg[1:]):
         assert abs(a - b) <= max(2e-3 * max(1.0, abs(a)), 3 * spread), (le, le2, lg)
-    bad = []
-    lr = 1e-4  # TrainStep's default: one AdamW update moves an element by about lr whatever its gradient's size
-    for (n, pa), pb, pc in zip(net.named_parameters(), net_b.parameters(), net_c.parameters()):
-        if pa.requires_grad:
-            err, pspread = (pa - pb).norm().item(), (pa - pc).norm().item()
-            if err > max(2e-3 * pa.norm().item(), 3 * pspread, lr * pa.numel() ** 0.5):
-                bad.append((n, err, pspread, pa.norm().item()))
+    # compare the update DIRECTIONS (p_after - p_before), which a replay with stale or
+    # mis-addressed gradients would turn, not only their size (AdamW moves every element by ~lr whatever
+    # its gradient).  Parameters whose two eager runs already disagree in direction (noise-level gradients,
+    # e.g. the BatchNorm bias of a 1-channel map) are exempt; they must be a small share of the elements.
+    bad, checked, total = [], 0, 0
+    cos = torch.nn.functional.cosine_similarity
+    for (n, pa), pb, pc, pi in zip(net.named_parameters(), net_b.parameters(), net_c.parameters(), p0):
+        if not pa.requires_grad:
+            continue
+        de, dg, de2 = (pa - pi).flatten(), (pb - pi).flatten(), (pc - pi).flatten()
+        total += pa.numel()
+        if de.norm() == 0 or cos(de, de2, dim=0).item() < 0.999:
+            continue
+        checked += pa.numel()
+        c = cos(de, dg, dim=0).item()
+        if c < 0.99:
+            bad.append((n, c))
     assert not bad, bad[:5]
+    assert checked >= 0.95 * total, (checked, total)
     before = [p.detach().clone() for p in net_b.parameters() if p.requires_grad][:4]
     graphed.replay(*batches[0])
     torch.cuda.synchronize()
