@@ -260,6 +260,65 @@ def mam_batched(rt, B=32, per_graph=20, replays=10):
                                S, d.ntok, d.C, 2)
 
 
+def golden_box_err(variant, dtype):
+    """Box error of the forward in `dtype` against the reference-made golden of `variant` at B = 1
+    (tests/golden/model_<variant>_b1.npz: the reference's outputs for its own synthetic weights and inputs,
+    tests/golden/make_golden.py), measured in this run (None when the variant has no golden)."""
+    import json as _json
+    import numpy as np
+    from mmt_amd import synthetic
+    from mmt_amd.runtime import MixFormerRGBTRuntime
+    gdir = os.path.join(ROOT, "tests", "golden")
+    gpath, kpath = os.path.join(gdir, "model_%s_b1.npz" % variant), os.path.join(gdir, "state_dict_%s.json" % variant)
+    if not (os.path.exists(gpath) and os.path.exists(kpath)):
+        return None
+    keys = _json.load(open(kpath))
+    sd = {k: torch.from_numpy(v) for k, v in synthetic.synth_state_dict(keys).items()}
+    rt = MixFormerRGBTRuntime(sd, variant, dtype=dtype)
+    t, o, s = [[x.cuda() for x in z] for z in synthetic.synth_inputs(1)]
+    box, _ = rt.forward(t, o, s)
+    torch.cuda.synchronize()
+    gold = np.load(gpath)["pred_boxes"].reshape(1, 4)
+    return float(np.abs(box.cpu().numpy() - gold).max())
+
+
+def tracker_step(sd, variant, steps, warmup, H=480, W=640):
+    """The tracking loop's per-frame rate (the reference's per-frame time covers crop, H2D and the
+    D2H sync, tracker_rgbt.py:172-179): RGBTTrackerCore.track on a pair of uint8 (H, W, 3) frames already resident
+    in HBM -- the frame copy into the tracker's buffers, ONE hipGraph replay (both search crops with the resize /
+    normalise, the full template + search forward, map-back and clip on the device) and the `.tolist()` of the new
+    state, the step's one host round trip.  Synthetic frames and random-init weights: the predicted box wanders, so
+    the state is put back to the initial box before every frame (a 32-byte device copy) to keep the crops
+    stationary.  Beside the model-only `value`, not instead."""
+    if variant != "rgbt":
+        return None
+    from mmt_amd import model as M
+    from mmt_amd.tracking import RGBTTrackerCore
+    net = M.build_mixformer_vit_rgbt(M.hot_path_cfg(), train=False)
+    net.load_state_dict(sd, strict=True)
+    net = net.cuda().eval()
+    g = torch.Generator().manual_seed(5)
+    frames = [[torch.randint(0, 256, (H, W, 3), generator=g, dtype=torch.uint8).cuda() for _ in range(2)]
+              for _ in range(4)]
+    core = RGBTTrackerCore(net, 2.0, 128, 5.0, 320, [200], multimodal=False)
+    init = [W * 0.4, H * 0.4, 64.0, 48.0]
+    core.initialize(frames[0], init)
+    init_state = core.state.clone()
+    for i in range(warmup):
+        core.state.copy_(init_state)
+        core.track(frames[i % len(frames)])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        core.state.copy_(init_state)
+        core.track(frames[i % len(frames)])
+    el = time.perf_counter() - t0  # track() ends in a host sync (.tolist())
+    return {"value": round(steps / el, 2), "unit": "frames/s", "ms_per_frame": round(el / steps * 1e3, 4),
+            "frame": [H, W], "hip_graph": core._graph is not None,
+            "note": "RGBTTrackerCore.track per frame: uint8 frames resident, crop + resize + normalise + forward + "
+                    "map-back + clip as one hipGraph replay, plus the host round trip of the new box"}
+
+
 def fp16_line(sd, variant, pool, score, steps, warmup):
     """The headline workload with the fp16 compute type (same kernels, fp16 operands): its boxes meet
     the north star's 1e-3 on the reference goldens (<= 5.4e-4, tests/test_gpu_model.py) where bf16's
@@ -277,7 +336,9 @@ def fp16_line(sd, variant, pool, score, steps, warmup):
     el = time.perf_counter() - t0
     B = pool[0][0][0].shape[0]
     return {"value": round(B * steps / el, 2), "unit": "frames/s", "ms_per_step": round(el / steps * 1e3, 4),
-            "dtype": "fp16", "box_err_vs_reference": "<= 5.4e-4 (fp16) vs 1.3-3.5e-3 (bf16) on the goldens"}
+            "dtype": "fp16", "box_err_vs_reference": golden_box_err(variant, torch.float16),
+            "box_err_vs_reference_bf16": golden_box_err(variant, torch.bfloat16),
+            "box_err_note": "max |box - reference golden| at B = 1, measured in this run (tests/golden)"}
 
 
 def kv_cache_tracking(rt, pool, score, steps, warmup):
@@ -545,6 +606,7 @@ def main():
     ap.add_argument("--no-mam-batched", action="store_true", help="skip the batched MAM attention roofline")
     ap.add_argument("--no-kv-cache", action="store_true", help="skip the template K/V cache tracking-rate line")
     ap.add_argument("--no-fp16-line", action="store_true", help="skip the fp16 rate of the same workload")
+    ap.add_argument("--no-tracker-line", action="store_true", help="skip the tracking-loop (crop + forward + map-back) rate")
     ap.add_argument("--vitl", action="store_true",
                     help="BASELINE config 5 geometry: ViT-L (1024 wide, 24 blocks), 192px templates / 384px search")
     ap.add_argument("--total-seqs", type=int, default=0,
@@ -709,6 +771,11 @@ def main():
             out["tracking_kv_cache"] = kv_cache_tracking(rt, pool, score, args.steps, args.warmup)
         if use_graph and args.dtype == "bf16" and not args.no_fp16_line and args.variant != "asym_ce":
             out["fp16_line"] = fp16_line(sd, args.variant, pool, score, args.steps, args.warmup)
+        if use_graph and args.dtype == "bf16" and B == 1 and not args.no_tracker_line and not args.vitl:
+            try:
+                out["tracker_step"] = tracker_step(sd, args.variant, args.steps, args.warmup)
+            except Exception as e:  # noqa: BLE001  (reported, not raised: the headline line must still print)
+                out["tracker_step"] = {"error": "%s: %s" % (type(e).__name__, e)}
     if not args.no_train_line and args.variant == "rgbt" and not args.vitl and not sharded:
         # config 4's DDP step beside the replicas: the one data-path collective (RCCL gradient
         # all-reduce) is timed at every N of a scaling run; a failure is reported, not raised

@@ -210,6 +210,11 @@ typedef struct {
     int32_t tok_pitch; /* rows between consecutive sequences in qkv / out; 0 = ntok.  Candidate
                        elimination keeps each sequence's rows at the original pitch and runs on
                        its first ntok (template + surviving search) rows (not with lse). */
+    int32_t out_pitch; /* rows between consecutive sequences in out; 0 = as qkv (tok_pitch / ntok) */
+    int32_t out_q0;    /* query stored at row 0 of a sequence's out rows (0: row = query index).  The
+                          template K/V cache passes store compact activations: the template pass
+                          (q_part 1) out_pitch n_t, out_q0 0; the search pass (q_part 2) out_pitch
+                          ntok - n_t, out_q0 n_t.  Not with lse. */
 } mmt_attn_params;
 
 int mmt_mam_attention(const mmt_attn_params* p, int dtype, void* stream);

@@ -275,7 +275,7 @@ __global__ __launch_bounds__(256 / QT) void mam_attention_kernel(const mmt_attn_
         const float inv = 1.f / l;
         const int q = q0 + 16 * QT * w + 16 * qt + l16;
         if (q >= qend) continue;
-        T* op = out + ((int64_t)s * pitch + q) * C + h * D;
+        T* op = out + attn_out_row(p, s, q, pitch) * C + h * D;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) {
             if constexpr (Cfg::BF) {
@@ -532,7 +532,7 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(KG, KG
     const float inv = 1.f / lanegroup_sum(l_run);
     const int q = q0 + 16 * qw + l16;
     if (q < qend) {
-        T* op = (T*)p.out + ((int64_t)s * pitch + q) * C + h * D;
+        T* op = (T*)p.out + attn_out_row(p, s, q, pitch) * C + h * D;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt)
             *(uint2*)(op + dt * 16 + 4 * lg) =
@@ -776,7 +776,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
         if (q < qend && p.lse && lg == 0)  // training: log2-sum-exp2 of the pre-scaled scores
             p.lse[((int64_t)s * p.H + h) * ntok + q] = mr[qt] + __builtin_amdgcn_logf(lsum[qt][0]);
         if (q < qend) {
-            T* op = (T*)p.out + ((int64_t)s * pitch + q) * C + h * D;
+            T* op = (T*)p.out + attn_out_row(p, s, q, pitch) * C + h * D;
 #pragma unroll
             for (int dt = 0; dt < 4; ++dt)
                 *(uint2*)(op + dt * 16 + 4 * lg) = make_uint2(pack2<T>(o[dt][qt][0] * inv, o[dt][qt][1] * inv),
@@ -1093,7 +1093,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 #pragma unroll
     for (int r = 0; r < 16; ++r) chk += o[0][r] * 0.f + o[1][r] * 0.f;
     const bool ok = (l >= LZ_LO && l <= LZ_HI && chk == 0.f) || MMT_ATTN_ABLATE != 0;
-    bf16_t* op = (bf16_t*)p.out + ((int64_t)s * pitch + q) * C + h * D;
+    bf16_t* op = (bf16_t*)p.out + attn_out_row(p, s, q, pitch) * C + h * D;
     if (__builtin_expect(__all(ok), 1)) {
         const float inv = 1.f / l;
         if (q < qend) {
@@ -1421,7 +1421,7 @@ MMT_DEV void mam_lz2_item(const mmt_attn_params& p, char* lds, const int bx, con
             for (int r = 0; r < 16; ++r) chk += o[qb][0][r] * 0.f + o[qb][1][r] * 0.f;
             const bool ok = (l >= LZ_LO && l <= LZ_HI && chk == 0.f) || MMT_ATTN_ABLATE != 0;
             const int q = qbase + 32 * qb + l32;
-            bf16_t* op = (bf16_t*)p.out + ((int64_t)s * pitch + q) * C + h * D;
+            bf16_t* op = (bf16_t*)p.out + attn_out_row(p, s, q, pitch) * C + h * D;
             if (__builtin_expect(__all(ok), 1)) {
                 const float inv = 1.f / l;
                 if (q < qend) {
@@ -1796,7 +1796,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
         for (int r = 0; r < 16; ++r) chk += o[qb][0][r] * 0.f + o[qb][1][r] * 0.f;
         const bool ok = l >= LZ_LO && l <= LZ_HI && chk == 0.f;
         const int q = qbase + 32 * qb + l32;
-        bf16_t* op = (bf16_t*)p.out + ((int64_t)s * pitch + q) * C + h * D;
+        bf16_t* op = (bf16_t*)p.out + attn_out_row(p, s, q, pitch) * C + h * D;
         if (__builtin_expect(__all(ok), 1)) {
             const float inv = 1.f / l;
             if (q < qend) {
@@ -1874,6 +1874,12 @@ int launch_attn(const mmt_attn_params& p, hipStream_t st) {
     if (p.asym && (p.Bm <= 0 || p.S != 2 * p.Bm)) return MMT_EBADARG;
     if (((uintptr_t)p.qkv | (uintptr_t)p.out) & 15) return MMT_EBADARG;
     if (p.q_part < 0 || p.q_part > 2) return MMT_EBADARG;
+    {  // compact out rows: every stored query lands in [0, out_pitch) of its sequence
+        const int qa = p.q_part == 2 ? p.n_t : 0, qb = p.q_part == 1 ? p.n_t : p.ntok;
+        if (p.out_pitch < 0 || p.out_q0 < 0 || p.out_q0 > qa || ((p.out_pitch || p.out_q0) && p.lse) ||
+            (p.out_pitch > 0 && p.out_pitch < qb - p.out_q0))
+            return MMT_EBADARG;
+    }
     // q_part: 0 all queries, 1 template queries only, 2 search queries only (template K/V cache)
     auto qblocks = [&](int qt) {
         const int t = (p.n_t + qt - 1) / qt, sr = (p.ntok - p.n_t + qt - 1) / qt;

@@ -448,7 +448,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                 for (int r = 0; r < 16; ++r) chk += o[qb][0][r] * 0.f + o[qb][1][r] * 0.f;
                 const bool ok = l >= LZ_LO && l <= LZ_HI && chk == 0.f;
                 const int q = qbase + 32 * qb + l32;
-                bf16_t* op = (bf16_t*)p.out + ((int64_t)s * pitch + q) * C + h * D;
+                bf16_t* op = (bf16_t*)p.out + attn_out_row(p, s, q, pitch) * C + h * D;
                 if (__builtin_expect(__all(ok), 1)) {
                     const float inv = 1.f / l;
                     // lane (q, hf) holds d = 32 db + 8 g + 4 hf + [0, 4); a permlane32 swap of the column

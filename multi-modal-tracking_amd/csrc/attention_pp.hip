@@ -511,7 +511,7 @@ __global__ __launch_bounds__(128 * KS) __attribute__((amdgpu_waves_per_eu(1, 1))
             for (int r = 0; r < 16; ++r) chk += st.o[qb][0][r] * 0.f + st.o[qb][1][r] * 0.f;
             const bool ok = (l >= LZ_LO && l <= LZ_HI && chk == 0.f) || MMT_ATTN_ABLATE != 0;
             const int q = qbase + 32 * qb + l32;
-            bf16_t* op = (bf16_t*)p.out + ((int64_t)s * pitch + q) * C + h * D;
+            bf16_t* op = (bf16_t*)p.out + attn_out_row(p, s, q, pitch) * C + h * D;
             if (__builtin_expect(__all(ok), 1)) {
                 const float inv = 1.f / l;
                 if (q < qend) {

@@ -88,6 +88,12 @@ MMT_DEV void attn_wait_dyn(int n) {
     }
 }
 
+// first out row of query q of sequence s (mmt_attn_params.out_pitch / out_q0: compact activations of the
+// template K/V cache passes; identity layout by default)
+MMT_DEV int64_t attn_out_row(const mmt_attn_params& p, int s, int q, int64_t pitch) {
+    return (int64_t)s * (p.out_pitch > 0 ? p.out_pitch : pitch) + q - p.out_q0;
+}
+
 // V image swizzle: chunk c of row r at c ^ (r & 6) ^ ((r & 2) << 1): the 4 rows x 4 chunks a
 // half-wave reads per tr instruction then cover all 64 banks once.
 MMT_DEV int attn_vswz(int row) { return (row & 6) ^ ((row & 2) << 1); }

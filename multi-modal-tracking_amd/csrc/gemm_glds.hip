@@ -640,8 +640,14 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
     }
     const float inv_k = 1.f / (float)K;
     // output row map (template K/V cache: search rows of a [S][ntok] stream); identity if c_seg_rows == 0
+    // (32-bit unsigned division: M and the segment rows are < 2^31; a 64-bit one is a long software sequence)
     const int64_t csr = p.c_seg_rows > 0 ? p.c_seg_rows : INT64_MAX, csp = p.c_seg_pitch;
-    auto crow = [&](int m) -> int64_t { return csr == INT64_MAX ? (int64_t)m : (m / csr) * csp + m % csr; };
+    const uint32_t csr32 = (uint32_t)min(csr, (int64_t)INT32_MAX);
+    auto crow = [&](int m) -> int64_t {
+        if (csr == INT64_MAX) return (int64_t)m;
+        const uint32_t qd = (uint32_t)m / csr32;
+        return (int64_t)qd * csp + (int64_t)((uint32_t)m - qd * csr32);
+    };
     constexpr int PG = NPASS < 4 ? NPASS : 4;  // passes whose residual loads are in flight together
     for (int ep = 0; ep < EPASS; ++ep) {
     if (ep > 0) {  // the next wave row's accumulators into the (re-used) tile image
@@ -694,7 +700,7 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
                 }
             }
             if (m < M && n < N)
-                *(u32x4*)((T*)C + (int64_t)m * p.ldc + n) = u32x4{pack2<T>(va[0], va[1]), pack2<T>(va[2], va[3]),
+                *(u32x4*)((T*)C + crow(m) * p.ldc + n) = u32x4{pack2<T>(va[0], va[1]), pack2<T>(va[2], va[3]),
                                                                pack2<T>(vb[0], vb[1]), pack2<T>(vb[2], vb[3])};
         }
     } else if constexpr (EPI == 2) {  // compact residual producer: fp32 C = acc + bias + R, C2 its 16-bit copy,
@@ -950,7 +956,10 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
 // Whether the compact 16-bit epilogue (EPI 1) covers the GEMM's epilogue (bias, folded LayerNorm, ReLU / GELU,
 // the pre-activation copy of c2_copy 2).
 bool compact_epilogue(const mmt_gemm_params& p) {
-    if (p.c_f32 || (p.c2_copy != 0 && p.c2_copy != 2) || p.c_seg_rows || p.row_scale || p.act < 0 || p.act > 2)
+    // an output row map (the template K/V cache passes' qkv rows into the [S][ntok] cache) is fine; not with
+    // c2_copy 2's pre-activation copy, which is stored at the plain row
+    if (p.c_f32 || (p.c2_copy != 0 && p.c2_copy != 2) || (p.c_seg_rows && p.c2_copy == 2) || p.row_scale ||
+        p.act < 0 || p.act > 2)
         return false;
     for (int g = 0; g < p.groups; ++g)  // C2 only as c2_copy 2's pre-activation copy
         if (p.r[g] || p.ln_stats_out[g] || (p.c2[g] != nullptr) != (p.c2_copy == 2)) return false;

@@ -17,7 +17,9 @@
 //
 // mmt_ms_deform_attn_backward — drop-in for `ms_deform_attn_backward` (vision.cpp:13-16 ->
 //   ms_deform_attn_cuda.cu:83-153 -> ms_deformable_col2im kernels, ms_deform_im2col_cuda.cuh:86-235
-//   for the per-tap arithmetic): grad_value by float atomics at the four taps (w_k * g * a),
+//   for the per-tap arithmetic): grad_value = sum over the four taps of every sample of w_k * g * a,
+//   gathered per pixel in a fixed order (msda_bwd_value_kernel: deterministic, no atomics; heads wider than
+//   64 channels fall back to the reference's float atomics),
 //   grad_attn = sum_c g * bilinear, grad_loc = (W * dbil/dw, H * dbil/dh) * g * a summed over the
 //   channels.  One wave per (n, q, m) sample row, lanes over channels: the channel sums of
 //   grad_loc / grad_attn are wave reductions with one plain store each (the reference's
@@ -177,7 +179,8 @@ template <typename A> MMT_DEV A wave_sum_t(A v) {
     return v;
 }
 
-template <typename T>
+// ATOMIC: grad_value by float atomics here (the general fallback); else msda_bwd_value_kernel gathers it
+template <typename T, bool ATOMIC>
 __global__ __launch_bounds__(256) void msda_bwd_kernel(const T* __restrict__ value, const int64_t* __restrict__ shapes,
                                                        const int64_t* __restrict__ lstart, const T* __restrict__ loc,
                                                        const T* __restrict__ aw, const T* __restrict__ gout,
@@ -211,10 +214,10 @@ __global__ __launch_bounds__(256) void msda_bwd_kernel(const T* __restrict__ val
                     const T* v = value + base + c;
                     T* gv = gvalue + base + c;
                     A gh = 0, gw = 0, v1 = 0, v2 = 0, v3 = 0, v4 = 0;
-                    if (k1) { v1 = v[o1]; gh -= hw * v1; gw -= hh * v1; atomicAdd(gv + o1, w1 * tgv); }
-                    if (k2) { v2 = v[o2]; gh -= lw * v2; gw += hh * v2; atomicAdd(gv + o2, w2 * tgv); }
-                    if (k3) { v3 = v[o3]; gh += hw * v3; gw -= lh * v3; atomicAdd(gv + o3, w3 * tgv); }
-                    if (k4) { v4 = v[o4]; gh += lw * v4; gw += lh * v4; atomicAdd(gv + o4, w4 * tgv); }
+                    if (k1) { v1 = v[o1]; gh -= hw * v1; gw -= hh * v1; if (ATOMIC) atomicAdd(gv + o1, w1 * tgv); }
+                    if (k2) { v2 = v[o2]; gh -= lw * v2; gw += hh * v2; if (ATOMIC) atomicAdd(gv + o2, w2 * tgv); }
+                    if (k3) { v3 = v[o3]; gh += hw * v3; gw -= lh * v3; if (ATOMIC) atomicAdd(gv + o3, w3 * tgv); }
+                    if (k4) { v4 = v[o4]; gh += lw * v4; gw += lh * v4; if (ATOMIC) atomicAdd(gv + o4, w4 * tgv); }
                     sa += tg * (w1 * v1 + w2 * v2 + w3 * v3 + w4 * v4);
                     sx += (A)W * gw * tgv;
                     sy += (A)H * gh * tgv;
@@ -232,6 +235,139 @@ __global__ __launch_bounds__(256) void msda_bwd_kernel(const T* __restrict__ val
     }
 }
 
+// grad_value without atomics (deterministic): one workgroup per (n, m, level, chunk of 64 consecutive pixels of
+// the level in raster order).  Every sample of (n, m, level) -- Lq x P of them, in batches of MSDA_SB -- is expanded
+// into its four bilinear taps (the forward's validity rules, cuh:55-84); the taps that land in the chunk are counted
+// per pixel, bucketed (LDS), each bucket sorted by (sample, tap), and each pixel's channels summed in that fixed
+// order: grad_value[pixel, c] = sum w_k * (g[q, c] * a), written once.  Taps are the reference's atomics
+// (ms_deform_im2col_cuda.cuh:86-235, ms_deformable_col2im_*) re-ordered; thread (c, pixel group) owns 16 pixels.
+constexpr int MSDA_PIX = 64, MSDA_SB = 1024;
+
+template <typename T>
+__global__ __launch_bounds__(256) void msda_bwd_value_kernel(const T* __restrict__ loc, const T* __restrict__ aw,
+                                                             const T* __restrict__ gout, T* __restrict__ gvalue,
+                                                             const int64_t* __restrict__ shapes,
+                                                             const int64_t* __restrict__ lstart, int S, int M, int D,
+                                                             int Lq, int L, int P) {
+    using A = T;
+    __shared__ int cnt[MSDA_PIX + 1], cur[MSDA_PIX];
+    __shared__ int ekey[4 * MSDA_SB];
+    __shared__ A ew[4 * MSDA_SB];
+    __shared__ A sa[MSDA_SB];
+    __shared__ int sq[MSDA_SB];
+    const int t = threadIdx.x;
+    // (level, chunk) of this workgroup: chunks of every level back to back
+    int l = 0, chunk = blockIdx.x, H = 0, W = 0;
+    for (; l < L; ++l) {
+        H = (int)shapes[2 * l];
+        W = (int)shapes[2 * l + 1];
+        const int nc = (H * W + MSDA_PIX - 1) / MSDA_PIX;
+        if (chunk < nc) break;
+        chunk -= nc;
+    }
+    if (l >= L) return;  // past the last level's chunks (the grid is an upper bound): uniform
+    const int m = blockIdx.y, n = blockIdx.z;
+    const int p0 = chunk * MSDA_PIX, np = min(MSDA_PIX, H * W - p0);
+    const int c = t & 63, pg = t >> 6;  // channel, pixel group (pixels pg, pg + 4, ...)
+    A acc[MSDA_PIX / 4];
+#pragma unroll
+    for (int i = 0; i < MSDA_PIX / 4; ++i) acc[i] = 0;
+    const int ns = Lq * P;
+    // the taps of sample j (of this (n, m, l)) inside the chunk: f(k, pixel - p0, w_k)
+    auto taps = [&](int j, auto&& f) {
+        const int q = j / P, p = j - q * P;
+        const int64_t wi = (((int64_t)n * Lq + q) * M + m) * L * P + (int64_t)l * P + p;
+        const A lx = loc[2 * wi], ly = loc[2 * wi + 1];
+        const A h = ly * (A)H - (A)0.5, w = lx * (A)W - (A)0.5;
+        if (!(h > (A)-1 && w > (A)-1 && h < (A)H && w < (A)W)) return;
+        const int hl = (int)floor(h), wl = (int)floor(w), hh_ = hl + 1, wh_ = wl + 1;
+        const A lh = h - (A)hl, lw = w - (A)wl, hh = (A)1 - lh, hw = (A)1 - lw;
+        const int r1 = hl * W + wl - p0;
+        if (hl >= 0 && wl >= 0 && (unsigned)r1 < (unsigned)np) f(0, r1, hh * hw);
+        if (hl >= 0 && wh_ <= W - 1 && (unsigned)(r1 + 1) < (unsigned)np) f(1, r1 + 1, hh * lw);
+        if (hh_ <= H - 1 && wl >= 0 && (unsigned)(r1 + W) < (unsigned)np) f(2, r1 + W, lh * hw);
+        if (hh_ <= H - 1 && wh_ <= W - 1 && (unsigned)(r1 + W + 1) < (unsigned)np) f(3, r1 + W + 1, lh * lw);
+    };
+    for (int b0 = 0; b0 < ns; b0 += MSDA_SB) {
+        const int nb = min(MSDA_SB, ns - b0);
+        if (t <= MSDA_PIX) cnt[t] = 0;
+        __syncthreads();
+        for (int j = t; j < nb; j += 256) {  // count the chunk's taps per pixel; the samples' q and a
+            const int jj = b0 + j, q = jj / P, p = jj - q * P;
+            sq[j] = q;
+            sa[j] = aw[(((int64_t)n * Lq + q) * M + m) * L * P + (int64_t)l * P + p];
+            taps(jj, [&](int, int r, A) { atomicAdd(&cnt[r], 1); });
+        }
+        __syncthreads();
+        if (t < 64) {  // exclusive scan of the 64 counts (one wave)
+            const int v = cnt[t];
+            int x = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int y = __shfl_up(x, o, 64);
+                if (t >= o) x += y;
+            }
+            cur[t] = x - v;
+            if (t == 63) cnt[MSDA_PIX] = x;
+        }
+        __syncthreads();
+        if (t < MSDA_PIX) cnt[t] = cur[t];  // bucket starts (cnt[64] = total)
+        __syncthreads();
+        for (int j = t; j < nb; j += 256)
+            taps(b0 + j, [&](int k, int r, A wk) {
+                const int pos = atomicAdd(&cur[r], 1);
+                ekey[pos] = j * 4 + k;
+                ew[pos] = wk;
+            });
+        __syncthreads();
+        if (t < MSDA_PIX) {  // each bucket in (sample, tap) order: the fixed summation order
+            const int e0 = cnt[t], e1 = cnt[t + 1];
+            for (int e = e0 + 1; e < e1; ++e) {
+                const int k = ekey[e];
+                const A wv = ew[e];
+                int i = e - 1;
+                for (; i >= e0 && ekey[i] > k; --i) {
+                    ekey[i + 1] = ekey[i];
+                    ew[i + 1] = ew[i];
+                }
+                ekey[i + 1] = k;
+                ew[i + 1] = wv;
+            }
+        }
+        __syncthreads();
+        {  // the wave's 16 pixels advance together (pixels are wave-uniform): 16 independent gathers in flight
+            int e0[MSDA_PIX / 4], e1[MSDA_PIX / 4], len = 0;
+#pragma unroll
+            for (int i = 0; i < MSDA_PIX / 4; ++i) {
+                const int r = min(pg + 4 * i, np);  // past the chunk: an empty range
+                e0[i] = cnt[r];
+                e1[i] = r < np ? cnt[r + 1] : cnt[r];
+                len = max(len, e1[i] - e0[i]);
+            }
+            const int64_t gq = (int64_t)M * D, g0 = ((int64_t)n * Lq * M + m) * D + min(c, D - 1);
+            for (int k = 0; k < len; ++k) {
+#pragma unroll
+                for (int i = 0; i < MSDA_PIX / 4; ++i) {
+                    const int e = e0[i] + k;
+                    if (e < e1[i]) {
+                        const int j = ekey[e] >> 2;
+                        acc[i] += ew[e] * (gout[g0 + sq[j] * gq] * sa[j]);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (c < D) {
+        T* gv = gvalue + (((int64_t)n * S + lstart[l] + p0) * M + m) * D + c;
+#pragma unroll
+        for (int i = 0; i < MSDA_PIX / 4; ++i) {
+            const int r = pg + 4 * i;
+            if (r < np) gv[(int64_t)r * M * D] = acc[i];
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" int mmt_ms_deform_attn_backward(const void* value, const int64_t* spatial_shapes, const int64_t* level_start,
@@ -245,16 +381,31 @@ extern "C" int mmt_ms_deform_attn_backward(const void* value, const int64_t* spa
     const size_t esz = dtype == MMT_F64 ? 8 : dtype == MMT_F32 ? 4 : 0;
     if (!esz) return MMT_EBADARG;
     hipStream_t st = (hipStream_t)stream;
-    // grad_value accumulates by atomics; grad_loc / grad_attn are fully written by the kernel
-    if (const int e = zero_fill_async(grad_value, (size_t)N * S * M * D * esz, st)) return e;
     const int64_t nsamp = (int64_t)N * Lq * M;
     dim3 grid((unsigned)((nsamp + 3) / 4));
-#define MSDA_BWD_CASE(T)                                                                                          \
-    hipLaunchKernelGGL((msda_bwd_kernel<T>), grid, dim3(256), 0, st, (const T*)value, spatial_shapes, level_start, \
-                       (const T*)sampling_loc, (const T*)attn_weight, (const T*)grad_output, (T*)grad_value,       \
-                       (T*)grad_loc, (T*)grad_attn, S, M, D, Lq, L, P, nsamp)
-    if (dtype == MMT_F32) MSDA_BWD_CASE(float);
-    else MSDA_BWD_CASE(double);
+    // grad_value: the deterministic gather (msda_bwd_value_kernel) for up to 64 channels per head; wider heads
+    // accumulate by float atomics inside msda_bwd_kernel.  grad_loc / grad_attn are fully written either way.
+    const bool gather = D <= 64;
+    if (!gather)
+        if (const int e = zero_fill_async(grad_value, (size_t)N * S * M * D * esz, st)) return e;
+    // the gather's grid: (chunks of MSDA_PIX pixels over the levels, heads, batch); the sum over levels of
+    // ceil(HW_l / 64) is at most S / 64 + L (the shapes stay on the device: the kernel skips past the last)
+    const dim3 vgrid((unsigned)(S / MSDA_PIX + L), (unsigned)M, (unsigned)N);
+#define MSDA_BWD_CASE(T)                                                                                           \
+    if (gather) {                                                                                                  \
+        hipLaunchKernelGGL((msda_bwd_kernel<T, false>), grid, dim3(256), 0, st, (const T*)value, spatial_shapes,  \
+                           level_start, (const T*)sampling_loc, (const T*)attn_weight, (const T*)grad_output,       \
+                           (T*)grad_value, (T*)grad_loc, (T*)grad_attn, S, M, D, Lq, L, P, nsamp);                  \
+        hipLaunchKernelGGL((msda_bwd_value_kernel<T>), vgrid, dim3(256), 0, st, (const T*)sampling_loc,           \
+                           (const T*)attn_weight, (const T*)grad_output, (T*)grad_value, spatial_shapes,            \
+                           level_start, S, M, D, Lq, L, P);                                                         \
+    } else {                                                                                                       \
+        hipLaunchKernelGGL((msda_bwd_kernel<T, true>), grid, dim3(256), 0, st, (const T*)value, spatial_shapes,   \
+                           level_start, (const T*)sampling_loc, (const T*)attn_weight, (const T*)grad_output,       \
+                           (T*)grad_value, (T*)grad_loc, (T*)grad_attn, S, M, D, Lq, L, P, nsamp);                  \
+    }
+    if (dtype == MMT_F32) { MSDA_BWD_CASE(float) }
+    else { MSDA_BWD_CASE(double) }
 #undef MSDA_BWD_CASE
     return launch_status();
 }

@@ -44,7 +44,7 @@ class GemmParams(ctypes.Structure):
 class AttnParams(ctypes.Structure):
     _fields_ = [("qkv", vp), ("out", vp), ("S", i32), ("Bm", i32), ("ntok", i32), ("n_t", i32), ("C", i32),
                 ("H", i32), ("asym", i32), ("scale", f32), ("impl", i32), ("lse", vp), ("q_part", i32),
-                ("tok_pitch", i32)]
+                ("tok_pitch", i32), ("out_pitch", i32), ("out_q0", i32)]
 
 
 class AttnBwdParams(ctypes.Structure):

@@ -405,45 +405,56 @@ class MixFormerRGBTRuntime:
 
     def _plan_backbone(self, plan, ws, part, qkv_layers=None):
         """Patch embed + the ViT blocks over the token rows of `part`: None = all rows; "t" = the
-        template rows [0, n_t) of every sequence; "s" = the search rows [n_t, ntok).  A part's GEMMs
-        address their rows in the [S][ntok] streams through the A segment map and the output row
-        map (c_seg_rows / c_seg_pitch), and its attention launch takes the matching query part.
-        Template queries never attend search keys (the MAM is asymmetric, mixformer.py:61-76), so
-        the "t" pass run once per template update followed by "s" passes per frame equals the full
-        forward exactly, provided each layer's qkv rows persist: qkv_layers gives one
-        [S*ntok][3C] buffer per layer (None: the one QKV buffer, reused by every layer)."""
+        template rows [0, n_t) of every sequence; "s" = the search rows [n_t, ntok).  Template queries
+        never attend search keys (the MAM is asymmetric, mixformer.py:61-76), so the "t" pass run once
+        per template update followed by "s" passes per frame equals the full forward exactly, provided
+        each layer's qkv rows persist: qkv_layers gives one [S*ntok][3C] buffer per layer (None: the one
+        QKV buffer, reused by every layer).
+        A part's activations (X, XN, AO, HID and the LayerNorm statistics) are COMPACT: its nr rows of
+        every sequence back to back ([S][nr], modality groups of B sequences), so every GEMM reads and
+        writes plain rows (the compact epilogues and the LayerNorm-statistics hand-off apply); only the
+        qkv GEMM writes through an output row map into the [S][ntok] per-layer cache, and the attention
+        stores its part's rows compact (mmt_attn_params.out_pitch / out_q0)."""
         d, W, B = self.d, self.w, ws["B"]
         C, ntok = d.C, d.ntok
         S = d.nmod * B
-        R = S * ntok
         two = self.variant == "rgbt"
         nm_ = d.nmod  # modality groups of the per-modality LayerNorm GEMMs (1 for the RGB-only model)
         P = _ptr
         X, XN, AO, HID = ws["X"], ws["XN"], ws["AO"], ws["HID"]
         cdt = self.cdt
         off, nr = {None: (0, ntok), "t": (0, d.n_t), "s": (d.n_t, d.ns)}[part]
+        compact = part is not None
+        rp = nr if compact else ntok  # rows per sequence of the activation streams
+        R = S * rp
 
-        def rmap(ld):  # A segment map + output row map of the part's rows (identity for all rows)
-            if part is None and nr == ntok:
+        def at(t, ld, g=0):  # first row of the part in group g's block of B sequences (activations)
+            return P(t, (g * B * rp + (0 if compact else off)) * ld)
+
+        def qat(t, g=0):  # the same in the [S][ntok] qkv stream
+            return P(t, (g * B * ntok + off) * 3 * C)
+        qmap = dict(cmap=(nr, ntok)) if compact else {}  # qkv rows of the part into the [S][ntok] cache
+
+        def rmap(ld):  # after candidate elimination (full forward): the first nr rows of each pitch-ntok sequence
+            if compact or nr == ntok:
                 return {}
             return dict(seg=(nr, 1 << 30, ntok * ld, 0), cmap=(nr, ntok))
-
-        def at(t, ld, g=0):  # first row of the part in group g's block of B sequences
-            return P(t, (g * B * ntok + off) * ld)
         # --- patch embed (im2col + GEMM, + bias + pos-embed) -> X  (fold: + its bf16 copy XN)
         fold = self.fold_ln
         # the producers of XN (patch embed, proj, fc2) also write its per-64-column row statistics
         # (LNST), which the LayerNorm-folded consumers (qkv, fc1) read instead of summing them in
-        # their K loops; not for the template-cache passes (segment-mapped rows) or with candidate
-        # elimination (the gather moves rows).  The LDS-DMA GEMM takes the hand-off for K = C <= 1024 and
-        # producer widths N = C % 64 == 0 only (gemm_glds.hip glds_takes); wider models keep ln_fold 1
-        hand = fold and part is None and not self.ce and C % 64 == 0 and C <= 1024
+        # their K loops; not with candidate elimination (the gather moves rows).  The LDS-DMA GEMM takes
+        # the hand-off for K = C <= 1024 and producer widths N = C % 64 == 0 only (gemm_glds.hip
+        # glds_takes); wider models keep ln_fold 1
+        hand = fold and not self.ce and C % 64 == 0 and C <= 1024
         nst = 2 * (C // 64)
         LNST = ws["LNST"]
         plan.append((LIB.mmt_patch_im2col, self._image_args(ws["in_t"], ws["in_o"], ws["in_s"])
                      + (P(ws["PATCH"]), B, d.ht, d.hs, d.patch, cdt), "patch_im2col", None))
         KP = 3 * d.patch * d.patch
         gm = B * nr  # rows per modality group
+        pat = lambda g: P(ws["PATCH"], (g * B * ntok + off) * KP)  # noqa: E731  (im2col rows: [S][ntok])
+        pseg = dict(seg=(nr, 1 << 30, ntok * KP, 0)) if compact else {}
         cp = dict(c2_copy=1) if fold else {}
         if hand:
             cp["ln_stats_out"] = [at(LNST, nst, 0), at(LNST, nst, 1)] if two else [at(LNST, nst)]
@@ -451,16 +462,16 @@ class MixFormerRGBTRuntime:
         if two:
             if fold:
                 cp["c2"] = [at(XN, C, 0), at(XN, C, 1)]
-            self._gemm(plan, "patch_gemm", a=[at(ws["PATCH"], KP, 0), at(ws["PATCH"], KP, 1)],
+            self._gemm(plan, "patch_gemm", a=[pat(0), pat(1)],
                        w=[P(W["bb"][g]["patch_w"]) for g in range(2)], c=[at(X, C, 0), at(X, C, 1)], M=gm, N=C, K=KP,
                        lda=KP, ldc=C, bias=[P(W["bb"][g]["patch_b"]) for g in range(2)],
-                       r=[pos_at(g) for g in range(2)], ldr=C, r_mode=1, r_p0=nr, c_f32=1, **cp, **rmap(KP))
+                       r=[pos_at(g) for g in range(2)], ldr=C, r_mode=1, r_p0=nr, c_f32=1, **cp, **pseg)
         else:
             if fold:
                 cp["c2"] = [at(XN, C)]
-            self._gemm(plan, "patch_gemm", a=[at(ws["PATCH"], KP)], w=[P(W["bb"][0]["patch_w"])], c=[at(X, C)],
+            self._gemm(plan, "patch_gemm", a=[pat(0)], w=[P(W["bb"][0]["patch_w"])], c=[at(X, C)],
                        M=S * nr, N=C, K=KP, lda=KP, ldc=C, bias=[P(W["bb"][0]["patch_b"])], r=[pos_at(0)], ldr=C,
-                       r_mode=1, r_p0=nr, c_f32=1, **cp, **rmap(KP))
+                       r_mode=1, r_p0=nr, c_f32=1, **cp, **pseg)
         # --- transformer blocks
         if self.ce and part is not None:
             raise NotImplementedError("the template K/V cache is not defined for candidate elimination")
@@ -485,17 +496,20 @@ class MixFormerRGBTRuntime:
                 rows = lambda t, k: [at(t, k)]  # noqa: E731
                 Mg = S * nr
             rows2 = lambda t, k: [at(t, k, g) for g in range(nm_)]  # noqa: E731  (one group per modality)
+            qrows2 = [qat(QKV, g) for g in range(nm_)]
             if fold:  # LayerNorm 1 folded into qkv: A = XN = bf16 copy of the residual stream X
-                self._gemm(plan, "qkv", a=rows2(XN, C), w=fl("attn.qkv.fw"), c=rows2(QKV, 3 * C), M=gm, N=3 * C,
+                self._gemm(plan, "qkv", a=rows2(XN, C), w=fl("attn.qkv.fw"), c=qrows2, M=gm, N=3 * C,
                            K=C, lda=C, ldc=3 * C, bias=fl("attn.qkv.fb"), ln_colsum=fl("attn.qkv.fcs"), ln_eps=1e-6,
-                           ln_stats_in=rows2(LNST, nst) if hand else None, **rmap(C))
-            else:  # (the fp32 LayerNorm runs over all rows; rows outside the part are not read)
+                           ln_stats_in=rows2(LNST, nst) if hand else None, **(qmap if compact else rmap(C)))
+            else:
                 plan.append((LIB.mmt_layernorm, (P(X), None, 0, None, P(XN), P(n1[0][0]), P(n1[0][1]), P(n1[1][0]),
-                                                 P(n1[1][1]), R, B * ntok, C, 1e-6, cdt), "ln1", None))
-                self._gemm(plan, "qkv", a=rows(XN, C), w=wl("attn.qkv.w"), c=rows(QKV, 3 * C), M=Mg, N=3 * C, K=C,
-                           lda=C, ldc=3 * C, bias=wl("attn.qkv.b"), **rmap(C))
+                                                 P(n1[1][1]), R, B * rp, C, 1e-6, cdt), "ln1", None))
+                self._gemm(plan, "qkv", a=rows(XN, C), w=wl("attn.qkv.w"), c=[qat(QKV, g) for g in range(len(rows(XN, C)))],
+                           M=Mg, N=3 * C, K=C, lda=C, ldc=3 * C, bias=wl("attn.qkv.b"), **(qmap if compact else rmap(C)))
             ap = AttnParams()
             ap.qkv, ap.out, ap.S, ap.Bm, ap.ntok, ap.n_t, ap.C, ap.H = P(QKV), P(AO), S, B, ntok, d.n_t, C, d.H
+            if compact:  # the part's rows stored compact
+                ap.out_pitch, ap.out_q0 = nr, off
             if part is None and nr != ntok:  # after an elimination stage: first nr rows of each sequence
                 ap.ntok, ap.tok_pitch = nr, ntok
             ap.asym = 1 if self.variant in ("asym", "asym_online", "asym_ce") else 0
@@ -538,12 +552,11 @@ class MixFormerRGBTRuntime:
                            ln_eps=1e-6, ln_stats_in=rows2(LNST, nst) if hand else None, **rmap(C))
             else:
                 plan.append((LIB.mmt_layernorm, (P(X), None, 0, None, P(XN), P(n2[0][0]), P(n2[0][1]), P(n2[1][0]),
-                                                 P(n2[1][1]), R, B * ntok, C, 1e-6, cdt), "ln2", None))
+                                                 P(n2[1][1]), R, B * rp, C, 1e-6, cdt), "ln2", None))
                 self._gemm(plan, "fc1", a=rows(XN, C), w=wl("mlp.fc1.w"), c=rows(HID, d.hidden), M=Mg, N=d.hidden,
                            K=C, lda=C, ldc=d.hidden, bias=wl("mlp.fc1.b"), act=1, **rmap(C))
             self._gemm(plan, "fc2", a=rows(HID, d.hidden), w=wl("mlp.fc2.w"), c=rows(X, C), M=Mg, N=C, K=d.hidden,
-                       lda=d.hidden, ldc=C, bias=wl("mlp.fc2.b"), r=rows(X, C), ldr=C, c_f32=1, **cpx,
-                       **rmap(d.hidden))
+                       lda=d.hidden, ldc=C, bias=wl("mlp.fc2.b"), r=rows(X, C), ldr=C, c_f32=1, **cpx, **rmap(d.hidden))
         return (X, stage)
 
     def _image_args(self, t, o, s):
@@ -553,11 +566,14 @@ class MixFormerRGBTRuntime:
             return (_ptr(t[0]), None, _ptr(o[0]), None, _ptr(s[0]), None)
         return tuple(_ptr(x) for x in list(t) + list(o) + list(s))
 
-    def _plan_tail(self, plan, ws, score, xf=None, spm_kv1=True):
+    def _plan_tail(self, plan, ws, score, xf=None, spm_kv1=True, compact=False):
         """Fusion, corner head (and score head) on the backbone output's search rows.  xf = (the fp32
-        stream holding the backbone output, elimination stages run) from _plan_backbone."""
+        stream holding the backbone output, elimination stages run) from _plan_backbone; compact: the
+        search pass of the template K/V cache, whose streams hold only the search rows ([S][ns])."""
         d, W, B = self.d, self.w, ws["B"]
-        C, ntok, ns, dm = d.C, d.ntok, d.ns, d.d_model
+        C, ns, dm = d.C, d.ns, d.d_model
+        ntok = ns if compact else d.ntok  # rows per sequence of the backbone output
+        t0 = 0 if compact else d.n_t      # its first search row
         R = 2 * B * ntok
         P = _ptr
         X, XN = ws["X"], ws["XN"]
@@ -582,14 +598,14 @@ class MixFormerRGBTRuntime:
                 XT = ws["XH"]
                 plan.append((LIB.mmt_add_cast, (P(X), None, 0, None, P(XT), B * ntok * C, self.hcdt), "cast_head_in",
                              None))
-            self._plan_head(plan, ws, score, P(XT, d.n_t * C), C, (max(B * ns, 1), 1, ntok, 0))
+            self._plan_head(plan, ws, score, P(XT, t0 * C), C, None if compact else (max(B * ns, 1), 1, ntok, 0))
             return plan
         # --- fusion: adjust_v / adjust_i (1x1 conv on the search tokens) + GroupNorm
         Y1, SRC, SRCT, VAL = ws["Y1"], ws["SRC"], ws["SRCT"], ws["VAL"]
         Mf = B * ns
-        self._gemm(plan, "fusion_adjust", a=[P(XT, d.n_t * C), P(XT, B * ntok * C + d.n_t * C)],
+        self._gemm(plan, "fusion_adjust", a=[P(XT, t0 * C), P(XT, B * ntok * C + t0 * C)],
                    w=[P(W["adj_v.w"]), P(W["adj_i.w"])], c=[P(Y1), P(Y1, Mf * dm)], M=Mf, N=dm, K=C, lda=C, ldc=dm,
-                   bias=[P(W["adj_v.b"]), P(W["adj_i.b"])], seg=(ns, 1 << 30, ntok * C, 0), c_f32=1)
+                   bias=[P(W["adj_v.b"]), P(W["adj_i.b"])], seg=None if compact else (ns, 1 << 30, ntok * C, 0), c_f32=1)
         plan.append((LIB.mmt_groupnorm, (P(Y1), P(SRC), P(SRCT), P(W["adj_v.gn"][0]), P(W["adj_v.gn"][1]),
                                          P(W["adj_i.gn"][0]), P(W["adj_i.gn"][1]), 2 * B, B, ns, dm, 32, 1e-5, cdt),
                      "fusion_gn", None))
@@ -679,12 +695,14 @@ class MixFormerRGBTRuntime:
         if score:
             self._plan_spm(plan, ws, spm_kv1)
 
-    def _plan_spm_kv1(self, plan, ws):
+    def _plan_spm_kv1(self, plan, ws, compact=False):
         """K/V of the score decoder's second memory: the first template's tokens of both modalities
-        (the template pass computes it once per template update when the K/V cache is used)."""
+        (the template pass computes it once per template update when the K/V cache is used; its stream
+        holds only the template rows: compact)."""
         d, W, B, P, C = self.d, self.w, ws["B"], _ptr, self.d.C
+        rp = d.n_t if compact else d.ntok
         self._gemm(plan, "spm_kv1", a=[P(ws["X"])], w=[P(W["spm.kv1.w"])], c=[P(ws["KV1"])], M=B * 2 * d.nt1, N=2 * C,
-                   K=C, lda=C, ldc=2 * C, bias=[P(W["spm.kv1.b"])], seg=(d.nt1, 2, B * d.ntok * C, d.ntok * C),
+                   K=C, lda=C, ldc=2 * C, bias=[P(W["spm.kv1.b"])], seg=(d.nt1, 2, B * rp * C, rp * C),
                    c_f32=1, dtype=MMT_F32)
 
     def _plan_spm(self, plan, ws, kv1=True):
@@ -797,11 +815,11 @@ class MixFormerRGBTRuntime:
             ws["plan_t"] = []
             self._plan_backbone(ws["plan_t"], ws, "t", ws["QKVL"])
             if self.variant == "asym_online":  # the score head's template K/V: once per template update
-                self._plan_spm_kv1(ws["plan_t"], ws)
+                self._plan_spm_kv1(ws["plan_t"], ws, compact=True)
             for score in ((False, True) if self.variant == "asym_online" else (False,)):
                 plan = []
                 self._plan_backbone(plan, ws, "s", ws["QKVL"])
-                self._plan_tail(plan, ws, score, spm_kv1=False)
+                self._plan_tail(plan, ws, score, spm_kv1=False, compact=True)
                 ws["plan_s_score" if score else "plan_s"] = plan
         return ws
 

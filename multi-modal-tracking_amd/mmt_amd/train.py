@@ -1010,13 +1010,17 @@ def fusion_forward(fu, s_v, s_i, ops):
         query = src + lpos
         q_bi = torch.cat(torch.chunk(query, 2, 1), dim=2)
         value = lin(sa.value_proj, src).view(b, nl, sa.n_heads, d // sa.n_heads)
+        # The reference repeats the bimodal query's offsets / weights on both halves of its nl queries
+        # (ms_deform_attn_bimodal.py:113-118), and the two halves' reference points are the same cells, so both
+        # halves sample identically: sample the nl / 2 unique queries once and repeat the projected output
+        # (autograd of the repeat sums the halves' gradients, exactly the gradient of the reference's repeat).
         off = lin(sa.sampling_offsets, q_bi).view(b, nl // 2, sa.n_heads, sa.n_levels, sa.n_points, 2)
-        off = torch.cat([off, off], 1)
         aw = lin(sa.attention_weights, q_bi).view(b, nl // 2, sa.n_heads, sa.n_levels * sa.n_points)
-        aw = F.softmax(torch.cat([aw, aw], 1).float(), -1).view(b, nl, sa.n_heads, sa.n_levels, sa.n_points)
+        aw = F.softmax(aw.float(), -1).view(b, nl // 2, sa.n_heads, sa.n_levels, sa.n_points)
         wh = _const(("loc_norm", w, h), src.device, lambda: torch.tensor([w, h], dtype=torch.float32))
-        loc = ref[:, :, None, :, None, :] + off.float() / wh
+        loc = ref[:, :nl // 2, None, :, None, :] + off.float() / wh
         src2 = lin(sa.output_proj, ops.ms_deform_attn(value.float().contiguous(), h, loc.contiguous(), aw.contiguous()))
+        src2 = torch.cat([src2, src2], 1)
         src = src + layer.dropout1(src2)
         src = _ln_halves(ops, src, layer.norm1_v, layer.norm1_i)
         src = src + layer.dropout3(lin(layer.linear2, layer.dropout2(F.relu(lin(layer.linear1, src)))))

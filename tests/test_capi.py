@@ -98,6 +98,12 @@ def test_attention_impl_and_lse_gate():
         assert attn(impl=impl) == -10000, impl
     assert attn(impl=22, lse=fake) == -10000
     assert attn(impl=23, lse=fake) == -10000
+    # compact out rows (template K/V cache passes): pitch must hold the part's rows; not with lse
+    assert attn(q_part=2, out_pitch=399, out_q0=128) == -10000
+    assert attn(q_part=2, out_pitch=400, out_q0=129) == -10000
+    assert attn(q_part=1, out_pitch=127) == -10000
+    assert attn(q_part=1, out_pitch=128, lse=fake) == -10000
+    assert attn(out_pitch=-1) == -10000
     assert attn(dt=_lib.MMT_F16, impl=17) == -10000
     assert attn(dt=_lib.MMT_F16, lse=fake) == -10000
 

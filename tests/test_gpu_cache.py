@@ -110,6 +110,16 @@ def test_attention_query_parts_bit_exact(impl, asym):
     full, tp, sp = run(0), run(1), run(2)
     assert torch.equal(tp[:, :n_t], full[:, :n_t]) and bool((tp[:, n_t:] == 7.0).all())
     assert torch.equal(sp[:, n_t:], full[:, n_t:]) and bool((sp[:, :n_t] == 7.0).all())
+    # compact outputs of the cache passes (out_pitch / out_q0): the part's rows back to back per sequence
+    for part, rows, q0 in ((1, n_t, 0), (2, ntok - n_t, n_t)):
+        out = torch.full((S, rows + 3, C), 7.0, device="cuda", dtype=torch.bfloat16)  # 3 guard rows per sequence
+        p = AttnParams()
+        p.qkv, p.out, p.S, p.Bm, p.ntok, p.n_t, p.C, p.H, p.asym = qkv.data_ptr(), out.data_ptr(), S, 1, ntok, n_t, C, H, asym
+        p.scale, p.impl, p.q_part, p.out_pitch, p.out_q0 = 0.125, impl, part, rows + 3, q0
+        check(LIB.mmt_mam_attention(ctypes.byref(p), MMT_BF16, torch.cuda.current_stream().cuda_stream), "attn")
+        torch.cuda.synchronize()
+        assert torch.equal(out[:, :rows], full[:, q0:q0 + rows]), part
+        assert bool((out[:, rows:] == 7.0).all()), part
 
 
 @pytest.mark.parametrize("ln_fold", [0, 1])
