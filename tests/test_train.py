@@ -178,15 +178,16 @@ def _ddp_worker(rank, world, port, out_dir):
     torch.set_num_threads(4)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        net = _net()
-        step = TrainStep(net, TorchOps, lr=1e-4, ddp=True)
-        t, o, s, gt = _batch(2, 5)
-        sl = slice(rank, rank + 1)  # each rank its own sequence of the global batch of 2
-        step.backward([x[sl] for x in t], [x[sl] for x in o], [x[sl] for x in s], gt[sl])
-        grads = {n: p.grad.clone() for n, p in net.named_parameters() if p.grad is not None}
-        step.apply()
-        params = {n: p.detach().clone() for n, p in net.named_parameters()}
-        torch.save({"grads": grads, "params": params}, os.path.join(out_dir, "rank%d.pt" % rank))
+        for comp in ("none", "bf16"):  # exact fp32 all-reduce, and the default bf16-compressed buckets
+            net = _net()
+            step = TrainStep(net, TorchOps, lr=1e-4, ddp=True, grad_compress=comp)
+            t, o, s, gt = _batch(2, 5)
+            sl = slice(rank, rank + 1)  # each rank its own sequence of the global batch of 2
+            step.backward([x[sl] for x in t], [x[sl] for x in o], [x[sl] for x in s], gt[sl])
+            grads = {n: p.grad.clone() for n, p in net.named_parameters() if p.grad is not None}
+            step.apply()
+            params = {n: p.detach().clone() for n, p in net.named_parameters()}
+            torch.save({"grads": grads, "params": params}, os.path.join(out_dir, "rank%d_%s.pt" % (rank, comp)))
     finally:
         dist.destroy_process_group()
 
@@ -199,21 +200,24 @@ def test_ddp_gloo_two_ranks_matches_full_batch(tmp_path):
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
     mp.spawn(_ddp_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
-    r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
-    r1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
 
     torch.set_num_threads(8)
     net = _net()
     step = TrainStep(net, TorchOps, lr=1e-4)
     step.backward(*_batch(2, 5))
     full = {n: p.grad for n, p in net.named_parameters() if p.grad is not None}
-    assert set(full) == set(r0["grads"]) == set(r1["grads"])
-    for n, g in full.items():
-        assert torch.equal(r0["grads"][n], r1["grads"][n]), n  # all-reduced: identical on both ranks
-        scale = g.abs().max().item() + 1e-12
-        assert (r0["grads"][n] - g).abs().max().item() <= 1e-4 * scale + 1e-6, n  # mean over ranks == batch mean
-    for n in r0["params"]:
-        assert torch.equal(r0["params"][n], r1["params"][n]), n  # replicas stay in lockstep
+    # fp32 all-reduce: the batch mean within fp32 summation noise; bf16-compressed buckets: the
+    # mean rounded to bf16 (8 significant bits) once, within 2^-7 of each tensor's largest gradient
+    for comp, tol in (("none", 1e-4), ("bf16", 2 ** -7)):
+        r0 = torch.load(tmp_path / ("rank0_%s.pt" % comp), weights_only=True)
+        r1 = torch.load(tmp_path / ("rank1_%s.pt" % comp), weights_only=True)
+        assert set(full) == set(r0["grads"]) == set(r1["grads"])
+        for n, g in full.items():
+            assert torch.equal(r0["grads"][n], r1["grads"][n]), (comp, n)  # all-reduced: identical on both ranks
+            scale = g.abs().max().item() + 1e-12
+            assert (r0["grads"][n] - g).abs().max().item() <= tol * scale + 1e-6, (comp, n)  # mean == batch mean
+        for n in r0["params"]:
+            assert torch.equal(r0["params"][n], r1["params"][n]), (comp, n)  # replicas stay in lockstep
 
 
 # ----------------------------------------------------------------------------- module-level autograd
