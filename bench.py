@@ -476,13 +476,15 @@ def train_bench(world, rank, B, steps, warmup, device="cuda", ops=None, search=3
     # eager warm-up steps count as this harness's warm-up), each timed step = the copy of that step's
     # batch into the static inputs + one replay.  DDP (world > 1) stays eager.
     graphed = graph and device != "cpu" and world == 1 and ops is None
-    capture_error = None
     if graphed:
         static = [[x.clone() for x in z] if isinstance(z, (list, tuple)) else z.clone() for z in batches[0]]
         try:
             step_fn.capture(*static, warmup=max(1, warmup))
-        except RuntimeError as e:  # reported in the line; the step then runs eagerly
-            graphed, capture_error = False, str(e)[:200]
+        except RuntimeError as e:
+            # no eager fallback in this process: the warm-up steps have already moved the weights and a failed
+            # capture can leave the optimizer's pointer table half written and the stream invalidated
+            # (ADVICE r4); the caller reports the error (default line) or the run exits non-zero (--train)
+            raise RuntimeError("train step capture failed: %s" % str(e)[:300]) from e
     if graphed:
         def step(i):
             last["stats"] = step_fn.replay(*batches[i % 2])
@@ -500,8 +502,7 @@ def train_bench(world, rank, B, steps, warmup, device="cuda", ops=None, search=3
     return {"value": round(sps, 2), "unit": "samples/s", "ms_per_step": round(elapsed / steps * 1e3, 3),
             "batch_per_gpu": B, "steps": steps, "warmup": warmup,
             "parallelism": "ddp%d (RCCL gradient all-reduce)" % world if world > 1 else "single",
-            "step_issue": ("one hipGraph replay per step (whole step captured)" if graphed else
-                           "eager" + (" (capture failed: %s)" % capture_error if capture_error else "")),
+            "step_issue": "one hipGraph replay per step (whole step captured)" if graphed else "eager",
             "roofline": {"kernel": "train_step (whole step)", "bound": "mfma", "achieved": round(ach, 2),
                          "peak": PEAK["bf16"], "unit": "TFLOP/s", "frac": float("%.4g" % (ach / PEAK["bf16"])),
                          "flops_per_sample": TRAIN_FLOP_PER_SAMPLE, "traffic": None},

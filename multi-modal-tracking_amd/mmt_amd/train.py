@@ -1335,10 +1335,20 @@ class TrainStep:
         with torch.cuda.graph(self.graph):
             self.graph_stats = self(t, o, s, gt_xywh)
         self.static_inputs = (t, o, s, gt_xywh)
+        self._captured_hparams = self._hparams()
         return self.graph_stats
 
+    def _hparams(self):
+        return [(g.get("lr"), g.get("weight_decay"), tuple(g.get("betas", ())), g.get("eps")) for g in self.opt.param_groups]
+
     def replay(self, t=None, o=None, s=None, gt_xywh=None):
-        """One captured step; given inputs are first copied into the static ones (device copies)."""
+        """One captured step; given inputs are first copied into the static ones (device copies).  The
+        captured AdamW launches carry the learning rates / weight decays of capture time as kernel arguments,
+        so a changed optimizer hyper-parameter (an LR scheduler step) raises instead of replaying stale
+        values: capture() again after changing them."""
+        if self._hparams() != self._captured_hparams:
+            raise RuntimeError("TrainStep.replay: optimizer hyper-parameters changed since capture "
+                               "(%s -> %s); call capture() again" % (self._captured_hparams, self._hparams()))
         if t is not None:
             st, so, ss, sg = self.static_inputs
             for dst, src in zip(st + so + ss, t + o + s):

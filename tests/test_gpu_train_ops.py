@@ -925,6 +925,10 @@ def test_train_step_graph_replay_matches_eager():
     torch.cuda.synchronize()
     after = [p.detach() for p in net_b.parameters() if p.requires_grad][:4]
     assert any(not torch.equal(a, b) for a, b in zip(before, after))
+    # the captured AdamW launches hold capture-time learning rates: a scheduler step must not replay silently
+    graphed.opt.param_groups[0]["lr"] *= 0.5
+    with pytest.raises(RuntimeError, match="hyper-parameters changed"):
+        graphed.replay(*batches[0])
 
 
 @pytest.mark.parametrize("drop", [False, True])
