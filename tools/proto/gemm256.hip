@@ -104,9 +104,10 @@ __global__ __launch_bounds__(256) void gemm256_kernel(g256_args p) {
 #pragma unroll
             for (int mt = 0; mt < 8; ++mt)
                 // inline asm with the accumulator pinned to AGPRs ("+a": the 64 tiles fill all 256, so hipcc
-                // cannot shuttle them through VGPRs as it does for the builtin here); s_nop 1 covers a VALU
-                // write of a fragment register the compiler might place just before (it does not see the MFMA)
-                asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
+                // cannot shuttle them through VGPRs as it does for the builtin here).  No s_nop pad: the
+                // fragment registers are written only by ds_read (an s_nop costs 4 issue cycles per step of
+                // its count beside a 16-cycle MFMA, which holds the SIMD's issue for 8)
+                asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
                              : "+a"(acc[nt][mt])
                              : "v"(bf[nt]), "v"(af[mt]));
     };
