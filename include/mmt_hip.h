@@ -122,11 +122,12 @@ typedef struct {
     /* 1: C2 receives a copy of C (the value C holds, in `dtype`) instead of C = v, C2 = v + R */
     int32_t c2_copy;
     /* Split-K over workgroups (bf16 LDS-DMA kernel, GEMM and conv modes, not with ln_fold): each
-     * output tile's K-steps are cut into `splitk` slices computed by separate workgroups; every
-     * slice stores its fp32 partial tile in sk_ws, and the tile's last-arriving workgroup sums the
-     * partials in slice order (bitwise deterministic) and runs the epilogue.  splitk: 0 auto (cost
-     * model), 1 off, n >= 2 forced.  sk_ws: fp32 slab workspace of sk_ws_floats floats; sk_cnt:
-     * sk_cnt_n uint32 arrival tickets, zero before the first launch and left zero by every launch.
+     * output tile's K-steps are cut into `splitk` slices computed by separate workgroups; each slice
+     * draws an arrival ticket, every slice but the last-arriving one stores its fp32 partial tile in
+     * sk_ws, and the last one sums the partials in slice order (bitwise deterministic) and runs the
+     * epilogue.  splitk: 0 auto (cost model), 1 off, n >= 2 forced.  sk_ws: fp32 slab workspace of
+     * sk_ws_floats floats; sk_cnt: sk_cnt_n uint32 counters (tickets in the first half, published
+     * counts in the second), zero before the first launch and left zero by every launch.
      * Without both buffers (or when they are too small for the choice) no split is made. */
     int32_t splitk;
     float* sk_ws;

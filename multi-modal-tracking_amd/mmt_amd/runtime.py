@@ -344,8 +344,10 @@ class MixFormerRGBTRuntime:
     # ------------------------------------------------------------------ plan construction
     def _gemm(self, plan, name, *, a, w, c, M, N, K, lda, ldc, bias=None, r=None, ldr=0, c2=None, a1=None,
               k_split=0, act=0, c_f32=0, seg=None, r_mode=0, r_p0=0, r_p1=1, conv=None, r_t=0, dtype=None,
-              ln_colsum=None, ln_eps=0.0, c2_copy=0, cmap=None, ln_stats_in=None, ln_stats_out=None, defer=None):
-        """Append one mmt_gemm launch to plan; defer=list: collect (params, dtype) for _gemm_multi instead."""
+              ln_colsum=None, ln_eps=0.0, c2_copy=0, cmap=None, ln_stats_in=None, ln_stats_out=None, defer=None,
+              tile=None):
+        """Append one mmt_gemm launch to plan; defer=list: collect (params, dtype) for _gemm_multi instead.
+        tile=(impl, splitk): a measured per-entry choice, applied unless an A/B run forces gemm_impl / gemm_splitk."""
         p = GemmParams()
         G = len(a)
         for g in range(G):
@@ -382,6 +384,8 @@ class MixFormerRGBTRuntime:
         if cmap is not None:
             p.c_seg_rows, p.c_seg_pitch = cmap
         p.splitk = self.gemm_splitk
+        if tile is not None and self.gemm_impl == 0 and self.gemm_splitk == 0:
+            p.impl, p.splitk = tile
         p.sk_ws, p.sk_ws_floats = self._sk_ws.data_ptr(), self._sk_ws.numel()
         p.sk_cnt, p.sk_cnt_n = self._sk_cnt.data_ptr(), self._sk_cnt.numel()
         if defer is not None:
@@ -628,7 +632,10 @@ class MixFormerRGBTRuntime:
             self._gemm(plan, "enc_linear1", a=[P(SRCT)], w=[P(e["l1.w"])], c=[P(ws["H2"])], M=2 * Mf, N=d.ffn, K=dm,
                        lda=dm, ldc=d.ffn, bias=[P(e["l1.b"])], act=2)
             self._gemm(plan, "enc_linear2", a=[P(ws["H2"])], w=[P(e["l2.w"])], c=[P(SRC)], M=2 * Mf, N=dm, K=d.ffn,
-                       lda=d.ffn, ldc=dm, bias=[P(e["l2.b"])], r=[P(SRC)], ldr=dm, c_f32=1)
+                       lda=d.ffn, ldc=dm, bias=[P(e["l2.b"])], r=[P(SRC)], ldr=dm, c_f32=1,
+                       # unsplit: as fast as the cost model's 2-way split-K (10.9 vs 11.1 us at B = 1) without its
+                       # partial-tile traffic (profiles/r05_splitk_entry_ab.jsonl)
+                       tile=(0, 1))
             plan.append((LIB.mmt_layernorm, (P(SRC), None, 0, P(SRC), P(SRCT), P(e["norm2_v"][0]), P(e["norm2_v"][1]),
                                              P(e["norm2_i"][0]), P(e["norm2_i"][1]), 2 * Mf, Mf, dm, 1e-5, cdt),
                          "enc_ln2", None))

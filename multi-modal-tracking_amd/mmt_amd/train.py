@@ -1073,6 +1073,9 @@ def _hip_bn_ok(bn):
     return type(bn) is torch.nn.BatchNorm2d and bn.momentum is not None
 
 
+HEAD_SCORE_FP32 = True  # head_forward_nhwc: the 48 -> 1 conv5 in fp32 (False: bf16 under autocast, as aten's path)
+
+
 def head_forward_nhwc(hd, x, ops):
     """head_forward with NHWC maps and the 3x3 convolutions on ops.conv3x3 (HIP): every conv() block =
     conv (HIP) -> BatchNorm2d + ReLU on ops.bn_relu (HIP, the module's statistics semantics and running-stat
@@ -1095,7 +1098,12 @@ def head_forward_nhwc(hd, x, ops):
         return nhwc(seq[2](bn(nchw(y).contiguous()))).contiguous()
 
     def c1(mod, t):  # Conv2d(48, 1, 1) on channels-last rows
-        return F.linear(t, mod.weight.view(mod.weight.shape[0], -1), mod.bias)
+        if not HEAD_SCORE_FP32:
+            return F.linear(t, mod.weight.view(mod.weight.shape[0], -1), mod.bias)
+        # fp32 (autocast off): the score map feeds the soft-argmax directly, and conv5's output is its largest
+        # term, so its bf16 rounding was the largest single error on the corners (tools/head_stage_error.py)
+        with torch.autocast(t.device.type, enabled=False):
+            return F.linear(t.float(), mod.weight.view(mod.weight.shape[0], -1).float(), mod.bias.float())
 
     def up(t, f):
         return nhwc(F.interpolate(nchw(t), scale_factor=f))

@@ -762,7 +762,8 @@ def test_hip_batchnorm_relu(B, H, C, train):
 def test_head_forward_nhwc_matches_aten(bn_train):
     """The corner head on the HIP convs and batch norm (head_forward_nhwc, bf16 maps under autocast, as
     module_forward runs it) against head_forward on aten's fp32 convs (head.py:147-212) for the same module and
-    fused map, B = 2, output convs x30 (peaked maps): the normalised corners within max(3e-2, 1.5 x), the
+    fused map, B = 2, output convs x30 (peaked maps): the normalised corners within max(2e-2 (eval BN) / 3e-2
+    (train BN), 1.5 x), the
     gradients of the map and of every head parameter within max(0.1, 4 x) (a gross-error check: single bias /
     BN vectors of the 1-channel maps carry few, cancelling terms) and all head parameter gradients
     together within max(5e-2, 1.5 x) the distance of aten's own bf16 autocast path from fp32 --
@@ -790,10 +791,13 @@ def test_head_forward_nhwc_matches_aten(bn_train):
         outs.append(out.detach())
     torch.cuda.synchronize()
     err = lambda a, r: (a - r).abs().max().item()  # noqa: E731
-    # bf16 maps into x30 peaked soft-argmaxes: a corner moves 1e-2-2e-2 of the image under bf16 rounding alone
-    # (aten's autocast path 1.2e-2-1.4e-2 from fp32 depending on the box's MIOpen algorithm choice, the HIP path
-    # 2.1e-2 in train-mode BN), so the absolute floor is 3e-2
-    assert err(outs[0], outs[2]) <= max(3e-2, 1.5 * err(outs[1], outs[2])), outs
+    # bf16 maps into x30 peaked soft-argmaxes.  Eval-mode BN: the HIP corners sit 1.0e-3 from fp32 (aten's
+    # autocast path 7.3e-3): floor 2e-2.  Train-mode BN: the batch statistics amplify every stage's bf16 rounding
+    # along the chain in BOTH paths (aten's own autocast path 1.2e-2-1.9e-2 from fp32 depending on its MIOpen
+    # algorithm choice, the HIP path 2.05e-2) although each stage of the HIP head is closer to fp32 than aten's
+    # (profiles/r05_head_stage_error.jsonl; test_head_stages_match_aten_per_stage below), so that chain keeps 3e-2
+    floor = 3e-2 if bn_train else 2e-2
+    assert err(outs[0], outs[2]) <= max(floor, 1.5 * err(outs[1], outs[2])), outs
     grads = [[xi.grad] + [p.grad for _, p in h.named_parameters()] for h, xi in zip(heads, xs)]
     names = ["x"] + [n for n, _ in hd.named_parameters()]
     # gradients that vanish mathematically (biases ahead of a train-mode BatchNorm or of the soft-argmax's
@@ -808,6 +812,54 @@ def test_head_forward_nhwc_matches_aten(bn_train):
     # all head parameters as one vector (as test_module_forward_training_gpu_grads' groups)
     cat = [torch.cat([g.flatten().float() for g, r in zip(gs[1:], grads[2][1:]) if r is not None]) for gs in grads]
     assert rel(cat[0], cat[2]) <= max(5e-2, 1.5 * rel(cat[1], cat[2])), (rel(cat[0], cat[2]), rel(cat[1], cat[2]))
+
+
+@pytest.mark.parametrize("bn_train", [False, True])
+def test_head_stages_match_aten_per_stage(bn_train):
+    """VERDICT r4 #6, per stage: every conv() block of the HIP training head (HIP 3x3 conv + HIP BatchNorm+ReLU,
+    bf16 operands) and aten's bf16 autocast block, each fed the SAME fp32 input, against the aten fp32 block --
+    the HIP block within max(1e-2, 1.5 x aten's) relative (measured: HIP 0.3-0.7 %, aten 0.5-1.6 %), so the
+    head's own arithmetic is not noisier than aten's; tools/head_stage_error.py prints the full table."""
+    import copy
+    import torch.nn.functional as F
+    import mmt_amd.model as M
+    from mmt_amd.train import HipOps
+    torch.manual_seed(3)
+    net = M.build_mixformer_vit_rgbt(M.hot_path_cfg(), train=False)
+    hd = net.box_head.cuda()
+    hd.train(bn_train)
+    heads = [hd, copy.deepcopy(hd), copy.deepcopy(hd)]  # HIP, aten bf16, aten fp32
+    x = torch.randn(2, hd.conv1_tl[0].weight.shape[1], 20, 20, device="cuda").bfloat16().float()
+    nchw, nhwc = (lambda t: t.permute(0, 3, 1, 2)), (lambda t: t.permute(0, 2, 3, 1))
+    up = lambda t, f: F.interpolate(t, scale_factor=f)  # noqa: E731
+    bad = []
+
+    def stage(name, inp, idx=None):
+        outs = []
+        for i, h in enumerate(heads):
+            seq = getattr(h, name)
+            seq = seq if idx is None else seq[idx]
+            with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16, enabled=i < 2):
+                if i == 0:
+                    y = HipOps.conv3x3(nhwc(inp).to(torch.bfloat16).contiguous(), seq[0].weight, seq[0].bias)
+                    outs.append(nchw(HipOps.bn_relu(y, seq[1])).float())
+                else:
+                    outs.append(seq(inp).float())
+        sc = outs[2].abs().max().item() + 1e-12
+        e_hip, e_aten = [(o - outs[2]).abs().max().item() / sc for o in outs[:2]]
+        if e_hip > max(1e-2, 1.5 * e_aten):
+            bad.append((name, idx, e_hip, e_aten))
+        return outs[2]
+
+    for br in ("tl", "br"):
+        x1 = stage("conv1_" + br, x)
+        x2 = stage("conv2_" + br, x1)
+        a1 = stage("adjust1_" + br, x)
+        x3 = stage("conv3_" + br, up(a1, 2) + up(x2, 2))
+        stage("conv4_" + br, up(stage("adjust2_" + br, x), 4) + up(x3, 2))
+        stage("adjust3_" + br, stage("adjust3_" + br, stage("adjust3_" + br, x2, 0), 1), 2)
+        stage("adjust4_" + br, stage("adjust4_" + br, x3, 0), 1)
+    assert not bad, bad
 
 
 @pytest.mark.parametrize("norm", ["sync", "frozen"])

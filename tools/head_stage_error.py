@@ -104,14 +104,19 @@ def main():
                 rows.append({"bn_train": bn_train, "branch": br, "stage": name + (" (abs)" if name == "corner" else ""),
                              "hip_rel": float("%.3g" % ((outs["hip"][name] - r).abs().max().item() / sc)),
                              "aten_bf16_rel": float("%.3g" % ((outs["aten_bf16"][name] - r).abs().max().item() / sc))})
-        # whole chains (as the test): HIP head_forward_nhwc, aten autocast, aten fp32
+        # whole chains (as the test): HIP head_forward_nhwc (conv5 in fp32, and in bf16 as before round 5),
+        # aten autocast, aten fp32
+        import mmt_amd.train as T
         chain = {}
-        for k, h in heads.items():
+        for k, h in list(heads.items()) + [("hip_c5bf16", hd)]:
             h2 = copy.deepcopy(h)
+            T.HEAD_SCORE_FP32 = k != "hip_c5bf16"
             with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16, enabled=k != "fp32"):
-                chain[k] = head_forward(h2, x, HipOps if k == "hip" else None).float()
+                chain[k] = head_forward(h2, x, HipOps if k.startswith("hip") else None).float()
+        T.HEAD_SCORE_FP32 = True
         rows.append({"bn_train": bn_train, "branch": "both", "stage": "chain corners (abs)",
                      "hip_rel": float("%.3g" % (chain["hip"] - chain["fp32"]).abs().max().item()),
+                     "hip_c5bf16_rel": float("%.3g" % (chain["hip_c5bf16"] - chain["fp32"]).abs().max().item()),
                      "aten_bf16_rel": float("%.3g" % (chain["aten_bf16"] - chain["fp32"]).abs().max().item())})
         for r in rows:
             print(json.dumps(r), flush=True)
