@@ -139,10 +139,13 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
     // panel / W slice is fetched into that XCD's L2 once and re-read from it (instead of the A
     // panels streaming in again from the Infinity Cache for every column tile).
     // (compiled into the large-M tiles only: in the batch-1 tile shapes the extra prologue code cost
-    // ~1 % of the frame, interleaved bench A/B 953.5 vs 944.5 frames/s)
+    // ~1 % of the frame, interleaved bench A/B 953.5 vs 944.5 frames/s).  Round 5: also for the two-per-CU
+    // 128x128 tiles (impl 8), which ran row-fastest over grids of thousands of tiles, so every XCD streamed
+    // all of A from the Infinity Cache: fc1 at 16 pairs 149.0 -> 128.2 us, the training step 470-471 ->
+    // 484 samples/s interleaved (profiles/r05_gemm_occ2_rowgroup_ab.txt)
     constexpr int GM = 8;
     int tm, tn;
-    if (BM * BN >= 256 * 128 && gridDim.x * gridDim.y * gridDim.z > 512 && tiles_m > GM) {
+    if ((BM * BN >= 256 * 128 || OCC > 1) && gridDim.x * gridDim.y * gridDim.z > 512 && tiles_m > GM) {
         const int tiles_n = ntiles / tiles_m, grp = tile / (GM * tiles_n), first = grp * GM;
         const int gsz = min(tiles_m - first, GM), r = tile - grp * GM * tiles_n;
         tm = first + r % gsz;
