@@ -30,6 +30,10 @@
 #ifndef MMT_GEMM_ABLATE
 #define MMT_GEMM_ABLATE 0
 #endif
+// A/B build knob: row tiles per row group of the large-grid tile order (below)
+#ifndef MMT_GEMM_GM
+#define MMT_GEMM_GM 8
+#endif
 // A/B build knob (tools/build_ablate.sh noocc2): 1 = the cost model never switches to impl 8
 #ifndef MMT_GEMM_NO_OCC2
 #define MMT_GEMM_NO_OCC2 0
@@ -143,7 +147,7 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
     // 128x128 tiles (impl 8), which ran row-fastest over grids of thousands of tiles, so every XCD streamed
     // all of A from the Infinity Cache: fc1 at 16 pairs 149.0 -> 128.2 us, the training step 470-471 ->
     // 484 samples/s interleaved (profiles/r05_gemm_occ2_rowgroup_ab.txt)
-    constexpr int GM = 8;
+    constexpr int GM = MMT_GEMM_GM;
     int tm, tn;
     if ((BM * BN >= 256 * 128 || OCC > 1) && gridDim.x * gridDim.y * gridDim.z > 512 && tiles_m > GM) {
         const int tiles_n = ntiles / tiles_m, grp = tile / (GM * tiles_n), first = grp * GM;
