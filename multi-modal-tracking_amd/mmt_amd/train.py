@@ -81,18 +81,18 @@ _SPLITK = {}  # device -> (slab workspace, arrival tickets) of the dW GEMMs' spl
 def _splitk_ws(dev):
     ws = _SPLITK.get(dev)
     if ws is None:
-        ws = _SPLITK[dev] = (torch.empty(16 << 20, device=dev, dtype=torch.float32),
+        ws = _SPLITK[dev] = (torch.empty(32 << 20, device=dev, dtype=torch.float32),
                              torch.zeros(1 << 16, device=dev, dtype=torch.int32))
     return ws
 
 
 def _gemm(a, w, M, N, K, bias=None, out_f32=False, act=0, r=None, c2=None, c2_copy=0, c=None, ldc=None, a_t=0,
-          w_t=0, ldw=0, lda=None, splitk=False, impl=0, row_scale=None, row_scale_div=1):
+          w_t=0, ldw=0, lda=None, splitk=False, impl=0, row_scale=None, row_scale_div=1, nsk=0):
     """C[M][N] = A[M][K] W[N][K]^T (+ bias), bf16 operands, fp32 accumulation (mmt_gemm); act / r (bf16,
     [M][N]) / c2 / c2_copy as mmt_gemm_params (act 1 GELU, 5 GELU backward against r; c2_copy 2: c2 = the
     pre-activation; 3: the last 8 columns to c2 [M][8]); c / ldc: a preallocated output and its pitch;
     a_t / w_t / ldw / lda: MN-major operands (A^T [K][lda], W^T [K][ldw]); splitk: with a split-K
-    workspace (the cost model may split K over workgroups).
+    workspace (the cost model may split K over workgroups; nsk >= 1 forces the slice count, A/B tools).
     Grouped form (the two-stream backbones in lockstep): a and w (and bias / r / c2 / c) tuples, one entry
     per group, one launch; without c the output is one [groups * M][N] tensor, group g on rows g M ..."""
     from ._lib import LIB, GemmParams, MMT_BF16, check
@@ -114,6 +114,7 @@ def _gemm(a, w, M, N, K, bias=None, out_f32=False, act=0, r=None, c2=None, c2_co
     if splitk:
         ws, cnt = _splitk_ws(A[0].device)
         p.sk_ws, p.sk_ws_floats, p.sk_cnt, p.sk_cnt_n = ws.data_ptr(), ws.numel(), cnt.data_ptr(), cnt.numel()
+        p.splitk = nsk
     p.a_seg_rows, p.a_segs_a = M, 1
     p.M, p.N, p.K, p.groups, p.c_f32 = M, N, K, G, 1 if out_f32 else 0
     p.act = act
