@@ -84,7 +84,8 @@ extern "C" {
  *   `dtype`, no R needed -- the training step's fc1 keeps it for the GELU backward; c2_copy 3: a
  *   column split, output columns [0, N-8) to C with pitch ldc >= N-8 and the last 8 columns to C2
  *   [M][8] (pitch 8), N % 8 == 0, no R needed -- the training dW GEMM, whose last column is the
- *   bias gradient; 16-bit LDS-DMA kernels).
+ *   bias gradient; c2_copy 4: as 3, but only column N-8 goes to C2, as a contiguous [M] vector (fp32
+ *   C); 16-bit LDS-DMA kernels).
  *   R row index: r_mode 0 -> m, 1 -> m % r_p0, 2 -> conv map m=(b,y,x) of an r_p0 x r_p0 map read
  *   at (y / r_p1, x / r_p1) of an (r_p0/r_p1)^2 map.  R is fp32 (or dtype if r_t); C/C2 are fp32
  *   if c_f32 else dtype.
@@ -110,7 +111,9 @@ typedef struct {
                      (8 waves), 2 128x64 (K split over 2 wave groups), 3 64x64 (K split 2),
                      4 128x128 (4 waves), 5 256x128 / 6 128x256 (8 waves, large M), 7 256x256
                      (8 waves, plain GEMM mode only: no ln_fold / conv / split-K), 8 128x128 at two
-                     workgroups per CU (64 KiB ring; same restrictions as 7; auto on big unsplit grids) */
+                     workgroups per CU (64 KiB ring; same restrictions as 7; auto on big unsplit grids),
+                     9 (A/B builds only, MMT_GEMM_AB) 256x256 at one wave per SIMD (4 waves of 128x128
+                     with AGPR accumulators; plain GEMM mode, ln_fold 0 / 2, row_scale) */
     /* LayerNorm folded into the GEMM (bf16 LDS-DMA kernels, GEMM mode): A holds the raw rows x
      * (K = the LayerNorm width), W = W_lin * gamma (per column k), and the epilogue's v is
      *   rstd_m * (acc - mu_m * ln_colsum[g][n]) + bias[g][n],   mu / rstd over the K values of row m
@@ -260,6 +263,14 @@ int mmt_layernorm(const float* in, const float* add, int64_t add_rows, float* ou
 int mmt_layernorm_bwd(const float* x, const void* dy, int dy_dtype, const float* gamma0, const float* gamma1,
                       float* dx, float* dgb, int dgb_accumulate, float* ws, int64_t ws_floats, int64_t rows,
                       int64_t rows_per_group, int C, float eps, void* stream);
+
+/* mmt_layernorm_bwd with a second gradient of the LayerNorm input added in the same pass: dx = (the
+ * LayerNorm backward as above) + dres, dres [rows][C] fp32 (may be dx itself).  The pre-LN block's residual
+ * stream feeds the LayerNorm and the residual add (x + f(LN(x)), mixformer.py:136-139): its two gradients meet
+ * here instead of in an extra elementwise pass over the stream. */
+int mmt_layernorm_bwd_add(const float* x, const void* dy, int dy_dtype, const float* gamma0, const float* gamma1,
+                          const float* dres, float* dx, float* dgb, int dgb_accumulate, float* ws, int64_t ws_floats,
+                          int64_t rows, int64_t rows_per_group, int C, float eps, void* stream);
 
 /* GroupNorm over [n_inst][P][Ctot] fp32 (channels-last, P positions, Ctot channels in `groups`
  * equal groups), per-instance affine set chosen by inst / inst_per_set (2 sets max).  Outputs

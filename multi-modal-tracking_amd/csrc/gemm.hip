@@ -326,8 +326,9 @@ template <typename T>
 int check_gemm(const mmt_gemm_params& p) {
     const int EPC = 16 / (int)sizeof(T);
     if (p.M <= 0 || p.N <= 0 || p.K <= 0 || p.groups < 1 || p.groups > MMT_MAX_GROUPS) return MMT_EBADARG;
-    if (p.impl < -1 || p.impl > 8) return MMT_EBADARG;
-    if (p.act < 0 || (p.act > 2 && p.act != 5) || p.c2_copy < 0 || p.c2_copy > 3) return MMT_EBADARG;
+    if (p.impl < -1 || p.impl > 9) return MMT_EBADARG;
+    if (p.act < 0 || (p.act > 2 && p.act != 5) || p.c2_copy < 0 || p.c2_copy > 4) return MMT_EBADARG;
+    if (p.c2_copy == 4 && !p.c_f32) return MMT_EBADARG;
     if (p.K % EPC || p.lda % EPC) return MMT_EBADARG;
     if (p.conv_h > 0) {
         if (p.conv_cin % EPC || p.conv_up < 1 || p.conv_h % p.conv_up) return MMT_EBADARG;
@@ -354,7 +355,7 @@ int check_gemm(const mmt_gemm_params& p) {
         if (p.k_split > 0 && p.conv_h == 0 && (!p.a1[g] || ((uintptr_t)p.a1[g] & 15))) return MMT_EBADARG;
         if (p.c2[g] && !p.r[g] && p.c2_copy < 2) return MMT_EBADARG;
         if ((p.act == 5 && !p.r[g]) || (p.c2_copy >= 2 && !p.c2[g])) return MMT_EBADARG;
-        if (p.c2_copy == 3 && (p.N % 8 || p.ldc < p.N - 8)) return MMT_EBADARG;
+        if (p.c2_copy >= 3 && (p.N % 8 || p.ldc < p.N - 8)) return MMT_EBADARG;
         if (p.w_t && (((uintptr_t)p.w[g] & 15) || (p.a_t && ((uintptr_t)p.a[g] & 15)))) return MMT_EBADARG;
     }
     return 0;

@@ -34,6 +34,16 @@
 #ifndef MMT_GEMM_GM
 #define MMT_GEMM_GM 8
 #endif
+// A/B build (tools/build_ablate.sh ab): 1 = also compile impl 9 (the 256x256 one-wave-per-SIMD tile; measured
+// slower than the product's tiles with the fused epilogues)
+#ifndef MMT_GEMM_AB
+#define MMT_GEMM_AB 0
+#endif
+// A/B build knob (tools/build_ablate.sh occ2nores): 0 = the residual producers that hand LayerNorm statistics
+// on (inference proj / fc2 with ln_stats_out) stay off impl 8, as before round 5
+#ifndef MMT_GEMM_OCC2_RES
+#define MMT_GEMM_OCC2_RES 1
+#endif
 // A/B build knob (tools/build_ablate.sh noocc2): 1 = the cost model never switches to impl 8
 #ifndef MMT_GEMM_NO_OCC2
 #define MMT_GEMM_NO_OCC2 0
@@ -127,12 +137,19 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
     constexpr int WM = BM / WGM, WN = BN / WGN, MT = WM / 16, NT = WN / 16;
     static_assert(KS * ST * STAGE <= 160 * 1024, "LDS budget");
     constexpr bool SB = BM * BN >= 256 * 256 || OCC > 1;  // single-buffered fragments (impl 7's 256x256; impl 8)
-    static_assert(!SB || (KS == 1 && (LNM == 0 || LNM >= 3) && !CONV), "impl 7: plain GEMM only");
+    // impl 9: 256x256 at ONE wave per SIMD (4 waves of 128x128, the 256 accumulators pinned to AGPRs by
+    // inline-asm MFMAs), 2-slot ring of 64-deep stages; LayerNorm fold with handed-in statistics allowed
+    constexpr bool W4 = BM == 256 && BN == 256 && NW == 4;
+    static_assert(!W4 || (KS == 1 && ST == 2 && OCC == 1 && !CONV && (LNM == 0 || LNM == 2)), "impl 9 geometry");
+    static_assert(!SB || (KS == 1 && (LNM == 0 || LNM >= 3 || W4) && !CONV), "impl 7: plain GEMM only");
     // LNM 3: W given MN-major (W^T [K][ldw], the Linear backward's dX); 4: A and W MN-major (dW)
     constexpr bool TA = LNM == 4, TB = LNM == 3 || LNM == 4;
     static_assert(!TB || (BM == 128 && BN == 128 && !CONV), "MN-major operands: 128x128 tiles");
     static_assert(KS == 1 || BM * BN * 4 <= KS * ST * STAGE, "k-group reduction buffer");
-    __shared__ __attribute__((aligned(1024))) unsigned char lds[KS * ST * STAGE];
+    // impl 9: its half-tile fp32 image (128 x 260 floats) and the row statistics exceed the 128 KiB ring
+    constexpr int LDS_BYTES = W4 ? (BM / 2) * (BN + 4) * 4 + BM * 8 + 64 : KS * ST * STAGE;
+    static_assert(LDS_BYTES >= KS * ST * STAGE && LDS_BYTES <= 160 * 1024, "LDS budget");
+    __shared__ __attribute__((aligned(1024))) unsigned char lds[LDS_BYTES];
     MMT_STAMP(0, "s_memrealtime");
     MMT_STAMP(1, "s_memtime");
 
@@ -430,10 +447,78 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
             MMT_MMA(fa0, fb0, MTV);
         }
     };
-    const int mtv = __builtin_amdgcn_readfirstlane(min(max((M - m0_tile - wr * WM + 15) / 16, 0), MT));
-    if (mtv == 0) kloop(gemm_ic<0>{});
-    else if (mtv == 1 && MT > 1) kloop(gemm_ic<1>{});
-    else kloop(gemm_ic<MT>{});  // whole fragments (other partial counts: padding computed, not stored)
+    if constexpr (W4) {
+        // impl 9: one wave per SIMD, each a 128x128 wave tile = 64 v_mfma_f32_16x16x32 per 32-deep half.  The
+        // accumulators are inline-asm operands with the "a" constraint (all 256 AGPRs: through the builtin hipcc
+        // shuttled them through VGPRs every step and spilled).  Half t+1's fragments are read beside half t's 64
+        // MFMAs (two statically named fragment sets); one K-step of DMA is in flight behind the one multiplied
+        // (2-slot ring of 64 KiB stages: a 4-slot ring of 32-deep stages measured the same,
+        // profiles/r05_gemm256_proto.jsonl).  Rows past M (last row tile) are computed from clamped rows and not
+        // stored.  No MFMA sits under a branch (hipcc then keeps the accumulators in place).
+        u32x4 fa[2][MT], fb[2][NT];
+        auto rd = [&](int s, int t, u32x4 (&af)[MT], u32x4 (&bf)[NT]) {
+            const unsigned char* b_ = ring + (s % ST) * STAGE;
+            const int sw_ = (4 * t + lg) ^ (lane & 7);
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) af[mt] = frag_a(b_, t, sw_, mt);
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) bf[nt] = frag_b(b_, t, sw_, nt);
+        };
+        auto mma = [&](const u32x4 (&af)[MT], const u32x4 (&bf)[NT]) {
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt) {
+                    // s_nop 1: covers a VALU write of a fragment register hipcc might place just before (it does
+                    // not see the MFMA inside the asm)
+                    if constexpr (__is_same(T, bf16_t))
+                        asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
+                                     : "+a"(acc[nt][mt]) : "v"(bf[nt]), "v"(af[mt]));
+                    else
+                        asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_f16 %0, %1, %2, %0"
+                                     : "+a"(acc[nt][mt]) : "v"(bf[nt]), "v"(af[mt]));
+                }
+        };
+        issue(0);
+        if (ns > 1) {
+            issue(1);
+            wait_vm<L>();  // step 0 landed (step 1's L pieces may stay in flight)
+        } else {
+            wait_vm<0>();
+        }
+        lds_barrier();
+        rd(0, 0, fa[0], fb[0]);
+        for (int s = 0; s + 1 < ns; ++s) {
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0) as a builtin: hipcc then knows fa[0] / fb[0] are in
+            __builtin_amdgcn_sched_barrier(0);
+            rd(s, 1, fa[1], fb[1]);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(fa[0], fb[0]);
+            __builtin_amdgcn_sched_barrier(0);
+            wait_vm<0>();   // step s+1 landed (nothing newer in flight)
+            lds_barrier();  // every wave is past its reads of slot s % 2
+            if (s + 2 < ns) issue(s + 2);
+            rd(s + 1, 0, fa[0], fb[0]);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(fa[1], fb[1]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_sched_barrier(0);
+        rd(ns - 1, 1, fa[1], fb[1]);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(fa[0], fb[0]);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(fa[1], fb[1]);
+        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" ::: "memory");  // last MFMA results -> accvgpr reads
+    } else {
+        const int mtv = __builtin_amdgcn_readfirstlane(min(max((M - m0_tile - wr * WM + 15) / 16, 0), MT));
+        if (mtv == 0) kloop(gemm_ic<0>{});
+        else if (mtv == 1 && MT > 1) kloop(gemm_ic<1>{});
+        else kloop(gemm_ic<MT>{});  // whole fragments (other partial counts: padding computed, not stored)
+    }
 #undef MMT_READ
 #undef MMT_MMA
 #undef MMT_PIN
@@ -449,22 +534,24 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
     // EPASS: a tile whose fp32 image does not fit the stage ring (256x256) is assembled and written
     // out in WGM passes of one wave row (WM rows) each
     constexpr int EPASS = BM * TP * 4 + KS * BM * 8 + 16 <= KS * ST * STAGE ? 1 : WGM, EB = BM / EPASS;
-    static_assert(EPASS == 1 || (EB == WM && KS == 1 && (LNM == 0 || LNM >= 3)), "multi-pass epilogue: plain GEMM tiles");
-    static_assert(EB * TP * 4 <= KS * ST * STAGE, "epilogue pass fits in the stage ring");
+    static_assert(EPASS == 1 || (EB == WM && KS == 1 && (LNM == 0 || LNM >= 3 || (W4 && LNM == 2))),
+                  "multi-pass epilogue: plain GEMM tiles (impl 9: also with handed-in LayerNorm statistics)");
+    static_assert(EB * TP * 4 + KS * BM * 8 + 4 <= LDS_BYTES, "epilogue pass fits in LDS");
     constexpr int FLAG_OFF = EB * TP * 4 + KS * BM * 8;  // split-K "this workgroup sums" word
     float* ctile = (float*)lds;
-    float* rstat = ctile + BM * TP;  // LNF: [KS][BM][2] partial (sum x, sum x^2) per k-group
+    float* rstat = ctile + EB * TP;  // LNF: [KS][BM][2] partial (sum x, sum x^2) per k-group (all BM tile rows)
     // LNM 2: the handed-in row statistics (K/64 partial (sum, sum of squares) pairs per A row), read
     // now so that their latency overlaps the tile's LDS assembly: TPRW threads per tile row, each
     // loading every TPRW-th pair of its row (at most 8: K <= 64 * 8 * TPRW), summed below
     constexpr int NTH_E = TPG * KS, TPRW = NTH_E / BM;
     static_assert(TPRW >= 1 && (TPRW & (TPRW - 1)) == 0 && TPRW <= 64, "statistics reduction geometry");
-    f32x2 stp[8];
+    constexpr int NSP = TPRW >= 2 ? 8 : 16;  // pairs per thread (K <= 64 * 16, glds_takes)
+    f32x2 stp[NSP];
     const int kp = K / 64, srow = threadIdx.x / TPRW, spart = threadIdx.x % TPRW;
     if constexpr (LNM == 2) {
         const f32x2* st = (const f32x2*)p.ln_stats_in[g] + (int64_t)min(m0_tile + srow, M - 1) * kp;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < NSP; ++i) {
             const int j = spart + i * TPRW;
             stp[i] = j < kp ? st[j] : f32x2{0.f, 0.f};
         }
@@ -508,7 +595,7 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
     if constexpr (LNM == 2) {  // (sum, sum of squares) of the row, in pair order within each thread
         float sx = 0.f, sxx = 0.f;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < NSP; ++i) {
             sx += stp[i][0];
             sxx += stp[i][1];
         }
@@ -645,11 +732,14 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
         }
     }
     const int n = n0 + tc, nc = min(n, N - 8);
-    float* stats_out = p.c2_copy && p.c2_copy != 3 && C2 ? p.ln_stats_out[g] : nullptr;
-    // c2_copy 3: the last 8 output columns go to C2 (row pitch 8), the others to C (pitch ldc >= N - 8)
-    const bool colsplit = p.c2_copy == 3 && n >= N - 8;
+    const bool csplit = p.c2_copy == 3 || p.c2_copy == 4;
+    float* stats_out = p.c2_copy && !csplit && C2 ? p.ln_stats_out[g] : nullptr;
+    // c2_copy 3: the last 8 output columns go to C2 (row pitch 8), the others to C (pitch ldc >= N - 8);
+    // c2_copy 4: of those 8 only column N - 8, to C2 as one contiguous vector (row pitch 1: the training dW
+    // GEMM's bias gradient, handed to autograd as it is)
+    const bool colsplit = csplit && n >= N - 8;
     char* Cs = colsplit ? C2 : C;
-    if (p.c2_copy == 3) C2 = nullptr;
+    if (csplit) C2 = nullptr;
     f32x4 bn0 = {0.f, 0.f, 0.f, 0.f}, bn1 = bn0, cs0 = bn0, cs1 = bn0;
     if (bias) {
         bn0 = *(const f32x4*)(bias + nc);
@@ -695,8 +785,8 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
                 constexpr int NQ = LNM == 1 ? KS : 1;
 #pragma unroll
                 for (int q = 0; q < NQ; ++q) {
-                    sx += rstat[(q * BM + r) * 2];
-                    sxx += rstat[(q * BM + r) * 2 + 1];
+                    sx += rstat[(q * BM + ep * EB + r) * 2];
+                    sxx += rstat[(q * BM + ep * EB + r) * 2 + 1];
                 }
                 const float mu = sx * inv_k, var = fmaxf(sxx * inv_k - mu * mu, 0.f);
                 const float rstd = rsqrtf(var + p.ln_eps);
@@ -807,8 +897,8 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
                 constexpr int NQ = LNM == 1 ? KS : 1;  // LNM 2: one (sum, sum x^2) pair per row
 #pragma unroll
                 for (int q = 0; q < NQ; ++q) {
-                    sx += rstat[(q * BM + r) * 2];
-                    sxx += rstat[(q * BM + r) * 2 + 1];
+                    sx += rstat[(q * BM + ep * EB + r) * 2];
+                    sxx += rstat[(q * BM + ep * EB + r) * 2 + 1];
                 }
                 const float mu = sx * inv_k, var = fmaxf(sxx * inv_k - mu * mu, 0.f);
                 const float rstd = rsqrtf(var + p.ln_eps);
@@ -863,7 +953,9 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
             }
             if (m < M && n < N && (MMT_GEMM_ABLATE != 3 || oa[0] == -1.2345e30f)) {  // (3: measurement, no stores)
                 const int64_t e = crow(m) * p.ldc + n, es = colsplit ? crow(m) * 8 : e;
-                if (p.c_f32) {
+                if (colsplit && p.c2_copy == 4) {
+                    ((float*)Cs)[crow(m)] = oa[0];  // (fp32 outputs: the launcher checks)
+                } else if (p.c_f32) {
                     *(f32x4*)((float*)Cs + es) = oa;
                     *(f32x4*)((float*)Cs + es + 4) = ob;
                     if (C2 && p.c2_copy == 2) {  // the pre-activation in the compute dtype
@@ -950,6 +1042,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     gemm_glds_tile<T, 128, 128, 2, 4, 1, 2, false, LNM, 2, false, EPI>(p, g, tile, slice, nsk, gridDim.x);
 }
 
+// impl 9: the 256x256 tile at one wave per SIMD (4 waves of 128x128, accumulators in AGPRs), one workgroup per
+// CU; plain GEMM mode, optionally with the LayerNorm fold on handed-in statistics (LNM 2) or the row scale (RS)
+#if MMT_GEMM_AB
+template <typename T, int LNM, bool RS = false, int EPI = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_glds_kernel_w4(
+    const mmt_gemm_params p) {
+    const int lin = gemm_xcd_lin();
+    const int g = lin / gridDim.x, tile = lin - g * gridDim.x;
+    gemm_glds_tile<T, 256, 256, 2, 2, 1, 2, false, LNM, 1, RS, EPI>(p, g, tile, 0, 1, gridDim.x);
+}
+#endif
+
 // Several independent GEMMs of one kernel configuration in one launch (mmt_gemm_multi): problem i
 // owns the remapped linear ids [wg0[i], wg0[i + 1]), (group, tile) with the tile fastest, no split-K.
 // The head's parallel conv chains and the fusion encoder's value / offset Linears are each a
@@ -1025,6 +1129,32 @@ void launch(const mmt_gemm_params& p, int nsk, hipStream_t st) {
         hipLaunchKernelGGL((gemm_glds_kernel<T, BM, BN, WGM, WGN, KS, ST, false, 0>), grid, block, 0, st, p);
 }
 
+// impl 9's launch: 1 when the mode is not one it takes (LayerNorm summed in the K loop, conv, MN-major operands)
+template <typename T>
+int launch_w4(const mmt_gemm_params& p, hipStream_t st) {
+#if !MMT_GEMM_AB
+    return 1;  // A/B build only
+#else
+    if ((p.ln_fold != 0 && p.ln_fold != 2) || p.conv_h > 0 || p.a_t || p.w_t) return 1;
+    const dim3 grid((unsigned)(((p.M + 255) / 256) * ((p.N + 255) / 256)), 1, p.groups), block(256);
+    if (p.row_scale) {
+        if (p.ln_fold) return 1;
+        if (residual_epilogue(p, true)) hipLaunchKernelGGL((gemm_glds_kernel_w4<T, 0, true, 2>), grid, block, 0, st, p);
+        else hipLaunchKernelGGL((gemm_glds_kernel_w4<T, 0, true>), grid, block, 0, st, p);
+    } else if (p.ln_fold == 2) {
+        if (compact_epilogue(p)) hipLaunchKernelGGL((gemm_glds_kernel_w4<T, 2, false, 1>), grid, block, 0, st, p);
+        else hipLaunchKernelGGL((gemm_glds_kernel_w4<T, 2>), grid, block, 0, st, p);
+    } else if (compact_epilogue(p)) {
+        hipLaunchKernelGGL((gemm_glds_kernel_w4<T, 0, false, 1>), grid, block, 0, st, p);
+    } else if (residual_epilogue(p)) {
+        hipLaunchKernelGGL((gemm_glds_kernel_w4<T, 0, false, 2>), grid, block, 0, st, p);
+    } else {
+        hipLaunchKernelGGL((gemm_glds_kernel_w4<T, 0>), grid, block, 0, st, p);
+    }
+    return 0;
+#endif
+}
+
 bool aligned(const void* ptr, int bytes) { return ((uintptr_t)ptr & (uintptr_t)(bytes - 1)) == 0; }
 
 // Whether the shape / layout is one the LDS-DMA kernel takes.
@@ -1095,6 +1225,7 @@ int mmt_gemm_glds(const mmt_gemm_params& p, hipStream_t st, int force) {
     };
     int cfg = force, nsk = 1;
     if (p.row_scale) {  // the training step's residual branches: impl 8's tile with the row-scale epilogue
+        if (force == 9) return launch_w4<T>(p, st);
         if ((force != 0 && force != 8) || p.ln_fold || p.conv_h > 0 || p.a_t || p.w_t) return 1;
         const dim3 grid((unsigned)tiles_of(p, 128, 128), 1, p.groups);
         if (residual_epilogue(p, true))
@@ -1160,8 +1291,14 @@ int mmt_gemm_glds(const mmt_gemm_params& p, hipStream_t st, int force) {
         // 256x256 tile (impl 7) keeps its shapes (dX of fc2: 597 vs 525 TFLOP/s)
         // Not for the inference residual producers (C2 copy + LayerNorm statistics out: config 3 at 64
         // sequences 2650 -> 2541 frames/s with them on impl 8, interleaved, profiles/r03_gemm_occ2_ab.jsonl)
-        if (!MMT_GEMM_NO_OCC2 && big && nsk == 1 && !p.ln_fold && p.conv_h == 0 && !p.ln_stats_out[0] &&
-            (cfg == 1 || cfg == 5 || cfg == 6))
+        // Round 5: also instead of impl 7, since impl 8's row-group tile order (above) it is faster on every
+        // shape impl 7 took (two groups of 8448 rows: qkv 102.0 -> 81.5 us, the dX-like N 3072 / K 768 129.1 ->
+        // 104.3 us; profiles/r05_gemm_w4_ab.jsonl)
+        // Round 5: and for the residual producers with the LayerNorm-statistics hand-off (round 3 kept them off: config 3
+        // at 64 sequences 2650 -> 2541 frames/s; with the row-group order the proj entry of that plan runs 211.5 ->
+        // 180.4 us, fc2 444.0 -> 445.0, profiles/r05_c3_entry_ab.jsonl)
+        if (!MMT_GEMM_NO_OCC2 && big && nsk == 1 && !p.ln_fold && p.conv_h == 0 &&
+            (MMT_GEMM_OCC2_RES || !p.ln_stats_out[0]) && (cfg == 1 || cfg == 5 || cfg == 6 || cfg == 7))
             cfg = 8;
     } else if (cfg == 8) {
         nsk = 1;  // impl 8: no split-K
@@ -1202,6 +1339,7 @@ int mmt_gemm_glds(const mmt_gemm_params& p, hipStream_t st, int force) {
                     hipLaunchKernelGGL((gemm_glds_kernel_occ2<T, 128, 128, 2, 4, 1, 2>), grid, dim3(512), 0, st, p);
             }
             break;
+        case 9: return launch_w4<T>(p, st);
         default: return 1;
     }
     return 0;

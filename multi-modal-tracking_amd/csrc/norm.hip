@@ -3,7 +3,8 @@
 //                    per-modality norm1_v/_i, norm2_v/_i, mixformer_shared.py:149-157) and of the
 //                    fusion encoder (eps 1e-5, deformable_encoder_lnspecific.py:153-155 with the
 //                    src + output_proj residual fused in via a broadcast row map)
-//   mmt_layernorm_bwd  its backward for the training step (dx, per-group dgamma / dbeta)
+//   mmt_layernorm_bwd  its backward for the training step (dx, per-group dgamma / dbeta); _add: plus the
+//                      input's second gradient (the block's residual add) in the same pass
 //   mmt_groupnorm    nn.GroupNorm(32) after the fusion 1x1 convs (fusion_utils.py:252-268)
 //   mmt_groupnorm_bwd  its backward for the training step (dx, dgamma / dbeta; channels-last)
 //   mmt_add_cast     src + pos -> bf16 query staging (ms_deform_attn_bimodal.py:93-95)
@@ -165,11 +166,12 @@ __global__ __launch_bounds__(GN_THREADS) void groupnorm_kernel(const float* __re
 // workgroup order (deterministic, no atomics) into dgb.
 constexpr int LNB_RPW = 32;
 
+// dres != NULL: dx += dres (the input's second gradient, the residual add of a pre-LN block; may alias dx).
 template <typename TD, int V>
 __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restrict__ x, const TD* __restrict__ dy,
-                                                            const float* g0, const float* g1, float* __restrict__ dx,
-                                                            float* __restrict__ part, int64_t rows, int64_t rpg,
-                                                            float eps) {
+                                                            const float* g0, const float* g1, const float* dres,
+                                                            float* dx, float* __restrict__ part, int64_t rows,
+                                                            int64_t rpg, float eps) {
     constexpr int C = 256 * V;
     __shared__ float4 red[4][4][V][64];  // [wave][group x (dgamma, dbeta)][V][lane]
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -228,6 +230,10 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
             o.y = rstd * (d[i].y - mg - v[i].y * mgx);
             o.z = rstd * (d[i].z - mg - v[i].z * mgx);
             o.w = rstd * (d[i].w - mg - v[i].w * mgx);
+            if (dres) {  // wave-uniform
+                const float4 r = ((const float4*)(dres + row * C))[lane + 64 * i];
+                o.x += r.x; o.y += r.y; o.z += r.z; o.w += r.w;
+            }
             ((float4*)(dx + row * C))[lane + 64 * i] = o;
         }
     }
@@ -253,26 +259,36 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
     }
 }
 
-// dgb[j][c] += sum over workgroups b (in order) of part[b][j][c]; j = group * 2 + (0 gamma, 1 beta).
-// One thread per (j, c); the partials are loaded 16 at a time (independent loads in flight) and added
-// in workgroup order, so the sum is the same on every launch.
-__global__ __launch_bounds__(64) void layernorm_bwd_reduce_kernel(const float* __restrict__ part, float* dgb, int nwg,
-                                                                  int C, int sets, int accumulate) {
-    const int i = blockIdx.x * 64 + threadIdx.x;
-    if (i >= sets * C) return;
-    const float* col = part + i;
+// dgb[j][c] += sum over workgroups b of part[b][j][c]; j = group * 2 + (0 gamma, 1 beta).
+// 64 (j, c) columns per 256-thread workgroup, each column's partials cut into 4 contiguous runs of workgroups,
+// one wave per run: every thread adds its run in workgroup order (16 loads in flight), then the 4 run sums are
+// added in run order, so the sum is the same on every launch (round 5: one thread per column walked all of a
+// column's ~530 partials alone, 14 us per launch at 16 training pairs).
+__global__ __launch_bounds__(256) void layernorm_bwd_reduce_kernel(const float* __restrict__ part, float* dgb, int nwg,
+                                                                   int C, int sets, int accumulate) {
+    __shared__ float red[4][64];
+    const int lane = threadIdx.x & 63, run = threadIdx.x >> 6;
+    const int i = blockIdx.x * 64 + lane;
+    const int ic = min(i, sets * C - 1);
+    const float* col = part + ic;
     const int64_t st = (int64_t)4 * C;
+    const int b1 = (int)((int64_t)(run + 1) * nwg / 4);
     float s = 0.f;
-    int b = 0;
-    for (; b + 16 <= nwg; b += 16) {
+    int b = (int)((int64_t)run * nwg / 4);
+    for (; b + 16 <= b1; b += 16) {
         float v[16];
 #pragma unroll
         for (int u = 0; u < 16; ++u) v[u] = col[(b + u) * st];
 #pragma unroll
         for (int u = 0; u < 16; ++u) s += v[u];
     }
-    for (; b < nwg; ++b) s += col[b * st];
-    dgb[i] = accumulate ? dgb[i] + s : s;
+    for (; b < b1; ++b) s += col[b * st];
+    red[run][lane] = s;
+    __syncthreads();
+    if (run == 0 && i < sets * C) {
+        const float t = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+        dgb[i] = accumulate ? dgb[i] + t : t;
+    }
 }
 
 // GroupNorm backward (training step): one 512-thread workgroup per (instance, group) as the forward, the
@@ -493,14 +509,15 @@ extern "C" int mmt_layernorm(const float* in, const float* add, int64_t add_rows
     return launch_status();
 }
 
-extern "C" int mmt_layernorm_bwd(const float* x, const void* dy, int dy_dtype, const float* gamma0,
-                                 const float* gamma1, float* dx, float* dgb, int dgb_accumulate, float* ws,
-                                 int64_t ws_floats, int64_t rows, int64_t rows_per_group, int C, float eps,
-                                 void* stream) {
+extern "C" int mmt_layernorm_bwd_add(const float* x, const void* dy, int dy_dtype, const float* gamma0,
+                                     const float* gamma1, const float* dres, float* dx, float* dgb, int dgb_accumulate,
+                                     float* ws, int64_t ws_floats, int64_t rows, int64_t rows_per_group, int C,
+                                     float eps, void* stream) {
     if (!x || !dy || !gamma0 || !dx || !dgb || !ws || rows <= 0 || (C % 256) || C < 256 || C > 1024) return MMT_EBADARG;
     if (gamma1 && rows_per_group <= 0) return MMT_EBADARG;
     if (!gamma1) rows_per_group = rows;
-    if (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)gamma0 | (uintptr_t)gamma1 | (uintptr_t)dx | (uintptr_t)ws) & 15)
+    if (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)gamma0 | (uintptr_t)gamma1 | (uintptr_t)dx | (uintptr_t)ws |
+         (uintptr_t)dres) & 15)
         return MMT_EBADARG;
     const int64_t nwg = (rows + LNB_RPW - 1) / LNB_RPW;
     if (nwg > INT32_MAX || ws_floats < nwg * 4 * C) return MMT_EBADARG;
@@ -508,7 +525,7 @@ extern "C" int mmt_layernorm_bwd(const float* x, const void* dy, int dy_dtype, c
     const int V = C / 256;
 #define LNB_CASE(TD, VV)                                                                                           \
     hipLaunchKernelGGL((layernorm_bwd_kernel<TD, VV>), dim3((unsigned)nwg), dim3(256), 0, st, x, (const TD*)dy,    \
-                       gamma0, gamma1, dx, ws, rows, rows_per_group, eps)
+                       gamma0, gamma1, dres, dx, ws, rows, rows_per_group, eps)
 #define LNB_V(TD)                                                                                                  \
     if (V == 1) LNB_CASE(TD, 1); else if (V == 2) LNB_CASE(TD, 2); else if (V == 3) LNB_CASE(TD, 3); else LNB_CASE(TD, 4)
     if (dy_dtype == MMT_BF16) { LNB_V(bf16_t); }
@@ -518,9 +535,17 @@ extern "C" int mmt_layernorm_bwd(const float* x, const void* dy, int dy_dtype, c
 #undef LNB_V
 #undef LNB_CASE
     const int sets = gamma1 ? 4 : 2;
-    hipLaunchKernelGGL(layernorm_bwd_reduce_kernel, dim3((unsigned)((sets * C + 63) / 64)), dim3(64), 0, st, ws, dgb,
+    hipLaunchKernelGGL(layernorm_bwd_reduce_kernel, dim3((unsigned)((sets * C + 63) / 64)), dim3(256), 0, st, ws, dgb,
                        (int)nwg, C, sets, dgb_accumulate);
     return launch_status();
+}
+
+extern "C" int mmt_layernorm_bwd(const float* x, const void* dy, int dy_dtype, const float* gamma0,
+                                 const float* gamma1, float* dx, float* dgb, int dgb_accumulate, float* ws,
+                                 int64_t ws_floats, int64_t rows, int64_t rows_per_group, int C, float eps,
+                                 void* stream) {
+    return mmt_layernorm_bwd_add(x, dy, dy_dtype, gamma0, gamma1, nullptr, dx, dgb, dgb_accumulate, ws, ws_floats,
+                                 rows, rows_per_group, C, eps, stream);
 }
 
 extern "C" int mmt_groupnorm(const float* in, float* out_f32, void* out_t, const float* gamma0, const float* beta0,

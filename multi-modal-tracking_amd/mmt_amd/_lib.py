@@ -75,6 +75,7 @@ _PROTOS = {
     "mmt_batchnorm_relu_bwd": [vp, vp, vp, i64, i32, i32, vp, vp, i32, i32, vp, vp, i64, vp],
     "mmt_layernorm": [vp, vp, i64, vp, vp, vp, vp, vp, vp, i64, i64, i32, f32, i32, vp],
     "mmt_layernorm_bwd": [vp, vp, i32, vp, vp, vp, vp, i32, vp, i64, i64, i64, i32, f32, vp],
+    "mmt_layernorm_bwd_add": [vp, vp, i32, vp, vp, vp, vp, vp, i32, vp, i64, i64, i64, i32, f32, vp],
     "mmt_groupnorm": [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, f32, i32, vp],
     "mmt_groupnorm_bwd": [vp, vp, vp, vp, vp, i32, vp, i64, i32, i32, i32, i32, f32, vp],
     "mmt_add_cast": [vp, vp, i64, vp, vp, i64, i32, vp],

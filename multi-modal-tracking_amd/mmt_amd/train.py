@@ -90,7 +90,8 @@ def _gemm(a, w, M, N, K, bias=None, out_f32=False, act=0, r=None, c2=None, c2_co
           w_t=0, ldw=0, lda=None, splitk=False, impl=0, row_scale=None, row_scale_div=1, nsk=0):
     """C[M][N] = A[M][K] W[N][K]^T (+ bias), bf16 operands, fp32 accumulation (mmt_gemm); act / r (bf16,
     [M][N]) / c2 / c2_copy as mmt_gemm_params (act 1 GELU, 5 GELU backward against r; c2_copy 2: c2 = the
-    pre-activation; 3: the last 8 columns to c2 [M][8]); c / ldc: a preallocated output and its pitch;
+    pre-activation; 3: the last 8 columns to c2 [M][8]; 4: column N - 8 alone to c2 [M]); c / ldc: a
+    preallocated output and its pitch;
     a_t / w_t / ldw / lda: MN-major operands (A^T [K][lda], W^T [K][ldw]); splitk: with a split-K
     workspace (the cost model may split K over workgroups; nsk >= 1 forces the slice count, A/B tools).
     Grouped form (the two-stream backbones in lockstep): a and w (and bias / r / c2 / c) tuples, one entry
@@ -148,18 +149,19 @@ def _bf16_weight(w):
 def _weight_grads(dy, x, M, N, K):
     """dW [N][K] and db [N] of y = x W^T + b from one GEMM: dy^T [x | 1] (a row of ones appended to the
     transposed activations gives the bias gradient as output column K; fp32 accumulation).  The GEMM
-    writes dW contiguous and its last 8 columns (db, then zeros) to a [N][8] block behind it (c2_copy 3),
-    so autograd takes dW as the parameter's .grad as it is (no accumulate / copy pass)."""
-    buf = torch.empty(N * (K + 8), device=dy.device, dtype=torch.float32)
-    dw, db8 = buf[:N * K].view(N, K), buf[N * K:].view(N, 8)
+    writes dW contiguous and the bias column alone as a contiguous [N] vector behind it (c2_copy 4), so
+    autograd takes both as the parameters' .grad as they are (round 5: a strided db column was cloned by
+    AccumulateGrad, ~100 small copy launches per training step)."""
+    buf = torch.empty(N * (K + 1), device=dy.device, dtype=torch.float32)
+    dw, db = buf[:N * K].view(N, K), buf[N * K:]
     if MN_MAJOR and M % 8 == 0:  # dY [M][N] and X [M][K] read as they are (a_t, w_t 2: the ones column)
-        _gemm(dy, x, N, K + 8, M, out_f32=True, c=dw, ldc=K, c2=db8, c2_copy=3, a_t=1, w_t=2, ldw=K, lda=N,
+        _gemm(dy, x, N, K + 8, M, out_f32=True, c=dw, ldc=K, c2=db, c2_copy=4, a_t=1, w_t=2, ldw=K, lda=N,
               splitk=True)
-        return dw, db8[:, 0]
+        return dw, db
     Mp = (M + 7) // 8 * 8  # contraction over tokens, zero-padded to the GEMM's K granule
     _gemm(_transpose(dy, M, N, Mp), _transpose(x, M, K, Mp, ones_row=True), N, K + 8, Mp, out_f32=True,
-          c=dw, ldc=K, c2=db8, c2_copy=3)
-    return dw, db8[:, 0]
+          c=dw, ldc=K, c2=db, c2_copy=4)
+    return dw, db
 
 
 def _dx(dy, wb, M, N, K, act=0, r=None):
@@ -313,14 +315,14 @@ def _halves(t, M):
 
 def _weight_grads2(dy, x, M, N, K):
     """_weight_grads of both modalities (dy [2M][N], x [2M][K]) in one launch: ((dW, db) RGB, (dW, db) TIR)."""
-    bufs = [torch.empty(N * (K + 8), device=dy.device, dtype=torch.float32) for _ in range(2)]
+    bufs = [torch.empty(N * (K + 1), device=dy.device, dtype=torch.float32) for _ in range(2)]
     dws = tuple(b[:N * K].view(N, K) for b in bufs)
-    dbs = tuple(b[N * K:].view(N, 8) for b in bufs)
+    dbs = tuple(b[N * K:] for b in bufs)
     if not (MN_MAJOR and M % 8 == 0):
         return [_weight_grads(u, v, M, N, K) for u, v in zip(_halves(dy, M), _halves(x, M))]
-    _gemm(_halves(dy, M), _halves(x, M), N, K + 8, M, out_f32=True, c=dws, ldc=K, c2=dbs, c2_copy=3, a_t=1,
+    _gemm(_halves(dy, M), _halves(x, M), N, K + 8, M, out_f32=True, c=dws, ldc=K, c2=dbs, c2_copy=4, a_t=1,
           w_t=2, ldw=K, lda=N, splitk=True)
-    return [(dws[0], dbs[0][:, 0]), (dws[1], dbs[1][:, 0])]
+    return [(dws[0], dbs[0]), (dws[1], dbs[1])]
 
 
 def _dx2(dy, wbs, M, N, K, act=0, r=None):
@@ -449,6 +451,52 @@ class _HipMamAttention(torch.autograd.Function):
         return mam_attention_backward(qkv, out, dout, lse, ctx.n_t, ctx.heads), None, None
 
 
+def _ln_fwd(ctx, x, w0, b0, w1, b1, rows0, eps, out_f32):
+    """mmt_layernorm of x (fp32, last dim C) -> [rows][C] bf16 (fp32 with out_f32); saves what _ln_bwd needs."""
+    from ._lib import LIB, MMT_BF16, check
+    C = x.shape[-1]
+    x2 = x.reshape(-1, C).contiguous()
+    rows = x2.shape[0]
+    two = w1 is not None  # (LayerNorm parameters are contiguous fp32 leaves)
+    out = torch.empty(rows, C, device=x.device, dtype=torch.float32 if out_f32 else torch.bfloat16)
+    check(LIB.mmt_layernorm(x2.data_ptr(), None, 0, out.data_ptr() if out_f32 else None,
+                            None if out_f32 else out.data_ptr(), w0.data_ptr(), b0.data_ptr(),
+                            w1.data_ptr() if two else None, b1.data_ptr() if two else None, rows,
+                            rows0 if two else rows, C, eps, MMT_BF16, _stream()), "mmt_layernorm")
+    ctx.save_for_backward(x2, w0, w1 if two else w0)
+    ctx.two, ctx.rows0, ctx.eps, ctx.shape = two, rows0, eps, x.shape
+    return out
+
+
+def _ln_bwd(ctx, dy, dres=None):
+    """(dx, dgamma0, dbeta0, dgamma1, dbeta1) of _ln_fwd's LayerNorm; dres (fp32, the input's shape): a second
+    gradient of the input, added in the same kernel (mmt_layernorm_bwd_add)."""
+    from ._lib import LIB, MMT_BF16, MMT_F32, check
+    x2, g0, g1 = ctx.saved_tensors
+    rows, C = x2.shape
+    dy = dy.reshape(rows, C).contiguous()
+    code = {torch.bfloat16: MMT_BF16, torch.float32: MMT_F32}[dy.dtype]
+    sets = 4 if ctx.two else 2
+    nws = (rows + 31) // 32 * 4 * C
+    # dgamma / dbeta in their own small tensor: AccumulateGrad keeps them as .grad, and views into the
+    # dx / workspace buffer would hold its rows * C floats alive until the next zero_grad
+    buf = torch.empty(rows * C + nws, device=x2.device, dtype=torch.float32)
+    dx, ws = buf[:rows * C].view(rows, C), buf[rows * C:]
+    dgb = torch.empty(sets, C, device=x2.device, dtype=torch.float32)
+    args = (x2.data_ptr(), dy.data_ptr(), code, g0.data_ptr(), g1.data_ptr() if ctx.two else None)
+    tail = (dx.data_ptr(), dgb.data_ptr(), 0, ws.data_ptr(), ws.numel(), rows, ctx.rows0 if ctx.two else rows, C,
+            ctx.eps, _stream())
+    if dres is None:
+        check(LIB.mmt_layernorm_bwd(*args, *tail), "mmt_layernorm_bwd")
+    else:
+        dres = dres.reshape(rows, C).float().contiguous()
+        check(LIB.mmt_layernorm_bwd_add(*args, dres.data_ptr(), *tail), "mmt_layernorm_bwd_add")
+    dx = dx.view(ctx.shape)
+    if ctx.two:
+        return dx, dgb[0], dgb[1], dgb[2], dgb[3]
+    return dx, dgb[0], dgb[1], None, None
+
+
 class _HipLayerNorm(torch.autograd.Function):
     """nn.LayerNorm over the last dim of the fp32 residual stream -> bf16 (the next Linear's operand; fp32
     with out_f32), rows in alternating blocks of rows0 with (w0, b0) / (w1, b1) (the per-modality
@@ -458,41 +506,27 @@ class _HipLayerNorm(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w0, b0, w1, b1, rows0, eps, out_f32=False):
-        from ._lib import LIB, MMT_BF16, check
-        C = x.shape[-1]
-        x2 = x.reshape(-1, C).contiguous()
-        rows = x2.shape[0]
-        two = w1 is not None  # (LayerNorm parameters are contiguous fp32 leaves)
-        out = torch.empty(rows, C, device=x.device, dtype=torch.float32 if out_f32 else torch.bfloat16)
-        check(LIB.mmt_layernorm(x2.data_ptr(), None, 0, out.data_ptr() if out_f32 else None,
-                                None if out_f32 else out.data_ptr(), w0.data_ptr(), b0.data_ptr(),
-                                w1.data_ptr() if two else None, b1.data_ptr() if two else None, rows,
-                                rows0 if two else rows, C, eps, MMT_BF16, _stream()), "mmt_layernorm")
-        ctx.save_for_backward(x2, w0, w1 if two else w0)
-        ctx.two, ctx.rows0, ctx.eps, ctx.shape = two, rows0, eps, x.shape
-        return out.view(x.shape)
+        return _ln_fwd(ctx, x, w0, b0, w1, b1, rows0, eps, out_f32).view(x.shape)
 
     @staticmethod
     def backward(ctx, dy):
-        from ._lib import LIB, MMT_BF16, MMT_F32, check
-        x2, g0, g1 = ctx.saved_tensors
-        rows, C = x2.shape
-        dy = dy.reshape(rows, C).contiguous()
-        code = {torch.bfloat16: MMT_BF16, torch.float32: MMT_F32}[dy.dtype]
-        sets = 4 if ctx.two else 2
-        nws = (rows + 31) // 32 * 4 * C
-        # dgamma / dbeta in their own small tensor: AccumulateGrad keeps them as .grad, and views into the
-        # dx / workspace buffer would hold its rows * C floats alive until the next zero_grad
-        buf = torch.empty(rows * C + nws, device=x2.device, dtype=torch.float32)
-        dx, ws = buf[:rows * C].view(rows, C), buf[rows * C:]
-        dgb = torch.empty(sets, C, device=x2.device, dtype=torch.float32)
-        check(LIB.mmt_layernorm_bwd(x2.data_ptr(), dy.data_ptr(), code, g0.data_ptr(),
-                                    g1.data_ptr() if ctx.two else None, dx.data_ptr(), dgb.data_ptr(), 0,
-                                    ws.data_ptr(), ws.numel(), rows, ctx.rows0 if ctx.two else rows, C, ctx.eps,
-                                    _stream()), "mmt_layernorm_bwd")
-        if ctx.two:
-            return dx.view(ctx.shape), dgb[0], dgb[1], dgb[2], dgb[3], None, None, None
-        return dx.view(ctx.shape), dgb[0], dgb[1], None, None, None, None, None
+        return (*_ln_bwd(ctx, dy), None, None, None)
+
+
+class _HipLayerNormPass(torch.autograd.Function):
+    """_HipLayerNorm (bf16 out) that also hands its input through as a second output.  A pre-LN block's residual
+    stream x feeds both the LayerNorm and the residual op (x + f(LN(x)), mixformer.py:136-139), so autograd would
+    sum the two gradients of x with one more elementwise pass over the [rows][C] fp32 stream (24 per training
+    step); the consumers take the pass-through instead, and the backward adds its gradient inside the LayerNorm
+    backward kernel (mmt_layernorm_bwd_add)."""
+
+    @staticmethod
+    def forward(ctx, x, w0, b0, w1, b1, rows0, eps):
+        return _ln_fwd(ctx, x, w0, b0, w1, b1, rows0, eps, False).view(x.shape), x
+
+    @staticmethod
+    def backward(ctx, dy, dres):
+        return (*_ln_bwd(ctx, dy, dres), None, None)
 
 
 class _HipGroupNorm(torch.autograd.Function):
@@ -666,6 +700,15 @@ def _mlp(ops, x, mlp):
     return ops.linear(h, mlp.fc2.weight, mlp.fc2.bias, out_f32=True)
 
 
+def _layer_norm_pass(ops, x, a, b=None, eps=1e-6):
+    """(_layer_norm(ops, x, a, b, eps), x'), x' = x for the residual op: with HipOps the pass-through output of
+    the LayerNorm node (_HipLayerNormPass), so the two gradients of x are summed inside its backward kernel."""
+    fn = getattr(ops, "layer_norm_pass", None)
+    if fn is not None:
+        return fn(x, a.weight, a.bias, eps, b.weight if b is not None else None, b.bias if b is not None else None)
+    return _layer_norm(ops, x, a, b, eps), x
+
+
 def _layer_norm(ops, x, a, b=None, eps=1e-6):
     """LayerNorm of the fp32 stream x to ops.dtype: norm module a on every row, or a on the first half of
     the rows and b on the second (per-modality norms of the shared backbone).  ops.layer_norm when the
@@ -693,6 +736,12 @@ class HipOps:
         if w1 is not None and rows0 is None:
             rows0 = x.numel() // x.shape[-1] // 2
         return _HipLayerNorm.apply(x, w0, b0, w1, b1, rows0 or 0, eps, out_f32)
+
+    @staticmethod
+    def layer_norm_pass(x, w0, b0, eps, w1=None, b1=None):
+        """(layer_norm(x, ...) in bf16, x passed through for the residual op) (_HipLayerNormPass)."""
+        rows0 = x.numel() // x.shape[-1] // 2 if w1 is not None else 0
+        return _HipLayerNormPass.apply(x, w0, b0, w1, b1, rows0, eps)
 
     @staticmethod
     def linear(x, weight, bias, out_f32=False):
@@ -826,6 +875,23 @@ def _keep(x, p, training):
     return torch.empty(x.shape[0], device=x.device, dtype=torch.float32).bernoulli_(1.0 - p).div_(1.0 - p)
 
 
+def _keeps(x, ps, training):
+    """_keep for a list of rates at once (the residual branches of every block): one bernoulli draw and one
+    division over [len(ps)][batch] instead of two small launches per branch (round 5: 44 per training step).
+    Entries with rate 0 (or eval) are None, as _keep's."""
+    live = [i for i, p in enumerate(ps) if training and p > 0.0]
+    out = [None] * len(ps)
+    if not live:
+        return out
+    q = _const(("keep_q", tuple(ps[i] for i in live)), x.device,
+               lambda: torch.tensor([[1.0 - ps[i]] for i in live], dtype=torch.float32))
+    k = torch.empty(len(live), x.shape[0], device=x.device, dtype=torch.float32).bernoulli_(q.expand(-1, x.shape[0]))
+    k.div_(q)
+    for j, i in enumerate(live):
+        out[i] = k[j]
+    return out
+
+
 def _branch_residual(ops, x, a, lin, p, training):
     """x + DropPath(lin(a)) for the block's attention projection: one fused GEMM with HipOps."""
     fn = getattr(ops, "linear_residual", None)
@@ -869,12 +935,12 @@ def backbone_forward(bb, t, o, s, ops, drop_path_rate=DROP_PATH_RATE):
     depth = len(bb.blocks)
     for li, blk in enumerate(bb.blocks):
         dp = drop_path_rate * li / max(depth - 1, 1)
-        xn = _layer_norm(ops, x, blk.norm1)
+        xn, xr = _layer_norm_pass(ops, x, blk.norm1)
         qkv = ops.linear(xn.view(B * ntok, C), blk.attn.qkv.weight, blk.attn.qkv.bias).view(B, ntok, 3 * C)
         a = ops.mam_attention(qkv, n_t, H).view(B * ntok, C)
-        x = _branch_residual(ops, x, a, blk.attn.proj, dp, bb.training)
-        xn = _layer_norm(ops, x, blk.norm2)
-        x = _mlp_residual(ops, x, xn.view(B * ntok, C), blk.mlp, dp, bb.training)
+        x = _branch_residual(ops, xr, a, blk.attn.proj, dp, bb.training)
+        xn, xr = _layer_norm_pass(ops, x, blk.norm2)
+        x = _mlp_residual(ops, xr, xn.view(B * ntok, C), blk.mlp, dp, bb.training)
     xs = x[:, n_t:]
     return xs.transpose(1, 2).reshape(B, C, gs, gs)
 
@@ -898,19 +964,19 @@ def backbone_forward_pair(bv, bi, t, o, s, ops, drop_path_rate=DROP_PATH_RATE):
     x = (x.view(2, B, ntok, C) + pos).view(2 * B, ntok, C)
     depth = len(bv.blocks)
     M2 = 2 * B * ntok
+    keeps = _keeps(x, [drop_path_rate * (i // 2) / max(depth - 1, 1) for i in range(2 * depth)], bv.training)
     for li, (kv, ki) in enumerate(zip(bv.blocks, bi.blocks)):
-        dp = drop_path_rate * li / max(depth - 1, 1)
-        keep = _keep(x, dp, bv.training)
-        xn = _layer_norm(ops, x, kv.norm1, ki.norm1)
+        keep = keeps[2 * li]
+        xn, xr = _layer_norm_pass(ops, x, kv.norm1, ki.norm1)
         qkv = ops.linear2(xn.view(M2, C), kv.attn.qkv.weight, kv.attn.qkv.bias, ki.attn.qkv.weight,
                           ki.attn.qkv.bias).view(2 * B, ntok, 3 * C)
         a = ops.mam_attention(qkv, n_t, H).view(M2, C)
-        x = ops.linear_residual2(x, a, kv.attn.proj.weight, kv.attn.proj.bias, ki.attn.proj.weight,
+        x = ops.linear_residual2(xr, a, kv.attn.proj.weight, kv.attn.proj.bias, ki.attn.proj.weight,
                                  ki.attn.proj.bias, keep)
-        keep = _keep(x, dp, bv.training)
-        xn = _layer_norm(ops, x, kv.norm2, ki.norm2)
+        keep = keeps[2 * li + 1]
+        xn, xr = _layer_norm_pass(ops, x, kv.norm2, ki.norm2)
         mp = [(k.mlp.fc1.weight, k.mlp.fc1.bias, k.mlp.fc2.weight, k.mlp.fc2.bias) for k in (kv, ki)]
-        x = ops.mlp_residual2(x, xn.view(M2, C), mp[0], mp[1], keep)
+        x = ops.mlp_residual2(xr, xn.view(M2, C), mp[0], mp[1], keep)
     xs = x[:, n_t:].transpose(1, 2).reshape(2 * B, C, gs, gs)
     return xs[:B], xs[B:]
 
@@ -943,17 +1009,17 @@ def backbone_forward_stacked(bb, t, o, s, ops, asym=False, drop_path_rate=DROP_P
     x = x.view(B2, ntok, C) + pos
     depth = len(bb.blocks)
 
-    def ln2(x, a, b):  # norm*_v on the RGB half, norm*_i on the TIR half
-        return _layer_norm(ops, x, a, b)
+    def ln2(x, a, b):  # norm*_v on the RGB half, norm*_i on the TIR half (and x passed through)
+        return _layer_norm_pass(ops, x, a, b)
 
     for li, blk in enumerate(bb.blocks):
         dp = drop_path_rate * li / max(depth - 1, 1)
-        xn = ln2(x, blk.norm1_v, blk.norm1_i)
+        xn, xr = ln2(x, blk.norm1_v, blk.norm1_i)
         qkv = ops.linear(xn.view(B2 * ntok, C), blk.attn.qkv.weight, blk.attn.qkv.bias).view(B2, ntok, 3 * C)
         a = ops.mam_attention_asym(qkv, Bh, n_t, H) if asym else ops.mam_attention(qkv, n_t, H)
-        x = _branch_residual(ops, x, a.reshape(B2 * ntok, C), blk.attn.proj, dp, bb.training)
-        xn = ln2(x, blk.norm2_v, blk.norm2_i)
-        x = _mlp_residual(ops, x, xn.view(B2 * ntok, C), blk.mlp, dp, bb.training)
+        x = _branch_residual(ops, xr, a.reshape(B2 * ntok, C), blk.attn.proj, dp, bb.training)
+        xn, xr = ln2(x, blk.norm2_v, blk.norm2_i)
+        x = _mlp_residual(ops, xr, xn.view(B2 * ntok, C), blk.mlp, dp, bb.training)
     return x[:, n_t:].transpose(1, 2).reshape(B2, C, gs, gs), x[:, :gt * gt]
 
 

@@ -216,13 +216,47 @@ def test_gemm_gelu_backward_and_preact_epilogues(impl):
     assert (c5.float().cpu() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
 
 
+@pytest.mark.parametrize("impl", [0, 8])
+@pytest.mark.parametrize("c_f32", [1, 0])
+def test_gemm_row_scale_residual(impl, c_f32):
+    """row_scale (the training step's per-sample stochastic depth on a residual branch, mixformer.py:136-139):
+    C = R + keep[m // div] * (A W^T + b), as an fp32 C with its bf16 copy (the compact residual epilogue) or a bf16
+    C (the general epilogue), two groups, a partial last row tile; impl 0 / 8 (the 128x128 two-per-CU tile)."""
+    L = _lib()
+    M, N, K, div = 1100, 768, 768, 275
+    g = torch.Generator().manual_seed(impl * 2 + c_f32)
+    A = torch.randn(2, M, K, generator=g).bfloat16()
+    W = (torch.randn(2, N, K, generator=g) / math.sqrt(K)).bfloat16()
+    b = torch.randn(2, N, generator=g)
+    R = torch.randn(2, M, N, generator=g)
+    keep = torch.tensor([0.0, 1.25, 1.25, 0.0], dtype=torch.float32)
+    Ad, Wd, bd, Rd, kd = A.cuda(), W.cuda(), b.cuda(), R.cuda(), keep.cuda()
+    c = torch.empty(2, M, N, device="cuda", dtype=torch.float32 if c_f32 else torch.bfloat16)
+    c2 = torch.empty(2, M, N, device="cuda", dtype=torch.bfloat16)
+    kw = dict(c2=[c2[0].data_ptr(), c2[1].data_ptr()], c2_copy=1) if c_f32 else {}
+    p = _gemm_params([Ad[0].data_ptr(), Ad[1].data_ptr()], [Wd[0].data_ptr(), Wd[1].data_ptr()],
+                     [c[0].data_ptr(), c[1].data_ptr()], M, N, K, K, N, bias=[bd[0].data_ptr(), bd[1].data_ptr()],
+                     r=[Rd[0].data_ptr(), Rd[1].data_ptr()], ldr=N, c_f32=c_f32, impl=impl, **kw)
+    p.row_scale, p.row_scale_div = kd.data_ptr(), div
+    L.check(L.LIB.mmt_gemm(p, L.MMT_BF16, torch.cuda.current_stream().cuda_stream), "gemm row_scale")
+    torch.cuda.synchronize()
+    sc = keep[torch.arange(M) // div][None, :, None]
+    ref = R + sc * (torch.einsum("gmk,gnk->gmn", A.float(), W.float()) + b[:, None])
+    err = (c.float().cpu() - ref).abs().max().item()
+    assert err <= (1e-3 if c_f32 else 1e-2) * ref.abs().max().item() + 1e-4, err
+    if c_f32:
+        assert torch.equal(c2.cpu(), c.cpu().bfloat16())
+
+
 @pytest.mark.parametrize("impl", [-1, 0, 1, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("splitk", [0, 3])
 @pytest.mark.parametrize("N,K,M", [(768, 3072, 776), (3072, 768, 1024), (256, 2112, 264)])
-def test_gemm_column_split_epilogue(impl, splitk, N, K, M):
+@pytest.mark.parametrize("mode", [3, 4])
+def test_gemm_column_split_epilogue(impl, splitk, N, K, M, mode):
     """c2_copy 3 (the training dW GEMM, dy^T [x | 1]): output columns [0, M - 8) go to C with pitch
-    M - 8, the last 8 columns (the bias gradient, then zeros) to C2 [rows][8]; fp32 outputs.  Every
-    16-bit LDS-DMA configuration, with and without split-K (impl -1 rejects the mode)."""
+    M - 8, the last 8 columns (the bias gradient, then zeros) to C2 [rows][8]; c2_copy 4: only column M - 8
+    (the bias gradient) to C2 as a contiguous [rows] vector; fp32 outputs.  Every 16-bit LDS-DMA configuration,
+    with and without split-K (impl -1 rejects the mode)."""
     if splitk and impl in (5, 7, 8):
         pytest.skip("forced impl 5 / 7 / 8 take no split-K")
     L = _lib()
@@ -233,24 +267,28 @@ def test_gemm_column_split_epilogue(impl, splitk, N, K, M):
     X[M - 7:] = 0.0
     Xb = X.bfloat16()
     Ad, Xd = A.cuda(), Xb.cuda()
-    buf = torch.full((N * M,), float("nan"), device="cuda")
-    dw, db8 = buf[:N * (M - 8)].view(N, M - 8), buf[N * (M - 8):].view(N, 8)
+    buf = torch.full((N * M + 64,), float("nan"), device="cuda")
+    nb = 8 if mode == 3 else 1
+    dw, db8 = buf[:N * (M - 8)].view(N, M - 8), buf[N * (M - 8):N * (M - 8) + N * nb].view(N, nb)
     kw = {}
     if splitk:
         kw["sk"] = (splitk, torch.empty(8 << 20, device="cuda"), torch.zeros(1 << 16, device="cuda", dtype=torch.int32))
     p = _gemm_params([Ad.data_ptr()], [Xd.data_ptr()], [dw.data_ptr()], N, M, K, K, M - 8, c_f32=1,
-                     c2=[db8.data_ptr()], c2_copy=3, impl=impl, **kw)
+                     c2=[db8.data_ptr()], c2_copy=mode, impl=impl, **kw)
     rc = L.LIB.mmt_gemm(p, L.MMT_BF16, torch.cuda.current_stream().cuda_stream)
     if impl == -1:
         assert rc == -10000
         return
-    L.check(rc, "gemm c2_copy 3")
+    L.check(rc, "gemm c2_copy %d" % mode)
     torch.cuda.synchronize()
     ref = A.float() @ Xb.float().t()
     got = torch.cat([dw.cpu(), db8.cpu()], 1)
-    err = (got - ref).abs().max().item()
+    err = (got - ref[:, :M - 8 + nb]).abs().max().item()
     assert err <= 1e-3 * ref.abs().max().item() + 1e-4, err
-    assert torch.equal(db8[:, 1:].cpu(), torch.zeros(N, 7))
+    if mode == 3:
+        assert torch.equal(db8[:, 1:].cpu(), torch.zeros(N, 7))
+    else:  # nothing written past the vector
+        assert torch.isnan(buf[N * (M - 8) + N:].cpu()).all()
     if splitk:
         assert int(kw["sk"][2].abs().sum()) == 0
 
@@ -446,7 +484,7 @@ def test_gemm_layernorm_fold(dname, impl, M, N, K):
 
 
 @pytest.mark.parametrize("dname", ["bf16", "fp16"])
-@pytest.mark.parametrize("pimpl,cimpl", [(1, 1), (2, 3), (3, 2), (0, 0), (6, 5), (5, 6)])
+@pytest.mark.parametrize("pimpl,cimpl", [(1, 1), (2, 3), (3, 2), (0, 0), (6, 5), (5, 6), (8, 0)])
 def test_gemm_layernorm_stats_handoff(dname, pimpl, cimpl):
     """ln_stats_out / ln_fold 2: a producer GEMM (C fp32 = A W^T + b + R, C2 = its 16-bit copy) also
     writes the per-64-column row statistics of C2; the LayerNorm-folded consumer reads them instead

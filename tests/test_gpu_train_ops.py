@@ -550,6 +550,42 @@ def test_hip_layernorm_autograd(two):
         assert (a - b).abs().max().item() <= 1e-3 * max(1.0, b.abs().max().item())
 
 
+@pytest.mark.parametrize("two", [False, True])
+def test_hip_layernorm_pass_through_gradient(two):
+    """HipOps.layer_norm_pass (_HipLayerNormPass): the LayerNorm output and x handed through for the residual
+    op, as a pre-LN block uses them (y = x + f(LN(x))); the two gradients of x are summed inside the LayerNorm
+    backward kernel (mmt_layernorm_bwd_add).  Equal to HipOps.layer_norm with autograd's separate add up to
+    one rounding (the kernel may contract the last multiply into the add), the parameters' gradients identical."""
+    from mmt_amd.train import HipOps
+    g = torch.Generator().manual_seed(5 + two)
+    B, ntok, C = 4, 100, 768
+    x = (torch.randn(B, ntok, C, generator=g) * 2).cuda()
+    n = [torch.nn.LayerNorm(C, eps=1e-6).cuda() for _ in range(2)]
+    for m in n:
+        with torch.no_grad():
+            m.weight.copy_(torch.randn(C, generator=g).cuda())
+            m.bias.copy_(torch.randn(C, generator=g).cuda())
+    wq = torch.randn(C, C, generator=g).cuda() / C ** 0.5
+    dy = torch.randn(B, ntok, C, generator=g).cuda()
+    args = (n[0].weight, n[0].bias, 1e-6, n[1].weight if two else None, n[1].bias if two else None)
+    grads = []
+    for fused in (True, False):
+        for m in n:
+            m.weight.grad = m.bias.grad = None
+        xa = x.clone().requires_grad_(True)
+        if fused:
+            xn, xr = HipOps.layer_norm_pass(xa, *args)
+        else:
+            xn, xr = HipOps.layer_norm(xa, *args), xa
+        y = xr * 0.5 + (xn.float() @ wq)  # a residual consumer of the pass-through and a LayerNorm consumer
+        y.backward(dy)
+        grads.append([xa.grad] + [p.grad.clone() for m in (n if two else n[:1]) for p in (m.weight, m.bias)])
+    dxa, dxb = grads[0][0], grads[1][0]
+    assert (dxa - dxb).abs().max().item() <= 1e-6 * dxb.abs().max().item()
+    for a, b in zip(grads[0][1:], grads[1][1:]):
+        assert torch.equal(a, b)
+
+
 def test_hip_mlp_autograd():
     """HipOps.mlp (_HipMlp: fc1 with the GELU epilogue storing its pre-activation, fc2, and a backward
     whose fc2 dX GEMM applies GELU' in its epilogue) against the same MLP as torch fp32 autograd on the

@@ -35,7 +35,11 @@ SHAPES = [("qkv_ln", 2, 528, 2304, 768, 0, 0), ("fc1_ln", 2, 528, 3072, 768, 1, 
           ("g1_dX_qkv", 1, 8448, 768, 2304, 0, 0), ("g1_dX_fc1", 1, 8448, 768, 3072, 0, 0),
           ("g1_dX_fc2", 1, 8448, 3072, 768, 0, 0), ("g1_dX_proj", 1, 8448, 768, 768, 0, 0),
           ("g1_dW_qkv", 1, 2304, 776, 8448, 0, 0), ("g1_dW_fc1", 1, 3072, 776, 8448, 0, 0),
-          ("g1_dW_fc2", 1, 768, 3080, 8448, 0, 0), ("g1_dW_proj", 1, 768, 776, 8448, 0, 0)]
+          ("g1_dW_fc2", 1, 768, 3080, 8448, 0, 0), ("g1_dW_proj", 1, 768, 776, 8448, 0, 0),
+          # config 3 on one GPU (shared backbone, 64 sequences: 2 modality groups of 33792 rows; qkv / fc1 with
+          # the LayerNorm fold on handed-in statistics, "_ln2")
+          ("c3_qkv_ln2", 2, 33792, 2304, 768, 0, 0), ("c3_fc1_ln2", 2, 33792, 3072, 768, 1, 0),
+          ("c3_proj", 2, 33792, 768, 768, 0, 1), ("c3_fc2", 2, 33792, 768, 3072, 0, 1)]
 
 
 SK_WS = None
@@ -59,10 +63,15 @@ def run(name, G, M, N, K, act, res, impl, reps, splitk=1):
     p.M, p.N, p.K, p.act, p.c_f32, p.groups, p.impl = M, N, K, act, 1 if res else 0, G, impl
     p.splitk, p.sk_ws, p.sk_ws_floats = splitk, SK_WS[0].data_ptr(), SK_WS[0].numel()
     p.sk_cnt, p.sk_cnt_n = SK_WS[1].data_ptr(), SK_WS[1].numel()
-    if name.endswith("_ln"):  # LayerNorm folded (timing only: colsum = bias, reference check skipped)
-        p.ln_fold, p.ln_eps = 1, 1e-6
+    if name.endswith("_ln") or name.endswith("_ln2"):  # LayerNorm folded (timing only: colsum = bias, no check)
+        p.ln_fold, p.ln_eps = (2 if name.endswith("_ln2") else 1), 1e-6
+        st = torch.zeros(G, M, K // 64, 2, device="cuda")
+        st[..., 1] = 64.0  # (sum, sum of squares) per 64 columns: mean 0, variance 1
+        run.keep = st
         for g in range(G):
             p.ln_colsum[g] = b[g].data_ptr()
+            if p.ln_fold == 2:
+                p.ln_stats_in[g] = st[g].data_ptr()
     fn = lambda: L.check(L.LIB.mmt_gemm(L.ctypes.byref(p), L.MMT_BF16,  # noqa: E731
                                         torch.cuda.current_stream().cuda_stream), name)
     fn()
@@ -77,7 +86,7 @@ def run(name, G, M, N, K, act, res, impl, reps, splitk=1):
         ref = torch.relu(ref)
     if res:
         ref = ref + R
-    err = ((C.float() - ref).abs().max() / ref.abs().max()).item() if not name.endswith("_ln") else float("nan")
+    err = ((C.float() - ref).abs().max() / ref.abs().max()).item() if "_ln" not in name else float("nan")
     return us, err
 
 
