@@ -57,15 +57,23 @@ MMT_DEV f32x4 mfma(u32x4 a, u32x4 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
 }
 
-// 64 rows x 128 B of a [row][3C] bf16 buffer (column offset col) into a TP-pitch LDS tile; rows
-// past `rows` re-read row rows-1.  `c` != 1 scales the values (q' = bf16(q * c)).
-MMT_DEV void stage_tile(char* tile, const bf16_t* base, int64_t rs, int r0, int rows, float c) {
+// 64 rows x 128 B of a [row][rs] bf16 buffer into a TP-pitch LDS tile, in two halves: load_tile fetches
+// this thread's two 16-B chunks into registers (rows past `rows` re-read row rows-1), store_tile writes them
+// (scaled by c if c != 1: q' = bf16(q * c)).  The K loops fetch tile t+1 into registers before they multiply
+// tile t, so its global latency hides behind the MFMAs (round 5: the tile was loaded and stored between the
+// two barriers, every wave waiting on it).
+MMT_DEV void load_tile(u32x4 (&v)[2], const bf16_t* base, int64_t rs, int r0, int rows) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int idx = threadIdx.x + 256 * i, r = idx >> 3, ch = idx & 7;
-        u32x4 v = *(const u32x4*)(base + (int64_t)min(r0 + r, rows - 1) * rs + ch * 8);
-        if (c != 1.f) v = scale_bf16x8(v, c);
-        *(u32x4*)(tile + r * TP + ch * 16) = v;
+        v[i] = *(const u32x4*)(base + (int64_t)min(r0 + r, rows - 1) * rs + ch * 8);
+    }
+}
+MMT_DEV void store_tile(char* tile, const u32x4 (&v)[2], float c) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int idx = threadIdx.x + 256 * i, r = idx >> 3, ch = idx & 7;
+        *(u32x4*)(tile + r * TP + ch * 16) = c != 1.f ? scale_bf16x8(v[i], c) : v[i];
     }
 }
 
@@ -106,11 +114,18 @@ __global__ __launch_bounds__(256) void mam_bwd_dq_kernel(const mmt_attn_bwd_para
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int nkt = (Lk + 63) / 64;
+    u32x4 kr[2], vr[2];
+    load_tile(kr, qkv + C, rs, 0, Lk);
+    load_tile(vr, qkv + 2 * C, rs, 0, Lk);
     for (int kt = 0; kt < nkt; ++kt) {
+        __syncthreads();  // every wave is past its reads of tile kt-1
+        store_tile(kt_l, kr, 1.f);
+        store_tile(vt_l, vr, 1.f);
         __syncthreads();
-        stage_tile(kt_l, qkv + C, rs, kt * 64, Lk, 1.f);
-        stage_tile(vt_l, qkv + 2 * C, rs, kt * 64, Lk, 1.f);
-        __syncthreads();
+        if (kt + 1 < nkt) {  // tile kt+1 in flight while tile kt is multiplied
+            load_tile(kr, qkv + C, rs, (kt + 1) * 64, Lk);
+            load_tile(vr, qkv + 2 * C, rs, (kt + 1) * 64, Lk);
+        }
         f32x4 sp[4], dp[4];
 #pragma unroll
         for (int kt16 = 0; kt16 < 4; ++kt16) {
@@ -173,22 +188,27 @@ __global__ __launch_bounds__(256) void mam_bwd_dkv_kernel(const mmt_attn_bwd_par
     f32x4 dk[4], dv[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) dk[dt] = dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    u32x4 qr[2], dr[2];
+    float lr = 0.f, dl = 0.f;
+    auto fetch = [&](int t0) {  // the query tile at t0 into registers
+        load_tile(qr, qkv, rs, t0, ntok);
+        load_tile(dr, dO, C, t0, ntok);
+        if (threadIdx.x < 64) {
+            lr = lse[min(t0 + (int)threadIdx.x, ntok - 1)];
+            dl = del[min(t0 + (int)threadIdx.x, ntok - 1)];
+        }
+    };
+    fetch(q_lo);
     for (int qt0 = q_lo; qt0 < ntok; qt0 += 64) {
-        __syncthreads();
-        stage_tile(q_l, qkv, rs, qt0, ntok, c);
-        {
-            const int idx = threadIdx.x, r = idx >> 3, ch = idx & 7;
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const int rr = r + 32 * i;
-                *(u32x4*)(do_l + rr * TP + ch * 16) = *(const u32x4*)(dO + (int64_t)min(qt0 + rr, ntok - 1) * C + ch * 8);
-            }
-            if (idx < 64) {
-                lse_l[idx] = lse[min(qt0 + idx, ntok - 1)];
-                del_l[idx] = del[min(qt0 + idx, ntok - 1)];
-            }
+        __syncthreads();  // every wave is past its reads of the previous tile
+        store_tile(q_l, qr, c);
+        store_tile(do_l, dr, 1.f);
+        if (threadIdx.x < 64) {
+            lse_l[threadIdx.x] = lr;
+            del_l[threadIdx.x] = dl;
         }
         __syncthreads();
+        if (qt0 + 64 < ntok) fetch(qt0 + 64);  // the next tile in flight while this one is multiplied
         f32x4 sp[4], dp[4];
 #pragma unroll
         for (int qt16 = 0; qt16 < 4; ++qt16) {
