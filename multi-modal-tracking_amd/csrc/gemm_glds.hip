@@ -141,7 +141,7 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
     // inline-asm MFMAs), 2-slot ring of 64-deep stages; LayerNorm fold with handed-in statistics allowed
     constexpr bool W4 = BM == 256 && BN == 256 && NW == 4;
     static_assert(!W4 || (KS == 1 && ST == 2 && OCC == 1 && !CONV && (LNM == 0 || LNM == 2)), "impl 9 geometry");
-    static_assert(!SB || (KS == 1 && (LNM == 0 || LNM >= 3 || W4) && !CONV), "impl 7: plain GEMM only");
+    static_assert(!SB || (KS == 1 && (LNM == 0 || LNM >= 2) && !CONV), "impl 7 / 8 / 9: plain GEMM (or handed-in LN statistics)");
     // LNM 3: W given MN-major (W^T [K][ldw], the Linear backward's dX); 4: A and W MN-major (dW)
     constexpr bool TA = LNM == 4, TB = LNM == 3 || LNM == 4;
     static_assert(!TB || (BM == 128 && BN == 128 && !CONV), "MN-major operands: 128x128 tiles");
@@ -534,8 +534,8 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
     // EPASS: a tile whose fp32 image does not fit the stage ring (256x256) is assembled and written
     // out in WGM passes of one wave row (WM rows) each
     constexpr int EPASS = BM * TP * 4 + KS * BM * 8 + 16 <= KS * ST * STAGE ? 1 : WGM, EB = BM / EPASS;
-    static_assert(EPASS == 1 || (EB == WM && KS == 1 && (LNM == 0 || LNM >= 3 || (W4 && LNM == 2))),
-                  "multi-pass epilogue: plain GEMM tiles (impl 9: also with handed-in LayerNorm statistics)");
+    static_assert(EPASS == 1 || (EB == WM && KS == 1 && (LNM == 0 || LNM >= 2)),
+                  "multi-pass epilogue: plain GEMM tiles (also with handed-in LayerNorm statistics)");
     static_assert(EB * TP * 4 + KS * BM * 8 + 4 <= LDS_BYTES, "epilogue pass fits in LDS");
     constexpr int FLAG_OFF = EB * TP * 4 + KS * BM * 8;  // split-K "this workgroup sums" word
     float* ctile = (float*)lds;
@@ -1018,7 +1018,8 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
 // The same tile at two workgroups per CU (impl 8: 128x128, 8 waves, 2-slot ring = 64 KiB of LDS, <= 128
 // VGPRs): one workgroup's prologue / epilogue runs beside the other's K loop on the CU, which the one-
 // workgroup-per-CU tiles cannot overlap (large-M grids of short K: the training step's K = 768 GEMMs).
-template <typename T, int BM, int BN, int WGM, int WGN, int KS, int ST, bool RS = false, int EPI = 0>
+// (LNM 2: the LayerNorm fold on handed-in statistics, round 5 -- the inference qkv / fc1 of config 3)
+template <typename T, int BM, int BN, int WGM, int WGN, int KS, int ST, bool RS = false, int EPI = 0, int LNM = 0>
 __global__ __launch_bounds__(64 * WGM * WGN * KS)
     __attribute__((amdgpu_waves_per_eu(WGM * WGN * KS / 2, WGM * WGN * KS / 2))) void gemm_glds_kernel_occ2(
         const mmt_gemm_params p) {
@@ -1027,7 +1028,7 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS)
     const int per_g = gridDim.x * nsk;
     const int g = lin / per_g, rem_t = lin - g * per_g;
     const int tile = rem_t / nsk, slice = rem_t - tile * nsk;
-    gemm_glds_tile<T, BM, BN, WGM, WGN, KS, ST, false, 0, 2, RS, EPI>(p, g, tile, slice, nsk, gridDim.x);
+    gemm_glds_tile<T, BM, BN, WGM, WGN, KS, ST, false, LNM, 2, RS, EPI>(p, g, tile, slice, nsk, gridDim.x);
 }
 
 // impl 8's tile with MN-major operands (LNM 3: W; 4: A and W)
@@ -1297,8 +1298,12 @@ int mmt_gemm_glds(const mmt_gemm_params& p, hipStream_t st, int force) {
         // Round 5: and for the residual producers with the LayerNorm-statistics hand-off (round 3 kept them off: config 3
         // at 64 sequences 2650 -> 2541 frames/s; with the row-group order the proj entry of that plan runs 211.5 ->
         // 180.4 us, fc2 444.0 -> 445.0, profiles/r05_c3_entry_ab.jsonl)
-        if (!MMT_GEMM_NO_OCC2 && big && nsk == 1 && !p.ln_fold && p.conv_h == 0 &&
-            (MMT_GEMM_OCC2_RES || !p.ln_stats_out[0]) && (cfg == 1 || cfg == 5 || cfg == 6 || cfg == 7))
+        // and (round 5) for the LayerNorm fold on handed-in statistics, whatever tile the model picked (config 3's qkv /
+        // fc1 in the plan at 64 / 8 sequences: qkv 332.4 -> 321.8 / 51.9 -> 48.2 us, fc1 486.7 -> 484.2 / 69.6 -> 67.8,
+        // profiles/r05_c3_ln2_ab.jsonl)
+        if (!MMT_GEMM_NO_OCC2 && big && nsk == 1 && p.ln_fold != 1 && p.conv_h == 0 &&
+            (MMT_GEMM_OCC2_RES || !p.ln_stats_out[0]) &&
+            (cfg == 1 || cfg == 5 || cfg == 6 || cfg == 7 || (p.ln_fold == 2 && (cfg == 2 || cfg == 3))))
             cfg = 8;
     } else if (cfg == 8) {
         nsk = 1;  // impl 8: no split-K
@@ -1326,12 +1331,17 @@ int mmt_gemm_glds(const mmt_gemm_params& p, hipStream_t st, int force) {
             hipLaunchKernelGGL((gemm_glds_kernel<T, 256, 256, 4, 2, 1, 2, false, 0>),
                                dim3((unsigned)tiles_of(p, 256, 256), 1, p.groups), dim3(512), 0, st, p);
             break;
-        case 8:  // 128x128 at two workgroups per CU: plain GEMM mode (no folded LayerNorm / conv), and no split-K:
-                 // its 64 KiB ring holds the fp32 tile image only in two passes (as impl 7)
-            if (p.ln_fold || p.conv_h > 0 || nsk > 1) return 1;
+        case 8:  // 128x128 at two workgroups per CU: plain GEMM mode (LayerNorm fold only with handed-in statistics, no
+                 // conv), and no split-K: its 64 KiB ring holds the fp32 tile image only in two passes (as impl 7)
+            if (p.ln_fold == 1 || p.conv_h > 0 || nsk > 1) return 1;
             {
                 const dim3 grid((unsigned)tiles_of(p, 128, 128), nsk, p.groups);
-                if (compact_epilogue(p))
+                if (p.ln_fold == 2) {
+                    if (compact_epilogue(p))
+                        hipLaunchKernelGGL((gemm_glds_kernel_occ2<T, 128, 128, 2, 4, 1, 2, false, 1, 2>), grid, dim3(512), 0, st, p);
+                    else
+                        hipLaunchKernelGGL((gemm_glds_kernel_occ2<T, 128, 128, 2, 4, 1, 2, false, 0, 2>), grid, dim3(512), 0, st, p);
+                } else if (compact_epilogue(p))
                     hipLaunchKernelGGL((gemm_glds_kernel_occ2<T, 128, 128, 2, 4, 1, 2, false, 1>), grid, dim3(512), 0, st, p);
                 else if (residual_epilogue(p))
                     hipLaunchKernelGGL((gemm_glds_kernel_occ2<T, 128, 128, 2, 4, 1, 2, false, 2>), grid, dim3(512), 0, st, p);

@@ -484,7 +484,7 @@ def test_gemm_layernorm_fold(dname, impl, M, N, K):
 
 
 @pytest.mark.parametrize("dname", ["bf16", "fp16"])
-@pytest.mark.parametrize("pimpl,cimpl", [(1, 1), (2, 3), (3, 2), (0, 0), (6, 5), (5, 6), (8, 0)])
+@pytest.mark.parametrize("pimpl,cimpl", [(1, 1), (2, 3), (3, 2), (0, 0), (6, 5), (5, 6), (8, 0), (0, 8)])
 def test_gemm_layernorm_stats_handoff(dname, pimpl, cimpl):
     """ln_stats_out / ln_fold 2: a producer GEMM (C fp32 = A W^T + b + R, C2 = its 16-bit copy) also
     writes the per-64-column row statistics of C2; the LayerNorm-folded consumer reads them instead
@@ -526,7 +526,8 @@ def test_gemm_layernorm_stats_handoff(dname, pimpl, cimpl):
         if mode == 2:
             q.ln_stats_in[0] = stats.data_ptr()
         q.lda, q.ldc, q.a_seg_rows, q.a_segs_a = C, N, M, 1
-        q.M, q.N, q.K, q.c_f32, q.groups, q.impl, q.ln_fold, q.ln_eps = M, N, C, 1, 1, cimpl, mode, 1e-6
+        q.M, q.N, q.K, q.c_f32, q.groups, q.ln_fold, q.ln_eps = M, N, C, 1, 1, mode, 1e-6
+        q.impl = 0 if cimpl == 8 and mode == 1 else cimpl  # (impl 8 folds handed-in statistics only)
         L.check(L.LIB.mmt_gemm(q, _code(dt), torch.cuda.current_stream().cuda_stream), "consumer")
         torch.cuda.synchronize()
         outs.append(out.cpu())
