@@ -665,7 +665,10 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
     // workgroup barrier every wave reads the other partials with sc1 loads only (no acquire either), summing the
     // nsk partials in SLICE order (its own from LDS): the result does not depend on which slice arrives last.  It
     // alone runs the epilogue.  Tickets [0, sk_cnt_n / 2), published counts [sk_cnt_n / 2, sk_cnt_n).
-    if (nsk > 1) {
+    // (compiled only into the tiles the launcher may split: the two-per-CU and 256x256 tiles never are, and the
+    // hand-off's registers made their epilogues spill, round 5)
+    constexpr bool CAN_SPLIT = OCC == 1 && BM * BN < 256 * 256;
+    if (CAN_SPLIT && nsk > 1) {
         const int64_t tix = (int64_t)g * ntiles + tile;
         constexpr int SLAB = BM * BN * 4;  // bytes of one partial tile
         const __amdgpu_buffer_rsrc_t slabs = __builtin_amdgcn_make_buffer_rsrc(
