@@ -1063,7 +1063,13 @@ def fusion_forward(fu, s_v, s_i, ops):
         d = av.shape[1]
         src = torch.cat([av.flatten(2).transpose(1, 2), ai.flatten(2).transpose(1, 2)], 1)
     fa = fu.fusion_attention
-    pos = _sine_pos(b, d, h, w, s_v.device).flatten(2).transpose(1, 2)
+    # the sine table depends on the shapes only: built once per shape and device (~20 small launches per step,
+    # round 5).  The reference points stay computed on the device: they sit on pixel centres, where the bilinear
+    # sampling's location gradient is discontinuous, and the host's linspace differs from the device's in the last
+    # ulp -- enough to move the training gradients 0.17 -> 0.64 (relative L2) from the fp32 CPU reference in
+    # test_module_forward_training_gpu_grads
+    pos = _const(("sine_pos", b, d, h, w), s_v.device,
+                 lambda: _sine_pos(b, d, h, w, "cpu").flatten(2).transpose(1, 2).contiguous())
     lpos = torch.cat([pos + fa.level_embed[0].view(1, 1, -1), pos + fa.level_embed[1].view(1, 1, -1)], 1)
     ref = _ref_points(h, w, b, 2, s_v.device)
     nl = 2 * h * w
@@ -1115,9 +1121,11 @@ def _ln_halves(ops, src, nv, ni):
 def _soft_argmax(score_map, stride):
     """head.py:200-212, coord grids :138-145 (x = stride * col, y = stride * row)."""
     B, _, H, W = score_map.shape
-    idx = torch.arange(0, H, device=score_map.device).view(-1, 1) * stride
-    coord_x = idx.repeat((H, 1)).view((H * W,)).float()
-    coord_y = idx.repeat((1, H)).view((H * W,)).float()
+
+    def grids():
+        idx = torch.arange(0, H).view(-1, 1) * stride
+        return idx.repeat((H, 1)).view((H * W,)).float(), idx.repeat((1, H)).view((H * W,)).float()
+    coord_x, coord_y = _const(("softargmax", H, W, stride), score_map.device, grids)  # (shape constants: cached)
     prob = F.softmax(score_map.float().view(-1, H * W), dim=1)
     return (coord_x * prob).sum(1), (coord_y * prob).sum(1)
 
