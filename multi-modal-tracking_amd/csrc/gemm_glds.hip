@@ -44,6 +44,10 @@
 #ifndef MMT_GEMM_OCC2_RES
 #define MMT_GEMM_OCC2_RES 1
 #endif
+// A/B build knob (tools/build_ablate.sh skticket): 1 = the ticket-first split-K hand-off (round 5, first half)
+#ifndef MMT_GEMM_SK_TICKET_FIRST
+#define MMT_GEMM_SK_TICKET_FIRST 0
+#endif
 // A/B build knob (tools/build_ablate.sh noocc2): 1 = the cost model never switches to impl 8
 #ifndef MMT_GEMM_NO_OCC2
 #define MMT_GEMM_NO_OCC2 0
@@ -654,6 +658,7 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
     char* C2 = (char*)p.c2[g];
     const int tc = (threadIdx.x % TPR) * 8, tr = threadIdx.x / TPR;
 
+#if MMT_GEMM_SK_TICKET_FIRST
     // ---- split-K hand-off (cdna_hip_programming.md Guideline 16, form R1 in its counter variant), ticket
     // first: lane 0 draws an agent-scope arrival ticket BEFORE any partial is stored, so the slice that draws the
     // last one keeps its partial in LDS and never writes it (nsk - 1 slabs cross memory instead of nsk; round 5,
@@ -734,6 +739,73 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
             *(f32x4*)(ctile + r * TP + tc + 4) = sb;
         }
     }
+#else
+    // ---- split-K hand-off, store first (round 4; the product form again since round 5's end): every slice stores its
+    // fp32 partial tile WRITE-THROUGH (buffer_store ... sc1, so no release fence), every wave drains its stores, and
+    // after a workgroup barrier lane 0 takes an agent-scope arrival ticket.  The workgroup that draws the last ticket
+    // resets it and reads the other slices' partials with sc1 loads only (so no acquire either), summing the nsk
+    // partials in SLICE order (its own from LDS): the result does not depend on which slice arrives last.  It alone
+    // runs the epilogue.  (The ticket-first form above writes one partial less per tile -- head conv1 17.6 -> 12.1 MB
+    // -- but its last slice waits on the others' store drain: head conv1 27.8 -> 30.6 us and conv2 14.5 -> 17.1 us in
+    // the batch-1 frame, profiles/r05_splitk_form_ab.txt.)
+    constexpr bool CAN_SPLIT = OCC == 1 && BM * BN < 256 * 256;
+    if (CAN_SPLIT && nsk > 1) {
+        const int64_t tix = (int64_t)g * ntiles + tile;
+        constexpr int SLAB = BM * BN * 4;  // bytes of one partial tile
+        const __amdgpu_buffer_rsrc_t slabs = __builtin_amdgcn_make_buffer_rsrc(
+            p.sk_ws + tix * nsk * (BM * BN), (short)0, nsk * SLAB, 0x00020000);
+#pragma unroll
+        for (int ps = 0; ps < NPASS; ++ps) {
+            const int r = tr + ps * RPP, off = slice * SLAB + (r * BN + tc) * 4;
+            __builtin_amdgcn_raw_buffer_store_b128(*(const u32x4*)(ctile + r * TP + tc), slabs, off, 0, 16);
+            __builtin_amdgcn_raw_buffer_store_b128(*(const u32x4*)(ctile + r * TP + tc + 4), slabs, off + 16, 0, 16);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+        __syncthreads();
+        int* flag = (int*)(lds + FLAG_OFF);
+        if (threadIdx.x == 0) {
+            const uint32_t old = __hip_atomic_fetch_add(p.sk_cnt + tix, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int last = old == (uint32_t)(nsk - 1);
+            if (last) __hip_atomic_store(p.sk_cnt + tix, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            *flag = last;
+        }
+        __syncthreads();
+        if (!*flag) return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below
+#pragma unroll
+        for (int ps = 0; ps < NPASS; ++ps) {
+            const int r = tr + ps * RPP, off = (r * BN + tc) * 4;
+            f32x4 sa = {0.f, 0.f, 0.f, 0.f}, sb = sa;
+#pragma unroll
+            for (int q0 = 0; q0 < 8; q0 += 4) {  // 4 slices' loads in flight together, summed in order
+                u32x4 pa[4], pb[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int q = q0 + j;
+                    if (q < nsk && q != slice) {
+                        pa[j] = __builtin_amdgcn_raw_buffer_load_b128(slabs, q * SLAB + off, 0, 16);
+                        pb[j] = __builtin_amdgcn_raw_buffer_load_b128(slabs, q * SLAB + off + 16, 0, 16);
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int q = q0 + j;
+                    if (q < nsk) {
+                        if (q == slice) {
+                            sa += *(const f32x4*)(ctile + r * TP + tc);
+                            sb += *(const f32x4*)(ctile + r * TP + tc + 4);
+                        } else {
+                            sa += __builtin_bit_cast(f32x4, pa[j]);
+                            sb += __builtin_bit_cast(f32x4, pb[j]);
+                        }
+                    }
+                }
+            }
+            *(f32x4*)(ctile + r * TP + tc) = sa;  // this thread's own strip: no barrier needed
+            *(f32x4*)(ctile + r * TP + tc + 4) = sb;
+        }
+    }
+#endif
     const int n = n0 + tc, nc = min(n, N - 8);
     const bool csplit = p.c2_copy == 3 || p.c2_copy == 4;
     float* stats_out = p.c2_copy && !csplit && C2 ? p.ln_stats_out[g] : nullptr;

@@ -10,6 +10,7 @@
 #   ab:      the product plus the A/B-only attention kernels impl 23-28 (MMT_ATTN_AB=1) and GEMM impl 9 (MMT_GEMM_AB=1)
 #   noocc2:  the product without the cost model's switch to the two-per-CU 128x128 GEMM tile (impl 8)
 #   occ2nores: the product with the inference residual producers (LayerNorm statistics out) kept off impl 8
+#   skticket: the product with the ticket-first split-K hand-off (MMT_GEMM_SK_TICKET_FIRST=1)
 #   gm4 / gm16: the large-grid GEMM tile order with 4 / 16 row tiles per row group (MMT_GEMM_GM; product 8)
 # Use with MMT_HIP_LIB=multi-modal-tracking_amd/mmt_amd/_lib/<variant>/libmmt_hip.so.
 set -e
@@ -35,5 +36,6 @@ build ab "-DMMT_ATTN_AB=1 -DMMT_GEMM_AB=1"
 # impl 28 (the A/B-only ping-pong MAM kernel) stamp / ablation builds: tools/build_pg_variant.sh
 build noocc2 -DMMT_GEMM_NO_OCC2=1
 build occ2nores -DMMT_GEMM_OCC2_RES=0
+build skticket -DMMT_GEMM_SK_TICKET_FIRST=1
 build gm4 -DMMT_GEMM_GM=4
 build gm16 -DMMT_GEMM_GM=16
