@@ -10,6 +10,14 @@ import torch.multiprocessing as mp
 from conftest import ROOT
 
 
+def _free_port():
+    """A port the OS reports free on 127.0.0.1 (fixed ports collided under parallel test runs)."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
 def _worker(rank, world, port, out):
     import sys
     sys.path.insert(0, ROOT)
@@ -30,7 +38,7 @@ def _worker(rank, world, port, out):
 
 
 def test_timed_region_is_max_over_ranks_and_seeds_disjoint():
-    world, port = 2, 29613
+    world, port = 2, _free_port()
     with mp.Manager() as m:
         out = m.dict()
         mp.spawn(_worker, args=(world, port, out), nprocs=world, join=True)

@@ -63,6 +63,14 @@ def test_shard_ranges_partition():
         assert all(a[1] == b[0] for a, b in zip(got, got[1:]))
 
 
+def _free_port():
+    """A port the OS reports free on 127.0.0.1 (fixed ports collided under parallel test runs)."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
 def _sd():
     from mmt_amd import synthetic
     from mmt_amd.model import reference_state_dict_shapes
@@ -92,7 +100,7 @@ def test_sharded_slices_equal_single_process():
     sys.path.insert(0, ROOT)
     import bench
     from oracle.forward import forward
-    total, world, port = 4, 2, 29641
+    total, world, port = 4, 2, _free_port()
     with mp.Manager() as m:
         out = m.dict()
         mp.spawn(_worker, args=(world, port, total, out), nprocs=world, join=True)
@@ -125,7 +133,7 @@ def test_train_harness_gloo_two_ranks(tmp_path):
     all ranks, and the step's MFMA roofline field."""
     import json as _json
     import torch.multiprocessing as mp
-    port = 29500 + (os.getpid() % 500)
+    port = _free_port()
     mp.spawn(_train_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
     r0 = _json.load(open(tmp_path / "r0.json"))
     r1 = _json.load(open(tmp_path / "r1.json"))
