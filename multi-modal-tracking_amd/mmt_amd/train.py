@@ -1269,22 +1269,23 @@ def module_forward(net, template, online_template, search, ops, run_score_head=F
 
 # ----------------------------------------------------------------------------- loss / optimizer
 def ciou_loss(b1, b2):
-    """lib/utils/box_ops.py:100-152 for equal-length (N, 4) xyxy sets: (mean(1 - ciou), iou)."""
-    w1, h1 = b1[:, 2] - b1[:, 0], b1[:, 3] - b1[:, 1]
-    w2, h2 = b2[:, 2] - b2[:, 0], b2[:, 3] - b2[:, 1]
-    cx1, cy1 = (b1[:, 0] + b1[:, 2]) / 2.0, (b1[:, 1] + b1[:, 3]) / 2.0
-    cx2, cy2 = (b2[:, 0] + b2[:, 2]) / 2.0, (b2[:, 1] + b2[:, 3]) / 2.0
-    il, ir = torch.max(cx1 - w1 / 2, cx2 - w2 / 2), torch.min(cx1 + w1 / 2, cx2 + w2 / 2)
-    it, ib = torch.max(cy1 - h1 / 2, cy2 - h2 / 2), torch.min(cy1 + h1 / 2, cy2 + h2 / 2)
-    inter = torch.clamp(ir - il, min=0) * torch.clamp(ib - it, min=0)
-    cl, cr = torch.min(cx1 - w1 / 2, cx2 - w2 / 2), torch.max(cx1 + w1 / 2, cx2 + w2 / 2)
-    ct, cb = torch.min(cy1 - h1 / 2, cy2 - h2 / 2), torch.max(cy1 + h1 / 2, cy2 + h2 / 2)
-    inter_diag = (cx2 - cx1) ** 2 + (cy2 - cy1) ** 2
-    c_diag = torch.clamp(cr - cl, min=0) ** 2 + torch.clamp(cb - ct, min=0) ** 2
-    union = w1 * h1 + w2 * h2 - inter
+    """lib/utils/box_ops.py:100-152 for equal-length (N, 4) xyxy sets: (mean(1 - ciou), iou).  The x and y terms
+    are computed as (N, 2) pairs with the reference's operations in its order (same values; round 5: half the small
+    launches of the scalar-column form, forward and backward)."""
+    wh1, wh2 = b1[:, 2:] - b1[:, :2], b2[:, 2:] - b2[:, :2]
+    c1, c2 = (b1[:, :2] + b1[:, 2:]) / 2.0, (b2[:, :2] + b2[:, 2:]) / 2.0
+    lo1, hi1 = c1 - wh1 / 2, c1 + wh1 / 2
+    lo2, hi2 = c2 - wh2 / 2, c2 + wh2 / 2
+    iwh = torch.clamp(torch.min(hi1, hi2) - torch.max(lo1, lo2), min=0)
+    inter = iwh[:, 0] * iwh[:, 1]
+    ewh = torch.clamp(torch.max(hi1, hi2) - torch.min(lo1, lo2), min=0) ** 2
+    d2 = (c2 - c1) ** 2
+    inter_diag = d2[:, 0] + d2[:, 1]
+    c_diag = ewh[:, 0] + ewh[:, 1]
+    union = wh1[:, 0] * wh1[:, 1] + wh2[:, 0] * wh2[:, 1] - inter
     u = inter_diag / c_diag
     iou = inter / union
-    v = (4 / (math.pi ** 2)) * torch.pow(torch.atan(w2 / h2) - torch.atan(w1 / h1), 2)
+    v = (4 / (math.pi ** 2)) * torch.pow(torch.atan(wh2[:, 0] / wh2[:, 1]) - torch.atan(wh1[:, 0] / wh1[:, 1]), 2)
     with torch.no_grad():
         alpha = (iou > 0.5).float() * v / (1 - iou + v)
     cious = torch.clamp(iou - u - alpha * v, min=-1.0, max=1.0)
@@ -1293,10 +1294,9 @@ def ciou_loss(b1, b2):
 
 def box_loss(pred_cxcywh, gt_xywh, iou_weight=2.0, l1_weight=5.0):
     """MixFormerRGBTActor.compute_losses (actors/mixformer_rgbt.py:127-168)."""
-    xc, yc, w, h = pred_cxcywh.view(-1, 4).unbind(-1)
-    pred = torch.stack([xc - 0.5 * w, yc - 0.5 * h, xc + 0.5 * w, yc + 0.5 * h], -1)
-    x, y, gw, gh = gt_xywh.unbind(-1)
-    gt = torch.stack([x, y, x + gw, y + gh], -1).clamp(min=0.0, max=1.0)
+    p = pred_cxcywh.view(-1, 4)
+    pred = torch.cat([p[:, :2] - 0.5 * p[:, 2:], p[:, :2] + 0.5 * p[:, 2:]], -1)
+    gt = torch.cat([gt_xywh[:, :2], gt_xywh[:, :2] + gt_xywh[:, 2:]], -1).clamp(min=0.0, max=1.0)
     ciou, iou = ciou_loss(pred, gt)
     l1 = F.l1_loss(pred, gt)
     return iou_weight * ciou + l1_weight * l1, {"ciou": ciou.detach(), "l1": l1.detach(), "iou": iou.detach().mean()}

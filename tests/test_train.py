@@ -335,3 +335,50 @@ def test_ddp_gloo_two_ranks_through_module_forward(tmp_path):
     for n, g in full.items():
         assert torch.equal(r0[n], r1[n]), n
         assert (r0[n] - g).abs().max().item() <= 1e-4 * (g.abs().max().item() + 1e-12) + 1e-6, n
+
+
+def _ciou_loss_columns(b1, b2):
+    """The scalar-column form of lib/utils/box_ops.py:100-152 (mmt_amd.train.ciou_loss before round 5's (N, 2)
+    pairing), kept as the test's restatement."""
+    import math
+    w1, h1 = b1[:, 2] - b1[:, 0], b1[:, 3] - b1[:, 1]
+    w2, h2 = b2[:, 2] - b2[:, 0], b2[:, 3] - b2[:, 1]
+    cx1, cy1 = (b1[:, 0] + b1[:, 2]) / 2.0, (b1[:, 1] + b1[:, 3]) / 2.0
+    cx2, cy2 = (b2[:, 0] + b2[:, 2]) / 2.0, (b2[:, 1] + b2[:, 3]) / 2.0
+    il, ir = torch.max(cx1 - w1 / 2, cx2 - w2 / 2), torch.min(cx1 + w1 / 2, cx2 + w2 / 2)
+    it, ib = torch.max(cy1 - h1 / 2, cy2 - h2 / 2), torch.min(cy1 + h1 / 2, cy2 + h2 / 2)
+    inter = torch.clamp(ir - il, min=0) * torch.clamp(ib - it, min=0)
+    cl, cr = torch.min(cx1 - w1 / 2, cx2 - w2 / 2), torch.max(cx1 + w1 / 2, cx2 + w2 / 2)
+    ct, cb = torch.min(cy1 - h1 / 2, cy2 - h2 / 2), torch.max(cy1 + h1 / 2, cy2 + h2 / 2)
+    inter_diag = (cx2 - cx1) ** 2 + (cy2 - cy1) ** 2
+    c_diag = torch.clamp(cr - cl, min=0) ** 2 + torch.clamp(cb - ct, min=0) ** 2
+    union = w1 * h1 + w2 * h2 - inter
+    u = inter_diag / c_diag
+    iou = inter / union
+    v = (4 / (math.pi ** 2)) * torch.pow(torch.atan(w2 / h2) - torch.atan(w1 / h1), 2)
+    with torch.no_grad():
+        alpha = (iou > 0.5).float() * v / (1 - iou + v)
+    cious = torch.clamp(iou - u - alpha * v, min=-1.0, max=1.0)
+    return torch.mean(1 - cious), iou
+
+
+def test_ciou_loss_matches_column_form():
+    """mmt_amd.train.ciou_loss (x / y as (N, 2) pairs) against the scalar-column restatement of box_ops.py:100-152:
+    the same loss values bitwise, gradients within rounding, both iou > 0.5 (alpha active) and disjoint boxes."""
+    from mmt_amd.train import ciou_loss
+    g = torch.Generator().manual_seed(0)
+    for trial in range(12):
+        c = torch.rand(16, 2, generator=g) * 0.8 + 0.1
+        wh = torch.rand(16, 2, generator=g) * 0.3 + 0.05
+        b1 = torch.cat([c - wh / 2, c + wh / 2], 1).requires_grad_(True)
+        if trial % 2:
+            b2 = torch.cat([c - wh / 2 + 0.01, c + wh / 2 * 0.9], 1)  # overlapping: the alpha branch
+        else:
+            c2 = torch.rand(16, 2, generator=g)
+            b2 = torch.cat([c2 - wh / 3, c2 + wh / 3], 1)
+        la, ia = ciou_loss(b1, b2)
+        lb, ib = _ciou_loss_columns(b1, b2)
+        assert torch.equal(la, lb) and torch.equal(ia, ib)
+        ga, = torch.autograd.grad(la, b1)
+        gb, = torch.autograd.grad(lb, b1)
+        assert (ga - gb).abs().max().item() <= 1e-6 * gb.abs().max().item()
