@@ -499,13 +499,20 @@ def train_bench(world, rank, B, steps, warmup, device="cuda", ops=None, search=3
     elapsed = timed_steps(step, steps, world, sync, device)
     sps = world * B * steps / elapsed
     ach = sps / world * TRAIN_FLOP_PER_SAMPLE / 1e12  # per GPU
+    # HBM bytes of one whole step from the committed counter pass (tools/pmc_train_traffic.py; one GPU, graphed
+    # step, this batch), reported only on the kernel sources it was taken on
+    tr, tr_note = load_traffic("train", B, "bf16")
+    step_bytes = tr.get("step", {}).get("traffic_bytes") if (world == 1 and graphed) else None
     return {"value": round(sps, 2), "unit": "samples/s", "ms_per_step": round(elapsed / steps * 1e3, 3),
             "batch_per_gpu": B, "steps": steps, "warmup": warmup,
             "parallelism": "ddp%d (RCCL gradient all-reduce)" % world if world > 1 else "single",
             "step_issue": "one hipGraph replay per step (whole step captured)" if graphed else "eager",
             "roofline": {"kernel": "train_step (whole step)", "bound": "mfma", "achieved": round(ach, 2),
                          "peak": PEAK["bf16"], "unit": "TFLOP/s", "frac": float("%.4g" % (ach / PEAK["bf16"])),
-                         "flops_per_sample": TRAIN_FLOP_PER_SAMPLE, "traffic": None},
+                         "flops_per_sample": TRAIN_FLOP_PER_SAMPLE, "traffic": step_bytes,
+                         "traffic_unit": "bytes/step (HBM, PMC)",
+                         "traffic_source": tr_note if (world == 1 and graphed) else "not measured for this setup",
+                         "hbm_TBps": round(step_bytes / (elapsed / steps) / 1e12, 3) if step_bytes else None},
             "last_loss": round(float(last["stats"]["loss"]), 5),
             "opt_table_writes": getattr(step_fn.opt, "table_writes", None)}
 
