@@ -182,7 +182,7 @@ def load_traffic(variant, B, dtype):
     if not res:
         return {}, "no PMC pass for this workload"
     stamp = res.get("_stamp", {}).get("source_digest")
-    here = source_digest()
+    here = source_digest(train=variant == "train")
     if stamp != here:
         return {}, "PMC pass taken on sources %s, this tree is %s: not reported" % (stamp, here)
     return res, "PMC pass on this tree's sources (%s)" % here
@@ -454,7 +454,8 @@ def cpu_baseline(variant, B, budget_s=12.0, geo=None):
 TRAIN_FLOP_PER_SAMPLE = 3 * 218.59e9  # forward + backward ~ 3 x the 218.59 GFLOP forward
 
 
-def train_bench(world, rank, B, steps, warmup, device="cuda", ops=None, search=320, template=128, graph=True):
+def train_bench(world, rank, B, steps, warmup, device="cuda", ops=None, search=320, template=128, graph=True,
+                force_ddp=False):
     """BASELINE config 4: DDP training step of the two-stream MixViT-B RGB-T,
     B LaSOT-shaped synthetic pairs per GPU: forward with autograd on the HIP ops, CIoU + L1 box
     loss, backward with the RCCL gradient all-reduce (DistributedDataParallel, bucketed, overlapped
@@ -462,20 +463,22 @@ def train_bench(world, rank, B, steps, warmup, device="cuda", ops=None, search=3
     (mmt_amd.train.TrainStep; reference train_script_mixformer.py:105-140,
     actors/mixformer_rgbt.py:33-168).  Returns the result object (samples/s over all ranks by the
     max-over-ranks time, ms per step, an MFMA roofline of the whole step).  device / ops / image sizes:
-    the CPU harness test runs it over gloo with stand-in ops at small images (the product: HipOps)."""
+    the CPU harness test runs it over gloo with stand-in ops at small images (the product: HipOps).
+    force_ddp: the data-parallel step (bucketed all-reduce over the process group) even at world 1."""
     from mmt_amd.model import build_mixformer_vit_rgbt, hot_path_cfg
     from mmt_amd.train import HipOps, TrainStep, synthetic_batch
     torch.manual_seed(0)  # identical initial replicas (DDP also broadcasts rank 0's weights)
     net = build_mixformer_vit_rgbt(hot_path_cfg(search=search, template=template), train=False).to(device).train()
-    step_fn = TrainStep(net, ops or HipOps, ddp=world > 1)
+    ddp = world > 1 or force_ddp
+    step_fn = TrainStep(net, ops or HipOps, ddp=ddp)
     g = torch.Generator().manual_seed(100 + rank)  # each rank its own shard of the clip batch
     batches = [synthetic_batch(B, device, g, template, search) for _ in range(2)]
     sync = torch.cuda.synchronize if device != "cpu" else (lambda: None)
     last = {}
-    # single process on the device: the whole step captured as one hipGraph (TrainStep.capture; its
-    # eager warm-up steps count as this harness's warm-up), each timed step = the copy of that step's
-    # batch into the static inputs + one replay.  DDP (world > 1) stays eager.
-    graphed = graph and device != "cpu" and world == 1 and ops is None
+    # on the device: the whole step captured as one hipGraph (TrainStep.capture; its eager warm-up steps
+    # count as this harness's warm-up), each timed step = the copy of that step's batch into the static
+    # inputs + one replay.  Under DDP the bucketed RCCL all-reduces are captured with it.
+    graphed = graph and device != "cpu" and ops is None
     if graphed:
         static = [[x.clone() for x in z] if isinstance(z, (list, tuple)) else z.clone() for z in batches[0]]
         try:
@@ -505,7 +508,7 @@ def train_bench(world, rank, B, steps, warmup, device="cuda", ops=None, search=3
     step_bytes = tr.get("step", {}).get("traffic_bytes") if (world == 1 and graphed) else None
     return {"value": round(sps, 2), "unit": "samples/s", "ms_per_step": round(elapsed / steps * 1e3, 3),
             "batch_per_gpu": B, "steps": steps, "warmup": warmup,
-            "parallelism": "ddp%d (RCCL gradient all-reduce)" % world if world > 1 else "single",
+            "parallelism": ("ddp%d (bucketed RCCL gradient all-reduce, fp32)" % world if ddp else "single"),
             "step_issue": "one hipGraph replay per step (whole step captured)" if graphed else "eager",
             "roofline": {"kernel": "train_step (whole step)", "bound": "mfma", "achieved": round(ach, 2),
                          "peak": PEAK["bf16"], "unit": "TFLOP/s", "frac": float("%.4g" % (ach / PEAK["bf16"])),
@@ -626,6 +629,9 @@ def main():
                          "(default 16), --steps / --warmup default 20 / 5")
     ap.add_argument("--train-eager", action="store_true",
                     help="training step without the whole-step hipGraph (Python-issued kernels; A/B)")
+    ap.add_argument("--force-ddp", action="store_true",
+                    help="with --train at one GPU: the data-parallel step over a one-rank RCCL group (bucketed "
+                         "all-reduce captured into the step's hipGraph), timed beside the plain step")
     ap.add_argument("--no-train-line", action="store_true",
                     help="skip the short DDP training measurement (train_step) appended to the inference line")
     args = ap.parse_args()
@@ -669,7 +675,14 @@ def main():
     from mmt_amd.runtime import MixFormerRGBTRuntime
 
     if args.train:
-        res = train_bench(world, rank, args.batch, args.steps, args.warmup, graph=not args.train_eager)
+        if args.force_ddp and world == 1:  # a one-rank RCCL group for the DDP step
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(free_port()))
+            dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local))
+            plain = train_bench(1, 0, args.batch, args.steps, args.warmup, graph=not args.train_eager)
+            torch.cuda.empty_cache()
+        res = train_bench(world, rank, args.batch, args.steps, args.warmup, graph=not args.train_eager,
+                          force_ddp=args.force_ddp)
         if rank == 0:
             out = {"metric": "train samples/s (two-stream MixViT-B RGB-T DDP step, BASELINE config 4)",
                    "value": res["value"], "unit": "samples/s", "n_gpus": world, "steps": args.steps,
@@ -681,8 +694,11 @@ def main():
                               "batch_per_gpu": args.batch, "parallelism": res["parallelism"]},
                    "roofline": res["roofline"], "cpu_baseline": None, "last_loss": res["last_loss"],
                    "step_issue": res["step_issue"]}
+            if args.force_ddp and world == 1:
+                out["plain_step"] = {k: plain[k] for k in ("value", "ms_per_step", "parallelism", "step_issue")}
+                out["ddp_vs_plain"] = round(res["value"] / plain["value"], 4)
             print(json.dumps(out), flush=True)
-        if world > 1:
+        if world > 1 or args.force_ddp:
             dist.barrier()
             dist.destroy_process_group()
         return

@@ -19,9 +19,14 @@ def source_files():
     return files
 
 
-def source_digest():
+def train_source_files():
+    """The training step's launch mix also lives in the autograd Functions and the optimizer."""
+    return source_files() + [os.path.join(PKG, "mmt_amd", n) for n in ("train.py", "optim.py", "functional.py")]
+
+
+def source_digest(train=False):
     h = hashlib.sha256()
-    for f in source_files():
+    for f in (train_source_files() if train else source_files()):
         h.update(os.path.relpath(f, ROOT).encode())
         with open(f, "rb") as fh:
             h.update(hashlib.sha256(fh.read()).digest())

@@ -1331,18 +1331,96 @@ def synthetic_batch(B, device, generator=None, template=128, search=320):
     return t, o, s, torch.cat([c - wh / 2, wh], 1).to(device)
 
 
-class TrainStep:
-    """One optimisation step: forward, loss, backward, (DDP all-reduce), clip, AdamW.
+class GradBucketAllReduce:
+    """Data-parallel gradient averaging (what DistributedDataParallel's reducer does for the reference,
+    train_script_mixformer.py:104-110, run_training_ddp.py:94) issued by the step itself on its own
+    stream, so that the whole DDP step can be captured as one hipGraph (RCCL collectives record into a
+    graph; DDP's reducer does host-side bookkeeping that does not).
 
-    net: the two-stream model (mmt_amd.model.build_mixformer_vit_rgbt) on the device, or its DDP
-    wrapper's module; ddp: the DistributedDataParallel wrapper when world > 1 (its forward is the
-    hook point of the gradient all-reduce)."""
+    Buckets: the trainable parameters in reverse registration order (the order their gradients appear in
+    the backward), cut at `cap_bytes` of fp32 (one ViT block's parameters by default, ~27 MB at ViT-B).
+    A post-accumulate-grad hook on every parameter counts a bucket's arrivals; the last one launches the
+    bucket's all-reduce at once, so a block's exchange overlaps the backward of the blocks below it.
+    A bucket is one flat buffer (the gradients concatenated, divided by the world size, in fp32 or
+    rounded to bf16 with compress="bf16"), one all-reduce, and one multi-tensor copy back into the
+    .grad tensors.  finish() launches buckets whose parameters did not all receive a gradient, in bucket
+    order (every rank runs the same graph, so every rank launches the same sequence)."""
+
+    def __init__(self, params, world, group=None, cap_bytes=None, compress="none"):
+        import torch.distributed as dist
+        if compress not in (None, "none", "bf16"):
+            raise ValueError("grad_compress: 'bf16' or 'none'")
+        self.dist, self.group, self.world = dist, group, world
+        self.dtype = torch.bfloat16 if compress == "bf16" else None
+        params = [p for p in params if p.requires_grad][::-1]
+        cap = cap_bytes or 25 * 2 ** 20
+        self.buckets, cur, size = [], [], 0
+        for p in params:
+            if cur and size + p.numel() * 4 > cap:
+                self.buckets.append(cur)
+                cur, size = [], 0
+            cur.append(p)
+            size += p.numel() * 4
+        if cur:
+            self.buckets.append(cur)
+        self.bucket_of = {}
+        for i, b in enumerate(self.buckets):
+            for p in b:
+                self.bucket_of[id(p)] = i
+        self.handles = [p.register_post_accumulate_grad_hook(self._arrived) for p in params]
+        self.begin()
+
+    def begin(self):
+        self.left = [len(b) for b in self.buckets]
+        self.done = [False] * len(self.buckets)
+
+    def _arrived(self, p):
+        i = self.bucket_of[id(p)]
+        self.left[i] -= 1
+        if self.left[i] == 0:
+            self._launch(i)
+
+    def _launch(self, i):
+        self.done[i] = True
+        grads = [p.grad for p in self.buckets[i] if p.grad is not None]
+        if not grads:
+            return
+        flat = torch.cat([g.reshape(-1) for g in grads])
+        if self.dtype is not None:
+            flat = flat.to(self.dtype)
+        if self.world > 1:
+            flat.div_(self.world)
+        self.dist.all_reduce(flat, group=self.group)
+        views = [v.view_as(g) for v, g in zip(flat.split([g.numel() for g in grads]), grads)]
+        torch._foreach_copy_(grads, views)
+
+    def finish(self):
+        for i in range(len(self.buckets)):
+            if not self.done[i]:
+                self._launch(i)
+
+    def remove(self):
+        for h in self.handles:
+            h.remove()
+
+
+class TrainStep:
+    """One optimisation step: forward, loss, backward, (data-parallel gradient all-reduce), clip, AdamW.
+
+    net: the two-stream model (mmt_amd.model.build_mixformer_vit_rgbt) on the device.
+    ddp: False (one process), True (GradBucketAllReduce over the default process group: bucketed RCCL
+    all-reduce launched from the backward's gradient hooks, capturable with the rest of the step), or
+    "torch" (torch.nn.parallel.DistributedDataParallel around the step's module, the reference's wrap;
+    eager only).  grad_compress: "none" (fp32 buckets, the reference's semantics, the default) or "bf16"
+    (buckets rounded to bf16: half the bytes on the links, an explicit numerics deviation)."""
 
     def __init__(self, net, ops, lr=1e-4, weight_decay=1e-4, grad_clip=0.1, iou_weight=2.0, l1_weight=5.0,
-                 ddp=False, grad_compress="bf16"):
+                 ddp=False, grad_compress="none"):
         self.net = net
         self.ops = ops
         self.grad_clip, self.iou_weight, self.l1_weight = grad_clip, iou_weight, l1_weight
+        self._captured_hparams = None
+        self.reducer = None
         # on the device: clip + AdamW as three launches over every parameter (mmt_amd.optim.HipAdamW,
         # which also keeps the bf16 copies of the backbone Linear weights the GEMMs read); on the
         # host (stand-in ops in tests): torch.optim.AdamW + clip_grad_norm_
@@ -1357,30 +1435,42 @@ class TrainStep:
         self.hip_opt = next(net.parameters()).is_cuda
         if ddp and next(net.parameters()).is_cuda:  # train_script_mixformer.py:105
             net = self.net = torch.nn.SyncBatchNorm.convert_sync_batchnorm(net)
-        if ddp:
-            # Gradient all-reduce over RCCL (xGMI rings): buckets of one ViT block's gradients (about 27 MiB of
-            # fp32 for ViT-B), so a block's all-reduce starts as soon as its backward is done and overlaps the
-            # next block's, in ~12 buckets per backbone instead of DDP's default 25 MiB cut through the layers;
-            # and bf16 compression of the buckets (grad_compress="bf16", the default): half the 760 MB of fp32
-            # gradients per step on the links, the sum averaged in bf16 (the backbone's operands are bf16 already).
-            blocks = [m for m in net.modules() if type(m).__name__ in ("Block", "Block_Shared", "Block_Asym")]
-            cap_mb = max((sum(p.numel() for p in b.parameters()) for b in blocks), default=0) * 4 / 2 ** 20
+        if grad_compress not in (None, "none", "bf16"):
+            raise ValueError("grad_compress: 'bf16' or 'none'")
+        # Gradient all-reduce over RCCL (xGMI rings): buckets of one ViT block's gradients (about 27 MiB of
+        # fp32 for ViT-B), so a block's all-reduce starts as soon as its backward is done and overlaps the
+        # next block's, in ~12 buckets per backbone instead of a 25 MiB cut through the layers.
+        blocks = [m for m in net.modules() if type(m).__name__ in ("Block", "Block_Shared", "Block_Asym")]
+        cap_mb = max((sum(p.numel() for p in b.parameters()) for b in blocks), default=0) * 4 / 2 ** 20
+        cap_mb = cap_mb if cap_mb > 0 else 25
+        if ddp == "torch":
             self.model = torch.nn.parallel.DistributedDataParallel(_Wrapped(net, ops), broadcast_buffers=False,
-                                                                   bucket_cap_mb=cap_mb if cap_mb > 0 else 25)
+                                                                   bucket_cap_mb=cap_mb)
             if grad_compress == "bf16":
                 from torch.distributed.algorithms.ddp_comm_hooks import default_hooks
                 self.model.register_comm_hook(None, default_hooks.bf16_compress_hook)
-            elif grad_compress not in (None, "none"):
-                raise ValueError("grad_compress: 'bf16' or 'none'")
+        elif ddp:
+            import torch.distributed as dist
+            # replicas start from rank 0's parameters and buffers (DDP's construction-time broadcast)
+            with torch.no_grad():
+                for t in list(net.parameters()) + list(net.buffers()):
+                    dist.broadcast(t, 0)
+            self.reducer = GradBucketAllReduce(net.parameters(), dist.get_world_size(),
+                                               cap_bytes=int(cap_mb * 2 ** 20), compress=grad_compress)
+            self.model = _Wrapped(net, ops)
         else:
             self.model = _Wrapped(net, ops)
 
     def backward(self, t, o, s, gt_xywh):
         """Forward, loss and backward; under DDP the gradient all-reduce runs inside backward()."""
         self.opt.zero_grad(set_to_none=True)  # autograd then hands each fresh gradient over as .grad
+        if self.reducer is not None:
+            self.reducer.begin()
         pred = self.model(t, o, s)
         loss, stats = box_loss(pred, gt_xywh, self.iou_weight, self.l1_weight)
         loss.backward()
+        if self.reducer is not None:
+            self.reducer.finish()
         stats["loss"] = loss.detach()
         return stats
 
@@ -1404,9 +1494,11 @@ class TrainStep:
         libmmt_hip.so's or PyTorch's own, none of MIOpen's convolutions).  `warmup` eager steps on a side
         stream first (they update the weights like any step).  replay() then runs one step on whatever
         was copied into the static inputs, with no Python issue cost.  The learning rates and weight decay
-        are those at capture time."""
+        are those at capture time, and so are grad_clip and the loss weights.  With ddp=True the
+        bucketed RCCL all-reduces are captured too (GradBucketAllReduce); a torch DDP wrapper
+        (ddp="torch") cannot be captured."""
         if not self.hip_opt or isinstance(self.model, torch.nn.parallel.DistributedDataParallel):
-            raise RuntimeError("TrainStep.capture: single-process HIP training step only")
+            raise RuntimeError("TrainStep.capture: HIP training step without the torch DDP wrapper only")
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
@@ -1415,20 +1507,32 @@ class TrainStep:
         torch.cuda.current_stream().wait_stream(side)
         self.graph = torch.cuda.CUDAGraph()
         self.opt.zero_grad(set_to_none=True)
-        with torch.cuda.graph(self.graph):
+        # With a process group, its watchdog thread polls the events of earlier (eager) collectives; in the
+        # default global capture mode such a query from another thread fails the capture ("operation not
+        # permitted when stream is capturing") and the watchdog aborts the process.  thread_local mode
+        # forbids unsafe calls on the capturing thread only; kernels launched onto the captured stream from
+        # any thread (the autograd worker's) are recorded either way.
+        mode = "global"
+        if self.reducer is not None:
+            torch.cuda.synchronize()
+            mode = "thread_local"
+        with torch.cuda.graph(self.graph, capture_error_mode=mode):
             self.graph_stats = self(t, o, s, gt_xywh)
         self.static_inputs = (t, o, s, gt_xywh)
         self._captured_hparams = self._hparams()
         return self.graph_stats
 
     def _hparams(self):
-        return [(g.get("lr"), g.get("weight_decay"), tuple(g.get("betas", ())), g.get("eps")) for g in self.opt.param_groups]
+        return ([(g.get("lr"), g.get("weight_decay"), tuple(g.get("betas", ())), g.get("eps")) for g in self.opt.param_groups]
+                + [("grad_clip", self.grad_clip), ("iou_weight", self.iou_weight), ("l1_weight", self.l1_weight)])
 
     def replay(self, t=None, o=None, s=None, gt_xywh=None):
         """One captured step; given inputs are first copied into the static ones (device copies).  The
         captured AdamW launches carry the learning rates / weight decays of capture time as kernel arguments,
         so a changed optimizer hyper-parameter (an LR scheduler step) raises instead of replaying stale
         values: capture() again after changing them."""
+        if self._captured_hparams is None:
+            raise RuntimeError("TrainStep.replay: call capture() first")
         if self._hparams() != self._captured_hparams:
             raise RuntimeError("TrainStep.replay: optimizer hyper-parameters changed since capture "
                                "(%s -> %s); call capture() again" % (self._captured_hparams, self._hparams()))

@@ -178,16 +178,19 @@ def _ddp_worker(rank, world, port, out_dir):
     torch.set_num_threads(4)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        for comp in ("none", "bf16"):  # exact fp32 all-reduce, and the default bf16-compressed buckets
+        # the step's own bucketed all-reduce (fp32, the default, and bf16-compressed buckets) and the torch
+        # DistributedDataParallel wrapper (ddp="torch", fp32)
+        for mode, comp in ((True, "none"), (True, "bf16"), ("torch", "none")):
             net = _net()
-            step = TrainStep(net, TorchOps, lr=1e-4, ddp=True, grad_compress=comp)
+            step = TrainStep(net, TorchOps, lr=1e-4, ddp=mode, grad_compress=comp)
             t, o, s, gt = _batch(2, 5)
             sl = slice(rank, rank + 1)  # each rank its own sequence of the global batch of 2
             step.backward([x[sl] for x in t], [x[sl] for x in o], [x[sl] for x in s], gt[sl])
             grads = {n: p.grad.clone() for n, p in net.named_parameters() if p.grad is not None}
             step.apply()
             params = {n: p.detach().clone() for n, p in net.named_parameters()}
-            torch.save({"grads": grads, "params": params}, os.path.join(out_dir, "rank%d_%s.pt" % (rank, comp)))
+            tag = comp if mode is True else "torch_" + comp
+            torch.save({"grads": grads, "params": params}, os.path.join(out_dir, "rank%d_%s.pt" % (rank, tag)))
     finally:
         dist.destroy_process_group()
 
@@ -208,7 +211,7 @@ def test_ddp_gloo_two_ranks_matches_full_batch(tmp_path):
     full = {n: p.grad for n, p in net.named_parameters() if p.grad is not None}
     # fp32 all-reduce: the batch mean within fp32 summation noise; bf16-compressed buckets: the
     # mean rounded to bf16 (8 significant bits) once, within 2^-7 of each tensor's largest gradient
-    for comp, tol in (("none", 1e-4), ("bf16", 2 ** -7)):
+    for comp, tol in (("none", 1e-4), ("bf16", 2 ** -7), ("torch_none", 1e-4)):
         r0 = torch.load(tmp_path / ("rank0_%s.pt" % comp), weights_only=True)
         r1 = torch.load(tmp_path / ("rank1_%s.pt" % comp), weights_only=True)
         assert set(full) == set(r0["grads"]) == set(r1["grads"])

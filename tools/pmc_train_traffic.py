@@ -42,7 +42,7 @@ def main():
     from mmt_amd.stamp import source_digest
     res = {"step": {"fetch_bytes": round(fb), "write_bytes": round(wb), "traffic_bytes": round(fb + wb),
                     "launches": launches, "steps": len(vals["FETCH_SIZE"])},
-           "_stamp": {"source_digest": source_digest(), "git_head": os.environ.get("MMT_GIT_HEAD", "")}}
+           "_stamp": {"source_digest": source_digest(train=True), "git_head": os.environ.get("MMT_GIT_HEAD", "")}}
     try:
         allres = json.load(open(dst))
     except (OSError, ValueError):
