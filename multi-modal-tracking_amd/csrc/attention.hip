@@ -1849,6 +1849,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
 
 }  // namespace
 
+int mmt_attn_launch_ps(const mmt_attn_params& p, hipStream_t st);  // attention_ps.hip: impl 29 (persistent)
 #if MMT_ATTN_AB
 int mmt_attn_launch_pp(const mmt_attn_params& p, int ks, hipStream_t st);  // attention_pp.hip: impl 24 / 25
 int mmt_attn_launch_pg(const mmt_attn_params& p, hipStream_t st);          // attention_pg.hip: impl 28
@@ -1861,7 +1862,7 @@ int launch_attn(const mmt_attn_params& p, hipStream_t st) {
     // impl: 0 = the library's choice by dtype and grid size; forced (A/B and tests): 4 = latency kernel,
     // 8 = running-maximum throughput kernel, 17 / 21 / 22 = range-checked exponent kernels (22 = 64
     // queries per wave); A/B build: 23 = the block-pipelined form of 22 with 256-query workgroups
-    if (p.impl != 0 && p.impl != 4 && p.impl != 8 && p.impl != 17 && p.impl != 21 && p.impl != 22 &&
+    if (p.impl != 0 && p.impl != 4 && p.impl != 8 && p.impl != 17 && p.impl != 21 && p.impl != 22 && p.impl != 29 &&
         !(MMT_ATTN_AB && (p.impl == 23 || p.impl == 24 || p.impl == 25 || p.impl == 26 || p.impl == 27 || p.impl == 28)))
         return MMT_EBADARG;
     // lse (training forward) is written by impls 0 / 4 / 8 / 17 / 21 only: impls 22 / 23 never write it
@@ -1908,6 +1909,11 @@ int launch_attn(const mmt_attn_params& p, hipStream_t st) {
         if (impl == 17) hipLaunchKernelGGL((mam_attention_lz_kernel<3, 3, true>), fgrid, dim3(256), 0, st, p);
         else if (impl == 21) hipLaunchKernelGGL((mam_attention_lz_kernel<3, 3, true, true>), fgrid, dim3(256), 0, st, p);
         else if (impl == 22) hipLaunchKernelGGL((mam_attention_lz2_kernel<2>), fgrid, dim3(128), 0, st, p);
+        else if (impl == 29) {  // persistent kernel: bf16 only, its own shape check
+            if (!bf) return MMT_EBADARG;
+            const int rc = mmt_attn_launch_ps(p, st);
+            if (rc) return rc;
+        }
 #if MMT_ATTN_AB
         else if (impl == 24 || impl == 25) mmt_attn_launch_pp(p, impl == 25 ? 2 : 1, st);
         else if (impl == 28) mmt_attn_launch_pg(p, st);

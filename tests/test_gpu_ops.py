@@ -815,6 +815,81 @@ def test_mam_attention_pipelined_is_default_and_bitwise(asym):
     assert err <= 1.5e-2, err
 
 
+def _attn_run(L, qd, S, Bm, ntok, n_t, C, H, asym, impl, scale=1.0 / 1.4426950408889634, **kw):
+    out = torch.full((S, kw.get("out_rows", ntok), C), float("nan"), device="cuda", dtype=torch.bfloat16)
+    p = L.AttnParams()
+    p.qkv, p.out, p.S, p.Bm, p.ntok, p.n_t, p.C, p.H, p.asym = qd.data_ptr(), out.data_ptr(), S, Bm, ntok, n_t, C, H, asym
+    p.scale, p.impl = scale, impl
+    rc = L.LIB.mmt_mam_attention(p, L.MMT_BF16, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return rc, out
+
+
+@pytest.mark.parametrize("asym", [0, 1])
+@pytest.mark.parametrize("Bm", [1, 3, 8, 32])
+def test_mam_attention_persistent_bitwise(asym, Bm):
+    """impl 29 (persistent one-wave-per-SIMD workgroups walking (sequence, head) items over a continuous
+    K / V tile stream) computes impl 22's MFMAs and exponentials in the same order per query: bitwise
+    equal outputs at every grid size (B = 1: fewer items than CUs; B = 32: six items per workgroup),
+    on the joint and the cross-modal key streams, every output row written."""
+    L = _lib()
+    ntok, n_t, H = 528, 128, 12
+    S, C = 2 * Bm, 64 * H
+    g = torch.Generator().manual_seed(400 + Bm + asym)
+    qkv = torch.randn(S, ntok, 3 * C, generator=g) * 0.5
+    qkv[..., :C] *= 0.125 * 1.4426950408889634  # the runtime's pre-scaled q
+    qd = qkv.bfloat16().cuda()
+    rc22, o22 = _attn_run(L, qd, S, Bm, ntok, n_t, C, H, asym, 22)
+    rc29, o29 = _attn_run(L, qd, S, Bm, ntok, n_t, C, H, asym, 29)
+    assert rc22 == 0 and rc29 == 0
+    assert not torch.isnan(o29).any()
+    assert torch.equal(o22, o29)
+    if Bm <= 3:
+        qr = qkv.bfloat16().float()
+        qr[..., :C] /= 0.125 * 1.4426950408889634
+        ref = _attn_ref(qr, S, Bm, ntok, n_t, C, H, asym)
+        assert (o29.float().cpu() - ref).abs().max().item() <= 1.5e-2
+
+
+@pytest.mark.parametrize("asym", [0, 1])
+def test_mam_attention_persistent_natural_scale_and_fallback(asym):
+    """impl 29 with q at its natural scale (the kernel pre-scales Q in registers) and with scores outside
+    exp2's range without a reference point (the exact two-pass fallback, stored in place while the other
+    query blocks go through the staged stores): bitwise equal to impl 22 and to the fp64 softmax."""
+    L = _lib()
+    Bm, ntok, n_t, H = 2, 528, 128, 4
+    S, C = 2 * Bm, 64 * H
+    g = torch.Generator().manual_seed(31 + asym)
+    qkv = torch.randn(S, ntok, 3 * C, generator=g) * 0.5
+    qkv[:, 500, C:2 * C] = qkv[:, 300, :C] * 60
+    qkv[:, 310, :C] *= 40
+    qkv[:, 40, :C] *= 40  # a template query (template wave of the mixed item)
+    qkv[:, 520, :C] *= 40  # a query of the 16-query last block
+    qd = qkv.bfloat16().cuda()
+    rc22, o22 = _attn_run(L, qd, S, Bm, ntok, n_t, C, H, asym, 22, scale=0.125)
+    rc29, o29 = _attn_run(L, qd, S, Bm, ntok, n_t, C, H, asym, 29, scale=0.125)
+    assert rc22 == 0 and rc29 == 0
+    assert torch.equal(o22, o29)
+    ref = _attn_ref(qkv.bfloat16().double(), S, Bm, ntok, n_t, C, H, asym).float()
+    o = o29.float().cpu()
+    assert torch.isfinite(o).all()
+    assert (o - ref).abs().max().item() < 2.5e-2 * max(1.0, ref.abs().max().item())
+
+
+def test_mam_attention_persistent_rejects_other_shapes():
+    """impl 29 takes the ViT-B 128/320 token layout only (n_t 128, 400 search tokens, all queries):
+    other shapes and the template K/V cache's partial passes are refused, nothing launched."""
+    L = _lib()
+    qd = torch.zeros(2, 864, 3 * 128, device="cuda", dtype=torch.bfloat16)
+    assert _attn_run(L, qd, 2, 1, 864, 288, 128, 2, 0, 29)[0] == -10000
+    qd = torch.zeros(2, 528, 3 * 128, device="cuda", dtype=torch.bfloat16)
+    out = torch.empty(2, 528, 128, device="cuda", dtype=torch.bfloat16)
+    p = L.AttnParams()
+    p.qkv, p.out, p.S, p.Bm, p.ntok, p.n_t, p.C, p.H, p.asym = qd.data_ptr(), out.data_ptr(), 2, 1, 528, 128, 128, 2, 0
+    p.scale, p.impl, p.q_part = 1.0, 29, 2
+    assert L.LIB.mmt_mam_attention(p, L.MMT_BF16, torch.cuda.current_stream().cuda_stream) == -10000
+
+
 @pytest.mark.parametrize("dname", ["f32", "bf16", "fp16"])
 @pytest.mark.parametrize("C", [256, 512, 768, 1024])
 def test_layernorm_groups_and_add(dname, C):
