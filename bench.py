@@ -481,6 +481,8 @@ def train_bench(world, rank, B, steps, warmup, device="cuda", ops=None, search=3
     graphed = graph and device != "cpu" and ops is None
     if graphed:
         static = [[x.clone() for x in z] if isinstance(z, (list, tuple)) else z.clone() for z in batches[0]]
+        import mmt_amd.train as _T
+        _T.GEMM_ACCOUNT = {}  # every GEMM launch of the capture's steps (warm-up + the captured one), per step below
         try:
             step_fn.capture(*static, warmup=max(1, warmup))
         except RuntimeError as e:
@@ -488,7 +490,11 @@ def train_bench(world, rank, B, steps, warmup, device="cuda", ops=None, search=3
             # capture can leave the optimizer's pointer table half written and the stream invalidated
             # (ADVICE r4); the caller reports the error (default line) or the run exits non-zero (--train)
             raise RuntimeError("train step capture failed: %s" % str(e)[:300]) from e
+    gemm_acc = None
     if graphed:
+        gemm_acc = {k: v / (max(1, warmup) + 1) for k, v in _T.GEMM_ACCOUNT.items()}
+        _T.GEMM_ACCOUNT = None
+
         def step(i):
             last["stats"] = step_fn.replay(*batches[i % 2])
 
@@ -506,6 +512,9 @@ def train_bench(world, rank, B, steps, warmup, device="cuda", ops=None, search=3
     # step, this batch), reported only on the kernel sources it was taken on
     tr, tr_note = load_traffic("train", B, "bf16")
     step_bytes = tr.get("step", {}).get("traffic_bytes") if (world == 1 and graphed) else None
+    dominant = None
+    if graphed and rank == 0 and gemm_acc:
+        dominant = train_gemm_roofline(step, gemm_acc, tr if world == 1 else {}, tr_note)
     return {"value": round(sps, 2), "unit": "samples/s", "ms_per_step": round(elapsed / steps * 1e3, 3),
             "batch_per_gpu": B, "steps": steps, "warmup": warmup,
             "parallelism": ("ddp%d (bucketed RCCL gradient all-reduce, fp32)" % world if ddp else "single"),
@@ -515,9 +524,48 @@ def train_bench(world, rank, B, steps, warmup, device="cuda", ops=None, search=3
                          "flops_per_sample": TRAIN_FLOP_PER_SAMPLE, "traffic": step_bytes,
                          "traffic_unit": "bytes/step (HBM, PMC)",
                          "traffic_source": tr_note if (world == 1 and graphed) else "not measured for this setup",
-                         "hbm_TBps": round(step_bytes / (elapsed / steps) / 1e12, 3) if step_bytes else None},
+                         "hbm_TBps": round(step_bytes / (elapsed / steps) / 1e12, 3) if step_bytes else None,
+                         "dominant": dominant},
             "last_loss": round(float(last["stats"]["loss"]), 5),
             "opt_table_writes": getattr(step_fn.opt, "table_writes", None)}
+
+
+def train_gemm_roofline(step, acc, tr, tr_note, steps=6):
+    """The training step's dominant kernel family, the GEMMs (every mmt_gemm launch: Linear forward / dX / dW,
+    the head's implicit-GEMM convolutions): per step the FLOPs and algorithmic bytes counted by the step's own
+    GEMM calls (mmt_amd.train.GEMM_ACCOUNT over the capture), the device time of the gemm kernels from
+    `steps` graph replays under torch.profiler (the dispatch timestamps a rocprofv3 kernel trace reports), and
+    the family's HBM bytes per step from the committed counter pass when it was taken on these sources
+    (tools/pmc_train_traffic.py)."""
+    from torch.profiler import ProfilerActivity, profile
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        for i in range(steps):
+            step(i)
+        torch.cuda.synchronize()
+    tot = gem = 0.0
+    n_gem = n_all = 0
+    for e in prof.events():
+        if str(getattr(e, "device_type", "")).endswith("CUDA") and e.time_range.end > e.time_range.start:
+            d = (e.time_range.end - e.time_range.start) * 1e-6  # us -> s
+            tot += d
+            n_all += 1
+            if "gemm" in e.name:
+                gem += d
+                n_gem += 1
+    if gem <= 0:
+        return None
+    gem_s, tot_s = gem / steps, tot / steps
+    ach = acc["flops"] / gem_s / 1e12
+    fam = tr.get("gemm", {}) if tr else {}
+    traffic = fam.get("traffic_bytes")
+    return {"kernel": "gemm (every mmt_gemm launch of the step)", "bound": "mfma", "achieved": round(ach, 2),
+            "peak": PEAK["bf16"], "unit": "TFLOP/s", "frac": float("%.4g" % (ach / PEAK["bf16"])),
+            "flops_per_step": acc["flops"], "launches_per_step": round(acc.get("launches", 0)),
+            "device_ms_per_step": round(gem_s * 1e3, 3), "share_of_step_device_time": round(gem_s / tot_s, 4),
+            "kernel_launches_per_step": round(n_all / steps), "algorithmic_bytes_per_step": round(acc["bytes"]),
+            "traffic": traffic, "traffic_unit": "bytes/step (HBM, PMC, gemm kernels)",
+            "traffic_over_algorithmic": round(traffic / acc["bytes"], 3) if traffic else None,
+            "traffic_source": tr_note if traffic else "no gemm-family counter pass on these sources"}
 
 
 def timed_steps(step, steps, world, sync, device):

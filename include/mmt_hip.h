@@ -382,6 +382,19 @@ int mmt_corner_softargmax(const void* x4, const float* w5, const float* b5, cons
                           float* score_maps, float* boxes_cxcywh, float* boxes_xyxy, float* rois, float roi_scale,
                           int B, int fh, int c4, int stride, int dtype, void* stream);
 
+/* Training (train.py _HipCornerScore; head.py:191-192): ONE corner branch's score map, with its backward.
+ * score_map[b][p] fp32 = (x4[b][p] . w5 + b5) + a3[b][up4(p)] + a4[b][up2(p)]: x4 bf16 [B][fh*fh][c4] (NHWC
+ * rows, c4 % 8 == 0), w5 [c4] / b5 [1] fp32 (conv5 in fp32), a3 / a4 bf16 1-channel maps of (fh/4)^2 /
+ * (fh/2)^2 pixels at pixel strides s3 / s4 (elements).  The backward writes dx4 bf16 [B][fh*fh][c4], da3 /
+ * da4 bf16 contiguous, dw5 [c4] / db5 [1] fp32 (deterministic: fixed-order partial sums through ws, which
+ * holds mmt_corner_score_train_ws_floats(B, fh, c4) floats); fh <= 128, c4 < 64.  Replaces the reference
+ * path's Conv2d(48, 1, 1) + two F.interpolate + adds (and aten's / hipBLASLt's kernels for them). */
+int mmt_corner_score_train(const void* x4, const float* w5, const float* b5, const void* a3, int64_t s3,
+                           const void* a4, int64_t s4, float* score_map, int B, int fh, int c4, void* stream);
+int64_t mmt_corner_score_train_ws_floats(int B, int fh, int c4);
+int mmt_corner_score_train_bwd(const float* dsm, const void* x4, const float* w5, void* dx4, void* da3, void* da4,
+                               float* dw5, float* db5, float* ws, int B, int fh, int c4, void* stream);
+
 /* PrRoIPool2D forward.  features fp32 with strides (batch, channel, y, x) in elements, rois
  * [R][5] = (batch, x0, y0, x1, y1); out element (r, c, ph, pw) at r*o_r + c*o_c + (ph*pw_+pw)*o_p
  * (the reference's [R][C][ph][pw] is o_r = C*ph*pw, o_c = ph*pw, o_p = 1). */

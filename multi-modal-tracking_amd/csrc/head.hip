@@ -5,6 +5,7 @@
 //                          x2) (head.py:191-192), softmax over the 80x80 map and the expectation of the
 //                          coordinate grids (head.py:138-145, 200-212), /img_sz, box_xyxy_to_cxcywh
 //                          (lib/utils/box_ops.py:27-32); one workgroup per frame, both corners
+//   mmt_corner_score_train / _bwd  the training step's conv5 + pyramid adds of one branch and their backward
 //   mmt_prroi_pool_forward PrRoIPoolingForward (prroi_pooling_gpu_impl.cu:149-212) with explicit
 //                          feature strides so the channels-last fusion output is pooled in place
 //   mmt_spm_attention      ScoreDecoder single-query multi-head attention (score_decoder.py:55-61)
@@ -114,6 +115,110 @@ __global__ __launch_bounds__(256) void corner_score_kernel(const T* __restrict__
     s = (s + b5[g]) + a3[((int64_t)g * B + b) * f4 * f4 + (y / 4) * f4 + x / 4] +
         a4[((int64_t)g * B + b) * f2 * f2 + (y / 2) * f2 + x / 2];
     maps[((int64_t)g * B + b) * np + p] = s;
+}
+
+// ---- training (train.py _HipCornerScore): one corner branch's score map with autograd's backward.
+// sm[b][p] = (x4[b][p] . w5 + b5) + a3[b][up4(p)] + a4[b][up2(p)]  (head.py:191-192: conv5 1x1 48 -> 1 in fp32,
+// nearest-upsampled adjust3 / adjust4 maps); x4 bf16 NHWC rows [B][fh*fh][c4]; a3 / a4 bf16 1-channel maps at
+// pixel strides s3 / s4 (the 8-channel rows the HIP BatchNorm writes).  Replaces aten's fp32 F.linear through
+// hipBLASLt (~175 us a launch for 10 MFLOP), two nearest upsamplings and two adds, and their backward.
+__global__ __launch_bounds__(256) void corner_score_train_kernel(const bf16_t* __restrict__ x4, const float* __restrict__ w5,
+                                                                 const float* __restrict__ b5, const bf16_t* __restrict__ a3,
+                                                                 int64_t s3, const bf16_t* __restrict__ a4, int64_t s4,
+                                                                 float* __restrict__ out, int B, int fh, int c4) {
+    const int np = fh * fh, f4 = fh / 4, f2 = fh / 2;
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (int64_t)B * np) return;
+    const int b = idx / np, p = idx % np, y = p / fh, x = p % fh;
+    const bf16_t* px = x4 + idx * c4;
+    float s = 0.f;
+    for (int cc = 0; cc < c4; cc += 8) {
+        const uint4 v = *(const uint4*)(px + cc);
+        const uint32_t va[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const f32x2 vj = unpack2<bf16_t>(va[j]);
+            s += vj[0] * w5[cc + 2 * j];
+            s += vj[1] * w5[cc + 2 * j + 1];
+        }
+    }
+    s = (s + b5[0]) + bf2f(a3[((int64_t)b * f4 * f4 + (y / 4) * f4 + x / 4) * s3]) +
+        bf2f(a4[((int64_t)b * f2 * f2 + (y / 2) * f2 + x / 2) * s4]);
+    out[idx] = s;
+}
+
+// Backward of one branch: one workgroup per 4-row band of one map (fh threads per row, 4 rows): dx4[p][c] =
+// bf16(dsm[p] w5[c]); da3 (the band's fh/4 outputs, each the sum of its 4x4 dsm block) and da4 (2 rows of fh/2,
+// each a 2x2 sum), bf16 like the maps (contiguous [..][1]); the band's dw5 / db5 partial sums, in a fixed order
+// (pixels of the band in 6 interleaved groups per channel, then the groups in order) into part[band][c4 + 1]:
+// deterministic, no atomics.  corner_score_train_fin_kernel sums the bands in order.
+__global__ __launch_bounds__(512) void corner_score_train_bwd_kernel(const float* __restrict__ dsm, const bf16_t* __restrict__ x4,
+                                                                     const float* __restrict__ w5, bf16_t* __restrict__ dx4,
+                                                                     bf16_t* __restrict__ da3, bf16_t* __restrict__ da4,
+                                                                     float* __restrict__ part, int B, int fh, int c4) {
+    __shared__ float sd[4 * 128];       // the band's dsm (fh <= 128)
+    __shared__ float red[8][64 + 1];    // per-group partial sums of each channel (c4 <= 64) and the bias
+    const int np = fh * fh, bands = fh / 4, band = blockIdx.x;
+    const int b = band / bands, r0 = (band % bands) * 4;
+    const int nbp = 4 * fh;  // pixels of the band
+    const int64_t p0 = (int64_t)b * np + (int64_t)r0 * fh;
+    for (int t = threadIdx.x; t < nbp; t += blockDim.x) sd[t] = dsm[p0 + t];
+    __syncthreads();
+    // dx4: thread per (pixel, 8-channel chunk)
+    const int nchunk = c4 / 8;
+    for (int t = threadIdx.x; t < nbp * nchunk; t += blockDim.x) {
+        const int pp = t / nchunk, ck = t - pp * nchunk;
+        const float d = sd[pp];
+        uint32_t o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(d * w5[ck * 8 + 2 * j], d * w5[ck * 8 + 2 * j + 1]);
+        *(uint4*)(dx4 + (p0 + pp) * c4 + ck * 8) = uint4{o[0], o[1], o[2], o[3]};
+    }
+    // dw5 / db5 partials: channel c (c < c4) or the bias (c == c4) over pixel group gi (pixels gi, gi + 8, ...)
+    for (int t = threadIdx.x; t < 8 * (c4 + 1); t += blockDim.x) {
+        const int c = t % (c4 + 1), gi = t / (c4 + 1);
+        float acc = 0.f;
+        for (int pp = gi; pp < nbp; pp += 8) acc += c < c4 ? sd[pp] * bf2f(x4[(p0 + pp) * c4 + c]) : sd[pp];
+        red[gi][c] = acc;
+    }
+    // da3: fh / 4 outputs of this band; da4: 2 rows of fh / 2
+    const int f4 = fh / 4, f2 = fh / 2;
+    for (int t = threadIdx.x; t < f4 + 2 * f2; t += blockDim.x) {
+        if (t < f4) {
+            float acc = 0.f;
+#pragma unroll
+            for (int dy = 0; dy < 4; ++dy)
+#pragma unroll
+                for (int dx = 0; dx < 4; ++dx) acc += sd[dy * fh + 4 * t + dx];
+            da3[(int64_t)b * f4 * f4 + (r0 / 4) * f4 + t] = f2bf(acc);
+        } else {
+            const int u = t - f4, ry = u / f2, cx = u - ry * f2;
+            float acc = 0.f;
+#pragma unroll
+            for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+                for (int dx = 0; dx < 2; ++dx) acc += sd[(2 * ry + dy) * fh + 2 * cx + dx];
+            da4[(int64_t)b * f2 * f2 + (r0 / 2 + ry) * f2 + cx] = f2bf(acc);
+        }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c <= c4; c += blockDim.x) {
+        float acc = 0.f;
+#pragma unroll
+        for (int gi = 0; gi < 8; ++gi) acc += red[gi][c];
+        part[(int64_t)band * (c4 + 1) + c] = acc;
+    }
+}
+
+// dw5[c] = sum over the bands (in order) of part[band][c]; db5 = the same for column c4
+__global__ __launch_bounds__(64) void corner_score_train_fin_kernel(const float* __restrict__ part, float* __restrict__ dw5,
+                                                                   float* __restrict__ db5, int nbands, int c4) {
+    const int c = threadIdx.x;
+    if (c > c4) return;
+    float acc = 0.f;
+    for (int i = 0; i < nbands; ++i) acc += part[(int64_t)i * (c4 + 1) + c];
+    if (c < c4) dw5[c] = acc;
+    else db5[0] = acc;
 }
 
 // softmax over each fh x fh map + expectation of the coordinate grids; one workgroup per frame.
@@ -529,6 +634,34 @@ extern "C" int mmt_corner_softargmax(const void* x4, const float* w5, const floa
     else
         hipLaunchKernelGGL(softargmax_kernel<16>, dim3(B), dim3(SA_NT), 0, st, score_maps, boxes_cxcywh, boxes_xyxy,
                            rois, roi_scale, B, fh, stride);
+    return launch_status();
+}
+
+extern "C" int mmt_corner_score_train(const void* x4, const float* w5, const float* b5, const void* a3, int64_t s3,
+                                      const void* a4, int64_t s4, float* score_map, int B, int fh, int c4, void* stream) {
+    if (!x4 || !w5 || !b5 || !a3 || !a4 || !score_map || B <= 0 || fh <= 0 || fh % 4 || c4 <= 0 || c4 % 8 || s3 <= 0 ||
+        s4 <= 0)
+        return MMT_EBADARG;
+    hipLaunchKernelGGL(corner_score_train_kernel, dim3((unsigned)(((int64_t)B * fh * fh + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, (const bf16_t*)x4, w5, b5, (const bf16_t*)a3, s3, (const bf16_t*)a4, s4,
+                       score_map, B, fh, c4);
+    return launch_status();
+}
+
+extern "C" int64_t mmt_corner_score_train_ws_floats(int B, int fh, int c4) {
+    return (int64_t)B * (fh / 4) * (c4 + 1);
+}
+
+extern "C" int mmt_corner_score_train_bwd(const float* dsm, const void* x4, const float* w5, void* dx4, void* da3, void* da4,
+                                          float* dw5, float* db5, float* ws, int B, int fh, int c4, void* stream) {
+    if (!dsm || !x4 || !w5 || !dx4 || !da3 || !da4 || !dw5 || !db5 || !ws || B <= 0 || fh <= 0 || fh % 4 || fh > 128 ||
+        c4 <= 0 || c4 % 8 || c4 > 63)
+        return MMT_EBADARG;
+    hipStream_t st = (hipStream_t)stream;
+    const int nb = B * (fh / 4);
+    hipLaunchKernelGGL(corner_score_train_bwd_kernel, dim3(nb), dim3(512), 0, st, dsm, (const bf16_t*)x4, w5, (bf16_t*)dx4,
+                       (bf16_t*)da3, (bf16_t*)da4, ws, B, fh, c4);
+    hipLaunchKernelGGL(corner_score_train_fin_kernel, dim3(1), dim3(64), 0, st, ws, dw5, db5, nb, c4);
     return launch_status();
 }
 

@@ -87,6 +87,9 @@ _PROTOS = {
     "mmt_conv3x3_c1": [vp, vp, vp, vp, i32, i32, i32, i32, i64, i32, vp],
     "mmt_conv3x3_c1_pair": [vp, vp, vp, vp, i32, i64, vp, vp, vp, vp, i32, i64, i32, i32, i32, i32, vp],
     "mmt_corner_softargmax": [vp, vp, vp, vp, vp, vp, vp, vp, vp, f32, i32, i32, i32, i32, i32, vp],
+    "mmt_corner_score_train": [vp, vp, vp, vp, i64, vp, i64, vp, i32, i32, i32, vp],
+    "mmt_corner_score_train_ws_floats": [i32, i32, i32],
+    "mmt_corner_score_train_bwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp],
     "mmt_prroi_pool_forward": [vp, vp, vp, i32, i32, i32, i32, i64, i64, i64, i64, i32, i32, f32, i64, i64, i64, vp],
     "mmt_prroi_pool_backward": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, f32, vp],
     "mmt_prroi_pool_coor_backward": [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, f32, vp],
@@ -114,6 +117,7 @@ def _load():
         fn.argtypes = args
         fn.restype = ctypes.c_int
     lib.mmt_batchnorm_ws_floats.restype = ctypes.c_int64
+    lib.mmt_corner_score_train_ws_floats.restype = ctypes.c_int64
     lib.mmt_version.argtypes = []
     lib.mmt_version.restype = ctypes.c_char_p
     return lib

@@ -86,6 +86,21 @@ def _splitk_ws(dev):
     return ws
 
 
+# Per-step GEMM accounting for bench.py's train_step.roofline: None, or a dict that every GEMM launch of the
+# step adds to while it is set (one eager step: "flops" = 2 M N K per group, "bytes" = the launch's algorithmic
+# HBM bytes -- each operand read once, the output written once, bias / residual / second output included --
+# and "launches").  Host-side bookkeeping only; the launches themselves are unchanged.
+GEMM_ACCOUNT = None
+
+
+def _account(M, N, K, G, a_bytes, w_bytes, c_bytes, extra_bytes=0):
+    acc = GEMM_ACCOUNT
+    if acc is not None:
+        acc["flops"] = acc.get("flops", 0.0) + 2.0 * M * N * K * G
+        acc["bytes"] = acc.get("bytes", 0.0) + G * (M * K * a_bytes + N * K * w_bytes + M * N * c_bytes) + extra_bytes
+        acc["launches"] = acc.get("launches", 0) + 1
+
+
 def _gemm(a, w, M, N, K, bias=None, out_f32=False, act=0, r=None, c2=None, c2_copy=0, c=None, ldc=None, a_t=0,
           w_t=0, ldw=0, lda=None, splitk=False, impl=0, row_scale=None, row_scale_div=1, nsk=0):
     """C[M][N] = A[M][K] W[N][K]^T (+ bias), bf16 operands, fp32 accumulation (mmt_gemm); act / r (bf16,
@@ -133,6 +148,14 @@ def _gemm(a, w, M, N, K, bias=None, out_f32=False, act=0, r=None, c2=None, c2_co
             p.c2[g] = t.data_ptr()
         p.c2_copy = c2_copy
     check(LIB.mmt_gemm(p, MMT_BF16, _stream()), "mmt_gemm")
+    if GEMM_ACCOUNT is not None:
+        extra = G * N * 4 if bias is not None else 0
+        if r is not None:
+            extra += G * M * N * (r if not grouped else r[0]).element_size()
+        if c2 is not None:
+            t2 = c2 if not grouped else c2[0]
+            extra += G * t2.numel() * t2.element_size()
+        _account(M, N, K, G, 2, 2, 4 if out_f32 else 2, extra)
     return c
 
 
@@ -575,6 +598,8 @@ def _conv_gemm(x, wr, B, H, Cin, Cout, bias=None, flip=False):
     p.M, p.N, p.K, p.groups = M, Cout, 9 * Cin, 1
     p.conv_h, p.conv_up, p.conv_cin, p.conv_k3 = H, 1, Cin, 2 if flip else 1
     check(LIB.mmt_gemm(p, MMT_BF16, _stream()), "mmt_gemm (conv)")
+    # implicit GEMM: the input map is read once (B H H Cin), not the im2col matrix
+    _account(M, Cout, 9 * Cin, 1, 0, 2, 2, M * Cin * 2 + (Cout * 4 if bias is not None else 0))
     return y
 
 
@@ -621,6 +646,51 @@ class _HipBatchNormReLU(torch.autograd.Function):
         dw = dgb[0] if ctx.needs_input_grad[1] else None
         db = dgb[1] if ctx.needs_input_grad[2] else None
         return dx, dw, db, None, None, None, None, None, None
+
+
+class _HipCornerScore(torch.autograd.Function):
+    """One corner branch's score map in the training step (head.py:191-192): conv5 (Conv2d(48, 1, 1), in fp32 as
+    HEAD_SCORE_FP32) + up4(adjust3) + up2(adjust4) -> (B, fh*fh) fp32, forward and backward on
+    mmt_corner_score_train / _bwd.  x4 (B, fh, fh, c4) bf16 NHWC; a3 / a4 (B, fh/4, fh/4, 1) / (B, fh/2, fh/2, 1)
+    bf16 views (the HIP BatchNorm's 8-channel rows: pixel stride = their stride(2)).  Replaces aten's fp32
+    F.linear through hipBLASLt (~175 us a launch), two nearest upsamplings and two adds, and their backward."""
+
+    @staticmethod
+    def forward(ctx, x4, w5, b5, a3, a4):
+        from ._lib import LIB, check
+        B, fh, _, c4 = x4.shape
+        if x4.dtype != torch.bfloat16 or not x4.is_contiguous() or a3.dtype != torch.bfloat16 or a4.dtype != torch.bfloat16:
+            raise ValueError("HIP corner score: contiguous bf16 NHWC x4, bf16 adjust maps")
+        if a3.shape != (B, fh // 4, fh // 4, 1) or a4.shape != (B, fh // 2, fh // 2, 1):
+            raise ValueError("HIP corner score: adjust maps of fh/4 and fh/2")
+        for a in (a3, a4):
+            if a.stride(1) != a.stride(2) * a.shape[2] or a.stride(0) != a.stride(1) * a.shape[1]:
+                raise ValueError("HIP corner score: adjust maps must be pixel-strided views")
+        w = w5.detach().reshape(-1).float().contiguous()
+        b = b5.detach().reshape(-1).float().contiguous()
+        out = torch.empty(B, fh * fh, device=x4.device, dtype=torch.float32)
+        check(LIB.mmt_corner_score_train(x4.data_ptr(), w.data_ptr(), b.data_ptr(), a3.data_ptr(), a3.stride(2),
+                                         a4.data_ptr(), a4.stride(2), out.data_ptr(), B, fh, c4, _stream()),
+              "mmt_corner_score_train")
+        ctx.save_for_backward(x4, w)
+        ctx.wshape = w5.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, dsm):
+        from ._lib import LIB, check
+        x4, w = ctx.saved_tensors
+        B, fh, _, c4 = x4.shape
+        dsm = dsm.float().contiguous()
+        dx4 = torch.empty_like(x4)
+        da3 = torch.empty(B, fh // 4, fh // 4, 1, device=x4.device, dtype=torch.bfloat16)
+        da4 = torch.empty(B, fh // 2, fh // 2, 1, device=x4.device, dtype=torch.bfloat16)
+        dw = torch.empty(c4 + 1, device=x4.device, dtype=torch.float32)
+        ws = torch.empty(int(LIB.mmt_corner_score_train_ws_floats(B, fh, c4)), device=x4.device, dtype=torch.float32)
+        check(LIB.mmt_corner_score_train_bwd(dsm.data_ptr(), x4.data_ptr(), w.data_ptr(), dx4.data_ptr(), da3.data_ptr(),
+                                             da4.data_ptr(), dw.data_ptr(), dw[c4:].data_ptr(), ws.data_ptr(), B, fh, c4,
+                                             _stream()), "mmt_corner_score_train_bwd")
+        return dx4, dw[:c4].view(ctx.wshape), dw[c4:], da3, da4
 
 
 class _HipConv3x3(torch.autograd.Function):
@@ -795,6 +865,11 @@ class HipOps:
         """The corner head's 3x3 convolutions on NHWC maps (_HipConv3x3), operands cast to bf16 (autocast runs
         the nearest upsampling of the pyramid inputs in fp32)."""
         return _HipConv3x3.apply(x.to(torch.bfloat16), w, b)
+
+    @staticmethod
+    def corner_score(x4, conv5, a3, a4):
+        """conv5 (fp32) + up4(adjust3) + up2(adjust4) of one corner branch -> (B, fh*fh) fp32 (_HipCornerScore)."""
+        return _HipCornerScore.apply(x4.contiguous(), conv5.weight, conv5.bias, a3, a4)
 
     @staticmethod
     def bn_relu(x, bn):
@@ -1192,7 +1267,14 @@ def head_forward_nhwc(hd, x, ops):
         x3 = block(g("conv3"), up(block(g("adjust1"), xh), 2) + up(x2, 2))
         x4 = block(g("conv4"), up(block(g("adjust2"), xh), 4) + up(x3, 2))
         a3, a4 = g("adjust3"), g("adjust4")
-        sm = c1(g("conv5"), x4) + up(block(a3[2], block(a3[1], block(a3[0], x2))), 4) + up(block(a4[1], block(a4[0], x3)), 2)
+        m3, m4 = block(a3[2], block(a3[1], block(a3[0], x2))), block(a4[1], block(a4[0], x3))
+        score = getattr(ops, "corner_score", None)
+        if score is not None and HEAD_SCORE_FP32 and m3.dtype == torch.bfloat16 and m4.dtype == torch.bfloat16:
+            fh = x4.shape[1]
+            sm = score(x4, g("conv5"), m3, m4).view(-1, 1, fh, fh)  # (B, 1, fh, fh) fp32
+            coords += list(_soft_argmax(sm, hd.stride))
+            continue
+        sm = c1(g("conv5"), x4) + up(m3, 4) + up(m4, 2)
         coords += list(_soft_argmax(nchw(sm), hd.stride))
     return torch.stack(coords, dim=1) / hd.img_sz
 

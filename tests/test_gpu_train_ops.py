@@ -279,13 +279,18 @@ def test_module_forward_training_gpu_grads(variant, B):
     actors/mixformer_rgbt.py:82-98): net(t, o, s, gt_bboxes=...) on the HIP ops (bf16) at the bench
     shapes, B = 2 (head BatchNorms in eval mode) and B = 16 (the config-4 batch, BatchNorms in train mode:
     batch statistics on the HIP batch norm).  Box loss within 2e-2 of the fp32 stand-in on the CPU, each
-    parameter group's gradient within max(5e-2, 1.5 x the PyTorch-bf16 path's distance from fp32) (relative
-    L2)."""
+    parameter group's gradient within max(3e-2, 1.2 x the PyTorch-bf16 path's distance from fp32) (relative
+    L2).  Round 6: the corner head's output convs x6 (the golden fixtures' gain) instead of x30, whose peaked
+    score maps put torch-bf16 itself 22 % from fp32 (tools/grad_fixture_probe.py, profiles/r06_grad_fixture_probe.jsonl:
+    x6 -> 8-9 %, x2 -> 6-8 %; the floor is the train-mode BatchNorm's batch statistics at B = 16), and a
+    negative control at B = 16: every two-stream Linear weight gradient scaled by 0.9 (mmt_amd.train._weight_grads2)
+    must fail the same check."""
     import sys
     import os
     sys.path.insert(0, os.path.dirname(__file__))
     from test_train import TorchOps
     import mmt_amd.model as M
+    import mmt_amd.train as T
     from mmt_amd.train import box_loss, synthetic_batch
     builders = {"rgbt": M.build_mixformer_vit_rgbt, "shared": M.build_mixformer_vit_rgbt_shared,
                 "asym": M.build_asymmetric_shared}
@@ -293,7 +298,7 @@ def test_module_forward_training_gpu_grads(variant, B):
     net = builders[variant](M.hot_path_cfg(), train=False)
     with torch.no_grad():
         for br in ("tl", "br"):
-            getattr(net.box_head, "conv5_" + br).weight.mul_(30.0)
+            getattr(net.box_head, "conv5_" + br).weight.mul_(6.0)
         # The deformable encoder's default init (zero offset weights, integer grid bias) samples exactly on pixel
         # centres, where the bilinear location gradient is discontinuous: an ulp of difference anywhere upstream
         # then flips the branch and moves the gradients ~0.65 (relative L2) in either direction (DESIGN.md §7,
@@ -326,17 +331,30 @@ def test_module_forward_training_gpu_grads(variant, B):
     print("%s loss hip %.5f torch-bf16 %.5f fp32 %.5f" % (variant, hip_loss, tb_loss, ref_loss))
     assert abs(hip_loss - ref_loss) <= 2e-2
     groups = ("backbone_v", "backbone_i", "fusion_vi", "box_head") if variant == "rgbt" else ("backbone", "fusion_vi", "box_head")
-    bad = []
-    for grp in groups:
-        names = [n for n in ref if n.startswith(grp + ".")]
-        r = torch.cat([ref[n].flatten() for n in names])
-        g = torch.cat([hip[n].flatten() for n in names])
-        b = torch.cat([tb[n].flatten() for n in names])
-        rel, rel_tb = ((g - r).norm() / r.norm()).item(), ((b - r).norm() / r.norm()).item()
-        print("%s %s grad rel L2: hip %.3g, torch-bf16 %.3g" % (variant, grp, rel, rel_tb))
-        if rel > max(5e-2, 1.5 * rel_tb):
-            bad.append((grp, rel, rel_tb))
+
+    def check(grads, tag):
+        bad = []
+        for grp in groups:
+            names = [n for n in ref if n.startswith(grp + ".")]
+            r = torch.cat([ref[n].flatten() for n in names])
+            g = torch.cat([grads[n].flatten() for n in names])
+            b = torch.cat([tb[n].flatten() for n in names])
+            rel, rel_tb = ((g - r).norm() / r.norm()).item(), ((b - r).norm() / r.norm()).item()
+            print("%s %s %s grad rel L2: %.3g, torch-bf16 %.3g" % (variant, tag, grp, rel, rel_tb))
+            if rel > max(3e-2, 1.2 * rel_tb):
+                bad.append((grp, rel, rel_tb))
+        return bad
+
+    bad = check(hip, "hip")
     assert not bad, bad
+    if variant == "rgbt" and B == 16:  # negative control: a 10 % weight-gradient error is flagged
+        orig = T._weight_grads2
+        T._weight_grads2 = lambda *a, **k: [(dw * 0.9, db * 0.9) for dw, db in orig(*a, **k)]
+        try:
+            _, neg = run(None, "cuda")
+        finally:
+            T._weight_grads2 = orig
+        assert check(neg, "dW x0.9"), "the perturbed weight gradients passed the check"
 
 
 @pytest.mark.parametrize("max_norm", [0.0, 0.1, 1e6])
@@ -759,6 +777,62 @@ def test_hip_conv3x3_autograd(B, H, Cin, Cout):
     for name, a, r, tol in (("y", yd, yr, 1e-2), ("dx", xd.grad, xr.grad, 2e-2), ("dw", wd.grad, wr.grad, 2e-2),
                             ("db", bd.grad, br.grad, 2e-2)):
         a = a.detach().float().cpu()
+        assert a.shape == r.shape, (name, a.shape, r.shape)
+        err = ((a - r).norm() / r.norm()).item()
+        assert err <= tol, (name, err)
+
+
+@pytest.mark.parametrize("B,fh,c4", [(16, 80, 48), (3, 80, 48), (2, 96, 48), (1, 16, 8)])
+def test_hip_corner_score_autograd(B, fh, c4):
+    """HipOps.corner_score (_HipCornerScore: one corner branch's conv5 in fp32 + up4(adjust3) + up2(adjust4),
+    head.py:191-192) against the aten path it replaces (F.linear in fp32 + F.interpolate + adds) under fp32
+    autograd, on the same bf16 inputs; the adjust maps as the HIP BatchNorm leaves them (1-channel views of
+    8-channel rows).  Score map within 1e-5 (relative L2; fp32 sums in another order); dX4 / dA3 / dA4 within
+    1e-2 (bf16 results); dW5 / db5 within 1e-5; the backward bitwise repeatable (fixed-order reductions)."""
+    import torch.nn.functional as F
+    from mmt_amd.train import HipOps
+    g = torch.Generator().manual_seed(B + fh + c4)
+    x4 = torch.randn(B, fh, fh, c4, generator=g).bfloat16()
+    pad3 = torch.randn(B, fh // 4, fh // 4, 8, generator=g).bfloat16()
+    pad4 = torch.randn(B, fh // 2, fh // 2, 8, generator=g).bfloat16()
+    conv5 = torch.nn.Conv2d(c4, 1, 1)
+    with torch.no_grad():
+        conv5.weight.mul_(30.0)
+    dsm = torch.randn(B, fh * fh, generator=g)
+
+    def aten(x, a3, a4, w, b):
+        sm = F.linear(x.float().reshape(-1, c4), w.view(1, -1), b).view(B, fh, fh, 1)
+        up = lambda t, f: F.interpolate(t.float().permute(0, 3, 1, 2), scale_factor=f).permute(0, 2, 3, 1)  # noqa: E731
+        return (sm + up(a3, 4) + up(a4, 2)).reshape(B, fh * fh)
+
+    xr = x4.float().requires_grad_(True)
+    a3r = pad3[..., :1].float().requires_grad_(True)
+    a4r = pad4[..., :1].float().requires_grad_(True)
+    wr = conv5.weight.detach().clone().requires_grad_(True)
+    br = conv5.bias.detach().clone().requires_grad_(True)
+    ref = aten(xr, a3r, a4r, wr, br)
+    ref.backward(dsm)
+
+    conv = conv5.cuda()
+    xd = x4.cuda().requires_grad_(True)
+    p3, p4 = pad3.cuda().requires_grad_(True), pad4.cuda().requires_grad_(True)
+
+    def run():
+        for t in (xd, p3, p4, conv.weight, conv.bias):
+            t.grad = None
+        out = HipOps.corner_score(xd, conv, p3[..., :1], p4[..., :1])
+        out.backward(dsm.cuda())
+        torch.cuda.synchronize()
+        return [t.detach().float().cpu().clone() for t in (out, xd.grad, p3.grad[..., :1], p4.grad[..., :1],
+                                                            conv.weight.grad, conv.bias.grad)]
+
+    got = run()
+    again = run()
+    for a, b in zip(got, again):
+        assert torch.equal(a, b)
+    assert p3.grad[..., 1:].abs().max().item() == 0.0 and p4.grad[..., 1:].abs().max().item() == 0.0
+    for name, a, r, tol in (("sm", got[0], ref.detach(), 1e-5), ("dx4", got[1], xr.grad, 1e-2), ("da3", got[2], a3r.grad, 1e-2),
+                            ("da4", got[3], a4r.grad, 1e-2), ("dw5", got[4], wr.grad, 1e-5), ("db5", got[5], br.grad, 1e-5)):
         assert a.shape == r.shape, (name, a.shape, r.shape)
         err = ((a - r).norm() / r.norm()).item()
         assert err <= tol, (name, err)

@@ -15,11 +15,15 @@ import statistics
 import sys
 
 
-def per_step(path, counter):
+def per_step(path, counter, family=None):
+    """(launches, counter sum) of every step; family: only kernels whose name contains it (the dominant
+    training family, "gemm")."""
     rows = [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == counter]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
     ends = [i for i, r in enumerate(rows) if "adamw_step_kernel" in r["Kernel_Name"]]
-    steps = [(b - a, sum(float(r["Counter_Value"]) for r in rows[a + 1:b + 1])) for a, b in zip(ends, ends[1:])]
+    sel = (lambda r: True) if family is None else (lambda r: family in r["Kernel_Name"])
+    steps = [(sum(1 for r in rows[a + 1:b + 1] if sel(r)), sum(float(r["Counter_Value"]) for r in rows[a + 1:b + 1] if sel(r)))
+             for a, b in zip(ends, ends[1:])]
     return steps
 
 
@@ -27,12 +31,13 @@ def main():
     out = sys.argv[1]
     B = int(sys.argv[2]) if len(sys.argv) > 2 else 16
     dst = sys.argv[3] if len(sys.argv) > 3 else os.path.join(os.path.dirname(__file__), "..", "profiles", "pmc_traffic.json")
-    vals = {}
+    vals, gvals = {}, {}
     for f in glob.glob(os.path.join(out, "p*", "**", "*counter_collection.csv"), recursive=True):
         names = {r["Counter_Name"] for r in csv.DictReader(open(f))}
         for c in ("FETCH_SIZE", "WRITE_SIZE"):
             if c in names:
                 vals[c] = per_step(f, c)
+                gvals[c] = per_step(f, c, "gemm")
     if len(vals) != 2:
         sys.exit("FETCH_SIZE / WRITE_SIZE passes not found under %s" % out)
     fb = 2 * statistics.median(v for _, v in vals["FETCH_SIZE"]) * 1024
@@ -40,8 +45,12 @@ def main():
     launches = statistics.median(n for n, _ in vals["FETCH_SIZE"])
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "multi-modal-tracking_amd"))
     from mmt_amd.stamp import source_digest
+    gfb = 2 * statistics.median(v for _, v in gvals["FETCH_SIZE"]) * 1024
+    gwb = statistics.median(v for _, v in gvals["WRITE_SIZE"]) * 1024
     res = {"step": {"fetch_bytes": round(fb), "write_bytes": round(wb), "traffic_bytes": round(fb + wb),
                     "launches": launches, "steps": len(vals["FETCH_SIZE"])},
+           "gemm": {"fetch_bytes": round(gfb), "write_bytes": round(gwb), "traffic_bytes": round(gfb + gwb),
+                    "launches": statistics.median(n for n, _ in gvals["FETCH_SIZE"])},
            "_stamp": {"source_digest": source_digest(train=True), "git_head": os.environ.get("MMT_GIT_HEAD", "")}}
     try:
         allres = json.load(open(dst))
