@@ -386,14 +386,14 @@ int mmt_corner_softargmax(const void* x4, const float* w5, const float* b5, cons
  * score_map[b][p] fp32 = (x4[b][p] . w5 + b5) + a3[b][up4(p)] + a4[b][up2(p)]: x4 bf16 [B][fh*fh][c4] (NHWC
  * rows, c4 % 8 == 0), w5 [c4] / b5 [1] fp32 (conv5 in fp32), a3 / a4 bf16 1-channel maps of (fh/4)^2 /
  * (fh/2)^2 pixels at pixel strides s3 / s4 (elements).  The backward writes dx4 bf16 [B][fh*fh][c4], da3 /
- * da4 bf16 contiguous, dw5 [c4] / db5 [1] fp32 (deterministic: fixed-order partial sums through ws, which
+ * da4 bf16 rows of p3 / p4 channels (1..8: channel 0 the gradient, the padding channels 0), dw5 [c4] / db5 [1] fp32 (deterministic: fixed-order partial sums through ws, which
  * holds mmt_corner_score_train_ws_floats(B, fh, c4) floats); fh <= 128, c4 < 64.  Replaces the reference
  * path's Conv2d(48, 1, 1) + two F.interpolate + adds (and aten's / hipBLASLt's kernels for them). */
 int mmt_corner_score_train(const void* x4, const float* w5, const float* b5, const void* a3, int64_t s3,
                            const void* a4, int64_t s4, float* score_map, int B, int fh, int c4, void* stream);
 int64_t mmt_corner_score_train_ws_floats(int B, int fh, int c4);
-int mmt_corner_score_train_bwd(const float* dsm, const void* x4, const float* w5, void* dx4, void* da3, void* da4,
-                               float* dw5, float* db5, float* ws, int B, int fh, int c4, void* stream);
+int mmt_corner_score_train_bwd(const float* dsm, const void* x4, const float* w5, void* dx4, void* da3, int p3,
+                               void* da4, int p4, float* dw5, float* db5, float* ws, int B, int fh, int c4, void* stream);
 
 /* PrRoIPool2D forward.  features fp32 with strides (batch, channel, y, x) in elements, rois
  * [R][5] = (batch, x0, y0, x1, y1); out element (r, c, ph, pw) at r*o_r + c*o_c + (ph*pw_+pw)*o_p
@@ -467,6 +467,14 @@ int mmt_transpose_bf16(const void* in, void* out, int rows, int cols, int64_t ld
  * the corner head's weight gradients in the training step (dW = dY^T im2col(X), one GEMM over pixels;
  * replaces the autograd of nn.Conv2d 3x3 in lib/models/mixformer_cvt/head.py:7-20). */
 int mmt_im2col3x3_bf16(const void* in, void* out, int B, int H, int W, int C, void* stream);
+/* The same of the nearest-upsampled (x up: 1, 2, 4 or 8) map of in [B][H/up][W/up][C]; H, W the upsampled sizes
+ * (the training head's upsampling folded into its convolutions, head.py:187-189). */
+int mmt_im2col3x3_up_bf16(const void* in, void* out, int B, int H, int W, int C, int up, void* stream);
+/* Backward of nearest upsampling x up on NHWC bf16: out [B][Hi][Wi][C] = the up x up block sums of in
+ * [B][Hi*up][Wi*up][C] (fp32 sums in a fixed order, bf16 out). */
+int mmt_upsample_sum_bf16(const void* in, void* out, int B, int Hi, int Wi, int C, int up, void* stream);
+/* out [B][H][W][C] = bf16(up(a) + b), a [B][H/up][W/up][C], NHWC bf16 (the pyramid add up2(adjust2) + x3). */
+int mmt_add_up_bf16(const void* a, const void* b, void* out, int B, int H, int W, int C, int up, void* stream);
 
 /* BatchNorm2d (+ ReLU) of the corner head's conv() blocks in the training step (nn.BatchNorm2d -> nn.ReLU,
  * lib/models/mixformer_cvt/head.py:7-20) on an NHWC bf16 map x [M = B*H*W][pitch] with C valid channels

@@ -154,8 +154,8 @@ __global__ __launch_bounds__(256) void corner_score_train_kernel(const bf16_t* _
 // deterministic, no atomics.  corner_score_train_fin_kernel sums the bands in order.
 __global__ __launch_bounds__(512) void corner_score_train_bwd_kernel(const float* __restrict__ dsm, const bf16_t* __restrict__ x4,
                                                                      const float* __restrict__ w5, bf16_t* __restrict__ dx4,
-                                                                     bf16_t* __restrict__ da3, bf16_t* __restrict__ da4,
-                                                                     float* __restrict__ part, int B, int fh, int c4) {
+                                                                     bf16_t* __restrict__ da3, int p3, bf16_t* __restrict__ da4,
+                                                                     int p4, float* __restrict__ part, int B, int fh, int c4) {
     __shared__ float sd[4 * 128];       // the band's dsm (fh <= 128)
     __shared__ float red[8][64 + 1];    // per-group partial sums of each channel (c4 <= 64) and the bias
     const int np = fh * fh, bands = fh / 4, band = blockIdx.x;
@@ -190,7 +190,9 @@ __global__ __launch_bounds__(512) void corner_score_train_bwd_kernel(const float
             for (int dy = 0; dy < 4; ++dy)
 #pragma unroll
                 for (int dx = 0; dx < 4; ++dx) acc += sd[dy * fh + 4 * t + dx];
-            da3[(int64_t)b * f4 * f4 + (r0 / 4) * f4 + t] = f2bf(acc);
+            bf16_t* o = da3 + ((int64_t)b * f4 * f4 + (r0 / 4) * f4 + t) * p3;  // channel 0, padding channels 0
+            o[0] = f2bf(acc);
+            for (int j = 1; j < p3; ++j) o[j] = 0;
         } else {
             const int u = t - f4, ry = u / f2, cx = u - ry * f2;
             float acc = 0.f;
@@ -198,7 +200,9 @@ __global__ __launch_bounds__(512) void corner_score_train_bwd_kernel(const float
             for (int dy = 0; dy < 2; ++dy)
 #pragma unroll
                 for (int dx = 0; dx < 2; ++dx) acc += sd[(2 * ry + dy) * fh + 2 * cx + dx];
-            da4[(int64_t)b * f2 * f2 + (r0 / 2 + ry) * f2 + cx] = f2bf(acc);
+            bf16_t* o = da4 + ((int64_t)b * f2 * f2 + (r0 / 2 + ry) * f2 + cx) * p4;
+            o[0] = f2bf(acc);
+            for (int j = 1; j < p4; ++j) o[j] = 0;
         }
     }
     __syncthreads();
@@ -652,15 +656,16 @@ extern "C" int64_t mmt_corner_score_train_ws_floats(int B, int fh, int c4) {
     return (int64_t)B * (fh / 4) * (c4 + 1);
 }
 
-extern "C" int mmt_corner_score_train_bwd(const float* dsm, const void* x4, const float* w5, void* dx4, void* da3, void* da4,
-                                          float* dw5, float* db5, float* ws, int B, int fh, int c4, void* stream) {
+extern "C" int mmt_corner_score_train_bwd(const float* dsm, const void* x4, const float* w5, void* dx4, void* da3, int p3,
+                                          void* da4, int p4, float* dw5, float* db5, float* ws, int B, int fh, int c4,
+                                          void* stream) {
     if (!dsm || !x4 || !w5 || !dx4 || !da3 || !da4 || !dw5 || !db5 || !ws || B <= 0 || fh <= 0 || fh % 4 || fh > 128 ||
-        c4 <= 0 || c4 % 8 || c4 > 63)
+        c4 <= 0 || c4 % 8 || c4 > 63 || p3 < 1 || p3 > 8 || p4 < 1 || p4 > 8)
         return MMT_EBADARG;
     hipStream_t st = (hipStream_t)stream;
     const int nb = B * (fh / 4);
     hipLaunchKernelGGL(corner_score_train_bwd_kernel, dim3(nb), dim3(512), 0, st, dsm, (const bf16_t*)x4, w5, (bf16_t*)dx4,
-                       (bf16_t*)da3, (bf16_t*)da4, ws, B, fh, c4);
+                       (bf16_t*)da3, p3, (bf16_t*)da4, p4, ws, B, fh, c4);
     hipLaunchKernelGGL(corner_score_train_fin_kernel, dim3(1), dim3(64), 0, st, ws, dw5, db5, nb, c4);
     return launch_status();
 }

@@ -88,10 +88,12 @@ extern "C" int mmt_transpose_bf16(const void* in, void* out, int rows, int cols,
 // out[(b, y, x)][(ky * 3 + kx) * C + c] = in[b][y + ky - 1][x + kx - 1][c], 0 outside the map -- the A
 // operand layout of the implicit-GEMM conv (k = (ky * 3 + kx) * C + ci), materialised so that
 // dW = dY^T im2col(X) is one GEMM contracting over pixels.  One thread per 16 B (8 channels): coalesced
-// 16-B loads and stores, HBM-bound (9 x the map written, the map read ~9 x from L2).
+// 16-B loads and stores, HBM-bound (9 x the map written, the map read ~9 x from L2).  UP: the conv's input is
+// the nearest-upsampled (x UP, a power of two) map of in [B][H/UP][W/UP][C] -- H, W are the upsampled sizes:
+// the pixel (yy, xx) reads in[yy / UP][xx / UP] (round 6: the head's upsampling folded into the convs).
 namespace {
 __global__ __launch_bounds__(256) void im2col3x3_kernel(const u32x4* __restrict__ in, u32x4* __restrict__ out, int H,
-                                                         int W, int c8, int64_t total) {
+                                                         int W, int c8, int64_t total, int up_sh) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (pixel, tap, chunk)
     if (i >= total) return;
     const int ch = (int)(i % c8);
@@ -101,11 +103,97 @@ __global__ __launch_bounds__(256) void im2col3x3_kernel(const u32x4* __restrict_
     const int x = (int)(pix % W), y = (int)((pix / W) % H);
     const int64_t b = pix / ((int64_t)W * H);
     const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
+    const int hi = H >> up_sh, wi = W >> up_sh;
     u32x4 v = u32x4{0u, 0u, 0u, 0u};
-    if (yy >= 0 && yy < H && xx >= 0 && xx < W) v = in[((b * H + yy) * W + xx) * c8 + ch];
+    if (yy >= 0 && yy < H && xx >= 0 && xx < W) v = in[((b * hi + (yy >> up_sh)) * wi + (xx >> up_sh)) * c8 + ch];
     out[i] = v;
 }
+
+// Backward of nearest upsampling x UP on NHWC bf16: out[b][y][x][c] = bf16(sum over the UP x UP block of
+// in[b][UP y + dy][UP x + dx][c]) (fp32 sums, rows then columns: a fixed order); one thread per 8 channels
+__global__ __launch_bounds__(256) void upsample_sum_kernel(const u32x4* __restrict__ in, u32x4* __restrict__ out, int Hi,
+                                                            int Wi, int c8, int up, int64_t total) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (low-res pixel, chunk)
+    if (i >= total) return;
+    const int ch = (int)(i % c8);
+    const int64_t pix = i / c8;
+    const int x = (int)(pix % Wi), y = (int)((pix / Wi) % Hi);
+    const int64_t b = pix / ((int64_t)Wi * Hi);
+    const int W = Wi * up, H = Hi * up;
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    for (int dy = 0; dy < up; ++dy)
+        for (int dx = 0; dx < up; ++dx) {
+            const u32x4 v = in[((b * H + (int64_t)y * up + dy) * W + (int64_t)x * up + dx) * c8 + ch];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                acc[2 * j] += __uint_as_float(v[j] << 16);
+                acc[2 * j + 1] += __uint_as_float(v[j] & 0xffff0000u);
+            }
+        }
+    u32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(acc[2 * j], acc[2 * j + 1]);
+    out[i] = o;
+}
+
+// out = bf16(up(a) + b) on NHWC bf16 maps: a [B][H/UP][W/UP][C], b / out [B][H][W][C] (fp32 add): the corner
+// head's pyramid input x4 = up2(adjust2) + x3 (head.py:189), before the conv that upsamples it once more
+__global__ __launch_bounds__(256) void add_up_kernel(const u32x4* __restrict__ a, const u32x4* __restrict__ bm,
+                                                      u32x4* __restrict__ out, int H, int W, int c8, int up_sh,
+                                                      int64_t total) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (pixel, chunk)
+    if (i >= total) return;
+    const int ch = (int)(i % c8);
+    const int64_t pix = i / c8;
+    const int x = (int)(pix % W), y = (int)((pix / W) % H);
+    const int64_t b = pix / ((int64_t)W * H);
+    const u32x4 va = a[((b * (H >> up_sh) + (y >> up_sh)) * (W >> up_sh) + (x >> up_sh)) * c8 + ch], vb = bm[i];
+    u32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        o[j] = pack_bf16x2(__uint_as_float(va[j] << 16) + __uint_as_float(vb[j] << 16),
+                           __uint_as_float(va[j] & 0xffff0000u) + __uint_as_float(vb[j] & 0xffff0000u));
+    out[i] = o;
+}
 }  // namespace
+
+static int up_shift(int up) {
+    return up == 1 ? 0 : up == 2 ? 1 : up == 4 ? 2 : up == 8 ? 3 : -1;
+}
+
+extern "C" int mmt_im2col3x3_up_bf16(const void* in, void* out, int B, int H, int W, int C, int up, void* stream) {
+    const int sh = up_shift(up);
+    if (!in || !out || B <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 8 || sh < 0 || H % up || W % up) return MMT_EBADARG;
+    if (((uintptr_t)in | (uintptr_t)out) & 15) return MMT_EBADARG;
+    const int c8 = C / 8;
+    const int64_t total = (int64_t)B * H * W * 9 * c8;
+    hipLaunchKernelGGL(im2col3x3_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const u32x4*)in, (u32x4*)out, H, W, c8, total, sh);
+    return launch_status();
+}
+
+extern "C" int mmt_upsample_sum_bf16(const void* in, void* out, int B, int Hi, int Wi, int C, int up, void* stream) {
+    if (!in || !out || B <= 0 || Hi <= 0 || Wi <= 0 || C <= 0 || C % 8 || up_shift(up) < 0) return MMT_EBADARG;
+    if (((uintptr_t)in | (uintptr_t)out) & 15) return MMT_EBADARG;
+    const int c8 = C / 8;
+    const int64_t total = (int64_t)B * Hi * Wi * c8;
+    hipLaunchKernelGGL(upsample_sum_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const u32x4*)in, (u32x4*)out, Hi, Wi, c8, up, total);
+    return launch_status();
+}
+
+extern "C" int mmt_add_up_bf16(const void* a, const void* b, void* out, int B, int H, int W, int C, int up, void* stream) {
+    const int sh = up_shift(up);
+    if (!a || !b || !out || B <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 8 || sh < 0 || H % up || W % up) return MMT_EBADARG;
+    if (((uintptr_t)a | (uintptr_t)b | (uintptr_t)out) & 15) return MMT_EBADARG;
+    const int c8 = C / 8;
+    const int64_t total = (int64_t)B * H * W * c8;
+    hipLaunchKernelGGL(add_up_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const u32x4*)a, (const u32x4*)b, (u32x4*)out, H, W, c8, sh, total);
+    return launch_status();
+}
 
 extern "C" int mmt_im2col3x3_bf16(const void* in, void* out, int B, int H, int W, int C, void* stream) {
     if (!in || !out || B <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 8) return MMT_EBADARG;
@@ -113,6 +201,6 @@ extern "C" int mmt_im2col3x3_bf16(const void* in, void* out, int B, int H, int W
     const int c8 = C / 8;
     const int64_t total = (int64_t)B * H * W * 9 * c8;
     hipLaunchKernelGGL(im2col3x3_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                       (const u32x4*)in, (u32x4*)out, H, W, c8, total);
+                       (const u32x4*)in, (u32x4*)out, H, W, c8, total, 0);
     return launch_status();
 }

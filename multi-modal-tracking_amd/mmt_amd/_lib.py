@@ -88,8 +88,11 @@ _PROTOS = {
     "mmt_conv3x3_c1_pair": [vp, vp, vp, vp, i32, i64, vp, vp, vp, vp, i32, i64, i32, i32, i32, i32, vp],
     "mmt_corner_softargmax": [vp, vp, vp, vp, vp, vp, vp, vp, vp, f32, i32, i32, i32, i32, i32, vp],
     "mmt_corner_score_train": [vp, vp, vp, vp, i64, vp, i64, vp, i32, i32, i32, vp],
+    "mmt_im2col3x3_up_bf16": [vp, vp, i32, i32, i32, i32, i32, vp],
+    "mmt_upsample_sum_bf16": [vp, vp, i32, i32, i32, i32, i32, vp],
+    "mmt_add_up_bf16": [vp, vp, vp, i32, i32, i32, i32, i32, vp],
     "mmt_corner_score_train_ws_floats": [i32, i32, i32],
-    "mmt_corner_score_train_bwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp],
+    "mmt_corner_score_train_bwd": [vp, vp, vp, vp, vp, i32, vp, i32, vp, vp, vp, i32, i32, i32, vp],
     "mmt_prroi_pool_forward": [vp, vp, vp, i32, i32, i32, i32, i64, i64, i64, i64, i32, i32, f32, i64, i64, i64, vp],
     "mmt_prroi_pool_backward": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, f32, vp],
     "mmt_prroi_pool_coor_backward": [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, f32, vp],

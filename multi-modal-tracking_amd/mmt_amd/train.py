@@ -583,10 +583,11 @@ class _HipGroupNorm(torch.autograd.Function):
         return dx, dgb[0], dgb[1], None, None
 
 
-def _conv_gemm(x, wr, B, H, Cin, Cout, bias=None, flip=False):
+def _conv_gemm(x, wr, B, H, Cin, Cout, bias=None, flip=False, up=1):
     """NHWC 3x3 / pad-1 convolution as the implicit-GEMM conv mode of mmt_gemm: y [B*H*H][Cout] bf16 =
     im2col(x) wr^T (+ bias), x [B][H][H][Cin] bf16 (square maps), wr [Cout][(ky*3 + kx)*Cin + ci] bf16;
-    flip: the taps read in reverse order (conv_k3 2: the convolution with the flipped kernel)."""
+    flip: the taps read in reverse order (conv_k3 2: the convolution with the flipped kernel); up: x is
+    [B][H/up][H/up][Cin] and the conv runs on its nearest upsampling (conv_up: the map never materialised)."""
     from ._lib import LIB, GemmParams, MMT_BF16, check
     M = B * H * H
     y = torch.empty(M, Cout, device=x.device, dtype=torch.bfloat16)
@@ -596,10 +597,10 @@ def _conv_gemm(x, wr, B, H, Cin, Cout, bias=None, flip=False):
     p.lda, p.ldc = Cin, Cout
     p.a_seg_rows, p.a_segs_a = M, 1
     p.M, p.N, p.K, p.groups = M, Cout, 9 * Cin, 1
-    p.conv_h, p.conv_up, p.conv_cin, p.conv_k3 = H, 1, Cin, 2 if flip else 1
+    p.conv_h, p.conv_up, p.conv_cin, p.conv_k3 = H, up, Cin, 2 if flip else 1
     check(LIB.mmt_gemm(p, MMT_BF16, _stream()), "mmt_gemm (conv)")
-    # implicit GEMM: the input map is read once (B H H Cin), not the im2col matrix
-    _account(M, Cout, 9 * Cin, 1, 0, 2, 2, M * Cin * 2 + (Cout * 4 if bias is not None else 0))
+    # implicit GEMM: the input map is read once (B (H/up)^2 Cin), not the im2col matrix
+    _account(M, Cout, 9 * Cin, 1, 0, 2, 2, M // (up * up) * Cin * 2 + (Cout * 4 if bias is not None else 0))
     return y
 
 
@@ -661,11 +662,11 @@ class _HipCornerScore(torch.autograd.Function):
         B, fh, _, c4 = x4.shape
         if x4.dtype != torch.bfloat16 or not x4.is_contiguous() or a3.dtype != torch.bfloat16 or a4.dtype != torch.bfloat16:
             raise ValueError("HIP corner score: contiguous bf16 NHWC x4, bf16 adjust maps")
-        if a3.shape != (B, fh // 4, fh // 4, 1) or a4.shape != (B, fh // 2, fh // 2, 1):
+        if a3.shape[:3] != (B, fh // 4, fh // 4) or a4.shape[:3] != (B, fh // 2, fh // 2):
             raise ValueError("HIP corner score: adjust maps of fh/4 and fh/2")
-        for a in (a3, a4):
-            if a.stride(1) != a.stride(2) * a.shape[2] or a.stride(0) != a.stride(1) * a.shape[1]:
-                raise ValueError("HIP corner score: adjust maps must be pixel-strided views")
+        for a in (a3, a4):  # channel 0 of pixel-strided rows: (B, h, w, 1) views, or the padded 8-channel rows
+            if a.shape[3] not in (1, a.stride(2)) or a.stride(1) != a.stride(2) * a.shape[2] or a.stride(0) != a.stride(1) * a.shape[1]:
+                raise ValueError("HIP corner score: adjust maps must be pixel-strided rows")
         w = w5.detach().reshape(-1).float().contiguous()
         b = b5.detach().reshape(-1).float().contiguous()
         out = torch.empty(B, fh * fh, device=x4.device, dtype=torch.float32)
@@ -673,7 +674,7 @@ class _HipCornerScore(torch.autograd.Function):
                                          a4.data_ptr(), a4.stride(2), out.data_ptr(), B, fh, c4, _stream()),
               "mmt_corner_score_train")
         ctx.save_for_backward(x4, w)
-        ctx.wshape = w5.shape
+        ctx.wshape, ctx.c3, ctx.c4 = w5.shape, a3.shape[3], a4.shape[3]
         return out
 
     @staticmethod
@@ -683,13 +684,14 @@ class _HipCornerScore(torch.autograd.Function):
         B, fh, _, c4 = x4.shape
         dsm = dsm.float().contiguous()
         dx4 = torch.empty_like(x4)
-        da3 = torch.empty(B, fh // 4, fh // 4, 1, device=x4.device, dtype=torch.bfloat16)
-        da4 = torch.empty(B, fh // 2, fh // 2, 1, device=x4.device, dtype=torch.bfloat16)
+        # (padded rows: the kernel writes channel 0 and zeroes the padding channels)
+        da3 = torch.empty(B, fh // 4, fh // 4, ctx.c3, device=x4.device, dtype=torch.bfloat16)
+        da4 = torch.empty(B, fh // 2, fh // 2, ctx.c4, device=x4.device, dtype=torch.bfloat16)
         dw = torch.empty(c4 + 1, device=x4.device, dtype=torch.float32)
         ws = torch.empty(int(LIB.mmt_corner_score_train_ws_floats(B, fh, c4)), device=x4.device, dtype=torch.float32)
         check(LIB.mmt_corner_score_train_bwd(dsm.data_ptr(), x4.data_ptr(), w.data_ptr(), dx4.data_ptr(), da3.data_ptr(),
-                                             da4.data_ptr(), dw.data_ptr(), dw[c4:].data_ptr(), ws.data_ptr(), B, fh, c4,
-                                             _stream()), "mmt_corner_score_train_bwd")
+                                             ctx.c3, da4.data_ptr(), ctx.c4, dw.data_ptr(), dw[c4:].data_ptr(),
+                                             ws.data_ptr(), B, fh, c4, _stream()), "mmt_corner_score_train_bwd")
         return dx4, dw[:c4].view(ctx.wshape), dw[c4:], da3, da4
 
 
@@ -700,14 +702,19 @@ class _HipConv3x3(torch.autograd.Function):
     swapped), dW and the bias
     gradient as one GEMM over pixels against the im2col of X (mmt_im2col3x3_bf16; `_weight_grads`).  Replaces
     MIOpen's igemm forward / backward-data / backward-weights kernels, whose backward did not replay
-    correctly from a captured hipGraph."""
+    correctly from a captured hipGraph.
+    up (round 6): the conv of the nearest upsampling (x up) of x, the map never materialised (forward: the GEMM's
+    conv_up addressing; dX: the flipped conv at the upsampled size, then the up x up block sums,
+    mmt_upsample_sum_bf16; dW: im2col of the upsampled map, mmt_im2col3x3_up_bf16).  keep_pad: Cout < 8 outputs
+    stay in their 8-channel rows (padding channels 0) for the next HIP op, instead of a sliced view whose
+    backward zero-fills and copies."""
 
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, up=1, keep_pad=False):
         B, H, W, Cin = x.shape
         Cout = w.shape[0]
-        if H != W or Cin % 8 or w.shape[2:] != (3, 3) or x.dtype != torch.bfloat16:
-            raise ValueError("HIP conv3x3: square NHWC bf16 maps, input channels multiple of 8, 3x3 kernels")
+        if H != W or Cin % 8 or w.shape[2:] != (3, 3) or x.dtype != torch.bfloat16 or up not in (1, 2, 4):
+            raise ValueError("HIP conv3x3: square NHWC bf16 maps, input channels multiple of 8, 3x3 kernels, up 1/2/4")
         Cp = (Cout + 7) // 8 * 8  # output channels padded to the GEMM's N granule (the 48 -> 1 adjust convs)
         x = x.contiguous()
         wr = torch.empty(Cp, 3, 3, Cin, device=x.device, dtype=torch.bfloat16)  # [Cout][ky][kx][Cin]: one cast copy
@@ -716,23 +723,27 @@ class _HipConv3x3(torch.autograd.Function):
         if Cp != Cout:
             wr[Cout:].zero_()
             bp = F.pad(bp, (0, Cp - Cout))
-        y = _conv_gemm(x, wr.view(Cp, 9 * Cin), B, H, Cin, Cp, bias=bp)
+        Ho = H * up
+        y = _conv_gemm(x, wr.view(Cp, 9 * Cin), B, Ho, Cin, Cp, bias=bp, up=up)
         ctx.save_for_backward(x, w)
-        y = y.view(B, H, W, Cp)
-        return y if Cp == Cout else y[..., :Cout]
+        ctx.up = up
+        y = y.view(B, Ho, Ho, Cp)
+        return y if (Cp == Cout or keep_pad) else y[..., :Cout]
 
     @staticmethod
     def backward(ctx, dy):
         from ._lib import LIB, check
         x, w = ctx.saved_tensors
+        up = ctx.up
         B, H, W, Cin = x.shape
+        Ho = H * up
         Cout = w.shape[0]
         Cp = (Cout + 7) // 8 * 8
-        if Cp != Cout:
-            dyp = torch.zeros(B, H, W, Cp, device=dy.device, dtype=torch.bfloat16)
+        if dy.shape[-1] != Cp:  # a sliced output: back to the padded rows
+            dyp = torch.zeros(B, Ho, Ho, Cp, device=dy.device, dtype=torch.bfloat16)
             dyp[..., :Cout] = dy
             dy = dyp
-        else:
+        else:  # padded rows (keep_pad): the padding channels' gradient multiplies zero weights
             dy = dy.to(torch.bfloat16).contiguous()
         dx = None
         if ctx.needs_input_grad[0]:  # the flipped-tap conv of dY with W as [Cin][ky][kx][Cout] (no flip copy)
@@ -740,13 +751,52 @@ class _HipConv3x3(torch.autograd.Function):
             wt[..., :Cout].copy_(w.detach().permute(1, 2, 3, 0))
             if Cp != Cout:
                 wt[..., Cout:].zero_()
-            dx = _conv_gemm(dy, wt.view(Cin, 9 * Cp), B, H, Cp, Cin, flip=True).view(B, H, W, Cin)
-        M = B * H * W
+            dxu = _conv_gemm(dy, wt.view(Cin, 9 * Cp), B, Ho, Cp, Cin, flip=True).view(B, Ho, Ho, Cin)
+            if up == 1:
+                dx = dxu
+            else:
+                dx = torch.empty_like(x)
+                check(LIB.mmt_upsample_sum_bf16(dxu.data_ptr(), dx.data_ptr(), B, H, W, Cin, up, _stream()),
+                      "mmt_upsample_sum_bf16")
+        M = B * Ho * Ho
         col = torch.empty(M, 9 * Cin, device=x.device, dtype=torch.bfloat16)
-        check(LIB.mmt_im2col3x3_bf16(x.data_ptr(), col.data_ptr(), B, H, W, Cin, _stream()), "mmt_im2col3x3_bf16")
+        if up == 1:
+            check(LIB.mmt_im2col3x3_bf16(x.data_ptr(), col.data_ptr(), B, H, W, Cin, _stream()), "mmt_im2col3x3_bf16")
+        else:
+            check(LIB.mmt_im2col3x3_up_bf16(x.data_ptr(), col.data_ptr(), B, Ho, Ho, Cin, up, _stream()),
+                  "mmt_im2col3x3_up_bf16")
         dw, db = _weight_grads(dy.view(M, Cp), col, M, Cp, 9 * Cin)
         dw = dw[:Cout].view(Cout, 3, 3, Cin).permute(0, 3, 1, 2).contiguous()
-        return dx, dw, db[:Cout].contiguous()
+        return dx, dw, db[:Cout].contiguous(), None, None
+
+
+class _HipAddUp(torch.autograd.Function):
+    """bf16(up(a) + b) on NHWC bf16 maps (mmt_add_up_bf16; up 1 = a plain add): the corner head's pyramid adds
+    (head.py:187-189) at the lower of their two resolutions; backward: db = dout, da = its up x up block sums."""
+
+    @staticmethod
+    def forward(ctx, a, b, up):
+        from ._lib import LIB, check
+        B, H, W, C = b.shape
+        if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or a.shape != (B, H // up, W // up, C):
+            raise ValueError("HIP add_up: bf16 NHWC maps, a at 1/up of b")
+        a, b = a.contiguous(), b.contiguous()
+        out = torch.empty_like(b)
+        check(LIB.mmt_add_up_bf16(a.data_ptr(), b.data_ptr(), out.data_ptr(), B, H, W, C, up, _stream()), "mmt_add_up_bf16")
+        ctx.up, ctx.ashape = up, a.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        from ._lib import LIB, check
+        dout = dout.to(torch.bfloat16).contiguous()
+        if ctx.up == 1:
+            return dout, dout, None
+        B, H, W, C = dout.shape
+        da = torch.empty(ctx.ashape, device=dout.device, dtype=torch.bfloat16)
+        check(LIB.mmt_upsample_sum_bf16(dout.data_ptr(), da.data_ptr(), B, H // ctx.up, W // ctx.up, C, ctx.up, _stream()),
+              "mmt_upsample_sum_bf16")
+        return da, dout, None
 
 
 def _adjust_tokens(ops, seq, tok):
@@ -861,10 +911,16 @@ class HipOps:
         return asym_attention_from_mam(HipOps.mam_attention, qkv, Bh, n_t, heads)
 
     @staticmethod
-    def conv3x3(x, w, b):
+    def conv3x3(x, w, b, up=1, keep_pad=False):
         """The corner head's 3x3 convolutions on NHWC maps (_HipConv3x3), operands cast to bf16 (autocast runs
-        the nearest upsampling of the pyramid inputs in fp32)."""
-        return _HipConv3x3.apply(x.to(torch.bfloat16), w, b)
+        the nearest upsampling of the pyramid inputs in fp32); up: of the nearest upsampling of x (not
+        materialised); keep_pad: 1-channel outputs in their 8-channel rows."""
+        return _HipConv3x3.apply(x.to(torch.bfloat16), w, b, up, keep_pad)
+
+    @staticmethod
+    def add_up(a, b, up):
+        """bf16(up(a) + b) on NHWC bf16 maps (_HipAddUp)."""
+        return _HipAddUp.apply(a, b, up)
 
     @staticmethod
     def corner_score(x4, conv5, a3, a4):
@@ -877,25 +933,27 @@ class HipOps:
         eval semantics: batch statistics when training or not tracking, running statistics updated (and
         num_batches_tracked advanced) when training and tracking."""
         if isinstance(bn, FrozenBatchNorm2d):  # fixed statistics and affine (buffers): eval semantics
-            C = x.shape[-1]
+            C = bn.weight.shape[0]
             x = x.to(torch.bfloat16)
-            if C % 8:
+            padded = x.shape[-1] != C  # 8-channel rows in: padded rows out
+            if not padded and C % 8:
                 x = F.pad(x, (0, (C + 7) // 8 * 8 - C))
             y = _HipBatchNormReLU.apply(x.contiguous(), bn.weight, bn.bias, bn.running_mean, bn.running_var, 0.0,
                                         bn.eps, False, C)
-            return y if y.shape[-1] == C else y[..., :C]
+            return y if (padded or y.shape[-1] == C) else y[..., :C]
         training = bn.training or not bn.track_running_stats
         update = bn.training and bn.track_running_stats
         if update:
             bn.num_batches_tracked.add_(1)
         keep = update or not training
-        C = x.shape[-1]
+        C = bn.num_features
         x = x.to(torch.bfloat16)
-        if C % 8:  # the 1-channel maps: 8-channel rows, padding channels ignored (autograd slices dy back)
+        padded = x.shape[-1] != C  # 8-channel rows in (a keep_pad conv): padded rows out, padding channels 0
+        if not padded and C % 8:  # the 1-channel maps: 8-channel rows, padding channels ignored (autograd slices dy back)
             x = F.pad(x, (0, (C + 7) // 8 * 8 - C))
         y = _HipBatchNormReLU.apply(x.contiguous(), bn.weight, bn.bias, bn.running_mean if keep else None,
                                     bn.running_var if keep else None, bn.momentum, bn.eps, training, C)
-        return y if y.shape[-1] == C else y[..., :C]
+        return y if (padded or y.shape[-1] == C) else y[..., :C]
 
     @staticmethod
     def ms_deform_attn(value, hw, loc, aw):
@@ -1260,15 +1318,32 @@ def head_forward_nhwc(hd, x, ops):
 
     xh = nhwc(x).to(torch.bfloat16).contiguous()
     coords = []
+    score, add_up = getattr(ops, "corner_score", None), getattr(ops, "add_up", None)
+    fused = score is not None and add_up is not None and HEAD_SCORE_FP32 and bn_relu is not None
     for br in ("tl", "br"):
         g = lambda n: getattr(hd, n + "_" + br)  # noqa: E731
         x1 = block(g("conv1"), xh)
         x2 = block(g("conv2"), x1)
+        a3, a4 = g("adjust3"), g("adjust4")
+        if fused and all(_hip_bn_ok(m[1]) and type(m[2]) is torch.nn.ReLU
+                         for m in (g("conv3"), g("conv4"), a3[2], a4[1])):
+            # round 6: the pyramid's nearest upsamplings folded into the convolutions that consume them (exact:
+            # nearest upsampling commutes with the add of two maps at one resolution, and rounding the fp32 sum to
+            # bf16 before or after upsampling gives the same values), the adds on HIP, the 1-channel maps kept in
+            # their 8-channel rows, and conv5 + up4(adjust3) + up2(adjust4) in one HIP op
+            def blk(seq, t, up=1, keep_pad=False):
+                return bn_relu(ops.conv3x3(t, seq[0].weight, seq[0].bias, up, keep_pad), seq[1])
+            x3 = blk(g("conv3"), add_up(block(g("adjust1"), xh), x2, 1), up=2)  # conv3(up2(adjust1 + x2))
+            x4 = blk(g("conv4"), add_up(block(g("adjust2"), xh), x3, 2), up=2)  # conv4(up2(up2(adjust2) + x3))
+            m3 = blk(a3[2], block(a3[1], block(a3[0], x2)), keep_pad=True)
+            m4 = blk(a4[1], block(a4[0], x3), keep_pad=True)
+            fh = x4.shape[1]
+            sm = score(x4, g("conv5"), m3, m4).view(-1, 1, fh, fh)  # (B, 1, fh, fh) fp32 (padded rows in)
+            coords += list(_soft_argmax(sm, hd.stride))
+            continue
         x3 = block(g("conv3"), up(block(g("adjust1"), xh), 2) + up(x2, 2))
         x4 = block(g("conv4"), up(block(g("adjust2"), xh), 4) + up(x3, 2))
-        a3, a4 = g("adjust3"), g("adjust4")
         m3, m4 = block(a3[2], block(a3[1], block(a3[0], x2))), block(a4[1], block(a4[0], x3))
-        score = getattr(ops, "corner_score", None)
         if score is not None and HEAD_SCORE_FP32 and m3.dtype == torch.bfloat16 and m4.dtype == torch.bfloat16:
             fh = x4.shape[1]
             sm = score(x4, g("conv5"), m3, m4).view(-1, 1, fh, fh)  # (B, 1, fh, fh) fp32

@@ -782,13 +782,15 @@ def test_hip_conv3x3_autograd(B, H, Cin, Cout):
         assert err <= tol, (name, err)
 
 
+@pytest.mark.parametrize("padded", [False, True])
 @pytest.mark.parametrize("B,fh,c4", [(16, 80, 48), (3, 80, 48), (2, 96, 48), (1, 16, 8)])
-def test_hip_corner_score_autograd(B, fh, c4):
+def test_hip_corner_score_autograd(B, fh, c4, padded):
     """HipOps.corner_score (_HipCornerScore: one corner branch's conv5 in fp32 + up4(adjust3) + up2(adjust4),
     head.py:191-192) against the aten path it replaces (F.linear in fp32 + F.interpolate + adds) under fp32
     autograd, on the same bf16 inputs; the adjust maps as the HIP BatchNorm leaves them (1-channel views of
-    8-channel rows).  Score map within 1e-5 (relative L2; fp32 sums in another order); dX4 / dA3 / dA4 within
-    1e-2 (bf16 results); dW5 / db5 within 1e-5; the backward bitwise repeatable (fixed-order reductions)."""
+    8-channel rows, as (B, h, w, 1) views or -- padded, the fused head's form -- the 8-channel rows themselves,
+    whose padding channels' gradient is 0).  Score map within 1e-5 (relative L2; fp32 sums in another order);
+    dX4 / dA3 / dA4 within 1e-2 (bf16 results); dW5 / db5 within 1e-5; the backward bitwise repeatable."""
     import torch.nn.functional as F
     from mmt_amd.train import HipOps
     g = torch.Generator().manual_seed(B + fh + c4)
@@ -820,7 +822,7 @@ def test_hip_corner_score_autograd(B, fh, c4):
     def run():
         for t in (xd, p3, p4, conv.weight, conv.bias):
             t.grad = None
-        out = HipOps.corner_score(xd, conv, p3[..., :1], p4[..., :1])
+        out = HipOps.corner_score(xd, conv, p3 if padded else p3[..., :1], p4 if padded else p4[..., :1])
         out.backward(dsm.cuda())
         torch.cuda.synchronize()
         return [t.detach().float().cpu().clone() for t in (out, xd.grad, p3.grad[..., :1], p4.grad[..., :1],
@@ -836,6 +838,67 @@ def test_hip_corner_score_autograd(B, fh, c4):
         assert a.shape == r.shape, (name, a.shape, r.shape)
         err = ((a - r).norm() / r.norm()).item()
         assert err <= tol, (name, err)
+
+
+@pytest.mark.parametrize("B,H,Cin,Cout,up", [(2, 20, 192, 96, 2), (16, 40, 96, 48, 2), (2, 20, 48, 8, 4), (3, 10, 96, 1, 2)])
+def test_hip_conv3x3_upsampled_input(B, H, Cin, Cout, up):
+    """HipOps.conv3x3(x, w, b, up): the 3x3 conv of the nearest upsampling (x up) of x, the map never materialised
+    (the GEMM's conv_up addressing; dX = the flipped conv at the upsampled size + the up x up block sums, dW over
+    mmt_im2col3x3_up_bf16), against F.conv2d(F.interpolate(x)) autograd in fp32 on the same bf16 inputs: output
+    1e-2, dX / dW / db 2e-2 (relative L2); keep_pad leaves a 1-channel output in its 8-channel rows (padding 0)."""
+    import torch.nn.functional as F
+    from mmt_amd.train import HipOps
+    g = torch.Generator().manual_seed(B * H + Cin + Cout + up)
+    x = torch.randn(B, H, H, Cin, generator=g).bfloat16().float()
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) / (3 * Cin ** 0.5)).bfloat16().float()
+    b = torch.randn(Cout, generator=g)
+    dy = torch.randn(B, H * up, H * up, Cout, generator=g).bfloat16().float()
+    xr, wr, br = x.clone().requires_grad_(True), w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    yr = F.conv2d(F.interpolate(xr.permute(0, 3, 1, 2), scale_factor=up), wr, br, padding=1).permute(0, 2, 3, 1)
+    yr.backward(dy)
+    xd = x.bfloat16().cuda().requires_grad_(True)
+    wd, bd = w.cuda().requires_grad_(True), b.cuda().requires_grad_(True)
+    keep = Cout % 8 != 0
+    yd = HipOps.conv3x3(xd, wd, bd, up, keep)
+    if keep:
+        assert yd.shape[-1] == 8 and yd[..., Cout:].abs().max().item() == 0.0
+        dyd = torch.zeros(B, H * up, H * up, 8, device="cuda", dtype=torch.bfloat16)
+        dyd[..., :Cout] = dy.bfloat16().cuda()
+        yd.backward(dyd)
+        yd = yd[..., :Cout]
+    else:
+        yd.backward(dy.bfloat16().cuda())
+    torch.cuda.synchronize()
+    for name, a, r, tol in (("y", yd, yr, 1e-2), ("dx", xd.grad, xr.grad, 2e-2), ("dw", wd.grad, wr.grad, 2e-2),
+                            ("db", bd.grad, br.grad, 2e-2)):
+        a = a.detach().float().cpu()
+        assert a.shape == r.shape, (name, a.shape, r.shape)
+        err = ((a - r).norm() / r.norm()).item()
+        assert err <= tol, (name, err)
+
+
+@pytest.mark.parametrize("B,H,C,up", [(16, 40, 96, 2), (2, 20, 192, 1), (3, 80, 48, 4)])
+def test_hip_add_up(B, H, C, up):
+    """HipOps.add_up(a, b, up) = bf16(up(a) + b) and its backward (db = dout, da = the up x up block sums of dout,
+    fp32 sums) against the fp32 aten composition on the same bf16 inputs: the forward bit-identical to rounding
+    the fp32 sum, the gradients within 1e-2 (bf16)."""
+    import torch.nn.functional as F
+    from mmt_amd.train import HipOps
+    g = torch.Generator().manual_seed(B + H + C + up)
+    a = torch.randn(B, H // up, H // up, C, generator=g).bfloat16()
+    b = torch.randn(B, H, H, C, generator=g).bfloat16()
+    dout = torch.randn(B, H, H, C, generator=g).bfloat16()
+    ar, br = a.float().requires_grad_(True), b.float().requires_grad_(True)
+    ref = F.interpolate(ar.permute(0, 3, 1, 2), scale_factor=up).permute(0, 2, 3, 1) + br
+    ref.backward(dout.float())
+    ad, bd = a.cuda().requires_grad_(True), b.cuda().requires_grad_(True)
+    out = HipOps.add_up(ad, bd, up)
+    out.backward(dout.cuda())
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu(), ref.detach().bfloat16())
+    for name, got, r in (("da", ad.grad, ar.grad), ("db", bd.grad, br.grad)):
+        err = ((got.float().cpu() - r).norm() / r.norm()).item()
+        assert err <= 1e-2, (name, err)
 
 
 @pytest.mark.parametrize("B,H,C,train", [(2, 20, 384, True), (16, 80, 48, True), (3, 40, 96, True), (2, 20, 192, False),

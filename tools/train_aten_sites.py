@@ -24,6 +24,25 @@ def main():
     from torch.profiler import ProfilerActivity, profile
     from mmt_amd.model import build_mixformer_vit_rgbt, hot_path_cfg
     from mmt_amd.train import HipOps, TrainStep, synthetic_batch
+    # forward attribution: every function of mmt_amd.train (and HipOps' static methods) runs inside a
+    # record_function range of its own name, so an aten op's innermost enclosing range names its call site
+    import functools
+    import inspect
+    import mmt_amd.train as T
+    from torch.profiler import record_function
+
+    def wrap(name, fn):
+        @functools.wraps(fn)
+        def w(*a, **k):
+            with record_function("site::" + name):
+                return fn(*a, **k)
+        return w
+    for name, fn in list(vars(T).items()):
+        if inspect.isfunction(fn) and fn.__module__ == T.__name__ and not name.startswith("__"):
+            setattr(T, name, wrap(name, fn))
+    for name, fn in list(vars(T.HipOps).items()):
+        if isinstance(fn, staticmethod):
+            setattr(T.HipOps, name, staticmethod(wrap("HipOps." + name, fn.__func__)))
     torch.manual_seed(0)
     net = build_mixformer_vit_rgbt(hot_path_cfg(), train=False).cuda().train()
     step = TrainStep(net, HipOps)
@@ -34,24 +53,40 @@ def main():
     with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
         step(*batch)
         torch.cuda.synchronize()
-    # aten ops with device time, grouped by their 6 innermost Python frames (forward ops; the backward's run on
-    # autograd's thread without a Python stack and show as the op that created them is listed by name only)
-    ka = prof.key_averages(group_by_stack_n=6)
-    rows = []
-    for e in ka:
-        if not e.key.startswith("aten::"):
+    # every aten op with device time: attributed to its autograd backward node (the enclosing
+    # "autograd::engine::evaluate_function: <Node>" event) or, in the forward, to its innermost mmt_amd frames
+    import collections
+    agg = collections.defaultdict(lambda: [0.0, 0, set()])
+    top_total = 0.0
+    for e in prof.events():
+        if not e.name.startswith("aten::"):
             continue
         sdev = getattr(e, "self_device_time_total", None)
         if sdev is None:
             sdev = getattr(e, "self_cuda_time_total", 0.0)
         if sdev <= 0:
             continue
-        frames = [f.split("multi-modal-tracking_amd/")[-1] for f in (e.stack or []) if "mmt_amd" in f or "tools/" in f]
-        rows.append((sdev, e.count, e.key, " <- ".join(frames[:3]) or "(no python stack: autograd backward)"))
-    rows.sort(key=lambda r: -r[0])
-    print("aten self device time, one step: %.1f us" % sum(r[0] for r in rows))
-    for sdev, n, key, where in rows[:args.top]:
-        print("%9.1f us %4d  %-32s %s" % (sdev, n, key, where[:160]))
+        where, par = None, e.cpu_parent
+        while par is not None:
+            if par.name.startswith("autograd::engine::evaluate_function"):
+                where = "bwd " + par.name.split(": ", 1)[-1]
+                break
+            par = par.cpu_parent
+        if where is None:
+            par, names = e.cpu_parent, []
+            while par is not None and len(names) < 2:
+                if par.name.startswith("site::"):
+                    names.append(par.name[6:])
+                par = par.cpu_parent
+            where = "fwd " + (" <- ".join(names) if names else "?")
+        a = agg[where]
+        a[0] += sdev
+        a[1] += 1
+        a[2].add(e.name)
+        top_total += sdev
+    print("aten self device time, one step: %.1f us" % top_total)
+    for where, (us, n, names) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:args.top]:
+        print("%9.1f us %4d  %-90s %s" % (us, n, where[:90], ",".join(sorted(names))[:100]))
 
 
 if __name__ == "__main__":
