@@ -360,6 +360,17 @@ int mmt_ce_recover(const float* x, const int* gidx, int keep, void* out, int S, 
  * (128) | attention logits (64)] from the [q_v | q_i] Linear; value [2][B][nq][512] (dtype);
  * out[b*nq+q][512] (dtype) -- identical for both modalities, as in the reference. */
 int mmt_msda_bimodal(const float* offw, const void* value, void* out, int B, int hw, int dtype, void* stream);
+/* Training form of the bimodal MSDA middle (ms_deform_attn_bimodal.py:97-128 in the training step,
+ * mmt_amd.train.fusion_forward; 8 heads x 2 levels x 4 points, 64 channels per head, levels hw x hw, nq = hw^2
+ * <= 484), bf16 in and out: a = softmax(awl) per (query, head), loc = ref + off / hw, out = the sampled sum
+ * (msda_generic_kernel's arithmetic).  value [B][2][nq][512], off [B][nq][128], awl [B][nq][64], ref fp32
+ * [nq][2], out [B][nq][512].  Backward: grad_value (deterministic per-pixel gather), grad_off = gloc / hw,
+ * grad_awl = the softmax backward of the per-sample weight gradients, all bf16. */
+int mmt_msda_bimodal_train_fwd(const void* value, const void* off, const void* awl, const float* ref, void* out, int B,
+                               int hw, void* stream);
+int mmt_msda_bimodal_train_bwd(const void* value, const void* off, const void* awl, const float* ref,
+                               const void* grad_out, void* grad_value, void* grad_off, void* grad_awl, int B, int hw,
+                               void* stream);
 
 /* ---------------------------------------------------------------- corner head / SPM
  * Cout=1 3x3/pad-1 conv (+bias, BN folded) + ReLU on NHWC input [G][B][h*h][cin] (pixel stride
@@ -470,6 +481,28 @@ int mmt_im2col3x3_bf16(const void* in, void* out, int B, int H, int W, int C, vo
 /* The same of the nearest-upsampled (x up: 1, 2, 4 or 8) map of in [B][H/up][W/up][C]; H, W the upsampled sizes
  * (the training head's upsampling folded into its convolutions, head.py:187-189). */
 int mmt_im2col3x3_up_bf16(const void* in, void* out, int B, int H, int W, int C, int up, void* stream);
+/* The same with channel-major columns, out[pix][c * 9 + ky * 3 + kx] (PyTorch's Conv2d weight order, so the dW
+ * GEMM against it writes the [Cout][Cin][3][3] gradient directly); up 1, 2, 4 or 8 as above. */
+int mmt_im2col3x3_cm_bf16(const void* in, void* out, int B, int H, int W, int C, int up, void* stream);
+/* The training head's 3x3 conv weights to the bf16 operand layouts of its convs, up to MMT_WPREP_MAX convs in
+ * one launch (once per step, instead of two cast / permute copies per conv): w fp32 [cout][cin][3][3] ->
+ * wf bf16 [cp][3][3][cin] (forward) and wb bf16 [cin][3][3][cp] (dX), co in [cout, cp) zero; bp (optional)
+ * fp32 [cp] = b padded with zeros (b NULL: zeros). */
+#define MMT_WPREP_MAX 24
+typedef struct mmt_conv_wprep {
+    const float* w;
+    const float* b;
+    void* wf;
+    void* wb;
+    float* bp;
+    int32_t cout, cp, cin, pad_;
+} mmt_conv_wprep;
+typedef struct mmt_conv_wprep_batch {  /* kernel argument (by value) */
+    mmt_conv_wprep item[MMT_WPREP_MAX];
+    int32_t blk0[MMT_WPREP_MAX];
+    int32_t n;
+} mmt_conv_wprep_batch;
+int mmt_conv3x3_wprep(const mmt_conv_wprep* items, int n, void* stream);
 /* Backward of nearest upsampling x up on NHWC bf16: out [B][Hi][Wi][C] = the up x up block sums of in
  * [B][Hi*up][Wi*up][C] (fp32 sums in a fixed order, bf16 out). */
 int mmt_upsample_sum_bf16(const void* in, void* out, int B, int Hi, int Wi, int C, int up, void* stream);

@@ -368,7 +368,346 @@ __global__ __launch_bounds__(256) void msda_bwd_value_kernel(const T* __restrict
     }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Training form of MSDeformAttn_Bimodal's middle (ms_deform_attn_bimodal.py:97-128 as the training step runs it,
+// mmt_amd.train.fusion_forward): from the bf16 outputs of value_proj / sampling_offsets / attention_weights to the
+// bf16 input of output_proj, forward and backward, with the reference's arithmetic:
+//   a[q,m,:]  = softmax(float(awl[q, m*8 : m*8+8]))             (F.softmax(aw.float(), -1): torch's warp
+//               softmax order for 8 logits -- butterfly max / sum over lanes i^4, i^2, i^1, then e_i / sum)
+//   loc       = ref[q] + float(off[q,m,l,p,:]) / (hw, hw)        (ref: the device-computed reference points)
+//   out[q, m*64 + c] = bf16(sum_l sum_p a * bilinear(V_l[:, :, m, c], loc * hw - 0.5))   (msda_generic_kernel)
+// Backward: grad_value (bf16) = the deterministic per-pixel gather of msda_bwd_value_kernel (same (sample, tap)
+// summation order, so the same fp32 sums); grad_awl = bf16(a * (gaw - sum_j a_j gaw_j)) (softmax backward);
+// grad_off = bf16(gloc / hw) (the division's backward), gaw / gloc per sample as msda_bwd_kernel, summed over the
+// 64 channels in 8-lane groups.  Replaces the generic fp32 kernels plus the step's softmax, location, cast and
+// backward glue (round 6).  Layouts: value / grad_value [B][2][nq][8][64], off / grad_off [B][nq][8][2][4][2],
+// awl / grad_awl [B][nq][8][8], ref fp32 [nq][2] (x, y), out / grad_out [B][nq][512]; nq = hw * hw.
+constexpr int MT_NH = 8, MT_NL = 2, MT_NP = 4, MT_DH = 64, MT_CM = MT_NH * MT_DH, MT_NQ_MAX = 484;
+
+// torch's softmax of 8 logits (persistent warp softmax, 8 lanes): butterfly max and sum, e_i / sum
+MMT_DEV void mt_softmax8(const float* lg, float* a) {
+    float e[8];
+    float mx = lg[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) mx = fmaxf(mx, lg[i]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) e[i] = expf(lg[i] - mx);
+    const float s = ((e[0] + e[4]) + (e[2] + e[6])) + ((e[1] + e[5]) + (e[3] + e[7]));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = e[i] / s;
+}
+
+MMT_DEV void mt_load_logits(const bf16_t* awl, float* lg) {  // 8 consecutive bf16 (16 B)
+    const uint4 u = *(const uint4*)awl;
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        lg[2 * j] = __uint_as_float(w[j] << 16);
+        lg[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+    }
+}
+
+// sample geometry (msda_generic_kernel / msda_bwd_kernel): h_im / w_im, the in-range flag, the taps' corner
+struct MtGeom {
+    float h, w;
+    bool in;
+};
+MMT_DEV MtGeom mt_geom(float rx, float ry, float ox, float oy, int hw) {
+    const float lx = rx + ox / (float)hw, ly = ry + oy / (float)hw;
+    MtGeom g;
+    g.h = ly * (float)hw - 0.5f;
+    g.w = lx * (float)hw - 0.5f;
+    g.in = g.h > -1.f && g.w > -1.f && g.h < (float)hw && g.w < (float)hw;
+    return g;
+}
+
+MMT_DEV uint4 mt_ld(bool k, const bf16_t* p) {  // a valid tap's 16 B, else zeros (no select of addresses)
+    uint4 r = uint4{0u, 0u, 0u, 0u};
+    if (k) r = *(const uint4*)p;
+    return r;
+}
+
+MMT_DEV void mt_unpack8(uint4 u, float* v) {
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        v[2 * j] = __uint_as_float(w[j] << 16);
+        v[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+    }
+}
+
+// forward: one wave per (b, q); lane = (head m, 8-channel group)
+__global__ __launch_bounds__(64) void msda_train_fwd_kernel(const bf16_t* __restrict__ value, const bf16_t* __restrict__ off,
+                                                            const bf16_t* __restrict__ awl, const float* __restrict__ ref,
+                                                            bf16_t* __restrict__ out, int hw) {
+    const int nq = hw * hw;
+    const int64_t row = blockIdx.x;  // b * nq + q
+    const int b = (int)(row / nq), q = (int)(row % nq);
+    const int t = threadIdx.x, m = t >> 3, c0 = (t & 7) * 8;
+    float lg[8], a[8];
+    mt_load_logits(awl + row * (MT_NH * 8) + m * 8, lg);
+    mt_softmax8(lg, a);
+    const float rx = ref[2 * q], ry = ref[2 * q + 1];
+    const bf16_t* ob = off + row * (MT_NH * MT_NL * MT_NP * 2) + m * (MT_NL * MT_NP * 2);
+    float col[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) col[j] = 0.f;
+#pragma unroll
+    for (int l = 0; l < MT_NL; ++l) {
+        const bf16_t* vb = value + ((int64_t)(b * MT_NL + l) * nq) * MT_CM + m * MT_DH + c0;
+#pragma unroll
+        for (int p = 0; p < MT_NP; ++p) {
+            const int i = l * MT_NP + p;
+            const MtGeom g = mt_geom(rx, ry, bf2f(ob[2 * i]), bf2f(ob[2 * i + 1]), hw);
+            if (!g.in) continue;  // lane-group uniform
+            const int hl = (int)floorf(g.h), wl = (int)floorf(g.w), hh_ = hl + 1, wh_ = wl + 1;
+            const float lh = g.h - (float)hl, lw = g.w - (float)wl, hh = 1.f - lh, hwt = 1.f - lw;
+            const bool k1 = hl >= 0 && wl >= 0, k2 = hl >= 0 && wh_ <= hw - 1;
+            const bool k3 = hh_ <= hw - 1 && wl >= 0, k4 = hh_ <= hw - 1 && wh_ <= hw - 1;
+            float v1[8], v2[8], v3[8], v4[8];
+            mt_unpack8(mt_ld(k1, vb + (hl * hw + wl) * MT_CM), v1);
+            mt_unpack8(mt_ld(k2, vb + (hl * hw + wh_) * MT_CM), v2);
+            mt_unpack8(mt_ld(k3, vb + (hh_ * hw + wl) * MT_CM), v3);
+            mt_unpack8(mt_ld(k4, vb + (hh_ * hw + wh_) * MT_CM), v4);
+            const float w1 = hh * hwt, w2 = hh * lw, w3 = lh * hwt, w4 = lh * lw;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) col[j] += (w1 * v1[j] + w2 * v2[j] + w3 * v3[j] + w4 * v4[j]) * a[i];
+        }
+    }
+    bf16_t* o = out + row * MT_CM + m * MT_DH + c0;
+    *(uint4*)o = uint4{pack_bf16x2(col[0], col[1]), pack_bf16x2(col[2], col[3]), pack_bf16x2(col[4], col[5]),
+                       pack_bf16x2(col[6], col[7])};
+}
+
+// backward, per sample: gaw / gloc (msda_bwd_kernel's per-channel arithmetic, channel sums over the lane's 8
+// channels then the 8 lanes of the head), the softmax backward over the head's 8 samples, grad_off = gloc / hw
+__global__ __launch_bounds__(64) void msda_train_bwd_samp_kernel(const bf16_t* __restrict__ value,
+                                                                 const bf16_t* __restrict__ off,
+                                                                 const bf16_t* __restrict__ awl,
+                                                                 const float* __restrict__ ref,
+                                                                 const bf16_t* __restrict__ gout,
+                                                                 bf16_t* __restrict__ goff, bf16_t* __restrict__ gawl,
+                                                                 int hw) {
+    const int nq = hw * hw;
+    const int64_t row = blockIdx.x;
+    const int b = (int)(row / nq), q = (int)(row % nq);
+    const int t = threadIdx.x, m = t >> 3, cg = t & 7, c0 = cg * 8;
+    float lg[8], a[8];
+    mt_load_logits(awl + row * (MT_NH * 8) + m * 8, lg);
+    mt_softmax8(lg, a);
+    const float rx = ref[2 * q], ry = ref[2 * q + 1];
+    const bf16_t* ob = off + row * (MT_NH * MT_NL * MT_NP * 2) + m * (MT_NL * MT_NP * 2);
+    float g[8];
+    mt_unpack8(*(const uint4*)(gout + row * MT_CM + m * MT_DH + c0), g);
+    float gaw[8], gx[8], gy[8];
+#pragma unroll
+    for (int l = 0; l < MT_NL; ++l) {
+        const bf16_t* vb = value + ((int64_t)(b * MT_NL + l) * nq) * MT_CM + m * MT_DH + c0;
+#pragma unroll
+        for (int p = 0; p < MT_NP; ++p) {
+            const int i = l * MT_NP + p;
+            const MtGeom ge = mt_geom(rx, ry, bf2f(ob[2 * i]), bf2f(ob[2 * i + 1]), hw);
+            float sa = 0.f, sx = 0.f, sy = 0.f;
+            if (ge.in) {
+                const int hl = (int)floorf(ge.h), wl = (int)floorf(ge.w), hh_ = hl + 1, wh_ = wl + 1;
+                const float lh = ge.h - (float)hl, lw = ge.w - (float)wl, hh = 1.f - lh, hwt = 1.f - lw;
+                const float w1 = hh * hwt, w2 = hh * lw, w3 = lh * hwt, w4 = lh * lw;
+                const bool k1 = hl >= 0 && wl >= 0, k2 = hl >= 0 && wh_ <= hw - 1;
+                const bool k3 = hh_ <= hw - 1 && wl >= 0, k4 = hh_ <= hw - 1 && wh_ <= hw - 1;
+                float v1[8], v2[8], v3[8], v4[8];
+                mt_unpack8(mt_ld(k1, vb + (hl * hw + wl) * MT_CM), v1);
+                mt_unpack8(mt_ld(k2, vb + (hl * hw + wh_) * MT_CM), v2);
+                mt_unpack8(mt_ld(k3, vb + (hh_ * hw + wl) * MT_CM), v3);
+                mt_unpack8(mt_ld(k4, vb + (hh_ * hw + wh_) * MT_CM), v4);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float tg = g[j], tgv = tg * a[i];
+                    float gh = 0.f, gw = 0.f;
+                    if (k1) { gh -= hwt * v1[j]; gw -= hh * v1[j]; }
+                    if (k2) { gh -= lw * v2[j]; gw += hh * v2[j]; }
+                    if (k3) { gh += hwt * v3[j]; gw -= lh * v3[j]; }
+                    if (k4) { gh += lw * v4[j]; gw += lh * v4[j]; }
+                    sa += tg * (w1 * v1[j] + w2 * v2[j] + w3 * v3[j] + w4 * v4[j]);
+                    sx += (float)hw * gw * tgv;
+                    sy += (float)hw * gh * tgv;
+                }
+            }
+            // the head's 8 lanes: xor 1, 2, 4 (every lane ends with the head's channel sum)
+#pragma unroll
+            for (int o = 1; o < 8; o <<= 1) {
+                sa += __shfl_xor(sa, o, 64);
+                sx += __shfl_xor(sx, o, 64);
+                sy += __shfl_xor(sy, o, 64);
+            }
+            gaw[i] = sa;
+            gx[i] = sx;
+            gy[i] = sy;
+        }
+    }
+    // softmax backward (torch: a * (grad - sum(grad * a)), the sum in the warp butterfly order)
+    float ga[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ga[i] = gaw[i] * a[i];
+    const float s = ((ga[0] + ga[4]) + (ga[2] + ga[6])) + ((ga[1] + ga[5]) + (ga[3] + ga[7]));
+    // lane cg of the head stores sample i = cg: its logit gradient and its two offset gradients
+    float dl = 0.f, dx = 0.f, dy = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        if (i == cg) dl = a[i] * (gaw[i] - s), dx = gx[i] / (float)hw, dy = gy[i] / (float)hw;
+    gawl[row * (MT_NH * 8) + m * 8 + cg] = f2bf(dl);
+    *(uint32_t*)(goff + row * (MT_NH * MT_NL * MT_NP * 2) + (m * 8 + cg) * 2) = pack_bf16x2(dx, dy);
+}
+
+// backward, grad_value: one workgroup per (b, m, level) -- every sample of the level's nq queries expanded into its
+// taps (counted per pixel, bucketed, each bucket sorted by (sample, tap)), then per pixel and channel
+// sum w_k * (g[q, c] * a) in that order: msda_bwd_value_kernel's order with the grad_out rows and the level's
+// attention weights staged in LDS.  16 waves; lane = channel in the gather.
+constexpr int MT_VT = 1024;
+__global__ __launch_bounds__(MT_VT) void msda_train_bwd_value_kernel(const bf16_t* __restrict__ off,
+                                                                     const bf16_t* __restrict__ awl,
+                                                                     const float* __restrict__ ref,
+                                                                     const bf16_t* __restrict__ gout,
+                                                                     bf16_t* __restrict__ gvalue, int hw) {
+    __shared__ __attribute__((aligned(16))) bf16_t gl[MT_NQ_MAX * MT_DH];  // grad_out rows of head m
+    __shared__ float al[MT_NQ_MAX * MT_NP];                                  // a of this level's points
+    __shared__ int ekey[MT_NQ_MAX * MT_NP * 4];
+    __shared__ float ew[MT_NQ_MAX * MT_NP * 4];
+    __shared__ int cnt[MT_NQ_MAX + 1], cur[MT_NQ_MAX];
+    const int nq = hw * hw, t = threadIdx.x;
+    const int l = blockIdx.x, m = blockIdx.y, b = blockIdx.z;
+    const int64_t row0 = (int64_t)b * nq;
+    for (int i = t; i < nq * (MT_DH / 8); i += MT_VT) {  // 16-B pieces of the grad_out rows
+        const int q = i >> 3, k = i & 7;
+        *(uint4*)&gl[q * MT_DH + k * 8] = *(const uint4*)(gout + (row0 + q) * MT_CM + m * MT_DH + k * 8);
+    }
+    for (int q = t; q < nq; q += MT_VT) {
+        float lg[8], a[8];
+        mt_load_logits(awl + (row0 + q) * (MT_NH * 8) + m * 8, lg);
+        mt_softmax8(lg, a);
+#pragma unroll
+        for (int p = 0; p < MT_NP; ++p) al[q * MT_NP + p] = a[l * MT_NP + p];
+    }
+    for (int r = t; r <= nq; r += MT_VT) cnt[r] = 0;
+    __syncthreads();
+    const int ns = nq * MT_NP;
+    // the taps of sample j = q * 4 + p: f(k, pixel, w_k) for the valid ones (msda_bwd_value_kernel's rules)
+    auto taps = [&](int j, auto&& f) {
+        const int q = j >> 2, p = j & 3;
+        const bf16_t* o = off + (row0 + q) * (MT_NH * MT_NL * MT_NP * 2) + ((m * MT_NL + l) * MT_NP + p) * 2;
+        const MtGeom g = mt_geom(ref[2 * q], ref[2 * q + 1], bf2f(o[0]), bf2f(o[1]), hw);
+        if (!g.in) return;
+        const int hl = (int)floorf(g.h), wl = (int)floorf(g.w), hh_ = hl + 1, wh_ = wl + 1;
+        const float lh = g.h - (float)hl, lw = g.w - (float)wl, hh = 1.f - lh, hwt = 1.f - lw;
+        const int r1 = hl * hw + wl;
+        if (hl >= 0 && wl >= 0) f(0, r1, hh * hwt);
+        if (hl >= 0 && wh_ <= hw - 1) f(1, r1 + 1, hh * lw);
+        if (hh_ <= hw - 1 && wl >= 0) f(2, r1 + hw, lh * hwt);
+        if (hh_ <= hw - 1 && wh_ <= hw - 1) f(3, r1 + hw + 1, lh * lw);
+    };
+    for (int j = t; j < ns; j += MT_VT) taps(j, [&](int, int r, float) { atomicAdd(&cnt[r], 1); });
+    __syncthreads();
+    if (t < 64) {  // exclusive scan of the nq counts: lane t owns a run of ceil(nq / 64)
+        const int per = (nq + 63) / 64, r0 = t * per, r1 = min(r0 + per, nq);
+        int sum = 0;
+        for (int r = r0; r < r1; ++r) sum += cnt[r];
+        int x = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o, 64);
+            if (t >= o) x += y;
+        }
+        int run = x - sum;
+        for (int r = r0; r < r1; ++r) {
+            const int v = cnt[r];
+            cur[r] = run;
+            run += v;
+        }
+        if (t == 63) cnt[nq] = x;
+    }
+    __syncthreads();
+    for (int r = t; r < nq; r += MT_VT) cnt[r] = cur[r];  // bucket starts (cnt[nq] = total)
+    __syncthreads();
+    for (int j = t; j < ns; j += MT_VT)
+        taps(j, [&](int k, int r, float wk) {
+            const int pos = atomicAdd(&cur[r], 1);
+            ekey[pos] = j * 4 + k;
+            ew[pos] = wk;
+        });
+    __syncthreads();
+    for (int r = t; r < nq; r += MT_VT) {  // each bucket in (sample, tap) order
+        const int e0 = cnt[r], e1 = cnt[r + 1];
+        for (int e = e0 + 1; e < e1; ++e) {
+            const int k = ekey[e];
+            const float wv = ew[e];
+            int i = e - 1;
+            for (; i >= e0 && ekey[i] > k; --i) {
+                ekey[i + 1] = ekey[i];
+                ew[i + 1] = ew[i];
+            }
+            ekey[i + 1] = k;
+            ew[i + 1] = wv;
+        }
+    }
+    __syncthreads();
+    // gather: wave w takes pixels w, w + 16, ... four at a time (independent sums in flight); lane = channel
+    const int wave = t >> 6, c = t & 63;
+    constexpr int NW = MT_VT / 64, PS = 4;
+    bf16_t* gv = gvalue + ((int64_t)(b * MT_NL + l) * nq) * MT_CM + m * MT_DH + c;
+    for (int r0 = wave; r0 < nq; r0 += NW * PS) {
+        int e0[PS], e1[PS], len = 0;
+        float acc[PS];
+#pragma unroll
+        for (int i = 0; i < PS; ++i) {
+            const int r = r0 + i * NW;
+            e0[i] = r < nq ? cnt[r] : 0;
+            e1[i] = r < nq ? cnt[r + 1] : 0;
+            len = max(len, e1[i] - e0[i]);
+            acc[i] = 0.f;
+        }
+        for (int k = 0; k < len; ++k) {
+#pragma unroll
+            for (int i = 0; i < PS; ++i) {
+                const int e = e0[i] + k;
+                if (e < e1[i]) {
+                    const int j = ekey[e] >> 2;
+                    acc[i] += ew[e] * (bf2f(gl[(j >> 2) * MT_DH + c]) * al[j]);
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < PS; ++i) {
+            const int r = r0 + i * NW;
+            if (r < nq) gv[(int64_t)r * MT_CM] = f2bf(acc[i]);
+        }
+    }
+}
+
 }  // namespace
+
+extern "C" int mmt_msda_bimodal_train_fwd(const void* value, const void* off, const void* awl, const float* ref,
+                                          void* out, int B, int hw, void* stream) {
+    if (!value || !off || !awl || !ref || !out || B <= 0 || hw <= 0 || hw * hw > MT_NQ_MAX) return MMT_EBADARG;
+    if (((uintptr_t)value | (uintptr_t)awl | (uintptr_t)out) & 15) return MMT_EBADARG;
+    hipLaunchKernelGGL(msda_train_fwd_kernel, dim3((unsigned)(B * hw * hw)), dim3(64), 0, (hipStream_t)stream,
+                       (const bf16_t*)value, (const bf16_t*)off, (const bf16_t*)awl, ref, (bf16_t*)out, hw);
+    return launch_status();
+}
+
+extern "C" int mmt_msda_bimodal_train_bwd(const void* value, const void* off, const void* awl, const float* ref,
+                                          const void* grad_out, void* grad_value, void* grad_off, void* grad_awl, int B,
+                                          int hw, void* stream) {
+    if (!value || !off || !awl || !ref || !grad_out || !grad_value || !grad_off || !grad_awl || B <= 0 || hw <= 0 ||
+        hw * hw > MT_NQ_MAX)
+        return MMT_EBADARG;
+    if (((uintptr_t)value | (uintptr_t)awl | (uintptr_t)grad_out | (uintptr_t)grad_off) & 15) return MMT_EBADARG;
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(msda_train_bwd_samp_kernel, dim3((unsigned)(B * hw * hw)), dim3(64), 0, st, (const bf16_t*)value,
+                       (const bf16_t*)off, (const bf16_t*)awl, ref, (const bf16_t*)grad_out, (bf16_t*)grad_off,
+                       (bf16_t*)grad_awl, hw);
+    hipLaunchKernelGGL(msda_train_bwd_value_kernel, dim3(MT_NL, MT_NH, (unsigned)B), dim3(MT_VT), 0, st,
+                       (const bf16_t*)off, (const bf16_t*)awl, ref, (const bf16_t*)grad_out, (bf16_t*)grad_value, hw);
+    return launch_status();
+}
 
 extern "C" int mmt_ms_deform_attn_backward(const void* value, const int64_t* spatial_shapes, const int64_t* level_start,
                                            const void* sampling_loc, const void* attn_weight, const void* grad_output,

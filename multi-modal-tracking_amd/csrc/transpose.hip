@@ -157,6 +157,86 @@ __global__ __launch_bounds__(256) void add_up_kernel(const u32x4* __restrict__ a
                            __uint_as_float(va[j] & 0xffff0000u) + __uint_as_float(vb[j] & 0xffff0000u));
     out[i] = o;
 }
+
+// The same im2col with channel-major columns: out[pix][c * 9 + ky * 3 + kx] -- PyTorch's Conv2d weight order
+// [Cout][Cin][3][3], so the dW GEMM against it writes the parameter's gradient in place (no permute pass).
+// One thread per (pixel, 8 channels): nine 16-B tap loads (as im2col3x3_kernel), the 8 x 9 transpose in
+// registers -> its 144 contiguous output bytes; the wave's 64 x 144 B (contiguous: items are consecutive) go
+// out through LDS so that every 16-B store instruction covers 1 KiB of consecutive bytes.
+__global__ __launch_bounds__(256) void im2col3x3_cm_kernel(const u32x4* __restrict__ in, u32x4* __restrict__ out, int H,
+                                                            int W, int c8, int64_t total, int up_sh) {
+    __shared__ u32x4 stage[4][64 * 9];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (pixel, chunk)
+    uint16_t e[72];                                               // e[c * 9 + tap]
+    if (i < total) {
+        const int ch = (int)(i % c8);
+        const int64_t pix = i / c8;
+        const int x = (int)(pix % W), y = (int)((pix / W) % H);
+        const int64_t b = pix / ((int64_t)W * H);
+        const int hi = H >> up_sh, wi = W >> up_sh;
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
+            u32x4 v = u32x4{0u, 0u, 0u, 0u};
+            if (yy >= 0 && yy < H && xx >= 0 && xx < W) v = in[((b * hi + (yy >> up_sh)) * wi + (xx >> up_sh)) * c8 + ch];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                e[(2 * j) * 9 + tap] = (uint16_t)(v[j] & 0xffffu);
+                e[(2 * j + 1) * 9 + tap] = (uint16_t)(v[j] >> 16);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 72; ++k) e[k] = 0;
+    }
+#pragma unroll
+    for (int q = 0; q < 9; ++q)
+        stage[wave][lane * 9 + q] =
+            u32x4{(uint32_t)e[8 * q] | ((uint32_t)e[8 * q + 1] << 16), (uint32_t)e[8 * q + 2] | ((uint32_t)e[8 * q + 3] << 16),
+                  (uint32_t)e[8 * q + 4] | ((uint32_t)e[8 * q + 5] << 16), (uint32_t)e[8 * q + 6] | ((uint32_t)e[8 * q + 7] << 16)};
+    __syncthreads();
+    const int64_t base = ((int64_t)blockIdx.x * 256 + wave * 64) * 9, end = total * 9;
+#pragma unroll
+    for (int s = 0; s < 9; ++s) {
+        const int g = 64 * s + lane;
+        if (base + g < end) out[base + g] = stage[wave][g];
+    }
+}
+
+// The corner head's 3x3 conv weights, fp32 [Cout][Cin][3][3], to the two bf16 operand layouts of the training
+// convs, for up to MMT_WPREP_MAX convs in one launch: wf [Cp][ky][kx][Cin] (forward: the implicit-GEMM conv's W)
+// and wb [Cin][ky][kx][Cp] (dX: the flipped-tap conv's W), rows / columns co in [Cout, Cp) zero, and bp [Cp]
+// fp32 = the bias padded with zeros (when given).  Workgroups [blk0[i], blk0[i+1]) serve conv i: the first half
+// one thread per (co, ci) of the forward layout (adjacent threads: adjacent ci), the second per (ci, co) of the
+// backward layout (adjacent co), so both stores are coalesced; the reads (9 contiguous floats) go through L2.
+__global__ __launch_bounds__(256) void conv_wprep_kernel(mmt_conv_wprep_batch bt) {
+    int i = 0;
+    while (i + 1 < bt.n && (int)blockIdx.x >= bt.blk0[i + 1]) ++i;
+    const mmt_conv_wprep& c = bt.item[i];
+    const int64_t half = (int64_t)c.cp * c.cin;
+    const int64_t nb = (half + 255) / 256;
+    int64_t t = ((int64_t)blockIdx.x - bt.blk0[i]) * 256 + threadIdx.x;
+    const bool bwd = t >= nb * 256;
+    if (bwd) t -= nb * 256;
+    if (t >= half) return;
+    int co, ci;
+    if (!bwd) co = (int)(t / c.cin), ci = (int)(t % c.cin);
+    else ci = (int)(t / c.cp), co = (int)(t % c.cp);
+    float v[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) v[k] = co < c.cout ? c.w[((int64_t)co * c.cin + ci) * 9 + k] : 0.f;
+    bf16_t* wf = (bf16_t*)c.wf;
+    bf16_t* wb = (bf16_t*)c.wb;
+    if (!bwd) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) wf[((int64_t)co * 9 + k) * c.cin + ci] = f2bf(v[k]);
+        if (ci == 0 && c.bp) c.bp[co] = (co < c.cout && c.b) ? c.b[co] : 0.f;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) wb[((int64_t)ci * 9 + k) * c.cp + co] = f2bf(v[k]);
+    }
+}
 }  // namespace
 
 static int up_shift(int up) {
@@ -202,5 +282,33 @@ extern "C" int mmt_im2col3x3_bf16(const void* in, void* out, int B, int H, int W
     const int64_t total = (int64_t)B * H * W * 9 * c8;
     hipLaunchKernelGGL(im2col3x3_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                        (const u32x4*)in, (u32x4*)out, H, W, c8, total, 0);
+    return launch_status();
+}
+
+extern "C" int mmt_im2col3x3_cm_bf16(const void* in, void* out, int B, int H, int W, int C, int up, void* stream) {
+    const int sh = up_shift(up);
+    if (!in || !out || B <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 8 || sh < 0 || H % up || W % up) return MMT_EBADARG;
+    if (((uintptr_t)in | (uintptr_t)out) & 15) return MMT_EBADARG;
+    const int c8 = C / 8;
+    const int64_t total = (int64_t)B * H * W * c8;
+    hipLaunchKernelGGL(im2col3x3_cm_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const u32x4*)in, (u32x4*)out, H, W, c8, total, sh);
+    return launch_status();
+}
+
+extern "C" int mmt_conv3x3_wprep(const mmt_conv_wprep* items, int n, void* stream) {
+    if (!items || n <= 0 || n > MMT_WPREP_MAX) return MMT_EBADARG;
+    mmt_conv_wprep_batch bt;
+    bt.n = n;
+    int64_t blocks = 0;
+    for (int i = 0; i < n; ++i) {
+        const mmt_conv_wprep& c = items[i];
+        if (!c.w || !c.wf || !c.wb || c.cout <= 0 || c.cin <= 0 || c.cp < c.cout) return MMT_EBADARG;
+        bt.item[i] = c;
+        bt.blk0[i] = (int)blocks;
+        blocks += 2 * (((int64_t)c.cp * c.cin + 255) / 256);
+        if (blocks > INT32_MAX) return MMT_EBADARG;
+    }
+    hipLaunchKernelGGL(conv_wprep_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, bt);
     return launch_status();
 }

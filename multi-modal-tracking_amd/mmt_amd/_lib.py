@@ -63,6 +63,13 @@ class CropParams(ctypes.Structure):
                 ("lut", vp), ("mean", f32 * 3), ("std", f32 * 3), ("out", vp), ("patch", vp), ("crop", vp)]
 
 
+class ConvWprep(ctypes.Structure):
+    _fields_ = [("w", vp), ("b", vp), ("wf", vp), ("wb", vp), ("bp", vp), ("cout", i32), ("cp", i32), ("cin", i32),
+                ("pad_", i32)]
+
+
+WPREP_MAX = 24
+
 _PROTOS = {
     "mmt_gemm": [ctypes.POINTER(GemmParams), i32, vp],
     "mmt_gemm_multi": [ctypes.POINTER(GemmParams), i32, i32, vp],
@@ -84,6 +91,8 @@ _PROTOS = {
     "mmt_ms_deform_attn_forward": [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp],
     "mmt_ms_deform_attn_backward": [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp],
     "mmt_msda_bimodal": [vp, vp, vp, i32, i32, i32, vp],
+    "mmt_msda_bimodal_train_fwd": [vp, vp, vp, vp, vp, i32, i32, vp],
+    "mmt_msda_bimodal_train_bwd": [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp],
     "mmt_conv3x3_c1": [vp, vp, vp, vp, i32, i32, i32, i32, i64, i32, vp],
     "mmt_conv3x3_c1_pair": [vp, vp, vp, vp, i32, i64, vp, vp, vp, vp, i32, i64, i32, i32, i32, i32, vp],
     "mmt_corner_softargmax": [vp, vp, vp, vp, vp, vp, vp, vp, vp, f32, i32, i32, i32, i32, i32, vp],
@@ -91,6 +100,8 @@ _PROTOS = {
     "mmt_im2col3x3_up_bf16": [vp, vp, i32, i32, i32, i32, i32, vp],
     "mmt_upsample_sum_bf16": [vp, vp, i32, i32, i32, i32, i32, vp],
     "mmt_add_up_bf16": [vp, vp, vp, i32, i32, i32, i32, i32, vp],
+    "mmt_im2col3x3_cm_bf16": [vp, vp, i32, i32, i32, i32, i32, vp],
+    "mmt_conv3x3_wprep": [ctypes.POINTER(ConvWprep), i32, vp],
     "mmt_corner_score_train_ws_floats": [i32, i32, i32],
     "mmt_corner_score_train_bwd": [vp, vp, vp, vp, vp, i32, vp, i32, vp, vp, vp, i32, i32, i32, vp],
     "mmt_prroi_pool_forward": [vp, vp, vp, i32, i32, i32, i32, i64, i64, i64, i64, i32, i32, f32, i64, i64, i64, vp],

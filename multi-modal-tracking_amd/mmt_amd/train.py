@@ -695,6 +695,35 @@ class _HipCornerScore(torch.autograd.Function):
         return dx4, dw[:c4].view(ctx.wshape), dw[c4:], da3, da4
 
 
+def _conv_wprep(convs):
+    """The bf16 operand layouts of 3x3 convs [(weight [Cout][Cin][3][3] fp32, bias or None)] in one launch
+    (mmt_conv3x3_wprep): per conv (wf [Cp][9 Cin] forward, wb [Cin][9 Cp] dX, bp [Cp] fp32 padded bias),
+    Cp = Cout rounded up to 8, views of one bf16 and one fp32 buffer."""
+    from ._lib import LIB, ConvWprep, WPREP_MAX, check
+    out = []
+    for i in range(0, len(convs), WPREP_MAX):
+        part = convs[i:i + WPREP_MAX]
+        dims = [(w.shape[0], (w.shape[0] + 7) // 8 * 8, w.shape[1]) for w, _ in part]
+        dev = part[0][0].device
+        wbuf = torch.empty(sum(2 * cp * 9 * cin for _, cp, cin in dims), device=dev, dtype=torch.bfloat16)
+        bbuf = torch.empty(sum(cp for _, cp, _ in dims), device=dev, dtype=torch.float32)
+        items = (ConvWprep * len(part))()
+        ow = ob = 0
+        keep = []
+        for j, ((w, b), (cout, cp, cin)) in enumerate(zip(part, dims)):
+            w = w.detach().contiguous()
+            b = b.detach().float().contiguous() if b is not None else None
+            keep += [w, b]
+            n = cp * 9 * cin
+            wf, wb, bp = wbuf[ow:ow + n].view(cp, 9 * cin), wbuf[ow + n:ow + 2 * n].view(cin, 9 * cp), bbuf[ob:ob + cp]
+            ow, ob = ow + 2 * n, ob + cp
+            items[j] = ConvWprep(w.data_ptr(), b.data_ptr() if b is not None else None, wf.data_ptr(), wb.data_ptr(),
+                                 bp.data_ptr(), cout, cp, cin, 0)
+            out.append((wf, wb, bp))
+        check(LIB.mmt_conv3x3_wprep(items, len(part), _stream()), "mmt_conv3x3_wprep")
+    return out
+
+
 class _HipConv3x3(torch.autograd.Function):
     """nn.Conv2d(Cin, Cout, 3, padding=1) of the corner head's conv() blocks (lib/models/mixformer_cvt/head.py:
     7-20) on NHWC bf16 maps, all three products on the LDS-DMA GEMM: the forward and dX as implicit-GEMM
@@ -710,34 +739,33 @@ class _HipConv3x3(torch.autograd.Function):
     backward zero-fills and copies."""
 
     @staticmethod
-    def forward(ctx, x, w, b, up=1, keep_pad=False):
+    def forward(ctx, x, w, b, up=1, keep_pad=False, prep=None):
         B, H, W, Cin = x.shape
         Cout = w.shape[0]
         if H != W or Cin % 8 or w.shape[2:] != (3, 3) or x.dtype != torch.bfloat16 or up not in (1, 2, 4):
             raise ValueError("HIP conv3x3: square NHWC bf16 maps, input channels multiple of 8, 3x3 kernels, up 1/2/4")
         Cp = (Cout + 7) // 8 * 8  # output channels padded to the GEMM's N granule (the 48 -> 1 adjust convs)
         x = x.contiguous()
-        wr = torch.empty(Cp, 3, 3, Cin, device=x.device, dtype=torch.bfloat16)  # [Cout][ky][kx][Cin]: one cast copy
-        wr[:Cout].copy_(w.detach().permute(0, 2, 3, 1))
-        bp = b.detach().float().contiguous()
-        if Cp != Cout:
-            wr[Cout:].zero_()
-            bp = F.pad(bp, (0, Cp - Cout))
+        # the weight's two bf16 layouts and the padded bias: given (one launch for the whole head, _conv_wprep)
+        # or made here
+        wf, wb, bp = prep if prep is not None else _conv_wprep([(w, b)])[0]
+        if wf.shape != (Cp, 9 * Cin) or wb.shape != (Cin, 9 * Cp):
+            raise ValueError("HIP conv3x3: prepared weights of another conv")
         Ho = H * up
-        y = _conv_gemm(x, wr.view(Cp, 9 * Cin), B, Ho, Cin, Cp, bias=bp, up=up)
-        ctx.save_for_backward(x, w)
-        ctx.up = up
+        y = _conv_gemm(x, wf, B, Ho, Cin, Cp, bias=bp, up=up)
+        ctx.save_for_backward(x, wb)
+        ctx.up, ctx.wshape = up, w.shape
         y = y.view(B, Ho, Ho, Cp)
         return y if (Cp == Cout or keep_pad) else y[..., :Cout]
 
     @staticmethod
     def backward(ctx, dy):
         from ._lib import LIB, check
-        x, w = ctx.saved_tensors
+        x, wb = ctx.saved_tensors
         up = ctx.up
         B, H, W, Cin = x.shape
         Ho = H * up
-        Cout = w.shape[0]
+        Cout = ctx.wshape[0]
         Cp = (Cout + 7) // 8 * 8
         if dy.shape[-1] != Cp:  # a sliced output: back to the padded rows
             dyp = torch.zeros(B, Ho, Ho, Cp, device=dy.device, dtype=torch.bfloat16)
@@ -747,27 +775,58 @@ class _HipConv3x3(torch.autograd.Function):
             dy = dy.to(torch.bfloat16).contiguous()
         dx = None
         if ctx.needs_input_grad[0]:  # the flipped-tap conv of dY with W as [Cin][ky][kx][Cout] (no flip copy)
-            wt = torch.empty(Cin, 3, 3, Cp, device=x.device, dtype=torch.bfloat16)
-            wt[..., :Cout].copy_(w.detach().permute(1, 2, 3, 0))
-            if Cp != Cout:
-                wt[..., Cout:].zero_()
-            dxu = _conv_gemm(dy, wt.view(Cin, 9 * Cp), B, Ho, Cp, Cin, flip=True).view(B, Ho, Ho, Cin)
+            dxu = _conv_gemm(dy, wb, B, Ho, Cp, Cin, flip=True).view(B, Ho, Ho, Cin)
             if up == 1:
                 dx = dxu
             else:
                 dx = torch.empty_like(x)
                 check(LIB.mmt_upsample_sum_bf16(dxu.data_ptr(), dx.data_ptr(), B, H, W, Cin, up, _stream()),
                       "mmt_upsample_sum_bf16")
+        # dW against the channel-major im2col: the GEMM writes [Cout][Cin][3][3], the parameter's layout
         M = B * Ho * Ho
         col = torch.empty(M, 9 * Cin, device=x.device, dtype=torch.bfloat16)
-        if up == 1:
-            check(LIB.mmt_im2col3x3_bf16(x.data_ptr(), col.data_ptr(), B, H, W, Cin, _stream()), "mmt_im2col3x3_bf16")
-        else:
-            check(LIB.mmt_im2col3x3_up_bf16(x.data_ptr(), col.data_ptr(), B, Ho, Ho, Cin, up, _stream()),
-                  "mmt_im2col3x3_up_bf16")
+        check(LIB.mmt_im2col3x3_cm_bf16(x.data_ptr(), col.data_ptr(), B, Ho, Ho, Cin, up, _stream()),
+              "mmt_im2col3x3_cm_bf16")
         dw, db = _weight_grads(dy.view(M, Cp), col, M, Cp, 9 * Cin)
-        dw = dw[:Cout].view(Cout, 3, 3, Cin).permute(0, 3, 1, 2).contiguous()
-        return dx, dw, db[:Cout].contiguous(), None, None
+        return dx, dw[:Cout].view(ctx.wshape), db[:Cout], None, None, None
+
+
+class _HipMSDABimodal(torch.autograd.Function):
+    """The middle of MSDeformAttn_Bimodal in the training step (ms_deform_attn_bimodal.py:97-128; 8 heads, 2 levels,
+    4 points, 64 channels per head), from the bf16 outputs of value_proj / sampling_offsets / attention_weights to
+    the bf16 input of output_proj, on mmt_msda_bimodal_train_fwd / _bwd: softmax of the attention logits, sampling
+    locations ref + off / hw, the bilinear sampling sum, and their backward (grad_value by the deterministic
+    per-pixel gather) -- the arithmetic of F.softmax(aw.float()), ref + off.float() / wh and
+    MSDeformAttnFunction on value.float(), with the casts those imply.  value (B, 2 nq, 512), off (B, nq, 128),
+    awl (B, nq, 64) bf16; ref (nq, 2) fp32 (the device-computed reference points) -> (B, nq, 512) bf16."""
+
+    @staticmethod
+    def forward(ctx, value, off, awl, ref, hw):
+        from ._lib import LIB, check
+        B, nq = off.shape[0], hw * hw
+        for t, shp in ((value, (B, 2 * nq, 512)), (off, (B, nq, 128)), (awl, (B, nq, 64))):
+            if t.dtype != torch.bfloat16 or tuple(t.shape) != shp:
+                raise ValueError("HIP MSDA (training): bf16 value (B, 2 nq, 512), off (B, nq, 128), awl (B, nq, 64)")
+        if ref.dtype != torch.float32 or tuple(ref.shape) != (nq, 2):
+            raise ValueError("HIP MSDA (training): fp32 reference points (nq, 2)")
+        value, off, awl, ref = value.contiguous(), off.contiguous(), awl.contiguous(), ref.contiguous()
+        out = torch.empty(B, nq, 512, device=value.device, dtype=torch.bfloat16)
+        check(LIB.mmt_msda_bimodal_train_fwd(value.data_ptr(), off.data_ptr(), awl.data_ptr(), ref.data_ptr(),
+                                             out.data_ptr(), B, hw, _stream()), "mmt_msda_bimodal_train_fwd")
+        ctx.save_for_backward(value, off, awl, ref)
+        ctx.hw = hw
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        from ._lib import LIB, check
+        value, off, awl, ref = ctx.saved_tensors
+        gout = gout.to(torch.bfloat16).contiguous()
+        gv, goff, gawl = torch.empty_like(value), torch.empty_like(off), torch.empty_like(awl)
+        check(LIB.mmt_msda_bimodal_train_bwd(value.data_ptr(), off.data_ptr(), awl.data_ptr(), ref.data_ptr(),
+                                             gout.data_ptr(), gv.data_ptr(), goff.data_ptr(), gawl.data_ptr(),
+                                             off.shape[0], ctx.hw, _stream()), "mmt_msda_bimodal_train_bwd")
+        return gv, goff, gawl, None, None
 
 
 class _HipAddUp(torch.autograd.Function):
@@ -911,11 +970,17 @@ class HipOps:
         return asym_attention_from_mam(HipOps.mam_attention, qkv, Bh, n_t, heads)
 
     @staticmethod
-    def conv3x3(x, w, b, up=1, keep_pad=False):
+    def conv3x3(x, w, b, up=1, keep_pad=False, prep=None):
         """The corner head's 3x3 convolutions on NHWC maps (_HipConv3x3), operands cast to bf16 (autocast runs
         the nearest upsampling of the pyramid inputs in fp32); up: of the nearest upsampling of x (not
-        materialised); keep_pad: 1-channel outputs in their 8-channel rows."""
-        return _HipConv3x3.apply(x.to(torch.bfloat16), w, b, up, keep_pad)
+        materialised); keep_pad: 1-channel outputs in their 8-channel rows; prep: the weight layouts from
+        conv_wprep (else made per call)."""
+        return _HipConv3x3.apply(x.to(torch.bfloat16), w, b, up, keep_pad, prep)
+
+    @staticmethod
+    def conv_wprep(convs):
+        """[(weight, bias)] of 3x3 convs -> their bf16 operand layouts, one launch (_conv_wprep)."""
+        return _conv_wprep(convs)
 
     @staticmethod
     def add_up(a, b, up):
@@ -944,7 +1009,10 @@ class HipOps:
         training = bn.training or not bn.track_running_stats
         update = bn.training and bn.track_running_stats
         if update:
-            bn.num_batches_tracked.add_(1)
+            if _BN_TRACKED is not None:  # head_forward_nhwc: one multi-tensor add for the whole head
+                _BN_TRACKED.append(bn.num_batches_tracked)
+            else:
+                bn.num_batches_tracked.add_(1)
         keep = update or not training
         C = bn.num_features
         x = x.to(torch.bfloat16)
@@ -954,6 +1022,11 @@ class HipOps:
         y = _HipBatchNormReLU.apply(x.contiguous(), bn.weight, bn.bias, bn.running_mean if keep else None,
                                     bn.running_var if keep else None, bn.momentum, bn.eps, training, C)
         return y if (padded or y.shape[-1] == C) else y[..., :C]
+
+    @staticmethod
+    def msda_bimodal(value, off, awl, ref, hw):
+        """The bimodal MSDA middle of the training step, bf16 in / out (_HipMSDABimodal)."""
+        return _HipMSDABimodal.apply(value, off, awl, ref, hw)
 
     @staticmethod
     def ms_deform_attn(value, hw, loc, aw):
@@ -1204,17 +1277,36 @@ def fusion_forward(fu, s_v, s_i, ops):
     pos = _const(("sine_pos", b, d, h, w), s_v.device,
                  lambda: _sine_pos(b, d, h, w, "cpu").flatten(2).transpose(1, 2).contiguous())
     lpos = torch.cat([pos + fa.level_embed[0].view(1, 1, -1), pos + fa.level_embed[1].view(1, 1, -1)], 1)
-    ref = _ref_points(h, w, b, 2, s_v.device)
     nl = 2 * h * w
 
     def lin(mod, x):  # the encoder's nn.Linear layers on the backbone's GEMM op (bf16 operands, as autocast)
         y = ops.linear(x.reshape(-1, x.shape[-1]).to(ops.dtype).contiguous(), mod.weight, mod.bias)
         return y.view(*x.shape[:-1], -1)
 
+    sa0 = fa.encoder.layers[0].self_attn if len(fa.encoder.layers) else None
+    fused_msda = (getattr(ops, "msda_bimodal", None) is not None and sa0 is not None and h == w and
+                  (sa0.n_heads, sa0.n_levels, sa0.n_points, d) == (8, 2, 4, 512) and h * w <= 484)
+    if fused_msda:  # the reference points of the nl / 2 unique queries, one level: (h w, 2), computed on the
+        # device as _ref_points does (its values, to the last ulp) once per shape
+        ref_q = _const(("ref_q", h, w), s_v.device, lambda: _ref_points(h, w, 1, 2, s_v.device)[0, :h * w, 0, :].contiguous())
+    else:
+        ref = _ref_points(h, w, b, 2, s_v.device)
     for layer in fa.encoder.layers:
         sa = layer.self_attn
         query = src + lpos
         q_bi = torch.cat(torch.chunk(query, 2, 1), dim=2)
+        if fused_msda:  # round 6: softmax, locations, sampling and their backward in the HIP op, bf16 in / out
+            value = lin(sa.value_proj, src)
+            off = lin(sa.sampling_offsets, q_bi)
+            aw = lin(sa.attention_weights, q_bi)
+            ms = ops.msda_bimodal(value.to(ops.dtype), off.to(ops.dtype), aw.to(ops.dtype), ref_q, h)
+            src2 = lin(sa.output_proj, ms)
+            src2 = torch.cat([src2, src2], 1)
+            src = src + layer.dropout1(src2)
+            src = _ln_halves(ops, src, layer.norm1_v, layer.norm1_i)
+            src = src + layer.dropout3(lin(layer.linear2, layer.dropout2(F.relu(lin(layer.linear1, src)))))
+            src = _ln_halves(ops, src, layer.norm2_v, layer.norm2_i)
+            continue
         value = lin(sa.value_proj, src).view(b, nl, sa.n_heads, d // sa.n_heads)
         # The reference repeats the bimodal query's offsets / weights on both halves of its nl queries
         # (ms_deform_attn_bimodal.py:113-118), and the two halves' reference points are the same cells, so both
@@ -1281,10 +1373,26 @@ def _hip_bn_ok(bn):
     return type(bn) is torch.nn.BatchNorm2d and bn.momentum is not None
 
 
+_BN_TRACKED = None  # head_forward_nhwc: the num_batches_tracked counters its batch norms advance, added at its end
+
 HEAD_SCORE_FP32 = True  # head_forward_nhwc: the 48 -> 1 conv5 in fp32 (False: bf16 under autocast, as aten's path)
 
 
 def head_forward_nhwc(hd, x, ops):
+    """head_forward with NHWC maps and the 3x3 convolutions on ops.conv3x3 (HIP): _head_forward_nhwc, with the
+    HIP batch norms' num_batches_tracked advances gathered into one multi-tensor add at the end."""
+    global _BN_TRACKED
+    outer, _BN_TRACKED = _BN_TRACKED, ([] if getattr(ops, "bn_relu", None) is not None else None)
+    try:
+        out = _head_forward_nhwc(hd, x, ops)
+        if _BN_TRACKED:
+            torch._foreach_add_(_BN_TRACKED, 1)
+    finally:
+        _BN_TRACKED = outer
+    return out
+
+
+def _head_forward_nhwc(hd, x, ops):
     """head_forward with NHWC maps and the 3x3 convolutions on ops.conv3x3 (HIP): every conv() block =
     conv (HIP) -> BatchNorm2d + ReLU on ops.bn_relu (HIP, the module's statistics semantics and running-stat
     updates); SyncBatchNorm (its RCCL statistics), FrozenBatchNorm2d and the 1-channel maps call the modules
@@ -1294,9 +1402,15 @@ def head_forward_nhwc(hd, x, ops):
     nhwc = lambda t: t.permute(0, 2, 3, 1)  # noqa: E731
 
     bn_relu = getattr(ops, "bn_relu", None)
+    # every 3x3 conv's bf16 weight layouts in one launch (round 6; the weights are fixed within the step)
+    convs = [m for m in hd.modules() if isinstance(m, torch.nn.Conv2d) and m.kernel_size == (3, 3)]
+    wprep = getattr(ops, "conv_wprep", None)
+    prep = dict(zip(map(id, convs), wprep([(m.weight, m.bias) for m in convs]))) if wprep is not None and convs else {}
+    conv3x3 = lambda m, t, **kw: ops.conv3x3(t, m.weight, m.bias, prep=prep[id(m)], **kw) if id(m) in prep \
+        else ops.conv3x3(t, m.weight, m.bias, **kw)  # noqa: E731
 
     def block(seq, t):  # conv(): Conv2d 3x3 + BN + ReLU (head.py:7-20)
-        y = ops.conv3x3(t.contiguous(), seq[0].weight, seq[0].bias)
+        y = conv3x3(seq[0], t.contiguous())
         bn = seq[1]
         if bn_relu is not None and type(seq[2]) is torch.nn.ReLU and _hip_bn_ok(bn):
             return bn_relu(y, bn)  # HIP batch norm + ReLU on the NHWC map
@@ -1332,7 +1446,7 @@ def head_forward_nhwc(hd, x, ops):
             # bf16 before or after upsampling gives the same values), the adds on HIP, the 1-channel maps kept in
             # their 8-channel rows, and conv5 + up4(adjust3) + up2(adjust4) in one HIP op
             def blk(seq, t, up=1, keep_pad=False):
-                return bn_relu(ops.conv3x3(t, seq[0].weight, seq[0].bias, up, keep_pad), seq[1])
+                return bn_relu(conv3x3(seq[0], t, up=up, keep_pad=keep_pad), seq[1])
             x3 = blk(g("conv3"), add_up(block(g("adjust1"), xh), x2, 1), up=2)  # conv3(up2(adjust1 + x2))
             x4 = blk(g("conv4"), add_up(block(g("adjust2"), xh), x3, 2), up=2)  # conv4(up2(up2(adjust2) + x3))
             m3 = blk(a3[2], block(a3[1], block(a3[0], x2)), keep_pad=True)

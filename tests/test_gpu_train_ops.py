@@ -877,6 +877,105 @@ def test_hip_conv3x3_upsampled_input(B, H, Cin, Cout, up):
         assert err <= tol, (name, err)
 
 
+@pytest.mark.parametrize("B,hw,grid", [(2, 20, False), (16, 20, True), (3, 7, False), (1, 22, True)])
+def test_msda_bimodal_train_matches_generic(B, hw, grid):
+    """HipOps.msda_bimodal (mmt_msda_bimodal_train_fwd / _bwd: softmax, locations, sampling and the backward fused,
+    bf16 in / out) against the step's previous composition -- F.softmax(aw.float()), ref + off.float() / wh and
+    MSDeformAttnFunction (the drop-in mmt_ms_deform_attn_forward / _backward, fp32) on value.float(), with the
+    casts -- on the same bf16 inputs.  grid: integer offsets (Deformable DETR's initial pattern), so that samples
+    sit on pixel edges where the location gradient is discontinuous.  Forward and grad_value within one bf16
+    rounding (relative L2 1e-2; the fp32 sums are the same, only torch's softmax may differ in the last ulp),
+    grad_off / grad_awl 1e-2; two runs bitwise equal (deterministic value gather)."""
+    import torch.nn.functional as F
+    from mmt_amd.functional import MSDeformAttnFunction
+    from mmt_amd.train import HipOps, _ref_points
+    g = torch.Generator().manual_seed(B * 100 + hw)
+    nq = hw * hw
+    value = torch.randn(B, 2 * nq, 512, generator=g).bfloat16().cuda()
+    if grid:
+        base = torch.tensor([[1., 0.], [0., 1.], [-1., 0.], [0., -1.], [1., 1.], [-1., 1.], [-1., -1.], [1., -1.]])
+        pts = torch.arange(1, 5).float().view(1, 1, 4, 1)
+        off = (base.view(8, 1, 1, 2) * pts).expand(8, 2, 4, 2).reshape(1, 1, 128).repeat(B, nq, 1)
+        off = off + torch.randint(-1, 2, off.shape, generator=g).float() * (torch.rand(off.shape, generator=g) < 0.3)
+    else:
+        off = torch.randn(B, nq, 128, generator=g) * 2.0
+    off = off.bfloat16().cuda()
+    awl = torch.randn(B, nq, 64, generator=g).bfloat16().cuda()
+    gout = torch.randn(B, nq, 512, generator=g).bfloat16().cuda()
+    ref4 = _ref_points(hw, hw, B, 2, "cuda")
+    ref_q = ref4[0, :nq, 0, :].contiguous()
+
+    # the previous composition (fp32 MSDA through autograd)
+    vr, orr, ar = value.clone().requires_grad_(True), off.clone().requires_grad_(True), awl.clone().requires_grad_(True)
+    a = F.softmax(ar.view(B, nq, 8, 8).float(), -1).view(B, nq, 8, 2, 4)
+    wh = torch.tensor([hw, hw], dtype=torch.float32, device="cuda")
+    loc = ref4[:, :nq, None, :, None, :] + orr.view(B, nq, 8, 2, 4, 2).float() / wh
+    shapes = torch.tensor([[hw, hw]] * 2, dtype=torch.long, device="cuda")
+    starts = torch.arange(2, dtype=torch.long, device="cuda") * nq
+    yr = MSDeformAttnFunction.apply(vr.view(B, 2 * nq, 8, 64).float(), shapes, starts, loc.contiguous(), a.contiguous(),
+                                    64).to(torch.bfloat16)
+    yr.backward(gout)
+
+    def run():
+        v, o, w = value.clone().requires_grad_(True), off.clone().requires_grad_(True), awl.clone().requires_grad_(True)
+        y = HipOps.msda_bimodal(v, o, w, ref_q, hw)
+        y.backward(gout)
+        return y.detach(), v.grad, o.grad, w.grad
+
+    y1, gv1, go1, ga1 = run()
+    y2, gv2, go2, ga2 = run()
+    torch.cuda.synchronize()
+    for p1, p2 in ((y1, y2), (gv1, gv2), (go1, go2), (ga1, ga2)):
+        assert torch.equal(p1.view(torch.int16), p2.view(torch.int16))
+    for name, a_, r_ in (("out", y1, yr), ("grad_value", gv1, vr.grad), ("grad_off", go1, orr.grad),
+                         ("grad_awl", ga1, ar.grad)):
+        assert a_.dtype == torch.bfloat16 and a_.shape == r_.shape, name
+        a_, r_ = a_.float(), r_.float()
+        err = ((a_ - r_).norm() / r_.norm().clamp_min(1e-30)).item()
+        assert err <= 1e-2, (name, err)
+
+
+@pytest.mark.parametrize("B,H,C,up", [(16, 20, 768, 1), (2, 40, 96, 2), (3, 16, 48, 4), (1, 5, 8, 1)])
+def test_im2col3x3_channel_major_bitwise(B, H, C, up):
+    """mmt_im2col3x3_cm_bf16 (channel-major columns c * 9 + tap, LDS-staged) is the tap-major
+    mmt_im2col3x3_up_bf16 with its columns permuted: bitwise, on the upsampled (H = the output size) map."""
+    L = _lib()
+    g = torch.Generator().manual_seed(B + H + C + up)
+    x = torch.randn(B, H // up, H // up, C, generator=g).bfloat16().cuda()
+    M = B * H * H
+    tm = torch.empty(M, 9 * C, device="cuda", dtype=torch.bfloat16)
+    cm = torch.full((M, 9 * C), float("nan"), device="cuda", dtype=torch.bfloat16)
+    st = torch.cuda.current_stream().cuda_stream
+    L.check(L.LIB.mmt_im2col3x3_up_bf16(x.data_ptr(), tm.data_ptr(), B, H, H, C, up, st), "tap-major")
+    L.check(L.LIB.mmt_im2col3x3_cm_bf16(x.data_ptr(), cm.data_ptr(), B, H, H, C, up, st), "channel-major")
+    torch.cuda.synchronize()
+    want = tm.view(M, 9, C).transpose(1, 2).reshape(M, 9 * C)
+    assert torch.equal(cm.view(torch.int16), want.view(torch.int16))
+
+
+def test_conv_wprep_layouts_bitwise():
+    """mmt_conv3x3_wprep: several convs' weights in one launch -> wf [Cp][ky][kx][Cin] and wb [Cin][ky][kx][Cp]
+    (bf16, RNE as .to(bfloat16)), rows / columns past Cout zero, bp = the bias zero-padded (no bias: zeros)."""
+    from mmt_amd.train import _conv_wprep
+    g = torch.Generator().manual_seed(5)
+    shapes = [(384, 768), (1, 48), (96, 192), (8, 8), (3, 16)]
+    convs = [(torch.randn(co, ci, 3, 3, generator=g).cuda(), torch.randn(co, generator=g).cuda() if k != 4 else None)
+             for k, (co, ci) in enumerate(shapes)]
+    out = _conv_wprep(convs)
+    torch.cuda.synchronize()
+    for (w, b), (wf, wb, bp) in zip(convs, out):
+        co, ci = w.shape[:2]
+        cp = (co + 7) // 8 * 8
+        wpad = torch.zeros(cp, ci, 3, 3, device="cuda")
+        wpad[:co] = w
+        assert torch.equal(wf.view(torch.int16), wpad.permute(0, 2, 3, 1).reshape(cp, 9 * ci).bfloat16().view(torch.int16))
+        assert torch.equal(wb.view(torch.int16), wpad.permute(1, 2, 3, 0).reshape(ci, 9 * cp).bfloat16().view(torch.int16))
+        want = torch.zeros(cp, device="cuda")
+        if b is not None:
+            want[:co] = b
+        assert torch.equal(bp, want)
+
+
 @pytest.mark.parametrize("B,H,C,up", [(16, 40, 96, 2), (2, 20, 192, 1), (3, 80, 48, 4)])
 def test_hip_add_up(B, H, C, up):
     """HipOps.add_up(a, b, up) = bf16(up(a) + b) and its backward (db = dout, da = the up x up block sums of dout,

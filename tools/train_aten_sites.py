@@ -19,7 +19,7 @@ import torch  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=16)
-    ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--top", type=int, default=60)
     args = ap.parse_args()
     from torch.profiler import ProfilerActivity, profile
     from mmt_amd.model import build_mixformer_vit_rgbt, hot_path_cfg
@@ -55,7 +55,18 @@ def main():
         torch.cuda.synchronize()
     # every aten op with device time: attributed to its autograd backward node (the enclosing
     # "autograd::engine::evaluate_function: <Node>" event) or, in the forward, to its innermost mmt_amd frames
-    import collections
+    def site_of(e):  # the innermost two site:: ranges enclosing a forward event
+        par, names = e.cpu_parent, []
+        while par is not None and len(names) < 2:
+            if par.name.startswith("site::"):
+                names.append(par.name[6:])
+            par = par.cpu_parent
+        return " <- ".join(names) if names else "?"
+    # backward nodes carry the sequence number of the forward op that created them: name the node's forward site
+    fwd_site = {}
+    for e in prof.events():
+        if e.name.startswith("aten::") and getattr(e, "sequence_nr", -1) >= 0 and e.sequence_nr not in fwd_site:
+            fwd_site[e.sequence_nr] = "%s@%s" % (e.name[6:], site_of(e))
     agg = collections.defaultdict(lambda: [0.0, 0, set()])
     top_total = 0.0
     for e in prof.events():
@@ -70,15 +81,13 @@ def main():
         while par is not None:
             if par.name.startswith("autograd::engine::evaluate_function"):
                 where = "bwd " + par.name.split(": ", 1)[-1]
+                seq = getattr(par, "sequence_nr", -1)
+                if seq in fwd_site:
+                    where += " <- " + fwd_site[seq]
                 break
             par = par.cpu_parent
         if where is None:
-            par, names = e.cpu_parent, []
-            while par is not None and len(names) < 2:
-                if par.name.startswith("site::"):
-                    names.append(par.name[6:])
-                par = par.cpu_parent
-            where = "fwd " + (" <- ".join(names) if names else "?")
+            where = "fwd " + site_of(e)
         a = agg[where]
         a[0] += sdev
         a[1] += 1
@@ -86,7 +95,7 @@ def main():
         top_total += sdev
     print("aten self device time, one step: %.1f us" % top_total)
     for where, (us, n, names) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:args.top]:
-        print("%9.1f us %4d  %-90s %s" % (us, n, where[:90], ",".join(sorted(names))[:100]))
+        print("%9.1f us %4d  %-110s %s" % (us, n, where[:110], ",".join(sorted(names))[:100]))
 
 
 if __name__ == "__main__":
