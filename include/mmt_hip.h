@@ -364,13 +364,14 @@ int mmt_msda_bimodal(const float* offw, const void* value, void* out, int B, int
  * mmt_amd.train.fusion_forward; 8 heads x 2 levels x 4 points, 64 channels per head, levels hw x hw, nq = hw^2
  * <= 484), bf16 in and out: a = softmax(awl) per (query, head), loc = ref + off / hw, out = the sampled sum
  * (msda_generic_kernel's arithmetic).  value [B][2][nq][512], off [B][nq][128], awl [B][nq][64], ref fp32
- * [nq][2], out [B][nq][512].  Backward: grad_value (deterministic per-pixel gather), grad_off = gloc / hw,
+ * [nq][2], out [B][nq][512]; off / awl rows (and grad_off / grad_awl rows) off_pitch / awl_pitch elements apart
+ * (the [offsets | logits] columns of one Linear output: pitch 192).  Backward: grad_value (deterministic per-pixel gather), grad_off = gloc / hw,
  * grad_awl = the softmax backward of the per-sample weight gradients, all bf16. */
-int mmt_msda_bimodal_train_fwd(const void* value, const void* off, const void* awl, const float* ref, void* out, int B,
-                               int hw, void* stream);
-int mmt_msda_bimodal_train_bwd(const void* value, const void* off, const void* awl, const float* ref,
-                               const void* grad_out, void* grad_value, void* grad_off, void* grad_awl, int B, int hw,
-                               void* stream);
+int mmt_msda_bimodal_train_fwd(const void* value, const void* off, int off_pitch, const void* awl, int awl_pitch,
+                               const float* ref, void* out, int B, int hw, void* stream);
+int mmt_msda_bimodal_train_bwd(const void* value, const void* off, int off_pitch, const void* awl, int awl_pitch,
+                               const float* ref, const void* grad_out, void* grad_value, void* grad_off, void* grad_awl,
+                               int B, int hw, void* stream);
 
 /* ---------------------------------------------------------------- corner head / SPM
  * Cout=1 3x3/pad-1 conv (+bias, BN folded) + ReLU on NHWC input [G][B][h*h][cin] (pixel stride
@@ -503,6 +504,28 @@ typedef struct mmt_conv_wprep_batch {  /* kernel argument (by value) */
     int32_t n;
 } mmt_conv_wprep_batch;
 int mmt_conv3x3_wprep(const mmt_conv_wprep* items, int n, void* stream);
+
+/* The training step's deformable-encoder glue (deformable_encoder_lnspecific.py:131-160,
+ * ms_deform_attn_bimodal.py:97-128; mmt_amd.train.fusion_forward), one pass each, fp32 streams / bf16 branches:
+ *   mmt_ft_query_prep: src [B][2][nq][d], lpos [2][nq][d] -> qbi [B][nq][2d] = bf16(src + lpos) of both halves
+ *     side by side (the bimodal query), srcb = bf16(src); _bwd: dsrc = dthrough (optional) + unshuffle(dqbi) +
+ *     dsrcb, dlpos [2][nq][d] = the batch sum of unshuffle(dqbi) (fixed order).
+ *   mmt_ft_drop_residual: out [B][rows][d] = x + bf16(dropout(y)); dup: y [B][rows/2][d] on both halves;
+ *     _bwd: dy = bf16(dropout'(bf16(dout))), dup: the halves' sum.
+ *   mmt_ft_relu_drop: out = bf16(dropout(h)) (h >= 0, the ReLU epilogue's output); _bwd: dh = (h > 0) ?
+ *     bf16(dropout'(dy)) : 0.
+ * Dropout: keep with probability 1 - p (16-bit draws from a counter hash of rng = {seed, counter} on the device,
+ * the call site's salt and the element index), survivors * 1 / (1 - p); rng NULL or p == 0: no dropout. */
+int mmt_ft_query_prep(const float* src, const float* lpos, void* qbi, void* srcb, int B, int nq, int d, void* stream);
+int mmt_ft_query_prep_bwd(const void* dqbi, const void* dsrcb, const float* dthrough, float* dsrc, float* dlpos, int B,
+                          int nq, int d, void* stream);
+int mmt_ft_drop_residual(const float* x, const void* y, float* out, const int64_t* rng, int salt, float p, int B,
+                         int rows, int d, int dup, void* stream);
+int mmt_ft_drop_residual_bwd(const float* dout, void* dy, const int64_t* rng, int salt, float p, int B, int rows, int d,
+                             int dup, void* stream);
+int mmt_ft_relu_drop(const void* h, void* out, const int64_t* rng, int salt, float p, int64_t n, void* stream);
+int mmt_ft_relu_drop_bwd(const void* dy, const void* h, void* dh, const int64_t* rng, int salt, float p, int64_t n,
+                         void* stream);
 /* Backward of nearest upsampling x up on NHWC bf16: out [B][Hi][Wi][C] = the up x up block sums of in
  * [B][Hi*up][Wi*up][C] (fp32 sums in a fixed order, bf16 out). */
 int mmt_upsample_sum_bf16(const void* in, void* out, int B, int Hi, int Wi, int C, int up, void* stream);

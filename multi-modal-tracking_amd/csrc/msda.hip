@@ -439,16 +439,16 @@ MMT_DEV void mt_unpack8(uint4 u, float* v) {
 // forward: one wave per (b, q); lane = (head m, 8-channel group)
 __global__ __launch_bounds__(64) void msda_train_fwd_kernel(const bf16_t* __restrict__ value, const bf16_t* __restrict__ off,
                                                             const bf16_t* __restrict__ awl, const float* __restrict__ ref,
-                                                            bf16_t* __restrict__ out, int hw) {
+                                                            bf16_t* __restrict__ out, int hw, int op, int ap) {
     const int nq = hw * hw;
     const int64_t row = blockIdx.x;  // b * nq + q
     const int b = (int)(row / nq), q = (int)(row % nq);
     const int t = threadIdx.x, m = t >> 3, c0 = (t & 7) * 8;
     float lg[8], a[8];
-    mt_load_logits(awl + row * (MT_NH * 8) + m * 8, lg);
+    mt_load_logits(awl + row * ap + m * 8, lg);
     mt_softmax8(lg, a);
     const float rx = ref[2 * q], ry = ref[2 * q + 1];
-    const bf16_t* ob = off + row * (MT_NH * MT_NL * MT_NP * 2) + m * (MT_NL * MT_NP * 2);
+    const bf16_t* ob = off + row * op + m * (MT_NL * MT_NP * 2);
     float col[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) col[j] = 0.f;
@@ -487,16 +487,16 @@ __global__ __launch_bounds__(64) void msda_train_bwd_samp_kernel(const bf16_t* _
                                                                  const float* __restrict__ ref,
                                                                  const bf16_t* __restrict__ gout,
                                                                  bf16_t* __restrict__ goff, bf16_t* __restrict__ gawl,
-                                                                 int hw) {
+                                                                 int hw, int op, int ap) {
     const int nq = hw * hw;
     const int64_t row = blockIdx.x;
     const int b = (int)(row / nq), q = (int)(row % nq);
     const int t = threadIdx.x, m = t >> 3, cg = t & 7, c0 = cg * 8;
     float lg[8], a[8];
-    mt_load_logits(awl + row * (MT_NH * 8) + m * 8, lg);
+    mt_load_logits(awl + row * ap + m * 8, lg);
     mt_softmax8(lg, a);
     const float rx = ref[2 * q], ry = ref[2 * q + 1];
-    const bf16_t* ob = off + row * (MT_NH * MT_NL * MT_NP * 2) + m * (MT_NL * MT_NP * 2);
+    const bf16_t* ob = off + row * op + m * (MT_NL * MT_NP * 2);
     float g[8];
     mt_unpack8(*(const uint4*)(gout + row * MT_CM + m * MT_DH + c0), g);
     float gaw[8], gx[8], gy[8];
@@ -554,8 +554,8 @@ __global__ __launch_bounds__(64) void msda_train_bwd_samp_kernel(const bf16_t* _
 #pragma unroll
     for (int i = 0; i < 8; ++i)
         if (i == cg) dl = a[i] * (gaw[i] - s), dx = gx[i] / (float)hw, dy = gy[i] / (float)hw;
-    gawl[row * (MT_NH * 8) + m * 8 + cg] = f2bf(dl);
-    *(uint32_t*)(goff + row * (MT_NH * MT_NL * MT_NP * 2) + (m * 8 + cg) * 2) = pack_bf16x2(dx, dy);
+    gawl[row * ap + m * 8 + cg] = f2bf(dl);
+    *(uint32_t*)(goff + row * op + (m * 8 + cg) * 2) = pack_bf16x2(dx, dy);
 }
 
 // backward, grad_value: one workgroup per (b, m, level) -- every sample of the level's nq queries expanded into its
@@ -567,7 +567,7 @@ __global__ __launch_bounds__(MT_VT) void msda_train_bwd_value_kernel(const bf16_
                                                                      const bf16_t* __restrict__ awl,
                                                                      const float* __restrict__ ref,
                                                                      const bf16_t* __restrict__ gout,
-                                                                     bf16_t* __restrict__ gvalue, int hw) {
+                                                                     bf16_t* __restrict__ gvalue, int hw, int op, int ap) {
     __shared__ __attribute__((aligned(16))) bf16_t gl[MT_NQ_MAX * MT_DH];  // grad_out rows of head m
     __shared__ float al[MT_NQ_MAX * MT_NP];                                  // a of this level's points
     __shared__ int ekey[MT_NQ_MAX * MT_NP * 4];
@@ -582,7 +582,7 @@ __global__ __launch_bounds__(MT_VT) void msda_train_bwd_value_kernel(const bf16_
     }
     for (int q = t; q < nq; q += MT_VT) {
         float lg[8], a[8];
-        mt_load_logits(awl + (row0 + q) * (MT_NH * 8) + m * 8, lg);
+        mt_load_logits(awl + (row0 + q) * ap + m * 8, lg);
         mt_softmax8(lg, a);
 #pragma unroll
         for (int p = 0; p < MT_NP; ++p) al[q * MT_NP + p] = a[l * MT_NP + p];
@@ -593,7 +593,7 @@ __global__ __launch_bounds__(MT_VT) void msda_train_bwd_value_kernel(const bf16_
     // the taps of sample j = q * 4 + p: f(k, pixel, w_k) for the valid ones (msda_bwd_value_kernel's rules)
     auto taps = [&](int j, auto&& f) {
         const int q = j >> 2, p = j & 3;
-        const bf16_t* o = off + (row0 + q) * (MT_NH * MT_NL * MT_NP * 2) + ((m * MT_NL + l) * MT_NP + p) * 2;
+        const bf16_t* o = off + (row0 + q) * op + ((m * MT_NL + l) * MT_NP + p) * 2;
         const MtGeom g = mt_geom(ref[2 * q], ref[2 * q + 1], bf2f(o[0]), bf2f(o[1]), hw);
         if (!g.in) return;
         const int hl = (int)floorf(g.h), wl = (int)floorf(g.w), hh_ = hl + 1, wh_ = wl + 1;
@@ -684,28 +684,34 @@ __global__ __launch_bounds__(MT_VT) void msda_train_bwd_value_kernel(const bf16_
 
 }  // namespace
 
-extern "C" int mmt_msda_bimodal_train_fwd(const void* value, const void* off, const void* awl, const float* ref,
-                                          void* out, int B, int hw, void* stream) {
+extern "C" int mmt_msda_bimodal_train_fwd(const void* value, const void* off, int off_pitch, const void* awl,
+                                          int awl_pitch, const float* ref, void* out, int B, int hw, void* stream) {
     if (!value || !off || !awl || !ref || !out || B <= 0 || hw <= 0 || hw * hw > MT_NQ_MAX) return MMT_EBADARG;
-    if (((uintptr_t)value | (uintptr_t)awl | (uintptr_t)out) & 15) return MMT_EBADARG;
+    if (off_pitch < 128 || off_pitch % 2 || awl_pitch < 64 || awl_pitch % 8) return MMT_EBADARG;
+    if (((uintptr_t)value | (uintptr_t)awl | (uintptr_t)out) & 15 || (uintptr_t)off & 3) return MMT_EBADARG;
     hipLaunchKernelGGL(msda_train_fwd_kernel, dim3((unsigned)(B * hw * hw)), dim3(64), 0, (hipStream_t)stream,
-                       (const bf16_t*)value, (const bf16_t*)off, (const bf16_t*)awl, ref, (bf16_t*)out, hw);
+                       (const bf16_t*)value, (const bf16_t*)off, (const bf16_t*)awl, ref, (bf16_t*)out, hw, off_pitch,
+                       awl_pitch);
     return launch_status();
 }
 
-extern "C" int mmt_msda_bimodal_train_bwd(const void* value, const void* off, const void* awl, const float* ref,
-                                          const void* grad_out, void* grad_value, void* grad_off, void* grad_awl, int B,
-                                          int hw, void* stream) {
+extern "C" int mmt_msda_bimodal_train_bwd(const void* value, const void* off, int off_pitch, const void* awl,
+                                          int awl_pitch, const float* ref, const void* grad_out, void* grad_value,
+                                          void* grad_off, void* grad_awl, int B, int hw, void* stream) {
     if (!value || !off || !awl || !ref || !grad_out || !grad_value || !grad_off || !grad_awl || B <= 0 || hw <= 0 ||
         hw * hw > MT_NQ_MAX)
         return MMT_EBADARG;
-    if (((uintptr_t)value | (uintptr_t)awl | (uintptr_t)grad_out | (uintptr_t)grad_off) & 15) return MMT_EBADARG;
+    if (off_pitch < 128 || off_pitch % 2 || awl_pitch < 64 || awl_pitch % 8) return MMT_EBADARG;
+    if (((uintptr_t)value | (uintptr_t)awl | (uintptr_t)grad_out | (uintptr_t)grad_awl) & 15 ||
+        ((uintptr_t)off | (uintptr_t)grad_off) & 3)
+        return MMT_EBADARG;
     hipStream_t st = (hipStream_t)stream;
     hipLaunchKernelGGL(msda_train_bwd_samp_kernel, dim3((unsigned)(B * hw * hw)), dim3(64), 0, st, (const bf16_t*)value,
                        (const bf16_t*)off, (const bf16_t*)awl, ref, (const bf16_t*)grad_out, (bf16_t*)grad_off,
-                       (bf16_t*)grad_awl, hw);
+                       (bf16_t*)grad_awl, hw, off_pitch, awl_pitch);
     hipLaunchKernelGGL(msda_train_bwd_value_kernel, dim3(MT_NL, MT_NH, (unsigned)B), dim3(MT_VT), 0, st,
-                       (const bf16_t*)off, (const bf16_t*)awl, ref, (const bf16_t*)grad_out, (bf16_t*)grad_value, hw);
+                       (const bf16_t*)off, (const bf16_t*)awl, ref, (const bf16_t*)grad_out, (bf16_t*)grad_value, hw,
+                       off_pitch, awl_pitch);
     return launch_status();
 }
 

@@ -91,8 +91,14 @@ _PROTOS = {
     "mmt_ms_deform_attn_forward": [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp],
     "mmt_ms_deform_attn_backward": [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp],
     "mmt_msda_bimodal": [vp, vp, vp, i32, i32, i32, vp],
-    "mmt_msda_bimodal_train_fwd": [vp, vp, vp, vp, vp, i32, i32, vp],
-    "mmt_msda_bimodal_train_bwd": [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp],
+    "mmt_msda_bimodal_train_fwd": [vp, vp, i32, vp, i32, vp, vp, i32, i32, vp],
+    "mmt_msda_bimodal_train_bwd": [vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, i32, i32, vp],
+    "mmt_ft_query_prep": [vp, vp, vp, vp, i32, i32, i32, vp],
+    "mmt_ft_query_prep_bwd": [vp, vp, vp, vp, vp, i32, i32, i32, vp],
+    "mmt_ft_drop_residual": [vp, vp, vp, vp, i32, f32, i32, i32, i32, i32, vp],
+    "mmt_ft_drop_residual_bwd": [vp, vp, vp, i32, f32, i32, i32, i32, i32, vp],
+    "mmt_ft_relu_drop": [vp, vp, vp, i32, f32, i64, vp],
+    "mmt_ft_relu_drop_bwd": [vp, vp, vp, vp, i32, f32, i64, vp],
     "mmt_conv3x3_c1": [vp, vp, vp, vp, i32, i32, i32, i32, i64, i32, vp],
     "mmt_conv3x3_c1_pair": [vp, vp, vp, vp, i32, i64, vp, vp, vp, vp, i32, i64, i32, i32, i32, i32, vp],
     "mmt_corner_softargmax": [vp, vp, vp, vp, vp, vp, vp, vp, vp, f32, i32, i32, i32, i32, i32, vp],

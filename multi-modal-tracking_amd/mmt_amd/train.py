@@ -793,40 +793,215 @@ class _HipConv3x3(torch.autograd.Function):
 
 class _HipMSDABimodal(torch.autograd.Function):
     """The middle of MSDeformAttn_Bimodal in the training step (ms_deform_attn_bimodal.py:97-128; 8 heads, 2 levels,
-    4 points, 64 channels per head), from the bf16 outputs of value_proj / sampling_offsets / attention_weights to
-    the bf16 input of output_proj, on mmt_msda_bimodal_train_fwd / _bwd: softmax of the attention logits, sampling
-    locations ref + off / hw, the bilinear sampling sum, and their backward (grad_value by the deterministic
-    per-pixel gather) -- the arithmetic of F.softmax(aw.float()), ref + off.float() / wh and
-    MSDeformAttnFunction on value.float(), with the casts those imply.  value (B, 2 nq, 512), off (B, nq, 128),
-    awl (B, nq, 64) bf16; ref (nq, 2) fp32 (the device-computed reference points) -> (B, nq, 512) bf16."""
+    4 points, 64 channels per head), from the bf16 outputs of value_proj and the [sampling_offsets |
+    attention_weights] Linear to the bf16 input of output_proj, on mmt_msda_bimodal_train_fwd / _bwd: softmax of the
+    attention logits, sampling locations ref + off / hw, the bilinear sampling sum, and their backward (grad_value
+    by the deterministic per-pixel gather) -- the arithmetic of F.softmax(aw.float()), ref + off.float() / wh and
+    MSDeformAttnFunction on value.float(), with the casts those imply.  value (B, 2 nq, 512), offw (B, nq, >= 192)
+    bf16 with the offsets in columns [0, 128) and the logits in [128, 192) (row pitch = its last stride); ref
+    (nq, 2) fp32 (the device-computed reference points) -> (B, nq, 512) bf16."""
 
     @staticmethod
-    def forward(ctx, value, off, awl, ref, hw):
+    def forward(ctx, value, offw, ref, hw):
         from ._lib import LIB, check
-        B, nq = off.shape[0], hw * hw
-        for t, shp in ((value, (B, 2 * nq, 512)), (off, (B, nq, 128)), (awl, (B, nq, 64))):
-            if t.dtype != torch.bfloat16 or tuple(t.shape) != shp:
-                raise ValueError("HIP MSDA (training): bf16 value (B, 2 nq, 512), off (B, nq, 128), awl (B, nq, 64)")
+        B, nq = offw.shape[0], hw * hw
+        if value.dtype != torch.bfloat16 or tuple(value.shape) != (B, 2 * nq, 512) or offw.dtype != torch.bfloat16 \
+                or offw.shape[1:] != (nq, 192):
+            raise ValueError("HIP MSDA (training): bf16 value (B, 2 nq, 512) and offsets | logits (B, nq, 192)")
         if ref.dtype != torch.float32 or tuple(ref.shape) != (nq, 2):
             raise ValueError("HIP MSDA (training): fp32 reference points (nq, 2)")
-        value, off, awl, ref = value.contiguous(), off.contiguous(), awl.contiguous(), ref.contiguous()
+        value, offw, ref = value.contiguous(), offw.contiguous(), ref.contiguous()
         out = torch.empty(B, nq, 512, device=value.device, dtype=torch.bfloat16)
-        check(LIB.mmt_msda_bimodal_train_fwd(value.data_ptr(), off.data_ptr(), awl.data_ptr(), ref.data_ptr(),
-                                             out.data_ptr(), B, hw, _stream()), "mmt_msda_bimodal_train_fwd")
-        ctx.save_for_backward(value, off, awl, ref)
+        check(LIB.mmt_msda_bimodal_train_fwd(value.data_ptr(), offw.data_ptr(), 192, offw[..., 128:].data_ptr(), 192,
+                                             ref.data_ptr(), out.data_ptr(), B, hw, _stream()),
+              "mmt_msda_bimodal_train_fwd")
+        ctx.save_for_backward(value, offw, ref)
         ctx.hw = hw
         return out
 
     @staticmethod
     def backward(ctx, gout):
         from ._lib import LIB, check
-        value, off, awl, ref = ctx.saved_tensors
+        value, offw, ref = ctx.saved_tensors
         gout = gout.to(torch.bfloat16).contiguous()
-        gv, goff, gawl = torch.empty_like(value), torch.empty_like(off), torch.empty_like(awl)
-        check(LIB.mmt_msda_bimodal_train_bwd(value.data_ptr(), off.data_ptr(), awl.data_ptr(), ref.data_ptr(),
-                                             gout.data_ptr(), gv.data_ptr(), goff.data_ptr(), gawl.data_ptr(),
-                                             off.shape[0], ctx.hw, _stream()), "mmt_msda_bimodal_train_bwd")
-        return gv, goff, gawl, None, None
+        gv, gow = torch.empty_like(value), torch.empty_like(offw)
+        check(LIB.mmt_msda_bimodal_train_bwd(value.data_ptr(), offw.data_ptr(), 192, offw[..., 128:].data_ptr(), 192,
+                                             ref.data_ptr(), gout.data_ptr(), gv.data_ptr(), gow.data_ptr(),
+                                             gow[..., 128:].data_ptr(), offw.shape[0], ctx.hw, _stream()),
+              "mmt_msda_bimodal_train_bwd")
+        return gv, gow, None, None
+
+
+_DROP_RNG = {}  # device -> int64 [2] {seed, counter} of the encoder's dropout draws (csrc/fusion_train.hip)
+
+
+def _drop_rng(device):
+    """The device's dropout key {seed, counter}: the seed drawn from torch's default generator at first use (so
+    torch.manual_seed makes runs repeatable), the counter advanced once per training forward (_drop_advance)."""
+    st = _DROP_RNG.get(str(device))
+    if st is None:
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        st = _DROP_RNG[str(device)] = torch.tensor([seed, 0], dtype=torch.int64).to(device)
+    return st
+
+
+class _HipQueryPrep(torch.autograd.Function):
+    """The encoder layer's inputs from its fp32 stream src (B, 2 nq, d) and the level-embedded positions lpos
+    (1, 2 nq, d) (deformable_encoder_lnspecific.py:131-136, ms_deform_attn_bimodal.py:97-105): q_bi = the bimodal
+    query cat(chunk(src + lpos, 2, 1), 2) in bf16 (B, nq, 2 d), src in bf16 (value_proj's operand) and src handed
+    through for the residual -- one pass (mmt_ft_query_prep); the backward sums the three gradients of src and
+    reduces lpos's over the batch in one pass (mmt_ft_query_prep_bwd)."""
+
+    @staticmethod
+    def forward(ctx, src, lpos):
+        from ._lib import LIB, check
+        B, n2, d = src.shape
+        src, lp = src.contiguous(), lpos.detach().contiguous()
+        qbi = torch.empty(B, n2 // 2, 2 * d, device=src.device, dtype=torch.bfloat16)
+        srcb = torch.empty(B, n2, d, device=src.device, dtype=torch.bfloat16)
+        check(LIB.mmt_ft_query_prep(src.data_ptr(), lp.data_ptr(), qbi.data_ptr(), srcb.data_ptr(), B, n2 // 2, d,
+                                    _stream()), "mmt_ft_query_prep")
+        ctx.set_materialize_grads(False)
+        ctx.shape = (B, n2, d)
+        return qbi, srcb, src
+
+    @staticmethod
+    def backward(ctx, dqbi, dsrcb, dthrough):
+        from ._lib import LIB, check
+        B, n2, d = ctx.shape
+        dev = (dqbi if dqbi is not None else dsrcb).device
+        z = lambda shp: torch.zeros(shp, device=dev, dtype=torch.bfloat16)  # noqa: E731 (an unused output)
+        dqbi = dqbi.to(torch.bfloat16).contiguous() if dqbi is not None else z((B, n2 // 2, 2 * d))
+        dsrcb = dsrcb.to(torch.bfloat16).contiguous() if dsrcb is not None else z((B, n2, d))
+        dt = dthrough.float().contiguous() if dthrough is not None else None
+        dsrc = torch.empty(B, n2, d, device=dev, dtype=torch.float32)
+        dlpos = torch.empty(1, n2, d, device=dev, dtype=torch.float32)
+        check(LIB.mmt_ft_query_prep_bwd(dqbi.data_ptr(), dsrcb.data_ptr(), dt.data_ptr() if dt is not None else None,
+                                        dsrc.data_ptr(), dlpos.data_ptr(), B, n2 // 2, d, _stream()),
+              "mmt_ft_query_prep_bwd")
+        return dsrc, dlpos
+
+
+class _HipDropResidual(torch.autograd.Function):
+    """x + Dropout(y) of the encoder layer's branches (deformable_encoder_lnspecific.py:139-148): x the fp32 stream
+    (B, rows, d), y the bf16 branch (B, rows, d), or with dup its (B, rows / 2, d) unique rows repeated on both halves
+    (the bimodal query's output_proj, cat([y, y], 1)); p: the module's dropout rate when training, else 0 (one
+    pass, mmt_ft_drop_residual; backward: x's gradient handed through, y's one pass)."""
+
+    @staticmethod
+    def forward(ctx, x, y, p, salt, dup):
+        from ._lib import LIB, check
+        B, rows, d = x.shape
+        x, y = x.contiguous(), y.to(torch.bfloat16).contiguous()
+        rng = _drop_rng(x.device) if p > 0 else None
+        out = torch.empty_like(x)
+        check(LIB.mmt_ft_drop_residual(x.data_ptr(), y.data_ptr(), out.data_ptr(),
+                                       rng.data_ptr() if rng is not None else None, salt, float(p), B, rows, d, int(dup),
+                                       _stream()), "mmt_ft_drop_residual")
+        ctx.p, ctx.salt, ctx.dup, ctx.yshape = p, salt, dup, y.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        from ._lib import LIB, check
+        dout = dout.float().contiguous()
+        B, rows, d = dout.shape
+        rng = _drop_rng(dout.device) if ctx.p > 0 else None
+        dy = torch.empty(ctx.yshape, device=dout.device, dtype=torch.bfloat16)
+        check(LIB.mmt_ft_drop_residual_bwd(dout.data_ptr(), dy.data_ptr(), rng.data_ptr() if rng is not None else None,
+                                           ctx.salt, float(ctx.p), B, rows, d, int(ctx.dup), _stream()),
+              "mmt_ft_drop_residual_bwd")
+        return dout, dy, None, None, None
+
+
+class _HipEncoderFFN(torch.autograd.Function):
+    """x + Dropout3(linear2(Dropout2(ReLU(linear1(x))))) of the encoder layer (deformable_encoder_lnspecific.py:
+    145-148; forward_ffn), x the fp32 stream (M, d): linear1 with the ReLU epilogue, the hidden dropout one pass
+    (mmt_ft_relu_drop), linear2, the residual dropout-add one pass (mmt_ft_drop_residual); backward: the branch's
+    dropout backward, linear2's products, the hidden dropout + ReLU backward in one pass, linear1's dX GEMM with
+    the stream gradient added in its epilogue (fp32: the branch gradient is not rounded to bf16 before the add)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, p2, p3, salt):
+        from ._lib import LIB, check
+        M, d = x.shape
+        F_ = w1.shape[0]
+        x = x.contiguous()
+        xb = x.to(torch.bfloat16)
+        wb1, wb2 = _bf16_weight(w1), _bf16_weight(w2)
+        h = _gemm(xb, wb1, M, F_, d, bias=b1.detach(), act=2)  # relu(linear1(x)) in bf16
+        rng = _drop_rng(x.device) if (p2 > 0 or p3 > 0) else None
+        if p2 > 0:
+            hd = torch.empty_like(h)
+            check(LIB.mmt_ft_relu_drop(h.data_ptr(), hd.data_ptr(), rng.data_ptr(), salt + 1, float(p2), h.numel(),
+                                       _stream()), "mmt_ft_relu_drop")
+        else:
+            hd = h
+        y = _gemm(hd, wb2, M, d, F_, bias=b2.detach())
+        out = torch.empty_like(x)
+        check(LIB.mmt_ft_drop_residual(x.data_ptr(), y.data_ptr(), out.data_ptr(),
+                                       rng.data_ptr() if (rng is not None and p3 > 0) else None, salt + 2, float(p3),
+                                       1, M, d, 0, _stream()), "mmt_ft_drop_residual")
+        ctx.save_for_backward(xb, wb1, wb2, h, hd)
+        ctx.p2, ctx.p3, ctx.salt = p2, p3, salt
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        from ._lib import LIB, check
+        xb, wb1, wb2, h, hd = ctx.saved_tensors
+        M, d = xb.shape
+        F_ = wb1.shape[0]
+        dout = dout.float().contiguous()
+        rng = _drop_rng(dout.device) if (ctx.p2 > 0 or ctx.p3 > 0) else None
+        dy = torch.empty(M, d, device=dout.device, dtype=torch.bfloat16)
+        check(LIB.mmt_ft_drop_residual_bwd(dout.data_ptr(), dy.data_ptr(),
+                                           rng.data_ptr() if (rng is not None and ctx.p3 > 0) else None, ctx.salt + 2,
+                                           float(ctx.p3), 1, M, d, 0, _stream()), "mmt_ft_drop_residual_bwd")
+        dhd = _dx(dy, wb2, M, d, F_)
+        dw2, db2 = _weight_grads(dy, hd, M, d, F_)
+        dh = torch.empty_like(dhd)
+        check(LIB.mmt_ft_relu_drop_bwd(dhd.data_ptr(), h.data_ptr(), dh.data_ptr(),
+                                       rng.data_ptr() if (rng is not None and ctx.p2 > 0) else None, ctx.salt + 1,
+                                       float(ctx.p2), dh.numel(), _stream()), "mmt_ft_relu_drop_bwd")
+        dw1, db1 = _weight_grads(dh, xb, M, F_, d)
+        dx = None
+        if ctx.needs_input_grad[0]:  # dX = dh W1 + the stream gradient (fp32 epilogue residual)
+            if MN_MAJOR:
+                dx = _gemm(dh, wb1, M, d, F_, r=dout, out_f32=True, w_t=1, ldw=d)
+            else:
+                dx = _gemm(dh, _transpose(wb1, F_, d), M, d, F_, r=dout, out_f32=True)
+        return dx, dw1, db1, dw2, db2, None, None, None
+
+
+class _HipLinearCat(torch.autograd.Function):
+    """Two nn.Linear layers on the same input as one GEMM (the bimodal query's sampling_offsets and
+    attention_weights, ms_deform_attn_bimodal.py:99-100): y = x [W0; W1]^T + [b0; b1] (bf16 x (M, K) -> bf16
+    (M, N0 + N1)); one dX GEMM (the two input gradients summed in its K loop) and one dW GEMM, whose rows are the
+    two weights' gradients."""
+
+    @staticmethod
+    def forward(ctx, x, w0, b0, w1, b1):
+        M, K = x.shape
+        N0, N1 = w0.shape[0], w1.shape[0]
+        x = x.contiguous()
+        wb = torch.cat([_bf16_weight(w0), _bf16_weight(w1)], 0)
+        bias = torch.cat([b0.detach().float(), b1.detach().float()], 0)
+        y = _gemm(x, wb, M, N0 + N1, K, bias=bias)
+        ctx.save_for_backward(x, wb)
+        ctx.n0 = N0
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wb = ctx.saved_tensors
+        M, K = x.shape
+        N = wb.shape[0]
+        dy = dy.to(torch.bfloat16).contiguous()
+        dx = _dx(dy, wb, M, N, K) if ctx.needs_input_grad[0] else None
+        dw, db = _weight_grads(dy, x, M, N, K)
+        n0 = ctx.n0
+        return dx, dw[:n0], db[:n0], dw[n0:], db[n0:]
 
 
 class _HipAddUp(torch.autograd.Function):
@@ -1024,9 +1199,14 @@ class HipOps:
         return y if (padded or y.shape[-1] == C) else y[..., :C]
 
     @staticmethod
-    def msda_bimodal(value, off, awl, ref, hw):
+    def msda_bimodal(value, offw, ref, hw):
         """The bimodal MSDA middle of the training step, bf16 in / out (_HipMSDABimodal)."""
-        return _HipMSDABimodal.apply(value, off, awl, ref, hw)
+        return _HipMSDABimodal.apply(value, offw, ref, hw)
+
+    @staticmethod
+    def encoder_layer(layer, src, lpos, ref_q, hw, li):
+        """One deformable encoder layer of the training step on the fused HIP ops (_encoder_layer_hip)."""
+        return _encoder_layer_hip(layer, src, lpos, ref_q, hw, li)
 
     @staticmethod
     def ms_deform_attn(value, hw, loc, aw):
@@ -1276,7 +1456,6 @@ def fusion_forward(fu, s_v, s_i, ops):
     # test_module_forward_training_gpu_grads
     pos = _const(("sine_pos", b, d, h, w), s_v.device,
                  lambda: _sine_pos(b, d, h, w, "cpu").flatten(2).transpose(1, 2).contiguous())
-    lpos = torch.cat([pos + fa.level_embed[0].view(1, 1, -1), pos + fa.level_embed[1].view(1, 1, -1)], 1)
     nl = 2 * h * w
 
     def lin(mod, x):  # the encoder's nn.Linear layers on the backbone's GEMM op (bf16 operands, as autocast)
@@ -1284,29 +1463,25 @@ def fusion_forward(fu, s_v, s_i, ops):
         return y.view(*x.shape[:-1], -1)
 
     sa0 = fa.encoder.layers[0].self_attn if len(fa.encoder.layers) else None
-    fused_msda = (getattr(ops, "msda_bimodal", None) is not None and sa0 is not None and h == w and
+    fused_msda = (getattr(ops, "encoder_layer", None) is not None and sa0 is not None and h == w and
                   (sa0.n_heads, sa0.n_levels, sa0.n_points, d) == (8, 2, 4, 512) and h * w <= 484)
     if fused_msda:  # the reference points of the nl / 2 unique queries, one level: (h w, 2), computed on the
         # device as _ref_points does (its values, to the last ulp) once per shape
         ref_q = _const(("ref_q", h, w), s_v.device, lambda: _ref_points(h, w, 1, 2, s_v.device)[0, :h * w, 0, :].contiguous())
     else:
         ref = _ref_points(h, w, b, 2, s_v.device)
-    for layer in fa.encoder.layers:
+    # the level-embedded positions; the fused layers take them once (1, 2 nq, d), the batch rows being equal
+    p1 = pos[:1] if fused_msda else pos
+    lpos = torch.cat([p1 + fa.level_embed[0].view(1, 1, -1), p1 + fa.level_embed[1].view(1, 1, -1)], 1)
+    if fused_msda:  # round 6: every encoder layer on the fused HIP ops
+        if any(m.training and m.p > 0 for m in fa.encoder.modules() if isinstance(m, torch.nn.Dropout)):
+            _drop_rng(src.device)[1:].add_(1)  # this step's dropout draws (one captured add)
+        for li, layer in enumerate(fa.encoder.layers):
+            src = ops.encoder_layer(layer, src, lpos, ref_q, h, li)
+    for layer in (fa.encoder.layers if not fused_msda else ()):
         sa = layer.self_attn
         query = src + lpos
         q_bi = torch.cat(torch.chunk(query, 2, 1), dim=2)
-        if fused_msda:  # round 6: softmax, locations, sampling and their backward in the HIP op, bf16 in / out
-            value = lin(sa.value_proj, src)
-            off = lin(sa.sampling_offsets, q_bi)
-            aw = lin(sa.attention_weights, q_bi)
-            ms = ops.msda_bimodal(value.to(ops.dtype), off.to(ops.dtype), aw.to(ops.dtype), ref_q, h)
-            src2 = lin(sa.output_proj, ms)
-            src2 = torch.cat([src2, src2], 1)
-            src = src + layer.dropout1(src2)
-            src = _ln_halves(ops, src, layer.norm1_v, layer.norm1_i)
-            src = src + layer.dropout3(lin(layer.linear2, layer.dropout2(F.relu(lin(layer.linear1, src)))))
-            src = _ln_halves(ops, src, layer.norm2_v, layer.norm2_i)
-            continue
         value = lin(sa.value_proj, src).view(b, nl, sa.n_heads, d // sa.n_heads)
         # The reference repeats the bimodal query's offsets / weights on both halves of its nl queries
         # (ms_deform_attn_bimodal.py:113-118), and the two halves' reference points are the same cells, so both
@@ -1330,6 +1505,30 @@ def fusion_forward(fu, s_v, s_i, ops):
     o_v = o_v.permute(0, 2, 1).reshape(b, -1, h, w)
     o_i = o_i.permute(0, 2, 1).reshape(b, -1, h, w)
     return fu.adjust_cat(torch.cat([o_v, o_i], 1))
+
+
+def _encoder_layer_hip(layer, src, lpos, ref_q, hw, li):
+    """DeformableTransformerEncoderLayer.forward (deformable_encoder_lnspecific.py:131-148) with
+    MSDeformAttn_Bimodal (ms_deform_attn_bimodal.py:83-130) on the fused HIP ops: the bimodal query and the bf16
+    value operand in one pass (_HipQueryPrep), value_proj, [sampling_offsets | attention_weights] as one GEMM
+    (_HipLinearCat), the sampling (_HipMSDABimodal), output_proj, the duplicated-halves dropout-residual
+    (_HipDropResidual), norm1, the FFN with its dropouts and residual (_HipEncoderFFN), norm2.  src (B, 2 nq, d)
+    fp32 -> fp32.  Dropout draws: salts 8 li + 1 .. 8 li + 3."""
+    sa = layer.self_attn
+    B, n2, d = src.shape
+    M = B * n2
+    drop = lambda m: m.p if m.training else 0.0  # noqa: E731
+    qbi, srcb, src = _HipQueryPrep.apply(src, lpos)
+    value = HipOps.linear(srcb.view(M, d), sa.value_proj.weight, sa.value_proj.bias).view(B, n2, d)
+    offw = _HipLinearCat.apply(qbi.view(M // 2, 2 * d), sa.sampling_offsets.weight, sa.sampling_offsets.bias,
+                               sa.attention_weights.weight, sa.attention_weights.bias).view(B, n2 // 2, -1)
+    ms = HipOps.msda_bimodal(value, offw, ref_q, hw)
+    src2 = HipOps.linear(ms.view(M // 2, d), sa.output_proj.weight, sa.output_proj.bias).view(B, n2 // 2, d)
+    src = _HipDropResidual.apply(src, src2, drop(layer.dropout1), 8 * li + 1, True)
+    src = _ln_halves(HipOps, src, layer.norm1_v, layer.norm1_i)
+    src = _HipEncoderFFN.apply(src.view(M, d), layer.linear1.weight, layer.linear1.bias, layer.linear2.weight,
+                               layer.linear2.bias, drop(layer.dropout2), drop(layer.dropout3), 8 * li + 1)
+    return _ln_halves(HipOps, src.view(B, n2, d), layer.norm2_v, layer.norm2_i)
 
 
 def _ln_halves(ops, src, nv, ni):

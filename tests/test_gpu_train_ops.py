@@ -916,11 +916,11 @@ def test_msda_bimodal_train_matches_generic(B, hw, grid):
                                     64).to(torch.bfloat16)
     yr.backward(gout)
 
-    def run():
-        v, o, w = value.clone().requires_grad_(True), off.clone().requires_grad_(True), awl.clone().requires_grad_(True)
-        y = HipOps.msda_bimodal(v, o, w, ref_q, hw)
+    def run():  # the offsets | logits as one (B, nq, 192) tensor, as the fused Linear writes them
+        v, ow = value.clone().requires_grad_(True), torch.cat([off, awl], -1).requires_grad_(True)
+        y = HipOps.msda_bimodal(v, ow, ref_q, hw)
         y.backward(gout)
-        return y.detach(), v.grad, o.grad, w.grad
+        return y.detach(), v.grad, ow.grad[..., :128], ow.grad[..., 128:]
 
     y1, gv1, go1, ga1 = run()
     y2, gv2, go2, ga2 = run()
@@ -933,6 +933,101 @@ def test_msda_bimodal_train_matches_generic(B, hw, grid):
         a_, r_ = a_.float(), r_.float()
         err = ((a_ - r_).norm() / r_.norm().clamp_min(1e-30)).item()
         assert err <= 1e-2, (name, err)
+
+
+def _fusion_module(seed=3):
+    from mmt_amd.model import Attention_Fusion_Bimodal_LNSpecific
+    torch.manual_seed(seed)
+    fu = Attention_Fusion_Bimodal_LNSpecific(768).cuda().train()
+    with torch.no_grad():  # non-trivial offsets (Deformable DETR's zero init would sample the reference points only)
+        for layer in fu.fusion_attention.encoder.layers:
+            layer.self_attn.sampling_offsets.weight.normal_(0, 0.02)
+            layer.self_attn.sampling_offsets.bias.uniform_(-2, 2)
+            layer.self_attn.attention_weights.weight.normal_(0, 0.02)
+        fu.fusion_attention.level_embed.normal_()
+    return fu
+
+
+def test_hip_encoder_layers_match_composition():
+    """fusion_forward with every deformable encoder layer on the fused HIP ops (_encoder_layer_hip: query prep,
+    [offsets | logits] GEMM, MSDA op, dropout-residuals, FFN) against the step's previous composition of HIP
+    Linears / LayerNorms and aten glue (HipOps without encoder_layer), dropout off, 16 pairs at 20 x 20: output
+    and every gradient (inputs, encoder weights, level embedding) within 2e-2 relative L2."""
+    from mmt_amd.train import HipOps, fusion_forward
+
+    class Composed(HipOps):
+        encoder_layer = None
+
+    fu = _fusion_module()
+    for m in fu.modules():
+        if isinstance(m, torch.nn.Dropout):
+            m.p = 0.0
+    g = torch.Generator().manual_seed(11)
+    sv, si = (torch.randn(16, 768, 20, 20, generator=g).cuda() for _ in range(2))
+    dout = torch.randn(16, 768, 20, 20, generator=g).cuda()
+    res = []
+    for ops in (HipOps, Composed):
+        fu.zero_grad(set_to_none=True)
+        a, b = sv.clone().requires_grad_(True), si.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = fusion_forward(fu, a, b, ops)
+        y.float().backward(dout)
+        grads = {n: p.grad.detach().clone() for n, p in fu.named_parameters() if p.grad is not None}
+        res.append((y.detach().float(), a.grad, b.grad, grads))
+    (y1, a1, b1, g1), (y0, a0, b0, g0) = res
+    assert set(g1) == set(g0)
+    checks = [("out", y1, y0), ("d s_v", a1, a0), ("d s_i", b1, b0)] + [(n, g1[n], g0[n]) for n in sorted(g0)]
+    worst = []
+    for name, x, r in checks:
+        err = ((x.float() - r.float()).norm() / r.float().norm().clamp_min(1e-30)).item()
+        worst.append((err, name))
+        assert err <= 2e-2, (name, err)
+    print("worst:", sorted(worst)[-3:])
+
+
+def test_hip_encoder_dropout_masks():
+    """The encoder's dropout kernels (csrc/fusion_train.hip): keep rate 1 - p (10^6 draws, p = 0.1: within 0.002),
+    survivors scaled by bf16(1 / (1 - p)) in the forward; the backward regenerates the same mask (the dropped
+    elements of the forward are exactly the zero gradients); the duplicated-halves form draws independently on the
+    two halves; the step counter changes the draws; equal keys reproduce them bitwise."""
+    from mmt_amd._lib import LIB, check
+    from mmt_amd.train import _drop_rng
+    st = torch.cuda.current_stream().cuda_stream
+    rng = _drop_rng("cuda")
+    B, rows, d, p = 4, 500, 512, 0.1
+    x = torch.zeros(B, rows, d, device="cuda")
+    y = torch.ones(B, rows // 2, d, device="cuda", dtype=torch.bfloat16)
+    out, out2 = torch.empty_like(x), torch.empty_like(x)
+    check(LIB.mmt_ft_drop_residual(x.data_ptr(), y.data_ptr(), out.data_ptr(), rng.data_ptr(), 5, p, B, rows, d, 1, st), "fwd")
+    check(LIB.mmt_ft_drop_residual(x.data_ptr(), y.data_ptr(), out2.data_ptr(), rng.data_ptr(), 5, p, B, rows, d, 1, st), "fwd")
+    dy = torch.empty(B, rows // 2, d, device="cuda", dtype=torch.bfloat16)
+    dout = torch.zeros(B, rows, d, device="cuda")
+    dout[:, :rows // 2] = 1.0  # the first half's gradient only: dy = its mask
+    check(LIB.mmt_ft_drop_residual_bwd(dout.data_ptr(), dy.data_ptr(), rng.data_ptr(), 5, p, B, rows, d, 1, st), "bwd")
+    torch.cuda.synchronize()
+    assert torch.equal(out, out2)
+    sc = torch.tensor(1 / (1 - p)).bfloat16().float().item()
+    vals = set(out.unique().tolist())
+    assert vals <= {0.0, sc}, vals
+    rate = (out != 0).float().mean().item()
+    assert abs(rate - (1 - p)) < 0.002, rate
+    assert torch.equal(dy.float() != 0, out[:, :rows // 2] != 0)
+    assert not torch.equal(out[:, :rows // 2] != 0, out[:, rows // 2:] != 0)  # the halves draw independently
+    rng[1:].add_(1)
+    check(LIB.mmt_ft_drop_residual(x.data_ptr(), y.data_ptr(), out2.data_ptr(), rng.data_ptr(), 5, p, B, rows, d, 1, st), "fwd")
+    h = torch.rand(1000, 2048, device="cuda").sub_(0.3).clamp_min_(0).bfloat16()
+    hd, dh = torch.empty_like(h), torch.empty_like(h)
+    check(LIB.mmt_ft_relu_drop(h.data_ptr(), hd.data_ptr(), rng.data_ptr(), 9, p, h.numel(), st), "relu_drop")
+    ones = torch.ones_like(h)
+    check(LIB.mmt_ft_relu_drop_bwd(ones.data_ptr(), h.data_ptr(), dh.data_ptr(), rng.data_ptr(), 9, p, h.numel(), st),
+          "relu_drop_bwd")
+    torch.cuda.synchronize()
+    assert not torch.equal(out, out2)
+    kept = hd != 0
+    assert torch.equal(hd.float()[kept], (h.float() * (1 / (1 - p))).bfloat16().float()[kept])
+    assert torch.equal(dh != 0, kept)  # h > 0 and kept
+    r2 = kept.float().sum().item() / (h > 0).float().sum().item()
+    assert abs(r2 - (1 - p)) < 0.002, r2
 
 
 @pytest.mark.parametrize("B,H,C,up", [(16, 20, 768, 1), (2, 40, 96, 2), (3, 16, 48, 4), (1, 5, 8, 1)])

@@ -37,6 +37,12 @@ class UnfusedResidualOps(HipOps):
     linear2 = None  # (the lockstep pair needs the fused residual Functions)
 
 
+class ComposedEncoderOps(HipOps):
+    """HipOps with the deformable encoder layers as before round 6's fusion: HIP Linears / LayerNorms, aten glue
+    (adds, cats, casts, softmax, dropout) and the drop-in fp32 MSDA kernels."""
+    encoder_layer = None
+
+
 class SplitMlpOps(HipOps):
     """HipOps with each MLP as fc1 / aten GELU / fc2 (three autograd nodes) instead of _HipMlp."""
     mlp = None
@@ -122,7 +128,7 @@ def main():
     variants = {"hip": HipOps, "aten_groupnorm": AtenGroupNormOps, "aten_layernorm": AtenLayerNormOps,
                 "split_mlp": SplitMlpOps, "unfused_residual": UnfusedResidualOps, "accum_grads": (HipOps, accumulated_grads),
                 "transposed": (HipOps, transposed_copies), "aten_scale_cast": (HipOps, aten_scale_cast),
-                "sequential": (HipOps, sequential_backbones)}
+                "sequential": (HipOps, sequential_backbones), "composed_encoder": ComposedEncoderOps}
     if args.only:
         variants = {k: v for k, v in variants.items() if k in args.only.split(",")}
     for r in range(args.rounds):
