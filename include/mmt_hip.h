@@ -516,6 +516,20 @@ int mmt_conv3x3_wprep(const mmt_conv_wprep* items, int n, void* stream);
  *     bf16(dropout'(dy)) : 0.
  * Dropout: keep with probability 1 - p (16-bit draws from a counter hash of rng = {seed, counter} on the device,
  * the call site's salt and the element index), survivors * 1 / (1 - p); rng NULL or p == 0: no dropout. */
+/* The training step's corner read-out and box loss (head.py:176-177, :200-212; actors/mixformer_rgbt.py:127-168
+ * with lib/utils/box_ops.py:100-152), fp32:
+ *   mmt_corner_boxes: score_tl / score_br [B][fh*fh] -> xyxy [B][4] = the soft-argmax expectations (coordinates
+ *     stride * (col, row)) times 1 / img_sz; stats [B][2][4] (max, sum of exp, E[x], E[y]) for the backward;
+ *     _bwd: dscore = the softmax backward of d xyxy's expectation gradient.
+ *   mmt_box_loss: pred cxcywh [B][4], gt xywh [B][4] -> out[4] = (iou_w mean(1 - CIoU) + l1_w mean|pred - gt|, the
+ *     CIoU loss, the L1, the mean IoU) on xyxy boxes (gt clamped to [0, 1]); _bwd: dpred [B][4] from dloss[0]. */
+int mmt_corner_boxes(const float* score_tl, const float* score_br, float* xyxy, float* stats, int B, int fh,
+                     float stride, float img_sz, void* stream);
+int mmt_corner_boxes_bwd(const float* score_tl, const float* score_br, const float* stats, const float* dxyxy,
+                         float* dscore_tl, float* dscore_br, int B, int fh, float stride, float img_sz, void* stream);
+int mmt_box_loss(const float* pred, const float* gt, float* out, int B, float iou_w, float l1_w, void* stream);
+int mmt_box_loss_bwd(const float* pred, const float* gt, const float* dloss, float* dpred, int B, float iou_w,
+                     float l1_w, void* stream);
 int mmt_ft_query_prep(const float* src, const float* lpos, void* qbi, void* srcb, int B, int nq, int d, void* stream);
 int mmt_ft_query_prep_bwd(const void* dqbi, const void* dsrcb, const float* dthrough, float* dsrc, float* dlpos, int B,
                           int nq, int d, void* stream);

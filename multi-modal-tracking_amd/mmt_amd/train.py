@@ -1004,6 +1004,64 @@ class _HipLinearCat(torch.autograd.Function):
         return dx, dw[:n0], db[:n0], dw[n0:], db[n0:]
 
 
+class _HipCornerBoxes(torch.autograd.Function):
+    """Both corners' soft-argmax (head.py:200-212) and the normalisation (head.py:176-177): score maps (B, fh*fh)
+    fp32 -> xyxy (B, 4) in [0, 1] (mmt_corner_boxes; backward mmt_corner_boxes_bwd, the softmax backward of the
+    expectations' gradient)."""
+
+    @staticmethod
+    def forward(ctx, s_tl, s_br, fh, stride, img_sz):
+        from ._lib import LIB, check
+        B = s_tl.shape[0]
+        s_tl, s_br = s_tl.float().contiguous(), s_br.float().contiguous()
+        xyxy = torch.empty(B, 4, device=s_tl.device, dtype=torch.float32)
+        stats = torch.empty(B, 2, 4, device=s_tl.device, dtype=torch.float32)
+        check(LIB.mmt_corner_boxes(s_tl.data_ptr(), s_br.data_ptr(), xyxy.data_ptr(), stats.data_ptr(), B, fh,
+                                   float(stride), float(img_sz), _stream()), "mmt_corner_boxes")
+        ctx.save_for_backward(s_tl, s_br, stats)
+        ctx.args = (fh, float(stride), float(img_sz))
+        return xyxy
+
+    @staticmethod
+    def backward(ctx, dxyxy):
+        from ._lib import LIB, check
+        s_tl, s_br, stats = ctx.saved_tensors
+        fh, stride, img_sz = ctx.args
+        dxyxy = dxyxy.float().contiguous()
+        d_tl, d_br = torch.empty_like(s_tl), torch.empty_like(s_br)
+        check(LIB.mmt_corner_boxes_bwd(s_tl.data_ptr(), s_br.data_ptr(), stats.data_ptr(), dxyxy.data_ptr(),
+                                       d_tl.data_ptr(), d_br.data_ptr(), s_tl.shape[0], fh, stride, img_sz, _stream()),
+              "mmt_corner_boxes_bwd")
+        return d_tl, d_br, None, None, None
+
+
+class _HipBoxLoss(torch.autograd.Function):
+    """box_loss (MixFormerRGBTActor.compute_losses, actors/mixformer_rgbt.py:127-168; CIoU of box_ops.py:100-152)
+    in one launch each way: pred cxcywh (B, 4), gt xywh (B, 4) -> (loss, ciou loss, l1, mean iou) as a (4,) fp32
+    tensor; only the loss (entry 0) carries a gradient (mmt_box_loss / _bwd)."""
+
+    @staticmethod
+    def forward(ctx, pred, gt, iou_w, l1_w):
+        from ._lib import LIB, check
+        pred, gt = pred.float().reshape(-1, 4).contiguous(), gt.detach().float().reshape(-1, 4).contiguous()
+        out = torch.empty(4, device=pred.device, dtype=torch.float32)
+        check(LIB.mmt_box_loss(pred.data_ptr(), gt.data_ptr(), out.data_ptr(), pred.shape[0], float(iou_w), float(l1_w),
+                               _stream()), "mmt_box_loss")
+        ctx.save_for_backward(pred, gt)
+        ctx.w = (float(iou_w), float(l1_w))
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        from ._lib import LIB, check
+        pred, gt = ctx.saved_tensors
+        dout = dout.float().contiguous()
+        dpred = torch.empty_like(pred)
+        check(LIB.mmt_box_loss_bwd(pred.data_ptr(), gt.data_ptr(), dout.data_ptr(), dpred.data_ptr(), pred.shape[0],
+                                   *ctx.w, _stream()), "mmt_box_loss_bwd")
+        return dpred, None, None, None
+
+
 class _HipAddUp(torch.autograd.Function):
     """bf16(up(a) + b) on NHWC bf16 maps (mmt_add_up_bf16; up 1 = a plain add): the corner head's pyramid adds
     (head.py:187-189) at the lower of their two resolutions; backward: db = dout, da = its up x up block sums."""
@@ -1197,6 +1255,18 @@ class HipOps:
         y = _HipBatchNormReLU.apply(x.contiguous(), bn.weight, bn.bias, bn.running_mean if keep else None,
                                     bn.running_var if keep else None, bn.momentum, bn.eps, training, C)
         return y if (padded or y.shape[-1] == C) else y[..., :C]
+
+    @staticmethod
+    def corner_boxes(s_tl, s_br, fh, stride, img_sz):
+        """Both corners' soft-argmax, normalised: (B, fh*fh) fp32 maps -> xyxy (B, 4) (_HipCornerBoxes)."""
+        return _HipCornerBoxes.apply(s_tl, s_br, fh, stride, img_sz)
+
+    @staticmethod
+    def box_loss(pred_cxcywh, gt_xywh, iou_weight=2.0, l1_weight=5.0):
+        """box_loss on mmt_box_loss (_HipBoxLoss): (loss, {"ciou", "l1", "iou"})."""
+        out = _HipBoxLoss.apply(pred_cxcywh.view(-1, 4), gt_xywh, iou_weight, l1_weight)
+        st = out.detach()
+        return out[0], {"ciou": st[1], "l1": st[2], "iou": st[3]}
 
     @staticmethod
     def msda_bimodal(value, offw, ref, hw):
@@ -1630,7 +1700,8 @@ def _head_forward_nhwc(hd, x, ops):
         return nhwc(F.interpolate(nchw(t), scale_factor=f))
 
     xh = nhwc(x).to(torch.bfloat16).contiguous()
-    coords = []
+    coords, maps = [], {}
+    boxes = getattr(ops, "corner_boxes", None)  # both soft-argmaxes + normalisation in one op (round 6)
     score, add_up = getattr(ops, "corner_score", None), getattr(ops, "add_up", None)
     fused = score is not None and add_up is not None and HEAD_SCORE_FP32 and bn_relu is not None
     for br in ("tl", "br"):
@@ -1651,8 +1722,10 @@ def _head_forward_nhwc(hd, x, ops):
             m3 = blk(a3[2], block(a3[1], block(a3[0], x2)), keep_pad=True)
             m4 = blk(a4[1], block(a4[0], x3), keep_pad=True)
             fh = x4.shape[1]
-            sm = score(x4, g("conv5"), m3, m4).view(-1, 1, fh, fh)  # (B, 1, fh, fh) fp32 (padded rows in)
-            coords += list(_soft_argmax(sm, hd.stride))
+            sm = score(x4, g("conv5"), m3, m4)  # (B, fh * fh) fp32 (padded rows in)
+            maps[br] = sm
+            if boxes is None:
+                coords += list(_soft_argmax(sm.view(-1, 1, fh, fh), hd.stride))
             continue
         x3 = block(g("conv3"), up(block(g("adjust1"), xh), 2) + up(x2, 2))
         x4 = block(g("conv4"), up(block(g("adjust2"), xh), 4) + up(x3, 2))
@@ -1664,6 +1737,15 @@ def _head_forward_nhwc(hd, x, ops):
             continue
         sm = c1(g("conv5"), x4) + up(m3, 4) + up(m4, 2)
         coords += list(_soft_argmax(nchw(sm), hd.stride))
+    if boxes is not None and len(maps) == 2:
+        fh = int(round(maps["tl"].shape[1] ** 0.5))
+        return boxes(maps["tl"], maps["br"], fh, hd.stride, hd.img_sz)
+    if len(coords) < 4:  # the fused path ran for one branch only: that branch's soft-argmax now
+        for br in ("tl", "br"):
+            if br in maps:
+                fh = int(round(maps[br].shape[1] ** 0.5))
+                c = list(_soft_argmax(maps[br].view(-1, 1, fh, fh), hd.stride))
+                coords = c + coords if br == "tl" else coords + c
     return torch.stack(coords, dim=1) / hd.img_sz
 
 
@@ -1937,7 +2019,8 @@ class TrainStep:
         if self.reducer is not None:
             self.reducer.begin()
         pred = self.model(t, o, s)
-        loss, stats = box_loss(pred, gt_xywh, self.iou_weight, self.l1_weight)
+        loss_fn = getattr(self.ops, "box_loss", None) or box_loss  # HipOps: one launch each way
+        loss, stats = loss_fn(pred, gt_xywh, self.iou_weight, self.l1_weight)
         loss.backward()
         if self.reducer is not None:
             self.reducer.finish()

@@ -935,6 +935,71 @@ def test_msda_bimodal_train_matches_generic(B, hw, grid):
         assert err <= 1e-2, (name, err)
 
 
+@pytest.mark.parametrize("B,fh,stride", [(16, 80, 4), (3, 20, 16), (1, 7, 2)])
+def test_hip_corner_boxes_autograd(B, fh, stride):
+    """HipOps.corner_boxes (mmt_corner_boxes / _bwd) against the composition it replaces -- _soft_argmax of both
+    maps (head.py:200-212), torch.stack / img_sz -- with autograd in fp32: xyxy within 1e-5 relative, the score
+    maps' gradients within 1e-4 (relative L2)."""
+    from mmt_amd.train import HipOps, _soft_argmax
+    g = torch.Generator().manual_seed(B * fh)
+    maps = [(torch.randn(B, fh * fh, generator=g) * 3).cuda() for _ in range(2)]
+    dxy = torch.randn(B, 4, generator=g).cuda()
+    img = fh * stride
+    ref = [m.clone().requires_grad_(True) for m in maps]
+    coords = []
+    for m in ref:
+        coords += list(_soft_argmax(m.view(B, 1, fh, fh), stride))
+    yr = torch.stack(coords, 1) / img
+    yr.backward(dxy)
+    hip = [m.clone().requires_grad_(True) for m in maps]
+    y = HipOps.corner_boxes(hip[0], hip[1], fh, stride, img)
+    y.backward(dxy)
+    torch.cuda.synchronize()
+    assert ((y - yr).abs().max() / yr.abs().max()).item() < 1e-5
+    for a, r in zip(hip, ref):
+        err = ((a.grad - r.grad).norm() / r.grad.norm()).item()
+        assert err < 1e-4, err
+
+
+def test_hip_box_loss_matches_autograd():
+    """HipOps.box_loss (mmt_box_loss / _bwd: CIoU + L1 of MixFormerRGBTActor.compute_losses with the hand-derived
+    backward) against train.box_loss under autograd in fp32, on random boxes and the edge cases the chain rule
+    has to get right: pred equal to gt (min / max ties split the gradient), disjoint boxes (intersection clamped to
+    0), IoU > 0.5 (alpha active), boxes reaching outside [0, 1] (gt clamped), equal widths (atan term 0):
+    loss and statistics within 1e-5 relative, d pred within 1e-4 of the gradient's scale (max abs)."""
+    from mmt_amd.train import HipOps, box_loss
+    g = torch.Generator().manual_seed(7)
+    B = 64
+    gt = torch.cat([torch.rand(B, 2, generator=g) * 0.6, 0.1 + torch.rand(B, 2, generator=g) * 0.4], 1)
+    pred = torch.cat([gt[:, :2] + gt[:, 2:] / 2 + torch.randn(B, 2, generator=g) * 0.05,
+                      gt[:, 2:] * (1 + torch.randn(B, 2, generator=g) * 0.2)], 1)
+    gt[0] = torch.tensor([0.25, 0.25, 0.5, 0.5])
+    pred[0] = torch.tensor([0.5, 0.5, 0.5, 0.52])                # shared x edges (ties); identical boxes would give
+    # the reference's NaN (alpha = 0 / 0), which the HIP loss propagates as well (checked below)
+    pred[1] = torch.tensor([0.9, 0.9, 0.05, 0.05])               # disjoint
+    gt[1] = torch.tensor([0.05, 0.05, 0.1, 0.1])
+    gt[2] = torch.tensor([0.8, 0.8, 0.5, 0.5])                   # reaches past 1: clamped
+    pred[2] = torch.tensor([0.95, 0.95, 0.3, 0.3])
+    pred[3] = torch.tensor([gt[3, 0] + gt[3, 2] / 2 + 0.01, gt[3, 1] + gt[3, 3] / 2, gt[3, 2], gt[3, 3]])  # same size
+    gt[4] = torch.tensor([0.3, 0.3, 0.2, 0.2])
+    pred[4] = torch.tensor([0.4, 0.45, 0.2, 0.3])                # shared left / right edges (ties)
+    pred, gt = pred.cuda().view(B, 1, 4), gt.cuda()
+    pr = pred.clone().requires_grad_(True)
+    loss_r, st_r = box_loss(pr, gt, 2.0, 5.0)
+    (3.0 * loss_r).backward()
+    ph = pred.clone().requires_grad_(True)
+    loss_h, st_h = HipOps.box_loss(ph, gt, 2.0, 5.0)
+    (3.0 * loss_h).backward()
+    torch.cuda.synchronize()
+    for a, r in ((loss_h, loss_r), (st_h["ciou"], st_r["ciou"]), (st_h["l1"], st_r["l1"]), (st_h["iou"], st_r["iou"])):
+        assert abs(a.item() - r.item()) <= 1e-5 * abs(r.item()) + 1e-7, (a.item(), r.item())
+    err = (ph.grad - pr.grad).abs().max().item() / pr.grad.abs().max().item()
+    assert err < 1e-4, (err, (ph.grad - pr.grad).abs().view(B, 4).max(1).values[:8])
+    same = gt[:1].clone()
+    same_pred = torch.cat([same[:, :2] + same[:, 2:] / 2, same[:, 2:]], 1).view(1, 1, 4)
+    assert math.isnan(box_loss(same_pred, same)[0].item()) and math.isnan(HipOps.box_loss(same_pred, same)[0].item())
+
+
 def _fusion_module(seed=3):
     from mmt_amd.model import Attention_Fusion_Bimodal_LNSpecific
     torch.manual_seed(seed)
