@@ -322,6 +322,14 @@ int mmt_ms_deform_attn_backward(const void* value, const int64_t* spatial_shapes
                                 const void* sampling_loc, const void* attn_weight, const void* grad_output,
                                 void* grad_value, void* grad_loc, void* grad_attn, int N, int S, int M, int D,
                                 int Lq, int L, int P, int dtype, void* stream);
+/* mmt_ms_deform_attn_backward with the grad_value gather chosen: value_impl 0 auto, 1 the 64-pixel-chunk workgroups,
+ * 2 one workgroup per (n, m, level) over the whole level (needs Lq * P <= 2048 and every level's H * W <= max_hw
+ * <= 1024; auto takes it then).  Both sum each pixel's taps in (sample, tap) order: equal results.  max_hw: an
+ * upper bound of the levels' H * W (the plain entry passes S). */
+int mmt_ms_deform_attn_backward_impl(const void* value, const int64_t* spatial_shapes, const int64_t* level_start,
+                                     const void* sampling_loc, const void* attn_weight, const void* grad_output,
+                                     void* grad_value, void* grad_loc, void* grad_attn, int N, int S, int M, int D,
+                                     int Lq, int L, int P, int max_hw, int value_impl, int dtype, void* stream);
 
 /* ---------------------------------------------------------------- candidate elimination
  * asymmetric_shared_ce.py (CE_Block_Shared :228-282, candidate_elimination :52-102,

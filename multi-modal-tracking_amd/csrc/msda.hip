@@ -368,6 +368,127 @@ __global__ __launch_bounds__(256) void msda_bwd_value_kernel(const T* __restrict
     }
 }
 
+// grad_value, one workgroup per (n, m, level) (round 6): the level's Lq x P samples expanded
+// into their taps ONCE (msda_bwd_value_kernel re-expanded them in every 64-pixel chunk workgroup), counted per pixel
+// of the whole level, bucketed, each bucket sorted by (sample, tap) -- the same summation order as
+// msda_bwd_value_kernel, so the same sums bit for bit -- then each pixel's channels summed, 16 waves over the
+// pixels with four independent sums in flight per wave.  Taken when a level's samples and pixels fit the LDS
+// lists (Lq P <= NML_S, H W <= NML_PIX) and D <= 64.
+constexpr int NML_T = 1024, NML_S = 2048, NML_PIX = 1024;
+template <typename T>
+__global__ __launch_bounds__(NML_T) void msda_bwd_value_nml_kernel(const T* __restrict__ loc, const T* __restrict__ aw,
+                                                                   const T* __restrict__ gout, T* __restrict__ gvalue,
+                                                                   const int64_t* __restrict__ shapes,
+                                                                   const int64_t* __restrict__ lstart, int S, int M,
+                                                                   int D, int Lq, int L, int P) {
+    using A = T;
+    __shared__ int cnt[NML_PIX + 1], cur[NML_PIX];
+    __shared__ int ekey[4 * NML_S];
+    __shared__ A ew[4 * NML_S];
+    __shared__ A sa[NML_S];
+    const int t = threadIdx.x;
+    const int l = blockIdx.x, m = blockIdx.y, n = blockIdx.z;
+    const int H = (int)shapes[2 * l], W = (int)shapes[2 * l + 1], np = H * W, ns = Lq * P;
+    for (int r = t; r <= np; r += NML_T) cnt[r] = 0;
+    for (int j = t; j < ns; j += NML_T) {
+        const int q = j / P, p = j - q * P;
+        sa[j] = aw[(((int64_t)n * Lq + q) * M + m) * L * P + (int64_t)l * P + p];
+    }
+    __syncthreads();
+    auto taps = [&](int j, auto&& f) {  // msda_bwd_value_kernel's tap rules, pixels of the whole level
+        const int q = j / P, p = j - q * P;
+        const int64_t wi = (((int64_t)n * Lq + q) * M + m) * L * P + (int64_t)l * P + p;
+        const A lx = loc[2 * wi], ly = loc[2 * wi + 1];
+        const A h = ly * (A)H - (A)0.5, w = lx * (A)W - (A)0.5;
+        if (!(h > (A)-1 && w > (A)-1 && h < (A)H && w < (A)W)) return;
+        const int hl = (int)floor(h), wl = (int)floor(w), hh_ = hl + 1, wh_ = wl + 1;
+        const A lh = h - (A)hl, lw = w - (A)wl, hh = (A)1 - lh, hw = (A)1 - lw;
+        const int r1 = hl * W + wl;
+        if (hl >= 0 && wl >= 0) f(0, r1, hh * hw);
+        if (hl >= 0 && wh_ <= W - 1) f(1, r1 + 1, hh * lw);
+        if (hh_ <= H - 1 && wl >= 0) f(2, r1 + W, lh * hw);
+        if (hh_ <= H - 1 && wh_ <= W - 1) f(3, r1 + W + 1, lh * lw);
+    };
+    for (int j = t; j < ns; j += NML_T) taps(j, [&](int, int r, A) { atomicAdd(&cnt[r], 1); });
+    __syncthreads();
+    if (t < 64) {  // exclusive scan of the np counts: lane t owns a run of ceil(np / 64)
+        const int per = (np + 63) / 64, r0 = min(t * per, np), r1 = min(r0 + per, np);
+        int sum = 0;
+        for (int r = r0; r < r1; ++r) sum += cnt[r];
+        int x = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o, 64);
+            if (t >= o) x += y;
+        }
+        int run = x - sum;
+        for (int r = r0; r < r1; ++r) {
+            const int v = cnt[r];
+            cur[r] = run;
+            run += v;
+        }
+        if (t == 63) cnt[np] = x;
+    }
+    __syncthreads();
+    for (int r = t; r < np; r += NML_T) cnt[r] = cur[r];
+    __syncthreads();
+    for (int j = t; j < ns; j += NML_T)
+        taps(j, [&](int k, int r, A wk) {
+            const int pos = atomicAdd(&cur[r], 1);
+            ekey[pos] = j * 4 + k;
+            ew[pos] = wk;
+        });
+    __syncthreads();
+    for (int r = t; r < np; r += NML_T) {  // each bucket in (sample, tap) order
+        const int e0 = cnt[r], e1 = cnt[r + 1];
+        for (int e = e0 + 1; e < e1; ++e) {
+            const int k = ekey[e];
+            const A wv = ew[e];
+            int i = e - 1;
+            for (; i >= e0 && ekey[i] > k; --i) {
+                ekey[i + 1] = ekey[i];
+                ew[i + 1] = ew[i];
+            }
+            ekey[i + 1] = k;
+            ew[i + 1] = wv;
+        }
+    }
+    __syncthreads();
+    const int wave = t >> 6, c = t & 63;
+    constexpr int NW = NML_T / 64, PS = 4;
+    const int64_t gq = (int64_t)M * D, g0 = ((int64_t)n * Lq * M + m) * D + min(c, D - 1);
+    for (int r0 = wave; r0 < np; r0 += NW * PS) {
+        int e0[PS], e1[PS], len = 0;
+        A acc[PS];
+#pragma unroll
+        for (int i = 0; i < PS; ++i) {
+            const int r = r0 + i * NW;
+            e0[i] = r < np ? cnt[r] : 0;
+            e1[i] = r < np ? cnt[r + 1] : 0;
+            len = max(len, e1[i] - e0[i]);
+            acc[i] = 0;
+        }
+        for (int k = 0; k < len; ++k) {
+#pragma unroll
+            for (int i = 0; i < PS; ++i) {
+                const int e = e0[i] + k;
+                if (e < e1[i]) {
+                    const int j = ekey[e] >> 2;
+                    acc[i] += ew[e] * (gout[g0 + (j / P) * gq] * sa[j]);
+                }
+            }
+        }
+        if (c < D) {
+            T* gv = gvalue + (((int64_t)n * S + lstart[l]) * M + m) * D + c;
+#pragma unroll
+            for (int i = 0; i < PS; ++i) {
+                const int r = r0 + i * NW;
+                if (r < np) gv[(int64_t)r * M * D] = acc[i];
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------------------------------------
 // Training form of MSDeformAttn_Bimodal's middle (ms_deform_attn_bimodal.py:97-128 as the training step runs it,
 // mmt_amd.train.fusion_forward): from the bf16 outputs of value_proj / sampling_offsets / attention_weights to the
@@ -715,10 +836,27 @@ extern "C" int mmt_msda_bimodal_train_bwd(const void* value, const void* off, in
     return launch_status();
 }
 
+extern "C" int mmt_ms_deform_attn_backward_impl(const void* value, const int64_t* spatial_shapes,
+                                                const int64_t* level_start, const void* sampling_loc,
+                                                const void* attn_weight, const void* grad_output, void* grad_value,
+                                                void* grad_loc, void* grad_attn, int N, int S, int M, int D, int Lq,
+                                                int L, int P, int max_hw, int value_impl, int dtype, void* stream);
+
 extern "C" int mmt_ms_deform_attn_backward(const void* value, const int64_t* spatial_shapes, const int64_t* level_start,
                                            const void* sampling_loc, const void* attn_weight, const void* grad_output,
                                            void* grad_value, void* grad_loc, void* grad_attn, int N, int S, int M, int D,
                                            int Lq, int L, int P, int dtype, void* stream) {
+    // without the level sizes on the host, the per-level gather is taken when every level fits whatever its shape:
+    // S (the pixels of all levels) bounds each level's
+    return mmt_ms_deform_attn_backward_impl(value, spatial_shapes, level_start, sampling_loc, attn_weight, grad_output,
+                                            grad_value, grad_loc, grad_attn, N, S, M, D, Lq, L, P, S, 0, dtype, stream);
+}
+
+extern "C" int mmt_ms_deform_attn_backward_impl(const void* value, const int64_t* spatial_shapes,
+                                                const int64_t* level_start, const void* sampling_loc,
+                                                const void* attn_weight, const void* grad_output, void* grad_value,
+                                                void* grad_loc, void* grad_attn, int N, int S, int M, int D, int Lq,
+                                                int L, int P, int max_hw, int value_impl, int dtype, void* stream) {
     if (!value || !spatial_shapes || !level_start || !sampling_loc || !attn_weight || !grad_output || !grad_value ||
         !grad_loc || !grad_attn)
         return MMT_EBADARG;
@@ -736,14 +874,24 @@ extern "C" int mmt_ms_deform_attn_backward(const void* value, const int64_t* spa
     // the gather's grid: (chunks of MSDA_PIX pixels over the levels, heads, batch); the sum over levels of
     // ceil(HW_l / 64) is at most S / 64 + L (the shapes stay on the device: the kernel skips past the last)
     const dim3 vgrid((unsigned)(S / MSDA_PIX + L), (unsigned)M, (unsigned)N);
+    // the per-(n, m, level) gather when the lists fit (value_impl 0 auto / 2 forced; 1 = the 64-pixel chunks)
+    const bool nml_fits = (int64_t)Lq * P <= NML_S && max_hw <= NML_PIX && max_hw > 0;
+    if (value_impl == 2 && !nml_fits) return MMT_EBADARG;
+    const bool nml = gather && value_impl != 1 && nml_fits;
 #define MSDA_BWD_CASE(T)                                                                                           \
     if (gather) {                                                                                                  \
         hipLaunchKernelGGL((msda_bwd_kernel<T, false>), grid, dim3(256), 0, st, (const T*)value, spatial_shapes,  \
                            level_start, (const T*)sampling_loc, (const T*)attn_weight, (const T*)grad_output,       \
                            (T*)grad_value, (T*)grad_loc, (T*)grad_attn, S, M, D, Lq, L, P, nsamp);                  \
-        hipLaunchKernelGGL((msda_bwd_value_kernel<T>), vgrid, dim3(256), 0, st, (const T*)sampling_loc,           \
-                           (const T*)attn_weight, (const T*)grad_output, (T*)grad_value, spatial_shapes,            \
-                           level_start, S, M, D, Lq, L, P);                                                         \
+        if (nml)                                                                                                   \
+            hipLaunchKernelGGL((msda_bwd_value_nml_kernel<T>), dim3((unsigned)L, (unsigned)M, (unsigned)N),         \
+                               dim3(NML_T), 0, st, (const T*)sampling_loc, (const T*)attn_weight,                   \
+                               (const T*)grad_output, (T*)grad_value, spatial_shapes, level_start, S, M, D, Lq, L,  \
+                               P);                                                                                  \
+        else                                                                                                       \
+            hipLaunchKernelGGL((msda_bwd_value_kernel<T>), vgrid, dim3(256), 0, st, (const T*)sampling_loc,       \
+                               (const T*)attn_weight, (const T*)grad_output, (T*)grad_value, spatial_shapes,        \
+                               level_start, S, M, D, Lq, L, P);                                                     \
     } else {                                                                                                       \
         hipLaunchKernelGGL((msda_bwd_kernel<T, true>), grid, dim3(256), 0, st, (const T*)value, spatial_shapes,   \
                            level_start, (const T*)sampling_loc, (const T*)attn_weight, (const T*)grad_output,       \

@@ -90,6 +90,8 @@ _PROTOS = {
     "mmt_patch_im2col": [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp],
     "mmt_ms_deform_attn_forward": [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp],
     "mmt_ms_deform_attn_backward": [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp],
+    "mmt_ms_deform_attn_backward_impl": [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32,
+                                         i32, i32, vp],
     "mmt_msda_bimodal": [vp, vp, vp, i32, i32, i32, vp],
     "mmt_msda_bimodal_train_fwd": [vp, vp, i32, vp, i32, vp, vp, i32, i32, vp],
     "mmt_msda_bimodal_train_bwd": [vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, i32, i32, vp],

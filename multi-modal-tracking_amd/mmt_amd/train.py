@@ -79,11 +79,30 @@ _SPLITK = {}  # device -> (slab workspace, arrival tickets) of the dW GEMMs' spl
 
 
 def _splitk_ws(dev):
-    ws = _SPLITK.get(dev)
+    """The split-K workspace of the current stream (GEMMs on one stream run one after another, so one slab and one
+    ticket array per stream; the backward's side stream has its own)."""
+    key = (str(dev), torch.cuda.current_stream(dev).cuda_stream)
+    ws = _SPLITK.get(key)
     if ws is None:
-        ws = _SPLITK[dev] = (torch.empty(32 << 20, device=dev, dtype=torch.float32),
+        ws = _SPLITK[key] = (torch.empty(32 << 20, device=dev, dtype=torch.float32),
                              torch.zeros(1 << 16, device=dev, dtype=torch.int32))
     return ws
+
+
+# The pair backward's weight-gradient GEMMs on a side stream, beside the input-gradient GEMMs on the main stream
+# (round 6): the two are independent, so the second fills the CUs the first leaves idle in its last round of tiles
+# (the N = 768 GEMMs of the backbone run 1.55 rounds of 512 tile slots).  Measured no faster in an interleaved A/B
+# (tools/train_ab.py --only hip,single_stream: 569-576 dual vs 574-580 single samples/s, profiles/r06aa_train_ab.jsonl),
+# so off: an A/B knob.
+DUAL_STREAM = False
+_SIDE = {}
+
+
+def _side_stream(dev):
+    s = _SIDE.get(str(dev))
+    if s is None:
+        s = _SIDE[str(dev)] = torch.cuda.Stream(device=dev)
+    return s
 
 
 # Per-step GEMM accounting for bench.py's train_step.roofline: None, or a dict that every GEMM launch of the
@@ -332,13 +351,48 @@ class _HipMlpResidual(torch.autograd.Function):
 # One modality's dW GEMM (768-3080 output columns, K = the 8448 tokens of 16 pairs) is a 42-168 tile grid on
 # 256 CUs; the pair fills the chip twice as well (tools/dw_split_ab.py: 250-425 TFLOP/s at one group, 390-595
 # at two; the step 417 -> 462 samples/s, profiles/r04_train_pair_ab.jsonl).
+class _Beside:
+    """Runs work on the device's side stream beside the calling (main) stream: run(fn, ...) makes the side stream
+    wait for everything issued on the main stream so far, then issues fn there; leaving the block makes the main
+    stream wait for the side stream.  Every tensor the side work reads or writes must be allocated on the main
+    stream and stay referenced until the block ends (so no block is recycled while the side stream uses it).
+    Captured in a hipGraph as a fork / join.  With DUAL_STREAM False (or on the host) run() calls fn inline."""
+
+    def __init__(self, dev):
+        self.on = DUAL_STREAM and MN_MAJOR and torch.device(dev).type == "cuda"
+        self.dev = dev
+
+    def __enter__(self):
+        if self.on:
+            self.main, self.side = torch.cuda.current_stream(self.dev), _side_stream(self.dev)
+        return self
+
+    def run(self, fn, *a, **kw):
+        if not self.on:
+            return fn(*a, **kw)
+        self.side.wait_stream(self.main)
+        with torch.cuda.stream(self.side):
+            return fn(*a, **kw)
+
+    def __exit__(self, *exc):
+        if self.on:
+            self.main.wait_stream(self.side)
+        return False
+
+
 def _halves(t, M):
     return t[:M], t[M:]
 
 
-def _weight_grads2(dy, x, M, N, K):
-    """_weight_grads of both modalities (dy [2M][N], x [2M][K]) in one launch: ((dW, db) RGB, (dW, db) TIR)."""
-    bufs = [torch.empty(N * (K + 1), device=dy.device, dtype=torch.float32) for _ in range(2)]
+def _wg2_bufs(dev, N, K):
+    """The two modalities' [dW | db] buffers of _weight_grads2 (allocated on the calling stream)."""
+    return [torch.empty(N * (K + 1), device=dev, dtype=torch.float32) for _ in range(2)]
+
+
+def _weight_grads2(dy, x, M, N, K, bufs=None):
+    """_weight_grads of both modalities (dy [2M][N], x [2M][K]) in one launch: ((dW, db) RGB, (dW, db) TIR).
+    bufs: preallocated _wg2_bufs (the dual-stream backward allocates on the main stream)."""
+    bufs = bufs if bufs is not None else _wg2_bufs(dy.device, N, K)
     dws = tuple(b[:N * K].view(N, K) for b in bufs)
     dbs = tuple(b[N * K:] for b in bufs)
     if not (MN_MAJOR and M % 8 == 0):
@@ -375,8 +429,9 @@ class _HipLinear2(torch.autograd.Function):
         M2, K = x.shape
         M, N = M2 // 2, wb0.shape[0]
         dy = dy.to(torch.bfloat16).contiguous()
-        dx = _dx2(dy, (wb0, wb1), M, N, K) if ctx.needs_input_grad[0] else None
-        (dw0, db0), (dw1, db1) = _weight_grads2(dy, x, M, N, K)
+        with _Beside(dy.device) as side:
+            (dw0, db0), (dw1, db1) = side.run(_weight_grads2, dy, x, M, N, K, bufs=_wg2_bufs(dy.device, N, K))
+            dx = _dx2(dy, (wb0, wb1), M, N, K) if ctx.needs_input_grad[0] else None
         return dx, dw0, db0, dw1, db1, None
 
 
@@ -416,8 +471,9 @@ class _HipLinearResidual2(torch.autograd.Function):
         M2, K = a.shape
         M, N = M2 // 2, wb0.shape[0]
         dy = _scaled_bf16(dout.reshape(M2, N), keep, ctx.rows)
-        da = _dx2(dy, (wb0, wb1), M, N, K) if ctx.needs_input_grad[1] else None
-        (dw0, db0), (dw1, db1) = _weight_grads2(dy, a, M, N, K)
+        with _Beside(dy.device) as side:
+            (dw0, db0), (dw1, db1) = side.run(_weight_grads2, dy, a, M, N, K, bufs=_wg2_bufs(dy.device, N, K))
+            da = _dx2(dy, (wb0, wb1), M, N, K) if ctx.needs_input_grad[1] else None
         return dout, da, dw0, db0, dw1, db1, None
 
 
@@ -447,10 +503,11 @@ class _HipMlpResidual2(torch.autograd.Function):
         M2, C = xn.shape
         M, F4 = M2 // 2, wb10.shape[0]
         dy = _scaled_bf16(dout.reshape(M2, C), keep, ctx.rows)
-        dhp = _dx2(dy, (wb20, wb21), M, C, F4, act=5, r=hp)
-        (dw20, db20), (dw21, db21) = _weight_grads2(dy, h, M, C, F4)
-        dxn = _dx2(dhp, (wb10, wb11), M, F4, C) if ctx.needs_input_grad[1] else None
-        (dw10, db10), (dw11, db11) = _weight_grads2(dhp, xn, M, F4, C)
+        with _Beside(dy.device) as side:
+            (dw20, db20), (dw21, db21) = side.run(_weight_grads2, dy, h, M, C, F4, bufs=_wg2_bufs(dy.device, C, F4))
+            dhp = _dx2(dy, (wb20, wb21), M, C, F4, act=5, r=hp)
+            (dw10, db10), (dw11, db11) = side.run(_weight_grads2, dhp, xn, M, F4, C, bufs=_wg2_bufs(dy.device, F4, C))
+            dxn = _dx2(dhp, (wb10, wb11), M, F4, C) if ctx.needs_input_grad[1] else None
         return dout, dxn, dw10, db10, dw20, db20, dw11, db11, dw21, db21, None
 
 

@@ -74,6 +74,39 @@ def test_msda_backward_deterministic(N, Lq, M, D, shapes, P):
         assert all(torch.equal(a, b) for a, b in zip(grads[0], g))
 
 
+@pytest.mark.parametrize("N,Lq,M,D,shapes,P", [(16, 400, 8, 64, [(20, 20), (20, 20)], 4),
+                                              (2, 37, 3, 32, [(6, 5), (3, 7), (1, 1)], 3),
+                                              (1, 512, 2, 64, [(32, 32)], 4)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_msda_backward_value_gathers_equal(N, Lq, M, D, shapes, P, dtype):
+    """grad_value from the per-(n, m, level) gather (value_impl 2) equals the 64-pixel-chunk
+    gather's (value_impl 1) bit for bit -- both sum each pixel's taps in (sample, tap) order -- and so do grad_loc /
+    grad_attn; the auto choice (the plain entry) equals them too."""
+    from mmt_amd import _lib as L_
+    (v, loc, w, go), shp, starts = _msda_case(N, Lq, M, D, shapes, P, dtype, seed=5)
+    v, loc, w, go = (x.cuda().contiguous() for x in (v, loc, w, go))
+    sh = torch.tensor(shp, dtype=torch.long, device="cuda")
+    st = torch.tensor(starts, dtype=torch.long, device="cuda")
+    S = v.shape[1]
+    dt = L_.MMT_F32 if dtype == torch.float32 else L_.MMT_F64
+    outs = []
+    for impl in (1, 2, None):
+        gv, gl, ga = torch.empty_like(v), torch.empty_like(loc), torch.empty_like(w)
+        args = (v.data_ptr(), sh.data_ptr(), st.data_ptr(), loc.data_ptr(), w.data_ptr(), go.data_ptr(), gv.data_ptr(),
+                gl.data_ptr(), ga.data_ptr(), N, S, M, D, Lq, len(shapes), P)
+        stream = torch.cuda.current_stream().cuda_stream
+        if impl is None:
+            L_.check(L_.LIB.mmt_ms_deform_attn_backward(*args, dt, stream), "auto")
+        else:
+            L_.check(L_.LIB.mmt_ms_deform_attn_backward_impl(*args, max(h * w_ for h, w_ in shp), impl, dt, stream),
+                     "impl %d" % impl)
+        torch.cuda.synchronize()
+        outs.append((gv, gl, ga))
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert torch.equal(a, b)
+
+
 def test_msda_backward_zero_for_skipped_samples():
     from mmt_amd.functional import MSDeformAttnFunction
     (v, loc, w, go), shapes, starts = _msda_case(1, 3, 2, 8, [(6, 4), (3, 2)], 2, torch.float32)

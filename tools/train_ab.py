@@ -107,6 +107,17 @@ def aten_scale_cast():
 
 
 @contextlib.contextmanager
+def dual_stream():
+    """The pair backward's weight-gradient GEMMs on a side stream beside the input-gradient GEMMs."""
+    from mmt_amd import train
+    train.DUAL_STREAM = True
+    try:
+        yield
+    finally:
+        train.DUAL_STREAM = False
+
+
+@contextlib.contextmanager
 def sequential_backbones():
     """The two-stream backbones one after the other (one-group GEMMs) instead of backbone_forward_pair."""
     from mmt_amd import train
@@ -128,7 +139,8 @@ def main():
     variants = {"hip": HipOps, "aten_groupnorm": AtenGroupNormOps, "aten_layernorm": AtenLayerNormOps,
                 "split_mlp": SplitMlpOps, "unfused_residual": UnfusedResidualOps, "accum_grads": (HipOps, accumulated_grads),
                 "transposed": (HipOps, transposed_copies), "aten_scale_cast": (HipOps, aten_scale_cast),
-                "sequential": (HipOps, sequential_backbones), "composed_encoder": ComposedEncoderOps}
+                "sequential": (HipOps, sequential_backbones), "composed_encoder": ComposedEncoderOps,
+                "dual_stream": (HipOps, dual_stream)}
     if args.only:
         variants = {k: v for k, v in variants.items() if k in args.only.split(",")}
     for r in range(args.rounds):
