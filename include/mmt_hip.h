@@ -538,6 +538,11 @@ int mmt_corner_boxes_bwd(const float* score_tl, const float* score_br, const flo
 int mmt_box_loss(const float* pred, const float* gt, float* out, int B, float iou_w, float l1_w, void* stream);
 int mmt_box_loss_bwd(const float* pred, const float* gt, const float* dloss, float* dpred, int B, float iou_w,
                      float l1_w, void* stream);
+/* mmt_ft_rows_cast: out [S][nrows][C] bf16 = the rows [row0, row0 + nrows) of x [S][rows][C] fp32 (the backbones'
+ * search tokens as the fusion's adjust Linears read them, mixformer.py:256-259 -> fusion_utils.py:270-275); _bwd: dx
+ * [S][rows][C] fp32 = dout on those rows, 0 elsewhere. */
+int mmt_ft_rows_cast(const float* x, void* out, int S, int rows, int row0, int nrows, int C, void* stream);
+int mmt_ft_rows_cast_bwd(const void* dout, float* dx, int S, int rows, int row0, int nrows, int C, void* stream);
 int mmt_ft_query_prep(const float* src, const float* lpos, void* qbi, void* srcb, int B, int nq, int d, void* stream);
 int mmt_ft_query_prep_bwd(const void* dqbi, const void* dsrcb, const float* dthrough, float* dsrc, float* dlpos, int B,
                           int nq, int d, void* stream);

@@ -215,6 +215,39 @@ __global__ __launch_bounds__(256) void ft_relu_drop_bwd_kernel(const bf16_t* __r
     st8_bf16(dh + i * 8, g);
 }
 
+// out [S][nrows][C] bf16 = bf16(x[s][row0 + r][c]) of x [S][rows][C] fp32 (the backbones' search tokens for the
+// fusion's adjust Linears); backward: dx [S][rows][C] fp32 = float(dout) on those rows, 0 on the others
+__global__ __launch_bounds__(256) void ft_rows_cast_kernel(const float* __restrict__ x, bf16_t* __restrict__ out,
+                                                           int rows, int row0, int nrows, int c8, int64_t total) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // chunk of out
+    if (i >= total) return;
+    const int c = (int)(i % c8);
+    const int64_t sr = i / c8;
+    const int r = (int)(sr % nrows);
+    const int64_t sq = sr / nrows;
+    float v[8];
+    ld8_f32(x + ((sq * rows + row0 + r) * c8 + c) * 8, v);
+    st8_bf16(out + i * 8, v);
+}
+
+__global__ __launch_bounds__(256) void ft_rows_cast_bwd_kernel(const bf16_t* __restrict__ dout, float* __restrict__ dx,
+                                                               int rows, int row0, int nrows, int c8, int64_t total) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // chunk of dx
+    if (i >= total) return;
+    const int c = (int)(i % c8);
+    const int64_t sr = i / c8;
+    const int r = (int)(sr % rows) - row0;
+    const int64_t sq = sr / rows;
+    float v[8];
+    if (r >= 0 && r < nrows) {
+        ld8_bf16(dout + ((sq * nrows + r) * c8 + c) * 8, v);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = 0.f;
+    }
+    st8_f32(dx + i * 8, v);
+}
+
 FtDrop make_drop(const int64_t* state, int salt, float p) {
     FtDrop d;
     d.state = state;
@@ -288,5 +321,26 @@ extern "C" int mmt_ft_relu_drop_bwd(const void* dy, const void* h, void* dh, con
     if (((uintptr_t)dy | (uintptr_t)h | (uintptr_t)dh) & 15) return MMT_EBADARG;
     hipLaunchKernelGGL(ft_relu_drop_bwd_kernel, dim3(grid_of(n / 8)), dim3(256), 0, (hipStream_t)stream,
                        (const bf16_t*)dy, (const bf16_t*)h, (bf16_t*)dh, make_drop(rng, salt, p), n / 8);
+    return launch_status();
+}
+
+extern "C" int mmt_ft_rows_cast(const float* x, void* out, int S, int rows, int row0, int nrows, int C, void* stream) {
+    if (!x || !out || S <= 0 || rows <= 0 || row0 < 0 || nrows <= 0 || row0 + nrows > rows || C <= 0 || C % 8)
+        return MMT_EBADARG;
+    if (((uintptr_t)x | (uintptr_t)out) & 15) return MMT_EBADARG;
+    const int64_t total = (int64_t)S * nrows * (C / 8);
+    hipLaunchKernelGGL(ft_rows_cast_kernel, dim3(grid_of(total)), dim3(256), 0, (hipStream_t)stream, x, (bf16_t*)out,
+                       rows, row0, nrows, C / 8, total);
+    return launch_status();
+}
+
+extern "C" int mmt_ft_rows_cast_bwd(const void* dout, float* dx, int S, int rows, int row0, int nrows, int C,
+                                    void* stream) {
+    if (!dout || !dx || S <= 0 || rows <= 0 || row0 < 0 || nrows <= 0 || row0 + nrows > rows || C <= 0 || C % 8)
+        return MMT_EBADARG;
+    if (((uintptr_t)dout | (uintptr_t)dx) & 15) return MMT_EBADARG;
+    const int64_t total = (int64_t)S * rows * (C / 8);
+    hipLaunchKernelGGL(ft_rows_cast_bwd_kernel, dim3(grid_of(total)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)dout, dx, rows, row0, nrows, C / 8, total);
     return launch_status();
 }

@@ -96,6 +96,8 @@ _PROTOS = {
     "mmt_msda_bimodal_train_fwd": [vp, vp, i32, vp, i32, vp, vp, i32, i32, vp],
     "mmt_msda_bimodal_train_bwd": [vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, i32, i32, vp],
     "mmt_ft_query_prep": [vp, vp, vp, vp, i32, i32, i32, vp],
+    "mmt_ft_rows_cast": [vp, vp, i32, i32, i32, i32, i32, vp],
+    "mmt_ft_rows_cast_bwd": [vp, vp, i32, i32, i32, i32, i32, vp],
     "mmt_corner_boxes": [vp, vp, vp, vp, i32, i32, f32, f32, vp],
     "mmt_corner_boxes_bwd": [vp, vp, vp, vp, vp, vp, i32, i32, f32, f32, vp],
     "mmt_box_loss": [vp, vp, vp, i32, f32, f32, vp],

@@ -902,6 +902,72 @@ def _drop_rng(device):
     return st
 
 
+class _HipSearchTokens(torch.autograd.Function):
+    """The two backbones' search tokens as the fusion's adjust Linears read them (mixformer.py:256-259 ->
+    fusion_utils.py:270-275): x (2B, ntok, C) fp32 (RGB sequences first) -> rows [n_t, ntok) as bf16 (2B, ns, C),
+    one pass (mmt_ft_rows_cast); backward: the stream's gradient with zero template rows, one pass (replaces the
+    slice / transpose / reshape / cast chain and its zero-filling slice backwards)."""
+
+    @staticmethod
+    def forward(ctx, x, n_t):
+        from ._lib import LIB, check
+        S, ntok, C = x.shape
+        x = x.contiguous()
+        out = torch.empty(S, ntok - n_t, C, device=x.device, dtype=torch.bfloat16)
+        check(LIB.mmt_ft_rows_cast(x.data_ptr(), out.data_ptr(), S, ntok, n_t, ntok - n_t, C, _stream()),
+              "mmt_ft_rows_cast")
+        ctx.args = (S, ntok, n_t, C)
+        return out
+
+    @staticmethod
+    def backward(ctx, d):
+        from ._lib import LIB, check
+        S, ntok, n_t, C = ctx.args
+        d = d.to(torch.bfloat16).contiguous()
+        dx = torch.empty(S, ntok, C, device=d.device, dtype=torch.float32)
+        check(LIB.mmt_ft_rows_cast_bwd(d.data_ptr(), dx.data_ptr(), S, ntok, n_t, ntok - n_t, C, _stream()),
+              "mmt_ft_rows_cast_bwd")
+        return dx, None
+
+
+class _HipGroupNorm2(torch.autograd.Function):
+    """The fusion's adjust_v / adjust_i GroupNorms (fusion_utils.py:252-268) on the stacked modalities' rows
+    x (2B, P, C) fp32 (RGB first), each half with its own affine -> (RGB (B, P, C), TIR (B, P, C)) as two tensors
+    (so the cat that follows hands each its gradient as a view); backward: one dx buffer for both halves."""
+
+    @staticmethod
+    def forward(ctx, x, w0, b0, w1, b1, groups, eps):
+        from ._lib import LIB, MMT_F32, check
+        n2, P, C = x.shape
+        B = n2 // 2
+        x = x.contiguous()
+        outs = []
+        for h, (w, b) in enumerate(((w0, b0), (w1, b1))):
+            o = torch.empty(B, P, C, device=x.device, dtype=torch.float32)
+            check(LIB.mmt_groupnorm(x[h * B:].data_ptr(), o.data_ptr(), None, w.data_ptr(), b.data_ptr(), None, None, B,
+                                    B, P, C, groups, eps, MMT_F32, _stream()), "mmt_groupnorm")
+            outs.append(o)
+        ctx.save_for_backward(x, w0, w1)
+        ctx.groups, ctx.eps = groups, eps
+        return outs[0], outs[1]
+
+    @staticmethod
+    def backward(ctx, dv, di):
+        from ._lib import LIB, check
+        x, w0, w1 = ctx.saved_tensors
+        n2, P, C = x.shape
+        B = n2 // 2
+        dx = torch.empty_like(x)
+        dgb = torch.empty(2, 2, C, device=x.device, dtype=torch.float32)
+        ws = torch.empty(B * 2 * C, device=x.device, dtype=torch.float32)
+        for h, (dy, w) in enumerate(((dv, w0), (di, w1))):
+            dy = dy.float().contiguous() if dy is not None else torch.zeros(B, P, C, device=x.device)
+            check(LIB.mmt_groupnorm_bwd(x[h * B:].data_ptr(), dy.data_ptr(), w.data_ptr(), dx[h * B:].data_ptr(),
+                                        dgb[h].data_ptr(), 0, ws.data_ptr(), ws.numel(), B, P, C, ctx.groups, ctx.eps,
+                                        _stream()), "mmt_groupnorm_bwd")
+        return dx, dgb[0, 0], dgb[0, 1], dgb[1, 0], dgb[1, 1], None, None
+
+
 class _HipQueryPrep(torch.autograd.Function):
     """The encoder layer's inputs from its fp32 stream src (B, 2 nq, d) and the level-embedded positions lpos
     (1, 2 nq, d) (deformable_encoder_lnspecific.py:131-136, ms_deform_attn_bimodal.py:97-105): q_bi = the bimodal
@@ -1458,7 +1524,7 @@ def backbone_forward(bb, t, o, s, ops, drop_path_rate=DROP_PATH_RATE):
     return xs.transpose(1, 2).reshape(B, C, gs, gs)
 
 
-def backbone_forward_pair(bv, bi, t, o, s, ops, drop_path_rate=DROP_PATH_RATE):
+def backbone_forward_pair(bv, bi, t, o, s, ops, drop_path_rate=DROP_PATH_RATE, tokens=False):
     """backbone_forward of the two-stream model's RGB (bv) and TIR (bi) backbones in lockstep, the
     modalities stacked on the batch ([rgb; tir], t / o / s pairs of (B, 3, H, W)): the same math per
     modality (mixformer.py:231-259, own weights, own norms, own DropPath draws), but every Linear and
@@ -1490,15 +1556,19 @@ def backbone_forward_pair(bv, bi, t, o, s, ops, drop_path_rate=DROP_PATH_RATE):
         xn, xr = _layer_norm_pass(ops, x, kv.norm2, ki.norm2)
         mp = [(k.mlp.fc1.weight, k.mlp.fc1.bias, k.mlp.fc2.weight, k.mlp.fc2.bias) for k in (kv, ki)]
         x = ops.mlp_residual2(xr, xn.view(M2, C), mp[0], mp[1], keep)
+    if tokens:  # the search tokens as bf16 rows (2B, ns, C), RGB first, for the fusion's token-row adjust
+        return _HipSearchTokens.apply(x, n_t), None
     xs = x[:, n_t:].transpose(1, 2).reshape(2 * B, C, gs, gs)
     return xs[:B], xs[B:]
 
 
-def _backbones_rgbt(net, template, online_template, search, ops, dpr):
+def _backbones_rgbt(net, template, online_template, search, ops, dpr, tokens=False):
     """(s_v, s_i) of the two-stream model: the lockstep pair when the ops provide grouped Linears (HipOps),
-    else one backbone after the other."""
+    else one backbone after the other.  tokens (lockstep pair only): (the search tokens of both as bf16 rows (2B, ns,
+    C), RGB first, None) instead of two (B, C, gs, gs) maps (fusion_forward takes either)."""
     if PAIR and getattr(ops, "linear2", None) is not None:
-        return backbone_forward_pair(net.backbone_v, net.backbone_i, template, online_template, search, ops, dpr)
+        return backbone_forward_pair(net.backbone_v, net.backbone_i, template, online_template, search, ops, dpr,
+                                     tokens=tokens)
     return (backbone_forward(net.backbone_v, template[0], online_template[0], search[0], ops, dpr),
             backbone_forward(net.backbone_i, template[1], online_template[1], search[1], ops, dpr))
 
@@ -1564,14 +1634,30 @@ def fusion_forward(fu, s_v, s_i, ops):
     """Attention_Fusion_Bimodal_LNSpecific.forward (fusion_utils.py:270-279) with the deformable
     encoder (deformable_encoder_lnspecific.py:131-160) and MSDeformAttn_Bimodal
     (ms_deform_attn_bimodal.py:83-130)."""
-    b, _, h, w = s_v.shape
     tokens = getattr(ops, "group_norm", None) is not None  # adjust_* on token rows (HIP GEMM + GroupNorm)
-    if tokens:
+    if s_i is None:  # both modalities' search tokens as bf16 rows (2B, ns, C) (_backbones_rgbt tokens=True)
+        b, P, Cin = s_v.shape[0] // 2, s_v.shape[1], s_v.shape[2]
+        h = w = int(round(P ** 0.5))
+        if not tokens or h * w != P or getattr(ops, "linear2", None) is None:
+            raise ValueError("fusion_forward: token-row inputs need the grouped token-row adjust (HipOps), square maps")
+        cv, ci = fu.adjust_v[0], fu.adjust_i[0]
+        y = ops.linear2(s_v.view(2 * b * P, Cin), cv.weight.view(cv.weight.shape[0], Cin), cv.bias,
+                        ci.weight.view(ci.weight.shape[0], Cin), ci.bias, out_f32=True)
+        gv, gi = fu.adjust_v[1], fu.adjust_i[1]
+        if (gv.num_groups, gv.eps) != (gi.num_groups, gi.eps):
+            raise ValueError("fusion_forward: the two adjust GroupNorms differ in groups / eps")
+        av, ai = _HipGroupNorm2.apply(y.view(2 * b, P, -1), gv.weight, gv.bias, gi.weight, gi.bias, gv.num_groups,
+                                      gv.eps)
+        d = av.shape[2]
+        src = torch.cat([av, ai], 1)
+    elif tokens:
+        b, _, h, w = s_v.shape
         av = _adjust_tokens(ops, fu.adjust_v, s_v.flatten(2).transpose(1, 2))
         ai = _adjust_tokens(ops, fu.adjust_i, s_i.flatten(2).transpose(1, 2))
         d = av.shape[2]
         src = torch.cat([av, ai], 1)
     else:
+        b, _, h, w = s_v.shape
         av, ai = fu.adjust_v(s_v), fu.adjust_i(s_i)
         d = av.shape[1]
         src = torch.cat([av.flatten(2).transpose(1, 2), ai.flatten(2).transpose(1, 2)], 1)
@@ -1824,11 +1910,19 @@ def head_forward(hd, x, ops=None):
     return torch.stack(coords, dim=1) / hd.img_sz
 
 
+def _token_rows(ops):
+    """The backbones hand the fusion bf16 token rows (HipOps: the lockstep pair and the token-row adjust)."""
+    return PAIR and TOKEN_ROWS and all(getattr(ops, n, None) is not None for n in ("linear2", "group_norm"))
+
+
+TOKEN_ROWS = True  # False: NCHW search maps between backbone and fusion (the pre-round-6 chain; A/B knob)
+
+
 def forward_boxes(net, template, online_template, search, ops):
     """MixFormer_RGBT.forward (mixformer.py:366-395) + forward_box_head (:419-432): pred_boxes
     (B, 1, 4) cxcywh.  Stochastic depth at the module's drop_path_rate (as module_forward)."""
     dpr = getattr(net, "drop_path_rate", DROP_PATH_RATE)
-    s_v, s_i = _backbones_rgbt(net, template, online_template, search, ops, dpr)
+    s_v, s_i = _backbones_rgbt(net, template, online_template, search, ops, dpr, tokens=_token_rows(ops))
     with torch.autocast(s_v.device.type, dtype=torch.bfloat16, enabled=s_v.device.type == "cuda"):
         fused = fusion_forward(net.fusion_vi, s_v, s_i, ops)
         xyxy = head_forward(net.box_head, fused, ops)
@@ -1847,7 +1941,7 @@ def module_forward(net, template, online_template, search, ops, run_score_head=F
     variant = net.variant
     dpr = getattr(net, "drop_path_rate", DROP_PATH_RATE)
     if variant == "rgbt":
-        s_v, s_i = _backbones_rgbt(net, template, online_template, search, ops, dpr)
+        s_v, s_i = _backbones_rgbt(net, template, online_template, search, ops, dpr, tokens=_token_rows(ops))
         tok = None
     elif variant in ("shared", "asym", "asym_online"):
         feats, tok = backbone_forward_stacked(net.backbone, torch.cat(template, 0), torch.cat(online_template, 0),

@@ -1000,6 +1000,42 @@ def test_hip_box_loss_matches_autograd():
     assert math.isnan(box_loss(same_pred, same)[0].item()) and math.isnan(HipOps.box_loss(same_pred, same)[0].item())
 
 
+def test_token_rows_match_maps():
+    """The backbones handing the fusion bf16 token rows (_HipSearchTokens, the adjust_v / adjust_i Linears as one
+    grouped launch and _HipGroupNorm2; round 6) against the NCHW search maps and per-modality adjusts
+    (TOKEN_ROWS False): pred boxes and every gradient of the rgbt module at B = 2 equal within 1e-6 relative L2
+    (the same values through the same kernels; only the dispatch differs)."""
+    import mmt_amd.model as M
+    import mmt_amd.train as T
+    from mmt_amd.train import HipOps, module_forward, synthetic_batch
+    torch.manual_seed(0)
+    net = M.build_mixformer_vit_rgbt(M.hot_path_cfg(), train=False).cuda().train()
+    net.drop_path_rate = 0.0
+    for m in net.modules():
+        if isinstance(m, torch.nn.Dropout):
+            m.p = 0.0
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.eval()
+    t, o, s, gt = synthetic_batch(2, "cuda", torch.Generator().manual_seed(7))
+    res = []
+    for rows in (True, False):
+        T.TOKEN_ROWS = rows
+        try:
+            net.zero_grad(set_to_none=True)
+            _, coord = module_forward(net, t, o, s, HipOps)
+            (coord.float() * torch.arange(1, 5, device="cuda").view(1, 1, 4)).sum().backward()
+        finally:
+            T.TOKEN_ROWS = True
+        res.append((coord.detach().float(), {n: p.grad.detach().clone() for n, p in net.named_parameters()
+                                             if p.grad is not None}))
+    (c1, g1), (c0, g0) = res
+    assert set(g1) == set(g0)
+    assert ((c1 - c0).norm() / c0.norm()).item() <= 1e-6
+    for n in g0:
+        err = ((g1[n].float() - g0[n].float()).norm() / g0[n].float().norm().clamp_min(1e-30)).item()
+        assert err <= 1e-6, (n, err)
+
+
 def _fusion_module(seed=3):
     from mmt_amd.model import Attention_Fusion_Bimodal_LNSpecific
     torch.manual_seed(seed)
