@@ -24,6 +24,26 @@ namespace {
 
 constexpr int D = 64, TP = 160;  // head dim, LDS row pitch (bytes)
 
+// Register budgets (A/B knobs; 0 = the compiler's choice): the dkv kernel at >= 3 waves per SIMD (147 registers, no
+// spills) instead of the compiler's 182 (2 waves): 252 -> 215 us for the training shape's backward, the same results
+// (tools/attn_bwd_ab.py, profiles/r06_attn_bwd_ab.txt).  4 waves spills.
+#ifndef MMT_BWD_DKV_WAVES
+#define MMT_BWD_DKV_WAVES 3
+#endif
+#ifndef MMT_BWD_DQ_WAVES
+#define MMT_BWD_DQ_WAVES 0
+#endif
+#if MMT_BWD_DKV_WAVES > 0
+#define MMT_BWD_DKV_ATTR __attribute__((amdgpu_waves_per_eu(MMT_BWD_DKV_WAVES)))
+#else
+#define MMT_BWD_DKV_ATTR
+#endif
+#if MMT_BWD_DQ_WAVES > 0
+#define MMT_BWD_DQ_ATTR __attribute__((amdgpu_waves_per_eu(MMT_BWD_DQ_WAVES)))
+#else
+#define MMT_BWD_DQ_ATTR
+#endif
+
 MMT_DEV bf16x8 tr_frag(const char* tile, int kk, int dt, int lg, int l16) {
     // A operand [16 rows of d][32 k] read transposed from a row-major [k][d] tile: rows
     // 32kk + 4lg + qr and +16 (the same permuted k order as pack_p below), d = dt*16 + 4pc..+3
@@ -77,7 +97,7 @@ MMT_DEV void store_tile(char* tile, const u32x4 (&v)[2], float c) {
     }
 }
 
-__global__ __launch_bounds__(256) void mam_bwd_dq_kernel(const mmt_attn_bwd_params p) {
+__global__ __launch_bounds__(256) MMT_BWD_DQ_ATTR void mam_bwd_dq_kernel(const mmt_attn_bwd_params p) {
     __shared__ __attribute__((aligned(16))) char kt_l[64 * TP];
     __shared__ __attribute__((aligned(16))) char vt_l[64 * TP];
     const int qb = blockIdx.x, h = blockIdx.y, s = blockIdx.z;
@@ -162,7 +182,7 @@ __global__ __launch_bounds__(256) void mam_bwd_dq_kernel(const mmt_attn_bwd_para
     }
 }
 
-__global__ __launch_bounds__(256) void mam_bwd_dkv_kernel(const mmt_attn_bwd_params p) {
+__global__ __launch_bounds__(256) MMT_BWD_DKV_ATTR void mam_bwd_dkv_kernel(const mmt_attn_bwd_params p) {
     __shared__ __attribute__((aligned(16))) char q_l[64 * TP];
     __shared__ __attribute__((aligned(16))) char do_l[64 * TP];
     __shared__ float lse_l[64], del_l[64];
