@@ -196,17 +196,17 @@ typedef struct {
     float scale;
     int32_t impl; /* bf16 kernel choice (results equal within bf16 rounding): 0 auto (bf16: the
                      latency kernel 4 below ~200 throughput workgroups, 21 up to ~900, 22 from
-                     there; the training forward (lse) and fp16 use 8 on large grids);
+                     there; the training forward (lse) 21 on large grids (round 6), fp16 8);
                      2 / 4 = latency kernel, key tiles split over 2 / 4 groups of 4 waves;
                      8 = running-maximum throughput kernel (128 queries per workgroup, 3 per CU);
                      9 = 8 with a 3-deep ring, 2 workgroups per CU; 10-12 = 32x32x16 variants of 8;
                      16-19 = range-checked exponent kernel variants, 17 = its MFMA row-sum form;
                      20 = persistent whole-pair kernel (ViT-B 128/320 shape only);
                      21 = 17 with its two key blocks per tile software-pipelined;
-                     22 = 21's math with 64 queries per wave (bf16; 16-22 without lse).
+                     22 = 21's math with 64 queries per wave (bf16; writes no lse).
                      q may arrive pre-multiplied by scale*log2(e); then pass scale = 1/log2(e). */
     float* lse;   /* NULL, or [S][H][ntok] fp32: per query the log2-sum-exp2 of its pre-scaled scores
-                     (training forward; selects the throughput kernel, bf16 only) */
+                     (training forward, bf16 only; impls 0 / 4 / 8 / 17 / 21) */
     int32_t q_part; /* 0: all queries; 1: template queries [0,n_t) only; 2: search queries
                        [n_t,ntok) only -- the template K/V cache: template rows of qkv computed
                        once per template update, only the search rows per frame.  Rows of `out`

@@ -1898,11 +1898,13 @@ int launch_attn(const mmt_attn_params& p, hipStream_t st) {
             // MMT_ATTN_LZ2_MIN_WG workgroups (impl 22), else with its two blocks per tile software-
             // pipelined (impl 21; B = 8 / 32: 27.2 / 78.9 us against 29.8 / 83.8 for impl 17 and 30-34 /
             // 84-93 for impl 8, profiles/r02_attn_ab.jsonl, r02_pipe_ab.jsonl); the training forward
-            // (lse) and fp16 keep the running-maximum throughput kernel; small grids (batch-1 tracking):
-            // the latency kernel (64 queries x 4 key groups)
+            // (lse) takes impl 21 too (round 6: 46.9 vs 56.2 us for impl 8 at the training shape, 32 sequences,
+            // tools/attn_fwd_lse_ab.py, profiles/r06_attn_fwd_lse_ab.txt; impl 22 writes no lse); fp16 keeps the
+            // running-maximum throughput kernel; small grids (batch-1 tracking): the latency kernel (64 queries x 4
+            // key groups)
             const int64_t wg = (int64_t)nfa * p.H * p.S;
             if (bf && !p.lse && wg >= MMT_ATTN_LZ2_MIN_WG) impl = 22;
-            else if (bf && !p.lse && wg >= MMT_ATTN_FA_MIN_WG) impl = 21;
+            else if (bf && wg >= MMT_ATTN_FA_MIN_WG) impl = 21;
             else if (p.lse || wg >= MMT_ATTN_FA_MIN_WG) impl = 8;
             else impl = 4;
         }
