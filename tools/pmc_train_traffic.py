@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""HBM traffic of one whole training step from the FETCH_SIZE / WRITE_SIZE passes of tools/session_r05tpmc.sh
+"""HBM traffic of one whole training step from the FETCH_SIZE / WRITE_SIZE passes of tools/sessions/session_r05tpmc.sh
 (rocprofv3 --pmc over `bench.py --train`, the step one hipGraph replay): the dispatches between consecutive AdamW
 update kernels are one step; traffic = 2 x FETCH_SIZE + WRITE_SIZE (KiB, gfx950 correction, MI355X_MICROARCH.md),
 the median over the recorded steps, merged into profiles/pmc_traffic.json under "train/B<batch>/bf16" with the

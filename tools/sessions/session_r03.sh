@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-3 GPU session: the given pytest selection, then optional tools, then the bench with the in-frame
-# profile.  Stops at the first crash / fault / timeout.  Usage: tools/session_r03.sh TAG "pytest args" [tool cmds...]
+# profile.  Stops at the first crash / fault / timeout.  Usage: tools/sessions/session_r03.sh TAG "pytest args" [tool cmds...]
 set -u
 TAG=$1; shift
 PT=$1; shift

@@ -7,5 +7,5 @@ timeout -k 10 500 python -u -m pytest tests/test_gpu_ops.py tests/test_gpu_train
 rc=$?; tail -2 $OUT/pytest.log; [ $rc -ne 0 ] && exit $rc
 bash tools/ab_lib_trainonly.sh r05d3 dwsplit 3 || exit 1
 cd "$ROOT" && bash tools/pmc_session.sh r05pmc3 > $OUT/pmc.log 2>&1; rc=$?; tail -3 $OUT/pmc.log; [ $rc -ne 0 ] && exit $rc
-cd "$ROOT" && bash tools/session_r05tpmc.sh
+cd "$ROOT" && bash tools/sessions/session_r05tpmc.sh
 exit 0

@@ -7,4 +7,4 @@ timeout -k 10 200 python -u tools/head_stage_error.py > $OUT/head_stage.jsonl 2>
 rc=$?; echo "head rc=$rc"; [ $rc -ne 0 ] && { tail -5 $OUT/head_stage.err; exit $rc; }
 timeout -k 10 200 python -u tools/plan_entry_ab.py --names head_conv1_adj12,enc_linear2 --cfgs 0:0,3:1,2:1,1:1,2:2,2:3,3:2 > $OUT/entry_ab.jsonl 2> $OUT/entry_ab.err
 rc=$?; echo "entry rc=$rc"; cat $OUT/entry_ab.jsonl; [ $rc -ne 0 ] && { tail -5 $OUT/entry_ab.err; exit $rc; }
-bash tools/session_r05p.sh
+bash tools/sessions/session_r05p.sh

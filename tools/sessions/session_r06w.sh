@@ -7,4 +7,4 @@ timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 rc=$?; tail -3 $OUT/msda_tests.log; [ $rc -ne 0 ] && { grep -E "Error|assert" $OUT/msda_tests.log | head -20; exit $rc; }
 timeout -k 10 120 python -u tools/msda_train_ab.py 2>&1 | grep -v amdgpu.ids
 rc=$?; [ $rc -ne 0 ] && exit $rc
-bash tools/session_r06t.sh ${T}_s
+bash tools/sessions/session_r06t.sh ${T}_s

@@ -2,7 +2,7 @@
 """Training-step kernels in isolation, for counter collection: the config-4 shapes (16 pairs,
 lockstep backbones: 2 x 8448 rows) of the backbone's Linear / MLP autograd Functions (forward, dX, dW) and the
 fusion encoder's MSDA forward + backward, each case run `--reps` times between marker kernels
-(torch.cuda._sleep), so that a rocprofv3 --pmc pass of this script (tools/session_r05p.sh) maps every dispatch to
+(torch.cuda._sleep), so that a rocprofv3 --pmc pass of this script (tools/sessions/session_r05p.sh) maps every dispatch to
 its case without the bench's training line (the profiler crashed under the full bench with counters on).
 
   python tools/train_kernels_pmc.py --reps 3                 # run (under rocprofv3 --pmc ...)
