@@ -43,6 +43,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_stats_kernel(const u32x4* __res
     for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
     unpack8(x[ck], piv);
     if (rl < R) {
+#pragma unroll 4
         for (int64_t r = r0 + rl; r < r1; r += R) {
             float v[8];
             unpack8(x[r * C8 + ck], v);
@@ -79,7 +80,23 @@ MMT_DEV void bn_lane_sums(const float* __restrict__ part, int nblk, int C, int c
                           double& b) {
     double s = 0.0, q = 0.0;
     if (c < C) {
-        for (int k = lane; k < nblk; k += BN_FLANES) {
+        // eight partials' loads in flight, then summed in k order (round 6: one load per iteration serialised the
+        // loop on its latency, ~9 us per finalize launch)
+        int k = lane;
+        for (; k + 7 * BN_FLANES < nblk; k += 8 * BN_FLANES) {
+            float a[8], b[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                a[j] = part[((int64_t)(k + j * BN_FLANES) * 2) * C + c];
+                b[j] = part[((int64_t)(k + j * BN_FLANES) * 2 + 1) * C + c];
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                s += (double)a[j];
+                q += (double)b[j];
+            }
+        }
+        for (; k < nblk; k += BN_FLANES) {
             s += (double)part[((int64_t)k * 2) * C + c];
             q += (double)part[((int64_t)k * 2 + 1) * C + c];
         }
@@ -172,6 +189,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_stats_kernel(const u32x4* _
         sh[j] = in ? save[3 * C + c0 + j] : 0.f;
     }
     if (rl < R) {
+#pragma unroll 4
         for (int64_t r = r0 + rl; r < r1; r += R) {
             float v[8], d[8];
             unpack8(x[r * C8 + ck], v);
