@@ -48,6 +48,11 @@
 #ifndef MMT_GEMM_SK_TICKET_FIRST
 #define MMT_GEMM_SK_TICKET_FIRST 0
 #endif
+// A/B build knob: the smallest weight-gradient grid (tiles x groups) that takes impl 8 with a K split (round 6);
+// a large value restores the round-5 choice (impl 1 below 257 tiles, impl 8 unsplit above)
+#ifndef MMT_GEMM_SK8_MIN
+#define MMT_GEMM_SK8_MIN 64
+#endif
 // A/B build knob (tools/build_ablate.sh noocc2): 1 = the cost model never switches to impl 8
 #ifndef MMT_GEMM_NO_OCC2
 #define MMT_GEMM_NO_OCC2 0
@@ -528,6 +533,64 @@ MMT_DEV void gemm_glds_tile(const mmt_gemm_params& p, const int g, const int til
 #undef MMT_PIN
 #undef MMT_WAIT_PIN
     MMT_STAMP(3, "s_memtime");
+
+    // ---- split-K hand-off of the two-per-CU MN-major tiles (impl 8 with a_t / w_t: the training step's dW / dX
+    // GEMMs; round 6).  Their grids are 0.6-1.6 rounds of the 512 two-per-CU slots (dW of fc1: 336 tiles of 132
+    // K-steps), so a K split evens the CUs' work out.  The one-per-CU tiles hand off through the assembled tile
+    // image (below); this tile's fp32 image does not fit its 64 KiB ring in one piece, so the hand-off runs on the
+    // accumulator registers instead, before the epilogue: every slice stores its fragments lane-linear (one 1-KiB
+    // wave-instruction per 16x16 fragment, so the slab layout is [wave][fragment][lane]), drains them and takes an
+    // agent-scope arrival ticket (the store-first form of the one-per-CU tiles, no waiting anywhere); the
+    // workgroup that draws the last ticket resets it, sums the nsk slabs in SLICE order (its own read back too,
+    // which frees its accumulators for the sum) and alone runs the epilogue.  The sum's order is fixed, so the
+    // result does not depend on arrival order; the same K ranges and fragment order as impl 1's split give
+    // bit-identical partials.
+    constexpr bool SK2 = OCC > 1 && TB && !W4;
+    if constexpr (SK2) {
+        if (nsk > 1) {
+            constexpr int FR = NT * MT, SLAB = BM * BN * 4;
+            static_assert(NW * FR * 64 * 16 == SLAB, "register slab covers the tile");
+            const int64_t tix = (int64_t)g * ntiles + tile;
+            const __amdgpu_buffer_rsrc_t slabs = __builtin_amdgcn_make_buffer_rsrc(
+                p.sk_ws + tix * nsk * (BM * BN), (short)0, nsk * SLAB, 0x00020000);
+            const int woff = (wid * FR * 64 + lane) * 16;
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[nt][mt]), slabs,
+                                                           slice * SLAB + woff + (nt * MT + mt) * 1024, 0, 16);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+            __syncthreads();
+            int* flag = (int*)lds;  // every wave is past its fragment reads (barrier above)
+            if (threadIdx.x == 0) {
+                const uint32_t old = __hip_atomic_fetch_add(p.sk_cnt + tix, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const int last = old == (uint32_t)(nsk - 1);
+                if (last) __hip_atomic_store(p.sk_cnt + tix, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                *flag = last;
+            }
+            __syncthreads();
+            if (!*flag) return;
+            __syncthreads();  // every wave has read the flag before the epilogue reuses the LDS
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int q = 0; q < nsk; ++q) {  // slice order
+                u32x4 v[NT][MT];
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt)
+                        v[nt][mt] = __builtin_amdgcn_raw_buffer_load_b128(slabs, q * SLAB + woff + (nt * MT + mt) * 1024, 0, 16);
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt) acc[nt][mt] += __builtin_bit_cast(f32x4, v[nt][mt]);
+            }
+        }
+    }
 
     // ---- epilogue through LDS.  Fragment-shaped stores (16 rows x 32 B per wave-instruction) ran
     // at a fraction of the store path's rate (5-8 us of a 15-19 us launch, per in-kernel stamps),
@@ -1312,9 +1375,18 @@ int mmt_gemm_glds(const mmt_gemm_params& p, hipStream_t st, int force) {
     }
     if (p.a_t || p.w_t) {  // MN-major operands: the 128x128 tiles (impl 1, or impl 8 on big unsplit grids)
         if (force != 0 && force != 1 && force != 8) return 1;
-        const bool big = tiles_of(p, 128, 128) * p.groups > 256;
+        const int64_t t8 = tiles_of(p, 128, 128) * p.groups;
+        const bool big = t8 > 256;
         const Cand& c = cands[0];
-        if (force == 1 || (force == 0 && !big)) {
+        // Round 6: the weight gradients (A and W MN-major) of >= MMT_GEMM_SK8_MIN tiles on impl 8 with the K split
+        // that fills ~480 of the 512 two-per-CU slots (the register hand-off above).  Isolated, two groups of 8448
+        // tokens (profiles/r06_sk8_gemm_ab.jsonl): dW of qkv 104.1 -> 100.3 us (impl 1 unsplit -> 2 slices), proj
+        // 49.7 -> 43.7 (impl 1 / 3 slices -> 6), fc1 144.6 -> 136.5 and fc2 134.8 -> 131.8 (impl 8 unsplit -> 2).
+        // The input gradients (W only MN-major) stay unsplit: every split measured slower (dX of fc1 108.7 -> 133).
+        if (force == 0 && p.a_t && t8 >= MMT_GEMM_SK8_MIN && p.splitk == 0 && max_split(c) > 1) {
+            cfg = 8;
+            nsk = (int)std::min<int64_t>(max_split(c), (480 + t8 - 1) / t8);
+        } else if (force == 1 || (force == 0 && !big)) {
             cfg = 1;
             const int nmax = p.splitk >= 1 ? std::min(p.splitk, max_split(c)) : max_split(c);
             float best = 1e30f;
@@ -1324,6 +1396,7 @@ int mmt_gemm_glds(const mmt_gemm_params& p, hipStream_t st, int force) {
             }
         } else {
             cfg = 8;
+            if (p.splitk >= 2) nsk = std::min(p.splitk, max_split(c));  // forced slice count (A/B tools)
         }
         const int lnm = p.a_t ? 4 : 3;
         const dim3 grid((unsigned)tiles_of(p, 128, 128), nsk, p.groups);

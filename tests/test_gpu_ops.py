@@ -304,9 +304,8 @@ def _mn_major(p, a_t, w_t, ldw):
 def test_gemm_mn_major_w(impl, splitk, M, N, K, act):
     """w_t 1 (the Linear backward's dX = dY W): W given MN-major as W^T [K][ldw] and read with
     ds_read_b64_tr_b16; plain and GELU-backward (act 5) epilogues, K tails (K % 64 != 0), row / column
-    tails, split-K; every launch repeats bitwise; impl -1 / 2 reject the mode."""
-    if splitk and impl == 8:
-        pytest.skip("impl 8 takes no split-K")
+    tails, split-K (impl 8's register hand-off: bit-identical to impl 1's split); every launch repeats bitwise;
+    impl -1 / 2 reject the mode."""
     L = _lib()
     g = torch.Generator().manual_seed(M + N + K + act)
     A = torch.randn(M, K, generator=g).bfloat16()
@@ -335,6 +334,13 @@ def test_gemm_mn_major_w(impl, splitk, M, N, K, act):
     assert torch.equal(outs[0], outs[1])
     if splitk:
         assert int(kw["sk"][2].abs().sum()) == 0
+    if splitk and impl == 8:  # the same slices on the one-per-CU tile
+        c = torch.full((M, N), float("nan"), device="cuda")
+        p = _mn_major(_gemm_params([Ad.data_ptr()], [Wd.data_ptr()], [c.data_ptr()], M, N, K, K, N, bias=[bd.data_ptr()],
+                                   act=act, c_f32=1, impl=1, **kw), 0, 1, N + 8)
+        L.check(L.LIB.mmt_gemm(p, L.MMT_BF16, torch.cuda.current_stream().cuda_stream), "gemm w_t 1")
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], c.cpu())
     for bad in (-1, 2):
         p = _mn_major(_gemm_params([Ad.data_ptr()], [Wd.data_ptr()], [c.data_ptr()], M, N, K, K, N, c_f32=1, impl=bad),
                       0, 1, N + 8)
@@ -347,9 +353,8 @@ def test_gemm_mn_major_w(impl, splitk, M, N, K, act):
 def test_gemm_mn_major_dw(impl, splitk, M, Kx, T):
     """a_t 1 + w_t 2 + c2_copy 3: the Linear backward's dW / db = dY^T [X | 1] straight from dY [T][M] and
     X [T][Kx] (both MN-major, no transposed copies): dW [M][Kx] contiguous, db in column 0 of C2 [M][8],
-    columns 1..7 zero; T (the contraction) not a multiple of 64; split-K; bitwise repeatable."""
-    if splitk and impl == 8:
-        pytest.skip("impl 8 takes no split-K")
+    columns 1..7 zero; T (the contraction) not a multiple of 64; split-K (impl 8's register hand-off: bit-identical
+    to impl 1's split); bitwise repeatable."""
     L = _lib()
     g = torch.Generator().manual_seed(M + Kx + T)
     dY = torch.randn(T, M, generator=g).bfloat16()
@@ -376,6 +381,14 @@ def test_gemm_mn_major_dw(impl, splitk, M, Kx, T):
     assert torch.equal(outs[0], outs[1])
     if splitk:
         assert int(kw["sk"][2].abs().sum()) == 0
+    if splitk and impl == 8:  # the same slices on the one-per-CU tile
+        buf = torch.full((M * (Kx + 8),), float("nan"), device="cuda")
+        dw, db8 = buf[:M * Kx].view(M, Kx), buf[M * Kx:].view(M, 8)
+        p = _mn_major(_gemm_params([dYd.data_ptr()], [Xd.data_ptr()], [dw.data_ptr()], M, Kx + 8, T, M, Kx, c_f32=1,
+                                   c2=[db8.data_ptr()], c2_copy=3, impl=1, **kw), 1, 2, Kx)
+        L.check(L.LIB.mmt_gemm(p, L.MMT_BF16, torch.cuda.current_stream().cuda_stream), "gemm a_t 1 w_t 2")
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], buf.cpu())
 
 
 @pytest.mark.parametrize("impl", [1, 2, 3, 4, 6])
