@@ -238,10 +238,71 @@ __global__ __launch_bounds__(256) void msda_bwd_kernel(const T* __restrict__ val
 // grad_value without atomics (deterministic): one workgroup per (n, m, level, chunk of 64 consecutive pixels of
 // the level in raster order).  Every sample of (n, m, level) -- Lq x P of them, in batches of MSDA_SB -- is expanded
 // into its four bilinear taps (the forward's validity rules, cuh:55-84); the taps that land in the chunk are counted
-// per pixel, bucketed (LDS), each bucket sorted by (sample, tap), and each pixel's channels summed in that fixed
+// per pixel, bucketed (LDS) in (sample, tap) order (bucket_pass), and each pixel's channels summed in that fixed
 // order: grad_value[pixel, c] = sum w_k * (g[q, c] * a), written once.  Taps are the reference's atomics
 // (ms_deform_im2col_cuda.cuh:86-235, ms_deformable_col2im_*) re-ordered; thread (c, pixel group) owns 16 pixels.
 constexpr int MSDA_PIX = 64, MSDA_SB = 1024;
+
+// Stable bucket placement (replaces the per-bucket one-thread insertion sort, whose cost grew with the square of a
+// bucket's length when sampling locations collapse onto a pixel).  A sample contributes at most one tap to a pixel,
+// so (sample, tap) order within a bucket is the order of the items i = 4 j + k.  The workgroup's NW waves own
+// contiguous runs of items; a wave walks its run 64 items at a time in order, finds the lanes whose taps land on the
+// same pixel by a bitwise ballot match over the NB bits of the pixel index, and places lane L at
+//   bucket start + earlier waves' items on the pixel + this wave's earlier items on it + #peers below L.
+// Counts live in tbl: NW rows of packed 16-bit (wave, pixel) counters, ceil(np / 2) words per row (a pixel's
+// items <= the samples, < 65536).  Same order as the sort, so the same sums bit for bit.
+template <int NB>
+MMT_DEV uint64_t bucket_peers(int r) {  // lanes whose pixel equals this lane's (r < 0: no tap, no peers)
+    uint64_t pe = __ballot(r >= 0);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const uint64_t m = __ballot((r >> b) & 1);
+        pe &= ((r >> b) & 1) ? m : ~m;
+    }
+    return r >= 0 ? pe : 0ull;
+}
+
+// One pass over this wave's items [i0, i1): item(i, r, w) sets the pixel r (< 0: no tap) and the weight.
+// place = false: add the counts into tbl_w.  place = true: tbl_w holds this wave's starting offsets (after
+// bucket_wave_offsets); put(pos, i, w) stores the entry.
+template <int NB, typename A, typename Item, typename Put>
+MMT_DEV void bucket_pass(uint32_t* tbl_w, const int* start, int i0, int i1, bool place, Item&& item, Put&& put) {
+    const int lane = threadIdx.x & 63;
+    for (int b = i0; b < i1; b += 64) {  // wave-uniform
+        const int i = b + lane;
+        int r = -1;
+        A wk = (A)0;
+        if (i < i1) item(i, r, wk);
+        const uint64_t pe = bucket_peers<NB>(r);
+        const uint64_t below = pe & ((1ull << lane) - 1ull);
+        const bool lead = r >= 0 && below == 0ull;
+        const uint32_t sh = 16u * (uint32_t)(r & 1);
+        uint32_t old = 0;
+        if (lead) old = atomicAdd(&tbl_w[r >> 1], (uint32_t)__popcll(pe) << sh);
+        if (place) {
+            const int leader = r >= 0 ? __ffsll((unsigned long long)pe) - 1 : lane;
+            old = __shfl(old, leader, 64);
+            if (r >= 0) put(start[r] + (int)((old >> sh) & 0xffffu) + __popcll(below), i, wk);
+        }
+    }
+}
+
+// After the counting pass: every (wave, pixel) counter becomes the items of earlier waves on that pixel, and
+// total[r] the pixel's count, for r < 2 * words (total holds that many).  Threads stride over the words.
+template <int NW>
+MMT_DEV void bucket_wave_offsets(uint32_t* tbl, int words, int* total, int nthreads) {
+    for (int x = threadIdx.x; x < words; x += nthreads) {
+        uint32_t run = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            const uint32_t v = tbl[w * words + x];
+            tbl[w * words + x] = run;
+            run += v;
+        }
+        total[2 * x] = (int)(run & 0xffffu);
+        total[2 * x + 1] = (int)(run >> 16);
+    }
+}
 
 template <typename T>
 __global__ __launch_bounds__(256) void msda_bwd_value_kernel(const T* __restrict__ loc, const T* __restrict__ aw,
@@ -250,7 +311,8 @@ __global__ __launch_bounds__(256) void msda_bwd_value_kernel(const T* __restrict
                                                              const int64_t* __restrict__ lstart, int S, int M, int D,
                                                              int Lq, int L, int P) {
     using A = T;
-    __shared__ int cnt[MSDA_PIX + 1], cur[MSDA_PIX];
+    __shared__ int cnt[MSDA_PIX + 1];
+    __shared__ uint32_t tbl[4 * (MSDA_PIX / 2)];  // the 4 waves' packed (wave, pixel) counters
     __shared__ int ekey[4 * MSDA_SB];
     __shared__ A ew[4 * MSDA_SB];
     __shared__ A sa[MSDA_SB];
@@ -288,18 +350,31 @@ __global__ __launch_bounds__(256) void msda_bwd_value_kernel(const T* __restrict
         if (hh_ <= H - 1 && wl >= 0 && (unsigned)(r1 + W) < (unsigned)np) f(2, r1 + W, lh * hw);
         if (hh_ <= H - 1 && wh_ <= W - 1 && (unsigned)(r1 + W + 1) < (unsigned)np) f(3, r1 + W + 1, lh * lw);
     };
+    const int wv = t >> 6;
     for (int b0 = 0; b0 < ns; b0 += MSDA_SB) {
         const int nb = min(MSDA_SB, ns - b0);
-        if (t <= MSDA_PIX) cnt[t] = 0;
-        __syncthreads();
-        for (int j = t; j < nb; j += 256) {  // count the chunk's taps per pixel; the samples' q and a
+        if (t < 4 * (MSDA_PIX / 2)) tbl[t] = 0;
+        for (int j = t; j < nb; j += 256) {  // the samples' q and a
             const int jj = b0 + j, q = jj / P, p = jj - q * P;
             sq[j] = q;
             sa[j] = aw[(((int64_t)n * Lq + q) * M + m) * L * P + (int64_t)l * P + p];
-            taps(jj, [&](int, int r, A) { atomicAdd(&cnt[r], 1); });
         }
         __syncthreads();
-        if (t < 64) {  // exclusive scan of the 64 counts (one wave)
+        // items i = 4 j + k of this batch, a contiguous run per wave; the chunk's taps counted, then placed stably
+        const int items = 4 * nb, per = (items + 4 * 64 - 1) / (4 * 64) * 64;
+        const int i0 = min(wv * per, items), i1 = min(i0 + per, items);
+        auto item = [&](int i, int& r, A& wk) {
+            const int k = i & 3;
+            taps(b0 + (i >> 2), [&](int kk, int rr, A ww) {
+                if (kk == k) r = rr, wk = ww;
+            });
+        };
+        uint32_t* tw = tbl + wv * (MSDA_PIX / 2);
+        bucket_pass<6, A>(tw, cnt, i0, i1, false, item, [](int, int, A) {});
+        __syncthreads();
+        bucket_wave_offsets<4>(tbl, MSDA_PIX / 2, cnt, 256);
+        __syncthreads();
+        if (t < 64) {  // exclusive scan of the 64 counts (one wave), in place: bucket starts, cnt[64] = total
             const int v = cnt[t];
             int x = v;
 #pragma unroll
@@ -307,33 +382,14 @@ __global__ __launch_bounds__(256) void msda_bwd_value_kernel(const T* __restrict
                 const int y = __shfl_up(x, o, 64);
                 if (t >= o) x += y;
             }
-            cur[t] = x - v;
+            cnt[t] = x - v;
             if (t == 63) cnt[MSDA_PIX] = x;
         }
         __syncthreads();
-        if (t < MSDA_PIX) cnt[t] = cur[t];  // bucket starts (cnt[64] = total)
-        __syncthreads();
-        for (int j = t; j < nb; j += 256)
-            taps(b0 + j, [&](int k, int r, A wk) {
-                const int pos = atomicAdd(&cur[r], 1);
-                ekey[pos] = j * 4 + k;
-                ew[pos] = wk;
-            });
-        __syncthreads();
-        if (t < MSDA_PIX) {  // each bucket in (sample, tap) order: the fixed summation order
-            const int e0 = cnt[t], e1 = cnt[t + 1];
-            for (int e = e0 + 1; e < e1; ++e) {
-                const int k = ekey[e];
-                const A wv = ew[e];
-                int i = e - 1;
-                for (; i >= e0 && ekey[i] > k; --i) {
-                    ekey[i + 1] = ekey[i];
-                    ew[i + 1] = ew[i];
-                }
-                ekey[i + 1] = k;
-                ew[i + 1] = wv;
-            }
-        }
+        bucket_pass<6, A>(tw, cnt, i0, i1, true, item, [&](int pos, int i, A wk) {
+            ekey[pos] = i;
+            ew[pos] = wk;
+        });
         __syncthreads();
         {  // the wave's 16 pixels advance together (pixels are wave-uniform): 16 independent gathers in flight
             int e0[MSDA_PIX / 4], e1[MSDA_PIX / 4], len = 0;
@@ -370,7 +426,7 @@ __global__ __launch_bounds__(256) void msda_bwd_value_kernel(const T* __restrict
 
 // grad_value, one workgroup per (n, m, level) (round 6): the level's Lq x P samples expanded
 // into their taps ONCE (msda_bwd_value_kernel re-expanded them in every 64-pixel chunk workgroup), counted per pixel
-// of the whole level, bucketed, each bucket sorted by (sample, tap) -- the same summation order as
+// of the whole level, bucketed in (sample, tap) order -- the same summation order as
 // msda_bwd_value_kernel, so the same sums bit for bit -- then each pixel's channels summed, 16 waves over the
 // pixels with four independent sums in flight per wave.  Taken when a level's samples and pixels fit the LDS
 // lists (Lq P <= NML_S, H W <= NML_PIX) and D <= 64.
@@ -382,14 +438,16 @@ __global__ __launch_bounds__(NML_T) void msda_bwd_value_nml_kernel(const T* __re
                                                                    const int64_t* __restrict__ lstart, int S, int M,
                                                                    int D, int Lq, int L, int P) {
     using A = T;
-    __shared__ int cnt[NML_PIX + 1], cur[NML_PIX];
+    __shared__ int cnt[NML_PIX + 2];
+    __shared__ uint32_t tbl[(NML_T / 64) * (NML_PIX / 2)];  // the 16 waves' packed (wave, pixel) counters
     __shared__ int ekey[4 * NML_S];
     __shared__ A ew[4 * NML_S];
     __shared__ A sa[NML_S];
     const int t = threadIdx.x;
     const int l = blockIdx.x, m = blockIdx.y, n = blockIdx.z;
     const int H = (int)shapes[2 * l], W = (int)shapes[2 * l + 1], np = H * W, ns = Lq * P;
-    for (int r = t; r <= np; r += NML_T) cnt[r] = 0;
+    const int words = (np + 1) / 2;
+    for (int x = t; x < (NML_T / 64) * words; x += NML_T) tbl[x] = 0;
     for (int j = t; j < ns; j += NML_T) {
         const int q = j / P, p = j - q * P;
         sa[j] = aw[(((int64_t)n * Lq + q) * M + m) * L * P + (int64_t)l * P + p];
@@ -409,10 +467,22 @@ __global__ __launch_bounds__(NML_T) void msda_bwd_value_nml_kernel(const T* __re
         if (hh_ <= H - 1 && wl >= 0) f(2, r1 + W, lh * hw);
         if (hh_ <= H - 1 && wh_ <= W - 1) f(3, r1 + W + 1, lh * lw);
     };
-    for (int j = t; j < ns; j += NML_T) taps(j, [&](int, int r, A) { atomicAdd(&cnt[r], 1); });
+    // items i = 4 j + k, a contiguous run per wave: counted, offsets, scanned, placed stably (no sort)
+    const int wv = t >> 6, items = 4 * ns, per = (items + NML_T - 1) / NML_T * 64;
+    const int i0 = min(wv * per, items), i1 = min(i0 + per, items);
+    auto item = [&](int i, int& r, A& wk) {
+        const int k = i & 3;
+        taps(i >> 2, [&](int kk, int rr, A ww) {
+            if (kk == k) r = rr, wk = ww;
+        });
+    };
+    uint32_t* tw = tbl + wv * words;
+    bucket_pass<10, A>(tw, cnt, i0, i1, false, item, [](int, int, A) {});
     __syncthreads();
-    if (t < 64) {  // exclusive scan of the np counts: lane t owns a run of ceil(np / 64)
-        const int per = (np + 63) / 64, r0 = min(t * per, np), r1 = min(r0 + per, np);
+    bucket_wave_offsets<NML_T / 64>(tbl, words, cnt, NML_T);
+    __syncthreads();
+    if (t < 64) {  // exclusive scan of the np counts in place: lane t owns a run of ceil(np / 64)
+        const int per_l = (np + 63) / 64, r0 = min(t * per_l, np), r1 = min(r0 + per_l, np);
         int sum = 0;
         for (int r = r0; r < r1; ++r) sum += cnt[r];
         int x = sum;
@@ -424,35 +494,16 @@ __global__ __launch_bounds__(NML_T) void msda_bwd_value_nml_kernel(const T* __re
         int run = x - sum;
         for (int r = r0; r < r1; ++r) {
             const int v = cnt[r];
-            cur[r] = run;
+            cnt[r] = run;
             run += v;
         }
         if (t == 63) cnt[np] = x;
     }
     __syncthreads();
-    for (int r = t; r < np; r += NML_T) cnt[r] = cur[r];
-    __syncthreads();
-    for (int j = t; j < ns; j += NML_T)
-        taps(j, [&](int k, int r, A wk) {
-            const int pos = atomicAdd(&cur[r], 1);
-            ekey[pos] = j * 4 + k;
-            ew[pos] = wk;
-        });
-    __syncthreads();
-    for (int r = t; r < np; r += NML_T) {  // each bucket in (sample, tap) order
-        const int e0 = cnt[r], e1 = cnt[r + 1];
-        for (int e = e0 + 1; e < e1; ++e) {
-            const int k = ekey[e];
-            const A wv = ew[e];
-            int i = e - 1;
-            for (; i >= e0 && ekey[i] > k; --i) {
-                ekey[i + 1] = ekey[i];
-                ew[i + 1] = ew[i];
-            }
-            ekey[i + 1] = k;
-            ew[i + 1] = wv;
-        }
-    }
+    bucket_pass<10, A>(tw, cnt, i0, i1, true, item, [&](int pos, int i, A wk) {
+        ekey[pos] = i;
+        ew[pos] = wk;
+    });
     __syncthreads();
     const int wave = t >> 6, c = t & 63;
     constexpr int NW = NML_T / 64, PS = 4;
@@ -680,7 +731,7 @@ __global__ __launch_bounds__(64) void msda_train_bwd_samp_kernel(const bf16_t* _
 }
 
 // backward, grad_value: one workgroup per (b, m, level) -- every sample of the level's nq queries expanded into its
-// taps (counted per pixel, bucketed, each bucket sorted by (sample, tap)), then per pixel and channel
+// taps (counted per pixel, bucketed in (sample, tap) order), then per pixel and channel
 // sum w_k * (g[q, c] * a) in that order: msda_bwd_value_kernel's order with the grad_out rows and the level's
 // attention weights staged in LDS.  16 waves; lane = channel in the gather.
 constexpr int MT_VT = 1024;
@@ -693,7 +744,8 @@ __global__ __launch_bounds__(MT_VT) void msda_train_bwd_value_kernel(const bf16_
     __shared__ float al[MT_NQ_MAX * MT_NP];                                  // a of this level's points
     __shared__ int ekey[MT_NQ_MAX * MT_NP * 4];
     __shared__ float ew[MT_NQ_MAX * MT_NP * 4];
-    __shared__ int cnt[MT_NQ_MAX + 1], cur[MT_NQ_MAX];
+    __shared__ int cnt[MT_NQ_MAX + 2];
+    __shared__ uint32_t tbl[(MT_VT / 64) * (MT_NQ_MAX / 2)];  // the 16 waves' packed (wave, pixel) counters
     const int nq = hw * hw, t = threadIdx.x;
     const int l = blockIdx.x, m = blockIdx.y, b = blockIdx.z;
     const int64_t row0 = (int64_t)b * nq;
@@ -708,7 +760,8 @@ __global__ __launch_bounds__(MT_VT) void msda_train_bwd_value_kernel(const bf16_
 #pragma unroll
         for (int p = 0; p < MT_NP; ++p) al[q * MT_NP + p] = a[l * MT_NP + p];
     }
-    for (int r = t; r <= nq; r += MT_VT) cnt[r] = 0;
+    const int words = (nq + 1) / 2;
+    for (int x = t; x < (MT_VT / 64) * words; x += MT_VT) tbl[x] = 0;
     __syncthreads();
     const int ns = nq * MT_NP;
     // the taps of sample j = q * 4 + p: f(k, pixel, w_k) for the valid ones (msda_bwd_value_kernel's rules)
@@ -725,10 +778,22 @@ __global__ __launch_bounds__(MT_VT) void msda_train_bwd_value_kernel(const bf16_
         if (hh_ <= hw - 1 && wl >= 0) f(2, r1 + hw, lh * hwt);
         if (hh_ <= hw - 1 && wh_ <= hw - 1) f(3, r1 + hw + 1, lh * lw);
     };
-    for (int j = t; j < ns; j += MT_VT) taps(j, [&](int, int r, float) { atomicAdd(&cnt[r], 1); });
+    // items i = 4 j + k, a contiguous run per wave: counted, offsets, scanned, placed stably (no sort)
+    const int wv = t >> 6, items = 4 * ns, per = (items + MT_VT - 1) / MT_VT * 64;
+    const int i0 = min(wv * per, items), i1 = min(i0 + per, items);
+    auto item = [&](int i, int& r, float& wk) {
+        const int k = i & 3;
+        taps(i >> 2, [&](int kk, int rr, float ww) {
+            if (kk == k) r = rr, wk = ww;
+        });
+    };
+    uint32_t* tw = tbl + wv * words;
+    bucket_pass<9, float>(tw, cnt, i0, i1, false, item, [](int, int, float) {});
     __syncthreads();
-    if (t < 64) {  // exclusive scan of the nq counts: lane t owns a run of ceil(nq / 64)
-        const int per = (nq + 63) / 64, r0 = t * per, r1 = min(r0 + per, nq);
+    bucket_wave_offsets<MT_VT / 64>(tbl, words, cnt, MT_VT);
+    __syncthreads();
+    if (t < 64) {  // exclusive scan of the nq counts in place: lane t owns a run of ceil(nq / 64)
+        const int per_l = (nq + 63) / 64, r0 = min(t * per_l, nq), r1 = min(r0 + per_l, nq);
         int sum = 0;
         for (int r = r0; r < r1; ++r) sum += cnt[r];
         int x = sum;
@@ -740,35 +805,16 @@ __global__ __launch_bounds__(MT_VT) void msda_train_bwd_value_kernel(const bf16_
         int run = x - sum;
         for (int r = r0; r < r1; ++r) {
             const int v = cnt[r];
-            cur[r] = run;
+            cnt[r] = run;
             run += v;
         }
         if (t == 63) cnt[nq] = x;
     }
     __syncthreads();
-    for (int r = t; r < nq; r += MT_VT) cnt[r] = cur[r];  // bucket starts (cnt[nq] = total)
-    __syncthreads();
-    for (int j = t; j < ns; j += MT_VT)
-        taps(j, [&](int k, int r, float wk) {
-            const int pos = atomicAdd(&cur[r], 1);
-            ekey[pos] = j * 4 + k;
-            ew[pos] = wk;
-        });
-    __syncthreads();
-    for (int r = t; r < nq; r += MT_VT) {  // each bucket in (sample, tap) order
-        const int e0 = cnt[r], e1 = cnt[r + 1];
-        for (int e = e0 + 1; e < e1; ++e) {
-            const int k = ekey[e];
-            const float wv = ew[e];
-            int i = e - 1;
-            for (; i >= e0 && ekey[i] > k; --i) {
-                ekey[i + 1] = ekey[i];
-                ew[i + 1] = ew[i];
-            }
-            ekey[i + 1] = k;
-            ew[i + 1] = wv;
-        }
-    }
+    bucket_pass<9, float>(tw, cnt, i0, i1, true, item, [&](int pos, int i, float wk) {
+        ekey[pos] = i;
+        ew[pos] = wk;
+    });
     __syncthreads();
     // gather: wave w takes pixels w, w + 16, ... four at a time (independent sums in flight); lane = channel
     const int wave = t >> 6, c = t & 63;

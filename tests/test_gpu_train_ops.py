@@ -877,13 +877,15 @@ def test_hip_conv3x3_upsampled_input(B, H, Cin, Cout, up):
         assert err <= tol, (name, err)
 
 
-@pytest.mark.parametrize("B,hw,grid", [(2, 20, False), (16, 20, True), (3, 7, False), (1, 22, True)])
+@pytest.mark.parametrize("B,hw,grid", [(2, 20, False), (16, 20, True), (3, 7, False), (1, 22, True), (2, 20, "collapse")])
 def test_msda_bimodal_train_matches_generic(B, hw, grid):
     """HipOps.msda_bimodal (mmt_msda_bimodal_train_fwd / _bwd: softmax, locations, sampling and the backward fused,
     bf16 in / out) against the step's previous composition -- F.softmax(aw.float()), ref + off.float() / wh and
     MSDeformAttnFunction (the drop-in mmt_ms_deform_attn_forward / _backward, fp32) on value.float(), with the
     casts -- on the same bf16 inputs.  grid: integer offsets (Deformable DETR's initial pattern), so that samples
-    sit on pixel edges where the location gradient is discontinuous.  Forward and grad_value within one bf16
+    sit on pixel edges where the location gradient is discontinuous; "collapse": every sample of a level near one
+    point, so that four pixels take all 1600 taps of a (batch, head, level) (the value gather's stable bucket
+    placement).  Forward and grad_value within one bf16
     rounding (relative L2 1e-2; the fp32 sums are the same, only torch's softmax may differ in the last ulp),
     grad_off / grad_awl 1e-2; two runs bitwise equal (deterministic value gather)."""
     import torch.nn.functional as F
@@ -892,7 +894,12 @@ def test_msda_bimodal_train_matches_generic(B, hw, grid):
     g = torch.Generator().manual_seed(B * 100 + hw)
     nq = hw * hw
     value = torch.randn(B, 2 * nq, 512, generator=g).bfloat16().cuda()
-    if grid:
+    ref4 = _ref_points(hw, hw, B, 2, "cuda")
+    ref_q = ref4[0, :nq, 0, :].contiguous()
+    if grid == "collapse":  # loc = ref + off / hw near (0.4737, 0.4737) for every query: off = (0.4737 - ref) * hw
+        tgt = 0.4737 + (torch.rand(B, nq, 8, 2, 4, 2, generator=g) - 0.5) * 2e-3
+        off = ((tgt - ref_q.cpu().view(1, nq, 1, 1, 1, 2)) * hw).reshape(B, nq, 128)
+    elif grid:
         base = torch.tensor([[1., 0.], [0., 1.], [-1., 0.], [0., -1.], [1., 1.], [-1., 1.], [-1., -1.], [1., -1.]])
         pts = torch.arange(1, 5).float().view(1, 1, 4, 1)
         off = (base.view(8, 1, 1, 2) * pts).expand(8, 2, 4, 2).reshape(1, 1, 128).repeat(B, nq, 1)
@@ -902,8 +909,6 @@ def test_msda_bimodal_train_matches_generic(B, hw, grid):
     off = off.bfloat16().cuda()
     awl = torch.randn(B, nq, 64, generator=g).bfloat16().cuda()
     gout = torch.randn(B, nq, 512, generator=g).bfloat16().cuda()
-    ref4 = _ref_points(hw, hw, B, 2, "cuda")
-    ref_q = ref4[0, :nq, 0, :].contiguous()
 
     # the previous composition (fp32 MSDA through autograd)
     vr, orr, ar = value.clone().requires_grad_(True), off.clone().requires_grad_(True), awl.clone().requires_grad_(True)
