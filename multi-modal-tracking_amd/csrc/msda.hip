@@ -235,6 +235,31 @@ __global__ __launch_bounds__(256) void msda_bwd_kernel(const T* __restrict__ val
     }
 }
 
+MMT_DEV float fma_(float a, float b, float c) { return fmaf(a, b, c); }
+MMT_DEV double fma_(double a, double b, double c) { return fma(a, b, c); }
+
+// A bucket's ordered sum, acc = fma(w_e, x_e, acc) for e = e0 .. e1 - 1, with the loads of U entries issued before
+// their adds: the gathers take it for buckets longer than BUCKET_LONG (collapsed sampling locations: one chain of
+// thousands of entries would otherwise wait out a load latency per entry).  Same order, same bits as the
+// one-entry-per-step loops.
+constexpr int BUCKET_LONG = 24;
+template <int U, typename A, typename Wt, typename Val>
+MMT_DEV A bucket_sum(int e0, int e1, A acc, Wt&& wt, Val&& val) {
+    for (int e = e0; e < e1; e += U) {
+        A w[U], x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int ec = min(e + u, e1 - 1);
+            w[u] = wt(ec);
+            x[u] = val(ec);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (e + u < e1) acc = fma_(w[u], x[u], acc);
+    }
+    return acc;
+}
+
 // grad_value without atomics (deterministic): one workgroup per (n, m, level, chunk of 64 consecutive pixels of
 // the level in raster order).  Every sample of (n, m, level) -- Lq x P of them, in batches of MSDA_SB -- is expanded
 // into its four bilinear taps (the forward's validity rules, cuh:55-84); the taps that land in the chunk are counted
@@ -401,13 +426,20 @@ __global__ __launch_bounds__(256) void msda_bwd_value_kernel(const T* __restrict
                 len = max(len, e1[i] - e0[i]);
             }
             const int64_t gq = (int64_t)M * D, g0 = ((int64_t)n * Lq * M + m) * D + min(c, D - 1);
-            for (int k = 0; k < len; ++k) {
+            if (len > BUCKET_LONG) {  // wave-uniform: pixel by pixel, 8 entries' loads in flight
 #pragma unroll
-                for (int i = 0; i < MSDA_PIX / 4; ++i) {
-                    const int e = e0[i] + k;
-                    if (e < e1[i]) {
-                        const int j = ekey[e] >> 2;
-                        acc[i] += ew[e] * (gout[g0 + sq[j] * gq] * sa[j]);
+                for (int i = 0; i < MSDA_PIX / 4; ++i)
+                    acc[i] = bucket_sum<8>(e0[i], e1[i], acc[i], [&](int e) { return ew[e]; },
+                                           [&](int e) { const int j = ekey[e] >> 2; return gout[g0 + sq[j] * gq] * sa[j]; });
+            } else {
+                for (int k = 0; k < len; ++k) {
+#pragma unroll
+                    for (int i = 0; i < MSDA_PIX / 4; ++i) {
+                        const int e = e0[i] + k;
+                        if (e < e1[i]) {
+                            const int j = ekey[e] >> 2;
+                            acc[i] = fma_(ew[e], gout[g0 + sq[j] * gq] * sa[j], acc[i]);
+                        }
                     }
                 }
             }
@@ -519,13 +551,20 @@ __global__ __launch_bounds__(NML_T) void msda_bwd_value_nml_kernel(const T* __re
             len = max(len, e1[i] - e0[i]);
             acc[i] = 0;
         }
-        for (int k = 0; k < len; ++k) {
+        if (len > BUCKET_LONG) {  // wave-uniform: pixel by pixel, 8 entries' loads in flight
 #pragma unroll
-            for (int i = 0; i < PS; ++i) {
-                const int e = e0[i] + k;
-                if (e < e1[i]) {
-                    const int j = ekey[e] >> 2;
-                    acc[i] += ew[e] * (gout[g0 + (j / P) * gq] * sa[j]);
+            for (int i = 0; i < PS; ++i)
+                acc[i] = bucket_sum<8>(e0[i], e1[i], acc[i], [&](int e) { return ew[e]; },
+                                       [&](int e) { const int j = ekey[e] >> 2; return gout[g0 + (j / P) * gq] * sa[j]; });
+        } else {
+            for (int k = 0; k < len; ++k) {
+#pragma unroll
+                for (int i = 0; i < PS; ++i) {
+                    const int e = e0[i] + k;
+                    if (e < e1[i]) {
+                        const int j = ekey[e] >> 2;
+                        acc[i] = fma_(ew[e], gout[g0 + (j / P) * gq] * sa[j], acc[i]);
+                    }
                 }
             }
         }
@@ -831,13 +870,20 @@ __global__ __launch_bounds__(MT_VT) void msda_train_bwd_value_kernel(const bf16_
             len = max(len, e1[i] - e0[i]);
             acc[i] = 0.f;
         }
-        for (int k = 0; k < len; ++k) {
+        if (len > BUCKET_LONG) {  // wave-uniform: pixel by pixel, 8 entries' loads in flight
 #pragma unroll
-            for (int i = 0; i < PS; ++i) {
-                const int e = e0[i] + k;
-                if (e < e1[i]) {
-                    const int j = ekey[e] >> 2;
-                    acc[i] += ew[e] * (bf2f(gl[(j >> 2) * MT_DH + c]) * al[j]);
+            for (int i = 0; i < PS; ++i)
+                acc[i] = bucket_sum<8>(e0[i], e1[i], acc[i], [&](int e) { return ew[e]; },
+                                       [&](int e) { const int j = ekey[e] >> 2; return bf2f(gl[(j >> 2) * MT_DH + c]) * al[j]; });
+        } else {
+            for (int k = 0; k < len; ++k) {
+#pragma unroll
+                for (int i = 0; i < PS; ++i) {
+                    const int e = e0[i] + k;
+                    if (e < e1[i]) {
+                        const int j = ekey[e] >> 2;
+                        acc[i] = fma_(ew[e], bf2f(gl[(j >> 2) * MT_DH + c]) * al[j], acc[i]);
+                    }
                 }
             }
         }
