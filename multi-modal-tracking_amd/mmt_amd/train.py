@@ -2034,6 +2034,11 @@ def synthetic_batch(B, device, generator=None, template=128, search=320):
     return t, o, s, torch.cat([c - wh / 2, wh], 1).to(device)
 
 
+# GradBucketAllReduce: bucket all-reduces issued asynchronously and joined after the backward (False: each joined
+# at its launch, the form measured before round 6's end; A/B tools only)
+ALLREDUCE_ASYNC = True
+
+
 class GradBucketAllReduce:
     """Data-parallel gradient averaging (what DistributedDataParallel's reducer does for the reference,
     train_script_mixformer.py:104-110, run_training_ddp.py:94) issued by the step itself on its own
@@ -2043,7 +2048,8 @@ class GradBucketAllReduce:
     Buckets: the trainable parameters in reverse registration order (the order their gradients appear in
     the backward), cut at `cap_bytes` of fp32 (one ViT block's parameters by default, ~27 MB at ViT-B).
     A post-accumulate-grad hook on every parameter counts a bucket's arrivals; the last one launches the
-    bucket's all-reduce at once, so a block's exchange overlaps the backward of the blocks below it.
+    bucket's all-reduce at once, asynchronously (the process group's stream), so a block's exchange overlaps
+    the backward of the blocks below it; finish() joins them in launch order and copies the averages back.
     A bucket is one flat buffer (the gradients concatenated, divided by the world size, in fp32 or
     rounded to bf16 with compress="bf16"), one all-reduce, and one multi-tensor copy back into the
     .grad tensors.  finish() launches buckets whose parameters did not all receive a gradient, in bucket
@@ -2076,6 +2082,7 @@ class GradBucketAllReduce:
     def begin(self):
         self.left = [len(b) for b in self.buckets]
         self.done = [False] * len(self.buckets)
+        self.pending = []  # (work, flat bucket, its .grad tensors) of the launched, not yet joined all-reduces
 
     def _arrived(self, p):
         i = self.bucket_of[id(p)]
@@ -2093,14 +2100,21 @@ class GradBucketAllReduce:
             flat = flat.to(self.dtype)
         if self.world > 1:
             flat.div_(self.world)
-        self.dist.all_reduce(flat, group=self.group)
-        views = [v.view_as(g) for v, g in zip(flat.split([g.numel() for g in grads]), grads)]
-        torch._foreach_copy_(grads, views)
+        # asynchronous: the collective runs on the process group's own stream (RCCL: after an event on the step's
+        # stream), so the backward of the blocks below keeps the step's stream busy meanwhile; finish() joins it
+        work = self.dist.all_reduce(flat, group=self.group, async_op=ALLREDUCE_ASYNC)
+        self.pending.append((work, flat, grads))
 
     def finish(self):
         for i in range(len(self.buckets)):
             if not self.done[i]:
                 self._launch(i)
+        for work, flat, grads in self.pending:  # in launch order: the step's stream waits, then the averaged copy
+            if work is not None:
+                work.wait()
+            views = [v.view_as(g) for v, g in zip(flat.split([g.numel() for g in grads]), grads)]
+            torch._foreach_copy_(grads, views)
+        self.pending = []
 
     def remove(self):
         for h in self.handles:
