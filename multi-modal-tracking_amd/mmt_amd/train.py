@@ -2051,8 +2051,8 @@ class GradBucketAllReduce:
     bucket's all-reduce at once, asynchronously (the process group's stream), so a block's exchange overlaps
     the backward of the blocks below it; finish() joins them in launch order and copies the averages back.
     A bucket is one flat buffer (the gradients concatenated, divided by the world size, in fp32 or
-    rounded to bf16 with compress="bf16"), one all-reduce, and one multi-tensor copy back into the
-    .grad tensors.  finish() launches buckets whose parameters did not all receive a gradient, in bucket
+    rounded to bf16 with compress="bf16") and one all-reduce; the parameters' .grad then become views of the
+    averaged fp32 bucket (bf16 buckets: one multi-tensor copy back into the fp32 .grad tensors).  finish() launches buckets whose parameters did not all receive a gradient, in bucket
     order (every rank runs the same graph, so every rank launches the same sequence)."""
 
     def __init__(self, params, world, group=None, cap_bytes=None, compress="none"):
@@ -2092,7 +2092,8 @@ class GradBucketAllReduce:
 
     def _launch(self, i):
         self.done[i] = True
-        grads = [p.grad for p in self.buckets[i] if p.grad is not None]
+        ps = [p for p in self.buckets[i] if p.grad is not None]
+        grads = [p.grad for p in ps]
         if not grads:
             return
         flat = torch.cat([g.reshape(-1) for g in grads])
@@ -2103,17 +2104,21 @@ class GradBucketAllReduce:
         # asynchronous: the collective runs on the process group's own stream (RCCL: after an event on the step's
         # stream), so the backward of the blocks below keeps the step's stream busy meanwhile; finish() joins it
         work = self.dist.all_reduce(flat, group=self.group, async_op=ALLREDUCE_ASYNC)
-        self.pending.append((work, flat, grads))
+        self.pending.append((work, flat, ps, grads))
 
     def finish(self):
         for i in range(len(self.buckets)):
             if not self.done[i]:
                 self._launch(i)
-        for work, flat, grads in self.pending:  # in launch order: the step's stream waits, then the averaged copy
+        for work, flat, ps, grads in self.pending:  # in launch order: the step's stream waits, then the averages
             if work is not None:
                 work.wait()
             views = [v.view_as(g) for v, g in zip(flat.split([g.numel() for g in grads]), grads)]
-            torch._foreach_copy_(grads, views)
+            if self.dtype is None:  # fp32 buckets: the parameters' .grad become views of the averaged bucket (no copy)
+                for p, v in zip(ps, views):
+                    p.grad = v
+            else:  # bf16 buckets: the averages rounded back into the fp32 .grad tensors
+                torch._foreach_copy_(grads, views)
         self.pending = []
 
     def remove(self):
