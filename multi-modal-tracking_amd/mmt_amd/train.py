@@ -28,6 +28,7 @@ reference's AMP path.  The backbone ops are injected (`ops`), so the data-parall
 with stand-in ops in tests; the product's ops are `HipOps` and have no CPU path.
 """
 import math
+import time
 
 import torch
 import torch.nn.functional as F
@@ -2235,9 +2236,14 @@ class TrainStep:
         # permitted when stream is capturing") and the watchdog aborts the process.  thread_local mode
         # forbids unsafe calls on the capturing thread only; kernels launched onto the captured stream from
         # any thread (the autograd worker's) are recorded either way.
+        # The watchdog also keeps the eager collectives of the warm-up steps in its list until its next poll
+        # (every ~100 ms), and a query of such a work's event once the process group's stream has joined the
+        # capture fails the same way (hipErrorCapturedEvent, seen once in the one-rank test): the device is
+        # drained and the watchdog given a few polls to retire them before the capture starts.
         mode = "global"
         if self.reducer is not None:
             torch.cuda.synchronize()
+            time.sleep(0.5)
             mode = "thread_local"
         with torch.cuda.graph(self.graph, capture_error_mode=mode):
             self.graph_stats = self(t, o, s, gt_xywh)
