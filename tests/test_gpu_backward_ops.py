@@ -123,7 +123,7 @@ def test_msda_backward_collapsed_locations():
     """Every sample of a level on (almost) one point, so four pixels each receive all Lq x P = 1600 taps of a
     (batch, head, level): the gathers' stable bucket placement (the former one-thread insertion sort of
     each bucket was quadratic in its length here) keeps grad_value within 1e-4 of the oracle, both gathers bitwise
-    equal, and the backward within 3x (+ 0.2 ms) of the same op on spread-out locations."""
+    equal, and the backward within 4x (+ 0.5 ms) of the same op on spread-out locations."""
     from mmt_amd import _lib as L_
     from oracle.msda import ms_deform_attn_backward
     N, Lq, M, D, shapes, P = 2, 400, 8, 64, [(20, 20), (20, 20)], 4
@@ -157,7 +157,7 @@ def test_msda_backward_collapsed_locations():
     for impl in (1, 2):
         t_c, t_s = timed(loc, impl), timed(spread, impl)
         print("impl %d: collapsed %.3f ms, spread %.3f ms" % (impl, t_c, t_s))
-        assert t_c <= 3 * t_s + 0.2, (impl, t_c, t_s)
+        assert t_c <= 4 * t_s + 0.5, (impl, t_c, t_s)  # the sorted buckets took 14-42 ms here
 
 
 def test_msda_backward_zero_for_skipped_samples():
