@@ -140,4 +140,5 @@ def test_train_harness_gloo_two_ranks(tmp_path):
     assert r0["value"] == r1["value"] > 0 and r0["ms_per_step"] == r1["ms_per_step"]
     assert r0["parallelism"].startswith("ddp2")
     assert r0["roofline"]["bound"] == "mfma" and 0 < r0["roofline"]["frac"]
-    assert abs(r0["value"] - 2 * 2 * 2 / (r0["ms_per_step"] * 2e-3)) <= 1e-2 * r0["value"]
+    # value is rounded to 2 decimals: under a loaded CPU (a step of seconds) that rounding alone exceeds 1 %
+    assert abs(r0["value"] - 2 * 2 * 2 / (r0["ms_per_step"] * 2e-3)) <= max(1e-2 * r0["value"], 0.006)
